@@ -1,0 +1,372 @@
+"""TEST INFRASTRUCTURE ONLY — functional fp32 CPU restatement of the reference hot path.
+
+Every function names the reference file:line it restates (paths relative to the
+reference repo root, `timevqvae/...`).  The restatement is functional: it takes a
+state_dict-shaped mapping of tensors (same keys as the reference module tree) and
+returns outputs, so the same weights can be pushed through the product's HIP path
+and through this oracle.  Pinned against tests/golden/*.npz, which were produced
+by running the reference itself (tests/golden/make_golden.py).
+
+Float work uses torch CPU fp32 (the reference's own arithmetic); the STFT/iSTFT
+are written out as the explicit n_fft=4 DFT so the formula the HIP kernels follow
+is visible here.  The transformer (x-transformers, absent from the image) is a
+restatement from its published 1.3x behaviour: PARITY UNPINNED for T1 (see
+DESIGN.md §Oracle).
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+# ----------------------------------------------------------------------------
+# STFT / iSTFT, n_fft = 4, hop 1, periodic Hann, center+reflect, normalized
+# ----------------------------------------------------------------------------
+HANN4 = (0.0, 0.5, 1.0, 0.5)
+
+
+def stft4(x: torch.Tensor) -> torch.Tensor:
+    """time_to_timefreq (utils/train_utils.py:293-307): (B,C,T) -> (B,2C,3,T+1).
+
+    Channel 2c+0 is the real part, 2c+1 the imaginary part of bin f (H axis).
+    X[f,t] = 0.5 * sum_n w[n] xp[t+n] exp(-2*pi*i*f*n/4), xp = reflect-pad(x, 2).
+    """
+    B, C, T = x.shape
+    xp = F.pad(x.reshape(B * C, 1, T), (2, 2), mode="reflect").reshape(B, C, T + 4)
+    x1, x2, x3 = xp[..., 1:T + 2], xp[..., 2:T + 3], xp[..., 3:T + 4]
+    re0 = 0.5 * (0.5 * x1 + x2 + 0.5 * x3)
+    re1 = 0.5 * (-x2)
+    im1 = 0.5 * (-0.5 * x1 + 0.5 * x3)
+    re2 = 0.5 * (-0.5 * x1 + x2 - 0.5 * x3)
+    zero = torch.zeros_like(re0)
+    real = torch.stack([re0, re1, re2], dim=2)  # (B,C,3,T+1)
+    imag = torch.stack([zero, im1, zero], dim=2)
+    return torch.stack([real, imag], dim=2).reshape(B, 2 * C, 3, T + 1)
+
+
+def istft4(xf: torch.Tensor, C: int) -> torch.Tensor:
+    """timefreq_to_time (utils/train_utils.py:310-321): (B,2C,3,W) -> (B,C,W-1).
+
+    irfft of each frame (imag of DC/Nyquist ignored), Hann synthesis window,
+    overlap-add, division by the window envelope (1.25 at sample 0, else 1.5),
+    center trim of 2 samples.
+    """
+    B, C2, H, W = xf.shape
+    z = xf.reshape(B, C, 2, 3, W) * 2.0  # undo normalized=True
+    X0r, X1r, X1i, X2r = z[:, :, 0, 0], z[:, :, 0, 1], z[:, :, 1, 1], z[:, :, 0, 2]
+    y1 = (X0r - X2r - 2 * X1i) / 4  # frame sample n=1
+    y2 = (X0r + X2r - 2 * X1r) / 4  # n=2
+    y3 = (X0r - X2r + 2 * X1i) / 4  # n=3
+    L = W - 1
+    out = torch.zeros(B, C, L, dtype=xf.dtype)
+    # sample i <- frames i+1 (n=1), i (n=2), i-1 (n=3)
+    out += 0.5 * y1[..., 1:W]
+    out += 1.0 * y2[..., 0:L]
+    out[..., 1:] += 0.5 * y3[..., 0:L - 1]
+    env = torch.full((L,), 1.5, dtype=xf.dtype)
+    env[0] = 1.25
+    return out / env
+
+
+def band_lf(xf, copy=False):
+    """zero_pad_high_freq (utils/train_utils.py:361-372)."""
+    if copy:
+        return xf[:, :, :1, :].expand(-1, -1, xf.shape[2], -1).contiguous()
+    out = torch.zeros_like(xf)
+    out[:, :, 0] = xf[:, :, 0]
+    return out
+
+
+def band_hf(xf, copy=False):
+    """zero_pad_low_freq (utils/train_utils.py:375-386)."""
+    if copy:
+        return torch.cat([xf[:, :, 1:2], xf[:, :, 1:]], dim=2).contiguous()
+    out = torch.zeros_like(xf)
+    out[:, :, 1:] = xf[:, :, 1:]
+    return out
+
+
+def linear_interp(x, size):
+    """F.interpolate(mode='linear', align_corners=False) (stage1.py:103-113, vq_vae.py:254)."""
+    return F.interpolate(x, size, mode="linear")
+
+
+def compute_downsample_rate(input_length, n_fft, downsampled_width):
+    """utils/train_utils.py:413-418."""
+    if input_length >= downsampled_width:
+        return round(input_length / (np.log2(n_fft) - 1) / downsampled_width)
+    return 1
+
+
+# ----------------------------------------------------------------------------
+# Encoder / decoder (models/vq_vae.py)
+# ----------------------------------------------------------------------------
+def snake(x, a):
+    """SnakeActivation.forward (utils/train_utils.py:446-448): x + (1/a) sin(a x)^2."""
+    return x + (1 / a) * torch.sin(a * x) ** 2
+
+
+def encoder_plan(init_dim, hid_dim, num_channels, downsample_rate, n_res):
+    """Layer list of VQVAEEncoder (vq_vae.py:154-167): ('enc'|'res', cin, cout)."""
+    d = init_dim
+    plan = [("enc", num_channels, d)]
+    d *= 2
+    for _ in range(int(round(np.log2(downsample_rate))) - 1):
+        plan.append(("enc", d // 2, d))
+        for _ in range(n_res):
+            plan.append(("res", d, d))
+        d *= 2
+    plan.append(("res", d // 2, hid_dim))
+    return plan
+
+
+def decoder_plan(init_dim, hid_dim, num_channels, downsample_rate, n_res):
+    """Layer list of VQVAEDecoder (vq_vae.py:226-252): ('res'|'dec'|'convt', cin, cout)."""
+    L = int(round(np.log2(downsample_rate)))
+    d = int(init_dim * 2 ** (L - 1)) if L != 0 else int(init_dim)
+    plan = [("res", hid_dim, d)]
+    for _ in range(L - 1):
+        for _ in range(n_res):
+            plan.append(("res", d, d))
+        d //= 2
+        plan.append(("dec", 2 * d, d))
+    plan.append(("convt", d, num_channels))
+    plan.append(("convt", num_channels, num_channels))
+    return plan
+
+
+class Ctx:
+    """Carries training flag, dropout prob and the buffer updates of one pass."""
+
+    def __init__(self, training, dropout_p=0.0, dropout_gen=None):
+        self.training = training
+        self.dropout_p = dropout_p
+        self.gen = dropout_gen
+        self.updates = {}
+
+
+def _bn(ctx, sd, p, x):
+    """nn.BatchNorm2d/1d (momentum 0.1, eps 1e-5); running stats updated when training."""
+    rm = sd[p + "running_mean"].clone()
+    rv = sd[p + "running_var"].clone()
+    y = F.batch_norm(x, rm, rv, sd[p + "weight"], sd[p + "bias"], ctx.training, 0.1, 1e-5)
+    if ctx.training:
+        ctx.updates[p + "running_mean"] = rm
+        ctx.updates[p + "running_var"] = rv
+        ctx.updates[p + "num_batches_tracked"] = sd[p + "num_batches_tracked"] + 1
+    return y
+
+
+def _dropout(ctx, x, p):
+    if not ctx.training or p == 0.0:
+        return x
+    keep = (torch.rand(x.shape, generator=ctx.gen) >= p).to(x.dtype)
+    return x * keep / (1 - p)
+
+
+def enc_block(ctx, sd, p, x):
+    """VQVAEEncBlock (vq_vae.py:65-92): replicate-pad Conv2d(3x4, s(1,2)) -> BN -> Snake."""
+    x = F.pad(x, (1, 1, 1, 1), mode="replicate")
+    x = F.conv2d(x, sd[p + "block.0.weight"], sd[p + "block.0.bias"], stride=(1, 2))
+    x = _bn(ctx, sd, p + "block.1.", x)
+    return snake(x, sd[p + "block.2.a"])
+
+
+def res_block(ctx, sd, p, x):
+    """ResBlock (vq_vae.py:13-62): proj(x) + Drop(Conv(Snake(BN(Conv(Snake(x))))))."""
+    h = snake(x, sd[p + "convs.0.a"])
+    h = F.conv2d(h, sd[p + "convs.1.weight"], sd[p + "convs.1.bias"], padding=(1, 1))
+    h = _bn(ctx, sd, p + "convs.2.", h)
+    h = snake(h, sd[p + "convs.3.a"])
+    h = F.conv2d(h, sd[p + "convs.4.weight"], sd[p + "convs.4.bias"], padding=(1, 1))
+    h = _dropout(ctx, h, ctx.dropout_p)
+    if p + "proj.weight" in sd:
+        x = F.conv2d(x, sd[p + "proj.weight"], sd[p + "proj.bias"])
+    return x + h
+
+
+def dec_block(ctx, sd, p, x):
+    """VQVAEDecBlock (vq_vae.py:95-121): ConvTranspose2d(3x4, s(1,2), p(1,1)) -> BN -> Snake."""
+    x = F.conv_transpose2d(x, sd[p + "block.0.weight"], sd[p + "block.0.bias"],
+                           stride=(1, 2), padding=(1, 1))
+    x = _bn(ctx, sd, p + "block.1.", x)
+    return snake(x, sd[p + "block.2.a"])
+
+
+def encoder_forward(ctx, sd, prefix, x, plan, band):
+    """VQVAEEncoder.forward (vq_vae.py:174-188)."""
+    C = x.shape[1]
+    h = stft4(x)
+    h = band(h, copy=True)
+    for i, (kind, _, _) in enumerate(plan):
+        p = f"{prefix}encoder.{i}."
+        h = enc_block(ctx, sd, p, h) if kind == "enc" else res_block(ctx, sd, p, h)
+    return h
+
+
+def decoder_forward(ctx, sd, prefix, z, plan, band, x_channels, input_length):
+    """VQVAEDecoder.forward (vq_vae.py:257-264)."""
+    h = z
+    for i, (kind, _, _) in enumerate(plan):
+        p = f"{prefix}decoder.{i}."
+        if kind == "res":
+            h = res_block(ctx, sd, p, h)
+        elif kind == "dec":
+            h = dec_block(ctx, sd, p, h)
+        else:
+            h = F.conv_transpose2d(h, sd[p + "weight"], sd[p + "bias"], stride=(1, 2), padding=(1, 1))
+    h = band(h)
+    h = istft4(h, x_channels)
+    h = linear_interp(h, input_length)
+    return h + F.linear(h, sd[prefix + "linear.weight"], sd[prefix + "linear.bias"])
+
+
+# ----------------------------------------------------------------------------
+# Vector quantiser (models/vq.py)
+# ----------------------------------------------------------------------------
+def vq_forward(ctx, sd, prefix, x, decay=0.8, eps=1e-5):
+    """VectorQuantize.forward + EuclideanCodebook.forward (vq.py:197-251, 325-407).
+
+    x: (B,N,D).  Returns (quantize, embed_ind, commit_loss, perplexity).
+    Buffer updates (EMA, training only) go to ctx.updates.
+    """
+    cb = prefix + "_codebook."
+    embed = sd[cb + "embed"]
+    K = embed.shape[0]
+    flat = x.reshape(-1, x.shape[-1])
+    et = embed.t()
+    dist = -(flat.pow(2).sum(1, keepdim=True) - 2 * flat @ et + et.pow(2).sum(0, keepdim=True))
+    ind = dist.argmax(dim=-1)
+    onehot = F.one_hot(ind, K).to(x.dtype)
+    q = F.embedding(ind, embed).reshape(x.shape)
+    ind = ind.reshape(x.shape[:-1])
+    commit = torch.zeros(())
+    if ctx.training:
+        n = onehot.sum(0)
+        cs = sd[cb + "cluster_size"].detach().clone().mul_(decay).add_(n, alpha=1 - decay)
+        esum = flat.detach().t() @ onehot
+        ea = sd[cb + "embed_avg"].detach().clone().mul_(decay).add_(esum.t(), alpha=1 - decay)
+        tot = cs.sum()
+        cs_s = (cs + eps) / (tot + K * eps) * tot
+        ctx.updates[cb + "cluster_size"] = cs
+        ctx.updates[cb + "embed_avg"] = ea
+        ctx.updates[cb + "embed"] = ea / cs_s.unsqueeze(1)
+        q = x + (q - x).detach()
+        commit = F.mse_loss(q.detach(), x)
+    avg = onehot.mean(0)
+    perp = torch.exp(-torch.sum(avg * torch.log(avg + 1e-10)))
+    return q, ind, commit, perp
+
+
+def quantize(ctx, sd, prefix, z):
+    """utils/train_utils.py:338-358 (2-D latent): 'b c h w -> b (h w) c' and back."""
+    B, C, H, W = z.shape
+    zt = z.permute(0, 2, 3, 1).reshape(B, H * W, C)
+    q, ind, commit, perp = vq_forward(ctx, sd, prefix, zt)
+    return q.reshape(B, H, W, C).permute(0, 3, 1, 2), ind, commit, perp
+
+
+# ----------------------------------------------------------------------------
+# Stage1 (trainers/stage1.py)
+# ----------------------------------------------------------------------------
+class Stage1Spec:
+    """Architecture of trainers/stage1.py:16-87 for a given config."""
+
+    def __init__(self, input_length, in_channels, init_dim=4, hid_dim=128, n_res=2,
+                 width_lf=8, width_hf=32, n_fft=4):
+        self.T, self.C = input_length, in_channels
+        self.rate_l = compute_downsample_rate(input_length, n_fft, width_lf)
+        self.rate_h = compute_downsample_rate(input_length, n_fft, width_hf)
+        nc = 2 * in_channels
+        self.enc_l = encoder_plan(init_dim, hid_dim, nc, self.rate_l, n_res)
+        self.enc_h = encoder_plan(init_dim, hid_dim, nc, self.rate_h, n_res)
+        self.dec_l = decoder_plan(init_dim, hid_dim, nc, self.rate_l, n_res)
+        self.dec_h = decoder_plan(init_dim, hid_dim, nc, self.rate_h, n_res)
+
+
+def stage1_targets(x):
+    """stage1.py:101-113: LF/HF targets via STFT band split and iSTFT."""
+    B, C, T = x.shape
+    xf = stft4(x)
+    x_l = linear_interp(istft4(band_lf(xf), C), T)
+    x_h = linear_interp(istft4(band_hf(xf), C), T)
+    return x_l, x_h
+
+
+def stage1_forward(ctx, sd, spec, x, return_x_rec=False):
+    """Stage1.forward (stage1.py:89-168) + the loss of training_step (stage1.py:170-176)."""
+    x_l, x_h = stage1_targets(x)
+    z_l = encoder_forward(ctx, sd, "encoder_l.", x, spec.enc_l, band_lf)
+    zq_l, s_l, commit_l, perp_l = quantize(ctx, sd, "vq_model_l.", z_l)
+    xh_l = decoder_forward(ctx, sd, "decoder_l.", zq_l, spec.dec_l, band_lf, spec.C, spec.T)
+    z_h = encoder_forward(ctx, sd, "encoder_h.", x, spec.enc_h, band_hf)
+    zq_h, s_h, commit_h, perp_h = quantize(ctx, sd, "vq_model_h.", z_h)
+    xh_h = decoder_forward(ctx, sd, "decoder_h.", zq_h, spec.dec_h, band_hf, spec.C, spec.T)
+    if return_x_rec:
+        return xh_l + xh_h
+    rl = F.mse_loss(x_l, xh_l)
+    rh = F.l1_loss(x_h, xh_h)
+    loss = rl + rh + commit_l + commit_h
+    return dict(loss=loss, recons_lf=rl, recons_hf=rh, commit_lf=commit_l, commit_hf=commit_h,
+                perp_lf=perp_l, perp_hf=perp_h, z_l=z_l, z_h=z_h, s_l=s_l, s_h=s_h,
+                xhat_l=xh_l, xhat_h=xh_h)
+
+
+def lr_at(step, base_lr, max_steps, warmup_rate=0.1, min_lr=1e-6):
+    """Closed form of linear_warmup_cosine_annealingLR (utils/train_utils.py:451-483)."""
+    warm = int(max_steps * warmup_rate)
+    if step < warm:
+        return base_lr * step / max(1, warm)
+    t = step - warm
+    T = max_steps - warm
+    return min_lr + (base_lr - min_lr) * (1 + math.cos(math.pi * t / T)) / 2
+
+
+# ----------------------------------------------------------------------------
+# MaskGIT loops (models/maskgit.py) with injectable randomness
+# ----------------------------------------------------------------------------
+def gamma_cosine(r):
+    """maskgit.py:218-228 ('cosine')."""
+    return np.cos(r * np.pi / 2)
+
+
+def random_mask_tokens(s, mask_token_id, ratio, rand):
+    """_randomly_mask_tokens (maskgit.py:194-216) with the randomness injected.
+
+    ratio: (b,) uniform[0,1) numpy; rand: (b,n) uniform torch.  mask=True keeps the token.
+    Ties in `rand` resolve like torch.topk (larger first, then lower index).
+    """
+    b, n = s.shape
+    n_unmask = np.clip(np.floor(gamma_cosine(ratio) * n), 0, n - 1).astype(int)
+    mask = torch.zeros((b, n), dtype=torch.bool)
+    for i in range(b):
+        ind = rand[i].topk(int(n_unmask[i]), dim=-1).indices
+        mask[i, ind] = True
+    s_M = torch.where(mask, s, torch.full_like(s, mask_token_id))
+    return s_M, mask
+
+
+def sample_step(logits, s, mask_token_id, t, T, unknown0, temperature, u_cat, u_gumbel):
+    """One iteration of first_pass/second_pass (maskgit.py:302-346) with injected noise.
+
+    Categorical sampling by inverse CDF of softmax(logits) at u_cat (b,n); Gumbel noise
+    -log(-log(u_gumbel)).  Returns the re-masked token set.
+    """
+    probs = F.softmax(logits.double(), dim=-1).float()
+    cdf = torch.cumsum(probs, dim=-1)
+    sampled = torch.searchsorted(cdf, u_cat.unsqueeze(-1) * cdf[..., -1:]).squeeze(-1)
+    sampled = sampled.clamp(max=logits.shape[-1] - 1)
+    unknown = s == mask_token_id
+    sampled = torch.where(unknown, sampled, s)
+    ratio = (t + 1) / T
+    mask_ratio = gamma_cosine(ratio)
+    sel = torch.gather(F.softmax(logits, dim=-1), -1, sampled.unsqueeze(-1)).squeeze(-1)
+    sel = torch.where(unknown, sel, torch.full_like(sel, float("inf")))
+    mask_len = torch.clip(torch.floor(unknown0.float() * mask_ratio), min=0.0)
+    g = -torch.log((-torch.log(u_gumbel.clamp(min=1e-20))).clamp(min=1e-20))
+    conf = torch.log(sel + 1e-5) + temperature * (1.0 - ratio) * g
+    k = int(mask_len.unique().item())
+    idx = torch.topk(conf, k=k, dim=-1, largest=False).indices
+    masking = torch.zeros_like(conf, dtype=torch.bool)
+    masking.scatter_(1, idx, True)
+    return torch.where(masking, torch.full_like(sampled, mask_token_id), sampled)

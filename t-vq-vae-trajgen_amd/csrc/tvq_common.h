@@ -1,0 +1,80 @@
+// Shared helpers for the TimeVQVAE gfx950 kernels (CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tvq.h"
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace tvq {
+
+// thread-local last-error message returned by tvq_last_error()
+void set_error(const char* fmt, ...);
+
+inline int launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return TVQ_ERR_LAUNCH;
+  }
+  return TVQ_OK;
+}
+
+#define TVQ_CHECK_ARG(cond, ...)          \
+  do {                                    \
+    if (!(cond)) {                        \
+      ::tvq::set_error(__VA_ARGS__);      \
+      return TVQ_ERR_ARG;                 \
+    }                                     \
+  } while (0)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum, deterministic (fixed tree).  `red` needs blockDim/64 floats.
+// Returns the total in every thread.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+__device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float snake_f(float x, float a, float inv_a) {
+  float s = sinf(a * x);
+  return x + inv_a * (s * s);
+}
+
+// counter-based RNG (Philox-lite / splitmix hash) for dropout masks: uniform in [0,1)
+__device__ __forceinline__ uint32_t hash_u32(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(x >> 32);
+}
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t ctr) {
+  return (hash_u32(seed * 0xD1B54A32D192ED03ull + ctr) >> 8) * (1.0f / 16777216.0f);
+}
+
+}  // namespace tvq

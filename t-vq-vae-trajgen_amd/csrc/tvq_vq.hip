@@ -1,0 +1,369 @@
+// VQ codebook kernels (K7/K8/K9 in SURVEY.md §2.2) for gfx950.
+//
+// assign: 32 token rows per 256-thread workgroup.  Each wave keeps its 16 rows'
+// x values in registers as fp32 MFMA A-fragments (D/4 VGPRs) for the whole
+// launch and streams the codebook through LDS in 128-code chunks; waves 0/1 own
+// code columns [0,64) of every chunk, waves 2/3 columns [64,128).  x.E^T runs on
+// v_mfma_f32_16x16x4_f32 (exact fp32 FMA chains); the argmin is a running
+// per-lane (value, index) pair merged across the 16 code lanes by shuffles and
+// across the two code halves through LDS.  The epilogue gathers q = E[idx],
+// writes the straight-through value and per-block commitment partials.
+#include <float.h>
+#include <limits.h>
+
+#include "tvq_common.h"
+
+namespace tvq {
+
+constexpr int VQ_BM = 32;   // token rows per workgroup
+constexpr int VQ_CK = 128;  // codes per LDS chunk
+
+// (v, i) "better" for argmin of t with first-index tie break
+__device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
+  return v < bv || (v == bv && i < bi);
+}
+
+__global__ void vq_sqnorm_kernel(const float* __restrict__ E, int K, int D, float* __restrict__ ee) {
+  int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const float* e = E + (int64_t)k * D;
+  float s = 0.f;
+  for (int d = 0; d < D; ++d) s = fmaf(e[d], e[d], s);
+  ee[k] = s;
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void vq_assign_kernel(
+    const float* __restrict__ x, int64_t M, int64_t N, int64_t sB, int64_t sN, int64_t sD,
+    const float* __restrict__ E, const float* __restrict__ ee, int K, int training,
+    float* __restrict__ quant, int64_t* __restrict__ idx, int32_t* __restrict__ idx32,
+    float* __restrict__ commit_partial) {
+  constexpr int S = D + 8;  // LDS row stride (floats): conflict-free ds_read_b128 B-fragments
+  constexpr int NQ = D / 16;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* es = smem;                       // [VQ_CK][S]
+  float* xx_s = smem + VQ_CK * S;         // [VQ_BM]
+  float* bv_s = xx_s + VQ_BM;             // [2][VQ_BM]
+  int* bi_s = (int*)(bv_s + 2 * VQ_BM);   // [2][VQ_BM]
+  float* red = (float*)(bi_s + 2 * VQ_BM);  // [4]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int rg = wid & 1, ch = wid >> 1;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * VQ_BM;
+
+  // ---- A fragments: x[row0 + rg*16 + r16][16q + 4g + j] ----
+  float areg[NQ * 4];
+  {
+    const int64_t m = row0 + rg * 16 + r16;
+    const bool ok = m < M;
+    const int64_t b = ok ? m / N : 0, n = ok ? m - b * N : 0;
+    const float* xr = x + b * sB + n * sN;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) areg[q * 4 + j] = ok ? xr[(int64_t)(16 * q + 4 * g + j) * sD] : 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NQ * 4; ++i) s = fmaf(areg[i], areg[i], s);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (ch == 0 && g == 0) xx_s[rg * 16 + r16] = s;
+  }
+
+  float bestv[4];
+  int besti[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { bestv[r] = INFINITY; besti[r] = INT_MAX; }
+
+  for (int c0 = 0; c0 < K; c0 += VQ_CK) {
+    __syncthreads();  // previous chunk consumed (and xx_s visible on first pass)
+    // stage codebook chunk [c0, c0+VQ_CK) into LDS (float4, coalesced along d)
+    for (int e = tid; e < VQ_CK * (D / 4); e += 256) {
+      const int c = e / (D / 4), d4 = e - c * (D / 4);
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (c0 + c < K) v = *reinterpret_cast<const float4*>(E + (int64_t)(c0 + c) * D + 4 * d4);
+      *reinterpret_cast<float4*>(es + c * S + 4 * d4) = v;
+    }
+    __syncthreads();
+    floatx4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const float* eb = es + (ch * 64 + r16) * S + 4 * g;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      float4 bq[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bq[t] = *reinterpret_cast<const float4*>(eb + t * 16 * S + 16 * q);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[t] = mfma16x16x4(areg[q * 4 + 0], bq[t].x, acc[t]);
+        acc[t] = mfma16x16x4(areg[q * 4 + 1], bq[t].y, acc[t]);
+        acc[t] = mfma16x16x4(areg[q * 4 + 2], bq[t].z, acc[t]);
+        acc[t] = mfma16x16x4(areg[q * 4 + 3], bq[t].w, acc[t]);
+      }
+    }
+    // C layout: acc[t][r] -> row (4g + r) of the wave's 16 rows, code col r16 of tile t
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int code = c0 + ch * 64 + t * 16 + r16;
+      const float e2 = code < K ? ee[code] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float xx = xx_s[rg * 16 + 4 * g + r];
+        float v = (xx - 2.0f * acc[t][r]) + e2;
+        if (code >= K) v = INFINITY;
+        if (v < bestv[r]) { bestv[r] = v; besti[r] = code; }  // codes increase: strict < keeps first
+      }
+    }
+  }
+  // merge across the 16 code lanes of each row group
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      float ov = __shfl_xor(bestv[r], o, 64);
+      int oi = __shfl_xor(besti[r], o, 64);
+      if (better(ov, oi, bestv[r], besti[r])) { bestv[r] = ov; besti[r] = oi; }
+    }
+  }
+  if (r16 == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bv_s[ch * VQ_BM + rg * 16 + 4 * g + r] = bestv[r];
+      bi_s[ch * VQ_BM + rg * 16 + 4 * g + r] = besti[r];
+    }
+  }
+  __syncthreads();
+  if (tid < VQ_BM) {
+    float v0 = bv_s[tid], v1 = bv_s[VQ_BM + tid];
+    int i0 = bi_s[tid], i1 = bi_s[VQ_BM + tid];
+    int bi = better(v1, i1, v0, i0) ? i1 : i0;
+    if (bi < 0 || bi >= K) bi = 0;  // all-NaN row: reference argmax would return a NaN slot
+    bi_s[tid] = bi;
+    const int64_t m = row0 + tid;
+    if (m < M) {
+      idx[m] = bi;
+      idx32[m] = bi;
+    }
+  }
+  __syncthreads();
+  // epilogue: q = E[idx] (pre-update codebook); straight-through value; commit partial
+  float csum = 0.f;
+  const bool dfast = (sD == 1);
+  for (int e = tid; e < VQ_BM * D; e += 256) {
+    int r, d;
+    if (dfast) { r = e / D; d = e - r * D; } else { d = e / VQ_BM; r = e - d * VQ_BM; }
+    const int64_t m = row0 + r;
+    if (m >= M) continue;
+    const int64_t b = m / N, n = m - b * N;
+    const int64_t off = b * sB + n * sN + (int64_t)d * sD;
+    const float qv = E[(int64_t)bi_s[r] * D + d];
+    if (training) {
+      const float xv = x[off];
+      const float st = xv + (qv - xv);
+      const float df = st - xv;
+      csum = fmaf(df, df, csum);
+      quant[off] = st;
+    } else {
+      quant[off] = qv;
+    }
+  }
+  if (training && commit_partial) {
+    csum = wave_sum(csum);
+    if (lane == 0) red[wid] = csum;
+    __syncthreads();
+    if (tid == 0) commit_partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  }
+}
+
+// One workgroup per code: scan idx32 in row order, compact the matching rows in
+// LDS (ballot prefix), accumulate their D values in row order.  Deterministic.
+__global__ __launch_bounds__(256) void vq_stats_kernel(
+    const float* __restrict__ x, int64_t M, int64_t N, int64_t sB, int64_t sN, int64_t sD, int D,
+    const int32_t* __restrict__ idx32, int32_t* __restrict__ counts, float* __restrict__ cs_batch,
+    float* __restrict__ es_batch) {
+  __shared__ int rows[256];
+  __shared__ int wcnt[4];
+  const int k = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float acc0 = 0.f, acc1 = 0.f;  // dims tid and tid+256 (D <= 512)
+  int count = 0;
+  for (int64_t base = 0; base < M; base += 256) {
+    const int64_t m = base + tid;
+    const bool match = (m < M) && (idx32[m] == k);
+    const uint64_t bal = __ballot(match);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wcnt[wid] = __popcll(bal);
+    __syncthreads();
+    int woff = 0, total = 0;
+    for (int w = 0; w < 4; ++w) { if (w < wid) woff += wcnt[w]; total += wcnt[w]; }
+    if (match) rows[woff + pre] = (int)(m - base);
+    __syncthreads();
+    if (es_batch) {
+      for (int j = 0; j < total; ++j) {
+        const int64_t mm = base + rows[j];
+        const int64_t b = mm / N, n = mm - b * N;
+        const float* xr = x + b * sB + n * sN;
+        if (tid < D) acc0 += xr[(int64_t)tid * sD];
+        if (tid + 256 < D) acc1 += xr[(int64_t)(tid + 256) * sD];
+      }
+    }
+    count += total;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    counts[k] = count;
+    cs_batch[k] = (float)count;
+  }
+  if (es_batch) {
+    if (tid < D) es_batch[(int64_t)k * D + tid] = acc0;
+    if (tid + 256 < D) es_batch[(int64_t)k * D + tid + 256] = acc1;
+  }
+}
+
+__global__ void vq_ema_kernel(const float* __restrict__ cs_batch, const float* __restrict__ es_batch,
+                              int D, float decay, float alpha, float* __restrict__ cluster_size,
+                              float* __restrict__ embed_avg) {
+  const int k = blockIdx.x;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    const int64_t o = (int64_t)k * D + d;
+    embed_avg[o] = fmaf(es_batch[o], alpha, embed_avg[o] * decay);
+  }
+  if (threadIdx.x == 0) cluster_size[k] = fmaf(cs_batch[k], alpha, cluster_size[k] * decay);
+}
+
+__global__ __launch_bounds__(256) void vq_finalize_kernel(
+    const float* __restrict__ cluster_size, const float* __restrict__ embed_avg, int K, int D,
+    float eps, float* __restrict__ embed, const int32_t* __restrict__ counts, int64_t M,
+    float* __restrict__ perplexity, const float* __restrict__ commit_partial, int64_t nparts,
+    float* __restrict__ commit) {
+  __shared__ float red[4];
+  const int k = blockIdx.x, tid = threadIdx.x;
+  if (embed) {
+    float s = 0.f;
+    for (int j = tid; j < K; j += 256) s += cluster_size[j];
+    const float tot = block_sum(s, red);
+    const float denom = tot + (float)K * eps;
+    const float c = (cluster_size[k] + eps) / denom * tot;
+    for (int d = tid; d < D; d += 256) embed[(int64_t)k * D + d] = embed_avg[(int64_t)k * D + d] / c;
+  }
+  if (k == 0) {
+    if (perplexity) {
+      float h = 0.f;
+      for (int j = tid; j < K; j += 256) {
+        const float p = (float)counts[j] / (float)M;
+        h += p * logf(p + 1e-10f);
+      }
+      const float ht = block_sum(h, red);
+      if (tid == 0) perplexity[0] = expf(-ht);
+    }
+    if (commit) {
+      float s = 0.f;
+      for (int64_t j = tid; j < nparts; j += 256) s += commit_partial[j];
+      const float st = block_sum(s, red);
+      if (tid == 0) commit[0] = st / ((float)M * (float)D);
+    }
+  }
+}
+
+__global__ void vq_backward_kernel(const float* __restrict__ x, const float* __restrict__ q,
+                                   const float* __restrict__ dq, const float* __restrict__ gc,
+                                   int64_t n, float inv_numel2, float* __restrict__ dx) {
+  const float c = gc ? gc[0] * inv_numel2 : 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dx[i] = dq[i] + c * (x[i] - q[i]);
+}
+
+}  // namespace tvq
+
+using namespace tvq;
+
+extern "C" int tvq_vq_sqnorm(const float* E, int64_t K, int64_t D, float* ee, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(E && ee && K > 0 && D > 0, "tvq_vq_sqnorm: bad arguments");
+  hipLaunchKernelGGL(vq_sqnorm_kernel, dim3((K + 255) / 256), dim3(256), 0, (hipStream_t)stream, E,
+                     (int)K, (int)D, ee);
+  return launch_status("tvq_vq_sqnorm");
+}
+
+extern "C" int64_t tvq_vq_assign_nblocks(int64_t M) { return (M + VQ_BM - 1) / VQ_BM; }
+
+extern "C" int tvq_vq_assign(const float* x, int64_t B, int64_t N, int64_t D, int64_t sB,
+                             int64_t sN, int64_t sD, const float* E, const float* ee, int64_t K,
+                             int training, float* quant, int64_t* idx, int32_t* idx32,
+                             float* commit_partial, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && E && ee && quant && idx && idx32 && B > 0 && N > 0 && K > 0,
+                "tvq_vq_assign: bad arguments");
+  TVQ_CHECK_ARG(!training || commit_partial, "tvq_vq_assign: training needs commit_partial");
+  TVQ_CHECK_ARG(K < INT_MAX, "tvq_vq_assign: K too large");
+  const int64_t M = B * N;
+  const int64_t nb = tvq_vq_assign_nblocks(M);
+  const size_t lds_tail = (VQ_BM + 4 * VQ_BM) * 4 + 16;
+  hipStream_t st = (hipStream_t)stream;
+#define TVQ_ASSIGN(DD)                                                                       \
+  case DD: {                                                                                 \
+    const size_t lds = (size_t)VQ_CK * (DD + 8) * 4 + lds_tail;                              \
+    hipLaunchKernelGGL(vq_assign_kernel<DD>, dim3(nb), dim3(256), lds, st, x, M, N, sB, sN, \
+                       sD, E, ee, (int)K, training, quant, idx, idx32, commit_partial);     \
+    break;                                                                                   \
+  }
+  switch (D) {
+    TVQ_ASSIGN(32)
+    TVQ_ASSIGN(64)
+    TVQ_ASSIGN(128)
+    default:
+      set_error("tvq_vq_assign: unsupported codebook dim %lld (32/64/128)", (long long)D);
+      return TVQ_ERR_ARG;
+  }
+#undef TVQ_ASSIGN
+  return launch_status("tvq_vq_assign");
+}
+
+extern "C" int tvq_vq_stats(const float* x, int64_t B, int64_t N, int64_t D, int64_t sB,
+                            int64_t sN, int64_t sD, const int32_t* idx32, int64_t K,
+                            int32_t* counts, float* cs_batch, float* es_batch,
+                            tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && idx32 && counts && cs_batch && B > 0 && N > 0 && K > 0 && D > 0 && D <= 512,
+                "tvq_vq_stats: bad arguments");
+  hipLaunchKernelGGL(vq_stats_kernel, dim3(K), dim3(256), 0, (hipStream_t)stream, x, B * N, N, sB,
+                     sN, sD, (int)D, idx32, counts, cs_batch, es_batch);
+  return launch_status("tvq_vq_stats");
+}
+
+extern "C" int tvq_vq_ema(const float* cs_batch, const float* es_batch, int64_t K, int64_t D,
+                          float decay, float* cluster_size, float* embed_avg,
+                          tvq_stream_t stream) {
+  TVQ_CHECK_ARG(cs_batch && es_batch && cluster_size && embed_avg && K > 0 && D > 0,
+                "tvq_vq_ema: bad arguments");
+  const float alpha = (float)(1.0 - (double)decay);
+  hipLaunchKernelGGL(vq_ema_kernel, dim3(K), dim3(128), 0, (hipStream_t)stream, cs_batch, es_batch,
+                     (int)D, decay, alpha, cluster_size, embed_avg);
+  return launch_status("tvq_vq_ema");
+}
+
+extern "C" int tvq_vq_finalize(const float* cluster_size, const float* embed_avg, int64_t K,
+                               int64_t D, float eps, float* embed, const int32_t* counts,
+                               int64_t M, float* perplexity, const float* commit_partial,
+                               int64_t nparts, float* commit, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(K > 0 && D > 0, "tvq_vq_finalize: bad arguments");
+  TVQ_CHECK_ARG(!embed || (cluster_size && embed_avg), "tvq_vq_finalize: embed needs buffers");
+  TVQ_CHECK_ARG(!perplexity || counts, "tvq_vq_finalize: perplexity needs counts");
+  TVQ_CHECK_ARG(!commit || commit_partial, "tvq_vq_finalize: commit needs partials");
+  const int grid = embed ? (int)K : 1;
+  hipLaunchKernelGGL(vq_finalize_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                     cluster_size, embed_avg, (int)K, (int)D, eps, embed, counts, M, perplexity,
+                     commit_partial, nparts, commit);
+  return launch_status("tvq_vq_finalize");
+}
+
+extern "C" int tvq_vq_backward(const float* x, const float* quant, const float* dquant,
+                               const float* gcommit, int64_t n, int64_t numel, float* dx,
+                               tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && quant && dquant && dx && n >= 0 && numel > 0, "tvq_vq_backward: bad args");
+  if (n == 0) return TVQ_OK;
+  const int64_t blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
+  hipLaunchKernelGGL(vq_backward_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, quant,
+                     dquant, gcommit, n, (float)(2.0 / (double)numel), dx);
+  return launch_status("tvq_vq_backward");
+}

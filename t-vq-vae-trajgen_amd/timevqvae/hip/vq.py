@@ -1,0 +1,104 @@
+"""VQ codebook ops on the HIP path (include/tvq.h §VQ codebook).
+
+Replaces EuclideanCodebook.forward + the straight-through/commitment part of
+VectorQuantize.forward (reference timevqvae/models/vq.py:197-251, 357-366):
+  assign (L2 + argmin + gather, fp32 MFMA)  ->  per-code stats (deterministic)
+  -> [optional all-reduce of the stats: sync_codebook, vq.py:229,234]
+  -> EMA blend -> Laplace-normalised codebook + perplexity + commit loss.
+"""
+import torch
+
+from ._native import call, ptr, stream_ptr, value
+
+
+def _same_dense_layout(a, b):
+    return a.shape == b.shape and a.stride() == b.stride()
+
+
+def _check_dense(x):
+    order = sorted(range(x.dim()), key=lambda i: -x.stride(i))
+    if not x.permute(order).is_contiguous():
+        raise ValueError("tvq VQ: input must be a dense (possibly permuted) tensor")
+
+
+def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema, decay, eps,
+                     sync=None):
+    """One codebook pass over x (B,N,D).
+
+    Returns (out, idx, commit, perplexity, counts):
+      out   = x + (E[idx]-x) if straight_through else E[idx]  (pre-update codebook)
+      idx   = int64 (B,N);  commit = mean((out-x)^2) (0-dim) if straight_through else None
+      perplexity 0-dim;     counts = int32 (K,)
+    With ema=True the buffers cluster_size/embed_avg/embed are updated in place.
+    """
+    B, N, D = x.shape
+    K = embed.shape[0]
+    M = B * N
+    _check_dense(x)
+    dev = x.device
+    s = stream_ptr()
+    ee = torch.empty(K, device=dev, dtype=torch.float32)
+    call("tvq_vq_sqnorm", ptr(embed), K, D, ptr(ee), s)
+    out = torch.empty_like(x)
+    assert _same_dense_layout(out, x)
+    idx = torch.empty((B, N), device=dev, dtype=torch.long)
+    idx32 = torch.empty(M, device=dev, dtype=torch.int32)
+    nb = value("tvq_vq_assign_nblocks", M)
+    partial = torch.empty(nb, device=dev, dtype=torch.float32) if straight_through else None
+    sB, sN, sD = x.stride()
+    call("tvq_vq_assign", ptr(x), B, N, D, sB, sN, sD, ptr(embed), ptr(ee), K,
+         int(bool(straight_through)), ptr(out), ptr(idx), ptr(idx32), ptr(partial), s)
+    counts = torch.empty(K, device=dev, dtype=torch.int32)
+    cs_b = torch.empty(K, device=dev, dtype=torch.float32)
+    es_b = torch.empty((K, D), device=dev, dtype=torch.float32) if ema else None
+    call("tvq_vq_stats", ptr(x), B, N, D, sB, sN, sD, ptr(idx32), K, ptr(counts), ptr(cs_b),
+         ptr(es_b), s)
+    perp = torch.empty((), device=dev, dtype=torch.float32)
+    commit = torch.empty((), device=dev, dtype=torch.float32) if straight_through else None
+    if ema:
+        if sync is not None:
+            sync(cs_b)
+            sync(es_b)
+            s = stream_ptr()
+        call("tvq_vq_ema", ptr(cs_b), ptr(es_b), K, D, float(decay), ptr(cluster_size),
+             ptr(embed_avg), s)
+        call("tvq_vq_finalize", ptr(cluster_size), ptr(embed_avg), K, D, float(eps), ptr(embed),
+             ptr(counts), M, ptr(perp), ptr(partial), nb if partial is not None else 0,
+             ptr(commit), s)
+    else:
+        call("tvq_vq_finalize", None, None, K, D, float(eps), None, ptr(counts), M, ptr(perp),
+             ptr(partial), nb if partial is not None else 0, ptr(commit), s)
+    return out, idx, commit, perp, counts
+
+
+class _VQStraightThrough(torch.autograd.Function):
+    """Training pass: forward = codebook pass with EMA; backward of vq.py:358,364."""
+
+    @staticmethod
+    def forward(ctx, x, embed, cluster_size, embed_avg, ema, decay, eps, sync):
+        out, idx, commit, perp, _ = vq_codebook_pass(
+            x, embed, cluster_size, embed_avg, straight_through=True, ema=ema, decay=decay,
+            eps=eps, sync=sync)
+        ctx.save_for_backward(x, out)
+        ctx.mark_non_differentiable(idx, perp)
+        return out, idx, commit, perp
+
+    @staticmethod
+    def backward(ctx, g_out, g_idx, g_commit, g_perp):
+        x, out = ctx.saved_tensors
+        if g_out is None:
+            g_out = torch.zeros_like(x)
+        elif not _same_dense_layout(g_out, x):
+            g = torch.empty_like(x)
+            g.copy_(g_out)
+            g_out = g
+        dx = torch.empty_like(x)
+        gc = g_commit.contiguous() if g_commit is not None else None
+        call("tvq_vq_backward", ptr(x), ptr(out), ptr(g_out), ptr(gc), x.numel(), x.numel(),
+             ptr(dx), stream_ptr())
+        return dx, None, None, None, None, None, None, None
+
+
+def vq_train(x, embed, cluster_size, embed_avg, *, ema, decay, eps, sync=None):
+    """Training-mode VQ with straight-through gradient. Returns (out, idx, commit, perp)."""
+    return _VQStraightThrough.apply(x, embed, cluster_size, embed_avg, ema, decay, eps, sync)

@@ -1,0 +1,311 @@
+"""Generate golden input/output vectors from the REFERENCE implementation.
+
+Runs only in the build container (it reads /root/reference, which does not
+exist on the GPU box).  The reference package cannot be imported as a whole
+(lightning, mlflow, x_transformers, traffic ... are absent), so the hot-path
+files are loaded by file path with minimal import stubs:
+
+  * timevqvae/models/vq.py            (torch + einops only)
+  * timevqvae/utils/train_utils.py     (stub: mlflow)
+  * timevqvae/models/vq_vae.py         (synthetic timevqvae.utils)
+  * timevqvae/trainers/stage1.py       (stub: lightning.LightningModule = nn.Module)
+  * timevqvae/models/maskgit.py        (stub transformer; sampling/masking loops only)
+
+Only the .npz outputs are committed (tests/golden/*.npz).  Usage:
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.npz
+"""
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from param_init import fill_state_dict  # noqa: E402
+
+REF = "/root/reference/timevqvae"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_reference():
+    """Load the hot-path reference files with import stubs; returns a namespace."""
+    # --- stubs for absent third-party packages (never executed on a hot path) ---
+    mlflow = types.ModuleType("mlflow")
+    mlflow.log_artifact = lambda *a, **k: None
+    sys.modules.setdefault("mlflow", mlflow)
+    lightning = types.ModuleType("lightning")
+    lightning.LightningModule = nn.Module
+    sys.modules.setdefault("lightning", lightning)
+
+    pkg = types.ModuleType("timevqvae")
+    pkg.__path__ = []
+    sys.modules["timevqvae"] = pkg
+    vq = _load("ref_vq", f"{REF}/models/vq.py")
+    tu = _load("ref_train_utils", f"{REF}/utils/train_utils.py")
+    utils = types.ModuleType("timevqvae.utils")
+    for k in dir(tu):
+        if not k.startswith("__"):
+            setattr(utils, k, getattr(tu, k))
+    sys.modules["timevqvae.utils"] = utils
+    vqvae = _load("ref_vq_vae", f"{REF}/models/vq_vae.py")
+    models = types.ModuleType("timevqvae.models")
+    models.VectorQuantize = vq.VectorQuantize
+    models.VQVAEEncoder = vqvae.VQVAEEncoder
+    models.VQVAEDecoder = vqvae.VQVAEDecoder
+    models.BidirectionalTransformer = object  # stub: x_transformers is absent
+    sys.modules["timevqvae.models"] = models
+    stage1 = _load("ref_stage1", f"{REF}/trainers/stage1.py")
+    maskgit = _load("ref_maskgit", f"{REF}/models/maskgit.py")
+    return types.SimpleNamespace(vq=vq, tu=tu, vqvae=vqvae, stage1=stage1, maskgit=maskgit)
+
+
+def _sd(module, prefix):
+    return {f"{prefix}{k}": v.detach().cpu().numpy().copy() for k, v in module.state_dict().items()}
+
+
+# --------------------------------------------------------------------------- G0/G1
+def gen_vq(ref):
+    out = {}
+    # G0: the reference's own __main__ known-answer test (vq.py:410-424)
+    torch.manual_seed(0)
+    x = torch.rand((1024, 32, 128))
+    vqm = ref.vq.VectorQuantize(dim=128, codebook_size=512)
+    q, ind, loss, perp = vqm(x)
+    out["kat_ind0"] = ind[0].numpy().astype(np.int64)
+    out["kat_n_unique"] = np.array(len(torch.unique(ind)))
+    out["kat_commit"] = np.array(float(loss["commit_loss"]))
+    out["kat_perplexity"] = np.array(float(perp))
+    out["kat_cs_sum"] = np.array(float(vqm._codebook.cluster_size.sum()))
+    out["kat_embed0"] = vqm._codebook.embed[0, :4].numpy().copy()
+    np.savez_compressed(f"{OUT}/g0_vq_kat.npz", **out)
+
+    # G1: full vectors, random codebook and data-near codebook, train (EMA) mode
+    for variant in ("random", "near"):
+        g = torch.Generator().manual_seed(1234 if variant == "random" else 4321)
+        B, N, D, K = 8, 128, 128, 512  # M = 1024 rows
+        x = torch.randn(B, N, D, generator=g)
+        vqm = ref.vq.VectorQuantize(dim=D, codebook_size=K)
+        if variant == "near":
+            flat = x.reshape(-1, D)
+            perm = torch.randperm(flat.shape[0], generator=g)[:K]
+            E = flat[perm] + 0.05 * torch.randn(K, D, generator=g)
+            vqm._codebook.embed.data.copy_(E)
+            vqm._codebook.embed_avg.data.copy_(E)
+        # pre-existing EMA state so the blend is exercised
+        vqm._codebook.cluster_size.data.copy_(torch.rand(K, generator=g) * 3)
+        d = {
+            "x": x.numpy(),
+            "embed": vqm._codebook.embed.numpy().copy(),
+            "embed_avg": vqm._codebook.embed_avg.numpy().copy(),
+            "cluster_size": vqm._codebook.cluster_size.numpy().copy(),
+        }
+        # eval-mode assignment first (no EMA), then one train-mode forward
+        vqm.eval()
+        q_e, ind_e, _, perp_e = vqm(x)
+        d["eval_ind"] = ind_e.numpy().astype(np.int64)
+        d["eval_perplexity"] = np.array(float(perp_e))
+        vqm.train()
+        xg = x.clone().requires_grad_(True)
+        q, ind, loss, perp = vqm(xg)
+        (q.square().sum() * 0.5 + loss["loss"].sum()).backward()
+        d["ind"] = ind.numpy().astype(np.int64)
+        d["commit"] = np.array(float(loss["commit_loss"]))
+        d["perplexity"] = np.array(float(perp))
+        d["post_cluster_size"] = vqm._codebook.cluster_size.numpy().copy()
+        d["post_embed_avg"] = vqm._codebook.embed_avg.numpy().copy()
+        d["post_embed"] = vqm._codebook.embed.numpy().copy()
+        d["x_grad"] = xg.grad.numpy()  # d/dx [0.5*sum(q_st^2) + commit]
+        # fp64 top-2 gap per row (to qualify near-ties)
+        f64 = x.double().reshape(-1, D)
+        E64 = torch.from_numpy(d["embed"]).double()
+        dist = (f64.pow(2).sum(1, keepdim=True) - 2 * f64 @ E64.t() + E64.pow(2).sum(1)[None])
+        top2 = dist.topk(2, dim=1, largest=False).values
+        d["gap64"] = (top2[:, 1] - top2[:, 0]).numpy()
+        np.savez_compressed(f"{OUT}/g1_vq_{variant}.npz", **d)
+
+
+# --------------------------------------------------------------------------- G2
+def gen_stft(ref):
+    tu = ref.tu
+    d = {}
+    for T in (128, 256):
+        g = torch.Generator().manual_seed(7 + T)
+        x = torch.cumsum(0.1 * torch.randn(4, 6, T, generator=g), -1)
+        xf = tu.time_to_timefreq(x, 4, 6)
+        d[f"x_T{T}"] = x.numpy()
+        d[f"xf_T{T}"] = xf.numpy()
+        d[f"lf_copy_T{T}"] = tu.zero_pad_high_freq(xf, copy=True).numpy()
+        d[f"hf_copy_T{T}"] = tu.zero_pad_low_freq(xf, copy=True).numpy()
+        u_l = tu.zero_pad_high_freq(xf)
+        u_h = tu.zero_pad_low_freq(xf)
+        d[f"u_l_T{T}"] = u_l.numpy()
+        d[f"u_h_T{T}"] = u_h.numpy()
+        x_l = torch.nn.functional.interpolate(tu.timefreq_to_time(u_l, 4, 6), T, mode="linear")
+        x_h = torch.nn.functional.interpolate(tu.timefreq_to_time(u_h, 4, 6), T, mode="linear")
+        d[f"x_l_T{T}"] = x_l.numpy()
+        d[f"x_h_T{T}"] = x_h.numpy()
+        # decoder-side istft on a 2x-upsampled random image (W = 2*T frames)
+        img = torch.randn(4, 12, 3, 2 * T, generator=g)
+        d[f"dec_img_T{T}"] = img.numpy()
+        d[f"dec_istft_lf_T{T}"] = tu.timefreq_to_time(tu.zero_pad_high_freq(img), 4, 6).numpy()
+        d[f"dec_istft_hf_T{T}"] = tu.timefreq_to_time(tu.zero_pad_low_freq(img), 4, 6).numpy()
+        d[f"snake_a_in_T{T}"] = img[:, :, :, :7].numpy()
+    np.savez_compressed(f"{OUT}/g2_stft.npz", **d)
+
+
+# --------------------------------------------------------------------------- G3/G4
+def _stage1_config(init_dim, hid_dim, K):
+    return {
+        "VQ-VAE": {"n_fft": 4, "codebook_sizes": {"lf": K, "hf": K}},
+        "encoder": {"init_dim": init_dim, "hid_dim": hid_dim, "n_resnet_blocks": 2,
+                    "downsampled_width": {"lf": 8, "hf": 32}},
+        "decoder": {"n_resnet_blocks": 2},
+        "exp_params": {"lr": 1e-3, "linear_warmup_rate": 0.1},
+        "trainer_params": {"max_steps": {"stage1": 1000, "stage2": 1000}},
+    }
+
+
+def gen_stage1(ref, tag, B, C, T, K, init_dim, hid_dim, seed):
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    cfg = _stage1_config(init_dim, hid_dim, K)
+    model = ref.stage1.Stage1(T, C, cfg)
+    # dropout off so the train-mode step is deterministic (SURVEY §7 hard parts)
+    for m in model.modules():
+        if isinstance(m, nn.Dropout):
+            m.p = 0.0
+    g = torch.Generator().manual_seed(seed + 1)
+    x = torch.cumsum(0.1 * torch.randn(B, C, T, generator=g), -1)
+    x = 2 * (x - x.amin(0, keepdim=True)) / (x.amax(0, keepdim=True) - x.amin(0, keepdim=True) + 1e-8) - 1
+    y = torch.randint(0, 5, (B, 1), generator=g)
+    d = {"x": x.numpy(), "y": y.numpy(), "cfg": np.array([B, C, T, K, init_dim, hid_dim]),
+         "seed": np.array(seed)}
+    # parameters/buffers from the shared deterministic rule (param_init.py)
+    vals = fill_state_dict(model.state_dict(), seed)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()}, strict=False)
+
+    # eval-mode reconstruction on the initial state
+    model.eval()
+    with torch.no_grad():
+        d["eval_x_rec"] = model((x, y), 0, return_x_rec=True).numpy()
+        z = model.encoder_l(x)
+        d["eval_z_l"] = z.numpy()
+        _, s, _, _ = ref.tu.quantize(z, model.vq_model_l)
+        d["eval_s_l"] = s.numpy().astype(np.int64)
+        z = model.encoder_h(x)
+        d["eval_z_h"] = z.numpy()
+        _, s, _, _ = ref.tu.quantize(z, model.vq_model_h)
+        d["eval_s_h"] = s.numpy().astype(np.int64)
+
+    # train-mode forward + backward (one step's gradients)
+    model.train()
+    cap = {}
+
+    def hook(name):
+        def f(mod, inp, out):
+            if isinstance(out, tuple):
+                cap[name] = out[0].detach().clone()
+                cap[name + "_ind"] = out[1].detach().clone()
+            else:
+                cap[name] = out.detach().clone()
+        return f
+
+    for name in ("encoder_l", "encoder_h", "vq_model_l", "vq_model_h", "decoder_l", "decoder_h"):
+        getattr(model, name).register_forward_hook(hook(name))
+    recons, vq_losses, perps = model((x, y), 0)
+    loss = recons["LF.time"] + recons["HF.time"] + vq_losses["LF"]["loss"] + vq_losses["HF"]["loss"]
+    loss.backward()
+    d["train_loss"] = np.array(float(loss))
+    d["train_recons_lf"] = np.array(float(recons["LF.time"]))
+    d["train_recons_hf"] = np.array(float(recons["HF.time"]))
+    d["train_commit_lf"] = np.array(float(vq_losses["LF"]["commit_loss"]))
+    d["train_commit_hf"] = np.array(float(vq_losses["HF"]["commit_loss"]))
+    d["train_perp_lf"] = np.array(float(perps["LF"]))
+    d["train_perp_hf"] = np.array(float(perps["HF"]))
+    for k, v in cap.items():
+        d[f"train_{k}"] = v.numpy()
+    for k, p in model.named_parameters():
+        if p.grad is not None:
+            d[f"grad/{k}"] = p.grad.numpy().copy()
+    d.update({f"post/{k}": v.detach().numpy().copy() for k, v in model.named_buffers()})
+    np.savez_compressed(f"{OUT}/g3_stage1_{tag}.npz", **d)
+
+
+# --------------------------------------------------------------------------- G5
+def gen_maskgit(ref):
+    MG = ref.maskgit.MaskGIT
+    mg = MG.__new__(MG)
+    nn.Module.__init__(mg)
+    K = 16
+    mg.T = {"lf": 10, "hf": 1}
+    mg.mask_token_ids = {"lf": K, "hf": K}
+    mg.choice_temperature_l, mg.choice_temperature_h = 10.0, 4.0
+    mg.cfg_scale = 1.0
+    mg.gamma = mg.gamma_func("cosine")
+    mg.num_tokens_l, mg.num_tokens_h = 6, 12
+
+    # deterministic stub transformers: logits = table lookup over (position, input token)
+    gt = torch.Generator().manual_seed(99)
+    tab_l = torch.randn(6, K + 1, K, generator=gt) * 2
+    tab_h = torch.randn(12, K + 1, K, generator=gt) * 2
+    tab_hl = torch.randn(K + 1, K, generator=gt)
+
+    def tf_l(s_l, class_condition=None):
+        return tab_l[torch.arange(6)[None, :], s_l]
+
+    def tf_h(s_l, s_h, class_condition=None):
+        return tab_h[torch.arange(12)[None, :], s_h] + tab_hl[s_l].mean(1, keepdim=True)
+
+    mg.transformer_l, mg.transformer_h = tf_l, tf_h
+    d = {"tab_l": tab_l.numpy(), "tab_h": tab_h.numpy(), "tab_hl": tab_hl.numpy(), "K": np.array(K)}
+    torch.manual_seed(5)
+    s_l, s_h = mg.iterative_decoding(num=8, device="cpu")
+    d["dec_s_l"] = s_l.numpy().astype(np.int64)
+    d["dec_s_h"] = s_h.numpy().astype(np.int64)
+
+    # training-time masking
+    np.random.seed(11)
+    torch.manual_seed(12)
+    s = torch.randint(0, K, (32, 24), generator=torch.Generator().manual_seed(13))
+    s_M, mask = mg._randomly_mask_tokens(s, K, "cpu")
+    d["mask_s"] = s.numpy().astype(np.int64)
+    d["mask_s_M"] = s_M.numpy().astype(np.int64)
+    d["mask_mask"] = mask.numpy()
+
+    # mask_by_random_topk with fixed probs
+    torch.manual_seed(21)
+    probs = torch.rand(4, 12)
+    probs[:, :3] = torch.inf
+    masking = mg.mask_by_random_topk(torch.full((4, 1), 5.0), probs, temperature=3.0)
+    d["topk_probs"] = probs.numpy()
+    d["topk_masking"] = masking.numpy()
+    np.savez_compressed(f"{OUT}/g5_maskgit.npz", **d)
+
+
+def main():
+    torch.set_num_threads(8)
+    ref = load_reference()
+    gen_vq(ref)
+    gen_stft(ref)
+    gen_stage1(ref, "small", B=4, C=6, T=128, K=64, init_dim=4, hid_dim=32, seed=3)
+    gen_stage1(ref, "cfgB", B=2, C=6, T=256, K=512, init_dim=4, hid_dim=128, seed=5)
+    gen_maskgit(ref)
+    for f in sorted(os.listdir(OUT)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+if __name__ == "__main__":
+    main()
