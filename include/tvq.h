@@ -92,6 +92,122 @@ int tvq_vq_backward(const float* x, const float* quant, const float* dquant,
                     const float* gcommit, int64_t n, int64_t numel, float* dx,
                     tvq_stream_t stream);
 
+
+/* ------------------------------------------------------------ STFT / iSTFT
+ * time_to_timefreq + zero_pad_{high,low}_freq(copy=True) + the stage1 targets
+ * (train_utils.py:293-321,361-386; vq_vae.py:179-180; stage1.py:101-113) in one
+ * pass: x (B,C,T) -> raw (B,2C,3,T+1) = time_to_timefreq(x), enc_l/enc_h the
+ * band-copied encoder inputs, tgt_l/tgt_h (B,C,T) = interp(istft(band(stft(x))));
+ * any output may be NULL. */
+int tvq_stft_encode(const float* x, int64_t B, int64_t C, int64_t T, float* raw, float* enc_l,
+                    float* enc_h, float* tgt_l, float* tgt_h, tvq_stream_t stream);
+
+/* VQVAEDecoder tail (vq_vae.py:258-262): zero_pad band mask (band 0 = LF keeps
+ * bin 0, 1 = HF keeps bins 1,2, 2 = none: plain timefreq_to_time) -> istft ->
+ * nn.Upsample(Tout, 'linear') (identity when Tout == W-1).
+ * h (B,2C,3,W) -> y (B,C,Tout).  bwd: dy (B,C,Tout) -> dh (B,2C,3,W). */
+int tvq_istft_decode(const float* h, int64_t B, int64_t C, int64_t W, int64_t band, int64_t Tout,
+                     float* y, tvq_stream_t stream);
+int tvq_istft_decode_bwd(const float* dy, int64_t B, int64_t C, int64_t W, int64_t band,
+                         int64_t Tout, float* dh, tvq_stream_t stream);
+
+/* ----------------------------------------------------------- convolutions
+ * nn.Conv2d / nn.ConvTranspose2d / nn.Conv1d of VQVAEEncBlock, ResBlock,
+ * VQVAEDecBlock, the decoder tail and Upscale (vq_vae.py:13-121,238-251;
+ * bidirectional_transformer.py:12-30).  NCHW fp32; supported kernels:
+ * (KH,KW,SW) = (3,4,2) [replicate or zero pad], (3,3,1), (1,1,1), (1,3,1);
+ * padding (KH/2, (KW-1)/2).  Epilogue of the forward conv: + bias, optional
+ * dropout (counter-based mask keyed by (*seed_ptr, offset) and the flat output
+ * index: the device seed advances once per step so graph replays differ) and + residual
+ * (ResBlock: proj(x) + Dropout(conv(..)), vq_vae.py:52,62). */
+int tvq_conv_out_width(int64_t Win, int64_t KW, int64_t SW, int64_t transposed);
+int tvq_conv2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi, const float* w,
+                   const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t SW,
+                   int64_t replicate, float* y, const float* residual, float drop_p,
+                   const int64_t* seed_ptr, uint64_t offset, tvq_stream_t stream);
+int tvq_convT2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi, const float* w,
+                    const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t SW, float* y,
+                    const float* residual, tvq_stream_t stream);
+int64_t tvq_conv2d_dgrad_workspace(int64_t B, int64_t Ci, int64_t H, int64_t Wi, int64_t KH,
+                                   int64_t KW, int64_t replicate);
+int tvq_conv2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t Wo,
+                     const float* w, int64_t Ci, int64_t KH, int64_t KW, int64_t SW,
+                     int64_t replicate, float* dx, int64_t Wi, float* workspace,
+                     tvq_stream_t stream);
+int tvq_convT2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t Wo,
+                      const float* w, int64_t Ci, int64_t KH, int64_t KW, int64_t SW, float* dx,
+                      int64_t Wi, tvq_stream_t stream);
+int64_t tvq_conv_wgrad_workspace(int64_t N, int64_t C, int64_t KH, int64_t KW, int64_t B,
+                                 int64_t Hout, int64_t Wo);
+int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
+                     const float* dy, int64_t Co, int64_t Wo, int64_t KH, int64_t KW, int64_t SW,
+                     int64_t replicate, float* dw, int64_t accumulate, float* workspace,
+                     tvq_stream_t stream);
+int tvq_convT2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
+                      const float* dy, int64_t Co, int64_t Wo, int64_t KH, int64_t KW, int64_t SW,
+                      float* dw, int64_t accumulate, float* workspace, tvq_stream_t stream);
+/* bias gradients: out[c] (+)= sum_{b,p} x[b,c,p] */
+int64_t tvq_channel_sum_workspace(int64_t B, int64_t C, int64_t HW);
+int tvq_channel_sum(const float* x, int64_t B, int64_t C, int64_t HW, float* out,
+                    int64_t accumulate, float* workspace, tvq_stream_t stream);
+
+/* ------------------------------------------------ BatchNorm + SnakeActivation
+ * nn.BatchNorm2d/1d (momentum 0.1) followed by SnakeActivation
+ * x + (1/a) sin(a x)^2 (train_utils.py:421-448) when snake_a != NULL
+ * (VQVAEEncBlock/DecBlock block.1-2, ResBlock convs.2-3).  fp64 statistics.
+ * scale_shift: 2*C floats kept for the backward; workspace: tvq_bn_workspace bytes. */
+int64_t tvq_bn_workspace(int64_t B, int64_t C, int64_t HW);
+int tvq_bn_train_fwd(const float* x, int64_t B, int64_t C, int64_t HW, const float* w,
+                     const float* b, float* running_mean, float* running_var,
+                     int64_t* num_batches_tracked, float momentum, float eps,
+                     const float* snake_a, float* y, float* save_mean, float* save_invstd,
+                     float* scale_shift, void* workspace, tvq_stream_t stream);
+int tvq_bn_eval_fwd(const float* x, int64_t B, int64_t C, int64_t HW, const float* w,
+                    const float* b, const float* running_mean, const float* running_var,
+                    float eps, const float* snake_a, float* y, float* scale_shift,
+                    tvq_stream_t stream);
+int tvq_bn_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t HW, const float* w,
+               const float* snake_a, const float* save_mean, const float* save_invstd,
+               const float* scale_shift, float* dx, float* dw, float* db, float* da,
+               int64_t accumulate, void* workspace, tvq_stream_t stream);
+/* standalone Snake (ResBlock convs.0, vq_vae.py:31); a: (C,) */
+int tvq_snake_fwd(const float* x, int64_t B, int64_t C, int64_t HW, const float* a, float* y,
+                  tvq_stream_t stream);
+int64_t tvq_snake_workspace(int64_t B, int64_t C, int64_t HW);
+int tvq_snake_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t HW,
+                  const float* a, float* dx, float* da, int64_t accumulate, void* workspace,
+                  tvq_stream_t stream);
+/* backward of the dropout fused in tvq_conv2d_fwd (same seed, same flat index) */
+int tvq_dropout_bwd(const float* dy, int64_t n, float p, const int64_t* seed_ptr,
+                    uint64_t offset, float* dx, tvq_stream_t stream);
+
+/* ------------------------------------------------------------- dense GEMM
+ * nn.Linear and friends: C[m,n] = epi(alpha * sum_k A(m,k) B(k,n)),
+ * A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn]; epi: + bias[n],
+ * act (0 none, 1 GELU-erf), + R[m*ldr+n], accumulate (C +=).  Workspace
+ * (tvq_gemm_workspace floats) enables deterministic split-K. */
+int64_t tvq_gemm_workspace(int64_t M, int64_t N, int64_t K);
+int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
+             float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha,
+             const float* bias, const float* R, int64_t ldr, int64_t act, int64_t accumulate,
+             float* workspace, tvq_stream_t stream);
+
+/* ------------------------------------------------------ losses, optimizer
+ * F.mse_loss (kind 0) / F.l1_loss (kind 1) means (stage1.py:129,133); backward
+ * gives d/d target (the reconstruction is the second argument there). */
+int64_t tvq_loss_workspace(int64_t n);
+int tvq_loss_fwd(const float* input, const float* target, int64_t n, int64_t kind, float* out,
+                 float* workspace, tvq_stream_t stream);
+int tvq_loss_bwd(const float* input, const float* target, int64_t n, int64_t kind,
+                 const float* gout, float* dtarget, tvq_stream_t stream);
+/* torch.optim.AdamW step over a flat buffer (stage1.py:230, stage2.py:113);
+ * lr_step = device {lr, step}; tvq_adamw_begin increments step and writes lr when
+ * lr >= 0 (pass -1 inside a captured graph and set lr[0] before each replay). */
+int tvq_adamw_begin(float* lr_step, float lr, tvq_stream_t stream);
+int tvq_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+              const float* lr_step, float beta1, float beta2, float eps, float weight_decay,
+              tvq_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,6 +73,12 @@ __device__ __forceinline__ uint32_t hash_u32(uint64_t x) {
   x ^= x >> 31;
   return (uint32_t)(x >> 32);
 }
+// dropout stream key: device-resident seed (advanced once per training step, so
+// hipGraph replays draw fresh masks) mixed with a host offset (call site / call count)
+__device__ __forceinline__ uint64_t mix_seed(const int64_t* seed_ptr, uint64_t offset) {
+  const uint64_t s = seed_ptr ? (uint64_t)(*seed_ptr) : 0ull;
+  return (s * 0x9E3779B97F4A7C15ull) ^ (offset * 0xC2B2AE3D27D4EB4Full + 0x165667B19E3779F9ull);
+}
 __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t ctr) {
   return (hash_u32(seed * 0xD1B54A32D192ED03ull + ctr) >> 8) * (1.0f / 16777216.0f);
 }

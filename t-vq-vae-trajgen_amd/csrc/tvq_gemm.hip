@@ -1,0 +1,206 @@
+// Dense fp32 GEMM on gfx950 MFMA (v_mfma_f32_16x16x4_f32) for the Linear layers
+// (decoder Linear(T,T) vq_vae.py:255,263; transformer projections/FFN; pred_head).
+//
+//   C[m, n] = epi( sum_k A(m,k) * B(k,n) )
+//   A(m,k) = A[m*sam + k*sak],  B(k,n) = B[k*sbk + n*sbn]   (any strides: X W^T,
+//   dY W, dY^T X are all the same kernel)
+//   epi: + bias[n], GELU (erf), + R[m*ldr + n], or accumulate into C.
+// Split-K over gridDim.z writes fp32 slabs reduced in split order (deterministic).
+#include <math.h>
+
+#include "tvq_common.h"
+
+namespace tvq {
+
+struct GemmArgs {
+  const float* A;
+  const float* B;
+  float* C;
+  int M, N, K;
+  int64_t sam, sak, sbk, sbn, ldc;
+  const float* bias;
+  const float* R;
+  int64_t ldr;
+  int act;         // 0 none, 1 GELU(erf)
+  int accumulate;  // C += result
+  float alpha;
+  int kper;        // K range per split
+  float* slab;     // split-K partials [split][M][N] (nullptr: write C directly)
+};
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+__device__ __forceinline__ float apply_epi(const GemmArgs& g, int m, int n, float v) {
+  v *= g.alpha;
+  if (g.bias) v += g.bias[n];
+  if (g.act == 1) v = gelu_erf(v);
+  if (g.R) v += g.R[(int64_t)m * g.ldr + n];
+  if (g.accumulate) v += g.C[(int64_t)m * g.ldc + n];
+  return v;
+}
+
+template <int TM, int TN, int WM, int WN>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+  constexpr int BK = 16;
+  constexpr int FM = TM / WM / 16, FN = TN / WN / 16;
+  constexpr int SA = ((TM + 31) / 32) * 32 + 16;
+  constexpr int SB = ((TN + 31) / 32) * 32 + 16;
+  constexpr int A_PER = TM * BK / 256, B_PER = TN * BK / 256;
+  static_assert(A_PER >= 1 && B_PER >= 1, "tile too small");
+  __shared__ float As[BK * SA];
+  __shared__ float Bs[BK * SB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid % WM, wn = wid / WM;
+  const int m0 = blockIdx.x * TM, n0 = blockIdx.y * TN;
+  const int kb = blockIdx.z * g.kper;
+  const int ke = min(g.K, kb + g.kper);
+  const bool a_kfast = (g.sak == 1);
+  const bool b_kfast = (g.sbn != 1);
+
+  float ra[A_PER], rb[B_PER];
+  int a_m[A_PER], a_k[A_PER], b_k[B_PER], b_n[B_PER];
+#pragma unroll
+  for (int j = 0; j < A_PER; ++j) {
+    const int e = tid + j * 256;
+    if (a_kfast) { a_k[j] = e % BK; a_m[j] = e / BK; } else { a_m[j] = e % TM; a_k[j] = e / TM; }
+  }
+#pragma unroll
+  for (int j = 0; j < B_PER; ++j) {
+    const int e = tid + j * 256;
+    if (b_kfast) { b_k[j] = e % BK; b_n[j] = e / BK; } else { b_n[j] = e % TN; b_k[j] = e / TN; }
+  }
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < A_PER; ++j) {
+      const int m = m0 + a_m[j], k = k0 + a_k[j];
+      ra[j] = (m < g.M && k < ke) ? g.A[(int64_t)m * g.sam + (int64_t)k * g.sak] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < B_PER; ++j) {
+      const int n = n0 + b_n[j], k = k0 + b_k[j];
+      rb[j] = (n < g.N && k < ke) ? g.B[(int64_t)k * g.sbk + (int64_t)n * g.sbn] : 0.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < A_PER; ++j) As[a_k[j] * SA + a_m[j]] = ra[j];
+#pragma unroll
+    for (int j = 0; j < B_PER; ++j) Bs[b_k[j] * SB + b_n[j]] = rb[j];
+  };
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15, g4 = lane >> 4;
+  if (kb < ke) {
+    load(kb);
+    for (int k0 = kb; k0 < ke; k0 += BK) {
+      __syncthreads();
+      store();
+      __syncthreads();
+      if (k0 + BK < ke) load(k0 + BK);
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 4) {
+        float af[FM], bf[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = As[(kk + g4) * SA + (wm * FM + i) * 16 + r16];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[j] = Bs[(kk + g4) * SB + (wn * FN + j) * 16 + r16];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x4(af[i], bf[j], acc[i][j]);
+      }
+    }
+  }
+  // C layout: acc[i][j][r] -> row m0 + (wm*FM+i)*16 + 4*g4 + r, col n0 + (wn*FN+j)*16 + r16
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + (wm * FM + i) * 16 + 4 * g4 + r;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + (wn * FN + j) * 16 + r16;
+        if (n >= g.N) continue;
+        if (g.slab) {
+          g.slab[((int64_t)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][r];
+        } else {
+          g.C[(int64_t)m * g.ldc + n] = apply_epi(g, m, n, acc[i][j][r]);
+        }
+      }
+    }
+}
+
+__global__ void gemm_splitk_reduce_kernel(GemmArgs g, int splits) {
+  const int64_t tot = (int64_t)g.M * g.N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += g.slab[(int64_t)z * tot + i];
+    const int m = (int)(i / g.N), n = (int)(i - (int64_t)m * g.N);
+    g.C[(int64_t)m * g.ldc + n] = apply_epi(g, m, n, s);
+  }
+}
+
+static int gemm_splits(int M, int N, int K, int tiles) {
+  if (K < 1024 || tiles >= 128) return 1;
+  int s = (512 + tiles - 1) / tiles;
+  const int maxs = K / 256;
+  if (s > maxs) s = maxs;
+  if (s > 64) s = 64;
+  return s < 1 ? 1 : s;
+}
+
+}  // namespace tvq
+
+using namespace tvq;
+
+extern "C" int64_t tvq_gemm_workspace(int64_t M, int64_t N, int64_t K) {
+  const int TM = M >= 128 ? 128 : 64, TN = N >= 64 ? 64 : 32;
+  const int tiles = (int)(((M + TM - 1) / TM) * ((N + TN - 1) / TN));
+  const int s = gemm_splits((int)M, (int)N, (int)K, tiles);
+  return s > 1 ? (int64_t)s * M * N : 0;
+}
+
+extern "C" int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
+                        int64_t sbn, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                        float alpha, const float* bias, const float* R, int64_t ldr, int64_t act,
+                        int64_t accumulate, float* workspace, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0, "tvq_gemm: bad arguments");
+  GemmArgs g;
+  g.A = A; g.B = B; g.C = C;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.sam = sam; g.sak = sak; g.sbk = sbk; g.sbn = sbn; g.ldc = ldc;
+  g.bias = bias; g.R = R; g.ldr = ldr; g.act = (int)act; g.accumulate = (int)accumulate;
+  g.alpha = alpha;
+  const int TM = M >= 128 ? 128 : 64, TN = N >= 64 ? 64 : 32;
+  const int tiles = (int)(((M + TM - 1) / TM) * ((N + TN - 1) / TN));
+  int splits = gemm_splits((int)M, (int)N, (int)K, tiles);
+  if (splits > 1 && !workspace) splits = 1;
+  int kper = (int)((K + splits - 1) / splits);
+  kper = (kper + 15) / 16 * 16;
+  splits = (int)((K + kper - 1) / kper);
+  g.kper = kper;
+  g.slab = splits > 1 ? workspace : nullptr;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((M + TM - 1) / TM), (unsigned)((N + TN - 1) / TN), (unsigned)splits);
+  if (TM == 128 && TN == 64)
+    hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2>), grid, dim3(256), 0, st, g);
+  else if (TM == 128)
+    hipLaunchKernelGGL((gemm_kernel<128, 32, 4, 1>), grid, dim3(256), 0, st, g);
+  else if (TN == 64)
+    hipLaunchKernelGGL((gemm_kernel<64, 64, 2, 2>), grid, dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL((gemm_kernel<64, 32, 2, 2>), grid, dim3(256), 0, st, g);
+  if (splits > 1) {
+    const int64_t tot = M * N;
+    const int blocks = (int)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096);
+    hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g, splits);
+  }
+  return launch_status("tvq_gemm");
+}

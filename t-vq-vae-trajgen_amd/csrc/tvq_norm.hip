@@ -1,0 +1,379 @@
+// BatchNorm2d/1d (+ fused SnakeActivation), standalone Snake, dropout backward.
+//
+// BN training statistics accumulate in fp64 (torch's CPU accumulator type for
+// fp32), two kernels: per-(channel, chunk) partial sums -> per-channel finalize
+// (mean, biased var for normalisation, unbiased var for running_var, momentum
+// 0.1, num_batches_tracked += 1) producing the affine form y = x*scale + shift
+// (scale = w*invstd, shift = b - mean*scale), then one streaming apply kernel
+// that also applies Snake:  x + (1/a) sin(a x)^2  (train_utils.py:421-448).
+// Backward recomputes the BN output from x and (mean, invstd); reductions are
+// fixed-order (deterministic).
+#include "tvq_common.h"
+
+namespace tvq {
+
+static int bn_chunks(int64_t B, int64_t HW) {
+  int64_t c = (B * HW + 4095) / 4096;
+  if (c > 64) c = 64;
+  if (c < 1) c = 1;
+  return (int)c;
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+  return t;
+}
+
+// partial [c][chunk][2] = (sum x, sum x^2)
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __restrict__ x, int B,
+                                                               int C, int HW, int chunks,
+                                                               double* __restrict__ part) {
+  __shared__ double red[4];
+  const int c = blockIdx.x, ch = blockIdx.y;
+  const int64_t tot = (int64_t)B * HW;
+  const int64_t per = (tot + chunks - 1) / chunks;
+  const int64_t lo = ch * per, hi = min(tot, lo + per);
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+    const int64_t b = i / HW, p = i - b * HW;
+    const double v = x[(b * C + c) * HW + p];
+    s1 += v;
+    s2 += v * v;
+  }
+  s1 = block_sum_d(s1, red);
+  s2 = block_sum_d(s2, red);
+  if (threadIdx.x == 0) {
+    part[((int64_t)c * chunks + ch) * 2 + 0] = s1;
+    part[((int64_t)c * chunks + ch) * 2 + 1] = s2;
+  }
+}
+
+__global__ void bn_stats_final_kernel(const double* __restrict__ part, int C, int chunks, int64_t N,
+                                      float eps, float momentum, const float* __restrict__ w,
+                                      const float* __restrict__ b, float* __restrict__ rmean,
+                                      float* __restrict__ rvar, int64_t* __restrict__ nbt,
+                                      float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                      float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) nbt[0] += 1;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = 0; i < chunks; ++i) {
+    s1 += part[((int64_t)c * chunks + i) * 2 + 0];
+    s2 += part[((int64_t)c * chunks + i) * 2 + 1];
+  }
+  const double mean = s1 / (double)N;
+  double var = s2 / (double)N - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const double invstd = 1.0 / sqrt(var + (double)eps);
+  if (rmean) {
+    const double unb = N > 1 ? var * (double)N / (double)(N - 1) : var;
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+  }
+  const float sc = (float)((double)(w ? w[c] : 1.f) * invstd);
+  save_mean[c] = (float)mean;
+  save_invstd[c] = (float)invstd;
+  scale[c] = sc;
+  shift[c] = (b ? b[c] : 0.f) - (float)mean * sc;
+}
+
+__global__ void bn_eval_prep_kernel(const float* __restrict__ w, const float* __restrict__ b,
+                                    const float* __restrict__ rm, const float* __restrict__ rv,
+                                    float eps, int C, float* __restrict__ scale,
+                                    float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = 1.0f / sqrtf(rv[c] + eps);
+  const float sc = (w ? w[c] : 1.f) * inv;
+  scale[c] = sc;
+  shift[c] = (b ? b[c] : 0.f) - rm[c] * sc;
+}
+
+__device__ __forceinline__ float snake_fwd(float s, float a) {
+  const float inv = 1.0f / a;
+  const float sn = sinf(a * s);
+  return s + inv * (sn * sn);
+}
+
+// y = snake?(x*scale[c] + shift[c]);  grid (chunks-of-HW, B*C)
+__global__ __launch_bounds__(256) void affine_snake_kernel(const float* __restrict__ x, int C,
+                                                           int HW, const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           const float* __restrict__ a,
+                                                           float* __restrict__ y) {
+  const int bc = blockIdx.y;
+  const int c = bc % C;
+  const float sc = scale ? scale[c] : 1.f, sh = shift ? shift[c] : 0.f;
+  const float av = a ? a[c] : 0.f;
+  const int64_t base = (int64_t)bc * HW;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
+    float s = fmaf(x[base + p], sc, sh);
+    if (a) s = snake_fwd(s, av);
+    y[base + p] = s;
+  }
+}
+
+// backward partials: [c][chunk][3] = (sum ds, sum ds*xhat, sum da-term)
+__global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, int B, int C, int HW, int chunks,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ a,
+    double* __restrict__ part) {
+  __shared__ double red[4];
+  const int c = blockIdx.x, ch = blockIdx.y;
+  const int64_t tot = (int64_t)B * HW;
+  const int64_t per = (tot + chunks - 1) / chunks;
+  const int64_t lo = ch * per, hi = min(tot, lo + per);
+  const float mu = mean[c], is = invstd[c], sc = scale[c], sh = shift[c];
+  const float av = a ? a[c] : 1.f, inv_a = 1.0f / av;
+  double s_ds = 0.0, s_dsx = 0.0, s_da = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+    const int64_t b = i / HW, p = i - b * HW;
+    const int64_t o = (b * C + c) * HW + p;
+    const float xv = x[o], g = dy[o];
+    float ds = g;
+    if (a) {
+      const float s = fmaf(xv, sc, sh);
+      float sn, cs;
+      sincosf(av * s, &sn, &cs);
+      const float t = 2.0f * sn * cs;
+      ds = g + g * inv_a * t * av;
+      s_da += (double)(g * inv_a * t * s) - (double)(g * (sn * sn) * inv_a * inv_a);
+    }
+    const float xhat = (xv - mu) * is;
+    s_ds += ds;
+    s_dsx += (double)ds * xhat;
+  }
+  s_ds = block_sum_d(s_ds, red);
+  s_dsx = block_sum_d(s_dsx, red);
+  s_da = block_sum_d(s_da, red);
+  if (threadIdx.x == 0) {
+    double* pp = part + ((int64_t)c * chunks + ch) * 3;
+    pp[0] = s_ds;
+    pp[1] = s_dsx;
+    pp[2] = s_da;
+  }
+}
+
+// coef[c][0] = sum ds, coef[c][1] = sum ds*xhat ; parameter grads
+__global__ void bn_bwd_final_kernel(const double* __restrict__ part, int C, int chunks,
+                                    float* __restrict__ coef, float* __restrict__ dw,
+                                    float* __restrict__ db, float* __restrict__ da,
+                                    int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int i = 0; i < chunks; ++i) {
+    const double* pp = part + ((int64_t)c * chunks + i) * 3;
+    s0 += pp[0];
+    s1 += pp[1];
+    s2 += pp[2];
+  }
+  coef[2 * c] = (float)s0;
+  coef[2 * c + 1] = (float)s1;
+  if (dw) dw[c] = accumulate ? dw[c] + (float)s1 : (float)s1;
+  if (db) db[c] = accumulate ? db[c] + (float)s0 : (float)s0;
+  if (da) da[c] = accumulate ? da[c] + (float)s2 : (float)s2;
+}
+
+// dx = w*invstd/N * (N*ds - sum ds - xhat * sum ds*xhat)
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, int C, int HW, int64_t N,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ w, const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ a, const float* __restrict__ coef, float* __restrict__ dx) {
+  const int bc = blockIdx.y;
+  const int c = bc % C;
+  const float mu = mean[c], is = invstd[c], sc = scale[c], sh = shift[c];
+  const float wc = w ? w[c] : 1.f;
+  const float av = a ? a[c] : 1.f, inv_a = 1.0f / av;
+  const float invN = 1.0f / (float)N;
+  const float mds = coef[2 * c] * invN, mdsx = coef[2 * c + 1] * invN;
+  const float k = wc * is;
+  const int64_t base = (int64_t)bc * HW;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
+    const float xv = x[base + p], g = dy[base + p];
+    float ds = g;
+    if (a) {
+      const float s = fmaf(xv, sc, sh);
+      float sn, cs;
+      sincosf(av * s, &sn, &cs);
+      ds = g + g * inv_a * (2.0f * sn * cs) * av;
+    }
+    const float xhat = (xv - mu) * is;
+    dx[base + p] = k * (ds - mds - xhat * mdsx);
+  }
+}
+
+__global__ __launch_bounds__(256) void snake_fwd_kernel(const float* __restrict__ x, int C, int HW,
+                                                        const float* __restrict__ a,
+                                                        float* __restrict__ y) {
+  const int bc = blockIdx.y;
+  const float av = a[bc % C];
+  const int64_t base = (int64_t)bc * HW;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256)
+    y[base + p] = snake_fwd(x[base + p], av);
+}
+
+// dx (elementwise) and per-(channel, chunk) partials of da
+__global__ __launch_bounds__(256) void snake_bwd_kernel(const float* __restrict__ dy,
+                                                        const float* __restrict__ x, int B, int C,
+                                                        int HW, int chunks,
+                                                        const float* __restrict__ a,
+                                                        float* __restrict__ dx,
+                                                        double* __restrict__ part) {
+  __shared__ double red[4];
+  const int c = blockIdx.x, ch = blockIdx.y;
+  const int64_t tot = (int64_t)B * HW;
+  const int64_t per = (tot + chunks - 1) / chunks;
+  const int64_t lo = ch * per, hi = min(tot, lo + per);
+  const float av = a[c], inv_a = 1.0f / av;
+  double s_da = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+    const int64_t b = i / HW, p = i - b * HW;
+    const int64_t o = (b * C + c) * HW + p;
+    const float xv = x[o], g = dy[o];
+    float sn, cs;
+    sincosf(av * xv, &sn, &cs);
+    const float t = 2.0f * sn * cs;
+    dx[o] = g + g * inv_a * t * av;
+    s_da += (double)(g * inv_a * t * xv) - (double)(g * (sn * sn) * inv_a * inv_a);
+  }
+  s_da = block_sum_d(s_da, red);
+  if (threadIdx.x == 0) part[(int64_t)c * chunks + ch] = s_da;
+}
+
+__global__ void snake_bwd_final_kernel(const double* __restrict__ part, int C, int chunks,
+                                       float* __restrict__ da, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int i = 0; i < chunks; ++i) s += part[(int64_t)c * chunks + i];
+  da[c] = accumulate ? da[c] + (float)s : (float)s;
+}
+
+__global__ void dropout_bwd_kernel(const float* __restrict__ dy, int64_t n, float p, float scale,
+                                   const int64_t* __restrict__ seed_ptr, uint64_t offset,
+                                   float* __restrict__ dx) {
+  const uint64_t seed = mix_seed(seed_ptr, offset);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dx[i] = (uniform01(seed, (uint64_t)i) >= p) ? dy[i] * scale : 0.f;
+}
+
+static dim3 ew_grid(int64_t B, int64_t C, int64_t HW) {
+  int gx = (int)((HW + 255) / 256);
+  if (gx > 64) gx = 64;
+  return dim3(gx, (unsigned)(B * C));
+}
+
+}  // namespace tvq
+
+using namespace tvq;
+
+extern "C" int64_t tvq_bn_workspace(int64_t B, int64_t C, int64_t HW) {
+  // bytes: partials (C*chunks*3 doubles) + 6*C floats
+  return (int64_t)C * bn_chunks(B, HW) * 3 * 8 + 6 * C * 4 + 64;
+}
+
+// Training-mode BatchNorm (+Snake).  save (3*C floats): mean | invstd | (scratch)
+// The workspace must hold tvq_bn_workspace() bytes; it keeps scale/shift for bwd.
+extern "C" int tvq_bn_train_fwd(const float* x, int64_t B, int64_t C, int64_t HW, const float* w,
+                                const float* b, float* running_mean, float* running_var,
+                                int64_t* num_batches_tracked, float momentum, float eps,
+                                const float* snake_a, float* y, float* save_mean,
+                                float* save_invstd, float* scale_shift, void* workspace,
+                                tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && y && save_mean && save_invstd && scale_shift && workspace && B > 0 && C > 0,
+                "tvq_bn_train_fwd: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  const int chunks = bn_chunks(B, HW);
+  double* part = (double*)workspace;
+  hipLaunchKernelGGL(bn_stats_partial_kernel, dim3((int)C, chunks), dim3(256), 0, st, x, (int)B,
+                     (int)C, (int)HW, chunks, part);
+  hipLaunchKernelGGL(bn_stats_final_kernel, dim3((int)((C + 63) / 64)), dim3(64), 0, st, part,
+                     (int)C, chunks, B * HW, eps, momentum, w, b, running_mean, running_var,
+                     num_batches_tracked, save_mean, save_invstd, scale_shift, scale_shift + C);
+  hipLaunchKernelGGL(affine_snake_kernel, ew_grid(B, C, HW), dim3(256), 0, st, x, (int)C, (int)HW,
+                     scale_shift, scale_shift + C, snake_a, y);
+  return launch_status("tvq_bn_train_fwd");
+}
+
+// Eval-mode BatchNorm (+Snake) from running statistics. scale_shift: 2*C floats scratch.
+extern "C" int tvq_bn_eval_fwd(const float* x, int64_t B, int64_t C, int64_t HW, const float* w,
+                               const float* b, const float* running_mean,
+                               const float* running_var, float eps, const float* snake_a, float* y,
+                               float* scale_shift, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && y && running_mean && running_var && scale_shift, "tvq_bn_eval_fwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_eval_prep_kernel, dim3((int)((C + 63) / 64)), dim3(64), 0, st, w, b,
+                     running_mean, running_var, eps, (int)C, scale_shift, scale_shift + C);
+  hipLaunchKernelGGL(affine_snake_kernel, ew_grid(B, C, HW), dim3(256), 0, st, x, (int)C, (int)HW,
+                     scale_shift, scale_shift + C, snake_a, y);
+  return launch_status("tvq_bn_eval_fwd");
+}
+
+extern "C" int tvq_bn_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t HW,
+                          const float* w, const float* snake_a, const float* save_mean,
+                          const float* save_invstd, const float* scale_shift, float* dx,
+                          float* dw, float* db, float* da, int64_t accumulate, void* workspace,
+                          tvq_stream_t stream) {
+  TVQ_CHECK_ARG(dy && x && dx && save_mean && save_invstd && scale_shift && workspace,
+                "tvq_bn_bwd: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  const int chunks = bn_chunks(B, HW);
+  double* part = (double*)workspace;
+  float* coef = (float*)(part + (int64_t)C * chunks * 3);
+  hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3((int)C, chunks), dim3(256), 0, st, dy, x, (int)B,
+                     (int)C, (int)HW, chunks, save_mean, save_invstd, scale_shift,
+                     scale_shift + C, snake_a, part);
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((int)((C + 63) / 64)), dim3(64), 0, st, part,
+                     (int)C, chunks, coef, dw, db, snake_a ? da : nullptr, (int)accumulate);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, ew_grid(B, C, HW), dim3(256), 0, st, dy, x, (int)C,
+                     (int)HW, B * HW, save_mean, save_invstd, w, scale_shift, scale_shift + C,
+                     snake_a, coef, dx);
+  return launch_status("tvq_bn_bwd");
+}
+
+extern "C" int tvq_snake_fwd(const float* x, int64_t B, int64_t C, int64_t HW, const float* a,
+                             float* y, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && a && y && B > 0 && C > 0 && HW > 0, "tvq_snake_fwd: bad arguments");
+  hipLaunchKernelGGL(snake_fwd_kernel, ew_grid(B, C, HW), dim3(256), 0, (hipStream_t)stream, x,
+                     (int)C, (int)HW, a, y);
+  return launch_status("tvq_snake_fwd");
+}
+
+extern "C" int64_t tvq_snake_workspace(int64_t B, int64_t C, int64_t HW) {
+  return (int64_t)C * bn_chunks(B, HW) * 8;
+}
+
+extern "C" int tvq_snake_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t HW,
+                             const float* a, float* dx, float* da, int64_t accumulate,
+                             void* workspace, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(dy && x && a && dx && da && workspace, "tvq_snake_bwd: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  const int chunks = bn_chunks(B, HW);
+  hipLaunchKernelGGL(snake_bwd_kernel, dim3((int)C, chunks), dim3(256), 0, st, dy, x, (int)B,
+                     (int)C, (int)HW, chunks, a, dx, (double*)workspace);
+  hipLaunchKernelGGL(snake_bwd_final_kernel, dim3((int)((C + 63) / 64)), dim3(64), 0, st,
+                     (const double*)workspace, (int)C, chunks, da, (int)accumulate);
+  return launch_status("tvq_snake_bwd");
+}
+
+extern "C" int tvq_dropout_bwd(const float* dy, int64_t n, float p, const int64_t* seed_ptr,
+                               uint64_t offset, float* dx, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(dy && dx && n >= 0 && p >= 0.f && p < 1.f, "tvq_dropout_bwd: bad arguments");
+  if (n == 0) return TVQ_OK;
+  const int blocks = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+  hipLaunchKernelGGL(dropout_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dy, n, p,
+                     1.0f / (1.0f - p), seed_ptr, offset, dx);
+  return launch_status("tvq_dropout_bwd");
+}

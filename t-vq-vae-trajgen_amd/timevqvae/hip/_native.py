@@ -40,6 +40,42 @@ sig("tvq_vq_ema", P, P, I64, I64, F32, P, P, P)
 sig("tvq_vq_finalize", P, P, I64, I64, F32, P, P, I64, P, P, I64, P, P)
 sig("tvq_vq_backward", P, P, P, P, I64, I64, P, P)
 
+U64 = ctypes.c_uint64
+# --- STFT / iSTFT ------------------------------------------------------------
+sig("tvq_stft_encode", P, I64, I64, I64, P, P, P, P, P, P)
+sig("tvq_istft_decode", P, I64, I64, I64, I64, I64, P, P)
+sig("tvq_istft_decode_bwd", P, I64, I64, I64, I64, I64, P, P)
+# --- convolutions --------------------------------------------------------------
+sig("tvq_conv_out_width", I64, I64, I64, I64)
+sig("tvq_conv2d_fwd", P, I64, I64, I64, I64, P, P, I64, I64, I64, I64, I64, P, P, F32, P, U64, P)
+sig("tvq_convT2d_fwd", P, I64, I64, I64, I64, P, P, I64, I64, I64, I64, P, P, P)
+sig("tvq_conv2d_dgrad_workspace", I64, I64, I64, I64, I64, I64, I64, restype=I64)
+sig("tvq_conv2d_dgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, P, I64, P, P)
+sig("tvq_convT2d_dgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, P, I64, P)
+sig("tvq_conv_wgrad_workspace", I64, I64, I64, I64, I64, I64, I64, restype=I64)
+sig("tvq_conv2d_wgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, I64, P, I64, P, P)
+sig("tvq_convT2d_wgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, P, I64, P, P)
+sig("tvq_channel_sum_workspace", I64, I64, I64, restype=I64)
+sig("tvq_channel_sum", P, I64, I64, I64, P, I64, P, P)
+# --- BatchNorm / Snake / dropout -----------------------------------------------
+sig("tvq_bn_workspace", I64, I64, I64, restype=I64)
+sig("tvq_bn_train_fwd", P, I64, I64, I64, P, P, P, P, P, F32, F32, P, P, P, P, P, P, P)
+sig("tvq_bn_eval_fwd", P, I64, I64, I64, P, P, P, P, F32, P, P, P, P)
+sig("tvq_bn_bwd", P, P, I64, I64, I64, P, P, P, P, P, P, P, P, P, I64, P, P)
+sig("tvq_snake_fwd", P, I64, I64, I64, P, P, P)
+sig("tvq_snake_workspace", I64, I64, I64, restype=I64)
+sig("tvq_snake_bwd", P, P, I64, I64, I64, P, P, P, I64, P, P)
+sig("tvq_dropout_bwd", P, I64, F32, P, U64, P, P)
+# --- dense GEMM --------------------------------------------------------------
+sig("tvq_gemm_workspace", I64, I64, I64, restype=I64)
+sig("tvq_gemm", P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, F32, P, P, I64, I64, I64, P, P)
+# --- losses / optimizer --------------------------------------------------------
+sig("tvq_loss_workspace", I64, restype=I64)
+sig("tvq_loss_fwd", P, P, I64, I64, P, P, P)
+sig("tvq_loss_bwd", P, P, I64, I64, P, P, P)
+sig("tvq_adamw_begin", P, F32, P)
+sig("tvq_adamw", P, P, P, P, I64, P, F32, F32, F32, F32, P)
+
 
 class NativeError(RuntimeError):
     pass

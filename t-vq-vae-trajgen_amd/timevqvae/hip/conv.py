@@ -1,0 +1,138 @@
+"""Convolutions on the HIP implicit-GEMM engine (include/tvq.h §convolutions).
+
+conv2d          nn.Conv2d  (VQVAEEncBlock replicate 3x4 s(1,2); ResBlock 3x3; 1x1 proj;
+                Conv1d k3 of Upscale as H=1) with fused bias / dropout / residual epilogue
+conv_transpose2d nn.ConvTranspose2d 3x4 s(1,2) (VQVAEDecBlock, decoder tail)
+Backward: dgrad (T/F gathers), wgrad (split positions, deterministic), bias = channel sum.
+"""
+import torch
+
+from . import rng
+from ._native import call, ptr, stream_ptr, value
+
+
+def _ws(n, dev):
+    return torch.empty(max(int(n), 1), device=dev, dtype=torch.float32)
+
+
+def _bias_grad(g, dev):
+    B, C = g.shape[0], g.shape[1]
+    HW = g.numel() // (B * C)
+    out = torch.empty(C, device=dev, dtype=torch.float32)
+    ws = _ws(value("tvq_channel_sum_workspace", B, C, HW), dev)
+    call("tvq_channel_sum", ptr(g), B, C, HW, ptr(out), 0, ptr(ws), stream_ptr())
+    return out
+
+
+def _as4d(x):
+    return x.unsqueeze(2) if x.dim() == 3 else x
+
+
+class _Conv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, SW, replicate, residual, drop_p, site):
+        squeeze = x.dim() == 3
+        x4 = _as4d(x).contiguous()
+        w4 = _as4d(w).contiguous() if w.dim() == 3 else w.contiguous()
+        B, Ci, H, Wi = x4.shape
+        Co, _, KH, KW = w4.shape
+        Wo = value("tvq_conv_out_width", Wi, KW, SW, 0)
+        y = torch.empty((B, Co, H, Wo), device=x.device, dtype=torch.float32)
+        res = _as4d(residual).contiguous() if residual is not None else None
+        seed = rng.seed_tensor(x.device) if drop_p > 0 else None
+        off = rng.call_offset(site) if drop_p > 0 else 0
+        call("tvq_conv2d_fwd", ptr(x4), B, Ci, H, Wi, ptr(w4), ptr(b), Co, KH, KW, SW,
+             int(replicate), ptr(y), ptr(res), float(drop_p), ptr(seed), off, stream_ptr())
+        ctx.save_for_backward(x4, w4)
+        ctx.cfg = (SW, replicate, drop_p, off, squeeze, b is not None, residual is not None,
+                   w.dim())
+        ctx.seed = seed
+        return y.squeeze(2) if squeeze else y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x4, w4 = ctx.saved_tensors
+        SW, replicate, drop_p, off, squeeze, has_b, has_res, wdim = ctx.cfg
+        B, Ci, H, Wi = x4.shape
+        Co, _, KH, KW = w4.shape
+        dev = x4.device
+        s = stream_ptr()
+        g = _as4d(gy).contiguous()
+        Wo = g.shape[3]
+        if drop_p > 0:
+            gd = torch.empty_like(g)
+            call("tvq_dropout_bwd", ptr(g), g.numel(), float(drop_p), ptr(ctx.seed), off, ptr(gd), s)
+        else:
+            gd = g
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x4)
+            wsz = value("tvq_conv2d_dgrad_workspace", B, Ci, H, Wi, KH, KW, int(replicate))
+            ws = _ws(wsz, dev) if replicate else None
+            call("tvq_conv2d_dgrad", ptr(gd), B, Co, H, Wo, ptr(w4), Ci, KH, KW, SW,
+                 int(replicate), ptr(dx), Wi, ptr(ws), s)
+            if squeeze:
+                dx = dx.squeeze(2)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w4)
+            ws = _ws(value("tvq_conv_wgrad_workspace", Co, Ci, KH, KW, B, H, Wo), dev)
+            call("tvq_conv2d_wgrad", ptr(x4), B, Ci, H, Wi, ptr(gd), Co, Wo, KH, KW, SW,
+                 int(replicate), ptr(dw), 0, ptr(ws), s)
+            if wdim == 3:
+                dw = dw.squeeze(2)
+        if has_b and ctx.needs_input_grad[2]:
+            db = _bias_grad(gd, dev)
+        dres = None
+        if has_res and ctx.needs_input_grad[5]:
+            dres = gy
+        return dx, dw, db, None, None, dres, None, None
+
+
+def conv2d(x, weight, bias=None, stride_w=1, replicate=False, residual=None, drop_p=0.0, site=0):
+    """y = residual + Dropout_p(conv(x) + bias).  x (B,C,H,W) or (B,C,L) with a (Co,Ci,KH,KW) /
+    (Co,Ci,K) weight; padding (KH//2, (KW-1)//2), zero or replicate."""
+    return _Conv2d.apply(x, weight, bias, int(stride_w), bool(replicate), residual, float(drop_p),
+                         int(site))
+
+
+class _ConvT2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, SW):
+        x = x.contiguous()
+        w = w.contiguous()
+        B, Ci, H, Wi = x.shape
+        _, Co, KH, KW = w.shape
+        Wo = value("tvq_conv_out_width", Wi, KW, SW, 1)
+        y = torch.empty((B, Co, H, Wo), device=x.device, dtype=torch.float32)
+        call("tvq_convT2d_fwd", ptr(x), B, Ci, H, Wi, ptr(w), ptr(b), Co, KH, KW, SW, ptr(y), None,
+             stream_ptr())
+        ctx.save_for_backward(x, w)
+        ctx.SW = SW
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        SW = ctx.SW
+        B, Ci, H, Wi = x.shape
+        _, Co, KH, KW = w.shape
+        g = gy.contiguous()
+        Wo = g.shape[3]
+        s = stream_ptr()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            call("tvq_convT2d_dgrad", ptr(g), B, Co, H, Wo, ptr(w), Ci, KH, KW, SW, ptr(dx), Wi, s)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w)
+            ws = _ws(value("tvq_conv_wgrad_workspace", Ci, Co, KH, KW, B, H, Wi), x.device)
+            call("tvq_convT2d_wgrad", ptr(x), B, Ci, H, Wi, ptr(g), Co, Wo, KH, KW, SW, ptr(dw), 0,
+                 ptr(ws), s)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = _bias_grad(g, x.device)
+        return dx, dw, db, None
+
+
+def conv_transpose2d(x, weight, bias=None, stride_w=2):
+    return _ConvT2d.apply(x, weight, bias, int(stride_w))

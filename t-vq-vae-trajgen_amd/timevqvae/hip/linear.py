@@ -1,0 +1,64 @@
+"""Dense GEMM ops (nn.Linear over the last dim) on the HIP path."""
+import torch
+
+from ._native import call, ptr, stream_ptr, value
+
+
+def gemm(A, sam, sak, B, sbk, sbn, M, N, K, out=None, ldc=None, alpha=1.0, bias=None, R=None,
+         ldr=0, act=0, accumulate=False):
+    dev = A.device
+    if out is None:
+        out = torch.empty((M, N), device=dev, dtype=torch.float32)
+        ldc = N
+    wsz = value("tvq_gemm_workspace", M, N, K)
+    ws = torch.empty(wsz, device=dev, dtype=torch.float32) if wsz > 0 else None
+    call("tvq_gemm", ptr(A), sam, sak, ptr(B), sbk, sbn, ptr(out), ldc, M, N, K, float(alpha),
+         ptr(bias), ptr(R), ldr, int(act), int(bool(accumulate)), ptr(ws), stream_ptr())
+    return out
+
+
+def _bias_grad_rows(g2):
+    M, N = g2.shape
+    out = torch.empty(N, device=g2.device, dtype=torch.float32)
+    ws = torch.empty(value("tvq_channel_sum_workspace", M, N, 1), device=g2.device)
+    call("tvq_channel_sum", ptr(g2), M, N, 1, ptr(out), 0, ptr(ws), stream_ptr())
+    return out
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, residual):
+        shp = x.shape
+        K = shp[-1]
+        N = w.shape[0]
+        x2 = x.reshape(-1, K).contiguous()
+        w = w.contiguous()
+        M = x2.shape[0]
+        R = residual.reshape(M, N).contiguous() if residual is not None else None
+        y = gemm(x2, K, 1, w, 1, K, M, N, K, bias=b, R=R, ldr=N)
+        ctx.save_for_backward(x2, w)
+        ctx.has = (b is not None, residual is not None)
+        ctx.shp = shp
+        return y.reshape(*shp[:-1], N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w = ctx.saved_tensors
+        M, K = x2.shape
+        N = w.shape[0]
+        g = gy.reshape(M, N).contiguous()
+        dx = dw = db = dres = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(g, N, 1, w, K, 1, M, K, N).reshape(ctx.shp)
+        if ctx.needs_input_grad[1]:
+            dw = gemm(g, 1, N, x2, K, 1, N, K, M)
+        if ctx.has[0] and ctx.needs_input_grad[2]:
+            db = _bias_grad_rows(g)
+        if ctx.has[1] and ctx.needs_input_grad[3]:
+            dres = gy
+        return dx, dw, db, dres
+
+
+def linear(x, weight, bias=None, residual=None):
+    """residual + x @ weight^T + bias over the last dim (nn.Linear; vq_vae.py:255,263)."""
+    return _Linear.apply(x, weight, bias, residual)

@@ -1,0 +1,89 @@
+"""BatchNorm (+ fused SnakeActivation) and standalone Snake on the HIP path."""
+import torch
+
+from ._native import call, ptr, stream_ptr, value
+
+
+def _dims(x):
+    B, C = x.shape[0], x.shape[1]
+    return B, C, x.numel() // (B * C)
+
+
+class _BNSnakeTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, a, running_mean, running_var, nbt, momentum, eps):
+        x = x.contiguous()
+        B, C, HW = _dims(x)
+        dev = x.device
+        y = torch.empty_like(x)
+        save = torch.empty(4 * C, device=dev, dtype=torch.float32)  # mean | invstd | scale | shift
+        ws = torch.empty(value("tvq_bn_workspace", B, C, HW), device=dev, dtype=torch.uint8)
+        call("tvq_bn_train_fwd", ptr(x), B, C, HW, ptr(w), ptr(b), ptr(running_mean),
+             ptr(running_var), ptr(nbt), float(momentum), float(eps), ptr(a), ptr(y),
+             ptr(save[:C]), ptr(save[C:2 * C]), ptr(save[2 * C:]), ptr(ws), stream_ptr())
+        ctx.save_for_backward(x, w, a, save)
+        ctx.has = (w is not None, b is not None, a is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, a, save = ctx.saved_tensors
+        B, C, HW = _dims(x)
+        dev = x.device
+        g = gy.contiguous()
+        dx = torch.empty_like(x)
+        has_w, has_b, has_a = ctx.has
+        dw = torch.empty(C, device=dev) if has_w else None
+        db = torch.empty(C, device=dev) if has_b else None
+        da = torch.empty(C, device=dev) if has_a else None
+        ws = torch.empty(value("tvq_bn_workspace", B, C, HW), device=dev, dtype=torch.uint8)
+        call("tvq_bn_bwd", ptr(g), ptr(x), B, C, HW, ptr(w), ptr(a), ptr(save[:C]),
+             ptr(save[C:2 * C]), ptr(save[2 * C:]), ptr(dx), ptr(dw), ptr(db), ptr(da), 0, ptr(ws),
+             stream_ptr())
+        return dx, dw, db, da, None, None, None, None, None
+
+
+def bn_snake(x, bn, a=None):
+    """snake_a(BatchNorm(x)) with the module `bn`'s parameters/buffers; a: (C,) or None."""
+    if bn.training:
+        if bn.momentum is None:
+            raise NotImplementedError("cumulative-average BatchNorm (momentum=None) is not on the path")
+        return _BNSnakeTrain.apply(x, bn.weight, bn.bias, a, bn.running_mean, bn.running_var,
+                                   bn.num_batches_tracked, bn.momentum, bn.eps)
+    if torch.is_grad_enabled() and (x.requires_grad or (bn.weight is not None and bn.weight.requires_grad)):
+        raise NotImplementedError("eval-mode BatchNorm backward is not on the TimeVQVAE path")
+    x = x.contiguous()
+    B, C, HW = _dims(x)
+    y = torch.empty_like(x)
+    ss = torch.empty(2 * C, device=x.device, dtype=torch.float32)
+    call("tvq_bn_eval_fwd", ptr(x), B, C, HW, ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
+         ptr(bn.running_var), float(bn.eps), ptr(a), ptr(y), ptr(ss), stream_ptr())
+    return y
+
+
+class _Snake(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, a):
+        x = x.contiguous()
+        B, C, HW = _dims(x)
+        y = torch.empty_like(x)
+        call("tvq_snake_fwd", ptr(x), B, C, HW, ptr(a), ptr(y), stream_ptr())
+        ctx.save_for_backward(x, a)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, a = ctx.saved_tensors
+        B, C, HW = _dims(x)
+        g = gy.contiguous()
+        dx = torch.empty_like(x)
+        da = torch.empty(C, device=x.device)
+        ws = torch.empty(value("tvq_snake_workspace", B, C, HW), device=x.device, dtype=torch.uint8)
+        call("tvq_snake_bwd", ptr(g), ptr(x), B, C, HW, ptr(a), ptr(dx), ptr(da), 0, ptr(ws),
+             stream_ptr())
+        return dx, da
+
+
+def snake(x, a):
+    """SnakeActivation (train_utils.py:446-448): x + (1/a) sin(a x)^2, a: (C,)."""
+    return _Snake.apply(x, a)

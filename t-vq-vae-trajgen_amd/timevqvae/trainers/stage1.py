@@ -1,0 +1,109 @@
+"""Stage1 VQ-VAE trainer — the reference trainers/stage1.py contract without Lightning.
+
+Same constructor (input_length, in_channels, config), module attributes
+(encoder_l/h, vq_model_l/h, decoder_l/h; state_dict keys identical),
+forward(batch, batch_idx, return_x_rec) and training_step(batch, batch_idx) ->
+loss_hist with the reference's logged scalar names (stage1.py:183-196).
+One fused STFT kernel produces both encoder inputs and both targets
+(stage1.py:101-113 + vq_vae.py:179-180).
+"""
+import torch
+import torch.nn as nn
+
+from ..hip.loss import l1_loss, mse_loss
+from ..hip.optim import FusedAdamW
+from ..hip.signal import stft_encode
+from ..models import VectorQuantize, VQVAEDecoder, VQVAEEncoder
+from ..utils import (compute_downsample_rate, linear_warmup_cosine_annealingLR, quantize,
+                     zero_pad_high_freq, zero_pad_low_freq)
+
+
+class Stage1(nn.Module):
+    def __init__(self, input_length: int, in_channels: int, config: dict, **kwargs):
+        super().__init__()
+        self.input_length = input_length
+        self.config = config
+        self.n_fft = config["VQ-VAE"]["n_fft"]
+        init_dim = config["encoder"]["init_dim"]
+        hid_dim = config["encoder"]["hid_dim"]
+        dw_l = config["encoder"]["downsampled_width"]["lf"]
+        dw_h = config["encoder"]["downsampled_width"]["hf"]
+        rate_l = compute_downsample_rate(input_length, self.n_fft, dw_l)
+        rate_h = compute_downsample_rate(input_length, self.n_fft, dw_h)
+        n_res = config["encoder"]["n_resnet_blocks"]
+        self.encoder_l = VQVAEEncoder(init_dim, hid_dim, 2 * in_channels, rate_l, n_res,
+                                      zero_pad_high_freq, self.n_fft, frequency_indepence=False)
+        self.encoder_h = VQVAEEncoder(init_dim, hid_dim, 2 * in_channels, rate_h, n_res,
+                                      zero_pad_low_freq, self.n_fft, frequency_indepence=False)
+        self.vq_model_l = VectorQuantize(hid_dim, config["VQ-VAE"]["codebook_sizes"]["lf"],
+                                         **config["VQ-VAE"])
+        self.vq_model_h = VectorQuantize(hid_dim, config["VQ-VAE"]["codebook_sizes"]["hf"],
+                                         **config["VQ-VAE"])
+        n_res_d = config["decoder"]["n_resnet_blocks"]
+        self.decoder_l = VQVAEDecoder(init_dim, hid_dim, 2 * in_channels, rate_l, n_res_d,
+                                      input_length, zero_pad_high_freq, self.n_fft, in_channels,
+                                      frequency_indepence=False)
+        self.decoder_h = VQVAEDecoder(init_dim, hid_dim, 2 * in_channels, rate_h, n_res_d,
+                                      input_length, zero_pad_low_freq, self.n_fft, in_channels,
+                                      frequency_indepence=False)
+        self._sched = None
+        self._opt = None
+
+    def forward(self, batch, batch_idx, return_x_rec: bool = False):
+        """stage1.py:89-168 (the validation-time plot is not reproduced)."""
+        x, y = batch
+        recons_loss = {"LF.time": 0.0, "HF.time": 0.0}
+        vq_losses = {"LF": None, "HF": None}
+        perplexities = {"LF": 0.0, "HF": 0.0}
+        need_tgt = not return_x_rec
+        s = stft_encode(x, enc_l=True, enc_h=True, tgt_l=need_tgt, tgt_h=need_tgt)
+        z_l = self.encoder_l.encode_timefreq(s["enc_l"])
+        z_q_l, s_l, vq_loss_l, perplexity_l = quantize(z_l, self.vq_model_l)
+        xhat_l = self.decoder_l(z_q_l)
+        z_h = self.encoder_h.encode_timefreq(s["enc_h"])
+        z_q_h, s_h, vq_loss_h, perplexity_h = quantize(z_h, self.vq_model_h)
+        xhat_h = self.decoder_h(z_q_h)
+        if return_x_rec:
+            return xhat_l + xhat_h
+        recons_loss["LF.time"] = mse_loss(s["tgt_l"], xhat_l)
+        perplexities["LF"] = perplexity_l
+        vq_losses["LF"] = vq_loss_l
+        recons_loss["HF.time"] = l1_loss(s["tgt_h"], xhat_h)
+        perplexities["HF"] = perplexity_h
+        vq_losses["HF"] = vq_loss_h
+        return recons_loss, vq_losses, perplexities
+
+    def training_step(self, batch, batch_idx):
+        """stage1.py:170-198: loss and the logged scalars; steps the LR scheduler."""
+        recons_loss, vq_losses, perplexities = self.forward(batch, batch_idx)
+        loss = ((recons_loss["LF.time"] + recons_loss["HF.time"]) + vq_losses["LF"]["loss"]
+                + vq_losses["HF"]["loss"])
+        if self._sched is not None:
+            self._sched.step()
+        return {
+            "loss": loss,
+            "recons_loss.time": recons_loss["LF.time"] + recons_loss["HF.time"],
+            "recons_loss.LF.time": recons_loss["LF.time"],
+            "recons_loss.HF.time": recons_loss["HF.time"],
+            "commit_loss.LF": vq_losses["LF"]["commit_loss"],
+            "commit_loss.HF": vq_losses["HF"]["commit_loss"],
+            "perplexity.LF": perplexities["LF"],
+            "perplexity.HF": perplexities["HF"],
+        }
+
+    @torch.no_grad()
+    def validation_step(self, batch, batch_idx):
+        self.eval()
+        recons_loss, vq_losses, perplexities = self.forward(batch, batch_idx)
+        return {"loss": (recons_loss["LF.time"] + recons_loss["HF.time"]),
+                "recons_loss.LF.time": recons_loss["LF.time"],
+                "recons_loss.HF.time": recons_loss["HF.time"],
+                "perplexity.LF": perplexities["LF"], "perplexity.HF": perplexities["HF"]}
+
+    def configure_optimizers(self):
+        """stage1.py:229-236: AdamW(lr) + linear warmup / cosine annealing."""
+        opt = FusedAdamW(self.parameters(), lr=self.config["exp_params"]["lr"])
+        sch = linear_warmup_cosine_annealingLR(opt, self.config["trainer_params"]["max_steps"]["stage1"],
+                                               self.config["exp_params"]["linear_warmup_rate"])
+        self._opt, self._sched = opt, sch
+        return {"optimizer": opt, "lr_scheduler": sch}

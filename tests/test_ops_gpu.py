@@ -1,0 +1,265 @@
+"""Per-kernel numerics: each HIP op vs the plain PyTorch fp32 CPU op (forward and
+backward).  Tolerance: rel-L2 <= 1e-5 (fp32 reassociation only), max-abs scaled."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def close(a, b, tol=1e-5, what=""):
+    r = rel(a, b)
+    assert r <= tol, f"{what}: rel-L2 {r:.3e} > {tol}"
+
+
+def _grads(fn, inputs):
+    outs = fn(*inputs)
+    g = torch.randn_like(outs)
+    outs.backward(g)
+    return outs, [t.grad for t in inputs], g
+
+
+def _run_both(fn_hip, fn_ref, shapes, cuda, seed=0):
+    gen = torch.Generator().manual_seed(seed)
+    cpu = [torch.randn(s, generator=gen).requires_grad_(True) for s in shapes]
+    dev = [t.detach().to(cuda).requires_grad_(True) for t in cpu]
+    out_c = fn_ref(*cpu)
+    g = torch.randn(out_c.shape, generator=gen)
+    out_c.backward(g)
+    out_d = fn_hip(*dev)
+    out_d.backward(g.to(cuda))
+    torch.cuda.synchronize()
+    return out_c, out_d, cpu, dev
+
+
+@pytest.mark.parametrize("B,Ci,Co,W,kind", [
+    (4, 12, 4, 257, "enc"), (3, 8, 16, 64, "enc"), (2, 32, 64, 16, "enc"),
+    (4, 8, 8, 64, "res"), (2, 64, 128, 8, "res"), (2, 16, 128, 32, "res"), (3, 128, 16, 32, "res"),
+    (2, 64, 128, 8, "proj"), (5, 3, 7, 33, "res"),
+])
+def test_conv2d(B, Ci, Co, W, kind, cuda):
+    from timevqvae.hip.conv import conv2d
+    if kind == "enc":
+        KH, KW, SW, rep = 3, 4, 2, True
+    elif kind == "res":
+        KH, KW, SW, rep = 3, 3, 1, False
+    else:
+        KH, KW, SW, rep = 1, 1, 1, False
+
+    def ref(x, w, b):
+        xp = F.pad(x, (1, 1, 1, 1), mode="replicate") if rep else x
+        pad = (0, 0) if rep else (KH // 2, (KW - 1) // 2)
+        return F.conv2d(xp, w, b, stride=(1, SW), padding=pad)
+
+    def hip(x, w, b):
+        return conv2d(x, w, b, stride_w=SW, replicate=rep)
+
+    oc, od, c, d = _run_both(hip, ref, [(B, Ci, 3, W), (Co, Ci, KH, KW), (Co,)], cuda)
+    close(od, oc, what="fwd")
+    for i, n in enumerate(("dx", "dw", "db")):
+        close(d[i].grad, c[i].grad, what=n)
+
+
+@pytest.mark.parametrize("B,Ci,Co,W", [(4, 64, 32, 8), (2, 8, 4, 64), (3, 4, 12, 128), (2, 12, 12, 256)])
+def test_conv_transpose2d(B, Ci, Co, W, cuda):
+    from timevqvae.hip.conv import conv_transpose2d
+
+    def ref(x, w, b):
+        return F.conv_transpose2d(x, w, b, stride=(1, 2), padding=(1, 1))
+
+    oc, od, c, d = _run_both(lambda x, w, b: conv_transpose2d(x, w, b), ref,
+                             [(B, Ci, 3, W), (Ci, Co, 3, 4), (Co,)], cuda)
+    close(od, oc, what="fwd")
+    for i, n in enumerate(("dx", "dw", "db")):
+        close(d[i].grad, c[i].grad, what=n)
+
+
+def test_conv1d_k3(cuda):
+    from timevqvae.hip.conv import conv2d
+    oc, od, c, d = _run_both(lambda x, w, b: conv2d(x, w, b), lambda x, w, b: F.conv1d(x, w, b, padding=1),
+                             [(8, 128, 96), (256, 128, 3), (256,)], cuda)
+    close(od, oc, what="fwd")
+    for i, n in enumerate(("dx", "dw", "db")):
+        close(d[i].grad, c[i].grad, what=n)
+
+
+def test_conv_residual_dropout(cuda):
+    """Fused epilogue: out = residual + Dropout(conv + b); mask regenerated in backward."""
+    from timevqvae.hip.conv import conv2d
+    gen = torch.Generator().manual_seed(1)
+    x = torch.randn(4, 16, 3, 32, generator=gen).to(cuda).requires_grad_(True)
+    w = torch.randn(16, 16, 3, 3, generator=gen).to(cuda).requires_grad_(True)
+    r = torch.randn(4, 16, 3, 32, generator=gen).to(cuda).requires_grad_(True)
+    y = conv2d(x, w, None, residual=r, drop_p=0.3, site=12345)
+    base = conv2d(x.detach(), w.detach(), None)
+    v = (y - r).detach()
+    kept = v != 0
+    frac = kept.float().mean().item()
+    assert 0.6 < frac < 0.8, frac
+    torch.testing.assert_close(v[kept], (base / 0.7)[kept], rtol=1e-5, atol=1e-5)
+    g = torch.randn_like(y)
+    y.backward(g)
+    torch.testing.assert_close(r.grad, g)
+    # dx = dgrad(g * mask / 0.7)
+    x2 = x.detach().clone().requires_grad_(True)
+    conv2d(x2, w.detach(), None).backward(g * kept / 0.7)
+    torch.testing.assert_close(x.grad, x2.grad, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("B,C,W,snake_on", [(8, 16, 32, True), (4, 4, 128, True), (16, 128, 8, True),
+                                            (8, 256, 96, False)])
+def test_bn_snake_train(B, C, W, snake_on, cuda):
+    from timevqvae.hip.norm import bn_snake
+    bn_c = torch.nn.BatchNorm2d(C).train()
+    with torch.no_grad():
+        bn_c.weight.uniform_(0.5, 1.5)
+        bn_c.bias.uniform_(-0.2, 0.2)
+        bn_c.running_var.uniform_(0.5, 1.5)
+    bn_d = torch.nn.BatchNorm2d(C).to(cuda).train()
+    bn_d.load_state_dict(bn_c.state_dict())
+    a_c = torch.empty(C).uniform_(0.2, 0.5).requires_grad_(True)
+    a_d = a_c.detach().to(cuda).requires_grad_(True)
+    gen = torch.Generator().manual_seed(2)
+    x_c = (torch.randn(B, C, 3, W, generator=gen) * 2 + 0.5).requires_grad_(True)
+    x_d = x_c.detach().to(cuda).requires_grad_(True)
+
+    def ref(x):
+        s = bn_c(x)
+        if snake_on:
+            a = a_c.view(1, C, 1, 1)
+            s = s + (1 / a) * torch.sin(a * s) ** 2
+        return s
+
+    y_c = ref(x_c)
+    y_d = bn_snake(x_d, bn_d, a_d if snake_on else None)
+    g = torch.randn(y_c.shape, generator=gen)
+    y_c.backward(g)
+    y_d.backward(g.to(cuda))
+    close(y_d, y_c, what="fwd")
+    close(x_d.grad, x_c.grad, tol=2e-5, what="dx")
+    close(bn_d.weight.grad, bn_c.weight.grad, what="dw")
+    close(bn_d.bias.grad, bn_c.bias.grad, what="db")
+    if snake_on:
+        close(a_d.grad, a_c.grad, tol=2e-5, what="da")
+    close(bn_d.running_mean, bn_c.running_mean, what="running_mean")
+    close(bn_d.running_var, bn_c.running_var, what="running_var")
+    assert int(bn_d.num_batches_tracked) == int(bn_c.num_batches_tracked)
+
+
+def test_bn_eval(cuda):
+    from timevqvae.hip.norm import bn_snake
+    bn_c = torch.nn.BatchNorm2d(32).eval()
+    with torch.no_grad():
+        bn_c.running_mean.uniform_(-1, 1)
+        bn_c.running_var.uniform_(0.5, 2)
+        bn_c.weight.uniform_(0.5, 1.5)
+    bn_d = torch.nn.BatchNorm2d(32).to(cuda).eval()
+    bn_d.load_state_dict(bn_c.state_dict())
+    x = torch.randn(4, 32, 3, 16)
+    a = torch.empty(32).uniform_(0.2, 0.5)
+    with torch.no_grad():
+        s = bn_c(x)
+        ref = s + (1 / a.view(1, -1, 1, 1)) * torch.sin(a.view(1, -1, 1, 1) * s) ** 2
+        got = bn_snake(x.to(cuda), bn_d, a.to(cuda))
+    close(got, ref, what="eval bn+snake")
+
+
+def test_snake(cuda):
+    from timevqvae.hip.norm import snake
+    C = 24
+    a_c = torch.empty(C).uniform_(0.2, 0.5).requires_grad_(True)
+    a_d = a_c.detach().to(cuda).requires_grad_(True)
+    oc, od, c, d = _run_both(lambda x: snake(x, a_d),
+                             lambda x: x + (1 / a_c.view(1, C, 1, 1)) * torch.sin(a_c.view(1, C, 1, 1) * x) ** 2,
+                             [(6, C, 3, 40)], cuda)
+    close(od, oc, what="fwd")
+    close(d[0].grad, c[0].grad, what="dx")
+    close(a_d.grad, a_c.grad, tol=2e-5, what="da")
+
+
+@pytest.mark.parametrize("T", [128, 256])
+def test_stft_encode_vs_golden(T, cuda):
+    from conftest import golden
+    from timevqvae.hip.signal import stft_encode
+    g = golden("g2_stft.npz")
+    x = torch.from_numpy(g[f"x_T{T}"]).to(cuda)
+    o = stft_encode(x, raw=True, enc_l=True, enc_h=True, tgt_l=True, tgt_h=True)
+    for k, gk in (("raw", "xf"), ("enc_l", "lf_copy"), ("enc_h", "hf_copy"), ("tgt_l", "x_l"), ("tgt_h", "x_h")):
+        np.testing.assert_allclose(o[k].cpu().numpy(), g[f"{gk}_T{T}"], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("T,band", [(128, "lf"), (256, "hf"), (256, "lf"), (128, "all")])
+def test_istft_decode(T, band, cuda):
+    """band-mask + iSTFT + Upsample(T, linear): fwd vs golden/oracle, bwd vs autograd of the oracle."""
+    from conftest import golden
+    from oracle import tvq_oracle as O
+    from timevqvae.hip.signal import istft_decode
+    g = golden("g2_stft.npz")
+    img = torch.from_numpy(g[f"dec_img_T{T}"])
+    mask = {"lf": O.band_lf, "hf": O.band_hf, "all": lambda z: z}[band]
+    img_c = img.clone().requires_grad_(True)
+    Tout = T if band != "all" else 2 * T - 1
+    y_c = O.linear_interp(O.istft4(mask(img_c), 6), Tout)
+    if band != "all":
+        np.testing.assert_allclose(O.istft4(mask(img), 6).numpy(), g[f"dec_istft_{band}_T{T}"], rtol=1e-5, atol=1e-6)
+    img_d = img.to(cuda).requires_grad_(True)
+    y_d = istft_decode(img_d, 6, band, Tout)
+    gy = torch.randn(y_c.shape)
+    y_c.backward(gy)
+    y_d.backward(gy.to(cuda))
+    close(y_d, y_c, what="fwd")
+    close(img_d.grad, img_c.grad, what="bwd")
+
+
+@pytest.mark.parametrize("M,K,N,res", [(1536, 256, 256, True), (100, 33, 70, False), (6400, 128, 513, False)])
+def test_linear(M, K, N, res, cuda):
+    from timevqvae.hip.linear import linear
+    shapes = [(M, K), (N, K), (N,)] + ([(M, N)] if res else [])
+
+    def ref(x, w, b, r=None):
+        y = F.linear(x, w, b)
+        return y + r if r is not None else y
+
+    def hip(x, w, b, r=None):
+        return linear(x, w, b, residual=r)
+
+    oc, od, c, d = _run_both(hip, ref, shapes, cuda)
+    close(od, oc, what="fwd")
+    for i in range(len(shapes)):
+        close(d[i].grad, c[i].grad, what=f"grad{i}")
+
+
+def test_losses(cuda):
+    from timevqvae.hip.loss import l1_loss, mse_loss
+    for f_hip, f_ref in ((mse_loss, F.mse_loss), (l1_loss, F.l1_loss)):
+        oc, od, c, d = _run_both(f_hip, f_ref, [(64, 6, 256), (64, 6, 256)], cuda)
+        close(od, oc, what="fwd")
+        close(d[0].grad, c[0].grad, what="d input")
+        close(d[1].grad, c[1].grad, what="d target")
+
+
+def test_adamw_matches_torch(cuda):
+    from timevqvae.hip.optim import FusedAdamW
+    gen = torch.Generator().manual_seed(3)
+    ps_c = [torch.randn(s, generator=gen).requires_grad_(True) for s in ((64, 32), (7,), (3, 3, 3))]
+    ps_d = [p.detach().to(cuda).requires_grad_(True) for p in ps_c]
+    oc = torch.optim.AdamW(ps_c, lr=1e-3)
+    od = FusedAdamW(ps_d, lr=1e-3)
+    for step in range(5):
+        grads = [torch.randn(p.shape, generator=gen) for p in ps_c]
+        oc.zero_grad()
+        od.zero_grad()
+        for pc, pd, g in zip(ps_c, ps_d, grads):
+            pc.grad = g.clone()
+            pd.grad.copy_(g)
+        oc.step()
+        od.step()
+    for pc, pd in zip(ps_c, ps_d):
+        torch.testing.assert_close(pd.detach().cpu(), pc.detach(), rtol=1e-6, atol=1e-6)
