@@ -1,0 +1,210 @@
+"""bench.py — stage1+stage2 train steps/s on synthetic (B,C,T) trajectories (BASELINE.json).
+
+One step = one stage1 VQ-VAE optimizer step + one stage2 MaskGIT optimizer step on a
+B=256, C=6, T=256 synthetic batch with K=512 codebooks (BASELINE configs[1..3];
+configs/config.yaml architecture otherwise).  N>1: one process per GPU, plain data
+parallel (RCCL all-reduce of the flat gradient buffer, the reference's sync_codebook
+EMA all-reduce), weak scaling (global batch 256*N).  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import copy
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "t-vq-vae-trajgen_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+B, C, T, K = 256, 6, 256, 512
+N_CLASSES = 5
+
+
+def config(sync):
+    return {
+        "VQ-VAE": {"n_fft": 4, "codebook_sizes": {"lf": K, "hf": K}, "sync_codebook": sync},
+        "encoder": {"init_dim": 4, "hid_dim": 128, "n_resnet_blocks": 2,
+                    "downsampled_width": {"lf": 8, "hf": 32}},
+        "decoder": {"n_resnet_blocks": 2},
+        "exp_params": {"lr": 1e-3, "linear_warmup_rate": 0.1},
+        "trainer_params": {"max_steps": {"stage1": 50000, "stage2": 200000}},
+        "MaskGIT": {
+            "choice_temperatures": {"lf": 10, "hf": 4}, "T": {"lf": 10, "hf": 1},
+            "prior_model_l": {"hidden_dim": 128, "n_layers": 4, "heads": 2, "ff_mult": 1,
+                              "use_rmsnorm": True, "p_unconditional": 0.2, "model_dropout": 0.3,
+                              "emb_dropout": 0.3},
+            "prior_model_h": {"hidden_dim": 32, "n_layers": 1, "heads": 1, "ff_mult": 1,
+                              "use_rmsnorm": True, "p_unconditional": 0.2, "model_dropout": 0.3,
+                              "emb_dropout": 0.3},
+            "cfg_scale": 1.0,
+        },
+    }
+
+
+def synthetic_batch(seed, device):
+    """random walk, min-max scaled per (c,t) to [-1,1]; y ~ U{0..4}."""
+    g = torch.Generator().manual_seed(seed)
+    x = torch.cumsum(0.1 * torch.randn(B, C, T, generator=g), -1)
+    lo, hi = x.amin(0, keepdim=True), x.amax(0, keepdim=True)
+    x = 2 * (x - lo) / (hi - lo + 1e-8) - 1
+    y = torch.randint(0, N_CLASSES, (B, 1), generator=g)
+    return x.to(device), y.to(device)
+
+
+class JointTrainer:
+    """stage1 step then stage2 step (stage2 trains on a frozen snapshot of stage1)."""
+
+    def __init__(self, device, world):
+        from timevqvae.trainers import Stage1, Stage2
+        from timevqvae.hip import rng
+        torch.manual_seed(0)
+        rng.manual_seed(1)
+        cfg = config(world > 1)
+        self.world = world
+        self.s1 = Stage1(T, C, cfg).to(device).train()
+        s1_frozen = copy.deepcopy(self.s1)
+        self.s2 = Stage2(None, None, T, C, N_CLASSES, config=cfg, stage1=s1_frozen).to(device).train()
+        self.opt1 = self.s1.configure_optimizers()["optimizer"]
+        self.opt2 = self.s2.configure_optimizers()["optimizer"]
+        if world > 1:  # identical initial replicas (DDP semantics)
+            for p in (self.opt1.flat, self.opt2.flat):
+                dist.broadcast(p, 0)
+            for m in (self.s1, self.s2):
+                for b in m.buffers():
+                    if b.is_floating_point():
+                        dist.broadcast(b, 0)
+        self.device = device
+
+    def _allreduce(self, opt):
+        if self.world > 1:
+            dist.all_reduce(opt.flat_grad)
+            opt.flat_grad.mul_(1.0 / self.world)
+
+    def step(self, batch):
+        from timevqvae.hip import rng
+        rng.advance(self.device)
+        self.opt1.zero_grad()
+        out1 = self.s1.training_step(batch, 0)
+        out1["loss"].sum().backward()
+        self._allreduce(self.opt1)
+        self.opt1.step()
+        self.opt2.zero_grad()
+        out2 = self.s2.training_step(batch, 0)
+        out2["loss"].backward()
+        self._allreduce(self.opt2)
+        self.opt2.step()
+        return out1, out2
+
+
+def roofline_leg(device):
+    """Average duration of the dominant kernel at its step shape, on the stream it runs on
+    (HIP events), with its algorithmic FLOPs -> achieved / peak."""
+    from timevqvae.hip.conv import conv2d
+    # HF encoder ResBlock(16->128) second conv: (256,128,3,32) x (128,128,3,3) -- the
+    # largest single launch of the step (7.25 GFLOP), SURVEY §2.2 K3
+    x = torch.randn(256, 128, 3, 32, device=device)
+    w = torch.randn(128, 128, 3, 3, device=device) * 0.03
+    b = torch.zeros(128, device=device)
+    for _ in range(3):
+        conv2d(x, w, b)
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 50
+    e0.record(st)
+    for _ in range(n):
+        conv2d(x, w, b)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    flops = 2.0 * (256 * 3 * 32) * 128 * (128 * 9)
+    achieved = flops / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": "conv_gemm_kernel<F,3,3,1> (ResBlock conv 128->128 @ 3x32, B=256)",
+            "achieved": round(achieved, 2), "peak": 157.3, "unit": "TFLOP/s",
+            "frac": round(achieved / 157.3, 4), "traffic": None, "avg_launch_ms": round(ms, 4),
+            "flops_per_launch": flops}
+
+
+def cpu_baseline_leg():
+    from oracle import cpu_baseline
+    threads = int(os.environ.get("TVQ_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    s = cpu_baseline.measure(threads, steps=2, warmup=1)
+    return {"value": round(1.0 / s, 4), "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"2 timed joint steps (after 1 warmup) of oracle/cpu_baseline.py at B=256,C=6,"
+                      f"T=256,K=512 on {threads} torch threads: {s:.3f} s/step; transformer "
+                      f"dropouts off in the restatement"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local)
+    tr = JointTrainer(device, world)
+    batch = synthetic_batch(1234 + rank, device)
+
+    for _ in range(args.warmup):
+        tr.step(batch)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out1, out2 = tr.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    loss1 = float(out1["loss"].detach().sum())
+    loss2 = float(out2["loss"].detach())
+
+    if rank == 0:
+        value = world * args.steps / elapsed
+        res = {
+            "metric": "stage1+stage2 train steps/sec on synthetic (B,C,T) trajectories, 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic",
+            "config": {"workload": "stage1 VQ-VAE + stage2 MaskGIT joint train step, per-GPU batch "
+                                   "(B=256,C=6,T=256), K=512, configs/config.yaml architecture",
+                       "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
+                       "trajectories_per_s": round(value * B, 1)},
+            "losses": {"stage1": round(loss1, 5), "stage2": round(loss2, 5)},
+        }
+        if not args.no_roofline:
+            res["roofline"] = roofline_leg(device)
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline_leg()
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

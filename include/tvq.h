@@ -183,14 +183,16 @@ int tvq_dropout_bwd(const float* dy, int64_t n, float p, const int64_t* seed_ptr
 
 /* ------------------------------------------------------------- dense GEMM
  * nn.Linear and friends: C[m,n] = epi(alpha * sum_k A(m,k) B(k,n)),
- * A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn]; epi: + bias[n],
- * act (0 none, 1 GELU-erf), + R[m*ldr+n], accumulate (C +=).  Workspace
+ * A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn]; epi: + bias[n]
+ * (pre-activation copy to `pre` if non-NULL), act (0 none, 1 GELU-erf),
+ * + R[(rmod ? m % rmod : m)*ldr + n] (residual, or the per-position logits bias
+ * of bidirectional_transformer.py:187), accumulate (C +=).  Workspace
  * (tvq_gemm_workspace floats) enables deterministic split-K. */
 int64_t tvq_gemm_workspace(int64_t M, int64_t N, int64_t K);
 int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
              float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha,
-             const float* bias, const float* R, int64_t ldr, int64_t act, int64_t accumulate,
-             float* workspace, tvq_stream_t stream);
+             const float* bias, const float* R, int64_t ldr, int64_t rmod, int64_t act, float* pre,
+             int64_t accumulate, float* workspace, tvq_stream_t stream);
 
 /* ------------------------------------------------------ losses, optimizer
  * F.mse_loss (kind 0) / F.l1_loss (kind 1) means (stage1.py:129,133); backward
@@ -207,6 +209,65 @@ int tvq_adamw_begin(float* lr_step, float lr, tvq_stream_t stream);
 int tvq_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
               const float* lr_step, float beta1, float beta2, float eps, float weight_decay,
               tvq_stream_t stream);
+
+/* ------------------------------------------------ MaskGIT transformer
+ * x-transformers internals used by BidirectionalTransformer
+ * (bidirectional_transformer.py:92-110; restated):
+ * RMSNorm F.normalize(x)*sqrt(D)*g; LayerNorm (post_emb_norm gamma-only, pred_head
+ * affine eps 1e-12, bidirectional_transformer.py:115); attention softmax(QK^T*scale)
+ * with dropout, head_dim 64, seq <= 128, Q/K/V/O in the Linear layout
+ * [(b*S+s)*ld + h*64 + d]; lse: [B*H*S] saved for the backward. */
+int tvq_rmsnorm_fwd(const float* x, int64_t M, int64_t D, const float* g, float scale, float* y,
+                    float* inv_norm, tvq_stream_t stream);
+int64_t tvq_norm_bwd_workspace(int64_t M, int64_t D);
+int tvq_rmsnorm_bwd(const float* dy, const float* x, int64_t M, int64_t D, const float* g,
+                    float scale, const float* inv_norm, float* dx, float* dg, int64_t accumulate,
+                    float* workspace, tvq_stream_t stream);
+int tvq_layernorm_fwd(const float* x, int64_t M, int64_t D, const float* gamma, const float* beta,
+                      float eps, float* y, float* mean, float* rstd, tvq_stream_t stream);
+int tvq_layernorm_bwd(const float* dy, const float* x, int64_t M, int64_t D, const float* gamma,
+                      const float* mean, const float* rstd, float* dx, float* dgamma,
+                      float* dbeta, int64_t accumulate, float* workspace, tvq_stream_t stream);
+int tvq_attention_fwd(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v,
+                      int64_t ldv, float* o, int64_t ldo, float* lse, int64_t B, int64_t H,
+                      int64_t S, int64_t Dh, float scale, float drop_p, const int64_t* seed_ptr,
+                      uint64_t offset, tvq_stream_t stream);
+int tvq_attention_bwd(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v,
+                      int64_t ldv, const float* out, int64_t ldout, const float* dout, int64_t ldd,
+                      const float* lse, int64_t B,
+                      int64_t H, int64_t S, int64_t Dh, float scale, float drop_p,
+                      const int64_t* seed_ptr, uint64_t offset, float* dq, float* dk, float* dv,
+                      int64_t ldg, tvq_stream_t stream);
+/* nn.Embedding lookups (tok_emb, pos/class emb) with the token-embedding dropout of
+ * _token_emb_dropout (bidirectional_transformer.py:152-164: dropout only where
+ * idx != mask_id); backward: deterministic per-row segmented sum. */
+int tvq_embedding_fwd(const int64_t* idx, int64_t M, int64_t D, const float* table, float* out,
+                      int64_t ldo, int64_t mask_id, float drop_p, const int64_t* seed_ptr,
+                      uint64_t offset, tvq_stream_t stream);
+int tvq_embedding_bwd(const int64_t* idx, int64_t M, int64_t D, const float* g, int64_t ldg,
+                      int64_t V, float* tgrad, int64_t accumulate, int64_t mask_id, float drop_p,
+                      const int64_t* seed_ptr, uint64_t offset, tvq_stream_t stream);
+/* F.cross_entropy(logits[~keep], s[~keep]) (maskgit.py:183-191); out = {loss, count}. */
+int64_t tvq_masked_ce_workspace(int64_t M);
+int tvq_masked_ce_fwd(const float* logits, int64_t ldl, int64_t M, int64_t K,
+                      const int64_t* target, const bool* keep, float* lse, float* out,
+                      float* workspace, tvq_stream_t stream);
+int tvq_masked_ce_bwd(const float* logits, int64_t ldl, int64_t M, int64_t K,
+                      const int64_t* target, const bool* keep, const float* lse,
+                      const float* stats, const float* gout, float* dlogits, int64_t ldd,
+                      tvq_stream_t stream);
+/* MaskGIT._randomly_mask_tokens (maskgit.py:194-216) on device: cosine schedule,
+ * per-row top-k of U[0,1) scores; ratio/rand may be given (testing) or NULL (device RNG). */
+int tvq_mask_tokens(const int64_t* s, int64_t B, int64_t n, int64_t mask_id,
+                    const int64_t* seed_ptr, uint64_t offset, const float* ratio,
+                    const float* rand, int64_t* s_M, bool* keep, tvq_stream_t stream);
+/* Upscale's F.interpolate(mode='nearest') (bidirectional_transformer.py:27) and GELU. */
+int tvq_upsample_nearest(const float* x, int64_t R, int64_t Lin, int64_t Lout, float* y,
+                         tvq_stream_t stream);
+int tvq_upsample_nearest_bwd(const float* dy, int64_t R, int64_t Lin, int64_t Lout, float* dx,
+                             tvq_stream_t stream);
+int tvq_gelu_fwd(const float* x, int64_t n, float* y, tvq_stream_t stream);
+int tvq_gelu_bwd(const float* dy, const float* x, int64_t n, float* dx, tvq_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,169 @@
+"""TEST INFRASTRUCTURE / CPU BASELINE ONLY — the reference's stage1+stage2 train step
+restated on torch CPU (the `cpu_baseline` leg of bench.py; "port" kind).
+
+Same work as one product joint step: stage1 forward/backward/AdamW
+(trainers/stage1.py:89-236) then stage2 forward/backward/AdamW with the frozen
+stage1 encoders (trainers/stage2.py:49-68, models/maskgit.py:155-216), dropout
+as in the reference (ResBlock 0.3; transformer dropouts off because the
+x-transformers restatement is inference-exact only — noted in the sample string).
+"""
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import tvq_oracle as O
+
+
+def _init_stage1(spec, K, hid, seed=0):
+    """Deterministic random weights shaped like trainers/stage1.py's module tree."""
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+
+    def conv(p, co, ci, kh, kw, t=False):
+        shape = (ci, co, kh, kw) if t else (co, ci, kh, kw)
+        sd[p + "weight"] = torch.randn(shape, generator=g) / np.sqrt(ci * kh * kw)
+        sd[p + "bias"] = torch.zeros(co)
+
+    def bn(p, c):
+        sd[p + "weight"] = torch.ones(c)
+        sd[p + "bias"] = torch.zeros(c)
+        sd[p + "running_mean"] = torch.zeros(c)
+        sd[p + "running_var"] = torch.ones(c)
+        sd[p + "num_batches_tracked"] = torch.tensor(0)
+
+    def snake(p, c):
+        sd[p + "a"] = torch.rand(1, c, 1, 1, generator=g) * 0.3 + 0.2
+
+    for br, enc, dec in (("l", spec.enc_l, spec.dec_l), ("h", spec.enc_h, spec.dec_h)):
+        for i, (kind, ci, co) in enumerate(enc):
+            p = f"encoder_{br}.encoder.{i}."
+            if kind == "enc":
+                conv(p + "block.0.", co, ci, 3, 4); bn(p + "block.1.", co); snake(p + "block.2.", co)
+            else:
+                _res(sd, p, ci, co, conv, bn, snake)
+        for i, (kind, ci, co) in enumerate(dec):
+            p = f"decoder_{br}.decoder.{i}."
+            if kind == "res":
+                _res(sd, p, ci, co, conv, bn, snake)
+            elif kind == "dec":
+                conv(p + "block.0.", co, ci, 3, 4, t=True); bn(p + "block.1.", co); snake(p + "block.2.", co)
+            else:
+                conv(p, co, ci, 3, 4, t=True)
+        sd[f"decoder_{br}.linear.weight"] = torch.randn(spec.T, spec.T, generator=g) / np.sqrt(spec.T)
+        sd[f"decoder_{br}.linear.bias"] = torch.zeros(spec.T)
+        E = torch.randn(K, hid, generator=g)
+        sd[f"vq_model_{br}._codebook.embed"] = E
+        sd[f"vq_model_{br}._codebook.embed_avg"] = E.clone()
+        sd[f"vq_model_{br}._codebook.cluster_size"] = torch.zeros(K)
+    return sd
+
+
+def _res(sd, p, ci, co, conv, bn, snake):
+    snake(p + "convs.0.", ci)
+    conv(p + "convs.1.", co, ci, 3, 3)
+    bn(p + "convs.2.", co)
+    snake(p + "convs.3.", co)
+    conv(p + "convs.4.", co, co, 3, 3)
+    if ci != co:
+        conv(p + "proj.", co, ci, 1, 1)
+
+
+def _init_xf(kind, K, emb, hidden, depth, heads, ntok, n_classes, seed):
+    g = torch.Generator().manual_seed(seed)
+    in_dim = emb if kind == "lf" else 2 * emb
+    r = lambda *s: torch.randn(*s, generator=g) * 0.02
+    sd = {"tok_emb_l.weight": r(K + 1, emb), "pos_emb.weight": r(ntok + 1, in_dim),
+          "class_condition_emb.weight": r(n_classes + 1, in_dim),
+          "blocks.project_in.weight": r(hidden, in_dim), "blocks.post_emb_norm.gamma": torch.ones(hidden),
+          "blocks.project_out.weight": r(in_dim, hidden),
+          "blocks.attn_layers.final_norm.g": torch.ones(hidden),
+          "pred_head.0.weight": r(emb, in_dim), "pred_head.0.bias": torch.zeros(emb),
+          "pred_head.2.weight": torch.ones(emb), "pred_head.2.bias": torch.zeros(emb),
+          "bias": torch.zeros(ntok, K + 1)}
+    if kind == "hf":
+        sd["tok_emb_h.weight"] = r(K + 1, emb)
+        sd["projector.conv.0.weight"] = r(2 * emb, emb, 3); sd["projector.conv.0.bias"] = torch.zeros(2 * emb)
+        sd["projector.conv.2.weight"] = torch.ones(2 * emb); sd["projector.conv.2.bias"] = torch.zeros(2 * emb)
+        sd["projector.conv.2.running_mean"] = torch.zeros(2 * emb)
+        sd["projector.conv.2.running_var"] = torch.ones(2 * emb)
+        sd["projector.conv.2.num_batches_tracked"] = torch.tensor(0)
+        sd["projector.conv.3.weight"] = r(emb, 2 * emb, 3); sd["projector.conv.3.bias"] = torch.zeros(emb)
+    for i in range(2 * depth):
+        p = f"blocks.attn_layers.layers.{i}."
+        sd[p + "0.0.g"] = torch.ones(hidden)
+        if i % 2 == 0:
+            for w in ("to_q", "to_k", "to_v"):
+                sd[p + f"1.{w}.weight"] = r(heads * 64, hidden)
+            sd[p + "1.to_out.weight"] = r(hidden, heads * 64)
+        else:
+            sd[p + "1.ff.0.0.weight"] = r(hidden, hidden); sd[p + "1.ff.0.0.bias"] = torch.zeros(hidden)
+            sd[p + "1.ff.2.weight"] = r(hidden, hidden); sd[p + "1.ff.2.bias"] = torch.zeros(hidden)
+    return sd
+
+
+class JointStep:
+    """One stage1 + one stage2 optimizer step of the reference, on torch CPU."""
+
+    def __init__(self, B=256, C=6, T=256, K=512, hid=128, n_classes=5, seed=0):
+        self.spec = O.Stage1Spec(T, C, 4, hid)
+        self.K = K
+        sd = _init_stage1(self.spec, K, hid, seed)
+        self.s1_params = {k: v.requires_grad_(True) for k, v in sd.items()
+                          if v.is_floating_point() and not k.split(".")[-1] in
+                          ("running_mean", "running_var", "embed", "embed_avg", "cluster_size")}
+        self.sd1 = sd
+        self.opt1 = torch.optim.AdamW(list(self.s1_params.values()), lr=1e-3)
+        self.frozen = {k: v.detach().clone() for k, v in sd.items()}
+        self.xl = _init_xf("lf", K, hid, 128, 4, 2, 24, n_classes, seed + 1)
+        self.xh = _init_xf("hf", K, hid, 32, 1, 1, 96, n_classes, seed + 2)
+        self.xf_params = [v.requires_grad_(True) for d in (self.xl, self.xh) for k, v in d.items()
+                          if v.is_floating_point() and "running" not in k]
+        self.opt2 = torch.optim.AdamW(self.xf_params, lr=1e-3)
+        g = torch.Generator().manual_seed(1234)
+        x = torch.cumsum(0.1 * torch.randn(B, C, T, generator=g), -1)
+        self.x = 2 * (x - x.amin(0, keepdim=True)) / (x.amax(0, keepdim=True) - x.amin(0, keepdim=True) + 1e-8) - 1
+        self.y = torch.randint(0, n_classes, (B, 1), generator=g)
+        self.rng = np.random.default_rng(0)
+
+    def step(self):
+        # ---- stage1
+        self.opt1.zero_grad()
+        ctx = O.Ctx(True, dropout_p=0.3)
+        out = O.stage1_forward(ctx, self.sd1, self.spec, self.x)
+        out["loss"].backward()
+        self.opt1.step()
+        with torch.no_grad():
+            for k, v in ctx.updates.items():
+                self.sd1[k] = v.detach()
+        # ---- stage2 (frozen stage1 snapshot, eval)
+        self.opt2.zero_grad()
+        with torch.no_grad():
+            e = O.Ctx(False)
+            z_l = O.encoder_forward(e, self.frozen, "encoder_l.", self.x, self.spec.enc_l, O.band_lf)
+            _, s_l, _, _ = O.quantize(e, self.frozen, "vq_model_l.", z_l)
+            z_h = O.encoder_forward(e, self.frozen, "encoder_h.", self.x, self.spec.enc_h, O.band_hf)
+            _, s_h, _, _ = O.quantize(e, self.frozen, "vq_model_h.", z_h)
+        B = s_l.shape[0]
+        sMl, kl = O.random_mask_tokens(s_l, self.K, self.rng.uniform(0, 1, B), torch.rand(s_l.shape))
+        sMh, kh = O.random_mask_tokens(s_h, self.K, self.rng.uniform(0, 1, B), torch.rand(s_h.shape))
+        c = O.Ctx(True)
+        ll = O.transformer_forward(c, self.xl, "lf", sMl, None, self.y, self.K, 2, 4)
+        lh = O.transformer_forward(c, self.xh, "hf", sMl, sMh, self.y, self.K, 1, 1)
+        loss = O.masked_ce(ll, s_l, kl) + O.masked_ce(lh, s_h, kh)
+        loss.backward()
+        self.opt2.step()
+        return float(out["loss"]), float(loss)
+
+
+def measure(threads, steps=2, warmup=1, B=256):
+    """Seconds per joint step of the CPU restatement (bounded sample)."""
+    torch.set_num_threads(threads)
+    js = JointStep(B=B)
+    for _ in range(warmup):
+        js.step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        js.step()
+    return (time.perf_counter() - t0) / steps

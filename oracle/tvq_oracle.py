@@ -370,3 +370,113 @@ def sample_step(logits, s, mask_token_id, t, T, unknown0, temperature, u_cat, u_
     masking = torch.zeros_like(conf, dtype=torch.bool)
     masking.scatter_(1, idx, True)
     return torch.where(masking, torch.full_like(sampled, mask_token_id), sampled)
+
+
+# ----------------------------------------------------------------------------
+# Bidirectional transformer (bidirectional_transformer.py:34-251) with the
+# x-transformers 1.3x encoder RESTATED (the package is absent: parity unpinned)
+# ----------------------------------------------------------------------------
+def xf_rmsnorm(x, g):
+    """x-transformers RMSNorm: F.normalize(x, dim=-1) * sqrt(D) * g."""
+    return F.normalize(x, dim=-1) * (x.shape[-1] ** 0.5) * g
+
+
+def xf_blocks(sd, p, x, heads, depth):
+    """ContinuousTransformerWrapper(project_in, post_emb_norm, Encoder(pre_norm), project_out)."""
+    h = F.linear(x, sd[p + "project_in.weight"])
+    h = F.layer_norm(h, h.shape[-1:]) * sd[p + "post_emb_norm.gamma"]
+    for i in range(2 * depth):
+        q = f"{p}attn_layers.layers.{i}."
+        n = xf_rmsnorm(h, sd[q + "0.0.g"])
+        if i % 2 == 0:
+            B, S, _ = n.shape
+            qq = F.linear(n, sd[q + "1.to_q.weight"]).view(B, S, heads, 64).transpose(1, 2)
+            kk = F.linear(n, sd[q + "1.to_k.weight"]).view(B, S, heads, 64).transpose(1, 2)
+            vv = F.linear(n, sd[q + "1.to_v.weight"]).view(B, S, heads, 64).transpose(1, 2)
+            att = torch.softmax(qq @ kk.transpose(-1, -2) * 64 ** -0.5, dim=-1)
+            o = (att @ vv).transpose(1, 2).reshape(B, S, heads * 64)
+            out = F.linear(o, sd[q + "1.to_out.weight"])
+        else:
+            u = F.gelu(F.linear(n, sd[q + "1.ff.0.0.weight"], sd[q + "1.ff.0.0.bias"]))
+            out = F.linear(u, sd[q + "1.ff.2.weight"], sd[q + "1.ff.2.bias"])
+        h = h + out
+    h = xf_rmsnorm(h, sd[p + "attn_layers.final_norm.g"])
+    return F.linear(h, sd[p + "project_out.weight"])
+
+
+def upscale(ctx, sd, p, x, m):
+    """Upscale (bidirectional_transformer.py:12-30): (b n d) -> (b m d)."""
+    x = F.interpolate(x.transpose(1, 2), size=(m,), mode="nearest")
+    x = F.conv1d(x, sd[p + "conv.0.weight"], sd[p + "conv.0.bias"], padding=1)
+    x = F.gelu(x)
+    x = _bn(ctx, sd, p + "conv.2.", x)
+    x = F.conv1d(x, sd[p + "conv.3.weight"], sd[p + "conv.3.bias"], padding=1)
+    return x.transpose(1, 2)
+
+
+def transformer_forward(ctx, sd, kind, s_l, s_h, cls_idx, K, heads, depth):
+    """forward_lf / forward_hf (bidirectional_transformer.py:166-236), dropout off;
+    cls_idx (b,1) is the (already drop-resolved) class index (n_classes = uncond)."""
+    tok = F.embedding(s_l, sd["tok_emb_l.weight"])
+    table = "tok_emb_l.weight"
+    if kind == "hf":
+        th = F.embedding(s_h, sd["tok_emb_h.weight"])
+        tok = torch.cat([upscale(ctx, sd, "projector.", tok, th.shape[1]), th], dim=-1)
+        table = "tok_emb_h.weight"
+    cls = F.embedding(cls_idx, sd["class_condition_emb.weight"])
+    n = tok.shape[1]
+    x = torch.cat([cls, tok + sd["pos_emb.weight"][:n]], dim=1)
+    x = xf_blocks(sd, "blocks.", x, heads, depth)
+    x = F.linear(x, sd["pred_head.0.weight"], sd["pred_head.0.bias"])
+    x = F.layer_norm(F.gelu(x), x.shape[-1:], sd["pred_head.2.weight"], sd["pred_head.2.bias"], 1e-12)
+    x = x[:, 1:, :]
+    logits = x @ sd[table].t() + sd["bias"]
+    return logits[:, :, :-1]
+
+
+def masked_ce(logits, s, keep):
+    """maskgit.py:183-191."""
+    return F.cross_entropy(logits[~keep].float(), s[~keep].long())
+
+
+def _mask_by_random_topk_torch(mask_len, probs, temperature):
+    """maskgit.py:238-267, same torch RNG consumption (uniform_ for the Gumbel noise)."""
+    def log(t, eps=1e-20):
+        return torch.log(t.clamp(min=eps))
+
+    noise = torch.zeros_like(probs).uniform_(0, 1)
+    confidence = torch.log(probs + 1e-5) + temperature * (-log(-log(noise)))
+    k = int(mask_len.unique().item())
+    ind = torch.topk(confidence, k=k, dim=-1, largest=False).indices
+    masking = torch.zeros_like(confidence)
+    masking.scatter_(1, ind, 1.0)
+    return masking.bool()
+
+
+def _pass_torch(logit_fn, s, mask_id, T, temp, unknown0):
+    """first_pass / second_pass (maskgit.py:294-411) with torch's own sampling calls."""
+    for t in range(T):
+        logits = logit_fn(s)
+        sampled = torch.distributions.categorical.Categorical(logits=logits).sample()
+        unknown = s == mask_id
+        sampled = torch.where(unknown, sampled, s)
+        ratio = 1.0 * (t + 1) / T
+        mask_ratio = gamma_cosine(ratio)
+        probs = F.softmax(logits, dim=-1)
+        sel = torch.gather(probs, dim=-1, index=sampled.unsqueeze(-1)).squeeze()
+        sel = torch.where(unknown, sel, torch.Tensor([torch.inf]))
+        mask_len = torch.clip(torch.unsqueeze(torch.floor(unknown0 * mask_ratio), 1), min=0.0)
+        masking = _mask_by_random_topk_torch(mask_len, sel, temp * (1.0 - ratio))
+        s = torch.where(masking, mask_id, sampled)
+    return s
+
+
+def iterative_decoding_torch(tf_l, tf_h, num, n_l, n_h, mask_l, mask_h, T, temp_l, temp_h):
+    """iterative_decoding (maskgit.py:413-446), unconditional, CPU, torch RNG."""
+    s_l = (mask_l * torch.ones((num, n_l))).to(torch.int64)
+    s_h = (mask_h * torch.ones((num, n_h))).to(torch.int64)
+    unk_l = torch.sum(s_l == mask_l, dim=-1)
+    unk_h = torch.sum(s_h == mask_h, dim=-1)
+    s_l = _pass_torch(tf_l, s_l, mask_l, T["lf"], temp_l, unk_l)
+    s_h = _pass_torch(lambda sh: tf_h(s_l, sh), s_h, mask_h, T["hf"], temp_h, unk_h)
+    return s_l, s_h

@@ -21,6 +21,8 @@ struct GemmArgs {
   const float* bias;
   const float* R;
   int64_t ldr;
+  int64_t rmod;    // R row = m % rmod when > 0 (per-position bias broadcast over the batch)
+  float* pre;      // optional: pre-activation output (ldc layout), for the GELU backward
   int act;         // 0 none, 1 GELU(erf)
   int accumulate;  // C += result
   float alpha;
@@ -35,8 +37,9 @@ __device__ __forceinline__ float gelu_erf(float x) {
 __device__ __forceinline__ float apply_epi(const GemmArgs& g, int m, int n, float v) {
   v *= g.alpha;
   if (g.bias) v += g.bias[n];
+  if (g.pre) g.pre[(int64_t)m * g.ldc + n] = v;
   if (g.act == 1) v = gelu_erf(v);
-  if (g.R) v += g.R[(int64_t)m * g.ldr + n];
+  if (g.R) v += g.R[(int64_t)(g.rmod > 0 ? m % g.rmod : m) * g.ldr + n];
   if (g.accumulate) v += g.C[(int64_t)m * g.ldc + n];
   return v;
 }
@@ -169,14 +172,16 @@ extern "C" int64_t tvq_gemm_workspace(int64_t M, int64_t N, int64_t K) {
 
 extern "C" int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
                         int64_t sbn, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                        float alpha, const float* bias, const float* R, int64_t ldr, int64_t act,
-                        int64_t accumulate, float* workspace, tvq_stream_t stream) {
+                        float alpha, const float* bias, const float* R, int64_t ldr, int64_t rmod,
+                        int64_t act, float* pre, int64_t accumulate, float* workspace,
+                        tvq_stream_t stream) {
   TVQ_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0, "tvq_gemm: bad arguments");
   GemmArgs g;
   g.A = A; g.B = B; g.C = C;
   g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.sam = sam; g.sak = sak; g.sbk = sbk; g.sbn = sbn; g.ldc = ldc;
-  g.bias = bias; g.R = R; g.ldr = ldr; g.act = (int)act; g.accumulate = (int)accumulate;
+  g.bias = bias; g.R = R; g.ldr = ldr; g.rmod = rmod; g.pre = pre;
+  g.act = (int)act; g.accumulate = (int)accumulate;
   g.alpha = alpha;
   const int TM = M >= 128 ? 128 : 64, TN = N >= 64 ? 64 : 32;
   const int tiles = (int)(((M + TM - 1) / TM) * ((N + TN - 1) / TN));

@@ -1,0 +1,758 @@
+// MaskGIT bidirectional-transformer kernels (K11-K16 in SURVEY.md §2.2).
+//
+//  rmsnorm     x-transformers RMSNorm: F.normalize(x) * sqrt(D) * g
+//  layernorm   LayerNorm over the last dim (gamma [+ beta]), eps given
+//  attention   softmax(Q K^T * scale) [dropout] V for seq <= 128, one workgroup
+//              per (batch, head): Q/K/V tiles and the score matrix live in LDS,
+//              scores/probabilities never touch HBM; backward recomputes P from
+//              the saved row log-sum-exp.  Q/K/V/O are read in the Linear layout
+//              [(b*S + s) * ld + h*Dh + d] so no head transposes are materialised.
+//  embedding   table gather (+ dropout on non-mask tokens) and a deterministic
+//              per-row scatter-add backward (no float atomics)
+//  masked CE   cross_entropy over the masked positions (maskgit.py:183-191)
+//  mask tokens _randomly_mask_tokens (maskgit.py:194-216) fully on device
+//  upsample    F.interpolate(mode='nearest') along the last dim and its backward
+//  gelu        elementwise GELU(erf) fwd/bwd
+#include <float.h>
+#include <math.h>
+
+#include "tvq_common.h"
+
+namespace tvq {
+
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+  const float pdf = 0.39894228040143267794f * expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// ------------------------------------------------------------------ RMSNorm
+// one wave per row
+__global__ void rmsnorm_fwd_kernel(const float* __restrict__ x, int64_t M, int D,
+                                   const float* __restrict__ g, float scale, float* __restrict__ y,
+                                   float* __restrict__ inv_norm) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + row * D;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) s += xr[d] * xr[d];
+  s = wave_sum(s);
+  const float inv = 1.0f / fmaxf(sqrtf(s), 1e-12f);
+  for (int d = lane; d < D; d += 64) y[row * D + d] = xr[d] * inv * scale * g[d];
+  if (lane == 0) inv_norm[row] = inv;
+}
+
+// dx; and per-block partial dg (deterministic, reduced by colsum_kernel)
+__global__ void rmsnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                   int64_t M, int D, const float* __restrict__ g, float scale,
+                                   const float* __restrict__ inv_norm, float* __restrict__ dx,
+                                   float* __restrict__ dg_part, int rows_per_block) {
+  extern __shared__ float sh[];  // [waves][D] partial dg
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int d = threadIdx.x; d < nw * D; d += blockDim.x) sh[d] = 0.f;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  for (int64_t row = r0 + wid; row < min(M, r0 + rows_per_block); row += nw) {
+    const float* xr = x + row * D;
+    const float* gr = dy + row * D;
+    const float inv = inv_norm[row];
+    // y = x * inv * scale * g ; norm = 1/inv (assumes ||x|| > 1e-12)
+    float dot = 0.f;
+    for (int d = lane; d < D; d += 64) dot += gr[d] * g[d] * xr[d];
+    dot = wave_sum(dot);
+    const float c = dot * scale * inv * inv * inv;
+    for (int d = lane; d < D; d += 64) {
+      dx[row * D + d] = gr[d] * g[d] * scale * inv - xr[d] * c;
+      sh[wid * D + d] += gr[d] * xr[d] * inv * scale;
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int w = 0; w < nw; ++w) s += sh[w * D + d];
+    dg_part[(int64_t)blockIdx.x * D + d] = s;
+  }
+}
+
+// out[d] (+)= sum_p part[p][d]
+__global__ void colsum_kernel(const float* __restrict__ part, int P, int D, float* __restrict__ out,
+                              int accumulate) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(int64_t)p * D + d];
+  out[d] = accumulate ? out[d] + s : s;
+}
+
+// ---------------------------------------------------------------- LayerNorm
+__global__ void layernorm_fwd_kernel(const float* __restrict__ x, int64_t M, int D,
+                                     const float* __restrict__ gamma,
+                                     const float* __restrict__ beta, float eps,
+                                     float* __restrict__ y, float* __restrict__ mean_out,
+                                     float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + row * D;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) s += xr[d];
+  const float mean = wave_sum(s) / (float)D;
+  float v = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float t = xr[d] - mean;
+    v += t * t;
+  }
+  const float var = wave_sum(v) / (float)D;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  for (int d = lane; d < D; d += 64) {
+    float t = (xr[d] - mean) * rstd * (gamma ? gamma[d] : 1.f);
+    if (beta) t += beta[d];
+    y[row * D + d] = t;
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+__global__ void layernorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                     int64_t M, int D, const float* __restrict__ gamma,
+                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                     float* __restrict__ dx, float* __restrict__ part,
+                                     int rows_per_block) {
+  extern __shared__ float sh[];  // [waves][2][D]: dgamma, dbeta partials
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int d = threadIdx.x; d < nw * 2 * D; d += blockDim.x) sh[d] = 0.f;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  for (int64_t row = r0 + wid; row < min(M, r0 + rows_per_block); row += nw) {
+    const float* xr = x + row * D;
+    const float* gr = dy + row * D;
+    const float mu = mean[row], rs = rstd[row];
+    float s1 = 0.f, s2 = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      const float xh = (xr[d] - mu) * rs;
+      const float gg = gr[d] * (gamma ? gamma[d] : 1.f);
+      s1 += gg;
+      s2 += gg * xh;
+      sh[(wid * 2) * D + d] += gr[d] * xh;
+      sh[(wid * 2 + 1) * D + d] += gr[d];
+    }
+    s1 = wave_sum(s1) / (float)D;
+    s2 = wave_sum(s2) / (float)D;
+    for (int d = lane; d < D; d += 64) {
+      const float xh = (xr[d] - mu) * rs;
+      const float gg = gr[d] * (gamma ? gamma[d] : 1.f);
+      dx[row * D + d] = rs * (gg - s1 - xh * s2);
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < 2 * D; d += blockDim.x) {
+    const int k = d / D, dd = d - k * D;
+    float s = 0.f;
+    for (int w = 0; w < nw; ++w) s += sh[(w * 2 + k) * D + dd];
+    part[((int64_t)blockIdx.x * 2 + k) * D + dd] = s;
+  }
+}
+
+// dgamma[d] (+)= sum_p ws[p][0][d], dbeta[d] (+)= sum_p ws[p][1][d]
+__global__ void ln_colsum2_kernel(const float* __restrict__ ws, int P, int D,
+                                  float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                  int accumulate) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 2 * D) return;
+  const int k = e / D, d = e - k * D;
+  float* dst = k == 0 ? dgamma : dbeta;
+  if (!dst) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += ws[((int64_t)p * 2 + k) * D + d];
+  dst[d] = accumulate ? dst[d] + s : s;
+}
+
+// ---------------------------------------------------------------- attention
+// Q/K/V/O element (b, s, h, d) at base + (b*S + s)*ld + h*DH + d.  One 256-thread
+// workgroup per (b, h).  LDS: Qs, Ks, Vs [S][DH+1], P [S][S+1].
+constexpr int ATT_DH = 64;
+
+struct AttnArgs {
+  const float* q; const float* k; const float* v;
+  int64_t ldq, ldk, ldv;
+  float* o; int64_t ldo;
+  float* lse;  // [B*H*S]
+  int B, H, S;
+  float scale;
+  float drop_p;
+  const int64_t* seed_ptr;
+  uint64_t offset;
+};
+
+__device__ __forceinline__ bool attn_keep(uint64_t seed, int64_t bh, int S, int i, int j, float p) {
+  return uniform01(seed, ((uint64_t)bh * S + i) * S + j) >= p;
+}
+
+__global__ __launch_bounds__(256) void attention_fwd_kernel(AttnArgs a) {
+  extern __shared__ float sm[];
+  const int S = a.S;
+  constexpr int LD = ATT_DH + 1;
+  float* Qs = sm;
+  float* Ks = Qs + S * LD;
+  float* Vs = Ks + S * LD;
+  float* P = Vs + S * LD;  // [S][S+1]
+  const int PL = S + 1;
+  const int bh = blockIdx.x;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < S * ATT_DH; e += 256) {
+    const int s = e / ATT_DH, d = e - s * ATT_DH;
+    const int64_t r = (int64_t)b * S + s;
+    Qs[s * LD + d] = a.q[r * a.ldq + h * ATT_DH + d];
+    Ks[s * LD + d] = a.k[r * a.ldk + h * ATT_DH + d];
+    Vs[s * LD + d] = a.v[r * a.ldv + h * ATT_DH + d];
+  }
+  __syncthreads();
+  for (int e = tid; e < S * S; e += 256) {
+    const int i = e / S, j = e - i * S;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int d = 0; d < ATT_DH; ++d) acc = fmaf(Qs[i * LD + d], Ks[j * LD + d], acc);
+    P[i * PL + j] = acc * a.scale;
+  }
+  __syncthreads();
+  // row softmax: one wave per row
+  const int lane = tid & 63, wid = tid >> 6;
+  const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
+  const float dscale = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  for (int i = wid; i < S; i += 4) {
+    float mx = -INFINITY;
+    for (int j = lane; j < S; j += 64) mx = fmaxf(mx, P[i * PL + j]);
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int j = lane; j < S; j += 64) {
+      const float e = expf(P[i * PL + j] - mx);
+      P[i * PL + j] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    const float inv = 1.0f / sum;
+    for (int j = lane; j < S; j += 64) {
+      float p = P[i * PL + j] * inv;
+      if (a.drop_p > 0.f) p = attn_keep(seed, bh, S, i, j, a.drop_p) ? p * dscale : 0.f;
+      P[i * PL + j] = p;
+    }
+    if (lane == 0) a.lse[(int64_t)bh * S + i] = mx + logf(sum);
+  }
+  __syncthreads();
+  for (int e = tid; e < S * ATT_DH; e += 256) {
+    const int i = e / ATT_DH, d = e - i * ATT_DH;
+    float acc = 0.f;
+    for (int j = 0; j < S; ++j) acc = fmaf(P[i * PL + j], Vs[j * LD + d], acc);
+    a.o[((int64_t)b * S + i) * a.ldo + h * ATT_DH + d] = acc;
+  }
+}
+
+struct AttnBwdArgs {
+  AttnArgs f;
+  const float* out; int64_t ldout;  // forward output O (for D_i = dO_i . O_i)
+  const float* dout; int64_t ldd;
+  float* dq; float* dk; float* dv; int64_t ldg;  // grads in the Q/K/V layout with stride ldg
+};
+
+// LDS: Qs, Ks, Vs, dOs [S][LD], A [S][S+1], Dr [S].  Two phases over one S x S array:
+//   1) A = P_drop (recomputed from lse)          -> dV = A^T dO
+//   2) A = dS = P * (dP - D_i), D_i = dO_i . O_i -> dQ = A K scale, dK = A^T Q scale
+// (sum_j P_ij dP_ij = dO_i . O_i holds with dropout since O = P_drop V).
+__global__ __launch_bounds__(256) void attention_bwd_kernel(AttnBwdArgs ab) {
+  extern __shared__ float sm[];
+  const AttnArgs& a = ab.f;
+  const int S = a.S;
+  constexpr int LD = ATT_DH + 1;
+  const int PL = S + 1;
+  float* Qs = sm;
+  float* Ks = Qs + S * LD;
+  float* Vs = Ks + S * LD;
+  float* dOs = Vs + S * LD;
+  float* A = dOs + S * LD;
+  float* Dr = A + S * PL;
+  const int bh = blockIdx.x;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int e = tid; e < S * ATT_DH; e += 256) {
+    const int s = e / ATT_DH, d = e - s * ATT_DH;
+    const int64_t r = (int64_t)b * S + s;
+    Qs[s * LD + d] = a.q[r * a.ldq + h * ATT_DH + d];
+    Ks[s * LD + d] = a.k[r * a.ldk + h * ATT_DH + d];
+    Vs[s * LD + d] = a.v[r * a.ldv + h * ATT_DH + d];
+    dOs[s * LD + d] = ab.dout[r * ab.ldd + h * ATT_DH + d];
+  }
+  for (int i = wid; i < S; i += 4) {
+    const int64_t r = (int64_t)b * S + i;
+    float t = 0.f;
+    for (int d = lane; d < ATT_DH; d += 64)
+      t += ab.dout[r * ab.ldd + h * ATT_DH + d] * ab.out[r * ab.ldout + h * ATT_DH + d];
+    t = wave_sum(t);
+    if (lane == 0) Dr[i] = t;
+  }
+  __syncthreads();
+  const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
+  const float dscale = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  // phase 1: A = P_drop
+  for (int e = tid; e < S * S; e += 256) {
+    const int i = e / S, j = e - i * S;
+    float s = 0.f;
+#pragma unroll 8
+    for (int d = 0; d < ATT_DH; ++d) s = fmaf(Qs[i * LD + d], Ks[j * LD + d], s);
+    float p = expf(s * a.scale - a.lse[(int64_t)bh * S + i]);
+    if (a.drop_p > 0.f) p = attn_keep(seed, bh, S, i, j, a.drop_p) ? p * dscale : 0.f;
+    A[i * PL + j] = p;
+  }
+  __syncthreads();
+  for (int e = tid; e < S * ATT_DH; e += 256) {
+    const int j = e / ATT_DH, d = e - j * ATT_DH;
+    float dv = 0.f;
+    for (int i = 0; i < S; ++i) dv = fmaf(A[i * PL + j], dOs[i * LD + d], dv);
+    ab.dv[((int64_t)b * S + j) * ab.ldg + h * ATT_DH + d] = dv;
+  }
+  __syncthreads();
+  // phase 2: A = dS
+  for (int e = tid; e < S * S; e += 256) {
+    const int i = e / S, j = e - i * S;
+    float s = 0.f, dp = 0.f;
+#pragma unroll 8
+    for (int d = 0; d < ATT_DH; ++d) {
+      s = fmaf(Qs[i * LD + d], Ks[j * LD + d], s);
+      dp = fmaf(dOs[i * LD + d], Vs[j * LD + d], dp);
+    }
+    const float p = expf(s * a.scale - a.lse[(int64_t)bh * S + i]);
+    if (a.drop_p > 0.f) dp = attn_keep(seed, bh, S, i, j, a.drop_p) ? dp * dscale : 0.f;
+    A[i * PL + j] = p * (dp - Dr[i]);
+  }
+  __syncthreads();
+  for (int e = tid; e < S * ATT_DH; e += 256) {
+    const int i = e / ATT_DH, d = e - i * ATT_DH;
+    float dq = 0.f, dk = 0.f;
+    for (int j = 0; j < S; ++j) {
+      dq = fmaf(A[i * PL + j], Ks[j * LD + d], dq);
+      dk = fmaf(A[j * PL + i], Qs[j * LD + d], dk);
+    }
+    const int64_t r = ((int64_t)b * S + i) * ab.ldg + h * ATT_DH + d;
+    ab.dq[r] = dq * a.scale;
+    ab.dk[r] = dk * a.scale;
+  }
+}
+
+// ---------------------------------------------------------------- embedding
+// out[m, :] = table[idx[m], :]  (* dropout where idx[m] != keep_id) ; out row stride ldo
+__global__ void embedding_fwd_kernel(const int64_t* __restrict__ idx, int64_t M, int D,
+                                     const float* __restrict__ table, float* __restrict__ out,
+                                     int64_t ldo, int64_t mask_id, float drop_p,
+                                     const int64_t* seed_ptr, uint64_t offset) {
+  const uint64_t seed = drop_p > 0.f ? mix_seed(seed_ptr, offset) : 0ull;
+  const float sc = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  const int64_t tot = M * D;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = e / D;
+    const int d = (int)(e - m * D);
+    const int64_t t = idx[m];
+    float v = table[t * D + d];
+    if (drop_p > 0.f && t != mask_id) v = uniform01(seed, (uint64_t)e) >= drop_p ? v * sc : 0.f;
+    out[m * ldo + d] = v;
+  }
+}
+
+// table_grad[r, :] (+)= sum_{m: idx[m] == r} g[m, :] * dropout-mask ; one block per table row
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(
+    const int64_t* __restrict__ idx, int64_t M, int D, const float* __restrict__ g, int64_t ldg,
+    float* __restrict__ tgrad, int accumulate, int64_t mask_id, float drop_p,
+    const int64_t* seed_ptr, uint64_t offset) {
+  __shared__ int rows[256];
+  __shared__ int wcnt[4];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint64_t seed = drop_p > 0.f ? mix_seed(seed_ptr, offset) : 0ull;
+  const float sc = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  const bool drop_here = drop_p > 0.f && (int64_t)r != mask_id;
+  float acc0 = 0.f, acc1 = 0.f;
+  for (int64_t base = 0; base < M; base += 256) {
+    const int64_t m = base + tid;
+    const bool match = m < M && idx[m] == r;
+    const uint64_t bal = __ballot(match);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wcnt[wid] = __popcll(bal);
+    __syncthreads();
+    int woff = 0, total = 0;
+    for (int w = 0; w < 4; ++w) { if (w < wid) woff += wcnt[w]; total += wcnt[w]; }
+    if (match) rows[woff + pre] = (int)(m - base);
+    __syncthreads();
+    for (int j = 0; j < total; ++j) {
+      const int64_t mm = base + rows[j];
+      if (tid < D) {
+        float v = g[mm * ldg + tid];
+        if (drop_here) v = uniform01(seed, (uint64_t)(mm * D + tid)) >= drop_p ? v * sc : 0.f;
+        acc0 += v;
+      }
+      if (tid + 256 < D) {
+        float v = g[mm * ldg + tid + 256];
+        if (drop_here) v = uniform01(seed, (uint64_t)(mm * D + tid + 256)) >= drop_p ? v * sc : 0.f;
+        acc1 += v;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < D) tgrad[(int64_t)r * D + tid] = accumulate ? tgrad[(int64_t)r * D + tid] + acc0 : acc0;
+  if (tid + 256 < D)
+    tgrad[(int64_t)r * D + tid + 256] = accumulate ? tgrad[(int64_t)r * D + tid + 256] + acc1 : acc1;
+}
+
+// ---------------------------------------------------------------- masked CE
+// per row (one wave): if !keep[m]: loss_m = lse(logits[m,:K]) - logits[m, t]; part sums
+__global__ __launch_bounds__(256) void masked_ce_fwd_kernel(const float* __restrict__ logits,
+                                                            int64_t ldl, int64_t M, int K,
+                                                            const int64_t* __restrict__ target,
+                                                            const bool* __restrict__ keep,
+                                                            float* __restrict__ lse_out,
+                                                            float* __restrict__ part) {
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float ls = 0.f, cnt = 0.f;
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wid; m < M; m += (int64_t)gridDim.x * 4) {
+    if (keep[m]) continue;  // only masked positions contribute
+    const float* lr = logits + m * ldl;
+    float mx = -INFINITY;
+    for (int k = lane; k < K; k += 64) mx = fmaxf(mx, lr[k]);
+    mx = wave_max(mx);
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s += expf(lr[k] - mx);
+    s = wave_sum(s);
+    const float lse = mx + logf(s);
+    if (lane == 0) {
+      lse_out[m] = lse;
+      ls += lse - lr[target[m]];
+      cnt += 1.f;
+    }
+  }
+  if (lane == 0) { red[0][wid] = ls; red[1][wid] = cnt; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    part[2 * blockIdx.x + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+}
+
+__global__ __launch_bounds__(256) void masked_ce_final_kernel(const float* __restrict__ part, int P,
+                                                              float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f, c = 0.f;
+  for (int i = threadIdx.x; i < P; i += 256) { s += part[2 * i]; c += part[2 * i + 1]; }
+  s = block_sum(s, red);
+  c = block_sum(c, red);
+  if (threadIdx.x == 0) { out[0] = s / c; out[1] = c; }
+}
+
+// dlogits[m,k] = keep[m] ? 0 : g/cnt * (softmax - onehot)
+__global__ void masked_ce_bwd_kernel(const float* __restrict__ logits, int64_t ldl, int64_t M, int K,
+                                     const int64_t* __restrict__ target,
+                                     const bool* __restrict__ keep, const float* __restrict__ lse,
+                                     const float* __restrict__ stats, const float* __restrict__ gout,
+                                     float* __restrict__ dlogits, int64_t ldd) {
+  const float gc = gout[0] / stats[1];
+  const int64_t tot = M * K;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = e / K;
+    const int k = (int)(e - m * K);
+    float v = 0.f;
+    if (!keep[m]) {
+      v = expf(logits[m * ldl + k] - lse[m]);
+      if (k == target[m]) v -= 1.0f;
+      v *= gc;
+    }
+    dlogits[m * ldd + k] = v;
+  }
+}
+
+// ---------------------------------------------------------------- masking
+// maskgit.py:194-216 on device.  Per row: ratio ~ U[0,1); n_unmask =
+// clip(floor(cos(ratio*pi/2) * n), 0, n-1); keep the n_unmask positions with the
+// largest U[0,1) scores (ties -> lower index, like torch.topk).  s_M = keep ? s : mask_id.
+__global__ void mask_tokens_kernel(const int64_t* __restrict__ s, int B, int n, int64_t mask_id,
+                                   const int64_t* seed_ptr, uint64_t offset,
+                                   const float* __restrict__ ratio_in,
+                                   const float* __restrict__ rand_in, int64_t* __restrict__ s_M,
+                                   bool* __restrict__ keep) {
+  extern __shared__ float sc[];  // [n]
+  const int b = blockIdx.x;
+  const uint64_t seed = mix_seed(seed_ptr, offset);
+  for (int j = threadIdx.x; j < n; j += blockDim.x)
+    sc[j] = rand_in ? rand_in[(int64_t)b * n + j] : uniform01(seed, (uint64_t)b * (n + 1) + 1 + j);
+  __syncthreads();
+  const double ratio = ratio_in ? (double)ratio_in[b] : (double)uniform01(seed, (uint64_t)b * (n + 1));
+  // numpy float64 in the reference: floor(cos(r*pi/2) * n), clip to [0, n-1]
+  double nu = floor(cos(ratio * 3.14159265358979323846 / 2.0) * (double)n);
+  nu = fmin(fmax(nu, 0.0), (double)(n - 1));
+  const int n_unmask = (int)nu;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const float v = sc[j];
+    int rank = 0;
+    for (int k = 0; k < n; ++k) rank += (sc[k] > v) || (sc[k] == v && k < j);
+    const bool kp = rank < n_unmask;
+    keep[(int64_t)b * n + j] = kp;
+    s_M[(int64_t)b * n + j] = kp ? s[(int64_t)b * n + j] : mask_id;
+  }
+}
+
+// ---------------------------------------------------------------- misc
+// nearest interpolation along the last dim: out[r, j] = in[r, floor(j * scale)]
+__global__ void upsample_nearest_kernel(const float* __restrict__ x, int64_t R, int Lin, int Lout,
+                                        float scale, float* __restrict__ y) {
+  const int64_t tot = R * Lout;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / Lout;
+    const int j = (int)(e - r * Lout);
+    int src = (int)floorf((float)j * scale);
+    if (src > Lin - 1) src = Lin - 1;
+    y[e] = x[r * Lin + src];
+  }
+}
+
+__global__ void upsample_nearest_bwd_kernel(const float* __restrict__ dy, int64_t R, int Lin,
+                                            int Lout, float scale, float* __restrict__ dx) {
+  const int64_t tot = R * Lin;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / Lin;
+    const int i = (int)(e - r * Lin);
+    float s = 0.f;
+    // outputs j with floor(j*scale) == i
+    int j0 = (int)floorf((float)i / scale) - 2;
+    if (j0 < 0) j0 = 0;
+    for (int j = j0; j < Lout; ++j) {
+      int src = (int)floorf((float)j * scale);
+      if (src > Lin - 1) src = Lin - 1;
+      if (src > i) break;
+      if (src == i) s += dy[r * Lout + j];
+    }
+    dx[e] = s;
+  }
+}
+
+__global__ void gelu_fwd_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ y) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = gelu_f(x[i]);
+}
+__global__ void gelu_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x, int64_t n,
+                                float* __restrict__ dx) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dx[i] = dy[i] * gelu_grad(x[i]);
+}
+
+static int grid_for(int64_t n, int cap = 8192) {
+  int64_t b = (n + 255) / 256;
+  if (b < 1) b = 1;
+  return (int)(b < cap ? b : cap);
+}
+
+static int norm_rows_per_block(int64_t M) {
+  // ~256 blocks of rows for the deterministic partial-sum backward
+  int64_t r = (M + 255) / 256;
+  return (int)(r < 4 ? 4 : r);
+}
+
+}  // namespace tvq
+
+using namespace tvq;
+
+extern "C" int tvq_rmsnorm_fwd(const float* x, int64_t M, int64_t D, const float* g, float scale,
+                               float* y, float* inv_norm, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && g && y && inv_norm && M > 0 && D > 0, "tvq_rmsnorm_fwd: bad arguments");
+  hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, x, M, (int)D, g, scale, y, inv_norm);
+  return launch_status("tvq_rmsnorm_fwd");
+}
+
+extern "C" int64_t tvq_norm_bwd_workspace(int64_t M, int64_t D) {
+  const int rpb = norm_rows_per_block(M);
+  return ((M + rpb - 1) / rpb) * 2 * D;
+}
+
+extern "C" int tvq_rmsnorm_bwd(const float* dy, const float* x, int64_t M, int64_t D,
+                               const float* g, float scale, const float* inv_norm, float* dx,
+                               float* dg, int64_t accumulate, float* workspace,
+                               tvq_stream_t stream) {
+  TVQ_CHECK_ARG(dy && x && g && inv_norm && dx && dg && workspace, "tvq_rmsnorm_bwd: bad args");
+  const int rpb = norm_rows_per_block(M);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(nb), dim3(256), 4 * D * sizeof(float), st, dy, x, M,
+                     (int)D, g, scale, inv_norm, dx, workspace, rpb);
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((D + 127) / 128)), dim3(128), 0, st, workspace,
+                     nb, (int)D, dg, (int)accumulate);
+  return launch_status("tvq_rmsnorm_bwd");
+}
+
+extern "C" int tvq_layernorm_fwd(const float* x, int64_t M, int64_t D, const float* gamma,
+                                 const float* beta, float eps, float* y, float* mean, float* rstd,
+                                 tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && y && mean && rstd && M > 0 && D > 0, "tvq_layernorm_fwd: bad arguments");
+  hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, x, M, (int)D, gamma, beta, eps, y, mean, rstd);
+  return launch_status("tvq_layernorm_fwd");
+}
+
+extern "C" int tvq_layernorm_bwd(const float* dy, const float* x, int64_t M, int64_t D,
+                                 const float* gamma, const float* mean, const float* rstd,
+                                 float* dx, float* dgamma, float* dbeta, int64_t accumulate,
+                                 float* workspace, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(dy && x && mean && rstd && dx && workspace, "tvq_layernorm_bwd: bad args");
+  const int rpb = norm_rows_per_block(M);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nb), dim3(256), 8 * D * sizeof(float), st, dy, x, M,
+                     (int)D, gamma, mean, rstd, dx, workspace, rpb);
+  hipLaunchKernelGGL(ln_colsum2_kernel, dim3((unsigned)((2 * D + 127) / 128)), dim3(128), 0, st,
+                     workspace, nb, (int)D, dgamma, dbeta, (int)accumulate);
+  return launch_status("tvq_layernorm_bwd");
+}
+
+extern "C" int tvq_attention_fwd(const float* q, int64_t ldq, const float* k, int64_t ldk,
+                                 const float* v, int64_t ldv, float* o, int64_t ldo, float* lse,
+                                 int64_t B, int64_t H, int64_t S, int64_t Dh, float scale,
+                                 float drop_p, const int64_t* seed_ptr, uint64_t offset,
+                                 tvq_stream_t stream) {
+  TVQ_CHECK_ARG(q && k && v && o && lse && B > 0 && H > 0, "tvq_attention_fwd: bad arguments");
+  TVQ_CHECK_ARG(Dh == ATT_DH && S >= 1 && S <= 128, "tvq_attention_fwd: need Dh=64, S<=128");
+  AttnArgs a;
+  a.q = q; a.k = k; a.v = v; a.ldq = ldq; a.ldk = ldk; a.ldv = ldv;
+  a.o = o; a.ldo = ldo; a.lse = lse;
+  a.B = (int)B; a.H = (int)H; a.S = (int)S; a.scale = scale;
+  a.drop_p = drop_p; a.seed_ptr = seed_ptr; a.offset = offset;
+  const size_t lds = (size_t)(3 * S * (ATT_DH + 1) + S * (S + 1)) * sizeof(float);
+  hipLaunchKernelGGL(attention_fwd_kernel, dim3((unsigned)(B * H)), dim3(256), lds,
+                     (hipStream_t)stream, a);
+  return launch_status("tvq_attention_fwd");
+}
+
+extern "C" int tvq_attention_bwd(const float* q, int64_t ldq, const float* k, int64_t ldk,
+                                 const float* v, int64_t ldv, const float* out, int64_t ldout,
+                                 const float* dout, int64_t ldd,
+                                 const float* lse, int64_t B, int64_t H, int64_t S, int64_t Dh,
+                                 float scale, float drop_p, const int64_t* seed_ptr,
+                                 uint64_t offset, float* dq, float* dk, float* dv, int64_t ldg,
+                                 tvq_stream_t stream) {
+  TVQ_CHECK_ARG(q && k && v && out && dout && lse && dq && dk && dv,
+                "tvq_attention_bwd: bad arguments");
+  TVQ_CHECK_ARG(Dh == ATT_DH && S >= 1 && S <= 128, "tvq_attention_bwd: need Dh=64, S<=128");
+  AttnBwdArgs ab;
+  ab.f.q = q; ab.f.k = k; ab.f.v = v; ab.f.ldq = ldq; ab.f.ldk = ldk; ab.f.ldv = ldv;
+  ab.f.o = nullptr; ab.f.ldo = 0; ab.f.lse = (float*)lse;
+  ab.f.B = (int)B; ab.f.H = (int)H; ab.f.S = (int)S; ab.f.scale = scale;
+  ab.f.drop_p = drop_p; ab.f.seed_ptr = seed_ptr; ab.f.offset = offset;
+  ab.out = out; ab.ldout = ldout;
+  ab.dout = dout; ab.ldd = ldd; ab.dq = dq; ab.dk = dk; ab.dv = dv; ab.ldg = ldg;
+  const size_t lds = (size_t)(4 * S * (ATT_DH + 1) + S * (S + 1) + S) * sizeof(float);
+  hipLaunchKernelGGL(attention_bwd_kernel, dim3((unsigned)(B * H)), dim3(256), lds,
+                     (hipStream_t)stream, ab);
+  return launch_status("tvq_attention_bwd");
+}
+
+extern "C" int tvq_embedding_fwd(const int64_t* idx, int64_t M, int64_t D, const float* table,
+                                 float* out, int64_t ldo, int64_t mask_id, float drop_p,
+                                 const int64_t* seed_ptr, uint64_t offset, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(idx && table && out && M > 0 && D > 0, "tvq_embedding_fwd: bad arguments");
+  hipLaunchKernelGGL(embedding_fwd_kernel, dim3(grid_for(M * D)), dim3(256), 0, (hipStream_t)stream,
+                     idx, M, (int)D, table, out, ldo, mask_id, drop_p, seed_ptr, offset);
+  return launch_status("tvq_embedding_fwd");
+}
+
+extern "C" int tvq_embedding_bwd(const int64_t* idx, int64_t M, int64_t D, const float* g,
+                                 int64_t ldg, int64_t V, float* tgrad, int64_t accumulate,
+                                 int64_t mask_id, float drop_p, const int64_t* seed_ptr,
+                                 uint64_t offset, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(idx && g && tgrad && M > 0 && D > 0 && D <= 512 && V > 0,
+                "tvq_embedding_bwd: bad arguments");
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3((unsigned)V), dim3(256), 0, (hipStream_t)stream,
+                     idx, M, (int)D, g, ldg, tgrad, (int)accumulate, mask_id, drop_p, seed_ptr,
+                     offset);
+  return launch_status("tvq_embedding_bwd");
+}
+
+extern "C" int64_t tvq_masked_ce_workspace(int64_t M) {
+  int64_t nb = (M + 3) / 4;
+  if (nb > 1024) nb = 1024;
+  return 2 * nb;
+}
+
+// out: device float[2] = {loss, count}; lse: [M] scratch kept for the backward
+extern "C" int tvq_masked_ce_fwd(const float* logits, int64_t ldl, int64_t M, int64_t K,
+                                 const int64_t* target, const bool* keep, float* lse, float* out,
+                                 float* workspace, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(logits && target && keep && lse && out && workspace && M > 0 && K > 0,
+                "tvq_masked_ce_fwd: bad arguments");
+  const int nb = (int)(tvq_masked_ce_workspace(M) / 2);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(masked_ce_fwd_kernel, dim3(nb), dim3(256), 0, st, logits, ldl, M, (int)K,
+                     target, keep, lse, workspace);
+  hipLaunchKernelGGL(masked_ce_final_kernel, dim3(1), dim3(256), 0, st, workspace, nb, out);
+  return launch_status("tvq_masked_ce_fwd");
+}
+
+extern "C" int tvq_masked_ce_bwd(const float* logits, int64_t ldl, int64_t M, int64_t K,
+                                 const int64_t* target, const bool* keep, const float* lse,
+                                 const float* stats, const float* gout, float* dlogits,
+                                 int64_t ldd, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(logits && target && keep && lse && stats && gout && dlogits,
+                "tvq_masked_ce_bwd: bad arguments");
+  hipLaunchKernelGGL(masked_ce_bwd_kernel, dim3(grid_for(M * K)), dim3(256), 0, (hipStream_t)stream,
+                     logits, ldl, M, (int)K, target, keep, lse, stats, gout, dlogits, ldd);
+  return launch_status("tvq_masked_ce_bwd");
+}
+
+extern "C" int tvq_mask_tokens(const int64_t* s, int64_t B, int64_t n, int64_t mask_id,
+                               const int64_t* seed_ptr, uint64_t offset, const float* ratio,
+                               const float* rand, int64_t* s_M, bool* keep, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(s && s_M && keep && B > 0 && n > 0 && n <= 4096, "tvq_mask_tokens: bad arguments");
+  hipLaunchKernelGGL(mask_tokens_kernel, dim3((unsigned)B), dim3(128), n * sizeof(float),
+                     (hipStream_t)stream, s, (int)B, (int)n, mask_id, seed_ptr, offset, ratio, rand,
+                     s_M, keep);
+  return launch_status("tvq_mask_tokens");
+}
+
+extern "C" int tvq_upsample_nearest(const float* x, int64_t R, int64_t Lin, int64_t Lout, float* y,
+                                    tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && y && R > 0 && Lin > 0 && Lout > 0, "tvq_upsample_nearest: bad arguments");
+  const float scale = (float)Lin / (float)Lout;
+  hipLaunchKernelGGL(upsample_nearest_kernel, dim3(grid_for(R * Lout)), dim3(256), 0,
+                     (hipStream_t)stream, x, R, (int)Lin, (int)Lout, scale, y);
+  return launch_status("tvq_upsample_nearest");
+}
+
+extern "C" int tvq_upsample_nearest_bwd(const float* dy, int64_t R, int64_t Lin, int64_t Lout,
+                                        float* dx, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(dy && dx && R > 0 && Lin > 0 && Lout > 0, "tvq_upsample_nearest_bwd: bad args");
+  const float scale = (float)Lin / (float)Lout;
+  hipLaunchKernelGGL(upsample_nearest_bwd_kernel, dim3(grid_for(R * Lin)), dim3(256), 0,
+                     (hipStream_t)stream, dy, R, (int)Lin, (int)Lout, scale, dx);
+  return launch_status("tvq_upsample_nearest_bwd");
+}
+
+extern "C" int tvq_gelu_fwd(const float* x, int64_t n, float* y, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && y && n >= 0, "tvq_gelu_fwd: bad arguments");
+  if (n == 0) return TVQ_OK;
+  hipLaunchKernelGGL(gelu_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, y);
+  return launch_status("tvq_gelu_fwd");
+}
+
+extern "C" int tvq_gelu_bwd(const float* dy, const float* x, int64_t n, float* dx,
+                            tvq_stream_t stream) {
+  TVQ_CHECK_ARG(dy && x && dx && n >= 0, "tvq_gelu_bwd: bad arguments");
+  if (n == 0) return TVQ_OK;
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dy, x, n,
+                     dx);
+  return launch_status("tvq_gelu_bwd");
+}

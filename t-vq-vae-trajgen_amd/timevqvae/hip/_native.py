@@ -68,13 +68,33 @@ sig("tvq_snake_bwd", P, P, I64, I64, I64, P, P, P, I64, P, P)
 sig("tvq_dropout_bwd", P, I64, F32, P, U64, P, P)
 # --- dense GEMM --------------------------------------------------------------
 sig("tvq_gemm_workspace", I64, I64, I64, restype=I64)
-sig("tvq_gemm", P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, F32, P, P, I64, I64, I64, P, P)
+sig("tvq_gemm", P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, F32, P, P, I64, I64, I64, P, I64, P, P)
 # --- losses / optimizer --------------------------------------------------------
 sig("tvq_loss_workspace", I64, restype=I64)
 sig("tvq_loss_fwd", P, P, I64, I64, P, P, P)
 sig("tvq_loss_bwd", P, P, I64, I64, P, P, P)
 sig("tvq_adamw_begin", P, F32, P)
 sig("tvq_adamw", P, P, P, P, I64, P, F32, F32, F32, F32, P)
+
+# --- MaskGIT transformer ---------------------------------------------------------
+sig("tvq_rmsnorm_fwd", P, I64, I64, P, F32, P, P, P)
+sig("tvq_norm_bwd_workspace", I64, I64, restype=I64)
+sig("tvq_rmsnorm_bwd", P, P, I64, I64, P, F32, P, P, P, I64, P, P)
+sig("tvq_layernorm_fwd", P, I64, I64, P, P, F32, P, P, P, P)
+sig("tvq_layernorm_bwd", P, P, I64, I64, P, P, P, P, P, P, I64, P, P)
+sig("tvq_attention_fwd", P, I64, P, I64, P, I64, P, I64, P, I64, I64, I64, I64, F32, F32, P, U64, P)
+sig("tvq_attention_bwd", P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, I64, I64, I64, F32, F32, P,
+    U64, P, P, P, I64, P)
+sig("tvq_embedding_fwd", P, I64, I64, P, P, I64, I64, F32, P, U64, P)
+sig("tvq_embedding_bwd", P, I64, I64, P, I64, I64, P, I64, I64, F32, P, U64, P)
+sig("tvq_masked_ce_workspace", I64, restype=I64)
+sig("tvq_masked_ce_fwd", P, I64, I64, I64, P, P, P, P, P, P)
+sig("tvq_masked_ce_bwd", P, I64, I64, I64, P, P, P, P, P, P, I64, P)
+sig("tvq_mask_tokens", P, I64, I64, I64, P, U64, P, P, P, P, P)
+sig("tvq_upsample_nearest", P, I64, I64, I64, P, P)
+sig("tvq_upsample_nearest_bwd", P, I64, I64, I64, P, P)
+sig("tvq_gelu_fwd", P, I64, P, P)
+sig("tvq_gelu_bwd", P, P, I64, P, P)
 
 
 class NativeError(RuntimeError):

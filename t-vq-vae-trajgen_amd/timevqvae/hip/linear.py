@@ -5,7 +5,7 @@ from ._native import call, ptr, stream_ptr, value
 
 
 def gemm(A, sam, sak, B, sbk, sbn, M, N, K, out=None, ldc=None, alpha=1.0, bias=None, R=None,
-         ldr=0, act=0, accumulate=False):
+         ldr=0, rmod=0, act=0, pre=None, accumulate=False):
     dev = A.device
     if out is None:
         out = torch.empty((M, N), device=dev, dtype=torch.float32)
@@ -13,7 +13,8 @@ def gemm(A, sam, sak, B, sbk, sbn, M, N, K, out=None, ldc=None, alpha=1.0, bias=
     wsz = value("tvq_gemm_workspace", M, N, K)
     ws = torch.empty(wsz, device=dev, dtype=torch.float32) if wsz > 0 else None
     call("tvq_gemm", ptr(A), sam, sak, ptr(B), sbk, sbn, ptr(out), ldc, M, N, K, float(alpha),
-         ptr(bias), ptr(R), ldr, int(act), int(bool(accumulate)), ptr(ws), stream_ptr())
+         ptr(bias), ptr(R), ldr, int(rmod), int(act), ptr(pre), int(bool(accumulate)), ptr(ws),
+         stream_ptr())
     return out
 
 

@@ -1,0 +1,288 @@
+"""MaskGIT transformer ops on the HIP path (include/tvq.h §MaskGIT transformer)."""
+import math
+
+import torch
+
+from . import rng
+from ._native import call, ptr, stream_ptr, value
+from .linear import _bias_grad_rows, gemm
+
+
+def _rows(x):
+    D = x.shape[-1]
+    return x.reshape(-1, D), x.numel() // D, D
+
+
+# ------------------------------------------------------------------ RMSNorm
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, scale):
+        x2, M, D = _rows(x.contiguous())
+        y = torch.empty_like(x2)
+        inv = torch.empty(M, device=x.device, dtype=torch.float32)
+        call("tvq_rmsnorm_fwd", ptr(x2), M, D, ptr(g), float(scale), ptr(y), ptr(inv), stream_ptr())
+        ctx.save_for_backward(x2, g, inv)
+        ctx.scale = scale
+        ctx.shape = x.shape
+        return y.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, g, inv = ctx.saved_tensors
+        M, D = x2.shape
+        dy = gy.reshape(M, D).contiguous()
+        dx = torch.empty_like(x2)
+        dg = torch.empty(D, device=x2.device)
+        ws = torch.empty(value("tvq_norm_bwd_workspace", M, D), device=x2.device)
+        call("tvq_rmsnorm_bwd", ptr(dy), ptr(x2), M, D, ptr(g), float(ctx.scale), ptr(inv), ptr(dx),
+             ptr(dg), 0, ptr(ws), stream_ptr())
+        return dx.reshape(ctx.shape), dg, None
+
+
+def rmsnorm(x, g):
+    """x-transformers RMSNorm: F.normalize(x, dim=-1) * sqrt(D) * g."""
+    return _RMSNorm.apply(x, g, math.sqrt(x.shape[-1]))
+
+
+# ---------------------------------------------------------------- LayerNorm
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        x2, M, D = _rows(x.contiguous())
+        y = torch.empty_like(x2)
+        mean = torch.empty(M, device=x.device)
+        rstd = torch.empty(M, device=x.device)
+        call("tvq_layernorm_fwd", ptr(x2), M, D, ptr(gamma), ptr(beta), float(eps), ptr(y),
+             ptr(mean), ptr(rstd), stream_ptr())
+        ctx.save_for_backward(x2, gamma, mean, rstd)
+        ctx.has = (gamma is not None, beta is not None)
+        ctx.shape = x.shape
+        return y.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, gamma, mean, rstd = ctx.saved_tensors
+        M, D = x2.shape
+        dy = gy.reshape(M, D).contiguous()
+        dx = torch.empty_like(x2)
+        dg = torch.empty(D, device=x2.device) if ctx.has[0] else None
+        db = torch.empty(D, device=x2.device) if ctx.has[1] else None
+        ws = torch.empty(value("tvq_norm_bwd_workspace", M, D), device=x2.device)
+        call("tvq_layernorm_bwd", ptr(dy), ptr(x2), M, D, ptr(gamma), ptr(mean), ptr(rstd), ptr(dx),
+             ptr(dg), ptr(db), 0, ptr(ws), stream_ptr())
+        return dx.reshape(ctx.shape), dg, db, None
+
+
+def layer_norm(x, gamma=None, beta=None, eps=1e-5):
+    return _LayerNorm.apply(x, gamma, beta, float(eps))
+
+
+# ---------------------------------------------------------------- Linear (+GELU)
+class _LinearAct(torch.autograd.Function):
+    """y = act(x W^T + b); act 1 = GELU(erf) with the pre-activation kept for backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        K = x.shape[-1]
+        N = w.shape[0]
+        x2 = x.reshape(-1, K).contiguous()
+        w = w.contiguous()
+        M = x2.shape[0]
+        pre = torch.empty((M, N), device=x.device) if act else None
+        y = gemm(x2, K, 1, w, 1, K, M, N, K, bias=b, act=act, pre=pre)
+        ctx.save_for_backward(x2, w, pre)
+        ctx.act = act
+        ctx.has_b = b is not None
+        ctx.shape = x.shape
+        return y.reshape(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w, pre = ctx.saved_tensors
+        M, K = x2.shape
+        N = w.shape[0]
+        g = gy.reshape(M, N).contiguous()
+        if ctx.act:
+            gp = torch.empty_like(g)
+            call("tvq_gelu_bwd", ptr(g), ptr(pre), g.numel(), ptr(gp), stream_ptr())
+            g = gp
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(g, N, 1, w, K, 1, M, K, N).reshape(ctx.shape)
+        if ctx.needs_input_grad[1]:
+            dw = gemm(g, 1, N, x2, K, 1, N, K, M)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = _bias_grad_rows(g)
+        return dx, dw, db, None
+
+
+def linear_act(x, weight, bias=None, gelu=False):
+    return _LinearAct.apply(x, weight, bias, 1 if gelu else 0)
+
+
+# ---------------------------------------------------------------- attention
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, heads, drop_p, site):
+        # q/k/v: (B, S, heads*64) contiguous
+        B, S, HD = q.shape
+        Dh = HD // heads
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        o = torch.empty_like(q)
+        lse = torch.empty(B * heads * S, device=q.device)
+        seed = rng.seed_tensor(q.device) if drop_p > 0 else None
+        off = rng.call_offset(site) if drop_p > 0 else 0
+        scale = Dh ** -0.5
+        call("tvq_attention_fwd", ptr(q), HD, ptr(k), HD, ptr(v), HD, ptr(o), HD, ptr(lse), B,
+             heads, S, Dh, float(scale), float(drop_p), ptr(seed), off, stream_ptr())
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.cfg = (heads, drop_p, off, scale)
+        ctx.seed = seed
+        return o
+
+    @staticmethod
+    def backward(ctx, go):
+        q, k, v, o, lse = ctx.saved_tensors
+        heads, drop_p, off, scale = ctx.cfg
+        B, S, HD = q.shape
+        Dh = HD // heads
+        go = go.contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        call("tvq_attention_bwd", ptr(q), HD, ptr(k), HD, ptr(v), HD, ptr(o), HD, ptr(go), HD,
+             ptr(lse), B,
+             heads, S, Dh, float(scale), float(drop_p), ptr(ctx.seed), off, ptr(dq), ptr(dk),
+             ptr(dv), HD, stream_ptr())
+        return dq, dk, dv, None, None, None
+
+
+def attention(q, k, v, heads, drop_p=0.0, site=0):
+    """softmax(q k^T / sqrt(64)) [dropout] v per head; q/k/v (B, S, heads*64)."""
+    return _Attention.apply(q, k, v, int(heads), float(drop_p), int(site))
+
+
+# ---------------------------------------------------------------- embedding
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, table, mask_id, drop_p, site):
+        idx = idx.contiguous()
+        M = idx.numel()
+        V, D = table.shape
+        out = torch.empty((M, D), device=table.device)
+        seed = rng.seed_tensor(table.device) if drop_p > 0 else None
+        off = rng.call_offset(site) if drop_p > 0 else 0
+        call("tvq_embedding_fwd", ptr(idx), M, D, ptr(table), ptr(out), D, int(mask_id),
+             float(drop_p), ptr(seed), off, stream_ptr())
+        ctx.save_for_backward(idx)
+        ctx.cfg = (V, D, mask_id, drop_p, off)
+        ctx.seed = seed
+        return out.reshape(*idx.shape, D)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        V, D, mask_id, drop_p, off = ctx.cfg
+        M = idx.numel()
+        g2 = g.reshape(M, D).contiguous()
+        tg = torch.empty((V, D), device=g.device)
+        call("tvq_embedding_bwd", ptr(idx), M, D, ptr(g2), D, V, ptr(tg), 0, int(mask_id),
+             float(drop_p), ptr(ctx.seed), off, stream_ptr())
+        return None, tg, None, None, None
+
+
+def embedding(idx, table, mask_id=-1, drop_p=0.0, site=0):
+    """table[idx] with dropout on positions where idx != mask_id (mask_id=-1: everywhere)."""
+    return _Embedding.apply(idx, table, int(mask_id), float(drop_p), int(site))
+
+
+# ---------------------------------------------------------------- masked CE
+class _MaskedCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, keep):
+        K = logits.shape[-1]
+        l2 = logits.reshape(-1, K).contiguous()
+        M = l2.shape[0]
+        t = target.reshape(-1).contiguous()
+        kp = keep.reshape(-1).contiguous()
+        lse = torch.empty(M, device=logits.device)
+        out = torch.empty(2, device=logits.device)
+        ws = torch.empty(value("tvq_masked_ce_workspace", M), device=logits.device)
+        call("tvq_masked_ce_fwd", ptr(l2), K, M, K, ptr(t), ptr(kp), ptr(lse), ptr(out), ptr(ws),
+             stream_ptr())
+        ctx.save_for_backward(l2, t, kp, lse, out)
+        ctx.shape = logits.shape
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        l2, t, kp, lse, stats = ctx.saved_tensors
+        M, K = l2.shape
+        dl = torch.empty_like(l2)
+        g = g.reshape(1).contiguous()
+        call("tvq_masked_ce_bwd", ptr(l2), K, M, K, ptr(t), ptr(kp), ptr(lse), ptr(stats), ptr(g),
+             ptr(dl), K, stream_ptr())
+        return dl.reshape(ctx.shape), None, None
+
+
+def masked_cross_entropy(logits, target, keep):
+    """F.cross_entropy(logits[~keep], target[~keep]) (maskgit.py:183-191)."""
+    return _MaskedCE.apply(logits, target, keep)
+
+
+def mask_tokens(s, mask_id, site, ratio=None, rand=None):
+    """_randomly_mask_tokens on device; returns (s_M int64, keep bool)."""
+    s = s.contiguous()
+    B, n = s.shape
+    s_M = torch.empty_like(s)
+    keep = torch.empty((B, n), device=s.device, dtype=torch.bool)
+    seed = rng.seed_tensor(s.device)
+    call("tvq_mask_tokens", ptr(s), B, n, int(mask_id), ptr(seed), rng.call_offset(site),
+         ptr(ratio.contiguous() if ratio is not None else None),
+         ptr(rand.contiguous() if rand is not None else None), ptr(s_M), ptr(keep), stream_ptr())
+    return s_M, keep
+
+
+# ---------------------------------------------------------------- misc
+class _UpNearest(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, Lout):
+        x = x.contiguous()
+        Lin = x.shape[-1]
+        R = x.numel() // Lin
+        y = torch.empty((*x.shape[:-1], Lout), device=x.device)
+        call("tvq_upsample_nearest", ptr(x), R, Lin, Lout, ptr(y), stream_ptr())
+        ctx.cfg = (x.shape, R, Lin, Lout)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        shape, R, Lin, Lout = ctx.cfg
+        g = gy.contiguous()
+        dx = torch.empty(shape, device=g.device)
+        call("tvq_upsample_nearest_bwd", ptr(g), R, Lin, Lout, ptr(dx), stream_ptr())
+        return dx, None
+
+
+def upsample_nearest(x, size):
+    return _UpNearest.apply(x, int(size))
+
+
+class _GELU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        call("tvq_gelu_fwd", ptr(x), x.numel(), ptr(y), stream_ptr())
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        g = gy.contiguous()
+        dx = torch.empty_like(x)
+        call("tvq_gelu_bwd", ptr(g), ptr(x), x.numel(), ptr(dx), stream_ptr())
+        return dx
+
+
+def gelu(x):
+    return _GELU.apply(x)

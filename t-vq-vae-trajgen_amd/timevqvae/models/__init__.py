@@ -1,4 +1,6 @@
 from .vq import VectorQuantize
 from .vq_vae import VQVAEDecoder, VQVAEEncoder
+from .bidirectional_transformer import BidirectionalTransformer
+from .maskgit import MaskGIT
 
-__all__ = ["VectorQuantize", "VQVAEEncoder", "VQVAEDecoder"]
+__all__ = ["VectorQuantize", "VQVAEEncoder", "VQVAEDecoder", "BidirectionalTransformer", "MaskGIT"]

@@ -1,0 +1,315 @@
+"""MaskGIT prior — same API as the reference timevqvae/models/bidirectional_transformer.py.
+
+The reference builds its encoder from the third-party x-transformers package
+(ContinuousTransformerWrapper + Encoder, bidirectional_transformer.py:92-110),
+which is absent from this image.  `blocks` below restates that module tree with
+the x-transformers 1.3x attribute names (project_in / post_emb_norm.gamma /
+attn_layers.layers.{i}.{0.0.g | 1.to_q,to_k,to_v,to_out | 1.ff.0.0, 1.ff.2} /
+attn_layers.final_norm.g / project_out) and its pre-norm semantics:
+
+    x = project_in(x); x = post_emb_norm(x)             # LayerNorm, gamma only
+    for (attn, ff) in depth: x = x + attn(RMSNorm(x)); x = x + ff(RMSNorm(x))
+      (each branch skipped with prob layer_dropout in training)
+    x = final RMSNorm(x); x = project_out(x)
+
+attention: q,k,v,out bias-free Linear, head dim 64, softmax(QK^T/8) + dropout;
+FF: Linear(+b) -> GELU -> Dropout -> Linear(+b).  PARITY UNPINNED: no reference
+output exists for this part; project_in/out are bias-free
+as in x-transformers >= 1.2x.
+"""
+import random
+from typing import Union
+
+import torch
+import torch.nn as nn
+
+from ..hip import rng
+from ..hip.conv import conv2d
+from ..hip.linear import _bias_grad_rows, gemm, linear
+from ..hip.norm import bn_snake
+from ..hip.xf import (attention, embedding, gelu, layer_norm, linear_act, rmsnorm,
+                      upsample_nearest)
+from ..hip._native import call, ptr, stream_ptr
+
+
+# ------------------------------------------------------------------ x-transformers tree
+class RMSNorm(nn.Module):
+    def __init__(self, dim):
+        super().__init__()
+        self.scale = dim ** 0.5
+        self.g = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x):
+        return rmsnorm(x, self.g)
+
+
+class LayerNorm(nn.Module):
+    """x-transformers LayerNorm: F.layer_norm without affine, times gamma."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.gamma = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x):
+        return layer_norm(x, self.gamma, None, 1e-5)
+
+
+class Attention(nn.Module):
+    def __init__(self, dim, heads, dim_head=64, dropout=0.0):
+        super().__init__()
+        inner = heads * dim_head
+        self.heads = heads
+        self.to_q = nn.Linear(dim, inner, bias=False)
+        self.to_k = nn.Linear(dim, inner, bias=False)
+        self.to_v = nn.Linear(dim, inner, bias=False)
+        self.to_out = nn.Linear(inner, dim, bias=False)
+        self.dropout = dropout
+        self._site = rng.new_site()
+
+    def forward(self, x, residual):
+        q = linear(x, self.to_q.weight)
+        k = linear(x, self.to_k.weight)
+        v = linear(x, self.to_v.weight)
+        o = attention(q, k, v, self.heads, self.dropout if self.training else 0.0, self._site)
+        return linear(o, self.to_out.weight, None, residual=residual)
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim, mult=1, dropout=0.0):
+        super().__init__()
+        inner = int(dim * mult)
+        self.ff = nn.Sequential(nn.Sequential(nn.Linear(dim, inner), nn.GELU()), nn.Dropout(dropout),
+                                nn.Linear(inner, dim))
+        self._site = rng.new_site()
+
+    def forward(self, x, residual):
+        lin1 = self.ff[0][0]
+        h = linear_act(x, lin1.weight, lin1.bias, gelu=True)
+        p = self.ff[1].p if self.training else 0.0
+        if p > 0:
+            h = dropout(h, p, self._site)
+        lin2 = self.ff[2]
+        return linear(h, lin2.weight, lin2.bias, residual=residual)
+
+
+class Residual(nn.Module):
+    def forward(self, x, residual):
+        return x + residual
+
+
+class Encoder(nn.Module):
+    """x-transformers Encoder(pre_norm=True, ...) restated."""
+
+    def __init__(self, dim, depth, heads, attn_dim_head=64, use_rmsnorm=True, ff_mult=1,
+                 layer_dropout=0.0, attn_dropout=0.0, ff_dropout=0.0):
+        super().__init__()
+        self.dim = dim
+        norm = (lambda: RMSNorm(dim)) if use_rmsnorm else (lambda: LayerNorm(dim))
+        self.layers = nn.ModuleList()
+        self.layer_types = ("a", "f") * depth
+        for t in self.layer_types:
+            block = (Attention(dim, heads, attn_dim_head, attn_dropout) if t == "a"
+                     else FeedForward(dim, ff_mult, ff_dropout))
+            self.layers.append(nn.ModuleList([nn.ModuleList([norm(), None, None]), block, Residual()]))
+        self.layer_dropout = layer_dropout
+        self.final_norm = norm()
+
+    def forward(self, x):
+        for norms, block, _ in self.layers:
+            if self.training and self.layer_dropout > 0.0 and random.random() < self.layer_dropout:
+                continue
+            x = block(norms[0](x), residual=x)
+        return self.final_norm(x)
+
+
+class ContinuousTransformerWrapper(nn.Module):
+    def __init__(self, dim_in, dim_out, max_seq_len, attn_layers, use_abs_pos_emb=False,
+                 post_emb_norm=True):
+        super().__init__()
+        if use_abs_pos_emb:
+            raise NotImplementedError("abs pos emb is off on the path (use_abs_pos_emb=False)")
+        dim = attn_layers.dim
+        self.max_seq_len = max_seq_len
+        self.post_emb_norm = LayerNorm(dim) if post_emb_norm else nn.Identity()
+        self.attn_layers = attn_layers
+        self.project_in = nn.Linear(dim_in, dim, bias=False)
+        self.project_out = nn.Linear(dim, dim_out, bias=False)
+
+    def forward(self, x):
+        x = linear(x, self.project_in.weight)
+        x = self.post_emb_norm(x)
+        x = self.attn_layers(x)
+        return linear(x, self.project_out.weight)
+
+
+# ------------------------------------------------------------------ helper ops
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, site):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        seed = rng.seed_tensor(x.device)
+        off = rng.call_offset(site)
+        call("tvq_dropout_bwd", ptr(x), x.numel(), float(p), ptr(seed), off, ptr(y), stream_ptr())
+        ctx.cfg = (p, off)
+        ctx.seed = seed
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        p, off = ctx.cfg
+        g = g.contiguous()
+        dx = torch.empty_like(g)
+        call("tvq_dropout_bwd", ptr(g), g.numel(), float(p), ptr(ctx.seed), off, ptr(dx), stream_ptr())
+        return dx, None, None
+
+
+def dropout(x, p, site):
+    return _Dropout.apply(x, float(p), int(site))
+
+
+class _TiedLogits(torch.autograd.Function):
+    """logits = embed @ W[:K]^T + bias[:, :K]  (bidirectional_transformer.py:186-191; the
+    mask-token column K is never computed since it is dropped)."""
+
+    @staticmethod
+    def forward(ctx, h, W, bias, K):
+        B, n, D = h.shape
+        h2 = h.reshape(B * n, D).contiguous()
+        M = B * n
+        out = gemm(h2, D, 1, W, 1, D, M, K, D, R=bias, ldr=bias.shape[1], rmod=n)
+        ctx.save_for_backward(h2, W)
+        ctx.cfg = (B, n, D, K, tuple(bias.shape))
+        return out.reshape(B, n, K)
+
+    @staticmethod
+    def backward(ctx, g):
+        h2, W = ctx.saved_tensors
+        B, n, D, K, bshape = ctx.cfg
+        M = B * n
+        g2 = g.reshape(M, K).contiguous()
+        dh = dW = dbias = None
+        if ctx.needs_input_grad[0]:
+            dh = gemm(g2, K, 1, W, D, 1, M, D, K).reshape(B, n, D)
+        if ctx.needs_input_grad[1]:
+            dW = torch.zeros_like(W)
+            gemm(g2, 1, K, h2, D, 1, K, D, M, out=dW, ldc=D)
+        if ctx.needs_input_grad[2]:
+            dbias = torch.zeros(bshape, device=g.device)
+            s = _bias_grad_rows(g2.reshape(B, n * K))  # sum over the batch
+            dbias[:, :K] = s.reshape(n, K)
+        return dh, dW, dbias, None
+
+
+class Upscale(nn.Module):
+    """bidirectional_transformer.py:12-30: nearest x(m/n) -> Conv1d(k3) -> GELU -> BN1d -> Conv1d(k3)."""
+
+    def __init__(self, in_channels: int, out_channels: int, h_dim: int) -> None:
+        super().__init__()
+        self.conv = nn.Sequential(
+            nn.Conv1d(in_channels, h_dim, kernel_size=3, stride=1, padding=1),
+            nn.GELU(),
+            nn.BatchNorm1d(h_dim),
+            nn.Conv1d(h_dim, out_channels, kernel_size=3, stride=1, padding=1),
+        )
+
+    def forward(self, x, upscale_size: int):
+        """x: (b n d) -> (b m d)."""
+        x = x.transpose(1, 2).contiguous()               # b d n
+        x = upsample_nearest(x, upscale_size)            # b d m
+        c = self.conv
+        x = gelu(conv2d(x, c[0].weight, c[0].bias))
+        x = bn_snake(x, c[2], None)
+        x = conv2d(x, c[3].weight, c[3].bias)
+        return x.transpose(1, 2)                         # b m d
+
+
+# ------------------------------------------------------------------ the prior
+class BidirectionalTransformer(nn.Module):
+    def __init__(self, kind: str, num_tokens: int, codebook_sizes: dict, embed_dim: int,
+                 hidden_dim: int, n_layers: int, heads: int, ff_mult: int, use_rmsnorm: bool,
+                 p_unconditional: float, n_classes: int, model_dropout: float = 0.3,
+                 emb_dropout: float = 0.3, **kwargs):
+        super().__init__()
+        kind = kind.lower()
+        assert kind in ["lf", "hf"], "invalid `kind`."
+        self.kind = kind
+        self.num_tokens = num_tokens
+        self.n_classes = n_classes
+        self.p_unconditional = p_unconditional
+        in_dim = embed_dim if kind == "lf" else 2 * embed_dim
+        out_dim = embed_dim
+        self.emb_dropout = emb_dropout
+        self.mask_token_ind = {"lf": codebook_sizes["lf"], "hf": codebook_sizes["hf"]}
+        self.tok_emb_l = nn.Embedding(codebook_sizes["lf"] + 1, embed_dim)
+        if kind == "hf":
+            self.tok_emb_h = nn.Embedding(codebook_sizes["hf"] + 1, embed_dim)
+        self.pos_emb = nn.Embedding(self.num_tokens + 1, in_dim)
+        self.class_condition_emb = nn.Embedding(n_classes + 1, in_dim)
+        self.blocks = ContinuousTransformerWrapper(
+            dim_in=in_dim, dim_out=in_dim, max_seq_len=self.num_tokens + 1, use_abs_pos_emb=False,
+            post_emb_norm=True,
+            attn_layers=Encoder(dim=hidden_dim, depth=n_layers, heads=heads, attn_dim_head=64,
+                                use_rmsnorm=use_rmsnorm, ff_mult=ff_mult,
+                                layer_dropout=model_dropout, attn_dropout=model_dropout,
+                                ff_dropout=model_dropout))
+        self.pred_head = nn.Sequential(nn.Linear(in_features=in_dim, out_features=out_dim),
+                                       nn.GELU(), nn.LayerNorm(out_dim, eps=1e-12))
+        codebook_size = codebook_sizes["lf"] if kind == "lf" else codebook_sizes["hf"]
+        self.codebook_size = codebook_size
+        self.bias = nn.Parameter(torch.zeros(self.num_tokens, codebook_size + 1))
+        if kind == "hf":
+            self.projector = Upscale(embed_dim, embed_dim, 2 * embed_dim)
+        self._site_l = rng.new_site()
+        self._site_h = rng.new_site()
+
+    def class_embedding(self, class_condition: Union[None, torch.Tensor], batch_size: int, device):
+        """bidirectional_transformer.py:124-150."""
+        if class_condition is None:
+            idx = torch.full((batch_size, 1), self.n_classes, dtype=torch.long, device=device)
+        else:
+            if self.training:
+                ind = torch.rand(class_condition.shape, device=device) > self.p_unconditional
+            else:
+                ind = torch.ones_like(class_condition, dtype=torch.bool)
+            idx = torch.where(ind, class_condition.long(), self.n_classes)
+        return embedding(idx, self.class_condition_emb.weight)  # (b 1 dim)
+
+    def _tok(self, s, table, kind, site):
+        p = self.emb_dropout if self.training else 0.0
+        return embedding(s, table, self.mask_token_ind[kind], p, site)
+
+    def _head(self, x):
+        lin, ln = self.pred_head[0], self.pred_head[2]
+        h = linear_act(x, lin.weight, lin.bias, gelu=True)
+        return layer_norm(h, ln.weight, ln.bias, ln.eps)
+
+    def forward_lf(self, s_M_l, class_condition: Union[None, torch.Tensor] = None):
+        """bidirectional_transformer.py:166-192."""
+        device = s_M_l.device
+        tok = self._tok(s_M_l, self.tok_emb_l.weight, "lf", self._site_l)
+        cls_emb = self.class_embedding(class_condition, s_M_l.shape[0], device)
+        n = tok.shape[1]
+        embed = torch.cat((cls_emb, tok + self.pos_emb.weight[:n, :]), dim=1)
+        embed = self.blocks(embed)
+        embed = self._head(embed[:, 1:, :])
+        return _TiedLogits.apply(embed, self.tok_emb_l.weight, self.bias, self.codebook_size)
+
+    def forward_hf(self, s_M_l, s_M_h, class_condition=None):
+        """bidirectional_transformer.py:194-236."""
+        device = s_M_l.device
+        tl = self._tok(s_M_l, self.tok_emb_l.weight, "lf", self._site_l)
+        th = self._tok(s_M_h, self.tok_emb_h.weight, "hf", self._site_h)
+        tl = self.projector(tl, upscale_size=th.shape[1])
+        tok = torch.cat((tl, th), dim=-1)
+        cls_emb = self.class_embedding(class_condition, s_M_l.shape[0], device)
+        n = tok.shape[1]
+        embed = torch.cat((cls_emb, tok + self.pos_emb.weight[:n, :]), dim=1)
+        embed = self.blocks(embed)
+        embed = self._head(embed[:, 1:, :])
+        return _TiedLogits.apply(embed, self.tok_emb_h.weight, self.bias, self.codebook_size)
+
+    def forward(self, s_M_l, s_M_h=None, class_condition: Union[None, torch.Tensor] = None):
+        if self.kind == "lf":
+            return self.forward_lf(s_M_l, class_condition)
+        return self.forward_hf(s_M_l, s_M_h, class_condition)

@@ -1,0 +1,170 @@
+"""MaskGIT (stage2) — same API as the reference timevqvae/models/maskgit.py.
+
+Training forward (maskgit.py:155-192): frozen stage1 encoders in eval mode (one
+fused STFT pass for both branches, eval BN+Snake, VQ assign), on-device random
+masking (_randomly_mask_tokens, no host loop), the two bidirectional
+transformers, and a fused masked cross-entropy.  Iterative decoding
+(maskgit.py:294-446) runs one fused HIP sampling kernel per step with no host
+synchronisation (the reference's per-row Python loop and .item() are gone).
+"""
+from typing import Callable, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ..hip import rng
+from ..hip.signal import stft_encode
+from ..hip.xf import mask_tokens, masked_cross_entropy
+from ..utils import freeze, quantize, zero_pad_high_freq, zero_pad_low_freq
+from .bidirectional_transformer import BidirectionalTransformer
+from .vq import VectorQuantize
+from .vq_vae import VQVAEEncoder
+
+
+def _latent_width(T: int, n_enc_blocks: int) -> int:
+    W = T + 1
+    for _ in range(n_enc_blocks):
+        W = (W + 2 - 4) // 2 + 1
+    return W
+
+
+class MaskGIT(nn.Module):
+    """ref: maskgit.py:20-477 (ESS / self-token-critic paths are disabled by config)."""
+
+    def __init__(self, stage1_ckpt_fname: str, input_length: int, in_channels: int, config: dict,
+                 n_classes: int, choice_temperatures: dict, T: dict, **kwargs):
+        super().__init__()
+        self.choice_temperature_l = choice_temperatures["lf"]
+        self.choice_temperature_h = choice_temperatures["hf"]
+        self.T = T
+        self.config = config
+        self.n_classes = n_classes
+        self.n_fft = config["VQ-VAE"]["n_fft"]
+        self.cfg_scale = config["MaskGIT"]["cfg_scale"]
+        self.mask_token_ids = {"lf": config["VQ-VAE"]["codebook_sizes"]["lf"],
+                               "hf": config["VQ-VAE"]["codebook_sizes"]["hf"]}
+        self.gamma = self.gamma_func("cosine")
+        from ..trainers.stage1 import Stage1  # circular import, as in the reference
+        stage1 = kwargs.get("stage1")
+        if stage1 is None:
+            stage1 = Stage1.load_from_checkpoint(stage1_ckpt_fname, input_length=input_length,
+                                                 in_channels=in_channels, config=config,
+                                                 map_location="cpu")
+        self.stage1 = stage1
+        freeze(self.stage1)
+        self.stage1.eval()
+        self.encoder_l = self.stage1.encoder_l
+        self.decoder_l = self.stage1.decoder_l
+        self.vq_model_l = self.stage1.vq_model_l
+        self.encoder_h = self.stage1.encoder_h
+        self.decoder_h = self.stage1.decoder_h
+        self.vq_model_h = self.stage1.vq_model_h
+        for enc in (self.encoder_l, self.encoder_h):
+            if int(enc.num_tokens) == 0:  # never run: derive H', W' from the conv plan
+                n_enc = sum(1 for m in enc.encoder if type(m).__name__ == "VQVAEEncBlock")
+                enc.H_prime = torch.tensor(3)
+                enc.W_prime = torch.tensor(_latent_width(input_length, n_enc))
+                enc.num_tokens = enc.H_prime * enc.W_prime
+        self.num_tokens_l = int(self.encoder_l.num_tokens)
+        self.num_tokens_h = int(self.encoder_h.num_tokens)
+        self.H_prime_l, self.H_prime_h = int(self.encoder_l.H_prime), int(self.encoder_h.H_prime)
+        self.W_prime_l, self.W_prime_h = int(self.encoder_l.W_prime), int(self.encoder_h.W_prime)
+        emb_dim = self.config["encoder"]["hid_dim"]
+        self.transformer_l = BidirectionalTransformer(
+            "lf", self.num_tokens_l, config["VQ-VAE"]["codebook_sizes"], emb_dim,
+            **config["MaskGIT"]["prior_model_l"], n_classes=n_classes)
+        self.transformer_h = BidirectionalTransformer(
+            "hf", self.num_tokens_h, config["VQ-VAE"]["codebook_sizes"], emb_dim,
+            **config["MaskGIT"]["prior_model_h"], n_classes=n_classes,
+            num_tokens_l=self.num_tokens_l)
+        self._site_mask_l = rng.new_site()
+        self._site_mask_h = rng.new_site()
+        self._site_sample = rng.new_site()
+
+    def train(self, mode: bool = True):
+        super().train(mode)
+        self.stage1.eval()  # stage1 stays frozen in eval mode (maskgit.py:61-62,161-164)
+        return self
+
+    @torch.no_grad()
+    def encode_to_z_q(self, x, encoder: VQVAEEncoder, vq_model: VectorQuantize,
+                      svq_temp: Union[float, None] = None):
+        """maskgit.py:117-134."""
+        z = encoder(x)
+        zq, s, _, _ = quantize(z, vq_model, svq_temp=svq_temp)
+        return zq, s
+
+    @torch.no_grad()
+    def encode_tokens(self, x):
+        """Both branches from one fused STFT pass: (s_l (b n), s_h (b m)) int64."""
+        st = stft_encode(x, enc_l=True, enc_h=True)
+        _, s_l, _, _ = quantize(self.encoder_l.encode_timefreq(st["enc_l"]), self.vq_model_l)
+        _, s_h, _, _ = quantize(self.encoder_h.encode_timefreq(st["enc_h"]), self.vq_model_h)
+        return s_l, s_h
+
+    def masked_prediction(self, transformer, class_condition, *s_in):
+        """maskgit.py:136-153 (classifier-free guidance)."""
+        if class_condition is None:
+            return transformer(*s_in, class_condition=None)
+        if self.cfg_scale == 1.0:
+            return transformer(*s_in, class_condition=class_condition)
+        logits_null = transformer(*s_in, class_condition=None)
+        logits = transformer(*s_in, class_condition=class_condition)
+        return logits_null + self.cfg_scale * (logits - logits_null)
+
+    def forward(self, x, y):
+        """maskgit.py:155-192 -> (loss, (loss_l, loss_h))."""
+        self.encoder_l.eval()
+        self.vq_model_l.eval()
+        self.encoder_h.eval()
+        self.vq_model_h.eval()
+        s_l, s_h = self.encode_tokens(x)
+        s_l_M, keep_l = self._randomly_mask_tokens(s_l, self.mask_token_ids["lf"], x.device)
+        s_h_M, keep_h = self._randomly_mask_tokens(s_h, self.mask_token_ids["hf"], x.device)
+        logits_l = self.masked_prediction(self.transformer_l, y, s_l_M)
+        logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
+        mask_pred_loss_l = masked_cross_entropy(logits_l, s_l, keep_l)
+        mask_pred_loss_h = masked_cross_entropy(logits_h, s_h, keep_h)
+        return mask_pred_loss_l + mask_pred_loss_h, (mask_pred_loss_l, mask_pred_loss_h)
+
+    def _randomly_mask_tokens(self, s, mask_token_id, device):
+        """maskgit.py:194-216 on device; returns (s_M, mask) with mask=True for kept tokens."""
+        site = self._site_mask_l if s.shape[1] == self.num_tokens_l else self._site_mask_h
+        return mask_tokens(s, mask_token_id, site)
+
+    def gamma_func(self, mode="cosine"):
+        """maskgit.py:218-228."""
+        if mode == "linear":
+            return lambda r: 1 - r
+        if mode == "cosine":
+            return lambda r: np.cos(r * np.pi / 2)
+        if mode == "square":
+            return lambda r: 1 - r ** 2
+        if mode == "cubic":
+            return lambda r: 1 - r ** 3
+        raise NotImplementedError
+
+    def create_input_tokens_normal(self, num, num_tokens, mask_token_ids, device):
+        """maskgit.py:230-236."""
+        return torch.full((num, num_tokens), mask_token_ids, dtype=torch.int64, device=device)
+
+    def decode_token_ind_to_timeseries(self, s: torch.Tensor, frequency: str,
+                                       return_representations: bool = False):
+        """maskgit.py:448-477."""
+        from ..hip.xf import embedding
+        frequency = frequency.lower()
+        assert frequency in ["lf", "hf"]
+        vq_model = self.vq_model_l if frequency == "lf" else self.vq_model_h
+        decoder = self.decoder_l if frequency == "lf" else self.decoder_h
+        H_prime = self.H_prime_l if frequency == "lf" else self.H_prime_h
+        W_prime = self.W_prime_l if frequency == "lf" else self.W_prime_h
+        with torch.no_grad():
+            zq = embedding(s, vq_model._codebook.embed)           # (b n d)
+            zq = vq_model.project_out(zq)
+            b, n, c = zq.shape
+            zq = zq.transpose(1, 2).reshape(b, c, H_prime, W_prime)
+            xhat = decoder(zq)
+        if return_representations:
+            return xhat, zq
+        return xhat

@@ -1,3 +1,4 @@
 from .stage1 import Stage1
+from .stage2 import Stage2
 
-__all__ = ["Stage1"]
+__all__ = ["Stage1", "Stage2"]

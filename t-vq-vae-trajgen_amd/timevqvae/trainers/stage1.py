@@ -100,6 +100,19 @@ class Stage1(nn.Module):
                 "recons_loss.HF.time": recons_loss["HF.time"],
                 "perplexity.LF": perplexities["LF"], "perplexity.HF": perplexities["HF"]}
 
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path, map_location="cpu", input_length=None,
+                             in_channels=None, config=None, **kwargs):
+        """Lightning-style loader: {'state_dict': ...} or a bare state_dict (weights only)."""
+        ckpt = torch.load(checkpoint_path, map_location=map_location, weights_only=True)
+        sd = ckpt.get("state_dict", ckpt) if isinstance(ckpt, dict) else ckpt
+        model = cls(input_length, in_channels, config)
+        model.load_state_dict(sd)
+        return model
+
+    def save_checkpoint(self, path):
+        torch.save({"state_dict": self.state_dict()}, path)
+
     def configure_optimizers(self):
         """stage1.py:229-236: AdamW(lr) + linear warmup / cosine annealing."""
         opt = FusedAdamW(self.parameters(), lr=self.config["exp_params"]["lr"])

@@ -1,0 +1,46 @@
+"""Stage2 (MaskGIT prior) trainer — the reference trainers/stage2.py contract without
+Lightning.  The validation-time sampling metrics (FID/IS via ROCKET, stage2.py:70-110)
+are evaluation, out of the hot-path scope; X_train/X_test/fcn args are accepted."""
+import torch
+import torch.nn as nn
+
+from ..hip.optim import FusedAdamW
+from ..models.maskgit import MaskGIT
+from ..utils import linear_warmup_cosine_annealingLR
+
+
+class Stage2(nn.Module):
+    def __init__(self, stage1_ckpt_fname: str, fcn_ckpt_fname: str, input_length: int,
+                 in_channels: int, n_classes: int, X_train=None, X_test=None, config: dict = None,
+                 device=None, feature_extractor_type: str = "supervised_fcn", **kwargs):
+        super().__init__()
+        self.config = config
+        self.maskgit = MaskGIT(stage1_ckpt_fname=stage1_ckpt_fname, input_length=input_length,
+                               in_channels=in_channels, config=config, n_classes=n_classes,
+                               **config["MaskGIT"], **kwargs)
+        self._sched = None
+        self._opt = None
+
+    def training_step(self, batch, batch_idx):
+        """stage2.py:49-68."""
+        x, y = batch
+        mask_pred_loss, (loss_l, loss_h) = self.maskgit(x, y)
+        if self._sched is not None:
+            self._sched.step()
+        return {"loss": mask_pred_loss, "mask_pred_loss": mask_pred_loss,
+                "mask_pred_loss_l": loss_l, "mask_pred_loss_h": loss_h}
+
+    @torch.no_grad()
+    def validation_step(self, batch, batch_idx):
+        self.eval()
+        x, y = batch
+        mask_pred_loss, (loss_l, loss_h) = self.maskgit(x, y)
+        return {"loss": mask_pred_loss, "mask_pred_loss_l": loss_l, "mask_pred_loss_h": loss_h}
+
+    def configure_optimizers(self):
+        """stage2.py:112-119 (frozen stage1 parameters carry no grad and are skipped)."""
+        opt = FusedAdamW(self.parameters(), lr=self.config["exp_params"]["lr"])
+        sch = linear_warmup_cosine_annealingLR(opt, self.config["trainer_params"]["max_steps"]["stage2"],
+                                               self.config["exp_params"]["linear_warmup_rate"])
+        self._opt, self._sched = opt, sch
+        return {"optimizer": opt, "lr_scheduler": sch}
