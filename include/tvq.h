@@ -59,13 +59,15 @@ int tvq_vq_assign(const float* x, int64_t B, int64_t N, int64_t D, int64_t sB, i
                   float* quant, int64_t* idx, int32_t* idx32, float* commit_partial,
                   tvq_stream_t stream);
 
-/* Per-code batch statistics, deterministic (no float atomics): counts[k] (int32),
- * cs_batch[k] = counts (float) = onehot.sum(0) (vq.py:228) and, if es_batch is
- * non-NULL, es_batch[k,:] = sum of rows assigned to k = (x^T onehot)^T (vq.py:233),
- * summed in row order.  es_batch: (K,D) row-major. */
+/* Per-code batch statistics, deterministic (no float atomics): a stable group-by
+ * (counting sort) of idx32, then per-code row sums in row order.
+ * counts[k] (int32), cs_batch[k] = counts (float) = onehot.sum(0) (vq.py:228) and, if
+ * es_batch is non-NULL, es_batch[k,:] = (x^T onehot)^T (vq.py:233), (K,D) row-major.
+ * workspace: tvq_vq_stats_workspace(M, K) int32s. */
+int64_t tvq_vq_stats_workspace(int64_t M, int64_t K);
 int tvq_vq_stats(const float* x, int64_t B, int64_t N, int64_t D, int64_t sB, int64_t sN,
                  int64_t sD, const int32_t* idx32, int64_t K, int32_t* counts, float* cs_batch,
-                 float* es_batch, tvq_stream_t stream);
+                 float* es_batch, int32_t* workspace, tvq_stream_t stream);
 
 /* EMA blend in place (vq.py:231,236 ema_inplace):
  *   cluster_size = cluster_size*decay + cs_batch*(1-decay)
@@ -139,9 +141,11 @@ int tvq_convT2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t
                       int64_t Wi, tvq_stream_t stream);
 int64_t tvq_conv_wgrad_workspace(int64_t N, int64_t C, int64_t KH, int64_t KW, int64_t B,
                                  int64_t Hout, int64_t Wo);
+/* weight gradient (+ the bias gradient sum dY into db when non-NULL, as an extra
+ * ones-column of the same GEMM); splits over positions reduced in a fixed order */
 int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
                      const float* dy, int64_t Co, int64_t Wo, int64_t KH, int64_t KW, int64_t SW,
-                     int64_t replicate, float* dw, int64_t accumulate, float* workspace,
+                     int64_t replicate, float* dw, float* db, int64_t accumulate, float* workspace,
                      tvq_stream_t stream);
 int tvq_convT2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
                       const float* dy, int64_t Co, int64_t Wo, int64_t KH, int64_t KW, int64_t SW,
@@ -181,6 +185,12 @@ int tvq_snake_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t
 int tvq_dropout_bwd(const float* dy, int64_t n, float p, const int64_t* seed_ptr,
                     uint64_t offset, float* dx, tvq_stream_t stream);
 
+/* deterministic column sums of a P x N slab: out[j] (+)= sum_p in[p*ld + j]
+ * (workspace: tvq_reduce_rows_workspace floats, may be 0). */
+int64_t tvq_reduce_rows_workspace(int64_t P, int64_t N);
+int tvq_reduce_rows(const float* in, int64_t P, int64_t N, int64_t ld, float* out,
+                    int64_t accumulate, float* workspace, tvq_stream_t stream);
+
 /* ------------------------------------------------------------- dense GEMM
  * nn.Linear and friends: C[m,n] = epi(alpha * sum_k A(m,k) B(k,n)),
  * A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn]; epi: + bias[n]
@@ -215,7 +225,7 @@ int tvq_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_
  * (bidirectional_transformer.py:92-110; restated):
  * RMSNorm F.normalize(x)*sqrt(D)*g; LayerNorm (post_emb_norm gamma-only, pred_head
  * affine eps 1e-12, bidirectional_transformer.py:115); attention softmax(QK^T*scale)
- * with dropout, head_dim 64, seq <= 128, Q/K/V/O in the Linear layout
+ * with dropout, head_dim 64, seq <= 104 (path: 25 / 97), Q/K/V/O in the Linear layout
  * [(b*S+s)*ld + h*64 + d]; lse: [B*H*S] saved for the backward. */
 int tvq_rmsnorm_fwd(const float* x, int64_t M, int64_t D, const float* g, float scale, float* y,
                     float* inv_norm, tvq_stream_t stream);
@@ -244,9 +254,11 @@ int tvq_attention_bwd(const float* q, int64_t ldq, const float* k, int64_t ldk, 
 int tvq_embedding_fwd(const int64_t* idx, int64_t M, int64_t D, const float* table, float* out,
                       int64_t ldo, int64_t mask_id, float drop_p, const int64_t* seed_ptr,
                       uint64_t offset, tvq_stream_t stream);
+int64_t tvq_embedding_bwd_workspace(int64_t M, int64_t V);
 int tvq_embedding_bwd(const int64_t* idx, int64_t M, int64_t D, const float* g, int64_t ldg,
                       int64_t V, float* tgrad, int64_t accumulate, int64_t mask_id, float drop_p,
-                      const int64_t* seed_ptr, uint64_t offset, tvq_stream_t stream);
+                      const int64_t* seed_ptr, uint64_t offset, int32_t* workspace,
+                      tvq_stream_t stream);
 /* F.cross_entropy(logits[~keep], s[~keep]) (maskgit.py:183-191); out = {loss, count}. */
 int64_t tvq_masked_ce_workspace(int64_t M);
 int tvq_masked_ce_fwd(const float* logits, int64_t ldl, int64_t M, int64_t K,

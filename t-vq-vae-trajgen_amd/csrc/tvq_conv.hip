@@ -19,6 +19,7 @@
 // Tiles are staged global -> registers -> LDS with the next K-step's loads in
 // flight during the current step's MFMAs.
 #include "tvq_common.h"
+#include "tvq_reduce.h"
 
 namespace tvq {
 
@@ -222,7 +223,8 @@ template <int KH, int KW, int SW, bool REPL, int TN, int TK, int WN, int WK>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict__ G,
                                                         const float* __restrict__ in,
                                                         float* __restrict__ slab, ConvGeom g,
-                                                        int pos_per_split) {
+                                                        int pos_per_split, int kcols) {
+  // kcols = Kred (+1: a column of ones whose result is the bias gradient sum_m G[n, m])
   constexpr int BK = 16;  // positions per K-step
   constexpr int KK = KH * KW;
   constexpr int FN = TN / WN / 16;
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
 #pragma unroll
     for (int j = 0; j < B_PER; ++j) {
       const int kp = kp0 + b_kbase + j * 16;
-      float v = 0.f;
+      float v = (pv && kp == g.Kred && kp < kcols) ? 1.0f : 0.f;
       if (pv && kp < g.Kred) {
         const int c = kp / KK, r = kp - c * KK;
         const int kh = r / KW, kw = r - kh * KW;
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
       }
     }
   }
-  float* sl = slab + (int64_t)blockIdx.z * g.N * g.Kred;
+  float* sl = slab + (int64_t)blockIdx.z * g.N * kcols;
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -327,24 +329,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + (wn * FN + i) * 16 + 4 * g4 + r;
         const int kp = kp0 + (wk * FK + j) * 16 + r16;
-        if (n < g.N && kp < g.Kred) sl[(int64_t)n * g.Kred + kp] = acc[i][j][r];
+        if (n < g.N && kp < kcols) sl[(int64_t)n * kcols + kp] = acc[i][j][r];
       }
-}
-
-// dW[n*wsn + c*wsc + r] = sum_z slab[z][n][k'] (+ accumulate into existing dW)
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int N, int Kred,
-                                    int KK, int64_t wsn, int64_t wsc, float* __restrict__ dw,
-                                    int accumulate) {
-  const int64_t tot = (int64_t)N * Kred;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += slab[(int64_t)z * tot + i];
-    const int n = (int)(i / Kred), kp = (int)(i - (int64_t)n * Kred);
-    const int c = kp / KK, r = kp - c * KK;
-    float* d = dw + n * wsn + c * wsc + r;
-    *d = accumulate ? *d + s : s;
-  }
 }
 
 // Fold the gradient of a replicate-padded input (B,C,H+2PH,W+2PW) onto (B,C,H,W).
@@ -429,15 +415,15 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
 
 template <int KH, int KW, int SW, bool REPL>
 static void launch_wgrad(const float* G, const float* in, float* slab, int splits, int pps,
-                         const ConvGeom& g, hipStream_t st) {
+                         const ConvGeom& g, int kcols, hipStream_t st) {
   if (g.N <= 16) {
-    dim3 grid((g.Kred + 63) / 64, (g.N + 15) / 16, splits);
+    dim3 grid((kcols + 63) / 64, (g.N + 15) / 16, splits);
     hipLaunchKernelGGL((conv_wgrad_kernel<KH, KW, SW, REPL, 16, 64, 1, 4>), grid, dim3(256), 0, st,
-                       G, in, slab, g, pps);
+                       G, in, slab, g, pps, kcols);
   } else {
-    dim3 grid((g.Kred + 63) / 64, (g.N + 63) / 64, splits);
+    dim3 grid((kcols + 63) / 64, (g.N + 63) / 64, splits);
     hipLaunchKernelGGL((conv_wgrad_kernel<KH, KW, SW, REPL, 64, 64, 2, 2>), grid, dim3(256), 0, st,
-                       G, in, slab, g, pps);
+                       G, in, slab, g, pps, kcols);
   }
 }
 
@@ -460,9 +446,9 @@ static int kind_of(int KH, int KW, int SW) {
 }
 
 static int wgrad_splits(const ConvGeom& g, int tiles, int* pps) {
-  // aim for ~1024 blocks, each with >= 256 positions
+  // aim for ~1024 blocks, each with >= 512 positions
   int splits = (1024 + tiles - 1) / tiles;
-  const int maxs = (g.Mpos + 255) / 256;
+  const int maxs = (g.Mpos + 511) / 512;
   if (splits > maxs) splits = maxs;
   if (splits < 1) splits = 1;
   if (splits > 256) splits = 256;
@@ -596,16 +582,17 @@ extern "C" int tvq_convT2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t
   return launch_status("tvq_convT2d_dgrad");
 }
 
-// Weight gradient workspace (floats) for a G of N channels at Mpos positions.
+// Weight gradient workspace (floats): split slabs [splits][N][Kred+1].
 static int64_t wgrad_ws(int64_t N, int64_t Kred, int64_t Mpos, int* splits_out, int* pps_out) {
   ConvGeom g;
   g.Mpos = (int)Mpos;
-  const int tiles = (int)(((Kred + 63) / 64) * ((N + (N <= 16 ? 15 : 63)) / (N <= 16 ? 16 : 64)));
+  const int64_t kc = Kred + 1;
+  const int tiles = (int)(((kc + 63) / 64) * ((N + (N <= 16 ? 15 : 63)) / (N <= 16 ? 16 : 64)));
   int pps;
   const int splits = wgrad_splits(g, tiles, &pps);
   if (splits_out) *splits_out = splits;
   if (pps_out) *pps_out = pps;
-  return (int64_t)splits * N * Kred;
+  return (int64_t)splits * N * kc + reduce_rows_scratch(splits, N * kc);
 }
 
 extern "C" int64_t tvq_conv_wgrad_workspace(int64_t N, int64_t C, int64_t KH, int64_t KW,
@@ -613,11 +600,20 @@ extern "C" int64_t tvq_conv_wgrad_workspace(int64_t N, int64_t C, int64_t KH, in
   return wgrad_ws(N, C * KH * KW, B * Hout * Wo, nullptr, nullptr);
 }
 
-// Conv2d weight gradient: dW[co,ci,kh,kw] (+)= sum dY[b,co,h,wo] X[b,ci,h+kh-PH, wo*SW+kw-PW]
+static void wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, float* dw,
+                         float* db, int accumulate, hipStream_t st) {
+  // deterministic split sum; kcols = Kred+1 splits out the bias column.  The level-1
+  // scratch follows the slab in the workspace.
+  reduce_rows(slab, splits, N * kcols, N * kcols, dw, db, kcols > 0 && db ? kcols : 0, accumulate,
+              slab + (int64_t)splits * N * kcols, st);
+}
+
+// Conv2d weight (+bias) gradient: dW[co,ci,kh,kw] (+)= sum dY[b,co,h,wo] X[b,ci,h+kh-PH, wo*SW+kw-PW],
+// db[co] (+)= sum dY[b,co,h,wo] (db may be NULL)
 extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
                                 const float* dy, int64_t Co, int64_t Wo, int64_t KH, int64_t KW,
-                                int64_t SW, int64_t replicate, float* dw, int64_t accumulate,
-                                float* workspace, tvq_stream_t stream) {
+                                int64_t SW, int64_t replicate, float* dw, float* db,
+                                int64_t accumulate, float* workspace, tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && dy && dw && workspace, "tvq_conv2d_wgrad: bad arguments");
   const int kind = kind_of((int)KH, (int)KW, (int)SW);
   TVQ_CHECK_ARG(kind >= 0, "tvq_conv2d_wgrad: unsupported kernel");
@@ -625,14 +621,12 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
                          (int)KW, PH_OF(KH), PW_OF(KW), Ci * KH * KW, KH * KW);
   int splits, pps;
   wgrad_ws(Co, g.Kred, g.Mpos, &splits, &pps);
+  const int kcols = g.Kred + (db ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
-#define M_(a, b_, c, d) launch_wgrad<a, b_, c, d>(dy, x, workspace, splits, pps, g, st);
+#define M_(a, b_, c, d) launch_wgrad<a, b_, c, d>(dy, x, workspace, splits, pps, g, kcols, st);
   TVQ_DISPATCH_KIND(kind, replicate, M_)
 #undef M_
-  const int64_t tot = Co * g.Kred;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)((tot + 255) / 256)), dim3(256), 0, st,
-                     workspace, splits, (int)Co, g.Kred, (int)(KH * KW), g.wsn, g.wsc, dw,
-                     (int)accumulate);
+  wgrad_finish(workspace, splits, Co, kcols, dw, db, (int)accumulate, st);
   return launch_status("tvq_conv2d_wgrad");
 }
 
@@ -650,17 +644,18 @@ extern "C" int tvq_convT2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t 
   int splits, pps;
   wgrad_ws(Ci, g.Kred, g.Mpos, &splits, &pps);
   hipStream_t st = (hipStream_t)stream;
-#define M_(a, b_, c, d) launch_wgrad<a, b_, c, false>(x, dy, workspace, splits, pps, g, st);
+#define M_(a, b_, c, d) launch_wgrad<a, b_, c, false>(x, dy, workspace, splits, pps, g, g.Kred, st);
   TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
-  const int64_t tot = Ci * g.Kred;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)((tot + 255) / 256)), dim3(256), 0, st,
-                     workspace, splits, (int)Ci, g.Kred, (int)(KH * KW), g.wsn, g.wsc, dw,
-                     (int)accumulate);
+  wgrad_finish(workspace, splits, Ci, g.Kred, dw, nullptr, (int)accumulate, st);
   return launch_status("tvq_convT2d_wgrad");
 }
 
 extern "C" int64_t tvq_channel_sum_workspace(int64_t B, int64_t C, int64_t HW) {
+  if (HW == 1) {
+    const int64_t r = reduce_rows_scratch(B, C);
+    return r > 0 ? r : 1;
+  }
   int64_t chunks = (B * HW + 8191) / 8192;
   if (chunks > 64) chunks = 64;
   if (chunks < 1) chunks = 1;
@@ -671,6 +666,10 @@ extern "C" int64_t tvq_channel_sum_workspace(int64_t B, int64_t C, int64_t HW) {
 extern "C" int tvq_channel_sum(const float* x, int64_t B, int64_t C, int64_t HW, float* out,
                                int64_t accumulate, float* workspace, tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && out && workspace && B > 0 && C > 0 && HW > 0, "tvq_channel_sum: bad args");
+  if (HW == 1) {  // row-major (B, C): coalesced column sums
+    reduce_rows(x, B, C, C, out, nullptr, 0, (int)accumulate, workspace, (hipStream_t)stream);
+    return launch_status("tvq_channel_sum");
+  }
   const int64_t chunks = tvq_channel_sum_workspace(B, C, HW) / C;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(chan_sum_partial_kernel, dim3((int)C, (int)chunks), dim3(256), 0, st, x,

@@ -1,0 +1,271 @@
+// Deterministic reduction primitives shared by the backward kernels.
+//
+// reduce_rows  out[j] (+)= sum_{p<P} in[p*ld + j]   (column sums of a P x N slab):
+//              two levels of 256-thread blocks (64 columns x 4 row groups, fixed
+//              combine order), coalesced along j; replaces one-thread-per-column
+//              loops that were latency bound (split-K / wgrad slabs, LayerNorm and
+//              RMSNorm gamma partials, Linear bias gradients).
+//              Optional split output: rows of length L -> out1 (first L-1 columns,
+//              dense) and out2 (last column): the fused conv weight|bias gradient.
+// group_by     stable counting sort of int indices in [0, V): offsets[V+1] and a
+//              permutation (positions grouped by value in increasing position
+//              order) -> segmented sums in a fixed order with no float atomics
+//              (VQ embed_sum, nn.Embedding backward).
+#include "tvq_common.h"
+#include "tvq_reduce.h"
+
+namespace tvq {
+
+constexpr int RR_COLS = 64, RR_GROUPS = 4, RR_ROWS = 64;
+
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ in, int64_t P,
+                                                          int64_t N, int64_t ld, int rows_per_blk,
+                                                          float* __restrict__ out,
+                                                          float* __restrict__ out2, int64_t L,
+                                                          int accumulate, int direct) {
+  __shared__ float sh[RR_GROUPS][RR_COLS];
+  const int c = threadIdx.x % RR_COLS, g = threadIdx.x / RR_COLS;
+  const int64_t j = (int64_t)blockIdx.x * RR_COLS + c;
+  const int64_t p0 = (int64_t)blockIdx.y * rows_per_blk;
+  const int64_t p1 = min(P, p0 + rows_per_blk);
+  float s = 0.f;
+  if (j < N) {
+#pragma unroll 4
+    for (int64_t p = p0 + g; p < p1; p += RR_GROUPS) s += in[p * ld + j];
+  }
+  sh[g][c] = s;
+  __syncthreads();
+  if (g == 0 && j < N) {
+    const float t = (sh[0][c] + sh[1][c]) + (sh[2][c] + sh[3][c]);
+    if (!direct) {  // level-1 partial
+      out[(int64_t)blockIdx.y * N + j] = t;
+    } else if (L > 0) {  // split output: [rows][L] -> out (L-1 cols) | out2 (last col)
+      const int64_t r = j / L, col = j - r * L;
+      float* d = col < L - 1 ? out + r * (L - 1) + col : out2 + r;
+      if (col < L - 1 || out2) *d = accumulate ? *d + t : t;
+    } else {
+      out[j] = accumulate ? out[j] + t : t;
+    }
+  }
+}
+
+int64_t reduce_rows_scratch(int64_t P, int64_t N) {
+  const int64_t R = (P + RR_ROWS - 1) / RR_ROWS;
+  return R > 1 ? R * N : 0;
+}
+
+void reduce_rows(const float* in, int64_t P, int64_t N, int64_t ld, float* out, float* out2,
+                 int64_t L, int accumulate, float* scratch, hipStream_t st) {
+  const unsigned gx = (unsigned)((N + RR_COLS - 1) / RR_COLS);
+  const int64_t R = (P + RR_ROWS - 1) / RR_ROWS;
+  if (R <= 1 || scratch == nullptr) {  // single level (no scratch): one block column per 64 cols
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3(gx, 1), dim3(256), 0, st, in, P, N, ld, (int)P,
+                       out, out2, L, accumulate, 1);
+    return;
+  }
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(gx, (unsigned)R), dim3(256), 0, st, in, P, N, ld,
+                     RR_ROWS, scratch, nullptr, (int64_t)0, 0, 0);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(gx, 1), dim3(256), 0, st, scratch, R, N, N, (int)R,
+                     out, out2, L, accumulate, 1);
+}
+
+// ---------------------------------------------------------------- group-by
+constexpr int GB_CHUNK = 256;
+constexpr int SEG_CH = 32;  // rows per segmented-sum chunk (skewed groups split over waves)
+
+template <typename IT>
+__global__ __launch_bounds__(256) void gb_hist_kernel(const IT* __restrict__ idx, int64_t M, int V,
+                                                      int* __restrict__ hist) {
+  extern __shared__ int h[];
+  for (int v = threadIdx.x; v < V; v += 256) h[v] = 0;
+  __syncthreads();
+  const int64_t m0 = (int64_t)blockIdx.x * GB_CHUNK;
+  for (int64_t m = m0 + threadIdx.x; m < min(M, m0 + GB_CHUNK); m += 256) {
+    const int v = (int)idx[m];
+    if (v >= 0 && v < V) atomicAdd(&h[v], 1);  // integer: exact
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < V; v += 256) hist[(int64_t)blockIdx.x * V + v] = h[v];
+}
+
+// one block: per-value totals over chunks, exclusive scan -> offsets[V+1];
+// chunk_off[chunk][v] = offsets[v] + sum_{c' < chunk} hist[c'][v]
+__global__ __launch_bounds__(1024) void gb_scan_kernel(const int* __restrict__ hist, int chunks,
+                                                       int V, int* __restrict__ chunk_off,
+                                                       int* __restrict__ offsets,
+                                                       int* __restrict__ seg_start) {
+  extern __shared__ int tot[];  // [V]
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    int s = 0;
+#pragma unroll 8
+    for (int c = 0; c < chunks; ++c) {
+      chunk_off[(int64_t)c * V + v] = s;
+      s += hist[(int64_t)c * V + v];
+    }
+    tot[v] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // V <= a few thousand: serial scan is cheap and deterministic
+    int run = 0, segs = 0;
+    for (int v = 0; v < V; ++v) {
+      const int t = tot[v];
+      tot[v] = run;
+      run += t;
+      if (seg_start) {
+        seg_start[v] = segs;
+        segs += (t + SEG_CH - 1) / SEG_CH;
+      }
+    }
+    offsets[V] = run;
+    if (seg_start) seg_start[V] = segs;
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    offsets[v] = tot[v];
+    for (int c = 0; c < chunks; ++c) chunk_off[(int64_t)c * V + v] += tot[v];
+  }
+}
+
+// stable placement: rank of m among equal values earlier in its chunk
+template <typename IT>
+__global__ __launch_bounds__(256) void gb_place_kernel(const IT* __restrict__ idx, int64_t M, int V,
+                                                       const int* __restrict__ chunk_off,
+                                                       int* __restrict__ perm) {
+  __shared__ int vals[GB_CHUNK];
+  const int64_t m0 = (int64_t)blockIdx.x * GB_CHUNK;
+  const int n = (int)min((int64_t)GB_CHUNK, M - m0);
+  for (int i = threadIdx.x; i < n; i += 256) vals[i] = (int)idx[m0 + i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const int v = vals[i];
+    if (v < 0 || v >= V) continue;
+    int r = 0;
+    for (int k = 0; k < i; ++k) r += (vals[k] == v);
+    perm[chunk_off[(int64_t)blockIdx.x * V + v] + r] = (int)(m0 + i);
+  }
+}
+
+int64_t group_by_scratch_ints(int64_t M, int64_t V) {
+  const int64_t chunks = (M + GB_CHUNK - 1) / GB_CHUNK;
+  return 2 * chunks * V + (V + 1);  // hist + chunk_off + seg_start
+}
+
+template <typename IT>
+static void group_by_t(const IT* idx, int64_t M, int64_t V, int* offsets, int* perm, int* scratch,
+                       hipStream_t st) {
+  const int chunks = (int)((M + GB_CHUNK - 1) / GB_CHUNK);
+  int* hist = scratch;
+  int* coff = scratch + (int64_t)chunks * V;
+  int* seg_start = coff + (int64_t)chunks * V;
+  hipLaunchKernelGGL(gb_hist_kernel<IT>, dim3(chunks), dim3(256), V * sizeof(int), st, idx, M,
+                     (int)V, hist);
+  hipLaunchKernelGGL(gb_scan_kernel, dim3(1), dim3(1024), V * sizeof(int), st, hist, chunks, (int)V,
+                     coff, offsets, seg_start);
+  hipLaunchKernelGGL(gb_place_kernel<IT>, dim3(chunks), dim3(256), 0, st, idx, M, (int)V, coff,
+                     perm);
+}
+
+void group_by_i32(const int32_t* idx, int64_t M, int64_t V, int* offsets, int* perm, int* scratch,
+                  hipStream_t st) {
+  group_by_t<int32_t>(idx, M, V, offsets, perm, scratch, st);
+}
+void group_by_i64(const int64_t* idx, int64_t M, int64_t V, int* offsets, int* perm, int* scratch,
+                  hipStream_t st) {
+  group_by_t<int64_t>(idx, M, V, offsets, perm, scratch, st);
+}
+
+// Pass 1: one wave per chunk of <= SEG_CH consecutive sorted rows of ONE value:
+// part[chunk, :] = sum of those rows (fixed order).  Pass 2: one wave per value sums its
+// chunk partials in chunk order.  Skewed groups (the MaskGIT mask token takes most
+// positions) are spread over many waves; results stay bitwise reproducible.
+__device__ __forceinline__ int value_of_chunk(const int* __restrict__ seg_start, int V, int c) {
+  int lo = 0, hi = V - 1;  // largest v with seg_start[v] <= c
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (seg_start[mid] <= c) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void seg_chunk_kernel(SegRows s, const int* __restrict__ offsets,
+                                                        const int* __restrict__ perm,
+                                                        const int* __restrict__ seg_start, int V,
+                                                        int max_chunks, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= max_chunks || c >= seg_start[V]) return;
+  const int v = value_of_chunk(seg_start, V, c);
+  const int r0 = offsets[v] + (c - seg_start[v]) * SEG_CH;
+  const int r1 = min(offsets[v + 1], r0 + SEG_CH);
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  const bool drop = s.drop_p > 0.f && (int64_t)v != s.mask_id;
+  const uint64_t seed = drop ? mix_seed(s.seed_ptr, s.offset) : 0ull;
+  const float sc = drop ? 1.0f / (1.0f - s.drop_p) : 1.0f;
+  for (int r = r0; r < r1; ++r) {
+    const int64_t m = perm[r];
+    const int64_t b = m / s.N, n = m - b * s.N;
+    const float* row = s.src + b * s.sB + n * s.sN;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int d = lane + 64 * i;
+      if (d < s.D) {
+        float x = row[(int64_t)d * s.sD];
+        if (drop) x = uniform01(seed, (uint64_t)(m * s.D + d)) >= s.drop_p ? x * sc : 0.f;
+        acc[i] += x;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int d = lane + 64 * i;
+    if (d < s.D) part[(int64_t)c * s.D + d] = acc[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void seg_combine_kernel(const float* __restrict__ part,
+                                                          const int* __restrict__ seg_start, int V,
+                                                          int D, float* __restrict__ out,
+                                                          int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)V * D) return;
+  const int v = (int)(e / D), d = (int)(e - (int64_t)v * D);
+  float t = 0.f;
+  for (int c = seg_start[v]; c < seg_start[v + 1]; ++c) t += part[(int64_t)c * D + d];
+  out[e] = accumulate ? out[e] + t : t;
+}
+
+int64_t seg_rowsum_scratch_floats(int64_t M, int64_t V, int64_t D) {
+  return ((M + SEG_CH - 1) / SEG_CH + V) * D;
+}
+
+void seg_rowsum(const SegRows& s, const int* offsets, const int* perm, const int* seg_start,
+                int64_t M, int64_t V, float* out, int accumulate, float* part, hipStream_t st) {
+  const int max_chunks = (int)((M + SEG_CH - 1) / SEG_CH + V);
+  hipLaunchKernelGGL(seg_chunk_kernel, dim3((unsigned)((max_chunks + 3) / 4)), dim3(256), 0, st, s,
+                     offsets, perm, seg_start, (int)V, max_chunks, part);
+  hipLaunchKernelGGL(seg_combine_kernel, dim3((unsigned)((V * s.D + 255) / 256)), dim3(256), 0, st,
+                     part, seg_start, (int)V, s.D, out, accumulate);
+}
+
+int* group_by_seg_start(int* scratch, int64_t M, int64_t V) {
+  const int64_t chunks = (M + GB_CHUNK - 1) / GB_CHUNK;
+  return scratch + 2 * chunks * V;
+}
+
+}  // namespace tvq
+
+using namespace tvq;
+
+extern "C" int64_t tvq_reduce_rows_workspace(int64_t P, int64_t N) {
+  return reduce_rows_scratch(P, N);
+}
+
+extern "C" int tvq_reduce_rows(const float* in, int64_t P, int64_t N, int64_t ld, float* out,
+                               int64_t accumulate, float* workspace, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(in && out && P > 0 && N > 0 && ld >= N, "tvq_reduce_rows: bad arguments");
+  TVQ_CHECK_ARG(reduce_rows_scratch(P, N) == 0 || workspace, "tvq_reduce_rows: needs workspace");
+  reduce_rows(in, P, N, ld, out, nullptr, 0, (int)accumulate, workspace, (hipStream_t)stream);
+  return launch_status("tvq_reduce_rows");
+}

@@ -12,6 +12,7 @@
 #include <limits.h>
 
 #include "tvq_common.h"
+#include "tvq_reduce.h"
 
 namespace tvq {
 
@@ -177,49 +178,14 @@ __global__ __launch_bounds__(256, 2) void vq_assign_kernel(
   }
 }
 
-// One workgroup per code: scan idx32 in row order, compact the matching rows in
-// LDS (ballot prefix), accumulate their D values in row order.  Deterministic.
-__global__ __launch_bounds__(256) void vq_stats_kernel(
-    const float* __restrict__ x, int64_t M, int64_t N, int64_t sB, int64_t sN, int64_t sD, int D,
-    const int32_t* __restrict__ idx32, int32_t* __restrict__ counts, float* __restrict__ cs_batch,
-    float* __restrict__ es_batch) {
-  __shared__ int rows[256];
-  __shared__ int wcnt[4];
-  const int k = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  float acc0 = 0.f, acc1 = 0.f;  // dims tid and tid+256 (D <= 512)
-  int count = 0;
-  for (int64_t base = 0; base < M; base += 256) {
-    const int64_t m = base + tid;
-    const bool match = (m < M) && (idx32[m] == k);
-    const uint64_t bal = __ballot(match);
-    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wcnt[wid] = __popcll(bal);
-    __syncthreads();
-    int woff = 0, total = 0;
-    for (int w = 0; w < 4; ++w) { if (w < wid) woff += wcnt[w]; total += wcnt[w]; }
-    if (match) rows[woff + pre] = (int)(m - base);
-    __syncthreads();
-    if (es_batch) {
-      for (int j = 0; j < total; ++j) {
-        const int64_t mm = base + rows[j];
-        const int64_t b = mm / N, n = mm - b * N;
-        const float* xr = x + b * sB + n * sN;
-        if (tid < D) acc0 += xr[(int64_t)tid * sD];
-        if (tid + 256 < D) acc1 += xr[(int64_t)(tid + 256) * sD];
-      }
-    }
-    count += total;
-    __syncthreads();
-  }
-  if (tid == 0) {
-    counts[k] = count;
-    cs_batch[k] = (float)count;
-  }
-  if (es_batch) {
-    if (tid < D) es_batch[(int64_t)k * D + tid] = acc0;
-    if (tid + 256 < D) es_batch[(int64_t)k * D + tid + 256] = acc1;
-  }
+// counts[k] = offsets[k+1] - offsets[k] (from the stable group-by of idx32)
+__global__ void vq_counts_kernel(const int* __restrict__ offsets, int K, int32_t* __restrict__ counts,
+                                 float* __restrict__ cs_batch) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const int c = offsets[k + 1] - offsets[k];
+  counts[k] = c;
+  cs_batch[k] = (float)c;
 }
 
 __global__ void vq_ema_kernel(const float* __restrict__ cs_batch, const float* __restrict__ es_batch,
@@ -320,14 +286,34 @@ extern "C" int tvq_vq_assign(const float* x, int64_t B, int64_t N, int64_t D, in
   return launch_status("tvq_vq_assign");
 }
 
+extern "C" int64_t tvq_vq_stats_workspace(int64_t M, int64_t K) {
+  // 4-byte words: offsets | perm | group-by scratch | (aligned) float chunk partials (D <= 512)
+  const int64_t ints = (K + 1) + M + group_by_scratch_ints(M, K);
+  return ((ints + 3) / 4) * 4 + seg_rowsum_scratch_floats(M, K, 512);
+}
+
 extern "C" int tvq_vq_stats(const float* x, int64_t B, int64_t N, int64_t D, int64_t sB,
                             int64_t sN, int64_t sD, const int32_t* idx32, int64_t K,
-                            int32_t* counts, float* cs_batch, float* es_batch,
+                            int32_t* counts, float* cs_batch, float* es_batch, int32_t* workspace,
                             tvq_stream_t stream) {
-  TVQ_CHECK_ARG(x && idx32 && counts && cs_batch && B > 0 && N > 0 && K > 0 && D > 0 && D <= 512,
-                "tvq_vq_stats: bad arguments");
-  hipLaunchKernelGGL(vq_stats_kernel, dim3(K), dim3(256), 0, (hipStream_t)stream, x, B * N, N, sB,
-                     sN, sD, (int)D, idx32, counts, cs_batch, es_batch);
+  TVQ_CHECK_ARG(x && idx32 && counts && cs_batch && workspace && B > 0 && N > 0 && K > 0 && D > 0 &&
+                    D <= 512, "tvq_vq_stats: bad arguments");
+  const int64_t M = B * N;
+  hipStream_t st = (hipStream_t)stream;
+  int* offsets = workspace;
+  int* perm = offsets + (K + 1);
+  int* scratch = perm + M;
+  const int64_t ints = (K + 1) + M + group_by_scratch_ints(M, K);
+  float* part = (float*)(workspace + ((ints + 3) / 4) * 4);
+  group_by_i32(idx32, M, K, offsets, perm, scratch, st);
+  hipLaunchKernelGGL(vq_counts_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st, offsets,
+                     (int)K, counts, cs_batch);
+  if (es_batch) {
+    SegRows r;
+    r.src = x; r.N = N; r.sB = sB; r.sN = sN; r.sD = sD; r.D = (int)D;
+    r.drop_p = 0.f; r.seed_ptr = nullptr; r.offset = 0; r.mask_id = -1;
+    seg_rowsum(r, offsets, perm, group_by_seg_start(scratch, M, K), M, K, es_batch, 0, part, st);
+  }
   return launch_status("tvq_vq_stats");
 }
 

@@ -2,7 +2,8 @@
 //
 //  rmsnorm     x-transformers RMSNorm: F.normalize(x) * sqrt(D) * g
 //  layernorm   LayerNorm over the last dim (gamma [+ beta]), eps given
-//  attention   softmax(Q K^T * scale) [dropout] V for seq <= 128, one workgroup
+//  attention   softmax(Q K^T * scale) [dropout] V for seq <= 104 (the path has 25
+//              and 97: token counts do not depend on T), one workgroup
 //              per (batch, head): Q/K/V tiles and the score matrix live in LDS,
 //              scores/probabilities never touch HBM; backward recomputes P from
 //              the saved row log-sum-exp.  Q/K/V/O are read in the Linear layout
@@ -17,6 +18,7 @@
 #include <math.h>
 
 #include "tvq_common.h"
+#include "tvq_reduce.h"
 
 namespace tvq {
 
@@ -364,49 +366,6 @@ __global__ void embedding_fwd_kernel(const int64_t* __restrict__ idx, int64_t M,
   }
 }
 
-// table_grad[r, :] (+)= sum_{m: idx[m] == r} g[m, :] * dropout-mask ; one block per table row
-__global__ __launch_bounds__(256) void embedding_bwd_kernel(
-    const int64_t* __restrict__ idx, int64_t M, int D, const float* __restrict__ g, int64_t ldg,
-    float* __restrict__ tgrad, int accumulate, int64_t mask_id, float drop_p,
-    const int64_t* seed_ptr, uint64_t offset) {
-  __shared__ int rows[256];
-  __shared__ int wcnt[4];
-  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint64_t seed = drop_p > 0.f ? mix_seed(seed_ptr, offset) : 0ull;
-  const float sc = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
-  const bool drop_here = drop_p > 0.f && (int64_t)r != mask_id;
-  float acc0 = 0.f, acc1 = 0.f;
-  for (int64_t base = 0; base < M; base += 256) {
-    const int64_t m = base + tid;
-    const bool match = m < M && idx[m] == r;
-    const uint64_t bal = __ballot(match);
-    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wcnt[wid] = __popcll(bal);
-    __syncthreads();
-    int woff = 0, total = 0;
-    for (int w = 0; w < 4; ++w) { if (w < wid) woff += wcnt[w]; total += wcnt[w]; }
-    if (match) rows[woff + pre] = (int)(m - base);
-    __syncthreads();
-    for (int j = 0; j < total; ++j) {
-      const int64_t mm = base + rows[j];
-      if (tid < D) {
-        float v = g[mm * ldg + tid];
-        if (drop_here) v = uniform01(seed, (uint64_t)(mm * D + tid)) >= drop_p ? v * sc : 0.f;
-        acc0 += v;
-      }
-      if (tid + 256 < D) {
-        float v = g[mm * ldg + tid + 256];
-        if (drop_here) v = uniform01(seed, (uint64_t)(mm * D + tid + 256)) >= drop_p ? v * sc : 0.f;
-        acc1 += v;
-      }
-    }
-    __syncthreads();
-  }
-  if (tid < D) tgrad[(int64_t)r * D + tid] = accumulate ? tgrad[(int64_t)r * D + tid] + acc0 : acc0;
-  if (tid + 256 < D)
-    tgrad[(int64_t)r * D + tid + 256] = accumulate ? tgrad[(int64_t)r * D + tid + 256] + acc1 : acc1;
-}
-
 // ---------------------------------------------------------------- masked CE
 // per row (one wave): if !keep[m]: loss_m = lse(logits[m,:K]) - logits[m, t]; part sums
 __global__ __launch_bounds__(256) void masked_ce_fwd_kernel(const float* __restrict__ logits,
@@ -578,7 +537,8 @@ extern "C" int tvq_rmsnorm_fwd(const float* x, int64_t M, int64_t D, const float
 
 extern "C" int64_t tvq_norm_bwd_workspace(int64_t M, int64_t D) {
   const int rpb = norm_rows_per_block(M);
-  return ((M + rpb - 1) / rpb) * 2 * D;
+  const int64_t nb = (M + rpb - 1) / rpb;
+  return nb * 2 * D + 2 * reduce_rows_scratch(nb, D);
 }
 
 extern "C" int tvq_rmsnorm_bwd(const float* dy, const float* x, int64_t M, int64_t D,
@@ -591,8 +551,8 @@ extern "C" int tvq_rmsnorm_bwd(const float* dy, const float* x, int64_t M, int64
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(nb), dim3(256), 4 * D * sizeof(float), st, dy, x, M,
                      (int)D, g, scale, inv_norm, dx, workspace, rpb);
-  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((D + 127) / 128)), dim3(128), 0, st, workspace,
-                     nb, (int)D, dg, (int)accumulate);
+  reduce_rows(workspace, nb, D, D, dg, nullptr, 0, (int)accumulate, workspace + (int64_t)nb * 2 * D,
+              st);
   return launch_status("tvq_rmsnorm_bwd");
 }
 
@@ -615,8 +575,12 @@ extern "C" int tvq_layernorm_bwd(const float* dy, const float* x, int64_t M, int
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nb), dim3(256), 8 * D * sizeof(float), st, dy, x, M,
                      (int)D, gamma, mean, rstd, dx, workspace, rpb);
-  hipLaunchKernelGGL(ln_colsum2_kernel, dim3((unsigned)((2 * D + 127) / 128)), dim3(128), 0, st,
-                     workspace, nb, (int)D, dgamma, dbeta, (int)accumulate);
+  // workspace [nb][2][D]: reduce both halves (rows of length 2D)
+  float* rs = workspace + (int64_t)nb * 2 * D;
+  if (dgamma) reduce_rows(workspace, nb, D, 2 * D, dgamma, nullptr, 0, (int)accumulate, rs, st);
+  if (dbeta)
+    reduce_rows(workspace + D, nb, D, 2 * D, dbeta, nullptr, 0, (int)accumulate,
+                rs + reduce_rows_scratch(nb, D), st);
   return launch_status("tvq_layernorm_bwd");
 }
 
@@ -626,7 +590,7 @@ extern "C" int tvq_attention_fwd(const float* q, int64_t ldq, const float* k, in
                                  float drop_p, const int64_t* seed_ptr, uint64_t offset,
                                  tvq_stream_t stream) {
   TVQ_CHECK_ARG(q && k && v && o && lse && B > 0 && H > 0, "tvq_attention_fwd: bad arguments");
-  TVQ_CHECK_ARG(Dh == ATT_DH && S >= 1 && S <= 128, "tvq_attention_fwd: need Dh=64, S<=128");
+  TVQ_CHECK_ARG(Dh == ATT_DH && S >= 1 && S <= 104, "tvq_attention_fwd: need Dh=64, S<=104");
   AttnArgs a;
   a.q = q; a.k = k; a.v = v; a.ldq = ldq; a.ldk = ldk; a.ldv = ldv;
   a.o = o; a.ldo = ldo; a.lse = lse;
@@ -647,7 +611,7 @@ extern "C" int tvq_attention_bwd(const float* q, int64_t ldq, const float* k, in
                                  tvq_stream_t stream) {
   TVQ_CHECK_ARG(q && k && v && out && dout && lse && dq && dk && dv,
                 "tvq_attention_bwd: bad arguments");
-  TVQ_CHECK_ARG(Dh == ATT_DH && S >= 1 && S <= 128, "tvq_attention_bwd: need Dh=64, S<=128");
+  TVQ_CHECK_ARG(Dh == ATT_DH && S >= 1 && S <= 104, "tvq_attention_bwd: need Dh=64, S<=104");
   AttnBwdArgs ab;
   ab.f.q = q; ab.f.k = k; ab.f.v = v; ab.f.ldq = ldq; ab.f.ldk = ldk; ab.f.ldv = ldv;
   ab.f.o = nullptr; ab.f.ldo = 0; ab.f.lse = (float*)lse;
@@ -670,15 +634,32 @@ extern "C" int tvq_embedding_fwd(const int64_t* idx, int64_t M, int64_t D, const
   return launch_status("tvq_embedding_fwd");
 }
 
+extern "C" int64_t tvq_embedding_bwd_workspace(int64_t M, int64_t V) {
+  // 4-byte words: offsets | perm | group-by scratch | (aligned) float chunk partials (D <= 512)
+  const int64_t ints = (V + 1) + M + group_by_scratch_ints(M, V);
+  return ((ints + 3) / 4) * 4 + seg_rowsum_scratch_floats(M, V, 512);
+}
+
+// table_grad[r, :] (+)= sum_{m: idx[m] == r} g[m, :] * dropout-mask, rows summed in position
+// order via a stable group-by (deterministic, no float atomics)
 extern "C" int tvq_embedding_bwd(const int64_t* idx, int64_t M, int64_t D, const float* g,
                                  int64_t ldg, int64_t V, float* tgrad, int64_t accumulate,
                                  int64_t mask_id, float drop_p, const int64_t* seed_ptr,
-                                 uint64_t offset, tvq_stream_t stream) {
-  TVQ_CHECK_ARG(idx && g && tgrad && M > 0 && D > 0 && D <= 512 && V > 0,
+                                 uint64_t offset, int32_t* workspace, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(idx && g && tgrad && workspace && M > 0 && D > 0 && D <= 512 && V > 0,
                 "tvq_embedding_bwd: bad arguments");
-  hipLaunchKernelGGL(embedding_bwd_kernel, dim3((unsigned)V), dim3(256), 0, (hipStream_t)stream,
-                     idx, M, (int)D, g, ldg, tgrad, (int)accumulate, mask_id, drop_p, seed_ptr,
-                     offset);
+  hipStream_t st = (hipStream_t)stream;
+  int* offsets = workspace;
+  int* perm = offsets + (V + 1);
+  int* scratch = perm + M;
+  const int64_t ints = (V + 1) + M + group_by_scratch_ints(M, V);
+  float* part = (float*)(workspace + ((ints + 3) / 4) * 4);
+  group_by_i64(idx, M, V, offsets, perm, scratch, st);
+  SegRows r;
+  r.src = g; r.N = M; r.sB = 0; r.sN = ldg; r.sD = 1; r.D = (int)D;
+  r.drop_p = drop_p; r.seed_ptr = seed_ptr; r.offset = offset; r.mask_id = mask_id;
+  seg_rowsum(r, offsets, perm, group_by_seg_start(scratch, M, V), M, V, tgrad, (int)accumulate,
+             part, st);
   return launch_status("tvq_embedding_bwd");
 }
 

@@ -35,7 +35,8 @@ def sig(name, *argtypes, restype=I32):
 sig("tvq_vq_sqnorm", P, I64, I64, P, P)
 sig("tvq_vq_assign_nblocks", I64, restype=I64)
 sig("tvq_vq_assign", P, I64, I64, I64, I64, I64, I64, P, P, I64, I32, P, P, P, P, P)
-sig("tvq_vq_stats", P, I64, I64, I64, I64, I64, I64, P, I64, P, P, P, P)
+sig("tvq_vq_stats_workspace", I64, I64, restype=I64)
+sig("tvq_vq_stats", P, I64, I64, I64, I64, I64, I64, P, I64, P, P, P, P, P)
 sig("tvq_vq_ema", P, P, I64, I64, F32, P, P, P)
 sig("tvq_vq_finalize", P, P, I64, I64, F32, P, P, I64, P, P, I64, P, P)
 sig("tvq_vq_backward", P, P, P, P, I64, I64, P, P)
@@ -53,7 +54,7 @@ sig("tvq_conv2d_dgrad_workspace", I64, I64, I64, I64, I64, I64, I64, restype=I64
 sig("tvq_conv2d_dgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, P, I64, P, P)
 sig("tvq_convT2d_dgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, P, I64, P)
 sig("tvq_conv_wgrad_workspace", I64, I64, I64, I64, I64, I64, I64, restype=I64)
-sig("tvq_conv2d_wgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, I64, P, I64, P, P)
+sig("tvq_conv2d_wgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, I64, P, P, I64, P, P)
 sig("tvq_convT2d_wgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, P, I64, P, P)
 sig("tvq_channel_sum_workspace", I64, I64, I64, restype=I64)
 sig("tvq_channel_sum", P, I64, I64, I64, P, I64, P, P)
@@ -66,6 +67,8 @@ sig("tvq_snake_fwd", P, I64, I64, I64, P, P, P)
 sig("tvq_snake_workspace", I64, I64, I64, restype=I64)
 sig("tvq_snake_bwd", P, P, I64, I64, I64, P, P, P, I64, P, P)
 sig("tvq_dropout_bwd", P, I64, F32, P, U64, P, P)
+sig("tvq_reduce_rows_workspace", I64, I64, restype=I64)
+sig("tvq_reduce_rows", P, I64, I64, I64, P, I64, P, P)
 # --- dense GEMM --------------------------------------------------------------
 sig("tvq_gemm_workspace", I64, I64, I64, restype=I64)
 sig("tvq_gemm", P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, F32, P, P, I64, I64, I64, P, I64, P, P)
@@ -86,7 +89,8 @@ sig("tvq_attention_fwd", P, I64, P, I64, P, I64, P, I64, P, I64, I64, I64, I64, 
 sig("tvq_attention_bwd", P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, I64, I64, I64, F32, F32, P,
     U64, P, P, P, I64, P)
 sig("tvq_embedding_fwd", P, I64, I64, P, P, I64, I64, F32, P, U64, P)
-sig("tvq_embedding_bwd", P, I64, I64, P, I64, I64, P, I64, I64, F32, P, U64, P)
+sig("tvq_embedding_bwd_workspace", I64, I64, restype=I64)
+sig("tvq_embedding_bwd", P, I64, I64, P, I64, I64, P, I64, I64, F32, P, U64, P, P)
 sig("tvq_masked_ce_workspace", I64, restype=I64)
 sig("tvq_masked_ce_fwd", P, I64, I64, I64, P, P, P, P, P, P)
 sig("tvq_masked_ce_bwd", P, I64, I64, I64, P, P, P, P, P, P, I64, P)
@@ -150,3 +154,15 @@ def call(name, *args):
 
 def value(name, *args):
     return getattr(lib(), name)(*args)
+
+
+def grad_sink(p):
+    """p.grad when FusedAdamW keeps it as a view of its flat gradient buffer: backward
+    kernels then accumulate straight into it and the autograd Function returns None
+    for p (no AccumulateGrad kernel).  None otherwise (standard autograd return)."""
+    if p is None or not getattr(p, "_tvq_flat", False) or not p.requires_grad:
+        return None
+    g = p.grad
+    if g is None or not g.is_contiguous():
+        return None
+    return g

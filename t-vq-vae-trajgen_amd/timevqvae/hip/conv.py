@@ -8,20 +8,22 @@ Backward: dgrad (T/F gathers), wgrad (split positions, deterministic), bias = ch
 import torch
 
 from . import rng
-from ._native import call, ptr, stream_ptr, value
+from ._native import call, grad_sink, ptr, stream_ptr, value
 
 
 def _ws(n, dev):
     return torch.empty(max(int(n), 1), device=dev, dtype=torch.float32)
 
 
-def _bias_grad(g, dev):
+def _bias_grad(g, dev, sink=None):
+    """Per-channel sum of g (B, C, ...) -> returned tensor, or accumulated into `sink`."""
     B, C = g.shape[0], g.shape[1]
     HW = g.numel() // (B * C)
-    out = torch.empty(C, device=dev, dtype=torch.float32)
+    out = sink if sink is not None else torch.empty(C, device=dev, dtype=torch.float32)
     ws = _ws(value("tvq_channel_sum_workspace", B, C, HW), dev)
-    call("tvq_channel_sum", ptr(g), B, C, HW, ptr(out), 0, ptr(ws), stream_ptr())
-    return out
+    call("tvq_channel_sum", ptr(g), B, C, HW, ptr(out), int(sink is not None), ptr(ws),
+         stream_ptr())
+    return None if sink is not None else out
 
 
 def _as4d(x):
@@ -47,6 +49,7 @@ class _Conv2d(torch.autograd.Function):
         ctx.cfg = (SW, replicate, drop_p, off, squeeze, b is not None, residual is not None,
                    w.dim())
         ctx.seed = seed
+        ctx.params = (w, b)
         return y.squeeze(2) if squeeze else y
 
     @staticmethod
@@ -73,15 +76,19 @@ class _Conv2d(torch.autograd.Function):
                  int(replicate), ptr(dx), Wi, ptr(ws), s)
             if squeeze:
                 dx = dx.squeeze(2)
-        if ctx.needs_input_grad[1]:
-            dw = torch.empty_like(w4)
+        need_w, need_b = ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]
+        if need_w or need_b:
+            w_p, b_p = ctx.params
+            sw, sb = grad_sink(w_p), grad_sink(b_p) if has_b else None
+            direct = need_w and sw is not None and (not need_b or sb is not None)
+            dwt = sw if direct else torch.empty_like(w4)
+            dbt = (sb if direct else torch.empty(Co, device=dev)) if need_b else None
             ws = _ws(value("tvq_conv_wgrad_workspace", Co, Ci, KH, KW, B, H, Wo), dev)
             call("tvq_conv2d_wgrad", ptr(x4), B, Ci, H, Wi, ptr(gd), Co, Wo, KH, KW, SW,
-                 int(replicate), ptr(dw), 0, ptr(ws), s)
-            if wdim == 3:
-                dw = dw.squeeze(2)
-        if has_b and ctx.needs_input_grad[2]:
-            db = _bias_grad(gd, dev)
+                 int(replicate), ptr(dwt), ptr(dbt), int(direct), ptr(ws), s)
+            if not direct:
+                dw = (dwt.squeeze(2) if wdim == 3 else dwt) if need_w else None
+                db = dbt
         dres = None
         if has_res and ctx.needs_input_grad[5]:
             dres = gy
@@ -109,6 +116,7 @@ class _ConvT2d(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.SW = SW
         ctx.has_b = b is not None
+        ctx.params = (w, b)
         return y
 
     @staticmethod
@@ -124,13 +132,16 @@ class _ConvT2d(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             call("tvq_convT2d_dgrad", ptr(g), B, Co, H, Wo, ptr(w), Ci, KH, KW, SW, ptr(dx), Wi, s)
+        w_p, b_p = ctx.params
         if ctx.needs_input_grad[1]:
-            dw = torch.empty_like(w)
+            sw = grad_sink(w_p)
+            dwt = sw if sw is not None else torch.empty_like(w)
             ws = _ws(value("tvq_conv_wgrad_workspace", Ci, Co, KH, KW, B, H, Wi), x.device)
-            call("tvq_convT2d_wgrad", ptr(x), B, Ci, H, Wi, ptr(g), Co, Wo, KH, KW, SW, ptr(dw), 0,
-                 ptr(ws), s)
+            call("tvq_convT2d_wgrad", ptr(x), B, Ci, H, Wi, ptr(g), Co, Wo, KH, KW, SW, ptr(dwt),
+                 int(sw is not None), ptr(ws), s)
+            dw = None if sw is not None else dwt
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = _bias_grad(g, x.device)
+            db = _bias_grad(g, x.device, grad_sink(b_p))
         return dx, dw, db, None
 
 

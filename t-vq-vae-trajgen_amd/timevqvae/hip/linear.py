@@ -1,7 +1,7 @@
 """Dense GEMM ops (nn.Linear over the last dim) on the HIP path."""
 import torch
 
-from ._native import call, ptr, stream_ptr, value
+from ._native import call, grad_sink, ptr, stream_ptr, value
 
 
 def gemm(A, sam, sak, B, sbk, sbn, M, N, K, out=None, ldc=None, alpha=1.0, bias=None, R=None,
@@ -18,12 +18,23 @@ def gemm(A, sam, sak, B, sbk, sbn, M, N, K, out=None, ldc=None, alpha=1.0, bias=
     return out
 
 
-def _bias_grad_rows(g2):
+def _bias_grad_rows(g2, sink=None):
+    """Column sums of a row-major (M, N) gradient: returned, or accumulated into `sink`."""
     M, N = g2.shape
-    out = torch.empty(N, device=g2.device, dtype=torch.float32)
+    out = sink if sink is not None else torch.empty(N, device=g2.device, dtype=torch.float32)
     ws = torch.empty(value("tvq_channel_sum_workspace", M, N, 1), device=g2.device)
-    call("tvq_channel_sum", ptr(g2), M, N, 1, ptr(out), 0, ptr(ws), stream_ptr())
-    return out
+    call("tvq_channel_sum", ptr(g2), M, N, 1, ptr(out), int(sink is not None), ptr(ws),
+         stream_ptr())
+    return None if sink is not None else out
+
+
+def weight_grad(g, x2, w_param, M, N, K):
+    """dW = g^T x (N x K): accumulated into the flat grad view when available."""
+    sink = grad_sink(w_param)
+    if sink is not None:
+        gemm(g, 1, N, x2, K, 1, N, K, M, out=sink, ldc=K, accumulate=True)
+        return None
+    return gemm(g, 1, N, x2, K, 1, N, K, M)
 
 
 class _Linear(torch.autograd.Function):
@@ -40,6 +51,7 @@ class _Linear(torch.autograd.Function):
         ctx.save_for_backward(x2, w)
         ctx.has = (b is not None, residual is not None)
         ctx.shp = shp
+        ctx.params = (w, b)
         return y.reshape(*shp[:-1], N)
 
     @staticmethod
@@ -52,9 +64,9 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = gemm(g, N, 1, w, K, 1, M, K, N).reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
-            dw = gemm(g, 1, N, x2, K, 1, N, K, M)
+            dw = weight_grad(g, x2, ctx.params[0], M, N, K)
         if ctx.has[0] and ctx.needs_input_grad[2]:
-            db = _bias_grad_rows(g)
+            db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
         if ctx.has[1] and ctx.needs_input_grad[3]:
             dres = gy
         return dx, dw, db, dres

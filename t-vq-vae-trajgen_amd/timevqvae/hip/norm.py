@@ -1,7 +1,7 @@
 """BatchNorm (+ fused SnakeActivation) and standalone Snake on the HIP path."""
 import torch
 
-from ._native import call, ptr, stream_ptr, value
+from ._native import call, grad_sink, ptr, stream_ptr, value
 
 
 def _dims(x):
@@ -12,6 +12,8 @@ def _dims(x):
 class _BNSnakeTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, a, running_mean, running_var, nbt, momentum, eps):
+        ctx.params = (w, b, a)
+        a = a.reshape(-1) if a is not None else None
         x = x.contiguous()
         B, C, HW = _dims(x)
         dev = x.device
@@ -33,18 +35,28 @@ class _BNSnakeTrain(torch.autograd.Function):
         g = gy.contiguous()
         dx = torch.empty_like(x)
         has_w, has_b, has_a = ctx.has
-        dw = torch.empty(C, device=dev) if has_w else None
-        db = torch.empty(C, device=dev) if has_b else None
-        da = torch.empty(C, device=dev) if has_a else None
+        sinks = [grad_sink(p) if h else None for p, h in zip(ctx.params, ctx.has)]
+        direct = all((s is not None) == h for s, h in zip(sinks, ctx.has))
+        if direct:
+            dw, db, da = sinks
+        else:
+            dw = torch.empty(C, device=dev) if has_w else None
+            db = torch.empty(C, device=dev) if has_b else None
+            da = torch.empty(C, device=dev) if has_a else None
         ws = torch.empty(value("tvq_bn_workspace", B, C, HW), device=dev, dtype=torch.uint8)
         call("tvq_bn_bwd", ptr(g), ptr(x), B, C, HW, ptr(w), ptr(a), ptr(save[:C]),
-             ptr(save[C:2 * C]), ptr(save[2 * C:]), ptr(dx), ptr(dw), ptr(db), ptr(da), 0, ptr(ws),
-             stream_ptr())
+             ptr(save[C:2 * C]), ptr(save[2 * C:]), ptr(dx), ptr(dw), ptr(db), ptr(da), int(direct),
+             ptr(ws), stream_ptr())
+        if direct:
+            return dx, None, None, None, None, None, None, None, None
+        if da is not None:
+            da = da.view_as(ctx.params[2])
         return dx, dw, db, da, None, None, None, None, None
 
 
 def bn_snake(x, bn, a=None):
-    """snake_a(BatchNorm(x)) with the module `bn`'s parameters/buffers; a: (C,) or None."""
+    """snake_a(BatchNorm(x)) with the module `bn`'s parameters/buffers; a: the Snake
+    parameter ((1,C,1,1) or (C,)) or None."""
     if bn.training:
         if bn.momentum is None:
             raise NotImplementedError("cumulative-average BatchNorm (momentum=None) is not on the path")
@@ -56,6 +68,7 @@ def bn_snake(x, bn, a=None):
     B, C, HW = _dims(x)
     y = torch.empty_like(x)
     ss = torch.empty(2 * C, device=x.device, dtype=torch.float32)
+    a = a.reshape(-1) if a is not None else None
     call("tvq_bn_eval_fwd", ptr(x), B, C, HW, ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
          ptr(bn.running_var), float(bn.eps), ptr(a), ptr(y), ptr(ss), stream_ptr())
     return y
@@ -64,6 +77,8 @@ def bn_snake(x, bn, a=None):
 class _Snake(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, a):
+        ctx.a_param = a
+        a = a.reshape(-1)
         x = x.contiguous()
         B, C, HW = _dims(x)
         y = torch.empty_like(x)
@@ -77,13 +92,15 @@ class _Snake(torch.autograd.Function):
         B, C, HW = _dims(x)
         g = gy.contiguous()
         dx = torch.empty_like(x)
-        da = torch.empty(C, device=x.device)
+        sink = grad_sink(ctx.a_param)
+        da = sink if sink is not None else torch.empty(C, device=x.device)
         ws = torch.empty(value("tvq_snake_workspace", B, C, HW), device=x.device, dtype=torch.uint8)
-        call("tvq_snake_bwd", ptr(g), ptr(x), B, C, HW, ptr(a), ptr(dx), ptr(da), 0, ptr(ws),
-             stream_ptr())
-        return dx, da
+        call("tvq_snake_bwd", ptr(g), ptr(x), B, C, HW, ptr(a), ptr(dx), ptr(da), int(sink is not None),
+             ptr(ws), stream_ptr())
+        return dx, (None if sink is not None else da.view_as(ctx.a_param))
 
 
 def snake(x, a):
-    """SnakeActivation (train_utils.py:446-448): x + (1/a) sin(a x)^2, a: (C,)."""
+    """SnakeActivation (train_utils.py:446-448): x + (1/a) sin(a x)^2; a: the (1,C,1,1)
+    parameter or a (C,) tensor."""
     return _Snake.apply(x, a)

@@ -36,6 +36,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 self.flat[off:off + k].copy_(p.reshape(-1))
                 p.data = self.flat[off:off + k].view_as(p)
                 p.grad = self.flat_grad[off:off + k].view_as(p)
+                p._tvq_flat = True
                 off += k
 
     def zero_grad(self, set_to_none: bool = False):

@@ -51,8 +51,9 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
     counts = torch.empty(K, device=dev, dtype=torch.int32)
     cs_b = torch.empty(K, device=dev, dtype=torch.float32)
     es_b = torch.empty((K, D), device=dev, dtype=torch.float32) if ema else None
+    ws = torch.empty(value("tvq_vq_stats_workspace", M, K), device=dev, dtype=torch.int32)
     call("tvq_vq_stats", ptr(x), B, N, D, sB, sN, sD, ptr(idx32), K, ptr(counts), ptr(cs_b),
-         ptr(es_b), s)
+         ptr(es_b), ptr(ws), s)
     perp = torch.empty((), device=dev, dtype=torch.float32)
     commit = torch.empty((), device=dev, dtype=torch.float32) if straight_through else None
     if ema:

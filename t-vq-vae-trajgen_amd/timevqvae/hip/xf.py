@@ -4,8 +4,8 @@ import math
 import torch
 
 from . import rng
-from ._native import call, ptr, stream_ptr, value
-from .linear import _bias_grad_rows, gemm
+from ._native import call, grad_sink, ptr, stream_ptr, value
+from .linear import _bias_grad_rows, gemm, weight_grad
 
 
 def _rows(x):
@@ -22,6 +22,7 @@ class _RMSNorm(torch.autograd.Function):
         inv = torch.empty(M, device=x.device, dtype=torch.float32)
         call("tvq_rmsnorm_fwd", ptr(x2), M, D, ptr(g), float(scale), ptr(y), ptr(inv), stream_ptr())
         ctx.save_for_backward(x2, g, inv)
+        ctx.g_param = g
         ctx.scale = scale
         ctx.shape = x.shape
         return y.reshape(x.shape)
@@ -32,11 +33,12 @@ class _RMSNorm(torch.autograd.Function):
         M, D = x2.shape
         dy = gy.reshape(M, D).contiguous()
         dx = torch.empty_like(x2)
-        dg = torch.empty(D, device=x2.device)
+        sink = grad_sink(ctx.g_param)
+        dg = sink if sink is not None else torch.empty(D, device=x2.device)
         ws = torch.empty(value("tvq_norm_bwd_workspace", M, D), device=x2.device)
         call("tvq_rmsnorm_bwd", ptr(dy), ptr(x2), M, D, ptr(g), float(ctx.scale), ptr(inv), ptr(dx),
-             ptr(dg), 0, ptr(ws), stream_ptr())
-        return dx.reshape(ctx.shape), dg, None
+             ptr(dg), int(sink is not None), ptr(ws), stream_ptr())
+        return dx.reshape(ctx.shape), (None if sink is not None else dg), None
 
 
 def rmsnorm(x, g):
@@ -55,6 +57,7 @@ class _LayerNorm(torch.autograd.Function):
         call("tvq_layernorm_fwd", ptr(x2), M, D, ptr(gamma), ptr(beta), float(eps), ptr(y),
              ptr(mean), ptr(rstd), stream_ptr())
         ctx.save_for_backward(x2, gamma, mean, rstd)
+        ctx.params = (gamma, beta)
         ctx.has = (gamma is not None, beta is not None)
         ctx.shape = x.shape
         return y.reshape(x.shape)
@@ -65,11 +68,18 @@ class _LayerNorm(torch.autograd.Function):
         M, D = x2.shape
         dy = gy.reshape(M, D).contiguous()
         dx = torch.empty_like(x2)
-        dg = torch.empty(D, device=x2.device) if ctx.has[0] else None
-        db = torch.empty(D, device=x2.device) if ctx.has[1] else None
+        sinks = [grad_sink(p) if h else None for p, h in zip(ctx.params, ctx.has)]
+        direct = all((s is not None) == h for s, h in zip(sinks, ctx.has))
+        if direct:
+            dg, db = sinks
+        else:
+            dg = torch.empty(D, device=x2.device) if ctx.has[0] else None
+            db = torch.empty(D, device=x2.device) if ctx.has[1] else None
         ws = torch.empty(value("tvq_norm_bwd_workspace", M, D), device=x2.device)
         call("tvq_layernorm_bwd", ptr(dy), ptr(x2), M, D, ptr(gamma), ptr(mean), ptr(rstd), ptr(dx),
-             ptr(dg), ptr(db), 0, ptr(ws), stream_ptr())
+             ptr(dg), ptr(db), int(direct), ptr(ws), stream_ptr())
+        if direct:
+            return dx.reshape(ctx.shape), None, None, None
         return dx.reshape(ctx.shape), dg, db, None
 
 
@@ -91,6 +101,7 @@ class _LinearAct(torch.autograd.Function):
         pre = torch.empty((M, N), device=x.device) if act else None
         y = gemm(x2, K, 1, w, 1, K, M, N, K, bias=b, act=act, pre=pre)
         ctx.save_for_backward(x2, w, pre)
+        ctx.params = (w, b)
         ctx.act = act
         ctx.has_b = b is not None
         ctx.shape = x.shape
@@ -110,9 +121,9 @@ class _LinearAct(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = gemm(g, N, 1, w, K, 1, M, K, N).reshape(ctx.shape)
         if ctx.needs_input_grad[1]:
-            dw = gemm(g, 1, N, x2, K, 1, N, K, M)
+            dw = weight_grad(g, x2, ctx.params[0], M, N, K)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = _bias_grad_rows(g)
+            db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
         return dx, dw, db, None
 
 
@@ -173,6 +184,7 @@ class _Embedding(torch.autograd.Function):
         call("tvq_embedding_fwd", ptr(idx), M, D, ptr(table), ptr(out), D, int(mask_id),
              float(drop_p), ptr(seed), off, stream_ptr())
         ctx.save_for_backward(idx)
+        ctx.table = table
         ctx.cfg = (V, D, mask_id, drop_p, off)
         ctx.seed = seed
         return out.reshape(*idx.shape, D)
@@ -183,10 +195,13 @@ class _Embedding(torch.autograd.Function):
         V, D, mask_id, drop_p, off = ctx.cfg
         M = idx.numel()
         g2 = g.reshape(M, D).contiguous()
-        tg = torch.empty((V, D), device=g.device)
-        call("tvq_embedding_bwd", ptr(idx), M, D, ptr(g2), D, V, ptr(tg), 0, int(mask_id),
-             float(drop_p), ptr(ctx.seed), off, stream_ptr())
-        return None, tg, None, None, None
+        sink = grad_sink(ctx.table)
+        tg = sink if sink is not None else torch.empty((V, D), device=g.device)
+        ws = torch.empty(value("tvq_embedding_bwd_workspace", M, V), device=g.device,
+                         dtype=torch.int32)
+        call("tvq_embedding_bwd", ptr(idx), M, D, ptr(g2), D, V, ptr(tg), int(sink is not None),
+             int(mask_id), float(drop_p), ptr(ctx.seed), off, ptr(ws), stream_ptr())
+        return None, (None if sink is not None else tg), None, None, None
 
 
 def embedding(idx, table, mask_id=-1, drop_p=0.0, site=0):

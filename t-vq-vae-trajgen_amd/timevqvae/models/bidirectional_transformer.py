@@ -29,7 +29,7 @@ from ..hip.linear import _bias_grad_rows, gemm, linear
 from ..hip.norm import bn_snake
 from ..hip.xf import (attention, embedding, gelu, layer_norm, linear_act, rmsnorm,
                       upsample_nearest)
-from ..hip._native import call, ptr, stream_ptr
+from ..hip._native import call, grad_sink, ptr, stream_ptr
 
 
 # ------------------------------------------------------------------ x-transformers tree
@@ -179,6 +179,7 @@ class _TiedLogits(torch.autograd.Function):
         M = B * n
         out = gemm(h2, D, 1, W, 1, D, M, K, D, R=bias, ldr=bias.shape[1], rmod=n)
         ctx.save_for_backward(h2, W)
+        ctx.W, ctx.bias = W, bias
         ctx.cfg = (B, n, D, K, tuple(bias.shape))
         return out.reshape(B, n, K)
 
@@ -192,12 +193,20 @@ class _TiedLogits(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dh = gemm(g2, K, 1, W, D, 1, M, D, K).reshape(B, n, D)
         if ctx.needs_input_grad[1]:
-            dW = torch.zeros_like(W)
-            gemm(g2, 1, K, h2, D, 1, K, D, M, out=dW, ldc=D)
+            sink = grad_sink(ctx.W)
+            if sink is not None:  # tied table: accumulate next to the embedding-lookup grad
+                gemm(g2, 1, K, h2, D, 1, K, D, M, out=sink, ldc=D, accumulate=True)
+            else:
+                dW = torch.zeros_like(W)
+                gemm(g2, 1, K, h2, D, 1, K, D, M, out=dW, ldc=D)
         if ctx.needs_input_grad[2]:
-            dbias = torch.zeros(bshape, device=g.device)
-            s = _bias_grad_rows(g2.reshape(B, n * K))  # sum over the batch
-            dbias[:, :K] = s.reshape(n, K)
+            s = _bias_grad_rows(g2.reshape(B, n * K)).reshape(n, K)  # sum over the batch
+            sink = grad_sink(ctx.bias)
+            if sink is not None:
+                sink[:, :K] += s
+            else:
+                dbias = torch.zeros(bshape, device=g.device)
+                dbias[:, :K] = s
         return dh, dW, dbias, None
 
 

@@ -26,7 +26,7 @@ from ..utils.train_utils import band_of
 
 
 def _a(snake_mod):
-    return snake_mod.a.reshape(-1)
+    return snake_mod.a  # the (1,C,1,1) Parameter: kernels read it flat, grads land in .grad
 
 
 class ResBlock(nn.Module):

@@ -127,8 +127,9 @@ class SnakeActivation(nn.Module):
             self.register_buffer("a", torch.full(shape, a_base, dtype=torch.float32))
 
     def forward(self, x):
-        return _snake(x, self.a.reshape(-1).expand(x.shape[1]).contiguous()
-                      if self.a.numel() == 1 else self.a.reshape(-1))
+        if self.a.numel() == 1:
+            return _snake(x, self.a.reshape(-1).expand(x.shape[1]).contiguous())
+        return _snake(x, self.a)
 
 
 def linear_warmup_cosine_annealingLR(optimizer: torch.optim.Optimizer, max_steps: int,

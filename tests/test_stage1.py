@@ -83,9 +83,14 @@ def test_stage1_eval_reconstruction(tag, cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tag", TAGS)
-def test_stage1_train_step_grads(tag, cuda):
+@pytest.mark.parametrize("tag,flat", [("small", False), ("cfgB", False), ("cfgB", True)])
+def test_stage1_train_step_grads(tag, flat, cuda):
+    """flat=True: FusedAdamW owns the gradients (kernels accumulate into the flat buffer)."""
     m, g = build(tag, cuda)
+    if flat:
+        from timevqvae.hip.optim import FusedAdamW
+        opt = FusedAdamW(m.parameters(), lr=1e-3)
+        opt.zero_grad()
     embeds = {n: getattr(m, n)._codebook.embed.detach().cpu().numpy().copy()
               for n in ("vq_model_l", "vq_model_h")}
     m.train()
