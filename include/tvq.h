@@ -121,24 +121,31 @@ int tvq_istft_decode_bwd(const float* dy, int64_t B, int64_t C, int64_t W, int64
  * padding (KH/2, (KW-1)/2).  Epilogue of the forward conv: + bias, optional
  * dropout (counter-based mask keyed by (*seed_ptr, offset) and the flat output
  * index: the device seed advances once per step so graph replays differ) and + residual
- * (ResBlock: proj(x) + Dropout(conv(..)), vq_vae.py:52,62). */
+ * (ResBlock: proj(x) + Dropout(conv(..)), vq_vae.py:52,62).
+ * wpack (nullable, weight-numel floats): scratch into which the weight is repacked
+ * tap-major / output-channel-contiguous before the GEMM (coalesced operand loads);
+ * NULL reads the weight in place. */
 int tvq_conv_out_width(int64_t Win, int64_t KW, int64_t SW, int64_t transposed);
+/* engine selection (process-wide): halo = 1 lets convs whose padded image and weight
+ * panel fit in 64 KB of LDS run on the halo-tile kernel, 0 forces the staged GEMM;
+ * < 0 only queries.  Returns the previous setting. */
+int tvq_conv_config(int64_t halo);
 int tvq_conv2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi, const float* w,
                    const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t SW,
                    int64_t replicate, float* y, const float* residual, float drop_p,
-                   const int64_t* seed_ptr, uint64_t offset, tvq_stream_t stream);
+                   const int64_t* seed_ptr, uint64_t offset, float* wpack, tvq_stream_t stream);
 int tvq_convT2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi, const float* w,
                     const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t SW, float* y,
-                    const float* residual, tvq_stream_t stream);
+                    const float* residual, float* wpack, tvq_stream_t stream);
 int64_t tvq_conv2d_dgrad_workspace(int64_t B, int64_t Ci, int64_t H, int64_t Wi, int64_t KH,
                                    int64_t KW, int64_t replicate);
 int tvq_conv2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t Wo,
                      const float* w, int64_t Ci, int64_t KH, int64_t KW, int64_t SW,
                      int64_t replicate, float* dx, int64_t Wi, float* workspace,
-                     tvq_stream_t stream);
+                     float* wpack, tvq_stream_t stream);
 int tvq_convT2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t Wo,
                       const float* w, int64_t Ci, int64_t KH, int64_t KW, int64_t SW, float* dx,
-                      int64_t Wi, tvq_stream_t stream);
+                      int64_t Wi, float* wpack, tvq_stream_t stream);
 int64_t tvq_conv_wgrad_workspace(int64_t N, int64_t C, int64_t KH, int64_t KW, int64_t B,
                                  int64_t Hout, int64_t Wo);
 /* weight gradient (+ the bias gradient sum dY into db when non-NULL, as an extra

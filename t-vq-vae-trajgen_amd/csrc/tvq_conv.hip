@@ -47,7 +47,7 @@ struct ConvGeom {
   int B, C, Hin, Win;  // gathered tensor
   int N, Hout, Wo;     // output / G positions
   int oph, opw;        // pad offsets: F: hi = h+kh-oph, wi = wo*SW+kw-opw;  T: hi = h-kh+oph, wn = wo-kw+opw
-  int64_t wsn, wsc;    // weight strides for (n, c); (kh, kw) contiguous: kh*KW + kw
+  int64_t wsn, wsc, wst;  // weight strides for (n, c, tap = kh*KW + kw)
   FastDiv fd_wo, fd_hwo;
   int Kred;            // C*KH*KW
   int Mpos;            // B*Hout*Wo
@@ -94,6 +94,61 @@ struct Epi {
   const int64_t* seed_ptr;
   uint64_t offset;
 };
+
+// Epilogue helpers.  Every global load here is unconditional (clamped index) so the
+// compiler issues them together instead of one load + wait per element.
+template <int FN>
+__device__ __forceinline__ void epi_load_bias(float (&bv)[FN][4], const float* __restrict__ bias,
+                                              int nbase, int N) {
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = min(nbase + i * 16 + r, N - 1);
+      bv[i][r] = bias ? bias[n] : 0.f;
+    }
+}
+
+// a[i][r]: channel nbase + i*16 + r at flat offset ob + n*hw (ob for a clamped position
+// when !pv, so every address is in bounds)
+template <int FN>
+__device__ __forceinline__ void epi_store(float* __restrict__ out, const Epi& e, uint64_t seed,
+                                          const float (&bv)[FN][4], const floatx4 (&a)[FN],
+                                          int64_t ob, int64_t hw, int nbase, int N, bool pv) {
+  float v[FN][4];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[i][r] = a[i][r] + bv[i][r];
+  if (e.drop_p > 0.f) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint64_t o = (uint64_t)(ob + (int64_t)(nbase + i * 16 + r) * hw);
+        v[i][r] = uniform01(seed, o) >= e.drop_p ? v[i][r] * e.drop_scale : 0.f;
+      }
+  }
+  if (e.residual) {
+    float rv[FN][4];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        rv[i][r] = e.residual[ob + (int64_t)min(nbase + i * 16 + r, N - 1) * hw];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[i][r] += rv[i][r];
+  }
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nbase + i * 16 + r;
+      if (pv && n < N) out[ob + (int64_t)n * hw] = v[i][r];
+    }
+}
 
 template <int MODE, int KH, int KW, int SW, bool REPL, int TN, int TM, int WN, int WM>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(const float* __restrict__ in,
@@ -145,7 +200,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const float* __restrict_
       float v = 0.f;
       if (an < g.N && k < g.Kred) {
         const int c = k / KK, r = k - c * KK;
-        v = wt[an * g.wsn + c * g.wsc + r];
+        v = wt[an * g.wsn + c * g.wsc + r * g.wst];
       }
       ra[j] = v;
     }
@@ -191,28 +246,156 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const float* __restrict_
 
   const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
   // epilogue: acc[i][j][r] -> channel n0 + (wn*FN+i)*16 + 4*g4 + r, position m0 + (wm*FM+j)*16 + r16
+  const int nbase = n0 + wn * FN * 16 + 4 * g4;
+  float bv[FN][4];
+  epi_load_bias<FN>(bv, e.bias, nbase, g.N);
+  const int64_t hw = (int64_t)g.Hout * g.Wo;
 #pragma unroll
   for (int j = 0; j < FM; ++j) {
     const int m = m0 + (wm * FM + j) * 16 + r16;
-    if (m >= g.Mpos) continue;
-    const uint32_t bh = fdiv((uint32_t)m, g.fd_wo);
-    const int w = m - (int)bh * g.Wo;
-    const int b = (int)fdiv((uint32_t)m, g.fd_hwo);
+    const bool pv = m < g.Mpos;
+    const int mc = pv ? m : 0;
+    const uint32_t bh = fdiv((uint32_t)mc, g.fd_wo);
+    const int w = mc - (int)bh * g.Wo;
+    const int b = (int)fdiv((uint32_t)mc, g.fd_hwo);
     const int h = (int)bh - b * g.Hout;
+    floatx4 a[FN];
 #pragma unroll
-    for (int i = 0; i < FN; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + (wn * FN + i) * 16 + 4 * g4 + r;
-        if (n >= g.N) continue;
-        const int64_t o = (((int64_t)b * g.N + n) * g.Hout + h) * g.Wo + w;
-        float v = acc[i][j][r];
-        if (e.bias) v += e.bias[n];
-        if (e.drop_p > 0.f) v = (uniform01(seed, (uint64_t)o) >= e.drop_p) ? v * e.drop_scale : 0.f;
-        if (e.residual) v += e.residual[o];
-        out[o] = v;
+    for (int i = 0; i < FN; ++i) a[i] = acc[i][j];
+    epi_store<FN>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + w, hw, nbase, g.N,
+                  pv);
+  }
+}
+
+// Tap-major variant for C % 16 == 0: the K loop runs over (tap, channel block), so a
+// thread's spatial source (and its validity) is computed once per tap and every
+// gathered element costs one multiply-add and one predicated load.
+template <int MODE, int KH, int KW, int SW, bool REPL, int TN, int TM, int WN, int WM, int BK>
+__global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__ in,
+                                                      const float* __restrict__ wt,
+                                                      float* __restrict__ out, ConvGeom g, Epi e) {
+  constexpr int KK = KH * KW;
+  constexpr int FN = TN / WN / 16;
+  constexpr int FM = TM / WM / 16;
+  constexpr int SA = ((TN + 31) / 32) * 32 + 16;
+  constexpr int SB = ((TM + 31) / 32) * 32 + 16;
+  constexpr int A_PER = TN * BK / 256;
+  constexpr int B_PER = TM * BK / 256;
+  constexpr int BK_STEP = 256 / TM;
+  constexpr int AK_STEP = 256 / TN;
+  static_assert(A_PER >= 1 && B_PER >= 1 && BK_STEP >= 1 && AK_STEP >= 1, "tile");
+  __shared__ float As[BK * SA];
+  __shared__ float Bs[BK * SB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid % WN, wm = wid / WN;
+  const int n0 = blockIdx.y * TN;
+  const int m0 = blockIdx.x * TM;
+  const int bm_local = tid % TM, bk_base = tid / TM;
+  const int mpos = m0 + bm_local;
+  const bool mvalid = mpos < g.Mpos;
+  int pb = 0, ph = 0, pw = 0;
+  if (mvalid) {
+    const uint32_t bh = fdiv((uint32_t)mpos, g.fd_wo);
+    pw = mpos - (int)bh * g.Wo;
+    pb = (int)fdiv((uint32_t)mpos, g.fd_hwo);
+    ph = (int)bh - pb * g.Hout;
+  }
+  const int64_t plane = (int64_t)g.Hin * g.Win;
+  const float* inb = in + (int64_t)pb * g.C * plane;
+  const int an_local = tid % TN, ak_base = tid / TN;
+  const int an = n0 + an_local;
+  const float* wrow = wt + (int64_t)(an < g.N ? an : 0) * g.wsn;
+  const int csteps = (g.C + BK - 1) / BK;
+  const int nsteps = KK * csteps;
+
+  float ra[A_PER], rb[B_PER];
+  auto load_tile = [&](int step) {
+    const int tap = step / csteps;
+    const int c0 = (step - tap * csteps) * BK;
+    const int kh = tap / KW, kw = tap - kh * KW;
+    int hi, wi;
+    bool ok = mvalid;
+    if (MODE == GATHER_F) {
+      hi = ph + kh - g.oph;
+      wi = pw * SW + kw - g.opw;
+      if (REPL) {
+        hi = hi < 0 ? 0 : (hi >= g.Hin ? g.Hin - 1 : hi);
+        wi = wi < 0 ? 0 : (wi >= g.Win ? g.Win - 1 : wi);
+      } else {
+        ok = ok && hi >= 0 && hi < g.Hin && wi >= 0 && wi < g.Win;
       }
+    } else {
+      hi = ph - kh + g.oph;
+      const int wn_ = pw - kw + g.opw;
+      ok = ok && hi >= 0 && hi < g.Hin && wn_ >= 0 && (SW == 1 || (wn_ & 1) == 0);
+      wi = wn_ / SW;
+      ok = ok && wi < g.Win;
     }
+    const float* src = inb + (ok ? (int64_t)hi * g.Win + wi : 0);
+#pragma unroll
+    for (int j = 0; j < B_PER; ++j) {
+      const int c = c0 + bk_base + j * BK_STEP;
+      rb[j] = (ok && c < g.C) ? src[(int64_t)c * plane] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < A_PER; ++j) {
+      const int c = c0 + ak_base + j * AK_STEP;
+      ra[j] = (an < g.N && c < g.C) ? wrow[(int64_t)c * g.wsc + tap * g.wst] : 0.f;
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int j = 0; j < A_PER; ++j) As[(ak_base + j * AK_STEP) * SA + an_local] = ra[j];
+#pragma unroll
+    for (int j = 0; j < B_PER; ++j) Bs[(bk_base + j * BK_STEP) * SB + bm_local] = rb[j];
+  };
+
+  floatx4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15, g4 = lane >> 4;
+  load_tile(0);
+  for (int step = 0; step < nsteps; ++step) {
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    if (step + 1 < nsteps) load_tile(step + 1);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      float af[FN], bf[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) af[i] = As[(kk + g4) * SA + (wn * FN + i) * 16 + r16];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) bf[j] = Bs[(kk + g4) * SB + (wm * FM + j) * 16 + r16];
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma16x16x4(af[i], bf[j], acc[i][j]);
+    }
+  }
+
+  const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
+  const int nbase = n0 + wn * FN * 16 + 4 * g4;
+  float bv[FN][4];
+  epi_load_bias<FN>(bv, e.bias, nbase, g.N);
+  const int64_t hw = (int64_t)g.Hout * g.Wo;
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const int m = m0 + (wm * FM + j) * 16 + r16;
+    const bool pv = m < g.Mpos;
+    const int mc = pv ? m : 0;
+    const uint32_t bh = fdiv((uint32_t)mc, g.fd_wo);
+    const int w = mc - (int)bh * g.Wo;
+    const int b = (int)fdiv((uint32_t)mc, g.fd_hwo);
+    const int h = (int)bh - b * g.Hout;
+    floatx4 a[FN];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) a[i] = acc[i][j];
+    epi_store<FN>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + w, hw, nbase, g.N,
+                  pv);
   }
 }
 
@@ -247,6 +430,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
   const int kk_t = tid % BK;  // each thread owns one position slot of the K-step
   const int a_nbase = tid / BK;
   const int b_kbase = tid / BK;
+  // the thread's k' columns are fixed for the whole launch: decompose them once
+  int bc_off[B_PER], bkh[B_PER], bkw[B_PER];
+  unsigned bmask = 0u, bones = 0u;
+#pragma unroll
+  for (int j = 0; j < B_PER; ++j) {
+    const int kp = kp0 + b_kbase + j * 16;
+    const int c = kp / KK, r = kp - c * KK;
+    bkh[j] = r / KW - g.oph;
+    bkw[j] = r - (r / KW) * KW - g.opw;
+    bc_off[j] = (kp < g.Kred) ? c * g.Hin * g.Win : 0;
+    if (kp < g.Kred) bmask |= 1u << j;
+    if (kp == g.Kred && kp < kcols) bones |= 1u << j;
+  }
 
   float ra[A_PER], rb[B_PER];
   auto load_tile = [&](int p0) {
@@ -268,12 +464,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
     const float* inb = in + (int64_t)b * g.C * g.Hin * g.Win;
 #pragma unroll
     for (int j = 0; j < B_PER; ++j) {
-      const int kp = kp0 + b_kbase + j * 16;
-      float v = (pv && kp == g.Kred && kp < kcols) ? 1.0f : 0.f;
-      if (pv && kp < g.Kred) {
-        const int c = kp / KK, r = kp - c * KK;
-        const int kh = r / KW, kw = r - kh * KW;
-        int hi = h + kh - g.oph, wi = w * SW + kw - g.opw;
+      float v = (pv && (bones >> j & 1u)) ? 1.0f : 0.f;
+      if (pv && (bmask >> j & 1u)) {
+        int hi = h + bkh[j], wi = w * SW + bkw[j];
         bool ok = true;
         if (REPL) {
           hi = hi < 0 ? 0 : (hi >= g.Hin ? g.Hin - 1 : hi);
@@ -281,7 +474,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
         } else {
           ok = hi >= 0 && hi < g.Hin && wi >= 0 && wi < g.Win;
         }
-        if (ok) v = inb[((int64_t)c * g.Hin + hi) * g.Win + wi];
+        if (ok) v = inb[bc_off[j] + (int64_t)hi * g.Win + wi];
       }
       rb[j] = v;
     }
@@ -386,7 +579,7 @@ static ConvGeom make_geom(int B, int C, int Hin, int Win, int N, int Hout, int W
   ConvGeom g;
   g.B = B; g.C = C; g.Hin = Hin; g.Win = Win; g.N = N; g.Hout = Hout; g.Wo = Wo;
   g.oph = oph; g.opw = opw;
-  g.wsn = wsn; g.wsc = wsc;
+  g.wsn = wsn; g.wsc = wsc; g.wst = 1;
   g.fd_wo = make_fastdiv((uint32_t)Wo);
   g.fd_hwo = make_fastdiv((uint32_t)(Hout * Wo));
   g.Kred = C * KH * KW;
@@ -394,10 +587,563 @@ static ConvGeom make_geom(int B, int C, int Hin, int Win, int N, int Hout, int W
   return g;
 }
 
+// ---------------------------------------------------------------- halo-tile path
+// For convolutions whose padded input image (Cp x HP x WP) and a weight panel of NB
+// output channels (K = Cp*KK columns) fit in LDS together -- the small-channel ResBlock,
+// encoder and decoder convs -- one block takes one image b and NB channels: both
+// tiles are loaded once (batched so many loads are in flight per thread, one sync),
+// then every MFMA operand is an LDS read: A from the panel, B from the halo image at
+// h*WP + w*SW + koff[k], koff[k] = c*PS + kh*WP + kw from a per-block table.  There is
+// no per-K-step global round trip, which is what bounds the staged GEMM at these sizes
+// (a few hundred positions per image, K <= 576).
+//   F  out[n,h,w] = sum W(n,c,kh,kw) In[c, h+kh-oh, w*SW+kw-ow]         (halo = In, padded)
+//   T  out[n,h,w] = sum W(n,c,kh,kw) D[c, h+KH-1-kh, w+KW-1-kw]          (D = In dilated by SW,
+//      oh = KH-1-PH, ow = KW-1-PW: the transposed gather as a stride-1 conv, taps flipped)
+// The weight panel keeps the raw (c, kh, kw) column order, so it is a straight copy of
+// the weight rows.  KS = 4 splits K across the 4 waves when the image has <= 4 position
+// tiles (partials reduced through LDS).
+// q = n / d by one v_mul_hi_u32, exact while n * d < 2^32 (halo indices and divisors
+// are both < 2^16 here); d >= 2
+struct Div16 {
+  uint32_t d, m;
+};
+static Div16 make_div16(int d) {
+  Div16 r;
+  r.d = (uint32_t)d;
+  r.m = (uint32_t)(((1ull << 32) + d - 1) / d);
+  return r;
+}
+__device__ __forceinline__ int div16(int n, const Div16& v) {
+  return (int)__umulhi((uint32_t)n, v.m);
+}
+
+struct HaloGeom {
+  Div16 dv_hw, dv_wp, dv_wo, dv_k;
+  int C, Cp, Hin, Win, N, Hout, Wo;
+  int oh, ow;          // halo (hp, wp) -> source row hp - oh, col (wp - ow) [/SW for T]
+  int HP, WP, PS;      // halo rows / cols; channel-plane stride (== 16 mod 32)
+  int P, MT;           // positions per image, 16-position tiles per image
+  int KST;             // weight-panel row stride (== 2 mod 32)
+  int64_t wsn, wsc;    // raw weight strides of (n, c); taps contiguous
+};
+
+static constexpr int HALO_U = 8;  // loads in flight per thread in the load phase
+
+template <int MODE, int KH, int KW, int SW, bool REPL>
+__device__ __forceinline__ void halo_fill(float* __restrict__ Hs, const float* __restrict__ inb,
+                                          int C, int Cp, int Hin, int Win, int HP, int WP, int PS,
+                                          int oh, int ow, const Div16& dv_hw, const Div16& dv_wp,
+                                          int tid) {
+  const int hw = HP * WP;
+  const int total = Cp * hw;
+  for (int base = tid; base < total; base += 256 * HALO_U) {
+    float v[HALO_U];
+    int dst[HALO_U];
+#pragma unroll
+    for (int u = 0; u < HALO_U; ++u) {
+      const int idx = base + u * 256;
+      v[u] = 0.f;
+      dst[u] = -1;
+      if (idx < total) {
+        const int c = div16(idx, dv_hw);
+        const int r = idx - c * hw;
+        const int hp = div16(r, dv_wp);
+        const int wp = r - hp * WP;
+        dst[u] = c * PS + r;
+        if (c < C) {
+          int hi = hp - oh;
+          if (MODE == GATHER_F) {
+            int wi = wp - ow;
+            if (REPL) {
+              hi = hi < 0 ? 0 : (hi >= Hin ? Hin - 1 : hi);
+              wi = wi < 0 ? 0 : (wi >= Win ? Win - 1 : wi);
+              v[u] = inb[((int64_t)c * Hin + hi) * Win + wi];
+            } else if (hi >= 0 && hi < Hin && wi >= 0 && wi < Win) {
+              v[u] = inb[((int64_t)c * Hin + hi) * Win + wi];
+            }
+          } else {
+            const int wn = wp - ow;
+            const int wi = wn / SW;
+            if (hi >= 0 && hi < Hin && wn >= 0 && wn - wi * SW == 0 && wi < Win)
+              v[u] = inb[((int64_t)c * Hin + hi) * Win + wi];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < HALO_U; ++u)
+      if (dst[u] >= 0) Hs[dst[u]] = v[u];
+  }
+}
+
+template <int MODE, int KH, int KW, int SW, bool REPL, int FN, int KS>
+__global__ __launch_bounds__(256) void conv_halo_kernel(const float* __restrict__ in,
+                                                       const float* __restrict__ wt,
+                                                       float* __restrict__ out, HaloGeom g,
+                                                       Epi e) {
+  constexpr int KK = KH * KW;
+  constexpr int NB = FN * 16;
+  constexpr int CSW = MODE == GATHER_F ? SW : 1;  // position stride inside the halo
+  extern __shared__ float smem[];
+  const int K = g.Cp * KK;
+  float* Hs = smem;                                  // [Cp][PS]
+  float* As = Hs + g.Cp * g.PS;                      // [NB][KST], columns (c, kh, kw)
+  int* koff = reinterpret_cast<int*>(As + NB * g.KST);  // [K]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b = blockIdx.x;
+  const int n0 = blockIdx.y * NB;
+
+  // ---- load phase
+  halo_fill<MODE, KH, KW, SW, REPL>(Hs, in + (int64_t)b * g.C * g.Hin * g.Win, g.C, g.Cp, g.Hin,
+                                    g.Win, g.HP, g.WP, g.PS, g.oh, g.ow, g.dv_hw, g.dv_wp, tid);
+  {
+    // panel element (nn, k = c*KK + t); walk the raw weight in its contiguous order
+    const bool n_inner = g.wsn < g.wsc;  // dgrad / convT layouts: (c, n, t)
+    const int total = NB * K;
+    for (int base = tid; base < total; base += 256 * HALO_U) {
+      float v[HALO_U];
+      int dst[HALO_U];
+#pragma unroll
+      for (int u = 0; u < HALO_U; ++u) {
+        const int idx = base + u * 256;
+        v[u] = 0.f;
+        dst[u] = -1;
+        if (idx < total) {
+          int nn, c, t;
+          if (n_inner) {
+            t = idx % KK;
+            const int r = idx / KK;
+            c = r / NB;
+            nn = r - c * NB;
+          } else {
+            nn = div16(idx, g.dv_k);
+            const int k = idx - nn * K;
+            c = k / KK;
+            t = k - c * KK;
+          }
+          dst[u] = nn * g.KST + c * KK + t;
+          const int n = n0 + nn;
+          if (n < g.N && c < g.C) v[u] = wt[(int64_t)n * g.wsn + (int64_t)c * g.wsc + t];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < HALO_U; ++u)
+        if (dst[u] >= 0) As[dst[u]] = v[u];
+    }
+    for (int k = tid; k < K; k += 256) {
+      const int c = k / KK, t = k - c * KK;
+      const int tl = MODE == GATHER_F ? t : KK - 1 - t;
+      koff[k] = c * g.PS + (tl / KW) * g.WP + (tl % KW);
+    }
+  }
+  __syncthreads();
+
+  const int j = lane & 15, kq = lane >> 4;
+  const int Q = K / 4;
+  const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
+
+  auto run = [&](int mt0, int mstep, int fa, int qs, int qe, floatx4 (&acc)[FN][4]) {
+    int base[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int p = (mt0 + f * mstep) * 16 + j;
+      const int pp = p < g.P ? p : 0;
+      const int h = div16(pp, g.dv_wo);
+      const int w = pp - h * g.Wo;
+      base[f] = h * g.WP + w * CSW;
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[i][f] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const float* ap = As + j * g.KST + kq;
+    for (int q = qs; q < qe; ++q) {
+      const int ko = koff[q * 4 + kq];
+      float af[FN];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) af[i] = ap[i * 16 * g.KST + q * 4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        if (f < fa) {
+          const float bf = Hs[base[f] + ko];
+#pragma unroll
+          for (int i = 0; i < FN; ++i) acc[i][f] = mfma16x16x4(af[i], bf, acc[i][f]);
+        }
+      }
+    }
+  };
+  const int nbase = n0 + kq * 4;
+  float bv[FN][4];
+  epi_load_bias<FN>(bv, e.bias, nbase, g.N);
+  const int64_t hwo = (int64_t)g.Hout * g.Wo;
+  auto store = [&](int mt, const floatx4 (&a)[FN]) {
+    const int p = mt * 16 + j;
+    const bool pv = p < g.P;
+    const int pp = pv ? p : 0;
+    const int h = div16(pp, g.dv_wo);
+    const int w = pp - h * g.Wo;
+    epi_store<FN>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + w, hwo, nbase,
+                  g.N, pv);
+  };
+
+  floatx4 acc[FN][4];
+  if (KS == 1) {
+    for (int mt0 = wid; mt0 < g.MT; mt0 += 16) {
+      const int fa = min(4, (g.MT - mt0 + 3) / 4);
+      run(mt0, 4, fa, 0, Q, acc);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        if (f < fa) {
+          floatx4 a[FN];
+#pragma unroll
+          for (int i = 0; i < FN; ++i) a[i] = acc[i][f];
+          store(mt0 + 4 * f, a);
+        }
+      }
+    }
+  } else {
+    // MT <= 4: every wave takes all position tiles over a quarter of K
+    const int fa = g.MT;
+    const int qs = wid * Q / 4, qe = (wid + 1) * Q / 4;
+    run(0, 1, fa, qs, qe, acc);
+    __syncthreads();  // all waves done with the tiles: reuse LDS for the partials
+    floatx4* red = reinterpret_cast<floatx4*>(smem);
+    if (wid > 0) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+          if (f < fa) red[(((wid - 1) * FN + i) * 4 + f) * 64 + lane] = acc[i][f];
+    }
+    __syncthreads();
+    if (wid == 0) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        if (f < fa) {
+          floatx4 a[FN];
+#pragma unroll
+          for (int i = 0; i < FN; ++i) {
+            a[i] = acc[i][f];
+#pragma unroll
+            for (int wv = 0; wv < 3; ++wv) {
+              const floatx4 t = red[((wv * FN + i) * 4 + f) * 64 + lane];
+              a[i][0] += t[0]; a[i][1] += t[1]; a[i][2] += t[2]; a[i][3] += t[3];
+            }
+          }
+          store(f, a);
+        }
+      }
+    }
+  }
+}
+
+static constexpr int HALO_LDS_MAX = 64 * 1024;
+
+struct HaloPlan {
+  HaloGeom g;
+  int FN, KS;
+  size_t lds;
+};
+
+// mode F: (oh, ow) = (PH, PW) of the conv;  T: (KH-1-oph, KW-1-opw) of the T gather
+static bool halo_plan(int mode, int B, int C, int Hin, int Win, int N, int Hout, int Wo, int KH,
+                      int KW, int SW, int oh, int ow, int64_t wsn, int64_t wsc, HaloPlan* pl) {
+  HaloGeom g;
+  g.C = C; g.Cp = (C + 3) & ~3; g.Hin = Hin; g.Win = Win; g.N = N; g.Hout = Hout; g.Wo = Wo;
+  g.oh = oh; g.ow = ow;
+  g.HP = Hout + KH - 1;
+  g.WP = mode == GATHER_F ? (Wo - 1) * SW + KW : Wo + KW - 1;
+  const int hw = g.HP * g.WP;
+  g.PS = hw + ((16 - hw % 32) + 32) % 32;
+  g.P = Hout * Wo;
+  g.MT = (g.P + 15) / 16;
+  g.wsn = wsn; g.wsc = wsc;
+  const int K = KH * KW * g.Cp;
+  if (Wo < 2 || g.WP < 2 || K < 2 || g.P >= (1 << 16)) return false;
+  g.dv_hw = make_div16(hw);
+  g.dv_wp = make_div16(g.WP);
+  g.dv_wo = make_div16(Wo);
+  g.dv_k = make_div16(K);
+  const int KST = K + ((2 - K % 32) + 32) % 32;
+  const int fn_cover = N <= 16 ? 1 : (N <= 32 ? 2 : 4);
+  for (int FN = fn_cover; FN >= 1; FN /= 2) {
+    const int NB = FN * 16;
+    if ((N + NB - 1) / NB > 4) break;  // the image would be re-staged by > 4 blocks
+    const int KS = g.MT <= 4 ? 4 : 1;
+    size_t fl = (size_t)g.Cp * g.PS + (size_t)NB * KST + K;
+    const size_t red = KS > 1 ? (size_t)3 * FN * 4 * 64 * 4 : 0;
+    if (red > fl) fl = red;
+    if (fl * 4 <= (size_t)HALO_LDS_MAX) {
+      g.KST = KST;
+      pl->g = g;
+      pl->FN = FN;
+      pl->KS = KS;
+      pl->lds = fl * 4;
+      return true;
+    }
+  }
+  (void)B;
+  return false;
+}
+
+template <int MODE, int KH, int KW, int SW, bool REPL>
+static void launch_halo(const float* in, const float* wt, float* out, const HaloPlan& pl, int B,
+                        const Epi& e, hipStream_t st) {
+  const dim3 grid(B, (pl.g.N + pl.FN * 16 - 1) / (pl.FN * 16));
+#define H_(FN_, KS_)                                                                          \
+  hipLaunchKernelGGL((conv_halo_kernel<MODE, KH, KW, SW, REPL, FN_, KS_>), grid, dim3(256), \
+                     pl.lds, st, in, wt, out, pl.g, e)
+  if (pl.KS == 4) {
+    if (pl.FN == 1) H_(1, 4); else if (pl.FN == 2) H_(2, 4); else H_(4, 4);
+  } else {
+    if (pl.FN == 1) H_(1, 1); else if (pl.FN == 2) H_(2, 1); else H_(4, 1);
+  }
+#undef H_
+}
+
+// Halo-tile weight gradient: dW[n, c, tap] = sum_{b,h,w} G[b,n,h,w] In[b,c, h+kh-oh, w*SW+kw-ow]
+// (+ a ones column for the bias gradient).  Block (s, nb, cb) loops over the images of
+// split s; per image the G tile (NB x P) and the halo of CB input channels are loaded
+// with all loads in flight, then the MFMAs reduce over the image's positions from LDS.
+// Partials go to slab[s][n][kcols] and are summed in split order (wgrad_finish).
+struct WHaloGeom {
+  Div16 dv_hw, dv_wp, dv_gst;
+  int B, C, Hin, Win, N, Hout, Wo;
+  int oh, ow, HP, WP, PS;
+  int P, GST, CB;
+  int Kred, kcols;   // kcols = Kred (+1: bias column)
+  int ips;           // images per split
+};
+
+template <int KH, int KW, int SW, bool REPL, int FN>
+__global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(const float* __restrict__ G,
+                                                             const float* __restrict__ in,
+                                                             float* __restrict__ slab,
+                                                             WHaloGeom g) {
+  constexpr int KK = KH * KW;
+  constexpr int NB = FN * 16;
+  extern __shared__ float smem[];
+  float* Gs = smem;                     // [NB][GST]
+  float* Hs = smem + NB * g.GST;        // [CB][PS], then a plane of ones
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int s = blockIdx.x;
+  const int n0 = blockIdx.y * NB;
+  const int c0 = blockIdx.z * g.CB;
+  const int cbn = min(g.CB, g.C - c0);
+  const bool last_cb = c0 + g.CB >= g.C;
+  const int kb = cbn * KK + ((last_cb && g.kcols > g.Kred) ? 1 : 0);  // columns of this block
+  const int KT = (kb + 15) / 16;
+  const int j = lane & 15, kq = lane >> 4;
+
+  for (int idx = tid; idx < g.PS; idx += 256) Hs[g.CB * g.PS + idx] = 1.0f;
+  int koff[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int kl = (wid + 4 * t) * 16 + j;
+    const int c = kl / KK, tap = kl - c * KK;
+    koff[t] = kl < cbn * KK ? c * g.PS + (tap / KW) * g.WP + (tap % KW) : g.CB * g.PS;
+  }
+  const int ktw = wid < KT ? (KT - wid + 3) / 4 : 0;  // k-tiles of this wave (<= 4)
+
+  floatx4 acc[FN][4];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int b_begin = s * g.ips, b_end = min(g.B, b_begin + g.ips);
+  for (int b = b_begin; b < b_end; ++b) {
+    __syncthreads();  // previous image consumed
+    const float* gb = G + ((int64_t)b * g.N + n0) * g.P;
+    const int gtot = NB * g.GST;
+    for (int base = tid; base < gtot; base += 256 * HALO_U) {
+      float v[HALO_U];
+#pragma unroll
+      for (int u = 0; u < HALO_U; ++u) {
+        const int idx = base + u * 256;
+        const int nn = div16(idx, g.dv_gst), m = idx - nn * g.GST;
+        v[u] = (idx < gtot && m < g.P && n0 + nn < g.N) ? gb[(int64_t)nn * g.P + m] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < HALO_U; ++u)
+        if (base + u * 256 < gtot) Gs[base + u * 256] = v[u];
+    }
+    halo_fill<GATHER_F, KH, KW, SW, REPL>(Hs, in + ((int64_t)b * g.C + c0) * g.Hin * g.Win, cbn,
+                                          cbn, g.Hin, g.Win, g.HP, g.WP, g.PS, g.oh, g.ow,
+                                          g.dv_hw, g.dv_wp, tid);
+    __syncthreads();
+    // positions m0..m0+3 lie in one row (Wo % 4 == 0); lane group kq takes m0 + kq
+    int h0 = 0, w0 = 0;
+    for (int m0 = 0; m0 < g.P; m0 += 4) {
+      const int base = h0 * g.WP + (w0 + kq) * SW;
+      float af[FN];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) af[i] = Gs[(i * 16 + j) * g.GST + m0 + kq];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < ktw) {
+          const float bf = Hs[base + koff[t]];
+#pragma unroll
+          for (int i = 0; i < FN; ++i) acc[i][t] = mfma16x16x4(af[i], bf, acc[i][t]);
+        }
+      }
+      w0 += 4;
+      if (w0 == g.Wo) { w0 = 0; ++h0; }
+    }
+  }
+  float* out = slab + (int64_t)s * g.N * g.kcols;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t >= ktw) continue;
+    const int kl = (wid + 4 * t) * 16 + j;
+    int kg;
+    if (kl < cbn * KK) kg = c0 * KK + kl;
+    else if (kl == cbn * KK && kb > cbn * KK) kg = g.Kred;
+    else continue;
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + i * 16 + kq * 4 + r;
+        if (n < g.N) out[(int64_t)n * g.kcols + kg] = acc[i][t][r];
+      }
+  }
+}
+
+struct WHaloPlan {
+  WHaloGeom g;
+  int FN, S, nblk, cblk;
+  size_t lds;
+};
+
+static constexpr int64_t WHALO_SLAB_MAX = 4 << 20;  // floats
+
+// split count depends only on (N, C, KK, B) so the workspace query can reproduce it
+static int whalo_splits(int64_t N, int64_t C, int KK, int64_t B, int nblk, int cblk) {
+  const int64_t kc = C * KK + 1;
+  int64_t S = 1024 / (nblk * cblk);
+  const int64_t cap = WHALO_SLAB_MAX / (N * kc);
+  if (S > cap) S = cap;
+  if (S > B) S = B;
+  if (S < 1) S = 1;
+  const int64_t ips = (B + S - 1) / S;
+  return (int)((B + ips - 1) / ips);
+}
+
+static void whalo_blocking(int64_t N, int64_t C, int KK, int* FN, int* CB) {
+  *FN = N <= 16 ? 1 : (N <= 32 ? 2 : 4);
+  int cb = 1;
+  while (cb * 2 <= C && (cb * 2) * KK + 1 <= 256) cb *= 2;  // <= 16 k-tiles of 16
+  if (cb > C) cb = (int)C;
+  *CB = cb;
+}
+
+static bool whalo_plan(int B, int C, int Hin, int Win, int N, int Hout, int Wo, int KH, int KW,
+                       int SW, int oh, int ow, int kcols, WHaloPlan* pl) {
+  if (Wo % 4 != 0) return false;
+  // long images with many channels (the Upscale Conv1d) run better on the split GEMM
+  if (Hout * Wo > 128 && C > 64) return false;
+  WHaloGeom g;
+  g.B = B; g.C = C; g.Hin = Hin; g.Win = Win; g.N = N; g.Hout = Hout; g.Wo = Wo;
+  g.oh = oh; g.ow = ow;
+  g.HP = Hout + KH - 1;
+  g.WP = (Wo - 1) * SW + KW;
+  const int hw = g.HP * g.WP;
+  g.PS = hw + ((16 - hw % 32) + 32) % 32;
+  g.P = Hout * Wo;
+  g.GST = g.P + ((2 - g.P % 32) + 32) % 32;
+  if (g.WP < 2 || g.P >= (1 << 16)) return false;
+  g.dv_hw = make_div16(hw);
+  g.dv_wp = make_div16(g.WP);
+  g.dv_gst = make_div16(g.GST);
+  const int KK = KH * KW;
+  int FN, CB;
+  whalo_blocking(N, C, KK, &FN, &CB);
+  g.CB = CB;
+  g.Kred = C * KK;
+  g.kcols = kcols;
+  const size_t fl = (size_t)FN * 16 * g.GST + (size_t)(CB + 1) * g.PS;
+  if (fl * 4 > (size_t)HALO_LDS_MAX) return false;
+  pl->nblk = (N + FN * 16 - 1) / (FN * 16);
+  pl->cblk = (C + CB - 1) / CB;
+  pl->S = whalo_splits(N, C, KK, B, pl->nblk, pl->cblk);
+  g.ips = (B + pl->S - 1) / pl->S;
+  pl->g = g;
+  pl->FN = FN;
+  pl->lds = fl * 4;
+  return true;
+}
+
+template <int KH, int KW, int SW, bool REPL>
+static void launch_wgrad_halo(const float* G, const float* in, float* slab, const WHaloPlan& pl,
+                              hipStream_t st) {
+  const dim3 grid(pl.S, pl.nblk, pl.cblk);
+#define W_(FN_)                                                                              \
+  hipLaunchKernelGGL((conv_wgrad_halo_kernel<KH, KW, SW, REPL, FN_>), grid, dim3(256), pl.lds, \
+                     st, G, in, slab, pl.g)
+  if (pl.FN == 1) W_(1); else if (pl.FN == 2) W_(2); else W_(4);
+#undef W_
+}
+
+// Repack a weight seen as (n, c, tap) with strides (wsn, wsc, 1) into [tap][c][n] so the
+// A-operand loads of a K-step read TN consecutive floats (one or two cache lines) instead
+// of TN rows a whole filter apart.
+__global__ void conv_pack_weight_kernel(const float* __restrict__ w, int N, int C, int KK,
+                                        int64_t wsn, int64_t wsc, float* __restrict__ out) {
+  const int64_t total = (int64_t)N * C * KK;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(i % N);
+    const int64_t r = i / N;
+    const int c = (int)(r % C);
+    const int tap = (int)(r / C);
+    out[i] = w[n * wsn + c * wsc + tap];
+  }
+}
+
+// Pack `wt` into `ws` (N*C*KK floats) when given and retarget the geometry's weight strides.
+static const float* pack_weight(const float* wt, ConvGeom& g, int KK, float* ws, hipStream_t st) {
+  if (!ws) return wt;
+  const int64_t total = (int64_t)g.N * g.C * KK;
+  const int blocks = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+  hipLaunchKernelGGL(conv_pack_weight_kernel, dim3(blocks), dim3(256), 0, st, wt, g.N, g.C, KK,
+                     g.wsn, g.wsc, ws);
+  g.wsn = 1;
+  g.wsc = g.N;
+  g.wst = (int64_t)g.N * g.C;
+  return ws;
+}
+
+template <int MODE, int KH, int KW, int SW, bool REPL, int BK>
+static void launch_tap(const float* in, const float* wt, float* out, const ConvGeom& g,
+                       const Epi& e, hipStream_t st) {
+  if (g.N <= 16) {
+    dim3 grid((g.Mpos + 255) / 256, (g.N + 15) / 16);
+    hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 16, 256, 1, 4, BK>), grid,
+                       dim3(256), 0, st, in, wt, out, g, e);
+  } else if (g.N <= 32) {
+    dim3 grid((g.Mpos + 127) / 128, (g.N + 31) / 32);
+    hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 32, 128, 2, 2, BK>), grid,
+                       dim3(256), 0, st, in, wt, out, g, e);
+  } else {
+    dim3 grid((g.Mpos + 127) / 128, (g.N + 63) / 64);
+    hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 64, 128, 2, 2, BK>), grid,
+                       dim3(256), 0, st, in, wt, out, g, e);
+  }
+}
+
 template <int MODE, int KH, int KW, int SW, bool REPL>
 static void launch_gemm(const float* in, const float* wt, float* out, const ConvGeom& g,
                         const Epi& e, hipStream_t st) {
-  // channel tile by output channel count; position tile keeps >= ~2 waves of blocks
+  if (g.C % 32 == 0) {
+    launch_tap<MODE, KH, KW, SW, REPL, 32>(in, wt, out, g, e, st);
+    return;
+  }
+  if (g.C % 16 == 0) {
+    launch_tap<MODE, KH, KW, SW, REPL, 16>(in, wt, out, g, e, st);
+    return;
+  }
+  // small channel counts: flat (c, kh, kw) K order keeps the K-steps full
   if (g.N <= 16) {
     dim3 grid((g.Mpos + 255) / 256, (g.N + 15) / 16);
     hipLaunchKernelGGL((conv_gemm_kernel<MODE, KH, KW, SW, REPL, 16, 256, 1, 4>), grid, dim3(256),
@@ -411,6 +1157,24 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
     hipLaunchKernelGGL((conv_gemm_kernel<MODE, KH, KW, SW, REPL, 64, 128, 2, 2>), grid, dim3(256),
                        0, st, in, wt, out, g, e);
   }
+}
+
+static int g_conv_halo = 3;  // tvq_conv_config bits: 1 = halo fwd/dgrad, 2 = halo wgrad
+
+// halo path when the image + weight panel fit in LDS, else the staged GEMM
+template <int MODE, int KH, int KW, int SW, bool REPL>
+static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g, float* wpack,
+                        const Epi& e, hipStream_t st) {
+  HaloPlan pl;
+  const int oh = MODE == GATHER_F ? g.oph : KH - 1 - g.oph;
+  const int ow = MODE == GATHER_F ? g.opw : KW - 1 - g.opw;
+  if ((g_conv_halo & 1) && halo_plan(MODE, g.B, g.C, g.Hin, g.Win, g.N, g.Hout, g.Wo, KH, KW, SW, oh,
+                               ow, g.wsn, g.wsc, &pl)) {
+    launch_halo<MODE, KH, KW, SW, REPL>(in, wt, out, pl, g.B, e, st);
+    return;
+  }
+  wt = pack_weight(wt, g, KH * KW, wpack, st);
+  launch_gemm<MODE, KH, KW, SW, REPL>(in, wt, out, g, e, st);
 }
 
 template <int KH, int KW, int SW, bool REPL>
@@ -475,6 +1239,12 @@ static Epi make_epi(const float* bias, const float* residual, float drop_p,
   return e;
 }
 
+extern "C" int tvq_conv_config(int64_t halo) {
+  const int prev = g_conv_halo;
+  if (halo >= 0) g_conv_halo = (int)(halo & 3);
+  return prev;
+}
+
 extern "C" int tvq_conv_out_width(int64_t Win, int64_t KW, int64_t SW, int64_t transposed) {
   const int64_t PW = (KW - 1) / 2;
   return (int)(transposed ? (Win - 1) * SW - 2 * PW + KW : (Win + 2 * PW - KW) / SW + 1);
@@ -487,7 +1257,7 @@ extern "C" int tvq_conv2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, 
                               const float* w, const float* bias, int64_t Co, int64_t KH,
                               int64_t KW, int64_t SW, int64_t replicate, float* y,
                               const float* residual, float drop_p, const int64_t* seed_ptr,
-                              uint64_t offset, tvq_stream_t stream) {
+                              uint64_t offset, float* wpack, tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && w && y && B > 0 && Ci > 0 && Co > 0, "tvq_conv2d_fwd: bad arguments");
   const int kind = kind_of((int)KH, (int)KW, (int)SW);
   TVQ_CHECK_ARG(kind >= 0, "tvq_conv2d_fwd: unsupported kernel %lldx%lld s%lld", (long long)KH,
@@ -498,7 +1268,7 @@ extern "C" int tvq_conv2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, 
                          PH_OF(KH), PW_OF(KW), Ci * KH * KW, KH * KW);
   Epi e = make_epi(bias, residual, drop_p, seed_ptr, offset);
   hipStream_t st = (hipStream_t)stream;
-#define M_(a, b_, c, d) launch_gemm<GATHER_F, a, b_, c, d>(x, w, y, g, e, st);
+#define M_(a, b_, c, d) launch_conv<GATHER_F, a, b_, c, d>(x, w, y, g, wpack, e, st);
   TVQ_DISPATCH_KIND(kind, replicate, M_)
 #undef M_
   return launch_status("tvq_conv2d_fwd");
@@ -507,7 +1277,7 @@ extern "C" int tvq_conv2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, 
 extern "C" int tvq_convT2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
                                const float* w, const float* bias, int64_t Co, int64_t KH,
                                int64_t KW, int64_t SW, float* y, const float* residual,
-                               tvq_stream_t stream) {
+                               float* wpack, tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && w && y && B > 0 && Ci > 0 && Co > 0, "tvq_convT2d_fwd: bad arguments");
   const int kind = kind_of((int)KH, (int)KW, (int)SW);
   TVQ_CHECK_ARG(kind >= 0, "tvq_convT2d_fwd: unsupported kernel");
@@ -517,7 +1287,7 @@ extern "C" int tvq_convT2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H,
                          PH_OF(KH), PW_OF(KW), KH * KW, Co * KH * KW);
   Epi e = make_epi(bias, residual, 0.f, nullptr, 0);
   hipStream_t st = (hipStream_t)stream;
-#define M_(a, b_, c, d) launch_gemm<GATHER_T, a, b_, c, false>(x, w, y, g, e, st);
+#define M_(a, b_, c, d) launch_conv<GATHER_T, a, b_, c, false>(x, w, y, g, wpack, e, st);
   TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
   return launch_status("tvq_convT2d_fwd");
@@ -532,7 +1302,7 @@ extern "C" int64_t tvq_conv2d_dgrad_workspace(int64_t B, int64_t Ci, int64_t H, 
 extern "C" int tvq_conv2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t Wo,
                                 const float* w, int64_t Ci, int64_t KH, int64_t KW, int64_t SW,
                                 int64_t replicate, float* dx, int64_t Wi, float* workspace,
-                                tvq_stream_t stream) {
+                                float* wpack, tvq_stream_t stream) {
   TVQ_CHECK_ARG(dy && w && dx && B > 0 && Ci > 0 && Co > 0, "tvq_conv2d_dgrad: bad arguments");
   const int kind = kind_of((int)KH, (int)KW, (int)SW);
   TVQ_CHECK_ARG(kind >= 0, "tvq_conv2d_dgrad: unsupported kernel");
@@ -543,7 +1313,7 @@ extern "C" int tvq_conv2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t 
   if (!replicate) {
     ConvGeom g = make_geom((int)B, (int)Co, (int)H, (int)Wo, (int)Ci, (int)H, (int)Wi, (int)KH,
                            (int)KW, PH_OF(KH), PW_OF(KW), KH * KW, Ci * KH * KW);
-#define M_(a, b_, c, d) launch_gemm<GATHER_T, a, b_, c, false>(dy, w, dx, g, e, st);
+#define M_(a, b_, c, d) launch_conv<GATHER_T, a, b_, c, false>(dy, w, dx, g, wpack, e, st);
     TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
     return launch_status("tvq_conv2d_dgrad");
@@ -554,7 +1324,8 @@ extern "C" int tvq_conv2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t 
   const int Hp = (int)H + 2 * PH_OF(KH), Wp = (int)Wi + 2 * PW_OF(KW);
   ConvGeom g = make_geom((int)B, (int)Co, (int)H, (int)Wo, (int)Ci, Hp, Wp, (int)KH, (int)KW, 0, 0,
                          KH * KW, Ci * KH * KW);
-#define M_(a, b_, c, d) launch_gemm<GATHER_T, a, b_, c, false>(dy, w, workspace, g, e, st);
+#define M_(a, b_, c, d) \
+  launch_conv<GATHER_T, a, b_, c, false>(dy, w, workspace, g, wpack, e, st);
   TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
   const int64_t tot = B * Ci * H * Wi;
@@ -566,7 +1337,7 @@ extern "C" int tvq_conv2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t 
 
 extern "C" int tvq_convT2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t Wo,
                                  const float* w, int64_t Ci, int64_t KH, int64_t KW, int64_t SW,
-                                 float* dx, int64_t Wi, tvq_stream_t stream) {
+                                 float* dx, int64_t Wi, float* wpack, tvq_stream_t stream) {
   TVQ_CHECK_ARG(dy && w && dx && B > 0 && Ci > 0 && Co > 0, "tvq_convT2d_dgrad: bad arguments");
   const int kind = kind_of((int)KH, (int)KW, (int)SW);
   TVQ_CHECK_ARG(kind >= 0, "tvq_convT2d_dgrad: unsupported kernel");
@@ -576,7 +1347,7 @@ extern "C" int tvq_convT2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t
                          (int)KW, PH_OF(KH), PW_OF(KW), Co * KH * KW, KH * KW);
   Epi e = make_epi(nullptr, nullptr, 0.f, nullptr, 0);
   hipStream_t st = (hipStream_t)stream;
-#define M_(a, b_, c, d) launch_gemm<GATHER_F, a, b_, c, false>(dy, w, dx, g, e, st);
+#define M_(a, b_, c, d) launch_conv<GATHER_F, a, b_, c, false>(dy, w, dx, g, wpack, e, st);
   TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
   return launch_status("tvq_convT2d_dgrad");
@@ -595,9 +1366,21 @@ static int64_t wgrad_ws(int64_t N, int64_t Kred, int64_t Mpos, int* splits_out, 
   return (int64_t)splits * N * kc + reduce_rows_scratch(splits, N * kc);
 }
 
+static int64_t whalo_ws(int64_t N, int64_t C, int64_t KH, int64_t KW, int64_t B) {
+  int FN, CB;
+  const int KK = (int)(KH * KW);
+  whalo_blocking(N, C, KK, &FN, &CB);
+  const int nblk = (int)((N + FN * 16 - 1) / (FN * 16)), cblk = (int)((C + CB - 1) / CB);
+  const int S = whalo_splits(N, C, KK, B, nblk, cblk);
+  const int64_t kc = C * KK + 1;
+  return (int64_t)S * N * kc + reduce_rows_scratch(S, N * kc);
+}
+
 extern "C" int64_t tvq_conv_wgrad_workspace(int64_t N, int64_t C, int64_t KH, int64_t KW,
                                             int64_t B, int64_t Hout, int64_t Wo) {
-  return wgrad_ws(N, C * KH * KW, B * Hout * Wo, nullptr, nullptr);
+  const int64_t a = wgrad_ws(N, C * KH * KW, B * Hout * Wo, nullptr, nullptr);
+  const int64_t h = whalo_ws(N, C, KH, KW, B);
+  return a > h ? a : h;
 }
 
 static void wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, float* dw,
@@ -619,10 +1402,20 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
   TVQ_CHECK_ARG(kind >= 0, "tvq_conv2d_wgrad: unsupported kernel");
   ConvGeom g = make_geom((int)B, (int)Ci, (int)H, (int)Wi, (int)Co, (int)H, (int)Wo, (int)KH,
                          (int)KW, PH_OF(KH), PW_OF(KW), Ci * KH * KW, KH * KW);
-  int splits, pps;
-  wgrad_ws(Co, g.Kred, g.Mpos, &splits, &pps);
   const int kcols = g.Kred + (db ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
+  WHaloPlan pl;
+  if ((g_conv_halo & 2) && whalo_plan((int)B, (int)Ci, (int)H, (int)Wi, (int)Co, (int)H, (int)Wo,
+                                      (int)KH, (int)KW, (int)SW, PH_OF(KH), PW_OF(KW), kcols,
+                                      &pl)) {
+#define M_(a, b_, c, d) launch_wgrad_halo<a, b_, c, d>(dy, x, workspace, pl, st);
+    TVQ_DISPATCH_KIND(kind, replicate, M_)
+#undef M_
+    wgrad_finish(workspace, pl.S, Co, kcols, dw, db, (int)accumulate, st);
+    return launch_status("tvq_conv2d_wgrad(halo)");
+  }
+  int splits, pps;
+  wgrad_ws(Co, g.Kred, g.Mpos, &splits, &pps);
 #define M_(a, b_, c, d) launch_wgrad<a, b_, c, d>(dy, x, workspace, splits, pps, g, kcols, st);
   TVQ_DISPATCH_KIND(kind, replicate, M_)
 #undef M_
@@ -641,9 +1434,19 @@ extern "C" int tvq_convT2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t 
   // G = X (N = Ci channels at X's positions), In = dY gathered F-style (C = Co)
   ConvGeom g = make_geom((int)B, (int)Co, (int)H, (int)Wo, (int)Ci, (int)H, (int)Wi, (int)KH,
                          (int)KW, PH_OF(KH), PW_OF(KW), Co * KH * KW, KH * KW);
+  hipStream_t st = (hipStream_t)stream;
+  WHaloPlan pl;
+  if ((g_conv_halo & 2) && whalo_plan((int)B, (int)Co, (int)H, (int)Wo, (int)Ci, (int)H, (int)Wi,
+                                      (int)KH, (int)KW, (int)SW, PH_OF(KH), PW_OF(KW), g.Kred,
+                                      &pl)) {
+#define M_(a, b_, c, d) launch_wgrad_halo<a, b_, c, false>(x, dy, workspace, pl, st);
+    TVQ_DISPATCH_KIND(kind, 0, M_)
+#undef M_
+    wgrad_finish(workspace, pl.S, Ci, g.Kred, dw, nullptr, (int)accumulate, st);
+    return launch_status("tvq_convT2d_wgrad(halo)");
+  }
   int splits, pps;
   wgrad_ws(Ci, g.Kred, g.Mpos, &splits, &pps);
-  hipStream_t st = (hipStream_t)stream;
 #define M_(a, b_, c, d) launch_wgrad<a, b_, c, false>(x, dy, workspace, splits, pps, g, g.Kred, st);
   TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_

@@ -26,6 +26,15 @@ def _bias_grad(g, dev, sink=None):
     return None if sink is not None else out
 
 
+PACK_WEIGHTS = True  # tests flip this to cover the in-place (strided) weight reads
+
+
+def _wpack(w, c_red):
+    """Scratch for the tap-major weight repack; only the tap-major GEMM (reduction channels
+    a multiple of 16) benefits, the flat small-channel path reads the weight in place."""
+    return torch.empty_like(w) if PACK_WEIGHTS and c_red % 16 == 0 else None
+
+
 def _as4d(x):
     return x.unsqueeze(2) if x.dim() == 3 else x
 
@@ -44,7 +53,8 @@ class _Conv2d(torch.autograd.Function):
         seed = rng.seed_tensor(x.device) if drop_p > 0 else None
         off = rng.call_offset(site) if drop_p > 0 else 0
         call("tvq_conv2d_fwd", ptr(x4), B, Ci, H, Wi, ptr(w4), ptr(b), Co, KH, KW, SW,
-             int(replicate), ptr(y), ptr(res), float(drop_p), ptr(seed), off, stream_ptr())
+             int(replicate), ptr(y), ptr(res), float(drop_p), ptr(seed), off,
+             ptr(_wpack(w4, Ci)), stream_ptr())
         ctx.save_for_backward(x4, w4)
         ctx.cfg = (SW, replicate, drop_p, off, squeeze, b is not None, residual is not None,
                    w.dim())
@@ -73,7 +83,7 @@ class _Conv2d(torch.autograd.Function):
             wsz = value("tvq_conv2d_dgrad_workspace", B, Ci, H, Wi, KH, KW, int(replicate))
             ws = _ws(wsz, dev) if replicate else None
             call("tvq_conv2d_dgrad", ptr(gd), B, Co, H, Wo, ptr(w4), Ci, KH, KW, SW,
-                 int(replicate), ptr(dx), Wi, ptr(ws), s)
+                 int(replicate), ptr(dx), Wi, ptr(ws), ptr(_wpack(w4, Co)), s)
             if squeeze:
                 dx = dx.squeeze(2)
         need_w, need_b = ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]
@@ -112,7 +122,7 @@ class _ConvT2d(torch.autograd.Function):
         Wo = value("tvq_conv_out_width", Wi, KW, SW, 1)
         y = torch.empty((B, Co, H, Wo), device=x.device, dtype=torch.float32)
         call("tvq_convT2d_fwd", ptr(x), B, Ci, H, Wi, ptr(w), ptr(b), Co, KH, KW, SW, ptr(y), None,
-             stream_ptr())
+             ptr(_wpack(w, Ci)), stream_ptr())
         ctx.save_for_backward(x, w)
         ctx.SW = SW
         ctx.has_b = b is not None
@@ -131,7 +141,8 @@ class _ConvT2d(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            call("tvq_convT2d_dgrad", ptr(g), B, Co, H, Wo, ptr(w), Ci, KH, KW, SW, ptr(dx), Wi, s)
+            call("tvq_convT2d_dgrad", ptr(g), B, Co, H, Wo, ptr(w), Ci, KH, KW, SW, ptr(dx), Wi,
+                 ptr(_wpack(w, Co)), s)
         w_p, b_p = ctx.params
         if ctx.needs_input_grad[1]:
             sw = grad_sink(w_p)

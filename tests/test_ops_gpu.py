@@ -26,6 +26,21 @@ def _grads(fn, inputs):
     return outs, [t.grad for t in inputs], g
 
 
+@pytest.fixture
+def conv_path(monkeypatch):
+    """Select the conv engine: halo-tile kernel (default), staged GEMM with packed
+    weights, or staged GEMM reading the weights in place."""
+    from timevqvae.hip import conv as conv_mod
+    from timevqvae.hip._native import value
+
+    def select(path):
+        monkeypatch.setattr(conv_mod, "PACK_WEIGHTS", path != "gemm_raw")
+        value("tvq_conv_config", 3 if path == "halo" else 0)
+
+    yield select
+    value("tvq_conv_config", 3)
+
+
 def _run_both(fn_hip, fn_ref, shapes, cuda, seed=0):
     gen = torch.Generator().manual_seed(seed)
     cpu = [torch.randn(s, generator=gen).requires_grad_(True) for s in shapes]
@@ -44,8 +59,10 @@ def _run_both(fn_hip, fn_ref, shapes, cuda, seed=0):
     (4, 8, 8, 64, "res"), (2, 64, 128, 8, "res"), (2, 16, 128, 32, "res"), (3, 128, 16, 32, "res"),
     (2, 64, 128, 8, "proj"), (5, 3, 7, 33, "res"),
 ])
-def test_conv2d(B, Ci, Co, W, kind, cuda):
+@pytest.mark.parametrize("path", ["halo", "gemm", "gemm_raw"])
+def test_conv2d(B, Ci, Co, W, kind, path, cuda, conv_path):
     from timevqvae.hip.conv import conv2d
+    conv_path(path)
     if kind == "enc":
         KH, KW, SW, rep = 3, 4, 2, True
     elif kind == "res":
@@ -67,9 +84,12 @@ def test_conv2d(B, Ci, Co, W, kind, cuda):
         close(d[i].grad, c[i].grad, what=n)
 
 
-@pytest.mark.parametrize("B,Ci,Co,W", [(4, 64, 32, 8), (2, 8, 4, 64), (3, 4, 12, 128), (2, 12, 12, 256)])
-def test_conv_transpose2d(B, Ci, Co, W, cuda):
+@pytest.mark.parametrize("B,Ci,Co,W", [(4, 64, 32, 8), (2, 8, 4, 64), (3, 4, 12, 128), (2, 12, 12, 256),
+                                        (2, 128, 128, 16)])
+@pytest.mark.parametrize("path", ["halo", "gemm", "gemm_raw"])
+def test_conv_transpose2d(B, Ci, Co, W, path, cuda, conv_path):
     from timevqvae.hip.conv import conv_transpose2d
+    conv_path(path)
 
     def ref(x, w, b):
         return F.conv_transpose2d(x, w, b, stride=(1, 2), padding=(1, 1))
@@ -263,3 +283,30 @@ def test_adamw_matches_torch(cuda):
         od.step()
     for pc, pd in zip(ps_c, ps_d):
         torch.testing.assert_close(pd.detach().cpu(), pc.detach(), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("Ci,Co,W", [(16, 16, 32), (64, 64, 8), (8, 8, 64)])
+def test_conv_paths_same_dropout_mask(Ci, Co, W, cuda):
+    """The dropout mask is a function of (seed, offset, output index) only: the halo
+    kernel and the staged GEMM drop exactly the same elements."""
+    from timevqvae.hip._native import call, ptr, stream_ptr, value
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(5, Ci, 3, W, generator=gen).to(cuda)
+    w = torch.randn(Co, Ci, 3, 3, generator=gen).to(cuda) * 0.1
+    b = torch.randn(Co, generator=gen).to(cuda)
+    r = torch.randn(5, Co, 3, W, generator=gen).to(cuda)
+    seed = torch.tensor([1234], dtype=torch.int64, device=cuda)
+    outs = []
+    try:
+        for halo in (1, 0):
+            value("tvq_conv_config", halo)
+            y = torch.empty(5, Co, 3, W, device=cuda)
+            call("tvq_conv2d_fwd", ptr(x), 5, Ci, 3, W, ptr(w), ptr(b), Co, 3, 3, 1, 0, ptr(y),
+                 ptr(r), 0.25, ptr(seed), 77, None, stream_ptr())
+            outs.append(y)
+    finally:
+        value("tvq_conv_config", 3)
+    torch.cuda.synchronize()
+    m0, m1 = outs[0] == r, outs[1] == r
+    assert torch.equal(m0, m1)
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-5, atol=1e-5)
