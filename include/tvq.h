@@ -122,32 +122,34 @@ int tvq_istft_decode_bwd(const float* dy, int64_t B, int64_t C, int64_t W, int64
  * dropout (counter-based mask keyed by (*seed_ptr, offset) and the flat output
  * index: the device seed advances once per step so graph replays differ) and + residual
  * (ResBlock: proj(x) + Dropout(conv(..)), vq_vae.py:52,62).
- * wpack (nullable, weight-numel floats): scratch into which the weight is repacked
- * tap-major / output-channel-contiguous before the GEMM (coalesced operand loads);
- * NULL reads the weight in place. */
+ * workspace: floats sized by tvq_conv_workspace(op, ...); nullable for the forward ops and
+ * the non-replicate dgrads (then no weight repack and no split-K).  It holds the
+ * replicate-pad canvas (dgrad), the tap-major repacked weight and split-K partials. */
 int tvq_conv_out_width(int64_t Win, int64_t KW, int64_t SW, int64_t transposed);
-/* engine selection (process-wide): halo = 1 lets convs whose padded image and weight
- * panel fit in 64 KB of LDS run on the halo-tile kernel, 0 forces the staged GEMM;
- * < 0 only queries.  Returns the previous setting. */
+/* engine selection (process-wide) bits: 1 = halo-tile kernel for fwd/dgrad convs whose
+ * padded image and weight panel fit in 64 KB of LDS, 2 = halo-tile weight gradient;
+ * 0 forces the staged GEMMs; < 0 only queries.  Returns the previous setting. */
 int tvq_conv_config(int64_t halo);
+/* op: 0 conv2d fwd, 1 convT2d fwd, 2 conv2d dgrad, 3 convT2d dgrad, 4 conv2d wgrad,
+ * 5 convT2d wgrad; (Ci, Co, Wi) = the layer's input channels, output channels, input
+ * width.  Returns the workspace size in floats (>= 1), -1 for a bad op. */
+int64_t tvq_conv_workspace(int64_t op, int64_t B, int64_t Ci, int64_t H, int64_t Wi, int64_t Co,
+                           int64_t KH, int64_t KW, int64_t SW, int64_t replicate);
 int tvq_conv2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi, const float* w,
                    const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t SW,
                    int64_t replicate, float* y, const float* residual, float drop_p,
-                   const int64_t* seed_ptr, uint64_t offset, float* wpack, tvq_stream_t stream);
+                   const int64_t* seed_ptr, uint64_t offset, float* workspace,
+                   tvq_stream_t stream);
 int tvq_convT2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi, const float* w,
                     const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t SW, float* y,
-                    const float* residual, float* wpack, tvq_stream_t stream);
-int64_t tvq_conv2d_dgrad_workspace(int64_t B, int64_t Ci, int64_t H, int64_t Wi, int64_t KH,
-                                   int64_t KW, int64_t replicate);
+                    const float* residual, float* workspace, tvq_stream_t stream);
 int tvq_conv2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t Wo,
                      const float* w, int64_t Ci, int64_t KH, int64_t KW, int64_t SW,
                      int64_t replicate, float* dx, int64_t Wi, float* workspace,
-                     float* wpack, tvq_stream_t stream);
+                     tvq_stream_t stream);
 int tvq_convT2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t Wo,
                       const float* w, int64_t Ci, int64_t KH, int64_t KW, int64_t SW, float* dx,
-                      int64_t Wi, float* wpack, tvq_stream_t stream);
-int64_t tvq_conv_wgrad_workspace(int64_t N, int64_t C, int64_t KH, int64_t KW, int64_t B,
-                                 int64_t Hout, int64_t Wo);
+                      int64_t Wi, float* workspace, tvq_stream_t stream);
 /* weight gradient (+ the bias gradient sum dY into db when non-NULL, as an extra
  * ones-column of the same GEMM); splits over positions reduced in a fixed order */
 int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,

@@ -56,6 +56,21 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// q = n / d by one v_mul_hi_u32 with m = ceil(2^32 / d): exact while n * d < 2^32
+// (callers check that bound on the host); d == 1 is encoded as m = 0
+struct Div16 {
+  uint32_t d, m;
+};
+static inline Div16 make_div16(int64_t d) {
+  Div16 r;
+  r.d = (uint32_t)d;
+  r.m = (uint32_t)(((1ull << 32) + (uint64_t)d - 1) / (uint64_t)d);
+  return r;
+}
+__device__ __forceinline__ int div16(int n, const Div16& v) {
+  return v.m ? (int)__umulhi((uint32_t)n, v.m) : n;
+}
+
 __device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }

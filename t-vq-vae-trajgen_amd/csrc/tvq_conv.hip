@@ -273,7 +273,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const float* __restrict_
 template <int MODE, int KH, int KW, int SW, bool REPL, int TN, int TM, int WN, int WM, int BK>
 __global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__ in,
                                                       const float* __restrict__ wt,
-                                                      float* __restrict__ out, ConvGeom g, Epi e) {
+                                                      float* __restrict__ out, ConvGeom g, Epi e,
+                                                      int steps_per_split, int64_t zstride) {
+  // split-K (gridDim.z > 1): block z covers K-steps [z*sps, (z+1)*sps) and stores raw
+  // partial sums to out + z*zstride (the caller passes a slab and a raw Epi)
   constexpr int KK = KH * KW;
   constexpr int FN = TN / WN / 16;
   constexpr int FM = TM / WM / 16;
@@ -307,7 +310,9 @@ __global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__
   const int an = n0 + an_local;
   const float* wrow = wt + (int64_t)(an < g.N ? an : 0) * g.wsn;
   const int csteps = (g.C + BK - 1) / BK;
-  const int nsteps = KK * csteps;
+  const int kbeg = blockIdx.z * steps_per_split;
+  const int nsteps = min(KK * csteps, kbeg + steps_per_split);
+  out += (int64_t)blockIdx.z * zstride;
 
   float ra[A_PER], rb[B_PER];
   auto load_tile = [&](int step) {
@@ -357,8 +362,8 @@ __global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int r16 = lane & 15, g4 = lane >> 4;
-  load_tile(0);
-  for (int step = 0; step < nsteps; ++step) {
+  if (kbeg < nsteps) load_tile(kbeg);
+  for (int step = kbeg; step < nsteps; ++step) {
     __syncthreads();
     store_tile();
     __syncthreads();
@@ -602,21 +607,6 @@ static ConvGeom make_geom(int B, int C, int Hin, int Win, int N, int Hout, int W
 // The weight panel keeps the raw (c, kh, kw) column order, so it is a straight copy of
 // the weight rows.  KS = 4 splits K across the 4 waves when the image has <= 4 position
 // tiles (partials reduced through LDS).
-// q = n / d by one v_mul_hi_u32, exact while n * d < 2^32 (halo indices and divisors
-// are both < 2^16 here); d >= 2
-struct Div16 {
-  uint32_t d, m;
-};
-static Div16 make_div16(int d) {
-  Div16 r;
-  r.d = (uint32_t)d;
-  r.m = (uint32_t)(((1ull << 32) + d - 1) / d);
-  return r;
-}
-__device__ __forceinline__ int div16(int n, const Div16& v) {
-  return (int)__umulhi((uint32_t)n, v.m);
-}
-
 struct HaloGeom {
   Div16 dv_hw, dv_wp, dv_wo, dv_k;
   int C, Cp, Hin, Win, N, Hout, Wo;
@@ -1085,6 +1075,24 @@ static void launch_wgrad_halo(const float* G, const float* in, float* slab, cons
 #undef W_
 }
 
+// out[o] = epi(sum_z slab[z][o]) in split order; channel n = (o / HW) % N.  The dropout
+// mask depends on (seed, offset, o) only, so it matches the unsplit epilogue exactly.
+__global__ __launch_bounds__(256) void conv_splitk_epi_kernel(const float* __restrict__ slab,
+                                                             int splits, int n_out, int N,
+                                                             Div16 dhw, Epi e,
+                                                             float* __restrict__ out) {
+  const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
+  for (int o = blockIdx.x * 256 + threadIdx.x; o < n_out; o += gridDim.x * 256) {
+    float v = 0.f;
+#pragma unroll 4
+    for (int z = 0; z < splits; ++z) v += slab[(int64_t)z * n_out + o];
+    if (e.bias) v += e.bias[div16(o, dhw) % N];
+    if (e.drop_p > 0.f) v = uniform01(seed, (uint64_t)o) >= e.drop_p ? v * e.drop_scale : 0.f;
+    if (e.residual) v += e.residual[o];
+    out[o] = v;
+  }
+}
+
 // Repack a weight seen as (n, c, tap) with strides (wsn, wsc, 1) into [tap][c][n] so the
 // A-operand loads of a K-step read TN consecutive floats (one or two cache lines) instead
 // of TN rows a whole filter apart.
@@ -1114,33 +1122,73 @@ static const float* pack_weight(const float* wt, ConvGeom& g, int KK, float* ws,
   return ws;
 }
 
-template <int MODE, int KH, int KW, int SW, bool REPL, int BK>
-static void launch_tap(const float* in, const float* wt, float* out, const ConvGeom& g,
-                       const Epi& e, hipStream_t st) {
-  if (g.N <= 16) {
-    dim3 grid((g.Mpos + 255) / 256, (g.N + 15) / 16);
-    hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 16, 256, 1, 4, BK>), grid,
-                       dim3(256), 0, st, in, wt, out, g, e);
-  } else if (g.N <= 32) {
-    dim3 grid((g.Mpos + 127) / 128, (g.N + 31) / 32);
-    hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 32, 128, 2, 2, BK>), grid,
-                       dim3(256), 0, st, in, wt, out, g, e);
-  } else {
-    dim3 grid((g.Mpos + 127) / 128, (g.N + 63) / 64);
-    hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 64, 128, 2, 2, BK>), grid,
-                       dim3(256), 0, st, in, wt, out, g, e);
-  }
+static void tap_tile(int N, int* TN, int* TM) {
+  if (N <= 16) { *TN = 16; *TM = 256; }
+  else if (N <= 32) { *TN = 32; *TM = 128; }
+  else { *TN = 64; *TM = 128; }
 }
 
+// split-K factor for the tap-major GEMM: only when the grid is small and K is deep
+static int tap_splits(const ConvGeom& g, int KK, int* sps) {
+  const int BK = g.C % 32 == 0 ? 32 : 16;
+  int TN, TM;
+  tap_tile(g.N, &TN, &TM);
+  const int tiles = ((g.Mpos + TM - 1) / TM) * ((g.N + TN - 1) / TN);
+  const int ksteps = KK * ((g.C + BK - 1) / BK);
+  int s = 1;
+  if (g.C % 16 == 0 && tiles < 512 && ksteps >= 8) {
+    s = (1024 + tiles - 1) / tiles;
+    if (s > ksteps / 4) s = ksteps / 4;
+    if (s > 16) s = 16;
+    if (s < 1) s = 1;
+  }
+  const int per = (ksteps + s - 1) / s;
+  *sps = per;
+  return (ksteps + per - 1) / per;
+}
+
+template <int MODE, int KH, int KW, int SW, bool REPL, int BK>
+static void launch_tap(const float* in, const float* wt, float* out, const ConvGeom& g,
+                       const Epi& e, int splits, int sps, int64_t zstride, hipStream_t st) {
+  int TN, TM;
+  tap_tile(g.N, &TN, &TM);
+  dim3 grid((g.Mpos + TM - 1) / TM, (g.N + TN - 1) / TN, splits);
+  if (TN == 16)
+    hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 16, 256, 1, 4, BK>), grid,
+                       dim3(256), 0, st, in, wt, out, g, e, sps, zstride);
+  else if (TN == 32)
+    hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 32, 128, 2, 2, BK>), grid,
+                       dim3(256), 0, st, in, wt, out, g, e, sps, zstride);
+  else
+    hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 64, 128, 2, 2, BK>), grid,
+                       dim3(256), 0, st, in, wt, out, g, e, sps, zstride);
+}
+
+// staged GEMM; `slab` (nullable) enables split-K with splits*N*Mpos floats of partials
 template <int MODE, int KH, int KW, int SW, bool REPL>
 static void launch_gemm(const float* in, const float* wt, float* out, const ConvGeom& g,
-                        const Epi& e, hipStream_t st) {
-  if (g.C % 32 == 0) {
-    launch_tap<MODE, KH, KW, SW, REPL, 32>(in, wt, out, g, e, st);
-    return;
-  }
+                        const Epi& e, float* slab, hipStream_t st) {
   if (g.C % 16 == 0) {
-    launch_tap<MODE, KH, KW, SW, REPL, 16>(in, wt, out, g, e, st);
+    int sps;
+    const int splits = slab ? tap_splits(g, KH * KW, &sps) : 1;
+    if (!slab) sps = KH * KW * ((g.C + 31) / 16);  // >= all K-steps
+    if (splits > 1) {
+      const int64_t n_out = (int64_t)g.Mpos * g.N;
+      const Epi raw = {nullptr, nullptr, 0.f, 1.f, nullptr, 0};
+      if (g.C % 32 == 0)
+        launch_tap<MODE, KH, KW, SW, REPL, 32>(in, wt, slab, g, raw, splits, sps, n_out, st);
+      else
+        launch_tap<MODE, KH, KW, SW, REPL, 16>(in, wt, slab, g, raw, splits, sps, n_out, st);
+      int blocks = (int)((n_out + 255) / 256);
+      if (blocks > 8192) blocks = 8192;
+      hipLaunchKernelGGL(conv_splitk_epi_kernel, dim3(blocks), dim3(256), 0, st, slab, splits,
+                         (int)n_out, g.N, make_div16((int64_t)g.Hout * g.Wo), e, out);
+      return;
+    }
+    if (g.C % 32 == 0)
+      launch_tap<MODE, KH, KW, SW, REPL, 32>(in, wt, out, g, e, 1, sps, 0, st);
+    else
+      launch_tap<MODE, KH, KW, SW, REPL, 16>(in, wt, out, g, e, 1, sps, 0, st);
     return;
   }
   // small channel counts: flat (c, kh, kw) K order keeps the K-steps full
@@ -1162,8 +1210,9 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
 static int g_conv_halo = 3;  // tvq_conv_config bits: 1 = halo fwd/dgrad, 2 = halo wgrad
 
 // halo path when the image + weight panel fit in LDS, else the staged GEMM
+// workspace (nullable) = [packed weight N*C*KK][split-K slab]; see conv_gemm_ws
 template <int MODE, int KH, int KW, int SW, bool REPL>
-static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g, float* wpack,
+static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g, float* ws,
                         const Epi& e, hipStream_t st) {
   HaloPlan pl;
   const int oh = MODE == GATHER_F ? g.oph : KH - 1 - g.oph;
@@ -1173,8 +1222,20 @@ static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g
     launch_halo<MODE, KH, KW, SW, REPL>(in, wt, out, pl, g.B, e, st);
     return;
   }
-  wt = pack_weight(wt, g, KH * KW, wpack, st);
-  launch_gemm<MODE, KH, KW, SW, REPL>(in, wt, out, g, e, st);
+  float* slab = nullptr;
+  if (ws && g.C % 16 == 0) {
+    wt = pack_weight(wt, g, KH * KW, ws, st);
+    slab = ws + (int64_t)g.N * g.C * KH * KW;
+  }
+  launch_gemm<MODE, KH, KW, SW, REPL>(in, wt, out, g, e, slab, st);
+}
+
+// floats of workspace launch_conv may use for this geometry (pack + split-K slab)
+static int64_t conv_gemm_ws(const ConvGeom& g, int KK) {
+  if (g.C % 16 != 0) return 0;
+  int sps;
+  const int s = tap_splits(g, KK, &sps);
+  return (int64_t)g.N * g.C * KK + (s > 1 ? (int64_t)s * g.N * g.Mpos : 0);
 }
 
 template <int KH, int KW, int SW, bool REPL>
@@ -1253,22 +1314,60 @@ extern "C" int tvq_conv_out_width(int64_t Win, int64_t KW, int64_t SW, int64_t t
 #define PH_OF(KH) ((int)(KH) / 2)
 #define PW_OF(KW) (((int)(KW) - 1) / 2)
 
+// ---- geometry of each op as one F/T gather launch
+static ConvGeom geom_conv_fwd(int64_t B, int64_t Ci, int64_t H, int64_t Wi, int64_t Co, int64_t KH,
+                              int64_t KW, int64_t SW) {
+  const int Wo = tvq_conv_out_width(Wi, KW, SW, 0);
+  return make_geom((int)B, (int)Ci, (int)H, (int)Wi, (int)Co, (int)H, Wo, (int)KH, (int)KW,
+                   PH_OF(KH), PW_OF(KW), Ci * KH * KW, KH * KW);
+}
+// ConvTranspose2d weight (Ci, Co, KH, KW): reduction channel c = ci (first dim)
+static ConvGeom geom_convT_fwd(int64_t B, int64_t Ci, int64_t H, int64_t Wi, int64_t Co,
+                               int64_t KH, int64_t KW, int64_t SW) {
+  const int Wo = tvq_conv_out_width(Wi, KW, SW, 1);
+  return make_geom((int)B, (int)Ci, (int)H, (int)Wi, (int)Co, (int)H, Wo, (int)KH, (int)KW,
+                   PH_OF(KH), PW_OF(KW), KH * KW, Co * KH * KW);
+}
+// conv weight (Co, Ci, KH, KW): reduction c = co, output channel n = ci.  Replicate pad:
+// gradient of the padded canvas (H+2PH, Wi+2PW) with zero offsets, folded afterwards.
+static ConvGeom geom_conv_dgrad(int64_t B, int64_t Ci, int64_t H, int64_t Wi, int64_t Co,
+                                int64_t KH, int64_t KW, int64_t SW, int64_t replicate) {
+  const int Wo = tvq_conv_out_width(Wi, KW, SW, 0);
+  if (!replicate)
+    return make_geom((int)B, (int)Co, (int)H, Wo, (int)Ci, (int)H, (int)Wi, (int)KH, (int)KW,
+                     PH_OF(KH), PW_OF(KW), KH * KW, Ci * KH * KW);
+  return make_geom((int)B, (int)Co, (int)H, Wo, (int)Ci, (int)H + 2 * PH_OF(KH),
+                   (int)Wi + 2 * PW_OF(KW), (int)KH, (int)KW, 0, 0, KH * KW, Ci * KH * KW);
+}
+// F-gather of dY with weight (Ci, Co, KH, KW) indexed (n = ci, c = co)
+static ConvGeom geom_convT_dgrad(int64_t B, int64_t Ci, int64_t H, int64_t Wi, int64_t Co,
+                                 int64_t KH, int64_t KW, int64_t SW) {
+  const int Wo = tvq_conv_out_width(Wi, KW, SW, 1);
+  return make_geom((int)B, (int)Co, (int)H, Wo, (int)Ci, (int)H, (int)Wi, (int)KH, (int)KW,
+                   PH_OF(KH), PW_OF(KW), Co * KH * KW, KH * KW);
+}
+
+static int64_t canvas_floats(const ConvGeom& g) { return (int64_t)g.B * g.N * g.Hout * g.Wo; }
+
+static bool geom_ok(const ConvGeom& g) {
+  return g.Wo > 0 && g.Win > 0 && (int64_t)g.B * g.Hout * g.Wo < (1 << 30) &&
+         (int64_t)g.B * g.N * g.Hout * g.Wo < (1ll << 31);
+}
+
 extern "C" int tvq_conv2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
                               const float* w, const float* bias, int64_t Co, int64_t KH,
                               int64_t KW, int64_t SW, int64_t replicate, float* y,
                               const float* residual, float drop_p, const int64_t* seed_ptr,
-                              uint64_t offset, float* wpack, tvq_stream_t stream) {
+                              uint64_t offset, float* workspace, tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && w && y && B > 0 && Ci > 0 && Co > 0, "tvq_conv2d_fwd: bad arguments");
   const int kind = kind_of((int)KH, (int)KW, (int)SW);
   TVQ_CHECK_ARG(kind >= 0, "tvq_conv2d_fwd: unsupported kernel %lldx%lld s%lld", (long long)KH,
                 (long long)KW, (long long)SW);
-  const int Wo = tvq_conv_out_width(Wi, KW, SW, 0);
-  TVQ_CHECK_ARG(Wo > 0 && B * H * Wo < (1 << 30), "tvq_conv2d_fwd: bad geometry");
-  ConvGeom g = make_geom((int)B, (int)Ci, (int)H, (int)Wi, (int)Co, (int)H, Wo, (int)KH, (int)KW,
-                         PH_OF(KH), PW_OF(KW), Ci * KH * KW, KH * KW);
+  ConvGeom g = geom_conv_fwd(B, Ci, H, Wi, Co, KH, KW, SW);
+  TVQ_CHECK_ARG(geom_ok(g), "tvq_conv2d_fwd: bad geometry");
   Epi e = make_epi(bias, residual, drop_p, seed_ptr, offset);
   hipStream_t st = (hipStream_t)stream;
-#define M_(a, b_, c, d) launch_conv<GATHER_F, a, b_, c, d>(x, w, y, g, wpack, e, st);
+#define M_(a, b_, c, d) launch_conv<GATHER_F, a, b_, c, d>(x, w, y, g, workspace, e, st);
   TVQ_DISPATCH_KIND(kind, replicate, M_)
 #undef M_
   return launch_status("tvq_conv2d_fwd");
@@ -1277,77 +1376,64 @@ extern "C" int tvq_conv2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, 
 extern "C" int tvq_convT2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
                                const float* w, const float* bias, int64_t Co, int64_t KH,
                                int64_t KW, int64_t SW, float* y, const float* residual,
-                               float* wpack, tvq_stream_t stream) {
+                               float* workspace, tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && w && y && B > 0 && Ci > 0 && Co > 0, "tvq_convT2d_fwd: bad arguments");
   const int kind = kind_of((int)KH, (int)KW, (int)SW);
   TVQ_CHECK_ARG(kind >= 0, "tvq_convT2d_fwd: unsupported kernel");
-  const int Wo = tvq_conv_out_width(Wi, KW, SW, 1);
-  // ConvTranspose2d weight (Ci, Co, KH, KW): reduction channel c = ci (first dim)
-  ConvGeom g = make_geom((int)B, (int)Ci, (int)H, (int)Wi, (int)Co, (int)H, Wo, (int)KH, (int)KW,
-                         PH_OF(KH), PW_OF(KW), KH * KW, Co * KH * KW);
+  ConvGeom g = geom_convT_fwd(B, Ci, H, Wi, Co, KH, KW, SW);
+  TVQ_CHECK_ARG(geom_ok(g), "tvq_convT2d_fwd: bad geometry");
   Epi e = make_epi(bias, residual, 0.f, nullptr, 0);
   hipStream_t st = (hipStream_t)stream;
-#define M_(a, b_, c, d) launch_conv<GATHER_T, a, b_, c, false>(x, w, y, g, wpack, e, st);
+#define M_(a, b_, c, d) launch_conv<GATHER_T, a, b_, c, false>(x, w, y, g, workspace, e, st);
   TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
   return launch_status("tvq_convT2d_fwd");
 }
 
-extern "C" int64_t tvq_conv2d_dgrad_workspace(int64_t B, int64_t Ci, int64_t H, int64_t Wi,
-                                              int64_t KH, int64_t KW, int64_t replicate) {
-  if (!replicate) return 0;
-  return B * Ci * (H + 2 * PH_OF(KH)) * (Wi + 2 * PW_OF(KW));
-}
-
+// workspace: [replicate canvas][pack + split-K slab]; required when replicate
 extern "C" int tvq_conv2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t Wo,
                                 const float* w, int64_t Ci, int64_t KH, int64_t KW, int64_t SW,
                                 int64_t replicate, float* dx, int64_t Wi, float* workspace,
-                                float* wpack, tvq_stream_t stream) {
+                                tvq_stream_t stream) {
   TVQ_CHECK_ARG(dy && w && dx && B > 0 && Ci > 0 && Co > 0, "tvq_conv2d_dgrad: bad arguments");
   const int kind = kind_of((int)KH, (int)KW, (int)SW);
   TVQ_CHECK_ARG(kind >= 0, "tvq_conv2d_dgrad: unsupported kernel");
   TVQ_CHECK_ARG(tvq_conv_out_width(Wi, KW, SW, 0) == Wo, "tvq_conv2d_dgrad: Wi/Wo mismatch");
   hipStream_t st = (hipStream_t)stream;
   Epi e = make_epi(nullptr, nullptr, 0.f, nullptr, 0);
-  // conv weight (Co, Ci, KH, KW): reduction c = co (first dim), output channel n = ci
+  ConvGeom g = geom_conv_dgrad(B, Ci, H, Wi, Co, KH, KW, SW, replicate);
+  TVQ_CHECK_ARG(geom_ok(g), "tvq_conv2d_dgrad: bad geometry");
   if (!replicate) {
-    ConvGeom g = make_geom((int)B, (int)Co, (int)H, (int)Wo, (int)Ci, (int)H, (int)Wi, (int)KH,
-                           (int)KW, PH_OF(KH), PW_OF(KW), KH * KW, Ci * KH * KW);
-#define M_(a, b_, c, d) launch_conv<GATHER_T, a, b_, c, false>(dy, w, dx, g, wpack, e, st);
+#define M_(a, b_, c, d) launch_conv<GATHER_T, a, b_, c, false>(dy, w, dx, g, workspace, e, st);
     TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
     return launch_status("tvq_conv2d_dgrad");
   }
-  // replicate pad: gradient of the padded canvas (H+2PH, Wi+2PW) with zero offsets,
-  // then fold the pad rows/columns onto the edges.
   TVQ_CHECK_ARG(workspace, "tvq_conv2d_dgrad: replicate needs a workspace");
-  const int Hp = (int)H + 2 * PH_OF(KH), Wp = (int)Wi + 2 * PW_OF(KW);
-  ConvGeom g = make_geom((int)B, (int)Co, (int)H, (int)Wo, (int)Ci, Hp, Wp, (int)KH, (int)KW, 0, 0,
-                         KH * KW, Ci * KH * KW);
-#define M_(a, b_, c, d) \
-  launch_conv<GATHER_T, a, b_, c, false>(dy, w, workspace, g, wpack, e, st);
+  float* canvas = workspace;
+  float* rest = workspace + canvas_floats(g);
+#define M_(a, b_, c, d) launch_conv<GATHER_T, a, b_, c, false>(dy, w, canvas, g, rest, e, st);
   TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
   const int64_t tot = B * Ci * H * Wi;
   const int blocks = (int)((tot + 255) / 256 < 8192 ? (tot + 255) / 256 : 8192);
-  hipLaunchKernelGGL(replicate_fold_kernel, dim3(blocks), dim3(256), 0, st, workspace, (int)B,
+  hipLaunchKernelGGL(replicate_fold_kernel, dim3(blocks), dim3(256), 0, st, canvas, (int)B,
                      (int)Ci, (int)H, (int)Wi, PH_OF(KH), PW_OF(KW), dx);
   return launch_status("tvq_conv2d_dgrad(replicate)");
 }
 
 extern "C" int tvq_convT2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t Wo,
                                  const float* w, int64_t Ci, int64_t KH, int64_t KW, int64_t SW,
-                                 float* dx, int64_t Wi, float* wpack, tvq_stream_t stream) {
+                                 float* dx, int64_t Wi, float* workspace, tvq_stream_t stream) {
   TVQ_CHECK_ARG(dy && w && dx && B > 0 && Ci > 0 && Co > 0, "tvq_convT2d_dgrad: bad arguments");
   const int kind = kind_of((int)KH, (int)KW, (int)SW);
   TVQ_CHECK_ARG(kind >= 0, "tvq_convT2d_dgrad: unsupported kernel");
   TVQ_CHECK_ARG(tvq_conv_out_width(Wi, KW, SW, 1) == Wo, "tvq_convT2d_dgrad: Wi/Wo mismatch");
-  // F-gather of dY with weight (Ci, Co, KH, KW) indexed (n = ci, c = co)
-  ConvGeom g = make_geom((int)B, (int)Co, (int)H, (int)Wo, (int)Ci, (int)H, (int)Wi, (int)KH,
-                         (int)KW, PH_OF(KH), PW_OF(KW), Co * KH * KW, KH * KW);
+  ConvGeom g = geom_convT_dgrad(B, Ci, H, Wi, Co, KH, KW, SW);
+  TVQ_CHECK_ARG(geom_ok(g), "tvq_convT2d_dgrad: bad geometry");
   Epi e = make_epi(nullptr, nullptr, 0.f, nullptr, 0);
   hipStream_t st = (hipStream_t)stream;
-#define M_(a, b_, c, d) launch_conv<GATHER_F, a, b_, c, false>(dy, w, dx, g, wpack, e, st);
+#define M_(a, b_, c, d) launch_conv<GATHER_F, a, b_, c, false>(dy, w, dx, g, workspace, e, st);
   TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
   return launch_status("tvq_convT2d_dgrad");
@@ -1376,11 +1462,37 @@ static int64_t whalo_ws(int64_t N, int64_t C, int64_t KH, int64_t KW, int64_t B)
   return (int64_t)S * N * kc + reduce_rows_scratch(S, N * kc);
 }
 
-extern "C" int64_t tvq_conv_wgrad_workspace(int64_t N, int64_t C, int64_t KH, int64_t KW,
-                                            int64_t B, int64_t Hout, int64_t Wo) {
+static int64_t conv_wgrad_ws(int64_t N, int64_t C, int64_t KH, int64_t KW, int64_t B,
+                             int64_t Hout, int64_t Wo) {
   const int64_t a = wgrad_ws(N, C * KH * KW, B * Hout * Wo, nullptr, nullptr);
   const int64_t h = whalo_ws(N, C, KH, KW, B);
   return a > h ? a : h;
+}
+
+// op: 0 conv2d fwd, 1 convT2d fwd, 2 conv2d dgrad, 3 convT2d dgrad, 4 conv2d wgrad,
+// 5 convT2d wgrad.  (Ci, Co, Wi) are the layer's input channels, output channels and
+// input width.  Returns floats (>= 1).
+extern "C" int64_t tvq_conv_workspace(int64_t op, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
+                                      int64_t Co, int64_t KH, int64_t KW, int64_t SW,
+                                      int64_t replicate) {
+  int64_t r = 0;
+  const int KK = (int)(KH * KW);
+  switch (op) {
+    case 0: r = conv_gemm_ws(geom_conv_fwd(B, Ci, H, Wi, Co, KH, KW, SW), KK); break;
+    case 1: r = conv_gemm_ws(geom_convT_fwd(B, Ci, H, Wi, Co, KH, KW, SW), KK); break;
+    case 2: {
+      const ConvGeom g = geom_conv_dgrad(B, Ci, H, Wi, Co, KH, KW, SW, replicate);
+      r = (replicate ? canvas_floats(g) : 0) + conv_gemm_ws(g, KK);
+      break;
+    }
+    case 3: r = conv_gemm_ws(geom_convT_dgrad(B, Ci, H, Wi, Co, KH, KW, SW), KK); break;
+    case 4:
+      r = conv_wgrad_ws(Co, Ci, KH, KW, B, H, tvq_conv_out_width(Wi, KW, SW, 0));
+      break;
+    case 5: r = conv_wgrad_ws(Ci, Co, KH, KW, B, H, Wi); break;
+    default: return -1;
+  }
+  return r > 0 ? r : 1;
 }
 
 static void wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, float* dw,

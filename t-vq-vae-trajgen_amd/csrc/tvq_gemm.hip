@@ -119,24 +119,86 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       }
     }
   }
-  // C layout: acc[i][j][r] -> row m0 + (wm*FM+i)*16 + 4*g4 + r, col n0 + (wn*FN+j)*16 + r16
+  // C layout: acc[i][j][r] -> row m0 + (wm*FM+i)*16 + 4*g4 + r, col n0 + (wn*FN+j)*16 + r16.
+  // Every epilogue load is unconditional (clamped indices) so they issue together.
+  int ncol[FN], ncl[FN];
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int j = 0; j < FN; ++j) {
+    ncol[j] = n0 + (wn * FN + j) * 16 + r16;
+    ncl[j] = min(ncol[j], g.N - 1);
+  }
+  if (g.slab) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + (wm * FM + i) * 16 + 4 * g4 + r;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          if (m < g.M && ncol[j] < g.N)
+            g.slab[((int64_t)blockIdx.z * g.M + m) * g.N + ncol[j]] = acc[i][j][r];
+      }
+    return;
+  }
+  float bv[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bv[j] = g.bias ? g.bias[ncl[j]] : 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    int mrow[4], mcl[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int m = m0 + (wm * FM + i) * 16 + 4 * g4 + r;
-      if (m >= g.M) continue;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + (wn * FN + j) * 16 + r16;
-        if (n >= g.N) continue;
-        if (g.slab) {
-          g.slab[((int64_t)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][r];
-        } else {
-          g.C[(int64_t)m * g.ldc + n] = apply_epi(g, m, n, acc[i][j][r]);
-        }
-      }
+      mrow[r] = m0 + (wm * FM + i) * 16 + 4 * g4 + r;
+      mcl[r] = min(mrow[r], g.M - 1);
     }
+    float v[4][FN];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) v[r][j] = acc[i][j][r] * g.alpha + bv[j];
+    if (g.pre) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          if (mrow[r] < g.M && ncol[j] < g.N) g.pre[(int64_t)mrow[r] * g.ldc + ncol[j]] = v[r][j];
+    }
+    if (g.act == 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) v[r][j] = gelu_erf(v[r][j]);
+    }
+    if (g.R) {
+      float rv[4][FN];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t rr = (int64_t)(g.rmod > 0 ? mcl[r] % g.rmod : mcl[r]) * g.ldr;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) rv[r][j] = g.R[rr + ncl[j]];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) v[r][j] += rv[r][j];
+    }
+    if (g.accumulate) {
+      float cv[4][FN];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) cv[r][j] = g.C[(int64_t)mcl[r] * g.ldc + ncl[j]];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) v[r][j] += cv[r][j];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        if (mrow[r] < g.M && ncol[j] < g.N) g.C[(int64_t)mrow[r] * g.ldc + ncol[j]] = v[r][j];
+  }
 }
 
 __global__ void gemm_splitk_reduce_kernel(GemmArgs g, int splits) {
@@ -144,6 +206,7 @@ __global__ void gemm_splitk_reduce_kernel(GemmArgs g, int splits) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot;
        i += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
+#pragma unroll 8
     for (int z = 0; z < splits; ++z) s += g.slab[(int64_t)z * tot + i];
     const int m = (int)(i / g.N), n = (int)(i - (int64_t)m * g.N);
     g.C[(int64_t)m * g.ldc + n] = apply_epi(g, m, n, s);

@@ -12,11 +12,26 @@
 
 namespace tvq {
 
+// per-channel reductions: chunks of ~2048 elements (8 per thread) so each thread has
+// all its loads in flight at once and C*chunks blocks fill the chip
+static constexpr int NU = 8;
 static int bn_chunks(int64_t B, int64_t HW) {
-  int64_t c = (B * HW + 4095) / 4096;
-  if (c > 64) c = 64;
+  int64_t c = (B * HW + 256 * NU - 1) / (256 * NU);
+  if (c > 512) c = 512;
   if (c < 1) c = 1;
   return (int)c;
+}
+
+// element i of channel c's (b, p) sequence -> flat NCHW offset; i*HW < 2^32 checked on host
+__device__ __forceinline__ int64_t chan_off(int i, int C, int c, int HW, const Div16& dhw) {
+  const int b = div16(i, dhw);
+  return ((int64_t)b * C + c) * HW + (i - b * HW);
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
 }
 
 __device__ __forceinline__ double block_sum_d(double v, double* red) {
@@ -33,19 +48,29 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
 
 // partial [c][chunk][2] = (sum x, sum x^2)
 __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __restrict__ x, int B,
-                                                               int C, int HW, int chunks,
+                                                               int C, int HW, Div16 dhw,
+                                                               int chunks,
                                                                double* __restrict__ part) {
   __shared__ double red[4];
   const int c = blockIdx.x, ch = blockIdx.y;
-  const int64_t tot = (int64_t)B * HW;
-  const int64_t per = (tot + chunks - 1) / chunks;
-  const int64_t lo = ch * per, hi = min(tot, lo + per);
+  const int tot = B * HW;
+  const int per = (tot + chunks - 1) / chunks;
+  const int lo = ch * per, hi = min(tot, lo + per);
   double s1 = 0.0, s2 = 0.0;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
-    const int64_t b = i / HW, p = i - b * HW;
-    const double v = x[(b * C + c) * HW + p];
-    s1 += v;
-    s2 += v * v;
+  for (int i0 = lo + threadIdx.x; i0 < hi; i0 += 256 * NU) {
+    float v[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = i0 + u * 256;
+      v[u] = x[chan_off(i < hi ? i : lo, C, c, HW, dhw)];
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      if (i0 + u * 256 < hi) {
+        s1 += (double)v[u];
+        s2 += (double)v[u] * (double)v[u];
+      }
+    }
   }
   s1 = block_sum_d(s1, red);
   s2 = block_sum_d(s2, red);
@@ -55,20 +80,23 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __re
   }
 }
 
-__global__ void bn_stats_final_kernel(const double* __restrict__ part, int C, int chunks, int64_t N,
-                                      float eps, float momentum, const float* __restrict__ w,
-                                      const float* __restrict__ b, float* __restrict__ rmean,
-                                      float* __restrict__ rvar, int64_t* __restrict__ nbt,
-                                      float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                      float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && nbt) nbt[0] += 1;
-  if (c >= C) return;
+// one wave per channel: lanes stride the chunk partials, fixed xor-tree combine
+__global__ __launch_bounds__(64) void bn_stats_final_kernel(
+    const double* __restrict__ part, int C, int chunks, int64_t N, float eps, float momentum,
+    const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ rmean,
+    float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
+    float* __restrict__ save_invstd, float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (c == 0 && lane == 0 && nbt) nbt[0] += 1;
   double s1 = 0.0, s2 = 0.0;
-  for (int i = 0; i < chunks; ++i) {
+  for (int i = lane; i < chunks; i += 64) {
     s1 += part[((int64_t)c * chunks + i) * 2 + 0];
     s2 += part[((int64_t)c * chunks + i) * 2 + 1];
   }
+  s1 = wave_sum_d(s1);
+  s2 = wave_sum_d(s2);
+  if (lane != 0) return;
   const double mean = s1 / (double)N;
   double var = s2 / (double)N - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -103,54 +131,61 @@ __device__ __forceinline__ float snake_fwd(float s, float a) {
   return s + inv * (sn * sn);
 }
 
-// y = snake?(x*scale[c] + shift[c]);  grid (chunks-of-HW, B*C)
-__global__ __launch_bounds__(256) void affine_snake_kernel(const float* __restrict__ x, int C,
-                                                           int HW, const float* __restrict__ scale,
+// y = snake?(x*scale[c] + shift[c]) over the flat NCHW tensor; channel = (i / HW) % C
+__global__ __launch_bounds__(256) void affine_snake_kernel(const float* __restrict__ x, int n,
+                                                           int C, int HW, Div16 dhw,
+                                                           const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
                                                            const float* __restrict__ a,
                                                            float* __restrict__ y) {
-  const int bc = blockIdx.y;
-  const int c = bc % C;
-  const float sc = scale ? scale[c] : 1.f, sh = shift ? shift[c] : 0.f;
-  const float av = a ? a[c] : 0.f;
-  const int64_t base = (int64_t)bc * HW;
-  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
-    float s = fmaf(x[base + p], sc, sh);
-    if (a) s = snake_fwd(s, av);
-    y[base + p] = s;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int c = div16(i, dhw) % C;
+    const float sc = scale ? scale[c] : 1.f, sh = shift ? shift[c] : 0.f;
+    float s = fmaf(x[i], sc, sh);
+    if (a) s = snake_fwd(s, a[c]);
+    y[i] = s;
   }
 }
 
 // backward partials: [c][chunk][3] = (sum ds, sum ds*xhat, sum da-term)
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
-    const float* __restrict__ dy, const float* __restrict__ x, int B, int C, int HW, int chunks,
-    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ dy, const float* __restrict__ x, int B, int C, int HW, Div16 dhw,
+    int chunks, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ a,
     double* __restrict__ part) {
   __shared__ double red[4];
   const int c = blockIdx.x, ch = blockIdx.y;
-  const int64_t tot = (int64_t)B * HW;
-  const int64_t per = (tot + chunks - 1) / chunks;
-  const int64_t lo = ch * per, hi = min(tot, lo + per);
+  const int tot = B * HW;
+  const int per = (tot + chunks - 1) / chunks;
+  const int lo = ch * per, hi = min(tot, lo + per);
   const float mu = mean[c], is = invstd[c], sc = scale[c], sh = shift[c];
   const float av = a ? a[c] : 1.f, inv_a = 1.0f / av;
   double s_ds = 0.0, s_dsx = 0.0, s_da = 0.0;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
-    const int64_t b = i / HW, p = i - b * HW;
-    const int64_t o = (b * C + c) * HW + p;
-    const float xv = x[o], g = dy[o];
-    float ds = g;
-    if (a) {
-      const float s = fmaf(xv, sc, sh);
-      float sn, cs;
-      sincosf(av * s, &sn, &cs);
-      const float t = 2.0f * sn * cs;
-      ds = g + g * inv_a * t * av;
-      s_da += (double)(g * inv_a * t * s) - (double)(g * (sn * sn) * inv_a * inv_a);
+  for (int i0 = lo + threadIdx.x; i0 < hi; i0 += 256 * NU) {
+    float xv[NU], g[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = i0 + u * 256;
+      const int64_t o = chan_off(i < hi ? i : lo, C, c, HW, dhw);
+      xv[u] = x[o];
+      g[u] = dy[o];
     }
-    const float xhat = (xv - mu) * is;
-    s_ds += ds;
-    s_dsx += (double)ds * xhat;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      if (i0 + u * 256 >= hi) continue;
+      float ds = g[u];
+      if (a) {
+        const float s = fmaf(xv[u], sc, sh);
+        float sn, cs;
+        sincosf(av * s, &sn, &cs);
+        const float t = 2.0f * sn * cs;
+        ds = g[u] + g[u] * inv_a * t * av;
+        s_da += (double)(g[u] * inv_a * t * s) - (double)(g[u] * (sn * sn) * inv_a * inv_a);
+      }
+      const float xhat = (xv[u] - mu) * is;
+      s_ds += ds;
+      s_dsx += (double)ds * xhat;
+    }
   }
   s_ds = block_sum_d(s_ds, red);
   s_dsx = block_sum_d(s_dsx, red);
@@ -163,20 +198,26 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
   }
 }
 
-// coef[c][0] = sum ds, coef[c][1] = sum ds*xhat ; parameter grads
-__global__ void bn_bwd_final_kernel(const double* __restrict__ part, int C, int chunks,
-                                    float* __restrict__ coef, float* __restrict__ dw,
-                                    float* __restrict__ db, float* __restrict__ da,
-                                    int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// coef[c][0] = sum ds, coef[c][1] = sum ds*xhat ; parameter grads.  One wave per channel.
+__global__ __launch_bounds__(64) void bn_bwd_final_kernel(const double* __restrict__ part, int C,
+                                                          int chunks, float* __restrict__ coef,
+                                                          float* __restrict__ dw,
+                                                          float* __restrict__ db,
+                                                          float* __restrict__ da,
+                                                          int accumulate) {
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  for (int i = 0; i < chunks; ++i) {
+  for (int i = lane; i < chunks; i += 64) {
     const double* pp = part + ((int64_t)c * chunks + i) * 3;
     s0 += pp[0];
     s1 += pp[1];
     s2 += pp[2];
   }
+  s0 = wave_sum_d(s0);
+  s1 = wave_sum_d(s1);
+  s2 = wave_sum_d(s2);
+  if (lane != 0) return;
   coef[2 * c] = (float)s0;
   coef[2 * c + 1] = (float)s1;
   if (dw) dw[c] = accumulate ? dw[c] + (float)s1 : (float)s1;
@@ -184,80 +225,87 @@ __global__ void bn_bwd_final_kernel(const double* __restrict__ part, int C, int 
   if (da) da[c] = accumulate ? da[c] + (float)s2 : (float)s2;
 }
 
-// dx = w*invstd/N * (N*ds - sum ds - xhat * sum ds*xhat)
+// dx = w*invstd/N * (N*ds - sum ds - xhat * sum ds*xhat), flat over NCHW
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
-    const float* __restrict__ dy, const float* __restrict__ x, int C, int HW, int64_t N,
-    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ dy, const float* __restrict__ x, int n, int C, int HW, Div16 dhw,
+    int64_t N, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ w, const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ a, const float* __restrict__ coef, float* __restrict__ dx) {
-  const int bc = blockIdx.y;
-  const int c = bc % C;
-  const float mu = mean[c], is = invstd[c], sc = scale[c], sh = shift[c];
-  const float wc = w ? w[c] : 1.f;
-  const float av = a ? a[c] : 1.f, inv_a = 1.0f / av;
   const float invN = 1.0f / (float)N;
-  const float mds = coef[2 * c] * invN, mdsx = coef[2 * c + 1] * invN;
-  const float k = wc * is;
-  const int64_t base = (int64_t)bc * HW;
-  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
-    const float xv = x[base + p], g = dy[base + p];
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int c = div16(i, dhw) % C;
+    const float mu = mean[c], is = invstd[c], sc = scale[c], sh = shift[c];
+    const float wc = w ? w[c] : 1.f;
+    const float mds = coef[2 * c] * invN, mdsx = coef[2 * c + 1] * invN;
+    const float xv = x[i], g = dy[i];
     float ds = g;
     if (a) {
+      const float av = a[c], inv_a = 1.0f / av;
       const float s = fmaf(xv, sc, sh);
       float sn, cs;
       sincosf(av * s, &sn, &cs);
       ds = g + g * inv_a * (2.0f * sn * cs) * av;
     }
     const float xhat = (xv - mu) * is;
-    dx[base + p] = k * (ds - mds - xhat * mdsx);
+    dx[i] = wc * is * (ds - mds - xhat * mdsx);
   }
 }
 
-__global__ __launch_bounds__(256) void snake_fwd_kernel(const float* __restrict__ x, int C, int HW,
+__global__ __launch_bounds__(256) void snake_fwd_kernel(const float* __restrict__ x, int n, int C,
+                                                        int HW, Div16 dhw,
                                                         const float* __restrict__ a,
                                                         float* __restrict__ y) {
-  const int bc = blockIdx.y;
-  const float av = a[bc % C];
-  const int64_t base = (int64_t)bc * HW;
-  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256)
-    y[base + p] = snake_fwd(x[base + p], av);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    y[i] = snake_fwd(x[i], a[div16(i, dhw) % C]);
 }
 
 // dx (elementwise) and per-(channel, chunk) partials of da
 __global__ __launch_bounds__(256) void snake_bwd_kernel(const float* __restrict__ dy,
                                                         const float* __restrict__ x, int B, int C,
-                                                        int HW, int chunks,
+                                                        int HW, Div16 dhw, int chunks,
                                                         const float* __restrict__ a,
                                                         float* __restrict__ dx,
                                                         double* __restrict__ part) {
   __shared__ double red[4];
   const int c = blockIdx.x, ch = blockIdx.y;
-  const int64_t tot = (int64_t)B * HW;
-  const int64_t per = (tot + chunks - 1) / chunks;
-  const int64_t lo = ch * per, hi = min(tot, lo + per);
+  const int tot = B * HW;
+  const int per = (tot + chunks - 1) / chunks;
+  const int lo = ch * per, hi = min(tot, lo + per);
   const float av = a[c], inv_a = 1.0f / av;
   double s_da = 0.0;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
-    const int64_t b = i / HW, p = i - b * HW;
-    const int64_t o = (b * C + c) * HW + p;
-    const float xv = x[o], g = dy[o];
-    float sn, cs;
-    sincosf(av * xv, &sn, &cs);
-    const float t = 2.0f * sn * cs;
-    dx[o] = g + g * inv_a * t * av;
-    s_da += (double)(g * inv_a * t * xv) - (double)(g * (sn * sn) * inv_a * inv_a);
+  for (int i0 = lo + threadIdx.x; i0 < hi; i0 += 256 * NU) {
+    float xv[NU], g[NU];
+    int64_t o[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = i0 + u * 256;
+      o[u] = chan_off(i < hi ? i : lo, C, c, HW, dhw);
+      xv[u] = x[o[u]];
+      g[u] = dy[o[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      if (i0 + u * 256 >= hi) continue;
+      float sn, cs;
+      sincosf(av * xv[u], &sn, &cs);
+      const float t = 2.0f * sn * cs;
+      dx[o[u]] = g[u] + g[u] * inv_a * t * av;
+      s_da += (double)(g[u] * inv_a * t * xv[u]) - (double)(g[u] * (sn * sn) * inv_a * inv_a);
+    }
   }
   s_da = block_sum_d(s_da, red);
   if (threadIdx.x == 0) part[(int64_t)c * chunks + ch] = s_da;
 }
 
-__global__ void snake_bwd_final_kernel(const double* __restrict__ part, int C, int chunks,
-                                       float* __restrict__ da, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(64) void snake_bwd_final_kernel(const double* __restrict__ part,
+                                                             int C, int chunks,
+                                                             float* __restrict__ da,
+                                                             int accumulate) {
+  const int c = blockIdx.x;
   double s = 0.0;
-  for (int i = 0; i < chunks; ++i) s += part[(int64_t)c * chunks + i];
-  da[c] = accumulate ? da[c] + (float)s : (float)s;
+  for (int i = threadIdx.x; i < chunks; i += 64) s += part[(int64_t)c * chunks + i];
+  s = wave_sum_d(s);
+  if (threadIdx.x == 0) da[c] = accumulate ? da[c] + (float)s : (float)s;
 }
 
 __global__ void dropout_bwd_kernel(const float* __restrict__ dy, int64_t n, float p, float scale,
@@ -269,10 +317,16 @@ __global__ void dropout_bwd_kernel(const float* __restrict__ dy, int64_t n, floa
     dx[i] = (uniform01(seed, (uint64_t)i) >= p) ? dy[i] * scale : 0.f;
 }
 
-static dim3 ew_grid(int64_t B, int64_t C, int64_t HW) {
-  int gx = (int)((HW + 255) / 256);
-  if (gx > 64) gx = 64;
-  return dim3(gx, (unsigned)(B * C));
+static dim3 ew_grid(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  if (g > 16384) g = 16384;
+  return dim3((unsigned)(g < 1 ? 1 : g));
+}
+
+// the flat index n = B*C*HW times HW must stay below 2^32 for div16
+static bool norm_dims_ok(int64_t B, int64_t C, int64_t HW) {
+  const int64_t n = B * C * HW;
+  return n < (1ll << 31) && n * HW < (1ll << 32);
 }
 
 }  // namespace tvq
@@ -294,16 +348,19 @@ extern "C" int tvq_bn_train_fwd(const float* x, int64_t B, int64_t C, int64_t HW
                                 tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && y && save_mean && save_invstd && scale_shift && workspace && B > 0 && C > 0,
                 "tvq_bn_train_fwd: bad arguments");
+  TVQ_CHECK_ARG(norm_dims_ok(B, C, HW), "tvq_bn_train_fwd: tensor too large");
   hipStream_t st = (hipStream_t)stream;
   const int chunks = bn_chunks(B, HW);
+  const Div16 dhw = make_div16(HW);
   double* part = (double*)workspace;
   hipLaunchKernelGGL(bn_stats_partial_kernel, dim3((int)C, chunks), dim3(256), 0, st, x, (int)B,
-                     (int)C, (int)HW, chunks, part);
-  hipLaunchKernelGGL(bn_stats_final_kernel, dim3((int)((C + 63) / 64)), dim3(64), 0, st, part,
+                     (int)C, (int)HW, dhw, chunks, part);
+  hipLaunchKernelGGL(bn_stats_final_kernel, dim3((int)C), dim3(64), 0, st, part,
                      (int)C, chunks, B * HW, eps, momentum, w, b, running_mean, running_var,
                      num_batches_tracked, save_mean, save_invstd, scale_shift, scale_shift + C);
-  hipLaunchKernelGGL(affine_snake_kernel, ew_grid(B, C, HW), dim3(256), 0, st, x, (int)C, (int)HW,
-                     scale_shift, scale_shift + C, snake_a, y);
+  hipLaunchKernelGGL(affine_snake_kernel, ew_grid(B * C * HW), dim3(256), 0, st, x,
+                     (int)(B * C * HW), (int)C, (int)HW, dhw, scale_shift, scale_shift + C, snake_a,
+                     y);
   return launch_status("tvq_bn_train_fwd");
 }
 
@@ -313,11 +370,13 @@ extern "C" int tvq_bn_eval_fwd(const float* x, int64_t B, int64_t C, int64_t HW,
                                const float* running_var, float eps, const float* snake_a, float* y,
                                float* scale_shift, tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && y && running_mean && running_var && scale_shift, "tvq_bn_eval_fwd: bad args");
+  TVQ_CHECK_ARG(norm_dims_ok(B, C, HW), "tvq_bn_eval_fwd: tensor too large");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_eval_prep_kernel, dim3((int)((C + 63) / 64)), dim3(64), 0, st, w, b,
                      running_mean, running_var, eps, (int)C, scale_shift, scale_shift + C);
-  hipLaunchKernelGGL(affine_snake_kernel, ew_grid(B, C, HW), dim3(256), 0, st, x, (int)C, (int)HW,
-                     scale_shift, scale_shift + C, snake_a, y);
+  hipLaunchKernelGGL(affine_snake_kernel, ew_grid(B * C * HW), dim3(256), 0, st, x,
+                     (int)(B * C * HW), (int)C, (int)HW, make_div16(HW), scale_shift,
+                     scale_shift + C, snake_a, y);
   return launch_status("tvq_bn_eval_fwd");
 }
 
@@ -328,26 +387,29 @@ extern "C" int tvq_bn_bwd(const float* dy, const float* x, int64_t B, int64_t C,
                           tvq_stream_t stream) {
   TVQ_CHECK_ARG(dy && x && dx && save_mean && save_invstd && scale_shift && workspace,
                 "tvq_bn_bwd: bad arguments");
+  TVQ_CHECK_ARG(norm_dims_ok(B, C, HW), "tvq_bn_bwd: tensor too large");
   hipStream_t st = (hipStream_t)stream;
   const int chunks = bn_chunks(B, HW);
+  const Div16 dhw = make_div16(HW);
   double* part = (double*)workspace;
   float* coef = (float*)(part + (int64_t)C * chunks * 3);
   hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3((int)C, chunks), dim3(256), 0, st, dy, x, (int)B,
-                     (int)C, (int)HW, chunks, save_mean, save_invstd, scale_shift,
+                     (int)C, (int)HW, dhw, chunks, save_mean, save_invstd, scale_shift,
                      scale_shift + C, snake_a, part);
-  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((int)((C + 63) / 64)), dim3(64), 0, st, part,
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((int)C), dim3(64), 0, st, part,
                      (int)C, chunks, coef, dw, db, snake_a ? da : nullptr, (int)accumulate);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, ew_grid(B, C, HW), dim3(256), 0, st, dy, x, (int)C,
-                     (int)HW, B * HW, save_mean, save_invstd, w, scale_shift, scale_shift + C,
-                     snake_a, coef, dx);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, ew_grid(B * C * HW), dim3(256), 0, st, dy, x,
+                     (int)(B * C * HW), (int)C, (int)HW, dhw, B * HW, save_mean, save_invstd, w,
+                     scale_shift, scale_shift + C, snake_a, coef, dx);
   return launch_status("tvq_bn_bwd");
 }
 
 extern "C" int tvq_snake_fwd(const float* x, int64_t B, int64_t C, int64_t HW, const float* a,
                              float* y, tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && a && y && B > 0 && C > 0 && HW > 0, "tvq_snake_fwd: bad arguments");
-  hipLaunchKernelGGL(snake_fwd_kernel, ew_grid(B, C, HW), dim3(256), 0, (hipStream_t)stream, x,
-                     (int)C, (int)HW, a, y);
+  TVQ_CHECK_ARG(norm_dims_ok(B, C, HW), "tvq_snake_fwd: tensor too large");
+  hipLaunchKernelGGL(snake_fwd_kernel, ew_grid(B * C * HW), dim3(256), 0, (hipStream_t)stream, x,
+                     (int)(B * C * HW), (int)C, (int)HW, make_div16(HW), a, y);
   return launch_status("tvq_snake_fwd");
 }
 
@@ -359,11 +421,12 @@ extern "C" int tvq_snake_bwd(const float* dy, const float* x, int64_t B, int64_t
                              const float* a, float* dx, float* da, int64_t accumulate,
                              void* workspace, tvq_stream_t stream) {
   TVQ_CHECK_ARG(dy && x && a && dx && da && workspace, "tvq_snake_bwd: bad arguments");
+  TVQ_CHECK_ARG(norm_dims_ok(B, C, HW), "tvq_snake_bwd: tensor too large");
   hipStream_t st = (hipStream_t)stream;
   const int chunks = bn_chunks(B, HW);
   hipLaunchKernelGGL(snake_bwd_kernel, dim3((int)C, chunks), dim3(256), 0, st, dy, x, (int)B,
-                     (int)C, (int)HW, chunks, a, dx, (double*)workspace);
-  hipLaunchKernelGGL(snake_bwd_final_kernel, dim3((int)((C + 63) / 64)), dim3(64), 0, st,
+                     (int)C, (int)HW, make_div16(HW), chunks, a, dx, (double*)workspace);
+  hipLaunchKernelGGL(snake_bwd_final_kernel, dim3((int)C), dim3(64), 0, st,
                      (const double*)workspace, (int)C, chunks, da, (int)accumulate);
   return launch_status("tvq_snake_bwd");
 }

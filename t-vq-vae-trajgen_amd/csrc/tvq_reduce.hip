@@ -90,39 +90,77 @@ __global__ __launch_bounds__(256) void gb_hist_kernel(const IT* __restrict__ idx
 
 // one block: per-value totals over chunks, exclusive scan -> offsets[V+1];
 // chunk_off[chunk][v] = offsets[v] + sum_{c' < chunk} hist[c'][v]
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// Exclusive block scan (1024 threads) of two per-thread counters; returns the totals.
+__device__ __forceinline__ void block_excl_scan2(int& a, int& b, int& tot_a, int& tot_b) {
+  __shared__ int wa[16], wb[16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+  if (lane == 63) { wa[wid] = ia; wb[wid] = ib; }
+  __syncthreads();
+  int pa = 0, pb = 0;
+  tot_a = 0;
+  tot_b = 0;
+  for (int w = 0; w < 16; ++w) {
+    if (w < wid) { pa += wa[w]; pb += wb[w]; }
+    tot_a += wa[w];
+    tot_b += wb[w];
+  }
+  a = pa + ia - a;
+  b = pb + ib - b;
+}
+
+// Column totals over chunks, a parallel exclusive scan over values (integer, so any
+// order is exact), then per-chunk offsets.  One block of 1024 threads; each thread owns
+// `per` consecutive values.
 __global__ __launch_bounds__(1024) void gb_scan_kernel(const int* __restrict__ hist, int chunks,
                                                        int V, int* __restrict__ chunk_off,
                                                        int* __restrict__ offsets,
                                                        int* __restrict__ seg_start) {
   extern __shared__ int tot[];  // [V]
-  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+  const int per = (V + 1023) / 1024;
+  const int v0 = threadIdx.x * per;
+  int t_loc = 0, s_loc = 0;
+  for (int u = 0; u < per; ++u) {
+    const int v = v0 + u;
+    if (v >= V) break;
     int s = 0;
-#pragma unroll 8
-    for (int c = 0; c < chunks; ++c) {
-      chunk_off[(int64_t)c * V + v] = s;
-      s += hist[(int64_t)c * V + v];
-    }
+#pragma unroll 16
+    for (int c = 0; c < chunks; ++c) s += hist[(int64_t)c * V + v];
     tot[v] = s;
+    t_loc += s;
+    s_loc += (s + SEG_CH - 1) / SEG_CH;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {  // V <= a few thousand: serial scan is cheap and deterministic
-    int run = 0, segs = 0;
-    for (int v = 0; v < V; ++v) {
-      const int t = tot[v];
-      tot[v] = run;
-      run += t;
-      if (seg_start) {
-        seg_start[v] = segs;
-        segs += (t + SEG_CH - 1) / SEG_CH;
-      }
+  int all_t, all_s;
+  block_excl_scan2(t_loc, s_loc, all_t, all_s);
+  int run = t_loc, segs = s_loc;
+  for (int u = 0; u < per; ++u) {
+    const int v = v0 + u;
+    if (v >= V) break;
+    offsets[v] = run;
+    if (seg_start) seg_start[v] = segs;
+    int s = run;
+#pragma unroll 16
+    for (int c = 0; c < chunks; ++c) {
+      const int h = hist[(int64_t)c * V + v];
+      chunk_off[(int64_t)c * V + v] = s;
+      s += h;
     }
-    offsets[V] = run;
-    if (seg_start) seg_start[V] = segs;
+    run += tot[v];
+    segs += (tot[v] + SEG_CH - 1) / SEG_CH;
   }
-  __syncthreads();
-  for (int v = threadIdx.x; v < V; v += blockDim.x) {
-    offsets[v] = tot[v];
-    for (int c = 0; c < chunks; ++c) chunk_off[(int64_t)c * V + v] += tot[v];
+  if (threadIdx.x == 0) {
+    offsets[V] = all_t;
+    if (seg_start) seg_start[V] = all_s;
   }
 }
 

@@ -49,12 +49,11 @@ sig("tvq_istft_decode_bwd", P, I64, I64, I64, I64, I64, P, P)
 # --- convolutions --------------------------------------------------------------
 sig("tvq_conv_out_width", I64, I64, I64, I64)
 sig("tvq_conv_config", I64)
+sig("tvq_conv_workspace", I64, I64, I64, I64, I64, I64, I64, I64, I64, I64, restype=I64)
 sig("tvq_conv2d_fwd", P, I64, I64, I64, I64, P, P, I64, I64, I64, I64, I64, P, P, F32, P, U64, P, P)
 sig("tvq_convT2d_fwd", P, I64, I64, I64, I64, P, P, I64, I64, I64, I64, P, P, P, P)
-sig("tvq_conv2d_dgrad_workspace", I64, I64, I64, I64, I64, I64, I64, restype=I64)
-sig("tvq_conv2d_dgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, P, I64, P, P, P)
+sig("tvq_conv2d_dgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, P, I64, P, P)
 sig("tvq_convT2d_dgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, P, I64, P, P)
-sig("tvq_conv_wgrad_workspace", I64, I64, I64, I64, I64, I64, I64, restype=I64)
 sig("tvq_conv2d_wgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, I64, P, P, I64, P, P)
 sig("tvq_convT2d_wgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, P, I64, P, P)
 sig("tvq_channel_sum_workspace", I64, I64, I64, restype=I64)

@@ -26,13 +26,19 @@ def _bias_grad(g, dev, sink=None):
     return None if sink is not None else out
 
 
-PACK_WEIGHTS = True  # tests flip this to cover the in-place (strided) weight reads
+USE_WORKSPACE = True  # tests flip this to cover the no-workspace (in-place weight) path
+
+# tvq_conv_workspace ops
+OP_FWD, OP_T_FWD, OP_DGRAD, OP_T_DGRAD, OP_WGRAD, OP_T_WGRAD = range(6)
 
 
-def _wpack(w, c_red):
-    """Scratch for the tap-major weight repack; only the tap-major GEMM (reduction channels
-    a multiple of 16) benefits, the flat small-channel path reads the weight in place."""
-    return torch.empty_like(w) if PACK_WEIGHTS and c_red % 16 == 0 else None
+def _conv_ws(op, dev, B, Ci, H, Wi, Co, KH, KW, SW, replicate=0, required=False):
+    """Workspace for one conv op (weight repack + split-K partials [+ replicate canvas]);
+    None for the optional forward-type workspaces when USE_WORKSPACE is off."""
+    if not (USE_WORKSPACE or required):
+        return None
+    n = value("tvq_conv_workspace", op, B, Ci, H, Wi, Co, KH, KW, SW, int(replicate))
+    return torch.empty(n, device=dev, dtype=torch.float32)
 
 
 def _as4d(x):
@@ -52,9 +58,10 @@ class _Conv2d(torch.autograd.Function):
         res = _as4d(residual).contiguous() if residual is not None else None
         seed = rng.seed_tensor(x.device) if drop_p > 0 else None
         off = rng.call_offset(site) if drop_p > 0 else 0
+        ws = _conv_ws(OP_FWD, x.device, B, Ci, H, Wi, Co, KH, KW, SW)
         call("tvq_conv2d_fwd", ptr(x4), B, Ci, H, Wi, ptr(w4), ptr(b), Co, KH, KW, SW,
-             int(replicate), ptr(y), ptr(res), float(drop_p), ptr(seed), off,
-             ptr(_wpack(w4, Ci)), stream_ptr())
+             int(replicate), ptr(y), ptr(res), float(drop_p), ptr(seed), off, ptr(ws),
+             stream_ptr())
         ctx.save_for_backward(x4, w4)
         ctx.cfg = (SW, replicate, drop_p, off, squeeze, b is not None, residual is not None,
                    w.dim())
@@ -80,10 +87,10 @@ class _Conv2d(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x4)
-            wsz = value("tvq_conv2d_dgrad_workspace", B, Ci, H, Wi, KH, KW, int(replicate))
-            ws = _ws(wsz, dev) if replicate else None
+            ws = _conv_ws(OP_DGRAD, dev, B, Ci, H, Wi, Co, KH, KW, SW, replicate,
+                          required=bool(replicate))
             call("tvq_conv2d_dgrad", ptr(gd), B, Co, H, Wo, ptr(w4), Ci, KH, KW, SW,
-                 int(replicate), ptr(dx), Wi, ptr(ws), ptr(_wpack(w4, Co)), s)
+                 int(replicate), ptr(dx), Wi, ptr(ws), s)
             if squeeze:
                 dx = dx.squeeze(2)
         need_w, need_b = ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]
@@ -93,7 +100,7 @@ class _Conv2d(torch.autograd.Function):
             direct = need_w and sw is not None and (not need_b or sb is not None)
             dwt = sw if direct else torch.empty_like(w4)
             dbt = (sb if direct else torch.empty(Co, device=dev)) if need_b else None
-            ws = _ws(value("tvq_conv_wgrad_workspace", Co, Ci, KH, KW, B, H, Wo), dev)
+            ws = _conv_ws(OP_WGRAD, dev, B, Ci, H, Wi, Co, KH, KW, SW, replicate, required=True)
             call("tvq_conv2d_wgrad", ptr(x4), B, Ci, H, Wi, ptr(gd), Co, Wo, KH, KW, SW,
                  int(replicate), ptr(dwt), ptr(dbt), int(direct), ptr(ws), s)
             if not direct:
@@ -121,8 +128,9 @@ class _ConvT2d(torch.autograd.Function):
         _, Co, KH, KW = w.shape
         Wo = value("tvq_conv_out_width", Wi, KW, SW, 1)
         y = torch.empty((B, Co, H, Wo), device=x.device, dtype=torch.float32)
+        ws = _conv_ws(OP_T_FWD, x.device, B, Ci, H, Wi, Co, KH, KW, SW)
         call("tvq_convT2d_fwd", ptr(x), B, Ci, H, Wi, ptr(w), ptr(b), Co, KH, KW, SW, ptr(y), None,
-             ptr(_wpack(w, Ci)), stream_ptr())
+             ptr(ws), stream_ptr())
         ctx.save_for_backward(x, w)
         ctx.SW = SW
         ctx.has_b = b is not None
@@ -141,13 +149,14 @@ class _ConvT2d(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
+            ws = _conv_ws(OP_T_DGRAD, x.device, B, Ci, H, Wi, Co, KH, KW, SW)
             call("tvq_convT2d_dgrad", ptr(g), B, Co, H, Wo, ptr(w), Ci, KH, KW, SW, ptr(dx), Wi,
-                 ptr(_wpack(w, Co)), s)
+                 ptr(ws), s)
         w_p, b_p = ctx.params
         if ctx.needs_input_grad[1]:
             sw = grad_sink(w_p)
             dwt = sw if sw is not None else torch.empty_like(w)
-            ws = _ws(value("tvq_conv_wgrad_workspace", Ci, Co, KH, KW, B, H, Wi), x.device)
+            ws = _conv_ws(OP_T_WGRAD, x.device, B, Ci, H, Wi, Co, KH, KW, SW, required=True)
             call("tvq_convT2d_wgrad", ptr(x), B, Ci, H, Wi, ptr(g), Co, Wo, KH, KW, SW, ptr(dwt),
                  int(sw is not None), ptr(ws), s)
             dw = None if sw is not None else dwt

@@ -34,7 +34,7 @@ def conv_path(monkeypatch):
     from timevqvae.hip._native import value
 
     def select(path):
-        monkeypatch.setattr(conv_mod, "PACK_WEIGHTS", path != "gemm_raw")
+        monkeypatch.setattr(conv_mod, "USE_WORKSPACE", path != "gemm_raw")
         value("tvq_conv_config", 3 if path == "halo" else 0)
 
     yield select
@@ -285,10 +285,11 @@ def test_adamw_matches_torch(cuda):
         torch.testing.assert_close(pd.detach().cpu(), pc.detach(), rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("Ci,Co,W", [(16, 16, 32), (64, 64, 8), (8, 8, 64)])
+@pytest.mark.parametrize("Ci,Co,W", [(16, 16, 32), (64, 64, 8), (8, 8, 64), (128, 16, 32)])
 def test_conv_paths_same_dropout_mask(Ci, Co, W, cuda):
     """The dropout mask is a function of (seed, offset, output index) only: the halo
-    kernel and the staged GEMM drop exactly the same elements."""
+    kernel, the staged GEMM and the split-K GEMM (partials + epilogue kernel) drop
+    exactly the same elements."""
     from timevqvae.hip._native import call, ptr, stream_ptr, value
     gen = torch.Generator().manual_seed(3)
     x = torch.randn(5, Ci, 3, W, generator=gen).to(cuda)
@@ -296,17 +297,20 @@ def test_conv_paths_same_dropout_mask(Ci, Co, W, cuda):
     b = torch.randn(Co, generator=gen).to(cuda)
     r = torch.randn(5, Co, 3, W, generator=gen).to(cuda)
     seed = torch.tensor([1234], dtype=torch.int64, device=cuda)
+    nws = value("tvq_conv_workspace", 0, 5, Ci, 3, W, Co, 3, 3, 1, 0)
+    ws = torch.empty(nws, device=cuda)
     outs = []
     try:
-        for halo in (1, 0):
+        for halo, wsp in ((3, None), (0, None), (0, ws)):
             value("tvq_conv_config", halo)
             y = torch.empty(5, Co, 3, W, device=cuda)
             call("tvq_conv2d_fwd", ptr(x), 5, Ci, 3, W, ptr(w), ptr(b), Co, 3, 3, 1, 0, ptr(y),
-                 ptr(r), 0.25, ptr(seed), 77, None, stream_ptr())
+                 ptr(r), 0.25, ptr(seed), 77, ptr(wsp), stream_ptr())
             outs.append(y)
     finally:
         value("tvq_conv_config", 3)
     torch.cuda.synchronize()
-    m0, m1 = outs[0] == r, outs[1] == r
-    assert torch.equal(m0, m1)
+    masks = [o == r for o in outs]
+    assert torch.equal(masks[0], masks[1]) and torch.equal(masks[0], masks[2])
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(outs[0], outs[2], rtol=1e-5, atol=1e-5)

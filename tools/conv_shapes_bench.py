@@ -71,26 +71,25 @@ def main():
         dx = torch.empty_like(x)
         dw = torch.empty_like(w)
         db = torch.empty_like(b)
-        wp = torch.empty_like(w)
+        def ws(op):
+            return torch.empty(value("tvq_conv_workspace", op, B, Ci, H, Wi, Co, KH, KW, SW, rep),
+                               device=dev)
         if not tr:
+            wf, wd, wg = ws(0), ws(2), ws(4)
             f = lambda: call("tvq_conv2d_fwd", ptr(x), B, Ci, H, Wi, ptr(w), ptr(b), Co, KH, KW, SW,  # noqa
-                             rep, ptr(y), None, 0.0, None, 0, ptr(wp) if Ci % 16 == 0 else None, stream_ptr())
-            wsd = torch.empty(max(1, value("tvq_conv2d_dgrad_workspace", B, Ci, H, Wi, KH, KW, rep)),
-                              device=dev)
+                             rep, ptr(y), None, 0.0, None, 0, ptr(wf), stream_ptr())
             d = lambda: call("tvq_conv2d_dgrad", ptr(dy), B, Co, H, Wo, ptr(w), Ci, KH, KW, SW, rep,  # noqa
-                             ptr(dx), Wi, ptr(wsd) if rep else None,
-                             ptr(wp) if Co % 16 == 0 else None, stream_ptr())
-            wsw = torch.empty(value("tvq_conv_wgrad_workspace", Co, Ci, KH, KW, B, H, Wo), device=dev)
+                             ptr(dx), Wi, ptr(wd), stream_ptr())
             g = lambda: call("tvq_conv2d_wgrad", ptr(x), B, Ci, H, Wi, ptr(dy), Co, Wo, KH, KW, SW,  # noqa
-                             rep, ptr(dw), ptr(db), 0, ptr(wsw), stream_ptr())
+                             rep, ptr(dw), ptr(db), 0, ptr(wg), stream_ptr())
         else:
+            wf, wd, wg = ws(1), ws(3), ws(5)
             f = lambda: call("tvq_convT2d_fwd", ptr(x), B, Ci, H, Wi, ptr(w), ptr(b), Co, KH, KW, SW,  # noqa
-                             ptr(y), None, ptr(wp) if Ci % 16 == 0 else None, stream_ptr())
+                             ptr(y), None, ptr(wf), stream_ptr())
             d = lambda: call("tvq_convT2d_dgrad", ptr(dy), B, Co, H, Wo, ptr(w), Ci, KH, KW, SW,  # noqa
-                             ptr(dx), Wi, ptr(wp) if Co % 16 == 0 else None, stream_ptr())
-            wsw = torch.empty(value("tvq_conv_wgrad_workspace", Ci, Co, KH, KW, B, H, Wi), device=dev)
+                             ptr(dx), Wi, ptr(wd), stream_ptr())
             g = lambda: call("tvq_convT2d_wgrad", ptr(x), B, Ci, H, Wi, ptr(dy), Co, Wo, KH, KW, SW,  # noqa
-                             ptr(dw), 0, ptr(wsw), stream_ptr())
+                             ptr(dw), 0, ptr(wg), stream_ptr())
         tf, td, tg = timeit(f), timeit(d), timeit(g)
         flops = 2.0 * B * H * (Wo if not tr else Wi) * Co * Ci * KH * KW
         byts = 4.0 * (x.numel() + y.numel())

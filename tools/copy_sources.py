@@ -20,18 +20,26 @@ def main():
     for _ in range(2):
         tr.step(batch)
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
         tr.step(batch)
         torch.cuda.synchronize()
     sites = collections.Counter()
+    kern = collections.Counter()
     for ev in prof.events():
-        if ev.name in ("aten::copy_", "aten::clone", "aten::contiguous", "aten::to", "aten::_to_copy",
-                       "aten::zero_", "aten::fill_", "aten::add_", "aten::zeros", "aten::cat",
-                       "aten::index_put_", "aten::mul_"):
-            stack = [f for f in (ev.stack or []) if "t-vq-vae-trajgen_amd" in f or "bench.py" in f]
-            sites[(ev.name, stack[0] if stack else "?")] += 1
-    for (name, site), n in sites.most_common(60):
-        print(f"{n:5d} {name:18s} {site}")
+        ks = [k.name for k in getattr(ev, "kernels", [])]
+        if not ks:
+            continue
+        for k in ks:
+            kern[k[:60]] += 1
+        if not any(("opy" in k or "emcpy" in k or "emset" in k) for k in ks):
+            continue
+        stack = [f for f in (ev.stack or []) if "site-packages" not in f and "dist-packages" not in f]
+        sites[(ev.name, " | ".join(stack[:3]) if stack else "?", ks[0][:30])] += 1
+    for (name, site, k), n in sites.most_common(60):
+        print(f"{n:5d} {name:22s} {k:30s} {site}")
+    print("--- device activity names")
+    for k, n in kern.most_common(15):
+        print(f"{n:5d} {k}")
 
 
 if __name__ == "__main__":
