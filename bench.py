@@ -56,18 +56,27 @@ def synthetic_batch(seed, device):
 
 
 class JointTrainer:
-    """stage1 step then stage2 step (stage2 trains on a frozen snapshot of stage1)."""
+    """stage1 step then stage2 step (stage2 trains on a frozen snapshot of stage1).
 
-    def __init__(self, device, world):
+    Graph mode (default): the step is captured as three hipGraph segments
+      [advance seed, zero_grad, stage1 fwd+bwd] -> [codebook EMA, AdamW1, zero_grad,
+      stage2 fwd+bwd] -> [AdamW2]
+    with the DP all-reduces (flat gradients, sync_codebook statistics) and the LR
+    schedulers run eagerly between / before the segments.
+    """
+
+    def __init__(self, device, world, cfg=None, length=T, channels=C):
         from timevqvae.trainers import Stage1, Stage2
         from timevqvae.hip import rng
-        torch.manual_seed(0)
+        from timevqvae.utils import set_seed
+        set_seed(0)  # python / numpy (Snake a init) / torch
         rng.manual_seed(1)
-        cfg = config(world > 1)
+        cfg = cfg if cfg is not None else config(world > 1)
         self.world = world
-        self.s1 = Stage1(T, C, cfg).to(device).train()
+        self.s1 = Stage1(length, channels, cfg).to(device).train()
         s1_frozen = copy.deepcopy(self.s1)
-        self.s2 = Stage2(None, None, T, C, N_CLASSES, config=cfg, stage1=s1_frozen).to(device).train()
+        self.s2 = Stage2(None, None, length, channels, N_CLASSES, config=cfg,
+                         stage1=s1_frozen).to(device).train()
         self.opt1 = self.s1.configure_optimizers()["optimizer"]
         self.opt2 = self.s2.configure_optimizers()["optimizer"]
         if world > 1:  # identical initial replicas (DDP semantics)
@@ -78,6 +87,8 @@ class JointTrainer:
                     if b.is_floating_point():
                         dist.broadcast(b, 0)
         self.device = device
+        self.graph = None
+        self._pending = []
 
     def _allreduce(self, opt):
         if self.world > 1:
@@ -85,6 +96,8 @@ class JointTrainer:
             opt.flat_grad.mul_(1.0 / self.world)
 
     def step(self, batch):
+        if self.graph is not None:
+            return self.graph.replay()[:2]
         from timevqvae.hip import rng
         rng.advance(self.device)
         self.opt1.zero_grad()
@@ -98,6 +111,54 @@ class JointTrainer:
         self._allreduce(self.opt2)
         self.opt2.step()
         return out1, out2
+
+    def capture(self, batch):
+        """Capture the step (runs 2 eager warmup steps first)."""
+        import contextlib
+        from timevqvae.hip import rng
+        from timevqvae.hip.graph import StepGraph
+        from timevqvae.hip.vq import deferred_codebook_updates
+        scheds = (self.s1._sched, self.s2._sched)
+        self.s1._sched = self.s2._sched = None  # stepped on the host before each replay
+        defer = self.world > 1  # sync_codebook all-reduce must sit between segments
+
+        def before():
+            for sch, opt in zip(scheds, (self.opt1, self.opt2)):
+                if sch is not None:
+                    sch.step()
+                opt.push_lr()
+
+        def seg1():
+            rng.advance(self.device)
+            self.opt1.zero_grad()
+            with (deferred_codebook_updates() if defer else contextlib.nullcontext([])) as pend:
+                out1 = self.s1.training_step(batch, 0)
+            self._pending = pend
+            out1["loss"].sum().backward()
+            return out1
+
+        def between1():
+            self._allreduce(self.opt1)
+            for u in self._pending:
+                u.reduce()
+
+        def seg2():
+            for u in self._pending:
+                u.apply()
+            self.opt1.step(lr_on_device=True)
+            self.opt2.zero_grad()
+            out2 = self.s2.training_step(batch, 0)
+            out2["loss"].backward()
+            return out2
+
+        def between2():
+            self._allreduce(self.opt2)
+
+        def seg3():
+            self.opt2.step(lr_on_device=True)
+
+        self.graph = StepGraph([seg1, seg2, seg3], [between1, between2, None], warmup=2,
+                               before=before).capture()
 
 
 def roofline_leg(device):
@@ -145,6 +206,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -156,6 +218,8 @@ def main():
     device = torch.device("cuda", local)
     tr = JointTrainer(device, world)
     batch = synthetic_batch(1234 + rank, device)
+    if not args.eager:
+        tr.capture(batch)
 
     for _ in range(args.warmup):
         tr.step(batch)
@@ -194,6 +258,7 @@ def main():
             "config": {"workload": "stage1 VQ-VAE + stage2 MaskGIT joint train step, per-GPU batch "
                                    "(B=256,C=6,T=256), K=512, configs/config.yaml architecture",
                        "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
+                       "launch": "eager" if args.eager else "hipgraph",
                        "trajectories_per_s": round(value * B, 1)},
             "losses": {"stage1": round(loss1, 5), "stage2": round(loss2, 5)},
         }

@@ -39,6 +39,11 @@ class FusedAdamW(torch.optim.Optimizer):
                 p._tvq_flat = True
                 off += k
 
+    def push_lr(self):
+        """Write param_groups[0]['lr'] into the device {lr, step} pair (for graph replays,
+        whose captured update reads the lr from the device: step(lr_on_device=True))."""
+        self.lr_step[0:1].fill_(float(self.param_groups[0]["lr"]))
+
     def zero_grad(self, set_to_none: bool = False):
         # gradients accumulate in place into the flat buffer views
         self.flat_grad.zero_()

@@ -6,9 +6,53 @@ VectorQuantize.forward (reference timevqvae/models/vq.py:197-251, 357-366):
   -> [optional all-reduce of the stats: sync_codebook, vq.py:229,234]
   -> EMA blend -> Laplace-normalised codebook + perplexity + commit loss.
 """
+import contextlib
+
 import torch
 
 from ._native import call, ptr, stream_ptr, value
+
+_pending = None  # list of CodebookUpdate while a deferral scope is active
+
+
+class CodebookUpdate:
+    """An EMA codebook update whose per-batch statistics are computed but not yet applied.
+
+    The forward outputs never read the updated codebook (quantize = E_old[idx]), so the
+    update can move after the backward: `reduce()` runs the sync_codebook all-reduce of
+    the statistics (eager, between captured graph segments) and `apply()` the EMA blend +
+    Laplace-normalised codebook (capturable).
+    """
+
+    def __init__(self, cs_b, es_b, cluster_size, embed_avg, embed, decay, eps, sync):
+        self.cs_b, self.es_b = cs_b, es_b
+        self.cluster_size, self.embed_avg, self.embed = cluster_size, embed_avg, embed
+        self.decay, self.eps, self.sync = decay, eps, sync
+        self.K, self.D = embed.shape
+
+    def reduce(self):
+        if self.sync is not None:
+            self.sync(self.cs_b)
+            self.sync(self.es_b)
+
+    def apply(self):
+        s = stream_ptr()
+        call("tvq_vq_ema", ptr(self.cs_b), ptr(self.es_b), self.K, self.D, float(self.decay),
+             ptr(self.cluster_size), ptr(self.embed_avg), s)
+        call("tvq_vq_finalize", ptr(self.cluster_size), ptr(self.embed_avg), self.K, self.D,
+             float(self.eps), ptr(self.embed), None, 0, None, None, 0, None, s)
+
+
+@contextlib.contextmanager
+def deferred_codebook_updates():
+    """Collect the EMA codebook updates of the passes run inside the scope instead of
+    applying them; yields the list of CodebookUpdate (reduce() then apply() each)."""
+    global _pending
+    prev, _pending = _pending, []
+    try:
+        yield _pending
+    finally:
+        _pending = prev
 
 
 def _same_dense_layout(a, b):
@@ -56,7 +100,11 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
          ptr(es_b), ptr(ws), s)
     perp = torch.empty((), device=dev, dtype=torch.float32)
     commit = torch.empty((), device=dev, dtype=torch.float32) if straight_through else None
-    if ema:
+    if ema and _pending is not None:
+        _pending.append(CodebookUpdate(cs_b, es_b, cluster_size, embed_avg, embed, decay, eps, sync))
+        call("tvq_vq_finalize", None, None, K, D, float(eps), None, ptr(counts), M, ptr(perp),
+             ptr(partial), nb if partial is not None else 0, ptr(commit), s)
+    elif ema:
         if sync is not None:
             sync(cs_b)
             sync(es_b)

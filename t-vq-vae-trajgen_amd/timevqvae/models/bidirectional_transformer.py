@@ -116,8 +116,14 @@ class Encoder(nn.Module):
 
     def forward(self, x):
         for norms, block, _ in self.layers:
-            if self.training and self.layer_dropout > 0.0 and random.random() < self.layer_dropout:
-                continue
+            if self.training and self.layer_dropout > 0.0:
+                if rng.decisions_on_device():
+                    # graph capture: skip-with-prob-p as a device Bernoulli gate on the branch
+                    keep = (torch.rand((), device=x.device) >= self.layer_dropout).to(x.dtype)
+                    x = torch.addcmul(x, block(norms[0](x), residual=None), keep)
+                    continue
+                if random.random() < self.layer_dropout:
+                    continue
             x = block(norms[0](x), residual=x)
         return self.final_norm(x)
 

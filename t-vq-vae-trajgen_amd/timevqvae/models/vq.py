@@ -137,7 +137,7 @@ class VectorQuantize(nn.Module):
         cb._check_svq(svq_temp)
         device = x.device
         vq_loss = {
-            "loss": torch.tensor([0.0], device=device, requires_grad=self.training),
+            "loss": torch.zeros(1, device=device).requires_grad_(self.training),
             "commit_loss": 0.0,
             "orthogonal_reg_loss": 0.0,
         }
