@@ -162,11 +162,16 @@ class JointTrainer:
 
 
 def roofline_leg(device):
-    """Average duration of the dominant kernel at its step shape, on the stream it runs on
-    (HIP events), with its algorithmic FLOPs -> achieved / peak."""
+    """Average duration of the dominant conv op at its step shape, on the stream it runs on
+    (HIP events), with its algorithmic FLOPs -> achieved / peak.
+
+    The op is the HF encoder ResBlock(16->128) second conv, (256,128,3,32) x (128,128,3,3):
+    the largest single conv of the step (7.25 GFLOP).  As in the step it
+    runs as conv_pack_weight + conv_tap_kernel (split-K x3) + conv_splitk_epi; the
+    committed rocprofv3 summary (profiles/r01_roofline_kernel_stats.csv) lists the three
+    and their averages sum to avg_launch_ms.  `traffic` is the PMC-measured HBM bytes per
+    op from profiles/r01_roofline_traffic.json (FETCH_SIZE + WRITE_SIZE passes)."""
     from timevqvae.hip.conv import conv2d
-    # HF encoder ResBlock(16->128) second conv: (256,128,3,32) x (128,128,3,3) -- the
-    # largest single launch of the step (7.25 GFLOP), SURVEY §2.2 K3
     x = torch.randn(256, 128, 3, 32, device=device)
     w = torch.randn(128, 128, 3, 3, device=device) * 0.03
     b = torch.zeros(128, device=device)
@@ -183,10 +188,16 @@ def roofline_leg(device):
     ms = e0.elapsed_time(e1) / n
     flops = 2.0 * (256 * 3 * 32) * 128 * (128 * 9)
     achieved = flops / (ms * 1e-3) / 1e12
-    return {"bound": "mfma", "kernel": "conv_gemm_kernel<F,3,3,1> (ResBlock conv 128->128 @ 3x32, B=256)",
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "r01_roofline_traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath))["traffic_bytes"]
+    return {"bound": "mfma", "kernel": "conv2d 128->128 3x3 @ (256,128,3,32): conv_pack_weight + "
+                                       "conv_tap_kernel<F,3,3,1,64x128> split-K x3 + conv_splitk_epi",
             "achieved": round(achieved, 2), "peak": 157.3, "unit": "TFLOP/s",
-            "frac": round(achieved / 157.3, 4), "traffic": None, "avg_launch_ms": round(ms, 4),
-            "flops_per_launch": flops}
+            "frac": round(achieved / 157.3, 4), "traffic": traffic,
+            "algorithmic_bytes": 4 * (256 * 128 * 3 * 32 * 2 + 128 * 128 * 9),
+            "avg_launch_ms": round(ms, 4), "flops_per_launch": flops}
 
 
 def cpu_baseline_leg():

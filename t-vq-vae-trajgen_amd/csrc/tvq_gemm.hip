@@ -226,8 +226,21 @@ static int gemm_splits(int M, int N, int K, int tiles) {
 
 using namespace tvq;
 
+// Largest tile that still gives >= 256 blocks (the step's GEMMs have K <= 512 and a few
+// thousand rows: latency-bound, so filling the 256 CUs matters more than tile reuse);
+// deep-K GEMMs that stay small get split-K instead.
+static void choose_tile(int64_t M, int64_t N, int* TM, int* TN) {
+  static const int cand[4][2] = {{128, 64}, {64, 64}, {64, 32}, {32, 32}};
+  for (int i = 0; i < 4; ++i) {
+    *TM = cand[i][0];
+    *TN = cand[i][1];
+    if (((M + *TM - 1) / *TM) * ((N + *TN - 1) / *TN) >= 256) return;
+  }
+}
+
 extern "C" int64_t tvq_gemm_workspace(int64_t M, int64_t N, int64_t K) {
-  const int TM = M >= 128 ? 128 : 64, TN = N >= 64 ? 64 : 32;
+  int TM, TN;
+  choose_tile(M, N, &TM, &TN);
   const int tiles = (int)(((M + TM - 1) / TM) * ((N + TN - 1) / TN));
   const int s = gemm_splits((int)M, (int)N, (int)K, tiles);
   return s > 1 ? (int64_t)s * M * N : 0;
@@ -246,7 +259,8 @@ extern "C" int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B
   g.bias = bias; g.R = R; g.ldr = ldr; g.rmod = rmod; g.pre = pre;
   g.act = (int)act; g.accumulate = (int)accumulate;
   g.alpha = alpha;
-  const int TM = M >= 128 ? 128 : 64, TN = N >= 64 ? 64 : 32;
+  int TM, TN;
+  choose_tile(M, N, &TM, &TN);
   const int tiles = (int)(((M + TM - 1) / TM) * ((N + TN - 1) / TN));
   int splits = gemm_splits((int)M, (int)N, (int)K, tiles);
   if (splits > 1 && !workspace) splits = 1;
@@ -257,14 +271,14 @@ extern "C" int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B
   g.slab = splits > 1 ? workspace : nullptr;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((M + TM - 1) / TM), (unsigned)((N + TN - 1) / TN), (unsigned)splits);
-  if (TM == 128 && TN == 64)
+  if (TM == 128)
     hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2>), grid, dim3(256), 0, st, g);
-  else if (TM == 128)
-    hipLaunchKernelGGL((gemm_kernel<128, 32, 4, 1>), grid, dim3(256), 0, st, g);
   else if (TN == 64)
     hipLaunchKernelGGL((gemm_kernel<64, 64, 2, 2>), grid, dim3(256), 0, st, g);
-  else
+  else if (TM == 64)
     hipLaunchKernelGGL((gemm_kernel<64, 32, 2, 2>), grid, dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL((gemm_kernel<32, 32, 2, 2>), grid, dim3(256), 0, st, g);
   if (splits > 1) {
     const int64_t tot = M * N;
     const int blocks = (int)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096);
