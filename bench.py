@@ -272,6 +272,7 @@ def main():
                        "launch": "eager" if args.eager else "hipgraph",
                        "trajectories_per_s": round(value * B, 1)},
             "losses": {"stage1": round(loss1, 5), "stage2": round(loss2, 5)},
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 3),
         }
         if not args.no_roofline:
             res["roofline"] = roofline_leg(device)
