@@ -290,6 +290,30 @@ int tvq_upsample_nearest_bwd(const float* dy, int64_t R, int64_t Lin, int64_t Lo
 int tvq_gelu_fwd(const float* x, int64_t n, float* y, tvq_stream_t stream);
 int tvq_gelu_bwd(const float* dy, const float* x, int64_t n, float* dx, tvq_stream_t stream);
 
+/* ---------------------------------------------------------------- MaskGIT sampling
+ * One iterative-decoding step of MaskGIT.first_pass / second_pass (maskgit.py:294-411):
+ * tvq_maskgit_sample draws, for every token equal to mask_id, a code from
+ * Categorical(softmax(logits)) (maskgit.py:302-310) by inverse CDF at u (double softmax and
+ * prefix), keeps the other tokens, and writes p(sampled) (fp32 softmax; +inf for kept
+ * tokens, maskgit.py:320-326).  logits (B, n, K) with batch/token strides (sb, sn).
+ * tvq_maskgit_remask: confidence = log(p + 1e-5) + temperature * Gumbel, re-mask exactly
+ * the k lowest-confidence tokens of each row (mask_by_random_topk, maskgit.py:238-267,
+ * ties by index) -> s_out (nullable) and/or masking (uint8, nullable).
+ * Noise: u_cat / u_gumbel (B*n uniforms) when given, else the counter hash of
+ * (*seed_ptr, offset, element). */
+int tvq_maskgit_sample(const float* logits, int64_t sb, int64_t sn, int64_t B, int64_t n,
+                       int64_t K, const int64_t* s_in, int64_t mask_id, const float* u_cat,
+                       const int64_t* seed_ptr, uint64_t offset, int64_t* sampled, float* selp,
+                       tvq_stream_t stream);
+int tvq_maskgit_remask(const float* selp, int64_t B, int64_t n, int64_t k, float temperature,
+                       const float* u_gumbel, const int64_t* seed_ptr, uint64_t offset,
+                       const int64_t* sampled, int64_t mask_id, int64_t* s_out, uint8_t* masking,
+                       tvq_stream_t stream);
+/* out[b, d, p] = E[idx[b, p], d]: the codebook lookup of decode_token_ind_to_timeseries
+ * (maskgit.py:461-469: F.embedding + 'b n c -> b c (h w)') written in NCHW. */
+int tvq_codebook_gather_nchw(const int64_t* idx, int64_t B, int64_t P, int64_t D, const float* E,
+                             float* out, tvq_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

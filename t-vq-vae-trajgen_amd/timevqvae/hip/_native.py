@@ -99,6 +99,10 @@ sig("tvq_upsample_nearest", P, I64, I64, I64, P, P)
 sig("tvq_upsample_nearest_bwd", P, I64, I64, I64, P, P)
 sig("tvq_gelu_fwd", P, I64, P, P)
 sig("tvq_gelu_bwd", P, P, I64, P, P)
+# --- MaskGIT sampling ------------------------------------------------------------
+sig("tvq_maskgit_sample", P, I64, I64, I64, I64, I64, P, I64, P, P, U64, P, P, P)
+sig("tvq_maskgit_remask", P, I64, I64, I64, F32, P, P, U64, P, I64, P, P, P)
+sig("tvq_codebook_gather_nchw", P, I64, I64, I64, P, P, P)
 
 
 class NativeError(RuntimeError):

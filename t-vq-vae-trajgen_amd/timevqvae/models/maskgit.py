@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 
 from ..hip import rng
+from ..hip.sample import codebook_gather_nchw, mask_len, maskgit_remask, maskgit_sample
 from ..hip.signal import stft_encode
 from ..hip.xf import mask_tokens, masked_cross_entropy
 from ..utils import freeze, quantize, zero_pad_high_freq, zero_pad_low_freq
@@ -149,10 +150,60 @@ class MaskGIT(nn.Module):
         """maskgit.py:230-236."""
         return torch.full((num, num_tokens), mask_token_ids, dtype=torch.int64, device=device)
 
+    def mask_by_random_topk(self, mask_len, probs, temperature=1.0, device="cpu"):
+        """maskgit.py:238-267: bool masking of exactly mask_len lowest-confidence tokens
+        per row, confidence = log(probs + 1e-5) + temperature * Gumbel noise."""
+        k = int(mask_len.unique().item()) if torch.is_tensor(mask_len) else int(mask_len)
+        return maskgit_remask(probs.float(), k, temperature, site=self._site_sample,
+                              want_masking=True)
+
+    def _decode_pass(self, transformer_call, s, mask_id, T, temperature, unknown0, gamma):
+        """One of first_pass / second_pass: T steps of (logits -> sample -> re-mask)."""
+        n0 = int(unknown0.max().item()) if torch.is_tensor(unknown0) else int(unknown0)
+        for t in range(T):
+            logits = transformer_call(s)
+            ratio = 1.0 * (t + 1) / T
+            k = mask_len(n0, gamma(ratio))
+            sampled, selp = maskgit_sample(logits, s, mask_id, site=self._site_sample)
+            s = maskgit_remask(selp, k, temperature * (1.0 - ratio), sampled, mask_id,
+                               site=self._site_sample)
+        return s
+
+    def first_pass(self, s_l: torch.Tensor, unknown_number_in_the_beginning_l,
+                   class_condition: Union[torch.Tensor, None], gamma: Callable, device):
+        """maskgit.py:294-355."""
+        return self._decode_pass(
+            lambda s: self.masked_prediction(self.transformer_l, class_condition, s), s_l,
+            self.mask_token_ids["lf"], self.T["lf"], self.choice_temperature_l,
+            unknown_number_in_the_beginning_l, gamma)
+
+    def second_pass(self, s_l: torch.Tensor, s_h: torch.Tensor, unknown_number_in_the_beginning_h,
+                    class_condition: Union[torch.Tensor, None], gamma: Callable, device):
+        """maskgit.py:357-411."""
+        return self._decode_pass(
+            lambda s: self.masked_prediction(self.transformer_h, class_condition, s_l, s), s_h,
+            self.mask_token_ids["hf"], self.T["hf"], self.choice_temperature_h,
+            unknown_number_in_the_beginning_h, gamma)
+
+    @torch.no_grad()
+    def iterative_decoding(self, num=1, mode="cosine", class_index=None, device="cpu"):
+        """maskgit.py:413-446 -> (s_l (num, n), s_h (num, m)) int64, on `device`.  Every
+        step stays on the device; the only host values are the per-step mask lengths,
+        known in advance (all tokens start masked)."""
+        s_l = self.create_input_tokens_normal(num, self.num_tokens_l, self.mask_token_ids["lf"],
+                                              device)
+        s_h = self.create_input_tokens_normal(num, self.num_tokens_h, self.mask_token_ids["hf"],
+                                              device)
+        gamma = self.gamma_func(mode)
+        class_condition = (torch.full((num, 1), int(class_index), dtype=torch.int32, device=device)
+                           if class_index is not None else None)
+        s_l = self.first_pass(s_l, self.num_tokens_l, class_condition, gamma, device)
+        s_h = self.second_pass(s_l, s_h, self.num_tokens_h, class_condition, gamma, device)
+        return s_l, s_h
+
     def decode_token_ind_to_timeseries(self, s: torch.Tensor, frequency: str,
                                        return_representations: bool = False):
         """maskgit.py:448-477."""
-        from ..hip.xf import embedding
         frequency = frequency.lower()
         assert frequency in ["lf", "hf"]
         vq_model = self.vq_model_l if frequency == "lf" else self.vq_model_h
@@ -160,10 +211,9 @@ class MaskGIT(nn.Module):
         H_prime = self.H_prime_l if frequency == "lf" else self.H_prime_h
         W_prime = self.W_prime_l if frequency == "lf" else self.W_prime_h
         with torch.no_grad():
-            zq = embedding(s, vq_model._codebook.embed)           # (b n d)
-            zq = vq_model.project_out(zq)
-            b, n, c = zq.shape
-            zq = zq.transpose(1, 2).reshape(b, c, H_prime, W_prime)
+            # project_out is Identity (codebook_dim == dim), so the lookup goes straight
+            # into the decoder's (b, c, h, w) layout
+            zq = codebook_gather_nchw(s, vq_model._codebook.embed, H_prime, W_prime)
             xhat = decoder(zq)
         if return_representations:
             return xhat, zq
