@@ -56,11 +56,14 @@ def synthetic_batch(seed, device):
 
 
 class JointTrainer:
-    """stage1 step then stage2 step (stage2 trains on a frozen snapshot of stage1).
+    """stage1 step and stage2 step (stage2 trains on a frozen snapshot of stage1).
 
-    Graph mode (default): the step is captured as three hipGraph segments
-      [advance seed, zero_grad, stage1 fwd+bwd] -> [codebook EMA, AdamW1, zero_grad,
-      stage2 fwd+bwd] -> [AdamW2]
+    The two steps are independent (the stage2 prior reads the frozen stage1, never the
+    one being trained), so stage2's forward+backward runs on a side stream concurrently
+    with stage1's, each with its own LF||HF branches (timevqvae.hip.streams).
+    Graph mode (default): the step is captured as two hipGraph segments
+      [advance seed, zero_grad x2, stage1 fwd+bwd || stage2 fwd+bwd]
+        -> [codebook EMA (if deferred), AdamW1, AdamW2]
     with the DP all-reduces (flat gradients, sync_codebook statistics) and the LR
     schedulers run eagerly between / before the segments.
     """
@@ -89,35 +92,46 @@ class JointTrainer:
         self.device = device
         self.graph = None
         self._pending = []
+        self.overlap = True
 
     def _allreduce(self, opt):
         if self.world > 1:
             dist.all_reduce(opt.flat_grad)
             opt.flat_grad.mul_(1.0 / self.world)
 
+    def _fwd_bwd(self, batch, defer):
+        """zero_grad, then stage2 fwd+bwd (side stream) || stage1 fwd+bwd; every stream is
+        joined when the region ends.  Returns (out1, out2, deferred codebook updates)."""
+        import contextlib
+        from timevqvae.hip import streams
+        from timevqvae.hip.vq import deferred_codebook_updates
+        self.opt1.zero_grad()
+        self.opt2.zero_grad()
+        with streams.concurrent():
+            with streams.branch(self.device, "stage2", enabled=self.overlap):
+                out2 = self.s2.training_step(batch, 0)
+                out2["loss"].backward()
+            with (deferred_codebook_updates() if defer else contextlib.nullcontext([])) as pend:
+                out1 = self.s1.training_step(batch, 0)
+            out1["loss"].sum().backward()
+        return out1, out2, pend
+
     def step(self, batch):
         if self.graph is not None:
-            return self.graph.replay()[:2]
+            return self.graph.replay()[0]
         from timevqvae.hip import rng
         rng.advance(self.device)
-        self.opt1.zero_grad()
-        out1 = self.s1.training_step(batch, 0)
-        out1["loss"].sum().backward()
+        out1, out2, _ = self._fwd_bwd(batch, defer=False)
         self._allreduce(self.opt1)
-        self.opt1.step()
-        self.opt2.zero_grad()
-        out2 = self.s2.training_step(batch, 0)
-        out2["loss"].backward()
         self._allreduce(self.opt2)
+        self.opt1.step()
         self.opt2.step()
         return out1, out2
 
     def capture(self, batch):
         """Capture the step (runs 2 eager warmup steps first)."""
-        import contextlib
         from timevqvae.hip import rng
         from timevqvae.hip.graph import StepGraph
-        from timevqvae.hip.vq import deferred_codebook_updates
         scheds = (self.s1._sched, self.s2._sched)
         self.s1._sched = self.s2._sched = None  # stepped on the host before each replay
         defer = self.world > 1  # sync_codebook all-reduce must sit between segments
@@ -130,15 +144,12 @@ class JointTrainer:
 
         def seg1():
             rng.advance(self.device)
-            self.opt1.zero_grad()
-            with (deferred_codebook_updates() if defer else contextlib.nullcontext([])) as pend:
-                out1 = self.s1.training_step(batch, 0)
-            self._pending = pend
-            out1["loss"].sum().backward()
-            return out1
+            out1, out2, self._pending = self._fwd_bwd(batch, defer)
+            return out1, out2
 
         def between1():
             self._allreduce(self.opt1)
+            self._allreduce(self.opt2)
             for u in self._pending:
                 u.reduce()
 
@@ -146,19 +157,9 @@ class JointTrainer:
             for u in self._pending:
                 u.apply()
             self.opt1.step(lr_on_device=True)
-            self.opt2.zero_grad()
-            out2 = self.s2.training_step(batch, 0)
-            out2["loss"].backward()
-            return out2
-
-        def between2():
-            self._allreduce(self.opt2)
-
-        def seg3():
             self.opt2.step(lr_on_device=True)
 
-        self.graph = StepGraph([seg1, seg2, seg3], [between1, between2, None], warmup=2,
-                               before=before).capture()
+        self.graph = StepGraph([seg1, seg2], [between1, None], warmup=2, before=before).capture()
 
 
 def roofline_leg(device):

@@ -167,3 +167,36 @@ def measure(threads, steps=2, warmup=1, B=256):
     for _ in range(steps):
         js.step()
     return (time.perf_counter() - t0) / steps
+
+
+def measure_sampler(threads, num=256, reps=1, seed=0, K=512, hid=128, n_classes=5, T=256, C=6):
+    """Seconds per `num` unconditional samples of the CPU restatement: iterative_decoding
+    (maskgit.py:413-446: 10 LF + 1 HF steps, torch sampling) + decode_token_ind_to_timeseries
+    for LF and HF (maskgit.py:448-477) -- the work of generation/sampler.py per batch."""
+    torch.set_num_threads(threads)
+    spec = O.Stage1Spec(T, C, 4, hid)
+    sd = _init_stage1(spec, K, hid, seed)
+    xl = _init_xf("lf", K, hid, 128, 4, 2, 24, n_classes, seed + 1)
+    xh = _init_xf("hf", K, hid, 32, 1, 1, 96, n_classes, seed + 2)
+    e = O.Ctx(False)
+    uncond = lambda b: torch.full((b, 1), n_classes, dtype=torch.int64)  # noqa: E731
+    tf_l = lambda s: O.transformer_forward(e, xl, "lf", s, None, uncond(s.shape[0]), K, 2, 4)  # noqa: E731
+    tf_h = lambda sl, sh: O.transformer_forward(e, xh, "hf", sl, sh, uncond(sl.shape[0]), K, 1, 1)  # noqa: E731
+
+    def run():
+        with torch.no_grad():
+            s_l, s_h = O.iterative_decoding_torch(tf_l, tf_h, num, 24, 96, K, K, {"lf": 10, "hf": 1},
+                                                  10, 4)
+            out = 0
+            for br, s, plan, band, W in (("l", s_l, spec.dec_l, O.band_lf, 8),
+                                         ("h", s_h, spec.dec_h, O.band_hf, 32)):
+                z = F.embedding(s, sd[f"vq_model_{br}._codebook.embed"])
+                z = z.transpose(1, 2).reshape(num, hid, 3, W)
+                out = out + O.decoder_forward(e, sd, f"decoder_{br}.", z, plan, band, C, T)
+            return out
+
+    run()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    return (time.perf_counter() - t0) / reps

@@ -5,9 +5,11 @@ conv2d          nn.Conv2d  (VQVAEEncBlock replicate 3x4 s(1,2); ResBlock 3x3; 1x
 conv_transpose2d nn.ConvTranspose2d 3x4 s(1,2) (VQVAEDecBlock, decoder tail)
 Backward: dgrad (T/F gathers), wgrad (split positions, deterministic), bias = channel sum.
 """
+import contextlib
+
 import torch
 
-from . import rng
+from . import rng, streams
 from ._native import call, grad_sink, ptr, stream_ptr, value
 
 
@@ -98,11 +100,14 @@ class _Conv2d(torch.autograd.Function):
             w_p, b_p = ctx.params
             sw, sb = grad_sink(w_p), grad_sink(b_p) if has_b else None
             direct = need_w and sw is not None and (not need_b or sb is not None)
-            dwt = sw if direct else torch.empty_like(w4)
-            dbt = (sb if direct else torch.empty(Co, device=dev)) if need_b else None
-            ws = _conv_ws(OP_WGRAD, dev, B, Ci, H, Wi, Co, KH, KW, SW, replicate, required=True)
-            call("tvq_conv2d_wgrad", ptr(x4), B, Ci, H, Wi, ptr(gd), Co, Wo, KH, KW, SW,
-                 int(replicate), ptr(dwt), ptr(dbt), int(direct), ptr(ws), s)
+            # gradients into the flat sinks are off the critical path: aux stream
+            with (streams.offload(x4, gd) if direct else contextlib.nullcontext()):
+                dwt = sw if direct else torch.empty_like(w4)
+                dbt = (sb if direct else torch.empty(Co, device=dev)) if need_b else None
+                ws = _conv_ws(OP_WGRAD, dev, B, Ci, H, Wi, Co, KH, KW, SW, replicate,
+                              required=True)
+                call("tvq_conv2d_wgrad", ptr(x4), B, Ci, H, Wi, ptr(gd), Co, Wo, KH, KW, SW,
+                     int(replicate), ptr(dwt), ptr(dbt), int(direct), ptr(ws), stream_ptr())
             if not direct:
                 dw = (dwt.squeeze(2) if wdim == 3 else dwt) if need_w else None
                 db = dbt
@@ -155,13 +160,16 @@ class _ConvT2d(torch.autograd.Function):
         w_p, b_p = ctx.params
         if ctx.needs_input_grad[1]:
             sw = grad_sink(w_p)
-            dwt = sw if sw is not None else torch.empty_like(w)
-            ws = _conv_ws(OP_T_WGRAD, x.device, B, Ci, H, Wi, Co, KH, KW, SW, required=True)
-            call("tvq_convT2d_wgrad", ptr(x), B, Ci, H, Wi, ptr(g), Co, Wo, KH, KW, SW, ptr(dwt),
-                 int(sw is not None), ptr(ws), s)
+            with (streams.offload(x, g) if sw is not None else contextlib.nullcontext()):
+                dwt = sw if sw is not None else torch.empty_like(w)
+                ws = _conv_ws(OP_T_WGRAD, x.device, B, Ci, H, Wi, Co, KH, KW, SW, required=True)
+                call("tvq_convT2d_wgrad", ptr(x), B, Ci, H, Wi, ptr(g), Co, Wo, KH, KW, SW,
+                     ptr(dwt), int(sw is not None), ptr(ws), stream_ptr())
             dw = None if sw is not None else dwt
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = _bias_grad(g, x.device, grad_sink(b_p))
+            sb = grad_sink(b_p)
+            with (streams.offload(g) if sb is not None else contextlib.nullcontext()):
+                db = _bias_grad(g, x.device, sb)
         return dx, dw, db, None
 
 

@@ -13,7 +13,7 @@ drawn on the device under `rng.device_decisions()`), fixed input buffers.
 """
 import torch
 
-from . import rng
+from . import rng, streams
 
 
 class StepGraph:
@@ -35,6 +35,7 @@ class StepGraph:
         outs = []
         for seg, btw in zip(self.segments, self.between):
             outs.append(seg())
+            streams.join(backward_done=True)
             if btw is not None:
                 btw()
         return outs
@@ -54,6 +55,7 @@ class StepGraph:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool):
                     out = seg()
+                    streams.join(backward_done=True)  # side-stream branches rejoin the capture
                 self.graphs.append(g)
                 self.outputs.append(out)
         return self

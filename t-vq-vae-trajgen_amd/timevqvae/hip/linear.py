@@ -1,6 +1,7 @@
 """Dense GEMM ops (nn.Linear over the last dim) on the HIP path."""
 import torch
 
+from . import streams
 from ._native import call, grad_sink, ptr, stream_ptr, value
 
 
@@ -21,18 +22,23 @@ def gemm(A, sam, sak, B, sbk, sbn, M, N, K, out=None, ldc=None, alpha=1.0, bias=
 def _bias_grad_rows(g2, sink=None):
     """Column sums of a row-major (M, N) gradient: returned, or accumulated into `sink`."""
     M, N = g2.shape
-    out = sink if sink is not None else torch.empty(N, device=g2.device, dtype=torch.float32)
+    if sink is not None:  # into the flat gradient: off the critical path
+        with streams.offload(g2):
+            ws = torch.empty(value("tvq_channel_sum_workspace", M, N, 1), device=g2.device)
+            call("tvq_channel_sum", ptr(g2), M, N, 1, ptr(sink), 1, ptr(ws), stream_ptr())
+        return None
+    out = torch.empty(N, device=g2.device, dtype=torch.float32)
     ws = torch.empty(value("tvq_channel_sum_workspace", M, N, 1), device=g2.device)
-    call("tvq_channel_sum", ptr(g2), M, N, 1, ptr(out), int(sink is not None), ptr(ws),
-         stream_ptr())
-    return None if sink is not None else out
+    call("tvq_channel_sum", ptr(g2), M, N, 1, ptr(out), 0, ptr(ws), stream_ptr())
+    return out
 
 
 def weight_grad(g, x2, w_param, M, N, K):
     """dW = g^T x (N x K): accumulated into the flat grad view when available."""
     sink = grad_sink(w_param)
-    if sink is not None:
-        gemm(g, 1, N, x2, K, 1, N, K, M, out=sink, ldc=K, accumulate=True)
+    if sink is not None:  # into the flat gradient: off the critical path
+        with streams.offload(g, x2):
+            gemm(g, 1, N, x2, K, 1, N, K, M, out=sink, ldc=K, accumulate=True)
         return None
     return gemm(g, 1, N, x2, K, 1, N, K, M)
 

@@ -9,6 +9,7 @@ through param_groups[0]['lr'].
 """
 import torch
 
+from . import streams
 from ._native import call, ptr, stream_ptr
 
 
@@ -51,6 +52,7 @@ class FusedAdamW(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None, lr_on_device=False):
         loss = closure() if closure is not None else None
+        streams.join(self.flat.device, backward_done=True)  # grads written on side streams
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         s = stream_ptr()

@@ -10,6 +10,7 @@ import contextlib
 
 import torch
 
+from . import streams
 from ._native import call, ptr, stream_ptr, value
 
 _pending = None  # list of CodebookUpdate while a deferral scope is active
@@ -80,6 +81,7 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
     M = B * N
     _check_dense(x)
     dev = x.device
+    streams.wait_fence(embed.data_ptr())  # an EMA update of this codebook may be in flight
     s = stream_ptr()
     ee = torch.empty(K, device=dev, dtype=torch.float32)
     call("tvq_vq_sqnorm", ptr(embed), K, D, ptr(ee), s)
@@ -92,6 +94,27 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
     sB, sN, sD = x.stride()
     call("tvq_vq_assign", ptr(x), B, N, D, sB, sN, sD, ptr(embed), ptr(ee), K,
          int(bool(straight_through)), ptr(out), ptr(idx), ptr(idx32), ptr(partial), s)
+    commit = None
+    if straight_through:  # the loss reads it: stays on the current stream
+        commit = torch.empty((), device=dev, dtype=torch.float32)
+        call("tvq_vq_finalize", None, None, K, D, float(eps), None, None, M, None, ptr(partial),
+             nb, ptr(commit), s)
+    # per-code statistics, EMA and perplexity: nothing downstream of the quantised output
+    # waits for them (inside streams.concurrent() they run on the aux stream; the region's
+    # join completes them before anyone reads the perplexity or the codebook)
+    with streams.offload(x, idx32, kind="vq"):
+        counts, perp = _codebook_stats(x, idx32, embed, cluster_size, embed_avg, ema, decay,
+                                       eps, sync)
+    return out, idx, commit, perp, counts
+
+
+def _codebook_stats(x, idx32, embed, cluster_size, embed_avg, ema, decay, eps, sync):
+    B, N, D = x.shape
+    K = embed.shape[0]
+    M = B * N
+    dev = x.device
+    sB, sN, sD = x.stride()
+    s = stream_ptr()
     counts = torch.empty(K, device=dev, dtype=torch.int32)
     cs_b = torch.empty(K, device=dev, dtype=torch.float32)
     es_b = torch.empty((K, D), device=dev, dtype=torch.float32) if ema else None
@@ -99,11 +122,10 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
     call("tvq_vq_stats", ptr(x), B, N, D, sB, sN, sD, ptr(idx32), K, ptr(counts), ptr(cs_b),
          ptr(es_b), ptr(ws), s)
     perp = torch.empty((), device=dev, dtype=torch.float32)
-    commit = torch.empty((), device=dev, dtype=torch.float32) if straight_through else None
     if ema and _pending is not None:
         _pending.append(CodebookUpdate(cs_b, es_b, cluster_size, embed_avg, embed, decay, eps, sync))
         call("tvq_vq_finalize", None, None, K, D, float(eps), None, ptr(counts), M, ptr(perp),
-             ptr(partial), nb if partial is not None else 0, ptr(commit), s)
+             None, 0, None, s)
     elif ema:
         if sync is not None:
             sync(cs_b)
@@ -112,12 +134,12 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
         call("tvq_vq_ema", ptr(cs_b), ptr(es_b), K, D, float(decay), ptr(cluster_size),
              ptr(embed_avg), s)
         call("tvq_vq_finalize", ptr(cluster_size), ptr(embed_avg), K, D, float(eps), ptr(embed),
-             ptr(counts), M, ptr(perp), ptr(partial), nb if partial is not None else 0,
-             ptr(commit), s)
+             ptr(counts), M, ptr(perp), None, 0, None, s)
+        streams.fence(embed.data_ptr())
     else:
         call("tvq_vq_finalize", None, None, K, D, float(eps), None, ptr(counts), M, ptr(perp),
-             ptr(partial), nb if partial is not None else 0, ptr(commit), s)
-    return out, idx, commit, perp, counts
+             None, 0, None, s)
+    return counts, perp
 
 
 class _VQStraightThrough(torch.autograd.Function):

@@ -1,9 +1,10 @@
 """MaskGIT transformer ops on the HIP path (include/tvq.h §MaskGIT transformer)."""
+import contextlib
 import math
 
 import torch
 
-from . import rng
+from . import rng, streams
 from ._native import call, grad_sink, ptr, stream_ptr, value
 from .linear import _bias_grad_rows, gemm, weight_grad
 
@@ -196,11 +197,14 @@ class _Embedding(torch.autograd.Function):
         M = idx.numel()
         g2 = g.reshape(M, D).contiguous()
         sink = grad_sink(ctx.table)
-        tg = sink if sink is not None else torch.empty((V, D), device=g.device)
-        ws = torch.empty(value("tvq_embedding_bwd_workspace", M, V), device=g.device,
-                         dtype=torch.int32)
-        call("tvq_embedding_bwd", ptr(idx), M, D, ptr(g2), D, V, ptr(tg), int(sink is not None),
-             int(mask_id), float(drop_p), ptr(ctx.seed), off, ptr(ws), stream_ptr())
+        # into the flat gradient: aux stream (same one as the tied-logits table grad)
+        with (streams.offload(idx, g2) if sink is not None else contextlib.nullcontext()):
+            tg = sink if sink is not None else torch.empty((V, D), device=g.device)
+            ws = torch.empty(value("tvq_embedding_bwd_workspace", M, V), device=g.device,
+                             dtype=torch.int32)
+            call("tvq_embedding_bwd", ptr(idx), M, D, ptr(g2), D, V, ptr(tg),
+                 int(sink is not None), int(mask_id), float(drop_p), ptr(ctx.seed), off, ptr(ws),
+                 stream_ptr())
         return None, (None if sink is not None else tg), None, None, None
 
 

@@ -23,7 +23,7 @@ from typing import Union
 import torch
 import torch.nn as nn
 
-from ..hip import rng
+from ..hip import rng, streams
 from ..hip.conv import conv2d
 from ..hip.linear import _bias_grad_rows, gemm, linear
 from ..hip.norm import bn_snake
@@ -201,16 +201,20 @@ class _TiedLogits(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.W)
             if sink is not None:  # tied table: accumulate next to the embedding-lookup grad
-                gemm(g2, 1, K, h2, D, 1, K, D, M, out=sink, ldc=D, accumulate=True)
+                # (both on the aux stream of this stream, so their order is fixed)
+                with streams.offload(g2, h2):
+                    gemm(g2, 1, K, h2, D, 1, K, D, M, out=sink, ldc=D, accumulate=True)
             else:
                 dW = torch.zeros_like(W)
                 gemm(g2, 1, K, h2, D, 1, K, D, M, out=dW, ldc=D)
         if ctx.needs_input_grad[2]:
-            s = _bias_grad_rows(g2.reshape(B, n * K)).reshape(n, K)  # sum over the batch
             sink = grad_sink(ctx.bias)
             if sink is not None:
-                sink[:, :K] += s
+                with streams.offload(g2):
+                    s = _bias_grad_rows(g2.reshape(B, n * K)).reshape(n, K)  # sum over the batch
+                    sink[:, :K] += s
             else:
+                s = _bias_grad_rows(g2.reshape(B, n * K)).reshape(n, K)
                 dbias = torch.zeros(bshape, device=g.device)
                 dbias[:, :K] = s
         return dh, dW, dbias, None

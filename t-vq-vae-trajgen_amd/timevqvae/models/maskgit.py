@@ -13,7 +13,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..hip import rng
+from ..hip import rng, streams
 from ..hip.sample import codebook_gather_nchw, mask_len, maskgit_remask, maskgit_sample
 from ..hip.signal import stft_encode
 from ..hip.xf import mask_tokens, masked_cross_entropy
@@ -100,8 +100,12 @@ class MaskGIT(nn.Module):
     def encode_tokens(self, x):
         """Both branches from one fused STFT pass: (s_l (b n), s_h (b m)) int64."""
         st = stft_encode(x, enc_l=True, enc_h=True)
+        with streams.branch(x.device) as br:  # HF encoder concurrently with LF
+            br.inputs(st)
+            _, s_h, _, _ = quantize(self.encoder_h.encode_timefreq(st["enc_h"]), self.vq_model_h)
+            br.outputs(s_h)
         _, s_l, _, _ = quantize(self.encoder_l.encode_timefreq(st["enc_l"]), self.vq_model_l)
-        _, s_h, _, _ = quantize(self.encoder_h.encode_timefreq(st["enc_h"]), self.vq_model_h)
+        br.join()
         return s_l, s_h
 
     def masked_prediction(self, transformer, class_condition, *s_in):
@@ -123,10 +127,14 @@ class MaskGIT(nn.Module):
         s_l, s_h = self.encode_tokens(x)
         s_l_M, keep_l = self._randomly_mask_tokens(s_l, self.mask_token_ids["lf"], x.device)
         s_h_M, keep_h = self._randomly_mask_tokens(s_h, self.mask_token_ids["hf"], x.device)
+        with streams.branch(x.device) as br:  # HF transformer concurrently with LF
+            br.inputs(y, s_l_M, s_h_M, s_h, keep_h)
+            logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
+            mask_pred_loss_h = masked_cross_entropy(logits_h, s_h, keep_h)
+            br.outputs(mask_pred_loss_h)
         logits_l = self.masked_prediction(self.transformer_l, y, s_l_M)
-        logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
         mask_pred_loss_l = masked_cross_entropy(logits_l, s_l, keep_l)
-        mask_pred_loss_h = masked_cross_entropy(logits_h, s_h, keep_h)
+        br.join()
         return mask_pred_loss_l + mask_pred_loss_h, (mask_pred_loss_l, mask_pred_loss_h)
 
     def _randomly_mask_tokens(self, s, mask_token_id, device):

@@ -10,6 +10,7 @@ One fused STFT kernel produces both encoder inputs and both targets
 import torch
 import torch.nn as nn
 
+from ..hip import streams
 from ..hip.loss import l1_loss, mse_loss
 from ..hip.optim import FusedAdamW
 from ..hip.signal import stft_encode
@@ -57,18 +58,24 @@ class Stage1(nn.Module):
         perplexities = {"LF": 0.0, "HF": 0.0}
         need_tgt = not return_x_rec
         s = stft_encode(x, enc_l=True, enc_h=True, tgt_l=need_tgt, tgt_h=need_tgt)
+        # the HF branch runs on the side stream, concurrently with the LF branch
+        with streams.branch(x.device) as br:
+            br.inputs(s)
+            z_h = self.encoder_h.encode_timefreq(s["enc_h"])
+            z_q_h, s_h, vq_loss_h, perplexity_h = quantize(z_h, self.vq_model_h)
+            xhat_h = self.decoder_h(z_q_h)
+            loss_h = None if return_x_rec else l1_loss(s["tgt_h"], xhat_h)
+            br.outputs(xhat_h, loss_h, vq_loss_h, perplexity_h)
         z_l = self.encoder_l.encode_timefreq(s["enc_l"])
         z_q_l, s_l, vq_loss_l, perplexity_l = quantize(z_l, self.vq_model_l)
         xhat_l = self.decoder_l(z_q_l)
-        z_h = self.encoder_h.encode_timefreq(s["enc_h"])
-        z_q_h, s_h, vq_loss_h, perplexity_h = quantize(z_h, self.vq_model_h)
-        xhat_h = self.decoder_h(z_q_h)
+        br.join()
         if return_x_rec:
             return xhat_l + xhat_h
         recons_loss["LF.time"] = mse_loss(s["tgt_l"], xhat_l)
         perplexities["LF"] = perplexity_l
         vq_losses["LF"] = vq_loss_l
-        recons_loss["HF.time"] = l1_loss(s["tgt_h"], xhat_h)
+        recons_loss["HF.time"] = loss_h
         perplexities["HF"] = perplexity_h
         vq_losses["HF"] = vq_loss_h
         return recons_loss, vq_losses, perplexities

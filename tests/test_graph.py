@@ -73,3 +73,28 @@ def test_graph_replays_advance(cuda):
     l2 = float(o1["loss"].sum())
     assert not torch.equal(p0, p1) and not torch.equal(p1, tr.opt1.flat)
     assert l1 != l2
+
+
+def test_streams_match_single_stream(cuda):
+    """The LF/HF branches on the side stream and the offloaded weight-gradient /
+    codebook-statistics work change the schedule, never the result: eager steps with
+    streams equal single-stream steps bit for bit (losses, parameters, optimizer state,
+    codebooks), at the bench's shape family (config B dims, reduced batch), dropout on.
+    test_graph_replay_matches_eager then covers the graphed multi-stream step."""
+    import bench
+    from timevqvae.hip import streams
+    batch = _batch(cuda, B=32, C=6, L=256)
+    prev = streams.ENABLED
+    try:
+        streams.ENABLED = False
+        single = bench.JointTrainer(cuda, 1, cfg=_cfg(), length=256, channels=6)
+        ls = [tuple(float(o["loss"].detach().sum()) for o in single.step(batch)) for _ in range(3)]
+        streams.ENABLED = True
+        multi = bench.JointTrainer(cuda, 1, cfg=_cfg(), length=256, channels=6)
+        lm = [tuple(float(o["loss"].detach().sum()) for o in multi.step(batch)) for _ in range(3)]
+    finally:
+        streams.ENABLED = prev
+    torch.cuda.synchronize()
+    assert ls == lm
+    for a, b in zip(_state(single), _state(multi)):
+        assert torch.equal(a, b)

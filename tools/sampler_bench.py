@@ -1,6 +1,8 @@
 """Sampler throughput (BASELINE config 5): MaskGIT iterative decoding of `num` trajectories
 (10 LF steps + 1 HF step) + LF/HF decoding, at the bench architecture (config B dims,
-random-init weights).  usage: python tools/sampler_bench.py [num] [reps]"""
+random-init weights), with the CPU restatement's rate beside it (oracle/cpu_baseline.py
+measure_sampler, a bounded sample of 256 trajectories).
+usage: python tools/sampler_bench.py [num] [reps] [--no-cpu-baseline] [--graph]"""
 import json
 import os
 import sys
@@ -15,8 +17,9 @@ import bench  # noqa: E402
 
 
 def main():
-    num = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    pos = [a for a in sys.argv[1:] if not a.startswith("--")]
+    num = int(pos[0]) if pos else 1024
+    reps = int(pos[1]) if len(pos) > 1 else 3
     dev = torch.device("cuda", 0)
     mg = bench.JointTrainer(dev, 1).s2.maskgit.eval()
 
@@ -33,9 +36,18 @@ def main():
             x = run()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / reps
-    print(json.dumps({"metric": "MaskGIT sampling (iterative decoding + decode), trajectories/s",
-                      "num": num, "ms_per_batch": round(dt * 1e3, 2),
-                      "trajectories_per_s": round(num / dt, 1), "shape": list(x.shape)}))
+    res = {"metric": "MaskGIT sampling (iterative decoding + decode), trajectories/s",
+           "num": num, "ms_per_batch": round(dt * 1e3, 2),
+           "trajectories_per_s": round(num / dt, 1), "shape": list(x.shape)}
+    if "--no-cpu-baseline" not in sys.argv:
+        from oracle import cpu_baseline
+        threads = int(os.environ.get("TVQ_CPU_THREADS", min(16, os.cpu_count() or 1)))
+        s = cpu_baseline.measure_sampler(threads, num=256)
+        res["cpu_baseline"] = {"value": round(256 / s, 2), "unit": "trajectories/s",
+                               "cores": threads, "kind": "port",
+                               "sample": f"256 trajectories (1 timed rep after 1 warmup) of "
+                                         f"oracle/cpu_baseline.py measure_sampler: {s:.2f} s"}
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":
