@@ -59,10 +59,11 @@ class JointTrainer:
     """stage1 step and stage2 step (stage2 trains on a frozen snapshot of stage1).
 
     The two steps are independent (the stage2 prior reads the frozen stage1, never the
-    one being trained), so stage2's forward+backward runs on a side stream concurrently
-    with stage1's, each with its own LF||HF branches (timevqvae.hip.streams).
+    one being trained), so they run concurrently: stage1's LF and HF bands each do
+    forward+backward on a side stream while stage2 runs on the current stream with its
+    HF encoder / HF transformer on side streams (timevqvae.hip.streams).
     Graph mode (default): the step is captured as two hipGraph segments
-      [advance seed, zero_grad x2, stage1 fwd+bwd || stage2 fwd+bwd]
+      [advance seed, zero_grad x2, stage1 LF | stage1 HF | stage2 fwd+bwd]
         -> [codebook EMA (if deferred), AdamW1, AdamW2]
     with the DP all-reduces (flat gradients, sync_codebook statistics) and the LR
     schedulers run eagerly between / before the segments.
@@ -92,7 +93,6 @@ class JointTrainer:
         self.device = device
         self.graph = None
         self._pending = []
-        self.overlap = True
 
     def _allreduce(self, opt):
         if self.world > 1:
@@ -100,21 +100,25 @@ class JointTrainer:
             opt.flat_grad.mul_(1.0 / self.world)
 
     def _fwd_bwd(self, batch, defer):
-        """zero_grad, then stage2 fwd+bwd (side stream) || stage1 fwd+bwd; every stream is
-        joined when the region ends.  Returns (out1, out2, deferred codebook updates)."""
+        """zero_grad, then stage1's LF and HF bands (forward+backward, one side stream
+        each) || stage2 forward+backward on the current stream (with its own HF side
+        streams); every stream is joined when the region ends.
+        Returns (out1, out2, deferred codebook updates)."""
         import contextlib
         from timevqvae.hip import streams
         from timevqvae.hip.vq import deferred_codebook_updates
         self.opt1.zero_grad()
         self.opt2.zero_grad()
+        only = os.environ.get("TVQ_BENCH_ONLY")  # diagnosis: time one stage alone
         with streams.concurrent():
-            with streams.branch(self.device, "stage2", enabled=self.overlap):
+            with (deferred_codebook_updates() if defer else contextlib.nullcontext([])) as pend:
+                hist1 = self.s1.forward_backward(batch, 0) if only != "stage2" else None
+            if only != "stage1":
                 out2 = self.s2.training_step(batch, 0)
                 out2["loss"].backward()
-            with (deferred_codebook_updates() if defer else contextlib.nullcontext([])) as pend:
-                out1 = self.s1.training_step(batch, 0)
-            out1["loss"].sum().backward()
-        return out1, out2, pend
+            else:
+                out2 = {"loss": torch.zeros(())}
+        return (hist1() if hist1 else {"loss": torch.zeros(())}), out2, pend
 
     def step(self, batch):
         if self.graph is not None:

@@ -33,6 +33,12 @@ typedef void* tvq_stream_t; /* hipStream_t */
 
 const char* tvq_last_error(void);
 int tvq_abi_version(void);
+/* Register a zeroed pool of n int32 counters on `device` (a HIP device index).  The
+ * kernels that finish a grid-level reduction in their last-arriving block (BatchNorm /
+ * Snake statistics, column sums, split-K slabs) take slots from it and leave them
+ * zero.  Without a pool, those reductions use a separate finishing launch (same
+ * result).  Call before the first launch on that device, outside graph capture. */
+int tvq_counter_pool(int64_t device, int32_t* zeroed, int64_t n);
 
 /* ---------------------------------------------------------------- VQ codebook
  * Replaces EuclideanCodebook.forward (timevqvae/models/vq.py:197-251) and the

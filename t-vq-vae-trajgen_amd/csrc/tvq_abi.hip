@@ -1,6 +1,10 @@
 // ABI plumbing: thread-local error string and version.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
 
 #include "tvq_common.h"
 
@@ -12,7 +16,56 @@ void set_error(const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
+
+namespace {
+struct CounterPool {
+  int* base = nullptr;
+  int64_t n = 0, cur = 0;
+};
+constexpr int kMaxDevices = 64;
+CounterPool g_pools[kMaxDevices];
+std::mutex g_pool_mu;
+// TVQ_FUSED_FINISH: comma list of the finish classes done in-launch (default
+// "norm,reduce"; "0" = none).  Split-K slabs (gemm, conv) finished by one block per
+// tile measured slower than the separate all-CU finishing launch, so they are off.
+bool fused_finish_enabled(FinishClass cls) {
+  static const unsigned mask = [] {
+    const char* e = getenv("TVQ_FUSED_FINISH");
+    const char* v = e ? e : "norm,reduce";
+    unsigned m = 0;
+    if (strstr(v, "norm")) m |= 1u << FIN_NORM;
+    if (strstr(v, "reduce")) m |= 1u << FIN_REDUCE;
+    if (strstr(v, "gemm")) m |= 1u << FIN_GEMM;
+    if (strstr(v, "conv")) m |= 1u << FIN_CONV;
+    return m;
+  }();
+  return (mask >> cls) & 1u;
+}
+}  // namespace
+
+int* counters(int64_t k, FinishClass cls) {
+  if (k <= 0 || !fused_finish_enabled(cls)) return nullptr;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+  std::lock_guard<std::mutex> lock(g_pool_mu);
+  CounterPool& p = g_pools[dev];
+  if (!p.base || k > p.n) return nullptr;
+  if (p.cur + k > p.n) p.cur = 0;
+  int* r = p.base + p.cur;
+  p.cur += k;
+  return r;
+}
 }  // namespace tvq
+
+extern "C" int tvq_counter_pool(int64_t device, int32_t* zeroed, int64_t n) {
+  TVQ_CHECK_ARG(device >= 0 && device < tvq::kMaxDevices && (zeroed || n == 0) && n >= 0,
+                "tvq_counter_pool: bad arguments");
+  std::lock_guard<std::mutex> lock(tvq::g_pool_mu);
+  tvq::g_pools[device].base = zeroed;
+  tvq::g_pools[device].n = n;
+  tvq::g_pools[device].cur = 0;
+  return TVQ_OK;
+}
 
 extern "C" const char* tvq_last_error(void) { return tvq::g_err; }
 extern "C" int tvq_abi_version(void) { return 1; }

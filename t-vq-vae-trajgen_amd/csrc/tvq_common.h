@@ -13,6 +13,13 @@ namespace tvq {
 // thread-local last-error message returned by tvq_last_error()
 void set_error(const char* fmt, ...);
 
+// k zeroed int32 counters from the current device's pool (tvq_counter_pool), or nullptr
+// when no pool is registered / fused finishes are disabled (TVQ_FUSED_FINISH=0): the
+// caller then falls back to a separate finishing launch.  Slots are handed out round
+// robin; a kernel returns every counter it used to zero before it exits.
+enum FinishClass { FIN_NORM = 0, FIN_REDUCE = 1, FIN_GEMM = 2, FIN_CONV = 3 };
+int* counters(int64_t k, FinishClass cls);
+
 inline int launch_status(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -54,6 +61,36 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   float t = 0.f;
   for (int i = 0; i < nw; ++i) t += red[i];
   return t;
+}
+
+// Grid-level finish without a second launch: every block of a group publishes its
+// partial results, then takes a ticket; the block that draws the last ticket combines
+// the group's partials in a fixed order, so the result does not depend on arrival
+// order.  The L2s of the 8 XCDs are not coherent, and an agent-scope release fence
+// writes back a whole L2 (measured: 2x slower step), so partials are published with
+// write-through stores (st_wt: agent-scope relaxed atomic store, `sc1`), drained with
+// s_waitcnt vmcnt(0) before the ticket, and read back with ld_wt (`sc1` loads that do
+// not hit a stale L2 line).  The last block re-zeroes the counter for the next launch.
+template <typename T>
+__device__ __forceinline__ void st_wt(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T ld_wt(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Returns the same value in every thread of the block.
+__device__ __forceinline__ bool last_block(int* counter, int total) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's st_wt stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = atomicAdd(counter, 1);
+    s_last = t == total - 1;
+    if (s_last) atomicExch(counter, 0);
+  }
+  __syncthreads();
+  return s_last != 0;
 }
 
 // q = n / d by one v_mul_hi_u32 with m = ceil(2^32 / d): exact while n * d < 2^32

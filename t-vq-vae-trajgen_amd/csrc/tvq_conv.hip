@@ -114,7 +114,8 @@ __device__ __forceinline__ void epi_load_bias(float (&bv)[FN][4], const float* _
 template <int FN>
 __device__ __forceinline__ void epi_store(float* __restrict__ out, const Epi& e, uint64_t seed,
                                           const float (&bv)[FN][4], const floatx4 (&a)[FN],
-                                          int64_t ob, int64_t hw, int nbase, int N, bool pv) {
+                                          int64_t ob, int64_t hw, int nbase, int N, bool pv,
+                                          bool wt = false) {
   float v[FN][4];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
@@ -146,7 +147,10 @@ __device__ __forceinline__ void epi_store(float* __restrict__ out, const Epi& e,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = nbase + i * 16 + r;
-      if (pv && n < N) out[ob + (int64_t)n * hw] = v[i][r];
+      if (pv && n < N) {
+        if (wt) st_wt(out + ob + (int64_t)n * hw, v[i][r]);  // split-K slab, last-block finish
+        else out[ob + (int64_t)n * hw] = v[i][r];
+      }
     }
 }
 
@@ -274,9 +278,13 @@ template <int MODE, int KH, int KW, int SW, bool REPL, int TN, int TM, int WN, i
 __global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__ in,
                                                       const float* __restrict__ wt,
                                                       float* __restrict__ out, ConvGeom g, Epi e,
-                                                      int steps_per_split, int64_t zstride) {
+                                                      int steps_per_split, int64_t zstride,
+                                                      int* __restrict__ cnt,
+                                                      float* __restrict__ fout, Epi fe) {
   // split-K (gridDim.z > 1): block z covers K-steps [z*sps, (z+1)*sps) and stores raw
-  // partial sums to out + z*zstride (the caller passes a slab and a raw Epi)
+  // partial sums to out + z*zstride (the caller passes a slab and a raw Epi); with
+  // `cnt` the last split block of the tile then sums the slabs in split order and
+  // applies the real epilogue `fe` into `fout` (what conv_splitk_epi_kernel does)
   constexpr int KK = KH * KW;
   constexpr int FN = TN / WN / 16;
   constexpr int FM = TM / WM / 16;
@@ -306,6 +314,7 @@ __global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__
   }
   const int64_t plane = (int64_t)g.Hin * g.Win;
   const float* inb = in + (int64_t)pb * g.C * plane;
+  float* const slab = out;
   const int an_local = tid % TN, ak_base = tid / TN;
   const int an = n0 + an_local;
   const float* wrow = wt + (int64_t)(an < g.N ? an : 0) * g.wsn;
@@ -400,7 +409,26 @@ __global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__
 #pragma unroll
     for (int i = 0; i < FN; ++i) a[i] = acc[i][j];
     epi_store<FN>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + w, hw, nbase, g.N,
-                  pv);
+                  pv, cnt != nullptr);
+  }
+  if (cnt && last_block(cnt + blockIdx.y * gridDim.x + blockIdx.x, (int)gridDim.z)) {
+    const uint64_t fseed = fe.drop_p > 0.f ? mix_seed(fe.seed_ptr, fe.offset) : 0ull;
+    for (int idx = tid; idx < TM * TN; idx += 256) {
+      const int m = m0 + idx % TM, n = n0 + idx / TM;
+      if (m >= g.Mpos || n >= g.N) continue;
+      const uint32_t bh = fdiv((uint32_t)m, g.fd_wo);
+      const int w = m - (int)bh * g.Wo;
+      const int b = (int)fdiv((uint32_t)m, g.fd_hwo);
+      const int h = (int)bh - b * g.Hout;
+      const int64_t o = (((int64_t)b * g.N + n) * g.Hout + h) * g.Wo + w;
+      float v = 0.f;
+#pragma unroll 4
+      for (int z = 0; z < (int)gridDim.z; ++z) v += ld_wt(slab + (int64_t)z * zstride + o);
+      if (fe.bias) v += fe.bias[n];
+      if (fe.drop_p > 0.f) v = uniform01(fseed, (uint64_t)o) >= fe.drop_p ? v * fe.drop_scale : 0.f;
+      if (fe.residual) v += fe.residual[o];
+      fout[o] = v;
+    }
   }
 }
 
@@ -552,11 +580,21 @@ __global__ void replicate_fold_kernel(const float* __restrict__ dpad, int B, int
   }
 }
 
-// Per-channel sum over (B, HW) of a (B, C, HW) tensor: out[c] (+)= sum. Two stages,
-// deterministic.  Stage 1: partial[c][chunk]; stage 2: fixed-order sum.
+// Per-channel sum over (B, HW) of a (B, C, HW) tensor: out[c] (+)= sum, deterministic.
+// Stage 1: partial[c][chunk]; stage 2 (fixed-order sum) in the last block of channel c
+// when `cnt` is given, else chan_sum_final_kernel.
+__device__ __forceinline__ void chan_sum_final_one(const float* part, int chunks, int c,
+                                                   float* out, int accumulate) {
+  float s = 0.f;
+  for (int i = 0; i < chunks; ++i) s += ld_wt(part + (int64_t)c * chunks + i);
+  out[c] = accumulate ? out[c] + s : s;
+}
 __global__ __launch_bounds__(256) void chan_sum_partial_kernel(const float* __restrict__ x, int B,
                                                                int C, int HW, int chunks,
-                                                               float* __restrict__ part) {
+                                                               float* __restrict__ part,
+                                                               int* __restrict__ cnt,
+                                                               float* __restrict__ out,
+                                                               int accumulate) {
   __shared__ float red[4];
   const int c = blockIdx.x, ch = blockIdx.y;
   const int64_t per = ((int64_t)B * HW + chunks - 1) / chunks;
@@ -567,15 +605,15 @@ __global__ __launch_bounds__(256) void chan_sum_partial_kernel(const float* __re
     s += x[(b * C + c) * HW + p];
   }
   s = block_sum(s, red);
-  if (threadIdx.x == 0) part[(int64_t)c * chunks + ch] = s;
+  if (threadIdx.x == 0) st_wt(part + (int64_t)c * chunks + ch, s);
+  if (cnt && last_block(cnt + c, chunks) && threadIdx.x == 0)
+    chan_sum_final_one(part, chunks, c, out, accumulate);
 }
 __global__ void chan_sum_final_kernel(const float* __restrict__ part, int C, int chunks,
                                       float* __restrict__ out, int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  float s = 0.f;
-  for (int i = 0; i < chunks; ++i) s += part[(int64_t)c * chunks + i];
-  out[c] = accumulate ? out[c] + s : s;
+  chan_sum_final_one(part, chunks, c, out, accumulate);
 }
 
 // ---------------------------------------------------------------- host dispatch
@@ -1031,8 +1069,10 @@ static void whalo_blocking(int64_t N, int64_t C, int KK, int* FN, int* CB) {
 static bool whalo_plan(int B, int C, int Hin, int Win, int N, int Hout, int Wo, int KH, int KW,
                        int SW, int oh, int ow, int kcols, WHaloPlan* pl) {
   if (Wo % 4 != 0) return false;
-  // long images with many channels (the Upscale Conv1d) run better on the split GEMM
+  // long images with many channels (the Upscale Conv1d) and the 128x128 ResBlock convs
+  // run better on the split GEMM (tools/conv_shapes_bench.py: 148 vs 178 us at W 32)
   if (Hout * Wo > 128 && C > 64) return false;
+  if ((int64_t)C * N >= 128 * 128) return false;
   WHaloGeom g;
   g.B = B; g.C = C; g.Hin = Hin; g.Win = Win; g.N = N; g.Hout = Hout; g.Wo = Wo;
   g.oh = oh; g.ow = ow;
@@ -1149,19 +1189,21 @@ static int tap_splits(const ConvGeom& g, int KK, int* sps) {
 
 template <int MODE, int KH, int KW, int SW, bool REPL, int BK>
 static void launch_tap(const float* in, const float* wt, float* out, const ConvGeom& g,
-                       const Epi& e, int splits, int sps, int64_t zstride, hipStream_t st) {
+                       const Epi& e, int splits, int sps, int64_t zstride, hipStream_t st,
+                       int* cnt = nullptr, float* fout = nullptr, const Epi* fe = nullptr) {
   int TN, TM;
   tap_tile(g.N, &TN, &TM);
   dim3 grid((g.Mpos + TM - 1) / TM, (g.N + TN - 1) / TN, splits);
+  const Epi fin = fe ? *fe : e;
   if (TN == 16)
     hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 16, 256, 1, 4, BK>), grid,
-                       dim3(256), 0, st, in, wt, out, g, e, sps, zstride);
+                       dim3(256), 0, st, in, wt, out, g, e, sps, zstride, cnt, fout, fin);
   else if (TN == 32)
     hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 32, 128, 2, 2, BK>), grid,
-                       dim3(256), 0, st, in, wt, out, g, e, sps, zstride);
+                       dim3(256), 0, st, in, wt, out, g, e, sps, zstride, cnt, fout, fin);
   else
     hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 64, 128, 2, 2, BK>), grid,
-                       dim3(256), 0, st, in, wt, out, g, e, sps, zstride);
+                       dim3(256), 0, st, in, wt, out, g, e, sps, zstride, cnt, fout, fin);
 }
 
 // staged GEMM; `slab` (nullable) enables split-K with splits*N*Mpos floats of partials
@@ -1175,10 +1217,16 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
     if (splits > 1) {
       const int64_t n_out = (int64_t)g.Mpos * g.N;
       const Epi raw = {nullptr, nullptr, 0.f, 1.f, nullptr, 0};
+      int TN, TM;
+      tap_tile(g.N, &TN, &TM);
+      int* cnt = counters((int64_t)((g.Mpos + TM - 1) / TM) * ((g.N + TN - 1) / TN), FIN_CONV);
       if (g.C % 32 == 0)
-        launch_tap<MODE, KH, KW, SW, REPL, 32>(in, wt, slab, g, raw, splits, sps, n_out, st);
+        launch_tap<MODE, KH, KW, SW, REPL, 32>(in, wt, slab, g, raw, splits, sps, n_out, st, cnt,
+                                               out, &e);
       else
-        launch_tap<MODE, KH, KW, SW, REPL, 16>(in, wt, slab, g, raw, splits, sps, n_out, st);
+        launch_tap<MODE, KH, KW, SW, REPL, 16>(in, wt, slab, g, raw, splits, sps, n_out, st, cnt,
+                                               out, &e);
+      if (cnt) return;
       int blocks = (int)((n_out + 255) / 256);
       if (blocks > 8192) blocks = 8192;
       hipLaunchKernelGGL(conv_splitk_epi_kernel, dim3(blocks), dim3(256), 0, st, slab, splits,
@@ -1207,7 +1255,22 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
   }
 }
 
-static int g_conv_halo = 3;  // tvq_conv_config bits: 1 = halo fwd/dgrad, 2 = halo wgrad
+// tvq_conv_config bits: 1 = halo fwd/dgrad, 2 = halo wgrad, 4 = halo fwd/dgrad wherever
+// it fits (ignore halo_preferred; tests)
+static int g_conv_halo = 3;
+
+// Measured per shape on MI355X (tools/conv_shapes_bench.py, halo vs staged GEMM at the
+// step's shapes): the halo tile wins while the gathered channel count is small (its
+// per-image restaging of the weight panel grows with C), loses to the tap-major GEMM
+// for 1x1 convs, for C >= 32, and for the stride-2 transposed gathers.  A register-
+// resident-weight variant (whole reduction row per wave in VGPRs) was 1.5-4x slower
+// than both (1 wave/SIMD, uncoalesced weight loads) and was dropped.
+static bool halo_preferred(int mode, int C, int KK, int SW) {
+  if (g_conv_halo & 4) return true;
+  if (KK == 1 || C >= 32) return false;
+  if (mode == GATHER_T && SW == 2) return false;
+  return true;
+}
 
 // halo path when the image + weight panel fit in LDS, else the staged GEMM
 // workspace (nullable) = [packed weight N*C*KK][split-K slab]; see conv_gemm_ws
@@ -1217,7 +1280,7 @@ static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g
   HaloPlan pl;
   const int oh = MODE == GATHER_F ? g.oph : KH - 1 - g.oph;
   const int ow = MODE == GATHER_F ? g.opw : KW - 1 - g.opw;
-  if ((g_conv_halo & 1) && halo_plan(MODE, g.B, g.C, g.Hin, g.Win, g.N, g.Hout, g.Wo, KH, KW, SW, oh,
+  if ((g_conv_halo & 1) && halo_preferred(MODE, g.C, KH * KW, SW) && halo_plan(MODE, g.B, g.C, g.Hin, g.Win, g.N, g.Hout, g.Wo, KH, KW, SW, oh,
                                ow, g.wsn, g.wsc, &pl)) {
     launch_halo<MODE, KH, KW, SW, REPL>(in, wt, out, pl, g.B, e, st);
     return;
@@ -1302,7 +1365,7 @@ static Epi make_epi(const float* bias, const float* residual, float drop_p,
 
 extern "C" int tvq_conv_config(int64_t halo) {
   const int prev = g_conv_halo;
-  if (halo >= 0) g_conv_halo = (int)(halo & 3);
+  if (halo >= 0) g_conv_halo = (int)(halo & 7);
   return prev;
 }
 
@@ -1587,9 +1650,11 @@ extern "C" int tvq_channel_sum(const float* x, int64_t B, int64_t C, int64_t HW,
   }
   const int64_t chunks = tvq_channel_sum_workspace(B, C, HW) / C;
   hipStream_t st = (hipStream_t)stream;
+  int* cnt = counters(C, FIN_REDUCE);
   hipLaunchKernelGGL(chan_sum_partial_kernel, dim3((int)C, (int)chunks), dim3(256), 0, st, x,
-                     (int)B, (int)C, (int)HW, (int)chunks, workspace);
-  hipLaunchKernelGGL(chan_sum_final_kernel, dim3((int)((C + 127) / 128)), dim3(128), 0, st,
-                     workspace, (int)C, (int)chunks, out, (int)accumulate);
+                     (int)B, (int)C, (int)HW, (int)chunks, workspace, cnt, out, (int)accumulate);
+  if (!cnt)
+    hipLaunchKernelGGL(chan_sum_final_kernel, dim3((int)((C + 127) / 128)), dim3(128), 0, st,
+                       workspace, (int)C, (int)chunks, out, (int)accumulate);
   return launch_status("tvq_channel_sum");
 }

@@ -5,7 +5,8 @@
 //   A(m,k) = A[m*sam + k*sak],  B(k,n) = B[k*sbk + n*sbn]   (any strides: X W^T,
 //   dY W, dY^T X are all the same kernel)
 //   epi: + bias[n], GELU (erf), + R[m*ldr + n], or accumulate into C.
-// Split-K over gridDim.z writes fp32 slabs reduced in split order (deterministic).
+// Split-K over gridDim.z writes fp32 slabs reduced in split order (deterministic), by
+// the last-arriving split block of each tile (or a separate reduce launch).
 #include <math.h>
 
 #include "tvq_common.h"
@@ -28,6 +29,7 @@ struct GemmArgs {
   float alpha;
   int kper;        // K range per split
   float* slab;     // split-K partials [split][M][N] (nullptr: write C directly)
+  int* cnt;        // split-K: one counter per (m, n) tile -> the last split block finishes
 };
 
 __device__ __forceinline__ float gelu_erf(float x) {
@@ -135,9 +137,26 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
         const int m = m0 + (wm * FM + i) * 16 + 4 * g4 + r;
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          if (m < g.M && ncol[j] < g.N)
-            g.slab[((int64_t)blockIdx.z * g.M + m) * g.N + ncol[j]] = acc[i][j][r];
+          if (m < g.M && ncol[j] < g.N) {
+            float* d = g.slab + ((int64_t)blockIdx.z * g.M + m) * g.N + ncol[j];
+            if (g.cnt) st_wt(d, acc[i][j][r]);  // read back by the last split block
+            else *d = acc[i][j][r];
+          }
       }
+    // the last split block of this tile sums the slabs in split order + epilogue
+    // (element for element what gemm_splitk_reduce_kernel does)
+    if (g.cnt && last_block(g.cnt + blockIdx.y * gridDim.x + blockIdx.x, (int)gridDim.z)) {
+      const int64_t tot = (int64_t)g.M * g.N;
+      for (int e = tid; e < TM * TN; e += 256) {
+        const int m = m0 + e / TN, n = n0 + e % TN;
+        if (m >= g.M || n >= g.N) continue;
+        const int64_t i = (int64_t)m * g.N + n;
+        float s = 0.f;
+#pragma unroll 8
+        for (int z = 0; z < (int)gridDim.z; ++z) s += ld_wt(g.slab + (int64_t)z * tot + i);
+        g.C[(int64_t)m * g.ldc + n] = apply_epi(g, m, n, s);
+      }
+    }
     return;
   }
   float bv[FN];
@@ -271,6 +290,7 @@ extern "C" int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B
   g.slab = splits > 1 ? workspace : nullptr;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((M + TM - 1) / TM), (unsigned)((N + TN - 1) / TN), (unsigned)splits);
+  g.cnt = splits > 1 ? counters((int64_t)grid.x * grid.y, FIN_GEMM) : nullptr;
   if (TM == 128)
     hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2>), grid, dim3(256), 0, st, g);
   else if (TN == 64)
@@ -279,7 +299,7 @@ extern "C" int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B
     hipLaunchKernelGGL((gemm_kernel<64, 32, 2, 2>), grid, dim3(256), 0, st, g);
   else
     hipLaunchKernelGGL((gemm_kernel<32, 32, 2, 2>), grid, dim3(256), 0, st, g);
-  if (splits > 1) {
+  if (splits > 1 && !g.cnt) {
     const int64_t tot = M * N;
     const int blocks = (int)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096);
     hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g, splits);

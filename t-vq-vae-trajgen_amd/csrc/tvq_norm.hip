@@ -1,7 +1,8 @@
 // BatchNorm2d/1d (+ fused SnakeActivation), standalone Snake, dropout backward.
 //
 // BN training statistics accumulate in fp64 (torch's CPU accumulator type for
-// fp32), two kernels: per-(channel, chunk) partial sums -> per-channel finalize
+// fp32): per-(channel, chunk) partial sums -> per-channel finalize (done by the last
+// block of the channel when a counter pool is registered, else a second launch)
 // (mean, biased var for normalisation, unbiased var for running_var, momentum
 // 0.1, num_batches_tracked += 1) producing the affine form y = x*scale + shift
 // (scale = w*invstd, shift = b - mean*scale), then one streaming apply kernel
@@ -46,11 +47,52 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
   return t;
 }
 
-// partial [c][chunk][2] = (sum x, sum x^2)
+struct BNFinal {  // per-channel finalize of the training statistics
+  int C, chunks;
+  int64_t N;
+  float eps, momentum;
+  const float *w, *b;
+  float *rmean, *rvar;
+  int64_t* nbt;
+  float *save_mean, *save_invstd, *scale, *shift;
+};
+
+// one wave (lane 0..63) finalizes channel c: lanes stride the chunk partials, fixed
+// xor-tree combine; running stats with momentum, unbiased running var
+__device__ __forceinline__ void bn_final_channel(const double* part, int c, int lane,
+                                                 const BNFinal& f) {
+  if (c == 0 && lane == 0 && f.nbt) f.nbt[0] += 1;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = lane; i < f.chunks; i += 64) {
+    s1 += ld_wt(part + ((int64_t)c * f.chunks + i) * 2 + 0);
+    s2 += ld_wt(part + ((int64_t)c * f.chunks + i) * 2 + 1);
+  }
+  s1 = wave_sum_d(s1);
+  s2 = wave_sum_d(s2);
+  if (lane != 0) return;
+  const double mean = s1 / (double)f.N;
+  double var = s2 / (double)f.N - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const double invstd = 1.0 / sqrt(var + (double)f.eps);
+  if (f.rmean) {
+    const double unb = f.N > 1 ? var * (double)f.N / (double)(f.N - 1) : var;
+    f.rmean[c] = (float)((1.0 - f.momentum) * f.rmean[c] + f.momentum * mean);
+    f.rvar[c] = (float)((1.0 - f.momentum) * f.rvar[c] + f.momentum * unb);
+  }
+  const float sc = (float)((double)(f.w ? f.w[c] : 1.f) * invstd);
+  f.save_mean[c] = (float)mean;
+  f.save_invstd[c] = (float)invstd;
+  f.scale[c] = sc;
+  f.shift[c] = (f.b ? f.b[c] : 0.f) - (float)mean * sc;
+}
+
+// partial [c][chunk][2] = (sum x, sum x^2); with `cnt`, the last block of channel c
+// finalizes it (bn_final_channel) instead of a separate launch
 __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __restrict__ x, int B,
                                                                int C, int HW, Div16 dhw,
                                                                int chunks,
-                                                               double* __restrict__ part) {
+                                                               double* __restrict__ part,
+                                                               int* __restrict__ cnt, BNFinal f) {
   __shared__ double red[4];
   const int c = blockIdx.x, ch = blockIdx.y;
   const int tot = B * HW;
@@ -75,42 +117,16 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __re
   s1 = block_sum_d(s1, red);
   s2 = block_sum_d(s2, red);
   if (threadIdx.x == 0) {
-    part[((int64_t)c * chunks + ch) * 2 + 0] = s1;
-    part[((int64_t)c * chunks + ch) * 2 + 1] = s2;
+    st_wt(part + ((int64_t)c * chunks + ch) * 2 + 0, s1);
+    st_wt(part + ((int64_t)c * chunks + ch) * 2 + 1, s2);
   }
+  if (cnt && last_block(cnt + c, chunks) && threadIdx.x < 64)
+    bn_final_channel(part, c, threadIdx.x, f);
 }
 
-// one wave per channel: lanes stride the chunk partials, fixed xor-tree combine
-__global__ __launch_bounds__(64) void bn_stats_final_kernel(
-    const double* __restrict__ part, int C, int chunks, int64_t N, float eps, float momentum,
-    const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ rmean,
-    float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
-    float* __restrict__ save_invstd, float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (c == 0 && lane == 0 && nbt) nbt[0] += 1;
-  double s1 = 0.0, s2 = 0.0;
-  for (int i = lane; i < chunks; i += 64) {
-    s1 += part[((int64_t)c * chunks + i) * 2 + 0];
-    s2 += part[((int64_t)c * chunks + i) * 2 + 1];
-  }
-  s1 = wave_sum_d(s1);
-  s2 = wave_sum_d(s2);
-  if (lane != 0) return;
-  const double mean = s1 / (double)N;
-  double var = s2 / (double)N - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const double invstd = 1.0 / sqrt(var + (double)eps);
-  if (rmean) {
-    const double unb = N > 1 ? var * (double)N / (double)(N - 1) : var;
-    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
-    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
-  }
-  const float sc = (float)((double)(w ? w[c] : 1.f) * invstd);
-  save_mean[c] = (float)mean;
-  save_invstd[c] = (float)invstd;
-  scale[c] = sc;
-  shift[c] = (b ? b[c] : 0.f) - (float)mean * sc;
+__global__ __launch_bounds__(64) void bn_stats_final_kernel(const double* __restrict__ part,
+                                                            BNFinal f) {
+  bn_final_channel(part, blockIdx.x, threadIdx.x, f);
 }
 
 __global__ void bn_eval_prep_kernel(const float* __restrict__ w, const float* __restrict__ b,
@@ -147,12 +163,40 @@ __global__ __launch_bounds__(256) void affine_snake_kernel(const float* __restri
   }
 }
 
-// backward partials: [c][chunk][3] = (sum ds, sum ds*xhat, sum da-term)
+struct BNBwdFinal {
+  int C, chunks;
+  float *coef, *dw, *db, *da;
+  int accumulate;
+};
+
+// coef[c] = (sum ds, sum ds*xhat) and the parameter grads of channel c (one wave)
+__device__ __forceinline__ void bn_bwd_final_channel(const double* part, int c, int lane,
+                                                     const BNBwdFinal& f) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int i = lane; i < f.chunks; i += 64) {
+    const double* pp = part + ((int64_t)c * f.chunks + i) * 3;
+    s0 += ld_wt(pp + 0);
+    s1 += ld_wt(pp + 1);
+    s2 += ld_wt(pp + 2);
+  }
+  s0 = wave_sum_d(s0);
+  s1 = wave_sum_d(s1);
+  s2 = wave_sum_d(s2);
+  if (lane != 0) return;
+  f.coef[2 * c] = (float)s0;
+  f.coef[2 * c + 1] = (float)s1;
+  if (f.dw) f.dw[c] = f.accumulate ? f.dw[c] + (float)s1 : (float)s1;
+  if (f.db) f.db[c] = f.accumulate ? f.db[c] + (float)s0 : (float)s0;
+  if (f.da) f.da[c] = f.accumulate ? f.da[c] + (float)s2 : (float)s2;
+}
+
+// backward partials: [c][chunk][3] = (sum ds, sum ds*xhat, sum da-term); with `cnt`
+// the last block of channel c finalizes it
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, int B, int C, int HW, Div16 dhw,
     int chunks, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ a,
-    double* __restrict__ part) {
+    double* __restrict__ part, int* __restrict__ cnt, BNBwdFinal f) {
   __shared__ double red[4];
   const int c = blockIdx.x, ch = blockIdx.y;
   const int tot = B * HW;
@@ -192,37 +236,17 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
   s_da = block_sum_d(s_da, red);
   if (threadIdx.x == 0) {
     double* pp = part + ((int64_t)c * chunks + ch) * 3;
-    pp[0] = s_ds;
-    pp[1] = s_dsx;
-    pp[2] = s_da;
+    st_wt(pp + 0, s_ds);
+    st_wt(pp + 1, s_dsx);
+    st_wt(pp + 2, s_da);
   }
+  if (cnt && last_block(cnt + c, chunks) && threadIdx.x < 64)
+    bn_bwd_final_channel(part, c, threadIdx.x, f);
 }
 
-// coef[c][0] = sum ds, coef[c][1] = sum ds*xhat ; parameter grads.  One wave per channel.
-__global__ __launch_bounds__(64) void bn_bwd_final_kernel(const double* __restrict__ part, int C,
-                                                          int chunks, float* __restrict__ coef,
-                                                          float* __restrict__ dw,
-                                                          float* __restrict__ db,
-                                                          float* __restrict__ da,
-                                                          int accumulate) {
-  const int c = blockIdx.x;
-  const int lane = threadIdx.x;
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  for (int i = lane; i < chunks; i += 64) {
-    const double* pp = part + ((int64_t)c * chunks + i) * 3;
-    s0 += pp[0];
-    s1 += pp[1];
-    s2 += pp[2];
-  }
-  s0 = wave_sum_d(s0);
-  s1 = wave_sum_d(s1);
-  s2 = wave_sum_d(s2);
-  if (lane != 0) return;
-  coef[2 * c] = (float)s0;
-  coef[2 * c + 1] = (float)s1;
-  if (dw) dw[c] = accumulate ? dw[c] + (float)s1 : (float)s1;
-  if (db) db[c] = accumulate ? db[c] + (float)s0 : (float)s0;
-  if (da) da[c] = accumulate ? da[c] + (float)s2 : (float)s2;
+__global__ __launch_bounds__(64) void bn_bwd_final_kernel(const double* __restrict__ part,
+                                                          BNBwdFinal f) {
+  bn_bwd_final_channel(part, blockIdx.x, threadIdx.x, f);
 }
 
 // dx = w*invstd/N * (N*ds - sum ds - xhat * sum ds*xhat), flat over NCHW
@@ -259,13 +283,24 @@ __global__ __launch_bounds__(256) void snake_fwd_kernel(const float* __restrict_
     y[i] = snake_fwd(x[i], a[div16(i, dhw) % C]);
 }
 
-// dx (elementwise) and per-(channel, chunk) partials of da
+__device__ __forceinline__ void snake_bwd_final_channel(const double* part, int C, int chunks,
+                                                        int c, float* da, int accumulate) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < chunks; i += 64) s += ld_wt(part + (int64_t)c * chunks + i);
+  s = wave_sum_d(s);
+  if (threadIdx.x == 0) da[c] = accumulate ? da[c] + (float)s : (float)s;
+}
+
+// dx (elementwise) and per-(channel, chunk) partials of da; with `cnt` the last block
+// of channel c sums them into da[c]
 __global__ __launch_bounds__(256) void snake_bwd_kernel(const float* __restrict__ dy,
                                                         const float* __restrict__ x, int B, int C,
                                                         int HW, Div16 dhw, int chunks,
                                                         const float* __restrict__ a,
                                                         float* __restrict__ dx,
-                                                        double* __restrict__ part) {
+                                                        double* __restrict__ part,
+                                                        int* __restrict__ cnt,
+                                                        float* __restrict__ da, int accumulate) {
   __shared__ double red[4];
   const int c = blockIdx.x, ch = blockIdx.y;
   const int tot = B * HW;
@@ -294,18 +329,16 @@ __global__ __launch_bounds__(256) void snake_bwd_kernel(const float* __restrict_
     }
   }
   s_da = block_sum_d(s_da, red);
-  if (threadIdx.x == 0) part[(int64_t)c * chunks + ch] = s_da;
+  if (threadIdx.x == 0) st_wt(part + (int64_t)c * chunks + ch, s_da);
+  if (cnt && last_block(cnt + c, chunks) && threadIdx.x < 64)
+    snake_bwd_final_channel(part, C, chunks, c, da, accumulate);
 }
 
 __global__ __launch_bounds__(64) void snake_bwd_final_kernel(const double* __restrict__ part,
                                                              int C, int chunks,
                                                              float* __restrict__ da,
                                                              int accumulate) {
-  const int c = blockIdx.x;
-  double s = 0.0;
-  for (int i = threadIdx.x; i < chunks; i += 64) s += part[(int64_t)c * chunks + i];
-  s = wave_sum_d(s);
-  if (threadIdx.x == 0) da[c] = accumulate ? da[c] + (float)s : (float)s;
+  snake_bwd_final_channel(part, C, chunks, blockIdx.x, da, accumulate);
 }
 
 __global__ void dropout_bwd_kernel(const float* __restrict__ dy, int64_t n, float p, float scale,
@@ -353,11 +386,13 @@ extern "C" int tvq_bn_train_fwd(const float* x, int64_t B, int64_t C, int64_t HW
   const int chunks = bn_chunks(B, HW);
   const Div16 dhw = make_div16(HW);
   double* part = (double*)workspace;
+  const BNFinal f = {(int)C, chunks, B * HW, eps, momentum, w, b, running_mean, running_var,
+                     num_batches_tracked, save_mean, save_invstd, scale_shift, scale_shift + C};
+  int* cnt = counters(C, FIN_NORM);
   hipLaunchKernelGGL(bn_stats_partial_kernel, dim3((int)C, chunks), dim3(256), 0, st, x, (int)B,
-                     (int)C, (int)HW, dhw, chunks, part);
-  hipLaunchKernelGGL(bn_stats_final_kernel, dim3((int)C), dim3(64), 0, st, part,
-                     (int)C, chunks, B * HW, eps, momentum, w, b, running_mean, running_var,
-                     num_batches_tracked, save_mean, save_invstd, scale_shift, scale_shift + C);
+                     (int)C, (int)HW, dhw, chunks, part, cnt, f);
+  if (!cnt)
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((int)C), dim3(64), 0, st, part, f);
   hipLaunchKernelGGL(affine_snake_kernel, ew_grid(B * C * HW), dim3(256), 0, st, x,
                      (int)(B * C * HW), (int)C, (int)HW, dhw, scale_shift, scale_shift + C, snake_a,
                      y);
@@ -393,11 +428,12 @@ extern "C" int tvq_bn_bwd(const float* dy, const float* x, int64_t B, int64_t C,
   const Div16 dhw = make_div16(HW);
   double* part = (double*)workspace;
   float* coef = (float*)(part + (int64_t)C * chunks * 3);
+  const BNBwdFinal f = {(int)C, chunks, coef, dw, db, snake_a ? da : nullptr, (int)accumulate};
+  int* cnt = counters(C, FIN_NORM);
   hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3((int)C, chunks), dim3(256), 0, st, dy, x, (int)B,
                      (int)C, (int)HW, dhw, chunks, save_mean, save_invstd, scale_shift,
-                     scale_shift + C, snake_a, part);
-  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((int)C), dim3(64), 0, st, part,
-                     (int)C, chunks, coef, dw, db, snake_a ? da : nullptr, (int)accumulate);
+                     scale_shift + C, snake_a, part, cnt, f);
+  if (!cnt) hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((int)C), dim3(64), 0, st, part, f);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, ew_grid(B * C * HW), dim3(256), 0, st, dy, x,
                      (int)(B * C * HW), (int)C, (int)HW, dhw, B * HW, save_mean, save_invstd, w,
                      scale_shift, scale_shift + C, snake_a, coef, dx);
@@ -424,10 +460,13 @@ extern "C" int tvq_snake_bwd(const float* dy, const float* x, int64_t B, int64_t
   TVQ_CHECK_ARG(norm_dims_ok(B, C, HW), "tvq_snake_bwd: tensor too large");
   hipStream_t st = (hipStream_t)stream;
   const int chunks = bn_chunks(B, HW);
+  int* cnt = counters(C, FIN_NORM);
   hipLaunchKernelGGL(snake_bwd_kernel, dim3((int)C, chunks), dim3(256), 0, st, dy, x, (int)B,
-                     (int)C, (int)HW, make_div16(HW), chunks, a, dx, (double*)workspace);
-  hipLaunchKernelGGL(snake_bwd_final_kernel, dim3((int)C), dim3(64), 0, st,
-                     (const double*)workspace, (int)C, chunks, da, (int)accumulate);
+                     (int)C, (int)HW, make_div16(HW), chunks, a, dx, (double*)workspace, cnt, da,
+                     (int)accumulate);
+  if (!cnt)
+    hipLaunchKernelGGL(snake_bwd_final_kernel, dim3((int)C), dim3(64), 0, st,
+                       (const double*)workspace, (int)C, chunks, da, (int)accumulate);
   return launch_status("tvq_snake_bwd");
 }
 

@@ -18,55 +18,89 @@ namespace tvq {
 
 constexpr int RR_COLS = 64, RR_GROUPS = 4, RR_ROWS = 64;
 
+// column block j0..j0+63, rows [p0, p1) of `in` (row stride ld): 4 row groups strided
+// by 4 each, combined (g0+g1)+(g2+g3) -- the fixed order of every level
+template <bool WT>
+__device__ __forceinline__ float rr_colsum(const float* __restrict__ in, int64_t p0, int64_t p1,
+                                           int64_t ld, int64_t j, int64_t N, float (*sh)[RR_COLS],
+                                           int c, int g) {
+  float s = 0.f;
+  if (j < N) {
+#pragma unroll 4
+    for (int64_t p = p0 + g; p < p1; p += RR_GROUPS) s += WT ? ld_wt(in + p * ld + j) : in[p * ld + j];
+  }
+  sh[g][c] = s;
+  __syncthreads();
+  const float t = (sh[0][c] + sh[1][c]) + (sh[2][c] + sh[3][c]);
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ void rr_store(float t, int64_t j, float* __restrict__ out,
+                                         float* __restrict__ out2, int64_t L, int accumulate) {
+  if (L > 0) {  // split output: [rows][L] -> out (L-1 cols) | out2 (last col)
+    const int64_t r = j / L, col = j - r * L;
+    float* d = col < L - 1 ? out + r * (L - 1) + col : out2 + r;
+    if (col < L - 1 || out2) *d = accumulate ? *d + t : t;
+  } else {
+    out[j] = accumulate ? out[j] + t : t;
+  }
+}
+
+// direct: one level, rows [0, P) -> out.  !direct: level 1 (row block blockIdx.y ->
+// scratch row); with `cnt` the last row block of column block x then runs level 2 over
+// the R scratch rows (same order as the separate level-2 launch) and writes out.
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ in, int64_t P,
                                                           int64_t N, int64_t ld, int rows_per_blk,
                                                           float* __restrict__ out,
                                                           float* __restrict__ out2, int64_t L,
-                                                          int accumulate, int direct) {
+                                                          int accumulate, int direct,
+                                                          float* __restrict__ scratch,
+                                                          int* __restrict__ cnt) {
   __shared__ float sh[RR_GROUPS][RR_COLS];
   const int c = threadIdx.x % RR_COLS, g = threadIdx.x / RR_COLS;
   const int64_t j = (int64_t)blockIdx.x * RR_COLS + c;
   const int64_t p0 = (int64_t)blockIdx.y * rows_per_blk;
   const int64_t p1 = min(P, p0 + rows_per_blk);
-  float s = 0.f;
-  if (j < N) {
-#pragma unroll 4
-    for (int64_t p = p0 + g; p < p1; p += RR_GROUPS) s += in[p * ld + j];
+  const float t = rr_colsum<false>(in, p0, p1, ld, j, N, sh, c, g);
+  if (direct) {
+    if (g == 0 && j < N) rr_store(t, j, out, out2, L, accumulate);
+    return;
   }
-  sh[g][c] = s;
-  __syncthreads();
   if (g == 0 && j < N) {
-    const float t = (sh[0][c] + sh[1][c]) + (sh[2][c] + sh[3][c]);
-    if (!direct) {  // level-1 partial
-      out[(int64_t)blockIdx.y * N + j] = t;
-    } else if (L > 0) {  // split output: [rows][L] -> out (L-1 cols) | out2 (last col)
-      const int64_t r = j / L, col = j - r * L;
-      float* d = col < L - 1 ? out + r * (L - 1) + col : out2 + r;
-      if (col < L - 1 || out2) *d = accumulate ? *d + t : t;
-    } else {
-      out[j] = accumulate ? out[j] + t : t;
-    }
+    if (cnt) st_wt(scratch + (int64_t)blockIdx.y * N + j, t);
+    else scratch[(int64_t)blockIdx.y * N + j] = t;
+  }
+  if (cnt && last_block(cnt + blockIdx.x, (int)gridDim.y)) {
+    const float u = rr_colsum<true>(scratch, 0, gridDim.y, N, j, N, sh, c, g);
+    if (g == 0 && j < N) rr_store(u, j, out, out2, L, accumulate);
   }
 }
 
+// one launch (each thread sums <= RR_ONE / 4 rows) when the slab is short; the
+// two-level split only pays for tall slabs, where one block column would serialise
+constexpr int64_t RR_ONE = 256;
+
 int64_t reduce_rows_scratch(int64_t P, int64_t N) {
   const int64_t R = (P + RR_ROWS - 1) / RR_ROWS;
-  return R > 1 ? R * N : 0;
+  return (R > 1 && P > RR_ONE) ? R * N : 0;
 }
 
 void reduce_rows(const float* in, int64_t P, int64_t N, int64_t ld, float* out, float* out2,
                  int64_t L, int accumulate, float* scratch, hipStream_t st) {
   const unsigned gx = (unsigned)((N + RR_COLS - 1) / RR_COLS);
   const int64_t R = (P + RR_ROWS - 1) / RR_ROWS;
-  if (R <= 1 || scratch == nullptr) {  // single level (no scratch): one block column per 64 cols
+  if (R <= 1 || P <= RR_ONE || scratch == nullptr) {  // single level: one block column per 64 cols
     hipLaunchKernelGGL(reduce_rows_kernel, dim3(gx, 1), dim3(256), 0, st, in, P, N, ld, (int)P,
-                       out, out2, L, accumulate, 1);
+                       out, out2, L, accumulate, 1, nullptr, nullptr);
     return;
   }
+  int* cnt = counters(gx, FIN_REDUCE);
   hipLaunchKernelGGL(reduce_rows_kernel, dim3(gx, (unsigned)R), dim3(256), 0, st, in, P, N, ld,
-                     RR_ROWS, scratch, nullptr, (int64_t)0, 0, 0);
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(gx, 1), dim3(256), 0, st, scratch, R, N, N, (int)R,
-                     out, out2, L, accumulate, 1);
+                     RR_ROWS, out, out2, L, accumulate, 0, scratch, cnt);
+  if (!cnt)
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3(gx, 1), dim3(256), 0, st, scratch, R, N, N, (int)R,
+                       out, out2, L, accumulate, 1, nullptr, nullptr);
 }
 
 // ---------------------------------------------------------------- group-by

@@ -31,6 +31,7 @@ def sig(name, *argtypes, restype=I32):
     SIGNATURES[name] = (list(argtypes), restype)
 
 
+sig("tvq_counter_pool", I64, P, I64)
 # --- VQ codebook -----------------------------------------------------------
 sig("tvq_vq_sqnorm", P, I64, I64, P, P)
 sig("tvq_vq_assign_nblocks", I64, restype=I64)
@@ -147,9 +148,32 @@ def ptr(t):
     return t.data_ptr()
 
 
+POOL_SLOTS = 1 << 20
+_pools = {}  # device index -> zeroed int32 counter pool registered with the library
+_pool_dev = [-1]
+
+
+def _ensure_pool(h):
+    """Register this device's counter pool (tvq_counter_pool) on first use.  The first
+    launch on a device is eager (warmup steps precede graph capture)."""
+    dev = torch.cuda.current_device()
+    if dev == _pool_dev[0]:
+        return
+    if dev not in _pools:
+        pool = torch.zeros(POOL_SLOTS, dtype=torch.int32, device=dev)
+        if not torch.cuda.is_current_stream_capturing():
+            torch.cuda.synchronize(dev)  # zeroed before any stream's kernel takes a slot
+        rc = h.tvq_counter_pool(dev, pool.data_ptr(), POOL_SLOTS)
+        if rc != 0:
+            raise NativeError(f"tvq_counter_pool failed: {h.tvq_last_error().decode()}")
+        _pools[dev] = pool
+    _pool_dev[0] = dev
+
+
 def call(name, *args):
     """Call an int-returning entry point; raise with tvq_last_error() on failure."""
     h = lib()
+    _ensure_pool(h)
     rc = getattr(h, name)(*args)
     if rc != 0:
         raise NativeError(f"{name} failed ({rc}): {h.tvq_last_error().decode()}")

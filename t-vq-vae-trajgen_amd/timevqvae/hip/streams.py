@@ -115,9 +115,10 @@ def branch(device, key="hf", enabled=True):
     """Run the body on side stream `key` of the current stream (forked off it)."""
     if (not (active() and enabled) or key in INLINE or _depth[0] > 0
             or torch.device(device).type != "cuda"):
-        # nested branches run inline: a stream forked off a forked stream makes the ROCm
-        # 7.2 runtime segfault in hipStreamEndCapture (measured), and two levels buy
-        # nothing over one here (bench: 10.4 ms either way)
+        # nested branches run inline: any dependency edge between two forked streams
+        # (a fork off a forked stream, or a root fork that also waits on another branch)
+        # makes the ROCm 7.2 runtime segfault in hipStreamEndCapture (measured), so the
+        # graph keeps to root -> branch -> root edges
         yield _Branch(device, None, None)
         return
     main = torch.cuda.current_stream(device)

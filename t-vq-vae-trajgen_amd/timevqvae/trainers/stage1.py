@@ -53,40 +53,71 @@ class Stage1(nn.Module):
     def forward(self, batch, batch_idx, return_x_rec: bool = False):
         """stage1.py:89-168 (the validation-time plot is not reproduced)."""
         x, y = batch
-        recons_loss = {"LF.time": 0.0, "HF.time": 0.0}
-        vq_losses = {"LF": None, "HF": None}
-        perplexities = {"LF": 0.0, "HF": 0.0}
         need_tgt = not return_x_rec
         s = stft_encode(x, enc_l=True, enc_h=True, tgt_l=need_tgt, tgt_h=need_tgt)
-        # the HF branch runs on the side stream, concurrently with the LF branch
-        with streams.branch(x.device) as br:
+        # the HF branch runs on a side stream, concurrently with the LF branch
+        with streams.branch(x.device, "s1hf") as br:
             br.inputs(s)
-            z_h = self.encoder_h.encode_timefreq(s["enc_h"])
-            z_q_h, s_h, vq_loss_h, perplexity_h = quantize(z_h, self.vq_model_h)
-            xhat_h = self.decoder_h(z_q_h)
-            loss_h = None if return_x_rec else l1_loss(s["tgt_h"], xhat_h)
-            br.outputs(xhat_h, loss_h, vq_loss_h, perplexity_h)
-        z_l = self.encoder_l.encode_timefreq(s["enc_l"])
-        z_q_l, s_l, vq_loss_l, perplexity_l = quantize(z_l, self.vq_model_l)
-        xhat_l = self.decoder_l(z_q_l)
+            hf = self._band("HF", s, return_x_rec)
+            br.outputs(hf)
+        lf = self._band("LF", s, return_x_rec)
         br.join()
         if return_x_rec:
-            return xhat_l + xhat_h
-        recons_loss["LF.time"] = mse_loss(s["tgt_l"], xhat_l)
-        perplexities["LF"] = perplexity_l
-        vq_losses["LF"] = vq_loss_l
-        recons_loss["HF.time"] = loss_h
-        perplexities["HF"] = perplexity_h
-        vq_losses["HF"] = vq_loss_h
+            return lf[0] + hf[0]
+        return self._assemble({"LF": lf, "HF": hf})
+
+    def _band(self, band, s, return_x_rec=False):
+        """One frequency band (stage1.py:115-166): encoder -> VQ -> decoder (-> loss).
+        Returns (xhat, recons_loss, vq_loss, perplexity)."""
+        if band == "LF":
+            enc, vq, dec, tgt, loss_fn = self.encoder_l, self.vq_model_l, self.decoder_l, "tgt_l", mse_loss
+            z = enc.encode_timefreq(s["enc_l"])
+        else:
+            enc, vq, dec, tgt, loss_fn = self.encoder_h, self.vq_model_h, self.decoder_h, "tgt_h", l1_loss
+            z = enc.encode_timefreq(s["enc_h"])
+        z_q, _, vq_loss, perplexity = quantize(z, vq)
+        xhat = dec(z_q)
+        rec = None if return_x_rec else loss_fn(s[tgt], xhat)
+        return xhat, rec, vq_loss, perplexity
+
+    @staticmethod
+    def _assemble(parts):
+        recons_loss = {"LF.time": parts["LF"][1], "HF.time": parts["HF"][1]}
+        vq_losses = {"LF": parts["LF"][2], "HF": parts["HF"][2]}
+        perplexities = {"LF": parts["LF"][3], "HF": parts["HF"][3]}
         return recons_loss, vq_losses, perplexities
+
+    def forward_backward(self, batch, batch_idx=0):
+        """training_step + backward of its loss, with each band's forward AND backward on
+        its own stream inside streams.concurrent() (both fork off the current stream).
+        The two bands are disjoint subgraphs of the loss sum, so backpropagating
+        (recons + vq loss) per band gives exactly the gradients of loss.sum().  Returns a
+        callable that builds training_step's dict; call it after the region's join."""
+        x, y = batch
+        s = stft_encode(x, enc_l=True, enc_h=True, tgt_l=True, tgt_h=True)
+        parts = {}
+        for band in ("HF", "LF"):
+            with streams.branch(x.device, "s1" + band.lower()) as br:
+                br.inputs(s)
+                part = self._band(band, s)
+                (part[1] + part[2]["loss"]).sum().backward()
+                parts[band] = part
+                br.outputs(part)
+        if self._sched is not None:
+            self._sched.step()
+        return lambda: self._loss_hist(*self._assemble(parts))
 
     def training_step(self, batch, batch_idx):
         """stage1.py:170-198: loss and the logged scalars; steps the LR scheduler."""
         recons_loss, vq_losses, perplexities = self.forward(batch, batch_idx)
-        loss = ((recons_loss["LF.time"] + recons_loss["HF.time"]) + vq_losses["LF"]["loss"]
-                + vq_losses["HF"]["loss"])
         if self._sched is not None:
             self._sched.step()
+        return self._loss_hist(recons_loss, vq_losses, perplexities)
+
+    @staticmethod
+    def _loss_hist(recons_loss, vq_losses, perplexities):
+        loss = ((recons_loss["LF.time"] + recons_loss["HF.time"]) + vq_losses["LF"]["loss"]
+                + vq_losses["HF"]["loss"])
         return {
             "loss": loss,
             "recons_loss.time": recons_loss["LF.time"] + recons_loss["HF.time"],

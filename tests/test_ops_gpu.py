@@ -28,17 +28,19 @@ def _grads(fn, inputs):
 
 @pytest.fixture
 def conv_path(monkeypatch):
-    """Select the conv engine: halo-tile kernel (default), staged GEMM with packed
-    weights, or staged GEMM reading the weights in place."""
+    """Select the conv engine: the default per-shape choice, the halo-tile kernel
+    wherever it fits, the staged GEMM with packed weights, or the staged GEMM reading
+    the weights in place."""
     from timevqvae.hip import conv as conv_mod
     from timevqvae.hip._native import value
+    prev = value("tvq_conv_config", -1)
 
     def select(path):
         monkeypatch.setattr(conv_mod, "USE_WORKSPACE", path != "gemm_raw")
-        value("tvq_conv_config", 3 if path == "halo" else 0)
+        value("tvq_conv_config", {"default": 3, "halo": 7}.get(path, 0))
 
     yield select
-    value("tvq_conv_config", 3)
+    value("tvq_conv_config", prev)
 
 
 def _run_both(fn_hip, fn_ref, shapes, cuda, seed=0):
@@ -59,7 +61,7 @@ def _run_both(fn_hip, fn_ref, shapes, cuda, seed=0):
     (4, 8, 8, 64, "res"), (2, 64, 128, 8, "res"), (2, 16, 128, 32, "res"), (3, 128, 16, 32, "res"),
     (2, 64, 128, 8, "proj"), (5, 3, 7, 33, "res"),
 ])
-@pytest.mark.parametrize("path", ["halo", "gemm", "gemm_raw"])
+@pytest.mark.parametrize("path", ["default", "halo", "gemm", "gemm_raw"])
 def test_conv2d(B, Ci, Co, W, kind, path, cuda, conv_path):
     from timevqvae.hip.conv import conv2d
     conv_path(path)
@@ -86,7 +88,7 @@ def test_conv2d(B, Ci, Co, W, kind, path, cuda, conv_path):
 
 @pytest.mark.parametrize("B,Ci,Co,W", [(4, 64, 32, 8), (2, 8, 4, 64), (3, 4, 12, 128), (2, 12, 12, 256),
                                         (2, 128, 128, 16)])
-@pytest.mark.parametrize("path", ["halo", "gemm", "gemm_raw"])
+@pytest.mark.parametrize("path", ["default", "halo", "gemm", "gemm_raw"])
 def test_conv_transpose2d(B, Ci, Co, W, path, cuda, conv_path):
     from timevqvae.hip.conv import conv_transpose2d
     conv_path(path)
@@ -288,8 +290,8 @@ def test_adamw_matches_torch(cuda):
 @pytest.mark.parametrize("Ci,Co,W", [(16, 16, 32), (64, 64, 8), (8, 8, 64), (128, 16, 32)])
 def test_conv_paths_same_dropout_mask(Ci, Co, W, cuda):
     """The dropout mask is a function of (seed, offset, output index) only: the halo
-    kernel, the staged GEMM and the split-K GEMM (partials + epilogue kernel) drop
-    exactly the same elements."""
+    kernel, the staged GEMM, the split-K GEMM (partials + epilogue) and the default
+    per-shape choice drop exactly the same elements."""
     from timevqvae.hip._native import call, ptr, stream_ptr, value
     gen = torch.Generator().manual_seed(3)
     x = torch.randn(5, Ci, 3, W, generator=gen).to(cuda)
@@ -300,17 +302,19 @@ def test_conv_paths_same_dropout_mask(Ci, Co, W, cuda):
     nws = value("tvq_conv_workspace", 0, 5, Ci, 3, W, Co, 3, 3, 1, 0)
     ws = torch.empty(nws, device=cuda)
     outs = []
+    prev = value("tvq_conv_config", -1)
     try:
-        for halo, wsp in ((3, None), (0, None), (0, ws)):
+        for halo, wsp in ((7, None), (0, None), (0, ws), (3, None)):
             value("tvq_conv_config", halo)
             y = torch.empty(5, Co, 3, W, device=cuda)
             call("tvq_conv2d_fwd", ptr(x), 5, Ci, 3, W, ptr(w), ptr(b), Co, 3, 3, 1, 0, ptr(y),
                  ptr(r), 0.25, ptr(seed), 77, ptr(wsp), stream_ptr())
             outs.append(y)
     finally:
-        value("tvq_conv_config", 3)
+        value("tvq_conv_config", prev)
     torch.cuda.synchronize()
     masks = [o == r for o in outs]
-    assert torch.equal(masks[0], masks[1]) and torch.equal(masks[0], masks[2])
+    assert all(torch.equal(masks[0], m) for m in masks[1:])
+    torch.testing.assert_close(outs[0], outs[3], rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(outs[0], outs[2], rtol=1e-5, atol=1e-5)

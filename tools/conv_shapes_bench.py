@@ -57,6 +57,8 @@ def timeit(fn, reps=20):
 def main():
     only = {int(a) for a in sys.argv[1].split(",")} if len(sys.argv) > 1 else None
     dev = torch.device("cuda", 0)
+    if "TVQ_CONV_HALO" in os.environ:  # 0: staged GEMM only, 1: halo fwd/dgrad, 2: halo wgrad
+        value("tvq_conv_config", int(os.environ["TVQ_CONV_HALO"]))
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "floor": 0.0}
     print(f"{'n':>3} {'Ci':>4} {'Co':>4} {'W':>4} k    {'fwd':>7} {'dgrad':>7} {'wgrad':>7}  floor(us)")
     for si, (n, Ci, Co, H, Wi, KH, KW, SW, rep, tr) in enumerate(SHAPES):

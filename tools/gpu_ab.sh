@@ -11,7 +11,7 @@ fi
 i=0
 for v in ${VARIANTS:-"X=1"}; do
   i=$((i+1))
-  env $v timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-roofline > gpurun_out/bench_$i.log 2>&1
+  env ${v//+/ } timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-roofline > gpurun_out/bench_$i.log 2>&1
   rc=$?; echo "$v: $(tail -1 gpurun_out/bench_$i.log | python -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["losses"])')"
   [ $rc -eq 0 ] || exit $rc
 done
