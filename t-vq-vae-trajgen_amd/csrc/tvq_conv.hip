@@ -21,6 +21,8 @@
 #include "tvq_common.h"
 #include "tvq_reduce.h"
 
+#include <stdlib.h>
+
 namespace tvq {
 
 struct FastDiv {  // q = n / d for 0 <= n < 2^30, d >= 1
@@ -431,6 +433,173 @@ __global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__
     }
   }
 }
+
+// Wide-channel implicit GEMM on v_mfma_f32_32x32x2_f32 for the C, N >= 128-class convs
+// (128->128 ResBlock convs at W 32, the Upscale Conv1d pair, their dgrads).  Block tile
+// 128 channels x 96 positions: 4 waves x 32 channels, each wave three 32x32
+// accumulators, so one block per CU covers the 24,576-position maps in 256 blocks
+// without split-K.  K runs tap-major over 64-channel stages (packed weights
+// [tap][c][n], n contiguous -> dwordx4 loads); the next stage is loaded into registers
+// while the current one feeds 96 MFMAs per wave from the other half of a
+// double-buffered LDS tile (112 KB), one barrier per stage.  Loads are raw buffer loads:
+// per-thread offsets are three position bases + compile-time row steps, and an invalid
+// (padding) source gets an offset past the buffer end, which the hardware returns as 0.
+// Each output is the same k-ordered fma chain as conv_tap_kernel's unsplit path
+// (tap-major, channel order within a stage), so the two kernels agree bit for bit.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0,
+                                           (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff),
+                                           0x00020000);
+}
+
+template <int MODE, int KH, int KW, int SW, bool REPL, int BK>
+__global__ __launch_bounds__(256) void conv_t32_kernel(const float* __restrict__ in,
+                                                      const float* __restrict__ wt,
+                                                      float* __restrict__ out, ConvGeom g,
+                                                      Epi e) {
+  constexpr int TN = 128, TM = 96;
+  constexpr int A4 = TN * BK / 4 / 256;  // dwordx4 A loads per thread (8)
+  constexpr int BL = TM * BK / 256;      // dword B loads per thread (24)
+  constexpr int BAD = 0x40000000;        // offset past any buffer end -> loads 0
+  extern __shared__ float smem[];
+  float* As = smem;                      // [2][BK][TN]
+  float* Bs = smem + 2 * BK * TN;        // [2][BK][TM]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int n0 = blockIdx.y * TN, m0 = blockIdx.x * TM;
+  const int csteps = g.C / BK;
+  const int nsteps = KH * KW * csteps;
+  const int plane = g.Hin * g.Win;
+  const __amdgpu_buffer_rsrc_t rin = buf_rsrc(in, (int64_t)g.B * g.C * plane * 4);
+  const __amdgpu_buffer_rsrc_t rwt = buf_rsrc(wt, (int64_t)KH * KW * g.C * g.N * 4);
+
+  // B element i (< BL) of this thread: e = tid + 256 i -> position (tid + 64 (i%3)) % 96,
+  // row k = (tid + 256 (i%3)) / 96 + 8 (i/3)
+  static_assert(BK % 8 == 0 && (TM * BK) % 768 == 0, "stage rows");
+  int pm_b[3], pm_h[3], pm_w[3], krow[3];
+  bool pm_ok[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int m = m0 + (tid + 64 * u) % TM;
+    krow[u] = (tid + 256 * u) / TM;
+    pm_ok[u] = m < g.Mpos;
+    const int mc = pm_ok[u] ? m : 0;
+    const uint32_t bh = fdiv((uint32_t)mc, g.fd_wo);
+    pm_w[u] = mc - (int)bh * g.Wo;
+    pm_b[u] = (int)fdiv((uint32_t)mc, g.fd_hwo);
+    pm_h[u] = (int)bh - pm_b[u] * g.Hout;
+  }
+  const int a_k = tid >> 5, a_n = n0 + ((tid & 31) << 2);
+  float4 ra[A4];
+  float rb[BL];
+  auto load = [&](int step) {
+    const int tap = step / csteps;
+    const int c0 = (step - tap * csteps) * BK;
+    const int kh = tap / KW, kw = tap - kh * KW;
+    const int abase = (((tap * g.C + c0 + a_k) * g.N) + a_n) * 4;
+#pragma unroll
+    for (int i = 0; i < A4; ++i)
+      ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rwt, abase, i * 8 * g.N * 4, 0));
+    int boff[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      int hi, wi;
+      bool v = pm_ok[u];
+      if (MODE == GATHER_F) {
+        hi = pm_h[u] + kh - g.oph;
+        wi = pm_w[u] * SW + kw - g.opw;
+        if (REPL) {
+          hi = hi < 0 ? 0 : (hi >= g.Hin ? g.Hin - 1 : hi);
+          wi = wi < 0 ? 0 : (wi >= g.Win ? g.Win - 1 : wi);
+        } else {
+          v = v && hi >= 0 && hi < g.Hin && wi >= 0 && wi < g.Win;
+        }
+      } else {
+        hi = pm_h[u] - kh + g.oph;
+        const int wn = pm_w[u] - kw + g.opw;
+        v = v && hi >= 0 && hi < g.Hin && wn >= 0 && (SW == 1 || (wn & 1) == 0);
+        wi = wn / SW;
+        v = v && wi < g.Win;
+      }
+      boff[u] = v ? (((pm_b[u] * g.C + c0 + krow[u]) * plane) + hi * g.Win + wi) * 4 : BAD;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i)
+      rb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            rin, boff[i % 3], (i / 3) * 8 * plane * 4, 0));
+  };
+  auto store = [&](int buf) {
+    float* a = As + buf * BK * TN + a_k * TN + ((tid & 31) << 2);
+#pragma unroll
+    for (int i = 0; i < A4; ++i) *reinterpret_cast<float4*>(a + i * 8 * TN) = ra[i];
+    float* bb = Bs + buf * BK * TM;
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int u = i % 3;
+      bb[(krow[u] + 8 * (i / 3)) * TM + (tid + 64 * u) % TM] = rb[i];
+    }
+  };
+
+  floatx16 acc[3];
+#pragma unroll
+  for (int jb = 0; jb < 3; ++jb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[jb][r] = 0.f;
+  const int r32 = lane & 31, hl = lane >> 5;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int buf = step & 1;
+    if (step + 1 < nsteps) load(step + 1);
+    const float* a = As + buf * BK * TN + hl * TN + wid * 32 + r32;
+    const float* bb = Bs + buf * BK * TM + hl * TM + r32;
+#pragma unroll
+    for (int kp = 0; kp < BK / 2; ++kp) {
+      const float av = a[2 * kp * TN];
+      float bv[3];
+#pragma unroll
+      for (int jb = 0; jb < 3; ++jb) bv[jb] = bb[2 * kp * TM + jb * 32];
+#pragma unroll
+      for (int jb = 0; jb < 3; ++jb)
+        acc[jb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[jb], acc[jb], 0, 0, 0);
+    }
+    if (step + 1 < nsteps) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: acc[jb][reg] = (channel n0 + 32 wid + (reg & 3) + 8 (reg >> 2) + 4 hl,
+  // position m0 + 32 jb + lane % 32); bias, dropout, residual as epi_store
+  const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
+  const int64_t hw = (int64_t)g.Hout * g.Wo;
+#pragma unroll
+  for (int jb = 0; jb < 3; ++jb) {
+    const int m = m0 + jb * 32 + r32;
+    const bool pv = m < g.Mpos;
+    const int mc = pv ? m : 0;
+    const uint32_t bh = fdiv((uint32_t)mc, g.fd_wo);
+    const int w = mc - (int)bh * g.Wo;
+    const int b = (int)fdiv((uint32_t)mc, g.fd_hwo);
+    const int h = (int)bh - b * g.Hout;
+    const int64_t ob = ((int64_t)b * g.N * g.Hout + h) * g.Wo + w;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = n0 + wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      if (!pv || n >= g.N) continue;
+      const int64_t o = ob + (int64_t)n * hw;
+      float v = acc[jb][r] + (e.bias ? e.bias[n] : 0.f);
+      if (e.drop_p > 0.f) v = uniform01(seed, (uint64_t)o) >= e.drop_p ? v * e.drop_scale : 0.f;
+      if (e.residual) v += e.residual[o];
+      out[o] = v;
+    }
+  }
+}
+
+// LDS per block: 2 stages x BK x (128 + 96) floats.  BK = 32 (56 KB) leaves room on
+// the CU for the concurrently running streams' kernels; BK = 64 (112 KB) is 5 % faster
+// alone but starves them (joint step 8.7 vs 7.3 ms), so 32 is the default.
+static int g_t32_bk = 32;
+static size_t t32_lds(int bk) { return (size_t)2 * bk * (128 + 96) * 4; }
 
 // Weight gradient: rows = n (channels of G), cols = k' = (c, kh, kw), reduction over
 // positions.  blockIdx.z = split index over positions; partial results go to
@@ -1206,11 +1375,34 @@ static void launch_tap(const float* in, const float* wt, float* out, const ConvG
                        dim3(256), 0, st, in, wt, out, g, e, sps, zstride, cnt, fout, fin);
 }
 
+static int g_conv_t32 = 1;  // conv_t32_kernel enabled (tvq_conv_config bit 8 turns it off)
+
 // staged GEMM; `slab` (nullable) enables split-K with splits*N*Mpos floats of partials
 template <int MODE, int KH, int KW, int SW, bool REPL>
 static void launch_gemm(const float* in, const float* wt, float* out, const ConvGeom& g,
                         const Epi& e, float* slab, hipStream_t st) {
   if (g.C % 16 == 0) {
+    // wide channels on a full grid: 32x32 MFMA tile, no split-K (needs packed weights)
+    const int64_t t32_blocks = (int64_t)((g.Mpos + 95) / 96) * ((g.N + 127) / 128);
+    if (g_conv_t32 && g.C % g_t32_bk == 0 && g.N % 128 == 0 && g.wsn == 1 && g.wsc == g.N &&
+        t32_blocks >= 192 && (int64_t)g.B * g.C * g.Hin * g.Win < (1ll << 29) &&
+        (int64_t)KH * KW * g.C * g.N < (1ll << 29)) {
+      dim3 grid((g.Mpos + 95) / 96, g.N / 128);
+      static bool lds_set = false;  // > 64 KB of dynamic LDS must be opted into once
+      if (!lds_set) {
+        (void)hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&conv_t32_kernel<MODE, KH, KW, SW, REPL, 64>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)t32_lds(64));
+        lds_set = true;
+      }
+      if (g_t32_bk == 64)
+        hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, 64>), grid, dim3(256),
+                           t32_lds(64), st, in, wt, out, g, e);
+      else
+        hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, 32>), grid, dim3(256),
+                           t32_lds(32), st, in, wt, out, g, e);
+      return;
+    }
     int sps;
     const int splits = slab ? tap_splits(g, KH * KW, &sps) : 1;
     if (!slab) sps = KH * KW * ((g.C + 31) / 16);  // >= all K-steps
@@ -1364,8 +1556,12 @@ static Epi make_epi(const float* bias, const float* residual, float drop_p,
 }
 
 extern "C" int tvq_conv_config(int64_t halo) {
-  const int prev = g_conv_halo;
-  if (halo >= 0) g_conv_halo = (int)(halo & 7);
+  const int prev = g_conv_halo | (g_conv_t32 ? 0 : 8) | (g_t32_bk == 64 ? 16 : 0);
+  if (halo >= 0) {
+    g_conv_halo = (int)(halo & 7);
+    g_conv_t32 = (halo & 8) ? 0 : 1;
+    g_t32_bk = (halo & 16) ? 64 : 32;
+  }
   return prev;
 }
 
@@ -1658,3 +1854,10 @@ extern "C" int tvq_channel_sum(const float* x, int64_t B, int64_t C, int64_t HW,
                        workspace, (int)C, (int)chunks, out, (int)accumulate);
   return launch_status("tvq_channel_sum");
 }
+
+// TVQ_CONV_CONFIG=<bits> sets tvq_conv_config at load time (benchmark A/B switches)
+static const int g_conv_config_env = [] {
+  const char* v = getenv("TVQ_CONV_CONFIG");
+  if (v && *v) tvq_conv_config(atoi(v));
+  return 0;
+}();

@@ -29,15 +29,16 @@ def _grads(fn, inputs):
 @pytest.fixture
 def conv_path(monkeypatch):
     """Select the conv engine: the default per-shape choice, the halo-tile kernel
-    wherever it fits, the staged GEMM with packed weights, or the staged GEMM reading
-    the weights in place."""
+    wherever it fits, the staged GEMMs with packed weights (32x32-MFMA wide tile where
+    eligible; "tap" = the 16x16 tap-major kernel only), or the staged GEMM reading the
+    weights in place."""
     from timevqvae.hip import conv as conv_mod
     from timevqvae.hip._native import value
     prev = value("tvq_conv_config", -1)
 
     def select(path):
         monkeypatch.setattr(conv_mod, "USE_WORKSPACE", path != "gemm_raw")
-        value("tvq_conv_config", {"default": 3, "halo": 7}.get(path, 0))
+        value("tvq_conv_config", {"default": 3, "halo": 7, "tap": 8}.get(path, 0))
 
     yield select
     value("tvq_conv_config", prev)
@@ -61,7 +62,7 @@ def _run_both(fn_hip, fn_ref, shapes, cuda, seed=0):
     (4, 8, 8, 64, "res"), (2, 64, 128, 8, "res"), (2, 16, 128, 32, "res"), (3, 128, 16, 32, "res"),
     (2, 64, 128, 8, "proj"), (5, 3, 7, 33, "res"),
 ])
-@pytest.mark.parametrize("path", ["default", "halo", "gemm", "gemm_raw"])
+@pytest.mark.parametrize("path", ["default", "halo", "gemm", "tap", "gemm_raw"])
 def test_conv2d(B, Ci, Co, W, kind, path, cuda, conv_path):
     from timevqvae.hip.conv import conv2d
     conv_path(path)
@@ -88,7 +89,7 @@ def test_conv2d(B, Ci, Co, W, kind, path, cuda, conv_path):
 
 @pytest.mark.parametrize("B,Ci,Co,W", [(4, 64, 32, 8), (2, 8, 4, 64), (3, 4, 12, 128), (2, 12, 12, 256),
                                         (2, 128, 128, 16)])
-@pytest.mark.parametrize("path", ["default", "halo", "gemm", "gemm_raw"])
+@pytest.mark.parametrize("path", ["default", "halo", "gemm", "tap", "gemm_raw"])
 def test_conv_transpose2d(B, Ci, Co, W, path, cuda, conv_path):
     from timevqvae.hip.conv import conv_transpose2d
     conv_path(path)
@@ -318,3 +319,49 @@ def test_conv_paths_same_dropout_mask(Ci, Co, W, cuda):
     torch.testing.assert_close(outs[0], outs[3], rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(outs[0], outs[2], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("op", ["fwd", "dgrad", "conv1d_fwd", "conv1d_dgrad"])
+def test_conv_wide_tile_matches_tap(op, cuda):
+    """The 32x32-MFMA wide-channel tile (C, N >= 128 on a full grid) computes each output as
+    the same k-ordered fma chain as the tap-major kernel's unsplit path: bitwise equal to it,
+    and within the fp32 tolerance of torch's CPU conv."""
+    from timevqvae.hip._native import call, ptr, stream_ptr, value
+    gen = torch.Generator().manual_seed(11)
+    if op.startswith("conv1d"):
+        B, Ci, Co, H, W, KH, KW = 256, 128, 256, 1, 96, 1, 3
+    else:
+        B, Ci, Co, H, W, KH, KW = 192, 128, 128, 3, 32, 3, 3
+    x = torch.randn(B, Ci, H, W, generator=gen)
+    w = torch.randn(Co, Ci, KH, KW, generator=gen) * 0.05
+    bias = torch.randn(Co, generator=gen)
+    dy = torch.randn(B, Co, H, W, generator=gen)
+    xd, wd, bd, dyd = x.to(cuda), w.to(cuda), bias.to(cuda), dy.to(cuda)
+    outs = []
+    prev = value("tvq_conv_config", -1)
+    try:
+        for cfg, use_ws in ((0, True), (8, False)):  # wide tile (packed) | tap, unsplit, raw
+            value("tvq_conv_config", cfg)
+            if op.endswith("fwd"):
+                y = torch.empty(B, Co, H, W, device=cuda)
+                ws = torch.empty(value("tvq_conv_workspace", 0, B, Ci, H, W, Co, KH, KW, 1, 0),
+                                 device=cuda) if use_ws else None
+                call("tvq_conv2d_fwd", ptr(xd), B, Ci, H, W, ptr(wd), ptr(bd), Co, KH, KW, 1, 0,
+                     ptr(y), None, 0.0, None, 0, ptr(ws), stream_ptr())
+            else:
+                y = torch.empty(B, Ci, H, W, device=cuda)
+                ws = torch.empty(value("tvq_conv_workspace", 2, B, Ci, H, W, Co, KH, KW, 1, 0),
+                                 device=cuda) if use_ws else None
+                call("tvq_conv2d_dgrad", ptr(dyd), B, Co, H, W, ptr(wd), Ci, KH, KW, 1, 0, ptr(y),
+                     W, ptr(ws), stream_ptr())
+            outs.append(y)
+    finally:
+        value("tvq_conv_config", prev)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    pad = (KH // 2, (KW - 1) // 2)
+    if op.endswith("fwd"):
+        ref = F.conv2d(x, w, bias, padding=pad)
+    else:
+        ref = torch.nn.grad.conv2d_input(x.shape, w, dy, padding=pad)
+    close(outs[0].cpu(), ref, what=op)

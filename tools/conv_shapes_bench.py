@@ -27,7 +27,7 @@ SHAPES = [
     (2, 4, 3, 3, 128, 3, 4, 2, 0, 1), (2, 8, 3, 3, 64, 3, 4, 2, 0, 1),
     (2, 12, 3, 3, 256, 3, 4, 2, 0, 1), (2, 16, 3, 3, 32, 3, 4, 2, 0, 1),
     (1, 32, 3, 3, 16, 3, 4, 2, 0, 1), (1, 64, 3, 3, 8, 3, 4, 2, 0, 1),
-    (1, 128, 96, 1, 256, 1, 3, 1, 0, 0), (1, 256, 96, 1, 128, 1, 3, 1, 0, 0),
+    (1, 128, 256, 1, 96, 1, 3, 1, 0, 0), (1, 256, 128, 1, 96, 1, 3, 1, 0, 0),
 ]
 B = 256
 
