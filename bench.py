@@ -172,10 +172,11 @@ def roofline_leg(device):
 
     The op is the HF encoder ResBlock(16->128) second conv, (256,128,3,32) x (128,128,3,3):
     the largest single conv of the step (7.25 GFLOP).  As in the step it
-    runs as conv_pack_weight + conv_tap_kernel (split-K x3) + conv_splitk_epi; the
-    committed rocprofv3 summary (profiles/r01_roofline_kernel_stats.csv) lists the three
-    and their averages sum to avg_launch_ms.  `traffic` is the PMC-measured HBM bytes per
-    op from profiles/r01_roofline_traffic.json (FETCH_SIZE + WRITE_SIZE passes)."""
+    runs as conv_pack_weight + conv_t32_kernel (128-channel x 96-position tile on the
+    32x32x2 fp32 MFMA, no split-K); the committed rocprofv3 summary
+    (profiles/r01c_roofline_kernel_stats.csv) lists the two and their averages sum to
+    avg_launch_ms.  `traffic` is the PMC-measured HBM bytes per op from
+    profiles/r01c_roofline_traffic.json (FETCH_SIZE x2 + WRITE_SIZE passes)."""
     from timevqvae.hip.conv import conv2d
     x = torch.randn(256, 128, 3, 32, device=device)
     w = torch.randn(128, 128, 3, 3, device=device) * 0.03
@@ -194,15 +195,41 @@ def roofline_leg(device):
     flops = 2.0 * (256 * 3 * 32) * 128 * (128 * 9)
     achieved = flops / (ms * 1e-3) / 1e12
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r01_roofline_traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "r01c_roofline_traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath))["traffic_bytes"]
     return {"bound": "mfma", "kernel": "conv2d 128->128 3x3 @ (256,128,3,32): conv_pack_weight + "
-                                       "conv_tap_kernel<F,3,3,1,64x128> split-K x3 + conv_splitk_epi",
+                                       "conv_t32_kernel<F,3,3,1,BK32> (32x32x2 fp32 MFMA)",
             "achieved": round(achieved, 2), "peak": 157.3, "unit": "TFLOP/s",
             "frac": round(achieved / 157.3, 4), "traffic": traffic,
             "algorithmic_bytes": 4 * (256 * 128 * 3 * 32 * 2 + 128 * 128 * 9),
             "avg_launch_ms": round(ms, 4), "flops_per_launch": flops}
+
+
+def sampler_leg(tr, device, num=1024, reps=5):
+    """BASELINE configs[4]: MaskGIT iterative decoding (LF 10 steps + HF 1 step) of `num`
+    trajectories + LF/HF decoding to (num, 6, 256), with the bench's stage2 weights
+    (tools/sampler_bench.py is the standalone version with a CPU baseline)."""
+    mg = tr.s2.maskgit
+    was = mg.training
+    mg.eval()
+
+    def run():
+        s_l, s_h = mg.iterative_decoding(num=num, device=device)
+        return mg.decode_token_ind_to_timeseries(s_l, "lf") + \
+            mg.decode_token_ind_to_timeseries(s_h, "hf")
+
+    with torch.no_grad():
+        run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+    mg.train(was)
+    return {"num": num, "ms_per_batch": round(dt * 1e3, 3),
+            "trajectories_per_s": round(num / dt, 1), "reps": reps}
 
 
 def cpu_baseline_leg():
@@ -222,6 +249,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-sampler", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     args = ap.parse_args()
 
@@ -281,6 +309,8 @@ def main():
         }
         if not args.no_roofline:
             res["roofline"] = roofline_leg(device)
+        if not args.no_sampler:
+            res["sampler"] = sampler_leg(tr, device)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline_leg()
         print(json.dumps(res), flush=True)

@@ -65,6 +65,18 @@ int tvq_vq_assign(const float* x, int64_t B, int64_t N, int64_t D, int64_t sB, i
                   float* quant, int64_t* idx, int32_t* idx32, float* commit_partial,
                   tvq_stream_t stream);
 
+/* Stochastic assignment (EuclideanCodebook.forward with svq_temp > 0, vq.py:216-222 via
+ * softmax_sample vq.py:51-56): idx ~ Categorical(logits = dist / temp), drawn as Gumbel-max
+ * argmax(dist/temp + g) in the same pass as tvq_vq_assign.  g = -log(-log u) with u from
+ * the device seed (*seed_ptr, offset, m*K + k), or injected: gumbel (M, K) row-major, for
+ * tests.  temp == 0 is tvq_vq_assign (deterministic argmax).  Other arguments as
+ * tvq_vq_assign. */
+int tvq_vq_assign_svq(const float* x, int64_t B, int64_t N, int64_t D, int64_t sB, int64_t sN,
+                      int64_t sD, const float* E, const float* ee, int64_t K, int training,
+                      float temp, const float* gumbel, const int64_t* seed_ptr, uint64_t offset,
+                      float* quant, int64_t* idx, int32_t* idx32, float* commit_partial,
+                      tvq_stream_t stream);
+
 /* Per-code batch statistics, deterministic (no float atomics): a stable group-by
  * (counting sort) of idx32, then per-code row sums in row order.
  * counts[k] (int32), cs_batch[k] = counts (float) = onehot.sum(0) (vq.py:228) and, if

@@ -224,19 +224,43 @@ def decoder_forward(ctx, sd, prefix, z, plan, band, x_channels, input_length):
 # ----------------------------------------------------------------------------
 # Vector quantiser (models/vq.py)
 # ----------------------------------------------------------------------------
-def vq_forward(ctx, sd, prefix, x, decay=0.8, eps=1e-5):
+def vq_dist(flat, embed):
+    """dist = -(|x|^2 - 2 x.E^T + |E|^2), the reference's evaluation order (vq.py:210-214)."""
+    et = embed.t()
+    return -(flat.pow(2).sum(1, keepdim=True) - 2 * flat @ et + et.pow(2).sum(0, keepdim=True))
+
+
+def vq_sample(dist, temp):
+    """softmax_sample (vq.py:51-56): argmax at temp 0, else Categorical(logits=dist/temp)
+    drawn from torch's CPU RNG (same draws as the reference under the same seed)."""
+    if not temp:
+        return dist.argmax(dim=-1)
+    return torch.distributions.Categorical(logits=dist / temp).sample()
+
+
+def vq_sample_gumbel(dist, temp, gumbel):
+    """The HIP path's Gumbel-max form of the same distribution: argmax(dist/temp + g),
+    g = -log(-log u) (vq.py:39-48 gumbel_sample); first index on ties.  Returns (idx,
+    fp64 top-2 gap of the perturbed logits)."""
+    z = dist / temp + gumbel
+    z64 = dist.double() / temp + gumbel.double()
+    top2 = torch.topk(z64, 2, dim=-1).values
+    return z.argmax(dim=-1), (top2[:, 0] - top2[:, 1])
+
+
+def vq_forward(ctx, sd, prefix, x, decay=0.8, eps=1e-5, svq_temp=None):
     """VectorQuantize.forward + EuclideanCodebook.forward (vq.py:197-251, 325-407).
 
     x: (B,N,D).  Returns (quantize, embed_ind, commit_loss, perplexity).
-    Buffer updates (EMA, training only) go to ctx.updates.
+    Buffer updates (EMA, training only) go to ctx.updates.  svq_temp > 0 samples the
+    indices (vq.py:216-222) from torch's RNG.
     """
     cb = prefix + "_codebook."
     embed = sd[cb + "embed"]
     K = embed.shape[0]
     flat = x.reshape(-1, x.shape[-1])
-    et = embed.t()
-    dist = -(flat.pow(2).sum(1, keepdim=True) - 2 * flat @ et + et.pow(2).sum(0, keepdim=True))
-    ind = dist.argmax(dim=-1)
+    dist = vq_dist(flat, embed)
+    ind = vq_sample(dist, svq_temp)
     onehot = F.one_hot(ind, K).to(x.dtype)
     q = F.embedding(ind, embed).reshape(x.shape)
     ind = ind.reshape(x.shape[:-1])

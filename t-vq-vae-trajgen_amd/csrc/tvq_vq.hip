@@ -33,12 +33,33 @@ __global__ void vq_sqnorm_kernel(const float* __restrict__ E, int K, int D, floa
   ee[k] = s;
 }
 
-template <int D>
+// Stochastic assignment (svq_temp > 0, vq.py:51-56 softmax_sample): idx ~
+// Categorical(logits = dist / temp), drawn by Gumbel-max inside the running argmax:
+// argmax(dist/temp + g) = argmin(v/temp - g) with v = -dist, g = -log(-log u).  u is a
+// counter hash of (device seed, offset, m*K + k), or g is injected (M x K, tests).
+struct Svq {
+  float temp;
+  const float* gumbel;       // nullable: injected noise, row-major (M, K)
+  const int64_t* seed_ptr;   // device seed (hip/rng.py)
+  uint64_t offset;
+};
+
+__device__ __forceinline__ float gumbel_at(const Svq& sv, uint64_t seed, int64_t m, int K,
+                                           int code) {
+  const uint64_t c = (uint64_t)m * (uint64_t)K + (uint64_t)code;
+  if (sv.gumbel) return sv.gumbel[c];
+  // u in (0, 1): 24-bit lattice offset by half a step, so log(u) is finite
+  const float u = ((float)(hash_u32(seed * 0xD1B54A32D192ED03ull + c) >> 8) + 0.5f) *
+                  (1.0f / 16777216.0f);
+  return -logf(-logf(u));
+}
+
+template <int D, bool STOCH>
 __global__ __launch_bounds__(256, 2) void vq_assign_kernel(
     const float* __restrict__ x, int64_t M, int64_t N, int64_t sB, int64_t sN, int64_t sD,
     const float* __restrict__ E, const float* __restrict__ ee, int K, int training,
     float* __restrict__ quant, int64_t* __restrict__ idx, int32_t* __restrict__ idx32,
-    float* __restrict__ commit_partial) {
+    float* __restrict__ commit_partial, Svq sv) {
   constexpr int S = D + 8;  // LDS row stride (floats): conflict-free ds_read_b128 B-fragments
   constexpr int NQ = D / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -72,6 +93,7 @@ __global__ __launch_bounds__(256, 2) void vq_assign_kernel(
     if (ch == 0 && g == 0) xx_s[rg * 16 + r16] = s;
   }
 
+  const uint64_t sseed = (STOCH && !sv.gumbel) ? mix_seed(sv.seed_ptr, sv.offset) : 0ull;
   float bestv[4];
   int besti[4];
 #pragma unroll
@@ -113,6 +135,10 @@ __global__ __launch_bounds__(256, 2) void vq_assign_kernel(
       for (int r = 0; r < 4; ++r) {
         const float xx = xx_s[rg * 16 + 4 * g + r];
         float v = (xx - 2.0f * acc[t][r]) + e2;
+        if (STOCH && code < K) {
+          const int64_t m = row0 + rg * 16 + 4 * g + r;
+          v = v / sv.temp - gumbel_at(sv, sseed, m < M ? m : 0, K, code);
+        }
         if (code >= K) v = INFINITY;
         if (v < bestv[r]) { bestv[r] = v; besti[r] = code; }  // codes increase: strict < keeps first
       }
@@ -259,19 +285,38 @@ extern "C" int tvq_vq_assign(const float* x, int64_t B, int64_t N, int64_t D, in
                              int64_t sN, int64_t sD, const float* E, const float* ee, int64_t K,
                              int training, float* quant, int64_t* idx, int32_t* idx32,
                              float* commit_partial, tvq_stream_t stream) {
+  return tvq_vq_assign_svq(x, B, N, D, sB, sN, sD, E, ee, K, training, 0.f, nullptr, nullptr, 0,
+                           quant, idx, idx32, commit_partial, stream);
+}
+
+extern "C" int tvq_vq_assign_svq(const float* x, int64_t B, int64_t N, int64_t D, int64_t sB,
+                                 int64_t sN, int64_t sD, const float* E, const float* ee,
+                                 int64_t K, int training, float temp, const float* gumbel,
+                                 const int64_t* seed_ptr, uint64_t offset, float* quant,
+                                 int64_t* idx, int32_t* idx32, float* commit_partial,
+                                 tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && E && ee && quant && idx && idx32 && B > 0 && N > 0 && K > 0,
                 "tvq_vq_assign: bad arguments");
+  TVQ_CHECK_ARG(temp >= 0.f && (temp == 0.f || gumbel || seed_ptr),
+                "tvq_vq_assign_svq: temp > 0 needs injected noise or a device seed");
   TVQ_CHECK_ARG(!training || commit_partial, "tvq_vq_assign: training needs commit_partial");
   TVQ_CHECK_ARG(K < INT_MAX, "tvq_vq_assign: K too large");
   const int64_t M = B * N;
   const int64_t nb = tvq_vq_assign_nblocks(M);
   const size_t lds_tail = (VQ_BM + 4 * VQ_BM) * 4 + 16;
   hipStream_t st = (hipStream_t)stream;
+  const Svq sv = {temp, gumbel, seed_ptr, offset};
 #define TVQ_ASSIGN(DD)                                                                       \
   case DD: {                                                                                 \
     const size_t lds = (size_t)VQ_CK * (DD + 8) * 4 + lds_tail;                              \
-    hipLaunchKernelGGL(vq_assign_kernel<DD>, dim3(nb), dim3(256), lds, st, x, M, N, sB, sN, \
-                       sD, E, ee, (int)K, training, quant, idx, idx32, commit_partial);     \
+    if (sv.temp > 0.f)                                                                       \
+      hipLaunchKernelGGL((vq_assign_kernel<DD, true>), dim3(nb), dim3(256), lds, st, x, M, N,  \
+                         sB, sN, sD, E, ee, (int)K, training, quant, idx, idx32,             \
+                         commit_partial, sv);                                                \
+    else                                                                                     \
+      hipLaunchKernelGGL((vq_assign_kernel<DD, false>), dim3(nb), dim3(256), lds, st, x, M, N, \
+                         sB, sN, sD, E, ee, (int)K, training, quant, idx, idx32,             \
+                         commit_partial, sv);                                                \
     break;                                                                                   \
   }
   switch (D) {

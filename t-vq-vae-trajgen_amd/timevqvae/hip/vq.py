@@ -10,8 +10,11 @@ import contextlib
 
 import torch
 
-from . import streams
+from . import rng, streams
 from ._native import call, ptr, stream_ptr, value
+
+_SVQ_SITE = 0x5F << 56  # noise stream of the stochastic assignment (svq_temp > 0); fixed, so
+# module-construction site numbering (rng.new_site) is unchanged
 
 _pending = None  # list of CodebookUpdate while a deferral scope is active
 
@@ -67,8 +70,12 @@ def _check_dense(x):
 
 
 def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema, decay, eps,
-                     sync=None):
+                     sync=None, svq_temp=None, gumbel=None):
     """One codebook pass over x (B,N,D).
+
+    svq_temp > 0: stochastic assignment idx ~ Categorical(softmax(dist / svq_temp))
+    (vq.py:51-56, 216-222), drawn on the device by Gumbel-max; `gumbel` (M, K) injects the
+    noise (tests), otherwise it comes from the device seed (hip/rng.py).
 
     Returns (out, idx, commit, perplexity, counts):
       out   = x + (E[idx]-x) if straight_through else E[idx]  (pre-update codebook)
@@ -92,8 +99,17 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
     nb = value("tvq_vq_assign_nblocks", M)
     partial = torch.empty(nb, device=dev, dtype=torch.float32) if straight_through else None
     sB, sN, sD = x.stride()
-    call("tvq_vq_assign", ptr(x), B, N, D, sB, sN, sD, ptr(embed), ptr(ee), K,
-         int(bool(straight_through)), ptr(out), ptr(idx), ptr(idx32), ptr(partial), s)
+    if svq_temp:
+        if gumbel is not None and (gumbel.shape != (M, K) or not gumbel.is_contiguous()):
+            raise ValueError("vq: injected gumbel noise must be a contiguous (M, K) tensor")
+        seed = rng.seed_tensor(dev) if gumbel is None else None
+        off = rng.call_offset(_SVQ_SITE) if gumbel is None else 0
+        call("tvq_vq_assign_svq", ptr(x), B, N, D, sB, sN, sD, ptr(embed), ptr(ee), K,
+             int(bool(straight_through)), float(svq_temp), ptr(gumbel), ptr(seed), off,
+             ptr(out), ptr(idx), ptr(idx32), ptr(partial), s)
+    else:
+        call("tvq_vq_assign", ptr(x), B, N, D, sB, sN, sD, ptr(embed), ptr(ee), K,
+             int(bool(straight_through)), ptr(out), ptr(idx), ptr(idx32), ptr(partial), s)
     commit = None
     if straight_through:  # the loss reads it: stays on the current stream
         commit = torch.empty((), device=dev, dtype=torch.float32)
@@ -146,10 +162,10 @@ class _VQStraightThrough(torch.autograd.Function):
     """Training pass: forward = codebook pass with EMA; backward of vq.py:358,364."""
 
     @staticmethod
-    def forward(ctx, x, embed, cluster_size, embed_avg, ema, decay, eps, sync):
+    def forward(ctx, x, embed, cluster_size, embed_avg, ema, decay, eps, sync, svq_temp):
         out, idx, commit, perp, _ = vq_codebook_pass(
             x, embed, cluster_size, embed_avg, straight_through=True, ema=ema, decay=decay,
-            eps=eps, sync=sync)
+            eps=eps, sync=sync, svq_temp=svq_temp)
         ctx.save_for_backward(x, out)
         ctx.mark_non_differentiable(idx, perp)
         return out, idx, commit, perp
@@ -167,9 +183,10 @@ class _VQStraightThrough(torch.autograd.Function):
         gc = g_commit.contiguous() if g_commit is not None else None
         call("tvq_vq_backward", ptr(x), ptr(out), ptr(g_out), ptr(gc), x.numel(), x.numel(),
              ptr(dx), stream_ptr())
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
-def vq_train(x, embed, cluster_size, embed_avg, *, ema, decay, eps, sync=None):
+def vq_train(x, embed, cluster_size, embed_avg, *, ema, decay, eps, sync=None, svq_temp=None):
     """Training-mode VQ with straight-through gradient. Returns (out, idx, commit, perp)."""
-    return _VQStraightThrough.apply(x, embed, cluster_size, embed_avg, ema, decay, eps, sync)
+    return _VQStraightThrough.apply(x, embed, cluster_size, embed_avg, ema, decay, eps, sync,
+                                    svq_temp)

@@ -75,22 +75,18 @@ class EuclideanCodebook(nn.Module):
             return lambda t: distributed.all_reduce(t)
         return None
 
-    def _check_svq(self, svq_temp):
-        if svq_temp:
-            raise NotImplementedError("stochastic VQ (svq_temp>0, vq.py:51-56) is a SURVEY §8(f) "
-                                      "'next' item and not implemented on the HIP path yet")
-
     @torch.no_grad()
     def forward(self, x, svq_temp: Union[float, None] = None):
-        """Returns (quantize = E_old[idx], embed_ind); EMA update when training (vq.py:197-251)."""
-        self._check_svq(svq_temp)
+        """Returns (quantize = E_old[idx], embed_ind); EMA update when training (vq.py:197-251).
+        svq_temp > 0 samples idx ~ Categorical(softmax(dist / svq_temp)) (vq.py:216-222)."""
         if self.threshold_ema_dead_code > 0 and self.training:
             raise NotImplementedError("threshold_ema_dead_code > 0 is not on the TimeVQVAE path")
         shape = x.shape
         x3 = x.reshape(1, -1, shape[-1]) if x.dim() != 3 else x
         q, idx, _, perp, counts = vq_codebook_pass(
             x3, self.embed, self.cluster_size, self.embed_avg, straight_through=False,
-            ema=self.training, decay=self.decay, eps=self.eps, sync=self._sync())
+            ema=self.training, decay=self.decay, eps=self.eps, sync=self._sync(),
+            svq_temp=svq_temp)
         self.perplexity = perp
         self.counts = counts
         return q.reshape(shape), idx.reshape(shape[:-1])
@@ -134,7 +130,6 @@ class VectorQuantize(nn.Module):
     def forward(self, x, svq_temp: Union[float, None] = None):
         """x: (B,N,D) -> (quantize, embed_ind (B,N), vq_loss dict, perplexity)."""
         cb = self._codebook
-        cb._check_svq(svq_temp)
         device = x.device
         vq_loss = {
             "loss": torch.zeros(1, device=device).requires_grad_(self.training),
@@ -151,7 +146,7 @@ class VectorQuantize(nn.Module):
                 raise NotImplementedError("threshold_ema_dead_code > 0 is not on the path")
             quantize, embed_ind, commit, perp = vq_train(
                 x, cb.embed, cb.cluster_size, cb.embed_avg, ema=True, decay=cb.decay, eps=cb.eps,
-                sync=cb._sync())
+                sync=cb._sync(), svq_temp=svq_temp)
             if self.commitment_weight > 0:
                 vq_loss["commit_loss"] = commit
                 vq_loss["loss"] = vq_loss["loss"] + commit * self.commitment_weight
@@ -159,7 +154,7 @@ class VectorQuantize(nn.Module):
             with torch.no_grad():
                 quantize, embed_ind, _, perp, counts = vq_codebook_pass(
                     x, cb.embed, cb.cluster_size, cb.embed_avg, straight_through=False,
-                    ema=False, decay=cb.decay, eps=cb.eps)
+                    ema=False, decay=cb.decay, eps=cb.eps, svq_temp=svq_temp)
             cb.counts = counts
         cb.perplexity = perp.detach()
         if not self.channel_last and not self.accept_image_fmap:

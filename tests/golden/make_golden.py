@@ -11,6 +11,8 @@ files are loaded by file path with minimal import stubs:
   * timevqvae/trainers/stage1.py       (stub: lightning.LightningModule = nn.Module)
   * timevqvae/models/maskgit.py        (stub transformer; sampling/masking loops only)
 
+G6 (stochastic VQ) alone: python tests/golden/make_golden.py svq
+
 Only the .npz outputs are committed (tests/golden/*.npz).  Usage:
 
     python tests/golden/make_golden.py            # writes tests/golden/*.npz
@@ -294,14 +296,50 @@ def gen_maskgit(ref):
     np.savez_compressed(f"{OUT}/g5_maskgit.npz", **d)
 
 
+# --------------------------------------------------------------------------- G6
+def gen_svq(ref):
+    """Stochastic VQ (svq_temp > 0): EuclideanCodebook.forward draws idx with
+    softmax_sample = Categorical(logits=dist/temp).sample() (vq.py:51-56, 216-222).  The
+    draws are torch's CPU RNG under the recorded seeds, so the oracle restatement
+    (same logits, same sampler, same seed) must reproduce them exactly; the HIP path
+    (Gumbel-max on the device) is pinned against the oracle's logits instead."""
+    d = {}
+    g = torch.Generator().manual_seed(61)
+    M, D, K = 512, 32, 64
+    x = torch.randn(1, M, D, generator=g)
+    E = torch.randn(K, D, generator=g) * 0.7
+    d["x"], d["embed"] = x.numpy(), E.numpy()
+    for j, temp in enumerate((0.5, 4.0)):
+        for mode in ("eval", "train"):
+            vqm = ref.vq.VectorQuantize(dim=D, codebook_size=K)
+            vqm._codebook.embed.copy_(E)
+            vqm._codebook.embed_avg.copy_(E)
+            vqm.train(mode == "train")
+            torch.manual_seed(1000 + j)
+            q, ind, loss, perp = vqm(x.clone(), svq_temp=temp)
+            key = f"t{j}_{mode}"
+            d[f"{key}_temp"] = np.float32(temp)
+            d[f"{key}_seed"] = np.int64(1000 + j)
+            d[f"{key}_ind"] = ind.numpy()
+            d[f"{key}_perplexity"] = np.float32(perp)
+            if mode == "train":
+                d[f"{key}_post_cluster_size"] = vqm._codebook.cluster_size.numpy().copy()
+                d[f"{key}_post_embed"] = vqm._codebook.embed.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "g6_svq.npz"), **d)
+
+
 def main():
     torch.set_num_threads(8)
     ref = load_reference()
+    if sys.argv[1:] == ["svq"]:  # regenerate only G6
+        gen_svq(ref)
+        return
     gen_vq(ref)
     gen_stft(ref)
     gen_stage1(ref, "small", B=4, C=6, T=128, K=64, init_dim=4, hid_dim=32, seed=3)
     gen_stage1(ref, "cfgB", B=2, C=6, T=256, K=512, init_dim=4, hid_dim=128, seed=5)
     gen_maskgit(ref)
+    gen_svq(ref)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

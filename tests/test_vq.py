@@ -169,3 +169,127 @@ def test_hip_vq_layout_independent(cuda):
     q2, i2, _, _ = a(xv.contiguous())
     assert torch.equal(i1, i2)
     assert torch.equal(q1, q2)
+
+
+# ----------------------------------------------------------------------------- stochastic VQ
+def _svq_oracle(g6, key, train):
+    """The oracle's VectorQuantize pass with svq_temp under the golden's seed."""
+    from oracle import tvq_oracle as O
+    E = torch.from_numpy(g6["embed"])
+    sd = {"_codebook.embed": E, "_codebook.cluster_size": torch.zeros(E.shape[0]),
+          "_codebook.embed_avg": E.clone()}
+    ctx = O.Ctx(training=train)
+    torch.manual_seed(int(g6[f"{key}_seed"]))
+    q, ind, _, perp = O.vq_forward(ctx, sd, "", torch.from_numpy(g6["x"]),
+                                   svq_temp=float(g6[f"{key}_temp"]))
+    return ind, perp, ctx.updates
+
+
+@pytest.mark.parametrize("j", [0, 1])
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_oracle_svq_matches_reference_golden(j, mode):
+    """G6: the reference's Categorical draws (vq.py:51-56,216-222) reproduced by the oracle
+    restatement under the same torch seed, including the EMA that follows them."""
+    g6 = golden("g6_svq.npz")
+    key = f"t{j}_{mode}"
+    ind, perp, upd = _svq_oracle(g6, key, mode == "train")
+    assert (ind.numpy() == g6[f"{key}_ind"]).all()
+    assert abs(float(perp) - float(g6[f"{key}_perplexity"])) < 1e-4 * float(perp)
+    if mode == "train":
+        np.testing.assert_allclose(upd["_codebook.cluster_size"].numpy(),
+                                   g6[f"{key}_post_cluster_size"], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(upd["_codebook.embed"].numpy(), g6[f"{key}_post_embed"],
+                                   rtol=1e-5, atol=1e-5)
+
+
+def test_oracle_svq_gumbel_form_is_the_same_distribution():
+    """Gumbel-max (the HIP path's draw) and Categorical (the reference's) sample the same
+    softmax(dist/temp): empirical frequencies over 20k draws of one row agree within 5 sigma."""
+    from oracle import tvq_oracle as O
+    g = torch.Generator().manual_seed(7)
+    E = torch.randn(16, 8, generator=g)
+    x = torch.randn(1, 8, generator=g)
+    temp = 3.0
+    dist = O.vq_dist(x, E)
+    p = torch.softmax(dist.double() / temp, -1)[0]
+    n = 20000
+    u = torch.rand(n, 16, generator=g, dtype=torch.float64).clamp_min(1e-300)
+    gum = (-torch.log(-torch.log(u))).float()
+    idx, _ = O.vq_sample_gumbel(dist.expand(n, -1), temp, gum)
+    freq = torch.bincount(idx, minlength=16).double() / n
+    sigma = torch.sqrt(p * (1 - p) / n)
+    assert ((freq - p).abs() <= 5 * sigma + 1e-4).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("temp", [0.5, 4.0])
+def test_hip_svq_injected_noise_vs_oracle(temp, cuda):
+    """Device Gumbel-max with injected noise == oracle argmax(dist/temp + g), except where
+    the fp64 top-2 gap of the perturbed logits is inside the fp32 distance bound / temp."""
+    from oracle import tvq_oracle as O
+    from timevqvae.hip.vq import vq_codebook_pass
+    g6 = golden("g6_svq.npz")
+    x = torch.from_numpy(g6["x"])
+    E = torch.from_numpy(g6["embed"])
+    M, K = x.shape[1], E.shape[0]
+    gen = torch.Generator().manual_seed(11)
+    gum = -torch.log(-torch.log(torch.rand(M, K, generator=gen).clamp(1e-7, 1 - 1e-7)))
+    want, gap = O.vq_sample_gumbel(O.vq_dist(x[0], E), temp, gum)
+    cs = torch.zeros(K, device=cuda)
+    _, idx, _, _, counts = vq_codebook_pass(
+        x.to(cuda), E.to(cuda), cs, E.clone().to(cuda), straight_through=False, ema=False,
+        decay=0.8, eps=1e-5, svq_temp=temp, gumbel=gum.to(cuda))
+    got = idx.reshape(-1).cpu().numpy()
+    tol = gap_tol(x[0].numpy(), E.numpy()) / temp + 1e-6
+    assert_index_parity(got, want.numpy(), gap.numpy(), tol, f"svq temp={temp}")
+    assert int(counts.sum()) == M
+
+
+@pytest.mark.gpu
+def test_hip_svq_device_rng_distribution(cuda):
+    """Device-seeded draws follow softmax(dist/temp) (the reference's Categorical): one row
+    replicated 32768 times, per-code frequencies within 5 sigma of the oracle's fp64 softmax;
+    temp -> 0 is the deterministic argmax; successive calls draw different samples."""
+    from oracle import tvq_oracle as O
+    from timevqvae.models import VectorQuantize
+    g = torch.Generator().manual_seed(5)
+    D, K, n = 32, 64, 32768
+    E = torch.randn(K, D, generator=g) * 0.3
+    row = torch.randn(1, D, generator=g) * 0.3
+    temp = 2.0
+    p = torch.softmax(O.vq_dist(row, E).double() / temp, -1)[0]
+    vq = VectorQuantize(D, K).to(cuda).eval()
+    vq._codebook.embed.copy_(E)
+    x = row.expand(n, D).reshape(1, n, D).contiguous().to(cuda)
+    _, ind, _, _ = vq(x, svq_temp=temp)
+    freq = torch.bincount(ind.reshape(-1).cpu(), minlength=K).double() / n
+    sigma = torch.sqrt(p * (1 - p) / n)
+    assert ((freq - p).abs() <= 5 * sigma + 2e-4).all(), (freq - p).abs().max()
+    _, ind2, _, _ = vq(x, svq_temp=temp)
+    assert (ind2 != ind).any()
+    _, ind0, _, _ = vq(x, svq_temp=None)
+    assert (ind0 == int(p.argmax())).all()
+
+
+@pytest.mark.gpu
+def test_hip_svq_training_ema_uses_sampled_indices(cuda):
+    """Training with svq_temp: the EMA statistics follow the sampled indices (vq.py:227-245),
+    checked against the C oracle's EMA on the device's own draws."""
+    from timevqvae.models import VectorQuantize
+    g6 = golden("g6_svq.npz")
+    x = g6["x"]
+    E = g6["embed"]
+    K, D = E.shape
+    vq = _vq_module(K, D, cuda, embed=E, embed_avg=E.copy(), cluster_size=np.zeros(K, np.float32))
+    vq.train()
+    xt = torch.from_numpy(x).to(cuda).requires_grad_(True)
+    q, ind, loss, perp = vq(xt, svq_temp=4.0)
+    torch.cuda.synchronize()
+    cs, ea, Enew, counts, p = vq_ref.ema(x.reshape(-1, D), ind.reshape(-1).cpu().numpy(),
+                                          np.zeros(K, np.float32), E)
+    np.testing.assert_allclose(vq._codebook.cluster_size.cpu().numpy(), cs, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(vq._codebook.embed.cpu().numpy(), Enew, rtol=1e-5, atol=1e-5)
+    assert abs(float(perp) - p) < 1e-4 * p
+    # the straight-through output is the (pre-update) codeword of the sampled index
+    np.testing.assert_allclose(q.detach().cpu().numpy()[0], E[ind.reshape(-1).cpu().numpy()],
+                               rtol=0, atol=2e-6)
