@@ -48,7 +48,10 @@ class MaskGIT(nn.Module):
         self.gamma = self.gamma_func("cosine")
         from ..trainers.stage1 import Stage1  # circular import, as in the reference
         stage1 = kwargs.get("stage1")
-        if stage1 is None:
+        if stage1 is None and stage1_ckpt_fname is None:
+            # weights to follow (Stage2.load_from_checkpoint: stage2.ckpt holds stage1's)
+            stage1 = Stage1(input_length, in_channels, config)
+        elif stage1 is None:
             stage1 = Stage1.load_from_checkpoint(stage1_ckpt_fname, input_length=input_length,
                                                  in_channels=in_channels, config=config,
                                                  map_location="cpu")

@@ -13,6 +13,7 @@ import torch.nn as nn
 from ..hip import streams
 from ..hip.loss import l1_loss, mse_loss
 from ..hip.optim import FusedAdamW
+from ..utils.checkpoint import adapt_state_dict, read_state_dict, save_checkpoint
 from ..hip.signal import stft_encode
 from ..models import VectorQuantize, VQVAEDecoder, VQVAEEncoder
 from ..utils import (compute_downsample_rate, linear_warmup_cosine_annealingLR, quantize,
@@ -140,16 +141,17 @@ class Stage1(nn.Module):
 
     @classmethod
     def load_from_checkpoint(cls, checkpoint_path, map_location="cpu", input_length=None,
-                             in_channels=None, config=None, **kwargs):
-        """Lightning-style loader: {'state_dict': ...} or a bare state_dict (weights only)."""
-        ckpt = torch.load(checkpoint_path, map_location=map_location, weights_only=True)
-        sd = ckpt.get("state_dict", ckpt) if isinstance(ckpt, dict) else ckpt
-        model = cls(input_length, in_channels, config)
-        model.load_state_dict(sd)
+                             in_channels=None, config=None, strict=True, weights_only=True,
+                             **kwargs):
+        """Lightning-style loader (maskgit.py:52-59): a reference `stage1.ckpt`
+        ({'state_dict': ...}) or a bare state_dict; tensors only (utils/checkpoint.py)."""
+        sd = read_state_dict(checkpoint_path, map_location, weights_only)
+        model = cls(input_length, in_channels, config, **kwargs)
+        model.load_state_dict(adapt_state_dict(sd, model), strict=strict)
         return model
 
-    def save_checkpoint(self, path):
-        torch.save({"state_dict": self.state_dict()}, path)
+    def save_checkpoint(self, path, **extra):
+        save_checkpoint(self, path, **extra)
 
     def configure_optimizers(self):
         """stage1.py:229-236: AdamW(lr) + linear warmup / cosine annealing."""

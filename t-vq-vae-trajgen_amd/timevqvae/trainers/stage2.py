@@ -7,6 +7,7 @@ import torch.nn as nn
 from ..hip.optim import FusedAdamW
 from ..models.maskgit import MaskGIT
 from ..utils import linear_warmup_cosine_annealingLR
+from ..utils.checkpoint import adapt_state_dict, read_state_dict, save_checkpoint
 
 
 class Stage2(nn.Module):
@@ -36,6 +37,24 @@ class Stage2(nn.Module):
         x, y = batch
         mask_pred_loss, (loss_l, loss_h) = self.maskgit(x, y)
         return {"loss": mask_pred_loss, "mask_pred_loss_l": loss_l, "mask_pred_loss_h": loss_h}
+
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path, map_location="cpu", strict=True,
+                             weights_only=True, **kwargs):
+        """Lightning-style loader as generation/sampler.py:76-90 calls it: the constructor
+        arguments come as kwargs (the reference saves no hyper-parameters), the frozen
+        stage1 is read from `stage1_ckpt_fname` by MaskGIT (maskgit.py:52-59), then every
+        tensor of `stage2.ckpt` (stage1 copies included) is loaded, x-transformers key
+        drift adapted (utils/checkpoint.py)."""
+        sd = read_state_dict(checkpoint_path, map_location, weights_only)
+        kwargs.setdefault("stage1_ckpt_fname", None)
+        kwargs.setdefault("fcn_ckpt_fname", None)
+        model = cls(**kwargs)
+        model.load_state_dict(adapt_state_dict(sd, model), strict=strict)
+        return model
+
+    def save_checkpoint(self, path, **extra):
+        save_checkpoint(self, path, **extra)
 
     def configure_optimizers(self):
         """stage2.py:112-119 (frozen stage1 parameters carry no grad and are skipped)."""
