@@ -174,9 +174,9 @@ def roofline_leg(device):
     the largest single conv of the step (7.25 GFLOP).  As in the step it
     runs as conv_pack_weight + conv_t32_kernel (128-channel x 96-position tile on the
     32x32x2 fp32 MFMA, no split-K); the committed rocprofv3 summary
-    (profiles/r01c_roofline_kernel_stats.csv) lists the two and their averages sum to
+    (profiles/r01d_roofline_kernel_stats.csv) lists the two and their averages sum to
     avg_launch_ms.  `traffic` is the PMC-measured HBM bytes per op from
-    profiles/r01c_roofline_traffic.json (FETCH_SIZE x2 + WRITE_SIZE passes)."""
+    profiles/r01d_roofline_traffic.json (FETCH_SIZE x2 + WRITE_SIZE passes)."""
     from timevqvae.hip.conv import conv2d
     x = torch.randn(256, 128, 3, 32, device=device)
     w = torch.randn(128, 128, 3, 3, device=device) * 0.03
@@ -195,11 +195,11 @@ def roofline_leg(device):
     flops = 2.0 * (256 * 3 * 32) * 128 * (128 * 9)
     achieved = flops / (ms * 1e-3) / 1e12
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r01c_roofline_traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "r01d_roofline_traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath))["traffic_bytes"]
     return {"bound": "mfma", "kernel": "conv2d 128->128 3x3 @ (256,128,3,32): conv_pack_weight + "
-                                       "conv_t32_kernel<F,3,3,1,BK32> (32x32x2 fp32 MFMA)",
+                                       "conv_t32_kernel<F,3,3,1,BK64,NW12> (32x32x2 fp32 MFMA)",
             "achieved": round(achieved, 2), "peak": 157.3, "unit": "TFLOP/s",
             "frac": round(achieved / 157.3, 4), "traffic": traffic,
             "algorithmic_bytes": 4 * (256 * 128 * 3 * 32 * 2 + 128 * 128 * 9),

@@ -147,7 +147,8 @@ int tvq_conv_out_width(int64_t Win, int64_t KW, int64_t SW, int64_t transposed);
 /* engine selection (process-wide) bits: 1 = halo-tile kernel for fwd/dgrad convs with
  * few gathered channels (whose padded image and weight panel fit in 64 KB of LDS),
  * 2 = halo-tile weight gradient, 4 = halo-tile wherever it fits, 8 = no 32x32-MFMA
- * wide-channel tile; 0 forces the staged GEMMs; < 0 only queries.  Default 3.
+ * wide-channel tile, 16 / 32 = its K stage BK = 32 / 16 (default 64), 64 = its 4-wave
+ * block (default 12 waves); 0 forces the staged GEMMs; < 0 only queries.  Default 3.
  * Returns the previous setting. */
 int tvq_conv_config(int64_t halo);
 /* op: 0 conv2d fwd, 1 convT2d fwd, 2 conv2d dgrad, 3 convT2d dgrad, 4 conv2d wgrad,

@@ -452,19 +452,32 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_
                                            0x00020000);
 }
 
-template <int MODE, int KH, int KW, int SW, bool REPL, int BK>
-__global__ __launch_bounds__(256) void conv_t32_kernel(const float* __restrict__ in,
+// NW = waves per block: 4 (each wave 32 channels x 96 positions, three accumulators) or
+// 12 (each wave one 32x32 tile, 3 waves per SIMD so one wave's barrier / address work
+// hides behind the others' MFMAs).  Same k order either way.
+template <int MODE, int KH, int KW, int SW, bool REPL, int BK, int NW>
+__global__ __launch_bounds__(NW * 64) void conv_t32_kernel(const float* __restrict__ in,
                                                       const float* __restrict__ wt,
                                                       float* __restrict__ out, ConvGeom g,
                                                       Epi e) {
   constexpr int TN = 128, TM = 96;
-  constexpr int A4 = TN * BK / 4 / 256;  // dwordx4 A loads per thread (8)
-  constexpr int BL = TM * BK / 256;      // dword B loads per thread (24)
+  // operand staging: NW = 4 -> every thread loads A and B; NW = 12 -> waves 0-3 load A
+  // (weights), waves 4-11 load B (input), so the staging work is spread over all SIMDs
+  constexpr int LB = NW == 12 ? 512 : 256;  // threads loading B
+  constexpr int PSTEP = LB % 96;            // position step between a thread's B rows
+  constexpr int KSTEP = 3 * LB / 96;        // k step per 3 B elements
+  constexpr int A4 = TN * BK / 4 / 256;     // dwordx4 A loads per A-loading thread
+  constexpr int BL = TM * BK / LB;          // dword B loads per B-loading thread
   constexpr int BAD = 0x40000000;        // offset past any buffer end -> loads 0
   extern __shared__ float smem[];
   float* As = smem;                      // [2][BK][TN]
   float* Bs = smem + 2 * BK * TN;        // [2][BK][TM]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int NJ = 12 / NW;  // 32-position tiles per wave
+  const bool aload = NW == 4 || tid < 256;
+  const bool bload = NW == 4 || tid >= 256;
+  const int bt = NW == 4 ? tid : tid - 256;  // index among the B-loading threads
+  const int wch = wid & 3, wpos = (wid >> 2) * NJ;
   const int n0 = blockIdx.y * TN, m0 = blockIdx.x * TM;
   const int csteps = g.C / BK;
   const int nsteps = KH * KW * csteps;
@@ -472,15 +485,15 @@ __global__ __launch_bounds__(256) void conv_t32_kernel(const float* __restrict__
   const __amdgpu_buffer_rsrc_t rin = buf_rsrc(in, (int64_t)g.B * g.C * plane * 4);
   const __amdgpu_buffer_rsrc_t rwt = buf_rsrc(wt, (int64_t)KH * KW * g.C * g.N * 4);
 
-  // B element i (< BL) of this thread: e = tid + 256 i -> position (tid + 64 (i%3)) % 96,
-  // row k = (tid + 256 (i%3)) / 96 + 8 (i/3)
-  static_assert(BK % 8 == 0 && (TM * BK) % 768 == 0, "stage rows");
+  // B element i (< BL) of this thread: e = bt + LB i -> position (bt + PSTEP (i%3)) % 96,
+  // row k = (bt + LB (i%3)) / 96 + KSTEP (i/3)
+  static_assert(BK % 8 == 0 && (TM * BK) % (3 * LB) == 0, "stage rows");
   int pm_b[3], pm_h[3], pm_w[3], krow[3];
   bool pm_ok[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
-    const int m = m0 + (tid + 64 * u) % TM;
-    krow[u] = (tid + 256 * u) / TM;
+    const int m = m0 + (bt + PSTEP * u) % TM;
+    krow[u] = (bt + LB * u) / TM;
     pm_ok[u] = m < g.Mpos;
     const int mc = pm_ok[u] ? m : 0;
     const uint32_t bh = fdiv((uint32_t)mc, g.fd_wo);
@@ -495,11 +508,14 @@ __global__ __launch_bounds__(256) void conv_t32_kernel(const float* __restrict__
     const int tap = step / csteps;
     const int c0 = (step - tap * csteps) * BK;
     const int kh = tap / KW, kw = tap - kh * KW;
-    const int abase = (((tap * g.C + c0 + a_k) * g.N) + a_n) * 4;
+    if (aload) {
+      const int abase = (((tap * g.C + c0 + a_k) * g.N) + a_n) * 4;
 #pragma unroll
-    for (int i = 0; i < A4; ++i)
-      ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rwt, abase, i * 8 * g.N * 4, 0));
+      for (int i = 0; i < A4; ++i)
+        ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               rwt, abase, i * 8 * g.N * 4, 0));
+    }
+    if (!bload) return;
     int boff[3];
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
@@ -526,23 +542,27 @@ __global__ __launch_bounds__(256) void conv_t32_kernel(const float* __restrict__
 #pragma unroll
     for (int i = 0; i < BL; ++i)
       rb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                            rin, boff[i % 3], (i / 3) * 8 * plane * 4, 0));
+                                            rin, boff[i % 3], (i / 3) * KSTEP * plane * 4, 0));
   };
   auto store = [&](int buf) {
-    float* a = As + buf * BK * TN + a_k * TN + ((tid & 31) << 2);
+    if (aload) {
+      float* a = As + buf * BK * TN + a_k * TN + ((tid & 31) << 2);
 #pragma unroll
-    for (int i = 0; i < A4; ++i) *reinterpret_cast<float4*>(a + i * 8 * TN) = ra[i];
-    float* bb = Bs + buf * BK * TM;
+      for (int i = 0; i < A4; ++i) *reinterpret_cast<float4*>(a + i * 8 * TN) = ra[i];
+    }
+    if (bload) {
+      float* bb = Bs + buf * BK * TM;
 #pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      const int u = i % 3;
-      bb[(krow[u] + 8 * (i / 3)) * TM + (tid + 64 * u) % TM] = rb[i];
+      for (int i = 0; i < BL; ++i) {
+        const int u = i % 3;
+        bb[(krow[u] + KSTEP * (i / 3)) * TM + (bt + PSTEP * u) % TM] = rb[i];
+      }
     }
   };
 
-  floatx16 acc[3];
+  floatx16 acc[NJ];
 #pragma unroll
-  for (int jb = 0; jb < 3; ++jb)
+  for (int jb = 0; jb < NJ; ++jb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[jb][r] = 0.f;
   const int r32 = lane & 31, hl = lane >> 5;
@@ -552,29 +572,46 @@ __global__ __launch_bounds__(256) void conv_t32_kernel(const float* __restrict__
   for (int step = 0; step < nsteps; ++step) {
     const int buf = step & 1;
     if (step + 1 < nsteps) load(step + 1);
-    const float* a = As + buf * BK * TN + hl * TN + wid * 32 + r32;
-    const float* bb = Bs + buf * BK * TM + hl * TM + r32;
+    const float* a = As + buf * BK * TN + hl * TN + wch * 32 + r32;
+    const float* bb = Bs + buf * BK * TM + hl * TM + wpos * 32 + r32;
+    // fragments of FG k-pairs are read one group ahead of the MFMAs that use them, so
+    // the LDS latency hides behind FG*3 MFMAs instead of stalling every one or two
+    constexpr int FG = 4, NG = BK / 2 / FG;
+    float fa[2][FG], fb[2][FG][NJ];
+    auto fread = [&](int grp, int slot) {
 #pragma unroll
-    for (int kp = 0; kp < BK / 2; ++kp) {
-      const float av = a[2 * kp * TN];
-      float bv[3];
+      for (int u = 0; u < FG; ++u) {
+        const int kp = grp * FG + u;
+        fa[slot][u] = a[2 * kp * TN];
 #pragma unroll
-      for (int jb = 0; jb < 3; ++jb) bv[jb] = bb[2 * kp * TM + jb * 32];
+        for (int jb = 0; jb < NJ; ++jb) fb[slot][u][jb] = bb[2 * kp * TM + jb * 32];
+      }
+    };
+    fread(0, 0);
 #pragma unroll
-      for (int jb = 0; jb < 3; ++jb)
-        acc[jb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[jb], acc[jb], 0, 0, 0);
+    for (int grp = 0; grp < NG; ++grp) {
+      if (grp + 1 < NG) fread(grp + 1, (grp + 1) & 1);
+#pragma unroll
+      for (int u = 0; u < FG; ++u)
+#pragma unroll
+        for (int jb = 0; jb < NJ; ++jb)
+          acc[jb] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[grp & 1][u], fb[grp & 1][u][jb],
+                                                         acc[jb], 0, 0, 0);
+      // emit the next group's LDS reads ahead of this group's MFMAs (T19)
+      __builtin_amdgcn_sched_group_barrier(0x100, (1 + NJ) * FG, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NJ * FG, 0);
     }
     if (step + 1 < nsteps) store(buf ^ 1);
     __syncthreads();
   }
 
-  // epilogue: acc[jb][reg] = (channel n0 + 32 wid + (reg & 3) + 8 (reg >> 2) + 4 hl,
-  // position m0 + 32 jb + lane % 32); bias, dropout, residual as epi_store
+  // epilogue: acc[jb][reg] = (channel n0 + 32 wch + (reg & 3) + 8 (reg >> 2) + 4 hl,
+  // position m0 + 32 (wpos + jb) + lane % 32); bias, dropout, residual as epi_store
   const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
   const int64_t hw = (int64_t)g.Hout * g.Wo;
 #pragma unroll
-  for (int jb = 0; jb < 3; ++jb) {
-    const int m = m0 + jb * 32 + r32;
+  for (int jb = 0; jb < NJ; ++jb) {
+    const int m = m0 + (wpos + jb) * 32 + r32;
     const bool pv = m < g.Mpos;
     const int mc = pv ? m : 0;
     const uint32_t bh = fdiv((uint32_t)mc, g.fd_wo);
@@ -584,7 +621,7 @@ __global__ __launch_bounds__(256) void conv_t32_kernel(const float* __restrict__
     const int64_t ob = ((int64_t)b * g.N * g.Hout + h) * g.Wo + w;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int n = n0 + wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const int n = n0 + wch * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
       if (!pv || n >= g.N) continue;
       const int64_t o = ob + (int64_t)n * hw;
       float v = acc[jb][r] + (e.bias ? e.bias[n] : 0.f);
@@ -595,10 +632,12 @@ __global__ __launch_bounds__(256) void conv_t32_kernel(const float* __restrict__
   }
 }
 
-// LDS per block: 2 stages x BK x (128 + 96) floats.  BK = 32 (56 KB) leaves room on
-// the CU for the concurrently running streams' kernels; BK = 64 (112 KB) is 5 % faster
-// alone but starves them (joint step 8.7 vs 7.3 ms), so 32 is the default.
-static int g_t32_bk = 32;
+// LDS per block: 2 stages x BK x (128 + 96) floats.  With 12 waves per block, BK = 64
+// (112 KB, 18 barriers for a 3x3 128-channel conv) runs the 128->128 conv at 78.7 us vs
+// 86.7 us for BK = 32 (56 KB); in the joint step, where the LDS is shared with the
+// concurrent streams' kernels, the two are within 0.5 % (7.29 vs 7.25 ms).
+static int g_t32_bk = 64;  // K-stage depth: 64, or 32 / 16 with tvq_conv_config bit 16 / 32
+static int g_t32_nw = 12;  // waves per block (12, or 4 with tvq_conv_config bit 64)
 static size_t t32_lds(int bk) { return (size_t)2 * bk * (128 + 96) * 4; }
 
 // Weight gradient: rows = n (channels of G), cols = k' = (c, kh, kw), reduction over
@@ -1391,16 +1430,26 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
       static bool lds_set = false;  // > 64 KB of dynamic LDS must be opted into once
       if (!lds_set) {
         (void)hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&conv_t32_kernel<MODE, KH, KW, SW, REPL, 64>),
+            reinterpret_cast<const void*>(&conv_t32_kernel<MODE, KH, KW, SW, REPL, 64, 4>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)t32_lds(64));
+        (void)hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&conv_t32_kernel<MODE, KH, KW, SW, REPL, 64, 12>),
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)t32_lds(64));
         lds_set = true;
       }
-      if (g_t32_bk == 64)
-        hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, 64>), grid, dim3(256),
-                           t32_lds(64), st, in, wt, out, g, e);
-      else
-        hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, 32>), grid, dim3(256),
-                           t32_lds(32), st, in, wt, out, g, e);
+#define TVQ_T32(BKV, NWV)                                                                   \
+  hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, BKV, NWV>), grid, dim3(64 * NWV), \
+                     t32_lds(BKV), st, in, wt, out, g, e)
+      if (g_t32_nw == 12) {
+        if (g_t32_bk == 64) TVQ_T32(64, 12);
+        else if (g_t32_bk == 16) TVQ_T32(16, 12);
+        else TVQ_T32(32, 12);
+      } else {
+        if (g_t32_bk == 64) TVQ_T32(64, 4);
+        else if (g_t32_bk == 16) TVQ_T32(16, 4);
+        else TVQ_T32(32, 4);
+      }
+#undef TVQ_T32
       return;
     }
     int sps;
@@ -1556,11 +1605,13 @@ static Epi make_epi(const float* bias, const float* residual, float drop_p,
 }
 
 extern "C" int tvq_conv_config(int64_t halo) {
-  const int prev = g_conv_halo | (g_conv_t32 ? 0 : 8) | (g_t32_bk == 64 ? 16 : 0);
+  const int prev = g_conv_halo | (g_conv_t32 ? 0 : 8) | (g_t32_bk == 32 ? 16 : 0) |
+                   (g_t32_bk == 16 ? 32 : 0) | (g_t32_nw == 4 ? 64 : 0);
   if (halo >= 0) {
     g_conv_halo = (int)(halo & 7);
     g_conv_t32 = (halo & 8) ? 0 : 1;
-    g_t32_bk = (halo & 16) ? 64 : 32;
+    g_t32_bk = (halo & 16) ? 32 : ((halo & 32) ? 16 : 64);
+    g_t32_nw = (halo & 64) ? 4 : 12;
   }
   return prev;
 }
