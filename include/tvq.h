@@ -335,6 +335,20 @@ int tvq_maskgit_remask(const float* selp, int64_t B, int64_t n, int64_t k, float
 int tvq_codebook_gather_nchw(const int64_t* idx, int64_t B, int64_t P, int64_t D, const float* E,
                              float* out, tvq_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * ROCKET features (evaluation/rocket_functions.py:60-126 apply_kernel / apply_kernels, the
+ * reference's numba CPU transform used by the FID/IS evaluation, sampler.py:184-189).
+ * X (n, L) float64 row stride ldx; the kernels as generate_kernels (:21-57) returns them:
+ * weights (sum of lengths) float64 packed back to back, woff[k] = offset of kernel k's
+ * weights, lengths (1..16), biases float64, dilations (>= 1), paddings; out (n, 2 nk)
+ * float64 = [ppv_k, max_k] per kernel.  float64, unfused multiply/add in the reference's
+ * order: equal to its interpreted loop bit for bit.  Kernels outside the contract get NaN
+ * features.  L <= 8192. */
+int tvq_rocket_apply(const double* X, int64_t n, int64_t L, int64_t ldx, const double* weights,
+                     const int32_t* woff, const int32_t* lengths, const double* biases,
+                     const int32_t* dilations, const int32_t* paddings, int64_t nk, double* out,
+                     tvq_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

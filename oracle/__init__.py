@@ -12,4 +12,7 @@ Contents
   vq_ref.c       plain-C restatement of the VQ assign (L2 + argmin) and EMA
                  update (vq.py:197-251), with an fp64 top-2 gap for near-tie
                  qualification; built into oracle/build/libvq_ref.so.
+  rocket_ref.c   plain-C fp64 restatement of the ROCKET transform
+                 (evaluation/rocket_functions.py:60-126), pthreads over examples for
+                 the CPU baseline; built into oracle/build/librocket_ref.so.
 """

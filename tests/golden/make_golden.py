@@ -12,6 +12,7 @@ files are loaded by file path with minimal import stubs:
   * timevqvae/models/maskgit.py        (stub transformer; sampling/masking loops only)
 
 G6 (stochastic VQ) alone: python tests/golden/make_golden.py svq
+G7 (ROCKET features, evaluation/rocket_functions.py with a numba stub) alone: ... rocket
 
 Only the .npz outputs are committed (tests/golden/*.npz).  Usage:
 
@@ -328,8 +329,44 @@ def gen_svq(ref):
     np.savez_compressed(os.path.join(OUT, "g6_svq.npz"), **d)
 
 
+# --------------------------------------------------------------------------- G7
+def gen_rocket():
+    """ROCKET features (evaluation/rocket_functions.py:21-118).  numba is absent, so the
+    file is loaded with `njit` as an identity decorator and `prange` as `range`: the same
+    Python source, run by the interpreter in float64 (numba's fastmath may reassociate;
+    the tests' tolerances cover it).  generate_kernels then draws from numpy's global RNG
+    (under numba it would draw from numba's own stream), seeded below."""
+    numba = types.ModuleType("numba")
+
+    def njit(*a, **k):
+        if len(a) == 1 and callable(a[0]) and not k:
+            return a[0]
+        return lambda f: f
+    numba.njit = njit
+    numba.prange = range
+    sys.modules["numba"] = numba
+    if not hasattr(np, "NINF"):  # numpy >= 2 dropped the alias the reference uses (:67)
+        np.NINF = -np.inf
+    rk = _load("ref_rocket", f"{REF}/evaluation/rocket_functions.py")
+    d = {}
+    for tag, (n, L, nk, seed) in {"a": (6, 128, 64, 7), "b": (3, 256, 40, 8)}.items():
+        np.random.seed(seed)
+        kern = rk.generate_kernels(L, nk)
+        X = np.cumsum(np.random.randn(n, L), axis=1)
+        X[0, :] = 0.0  # an all-zero series: every sum equals the bias
+        feats = rk.apply_kernels(X, kern)
+        w, lengths, biases, dil, pad = kern
+        d[f"{tag}_X"], d[f"{tag}_weights"], d[f"{tag}_lengths"] = X, w, lengths
+        d[f"{tag}_biases"], d[f"{tag}_dilations"], d[f"{tag}_paddings"] = biases, dil, pad
+        d[f"{tag}_features"] = feats
+    np.savez_compressed(os.path.join(OUT, "g7_rocket.npz"), **d)
+
+
 def main():
     torch.set_num_threads(8)
+    if sys.argv[1:] == ["rocket"]:  # regenerate only G7
+        gen_rocket()
+        return
     ref = load_reference()
     if sys.argv[1:] == ["svq"]:  # regenerate only G6
         gen_svq(ref)
@@ -340,6 +377,7 @@ def main():
     gen_stage1(ref, "cfgB", B=2, C=6, T=256, K=512, init_dim=4, hid_dim=128, seed=5)
     gen_maskgit(ref)
     gen_svq(ref)
+    gen_rocket()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
