@@ -151,6 +151,18 @@ int tvq_conv_out_width(int64_t Win, int64_t KW, int64_t SW, int64_t transposed);
  * block (default 12 waves); 0 forces the staged GEMMs; < 0 only queries.  Default 3.
  * Returns the previous setting. */
 int tvq_conv_config(int64_t halo);
+
+/* Per-step weight-pack cache for the staged-GEMM convs (their weights are repacked to
+ * [tap][c][n] on every call otherwise).  begin(id, arena, cap, stream) opens a scope: it
+ * repacks every (weight, view) recorded under `id` into `arena` with a few batched
+ * launches on `stream`; inside the scope a recorded weight is read from its arena slot and
+ * a new one is packed into a fresh slot and recorded (arena full -> the per-call path).
+ * A different id (or arena) drops the recorded entries.  The weights must not change
+ * between begin and end (open it around forward+backward, not the optimizer step); the
+ * scope is process-wide host state, one at a time.  entries() = recorded count. */
+int tvq_conv_packcache_begin(int64_t id, float* arena, int64_t cap_floats, tvq_stream_t stream);
+int tvq_conv_packcache_end(void);
+int64_t tvq_conv_packcache_entries(void);
 /* op: 0 conv2d fwd, 1 convT2d fwd, 2 conv2d dgrad, 3 convT2d dgrad, 4 conv2d wgrad,
  * 5 convT2d wgrad; (Ci, Co, Wi) = the layer's input channels, output channels, input
  * width.  Returns the workspace size in floats (>= 1), -1 for a bad op. */

@@ -23,6 +23,8 @@
 
 #include <stdlib.h>
 
+#include <vector>
+
 namespace tvq {
 
 struct FastDiv {  // q = n / d for 0 <= n < 2^30, d >= 1
@@ -1357,17 +1359,82 @@ __global__ void conv_pack_weight_kernel(const float* __restrict__ w, int N, int 
   }
 }
 
-// Pack `wt` into `ws` (N*C*KK floats) when given and retarget the geometry's weight strides.
+// Per-step weight-pack cache (tvq_conv_packcache_*).  Inside a scope, the first time a
+// (weight, view) is packed it gets a slot in the caller's arena and is recorded; at the
+// next scope's begin every recorded entry is repacked from the current weights by a few
+// batched launches, and the convs of the scope read their slot without packing again.
+// The scope must not contain weight updates (a trainer opens it around forward+backward,
+// the optimizer step is outside).  Entries belong to one cache id and are dropped when
+// another id begins, so a freed model's weights are never read.
+struct PackEntry {
+  const float* src;
+  int N, C, KK;
+  int64_t wsn, wsc, off;
+};
+static std::vector<PackEntry> g_pc;
+static int64_t g_pc_id = -1, g_pc_cap = 0, g_pc_used = 0;
+static float* g_pc_arena = nullptr;
+static bool g_pc_active = false;
+
+constexpr int PACK_BATCH = 24;
+struct PackBatch {
+  const float* src[PACK_BATCH];
+  int64_t wsn[PACK_BATCH], wsc[PACK_BATCH], off[PACK_BATCH];
+  int N[PACK_BATCH], C[PACK_BATCH], KK[PACK_BATCH];
+};
+
+// blockIdx.y = entry; blocks stride over the entry's N*C*KK elements ([tap][c][n] order)
+__global__ void conv_pack_multi_kernel(PackBatch b, float* __restrict__ arena) {
+  const int j = blockIdx.y;
+  const int N = b.N[j], C = b.C[j];
+  const int64_t total = (int64_t)N * C * b.KK[j];
+  const float* w = b.src[j];
+  float* out = arena + b.off[j];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(i % N);
+    const int64_t r = i / N;
+    const int c = (int)(r % C);
+    const int tap = (int)(r / C);
+    out[i] = w[n * b.wsn[j] + c * b.wsc[j] + tap];
+  }
+}
+
+static void pack_launch(const float* wt, int N, int C, int KK, int64_t wsn, int64_t wsc,
+                        float* dst, hipStream_t st) {
+  const int64_t total = (int64_t)N * C * KK;
+  const int blocks = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+  hipLaunchKernelGGL(conv_pack_weight_kernel, dim3(blocks), dim3(256), 0, st, wt, N, C, KK, wsn,
+                     wsc, dst);
+}
+
+// Pack `wt` into `ws` (N*C*KK floats) when given -- or serve it from the active pack cache
+// -- and retarget the geometry's weight strides.
 static const float* pack_weight(const float* wt, ConvGeom& g, int KK, float* ws, hipStream_t st) {
   if (!ws) return wt;
   const int64_t total = (int64_t)g.N * g.C * KK;
-  const int blocks = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
-  hipLaunchKernelGGL(conv_pack_weight_kernel, dim3(blocks), dim3(256), 0, st, wt, g.N, g.C, KK,
-                     g.wsn, g.wsc, ws);
+  float* dst = ws;
+  bool need = true;
+  if (g_pc_active) {
+    for (const PackEntry& p : g_pc)
+      if (p.src == wt && p.N == g.N && p.C == g.C && p.KK == KK && p.wsn == g.wsn &&
+          p.wsc == g.wsc) {
+        dst = g_pc_arena + p.off;
+        need = false;  // repacked at this scope's begin
+        break;
+      }
+    const int64_t slot = (total + 63) / 64 * 64;
+    if (need && g_pc_used + slot <= g_pc_cap) {
+      g_pc.push_back({wt, g.N, g.C, KK, g.wsn, g.wsc, g_pc_used});
+      dst = g_pc_arena + g_pc_used;
+      g_pc_used += slot;
+    }
+  }
+  if (need) pack_launch(wt, g.N, g.C, KK, g.wsn, g.wsc, dst, st);
   g.wsn = 1;
   g.wsc = g.N;
   g.wst = (int64_t)g.N * g.C;
-  return ws;
+  return dst;
 }
 
 static void tap_tile(int N, int* TN, int* TM) {
@@ -1603,6 +1670,43 @@ static Epi make_epi(const float* bias, const float* residual, float drop_p,
   e.offset = offset;
   return e;
 }
+
+extern "C" int tvq_conv_packcache_begin(int64_t id, float* arena, int64_t cap_floats,
+                                        tvq_stream_t stream) {
+  TVQ_CHECK_ARG(id >= 0 && arena && cap_floats > 0, "tvq_conv_packcache_begin: bad arguments");
+  TVQ_CHECK_ARG(!g_pc_active, "tvq_conv_packcache_begin: a scope is already open");
+  if (id != g_pc_id || arena != g_pc_arena || cap_floats != g_pc_cap) {
+    g_pc.clear();
+    g_pc_id = id;
+    g_pc_arena = arena;
+    g_pc_cap = cap_floats;
+    g_pc_used = 0;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  for (size_t i0 = 0; i0 < g_pc.size(); i0 += PACK_BATCH) {
+    PackBatch b;
+    int n = 0;
+    int64_t most = 0;
+    for (size_t i = i0; i < g_pc.size() && n < PACK_BATCH; ++i, ++n) {
+      const PackEntry& p = g_pc[i];
+      b.src[n] = p.src; b.wsn[n] = p.wsn; b.wsc[n] = p.wsc; b.off[n] = p.off;
+      b.N[n] = p.N; b.C[n] = p.C; b.KK[n] = p.KK;
+      const int64_t t = (int64_t)p.N * p.C * p.KK;
+      most = t > most ? t : most;
+    }
+    const int bx = (int)((most + 255) / 256 < 512 ? (most + 255) / 256 : 512);
+    hipLaunchKernelGGL(conv_pack_multi_kernel, dim3(bx, n), dim3(256), 0, st, b, g_pc_arena);
+  }
+  g_pc_active = true;
+  return launch_status("tvq_conv_packcache_begin");
+}
+
+extern "C" int tvq_conv_packcache_end(void) {
+  g_pc_active = false;
+  return TVQ_OK;
+}
+
+extern "C" int64_t tvq_conv_packcache_entries(void) { return (int64_t)g_pc.size(); }
 
 extern "C" int tvq_conv_config(int64_t halo) {
   const int prev = g_conv_halo | (g_conv_t32 ? 0 : 8) | (g_t32_bk == 32 ? 16 : 0) |

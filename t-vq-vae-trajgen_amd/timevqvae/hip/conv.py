@@ -30,6 +30,33 @@ def _bias_grad(g, dev, sink=None):
 
 USE_WORKSPACE = True  # tests flip this to cover the no-workspace (in-place weight) path
 
+
+class PackCache:
+    """Per-step weight-pack cache (include/tvq.h tvq_conv_packcache_*): inside `scope()` the
+    staged-GEMM convs read [tap][c][n]-packed weights from one arena that the scope's entry
+    repacks with a few batched launches, instead of one pack launch per conv call.  Open
+    the scope around forward+backward only: the weights must not change inside it."""
+
+    _next_id = [0]
+
+    def __init__(self, device, floats=1 << 23):
+        self.arena = torch.empty(int(floats), device=device, dtype=torch.float32)
+        self.id = PackCache._next_id[0]
+        PackCache._next_id[0] += 1
+
+    @contextlib.contextmanager
+    def scope(self):
+        call("tvq_conv_packcache_begin", self.id, ptr(self.arena), self.arena.numel(),
+             stream_ptr())
+        try:
+            yield self
+        finally:
+            call("tvq_conv_packcache_end")
+
+    @staticmethod
+    def entries():
+        return value("tvq_conv_packcache_entries")
+
 # tvq_conv_workspace ops
 OP_FWD, OP_T_FWD, OP_DGRAD, OP_T_DGRAD, OP_WGRAD, OP_T_WGRAD = range(6)
 

@@ -98,3 +98,34 @@ def test_streams_match_single_stream(cuda):
     assert ls == lm
     for a, b in zip(_state(single), _state(multi)):
         assert torch.equal(a, b)
+
+
+def test_pack_cache_matches_per_call_packing(cuda):
+    """The per-step weight-pack cache (one batched repack at the scope's begin, convs read
+    the arena) equals packing in every conv call bit for bit over several optimizer steps
+    (the weights change between steps, so a stale pack would show), eager and graphed."""
+    import bench
+    from timevqvae.hip.conv import PackCache
+    batch = _batch(cuda, B=32, C=6, L=256)
+    ref = bench.JointTrainer(cuda, 1, cfg=_cfg(), length=256, channels=6)
+    ref.packs = None
+    lr = [tuple(float(o["loss"].detach().sum()) for o in ref.step(batch)) for _ in range(3)]
+    cached = bench.JointTrainer(cuda, 1, cfg=_cfg(), length=256, channels=6)
+    assert cached.packs is not None
+    lc = [tuple(float(o["loss"].detach().sum()) for o in cached.step(batch)) for _ in range(3)]
+    assert PackCache.entries() > 0
+    torch.cuda.synchronize()
+    assert lr == lc
+    for a, b in zip(_state(ref), _state(cached)):
+        assert torch.equal(a, b)
+    # graphed with the cache == eager without it, two replays further
+    ref2 = [tuple(float(o["loss"].detach().sum()) for o in ref.step(batch)) for _ in range(4)]
+    g = bench.JointTrainer(cuda, 1, cfg=_cfg(), length=256, channels=6)
+    for _ in range(3):
+        g.step(batch)
+    g.capture(batch)  # 2 more eager warmup steps, then capture
+    lg = [tuple(float(o["loss"].detach().sum()) for o in g.step(batch)) for _ in range(2)]
+    torch.cuda.synchronize()
+    assert lg == ref2[2:]
+    for a, b in zip(_state(ref), _state(g)):
+        assert torch.equal(a, b)
