@@ -220,9 +220,11 @@ int tvq_bn_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t HW
 int tvq_snake_fwd(const float* x, int64_t B, int64_t C, int64_t HW, const float* a, float* y,
                   tvq_stream_t stream);
 int64_t tvq_snake_workspace(int64_t B, int64_t C, int64_t HW);
+/* dx = Snake'(x) dy (+ dx_add, nullable: the ResBlock skip path's gradient of the same x,
+ * summed here instead of by a separate autograd add); da (+)= its per-channel sum */
 int tvq_snake_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t HW,
-                  const float* a, float* dx, float* da, int64_t accumulate, void* workspace,
-                  tvq_stream_t stream);
+                  const float* a, const float* dx_add, float* dx, float* da, int64_t accumulate,
+                  void* workspace, tvq_stream_t stream);
 /* backward of the dropout fused in tvq_conv2d_fwd (same seed, same flat index) */
 int tvq_dropout_bwd(const float* dy, int64_t n, float p, const int64_t* seed_ptr,
                     uint64_t offset, float* dx, tvq_stream_t stream);

@@ -297,6 +297,7 @@ __global__ __launch_bounds__(256) void snake_bwd_kernel(const float* __restrict_
                                                         const float* __restrict__ x, int B, int C,
                                                         int HW, Div16 dhw, int chunks,
                                                         const float* __restrict__ a,
+                                                        const float* __restrict__ dx_add,
                                                         float* __restrict__ dx,
                                                         double* __restrict__ part,
                                                         int* __restrict__ cnt,
@@ -324,7 +325,8 @@ __global__ __launch_bounds__(256) void snake_bwd_kernel(const float* __restrict_
       float sn, cs;
       sincosf(av * xv[u], &sn, &cs);
       const float t = 2.0f * sn * cs;
-      dx[o[u]] = g[u] + g[u] * inv_a * t * av;
+      const float d = g[u] + g[u] * inv_a * t * av;
+      dx[o[u]] = dx_add ? d + dx_add[o[u]] : d;
       s_da += (double)(g[u] * inv_a * t * xv[u]) - (double)(g[u] * (sn * sn) * inv_a * inv_a);
     }
   }
@@ -454,15 +456,16 @@ extern "C" int64_t tvq_snake_workspace(int64_t B, int64_t C, int64_t HW) {
 }
 
 extern "C" int tvq_snake_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t HW,
-                             const float* a, float* dx, float* da, int64_t accumulate,
-                             void* workspace, tvq_stream_t stream) {
+                             const float* a, const float* dx_add, float* dx, float* da,
+                             int64_t accumulate, void* workspace, tvq_stream_t stream) {
   TVQ_CHECK_ARG(dy && x && a && dx && da && workspace, "tvq_snake_bwd: bad arguments");
   TVQ_CHECK_ARG(norm_dims_ok(B, C, HW), "tvq_snake_bwd: tensor too large");
   hipStream_t st = (hipStream_t)stream;
   const int chunks = bn_chunks(B, HW);
   int* cnt = counters(C, FIN_NORM);
   hipLaunchKernelGGL(snake_bwd_kernel, dim3((int)C, chunks), dim3(256), 0, st, dy, x, (int)B,
-                     (int)C, (int)HW, make_div16(HW), chunks, a, dx, (double*)workspace, cnt, da,
+                     (int)C, (int)HW, make_div16(HW), chunks, a, dx_add, dx, (double*)workspace,
+                     cnt, da,
                      (int)accumulate);
   if (!cnt)
     hipLaunchKernelGGL(snake_bwd_final_kernel, dim3((int)C), dim3(64), 0, st,

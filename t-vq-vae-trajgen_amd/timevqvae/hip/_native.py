@@ -68,7 +68,7 @@ sig("tvq_bn_eval_fwd", P, I64, I64, I64, P, P, P, P, F32, P, P, P, P)
 sig("tvq_bn_bwd", P, P, I64, I64, I64, P, P, P, P, P, P, P, P, P, I64, P, P)
 sig("tvq_snake_fwd", P, I64, I64, I64, P, P, P)
 sig("tvq_snake_workspace", I64, I64, I64, restype=I64)
-sig("tvq_snake_bwd", P, P, I64, I64, I64, P, P, P, I64, P, P)
+sig("tvq_snake_bwd", P, P, I64, I64, I64, P, P, P, P, I64, P, P)
 sig("tvq_dropout_bwd", P, I64, F32, P, U64, P, P)
 sig("tvq_reduce_rows_workspace", I64, I64, restype=I64)
 sig("tvq_reduce_rows", P, I64, I64, I64, P, I64, P, P)

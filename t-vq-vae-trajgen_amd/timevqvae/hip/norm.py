@@ -88,19 +88,47 @@ class _Snake(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        x, a = ctx.saved_tensors
-        B, C, HW = _dims(x)
-        g = gy.contiguous()
-        dx = torch.empty_like(x)
-        sink = grad_sink(ctx.a_param)
-        da = sink if sink is not None else torch.empty(C, device=x.device)
-        ws = torch.empty(value("tvq_snake_workspace", B, C, HW), device=x.device, dtype=torch.uint8)
-        call("tvq_snake_bwd", ptr(g), ptr(x), B, C, HW, ptr(a), ptr(dx), ptr(da), int(sink is not None),
-             ptr(ws), stream_ptr())
-        return dx, (None if sink is not None else da.view_as(ctx.a_param))
+        return _snake_bwd(ctx, gy, None)
+
+
+def _snake_bwd(ctx, gy, g_add):
+    x, a = ctx.saved_tensors
+    B, C, HW = _dims(x)
+    g = gy.contiguous()
+    if g_add is not None and (g_add.shape != x.shape or not g_add.is_contiguous()):
+        g_add = g_add.contiguous().view_as(x)
+    dx = torch.empty_like(x)
+    sink = grad_sink(ctx.a_param)
+    da = sink if sink is not None else torch.empty(C, device=x.device)
+    ws = torch.empty(value("tvq_snake_workspace", B, C, HW), device=x.device, dtype=torch.uint8)
+    call("tvq_snake_bwd", ptr(g), ptr(x), B, C, HW, ptr(a), ptr(g_add), ptr(dx), ptr(da),
+         int(sink is not None), ptr(ws), stream_ptr())
+    return dx, (None if sink is not None else da.view_as(ctx.a_param))
+
+
+class _SnakeSkip(torch.autograd.Function):
+    """(Snake(x), x): the second output is x itself for the ResBlock skip path, so the
+    backward receives both gradients of x and sums them in the Snake backward kernel
+    instead of autograd adding them in a separate launch."""
+
+    @staticmethod
+    def forward(ctx, x, a):
+        y = _Snake.forward(ctx, x, a)
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, gy, gx):
+        if gy is None:
+            return gx, None
+        return _snake_bwd(ctx, gy, gx)
 
 
 def snake(x, a):
     """SnakeActivation (train_utils.py:446-448): x + (1/a) sin(a x)^2; a: the (1,C,1,1)
     parameter or a (C,) tensor."""
     return _Snake.apply(x, a)
+
+
+def snake_skip(x, a):
+    """(snake(x, a), x) with the two gradients of x summed inside the Snake backward."""
+    return _SnakeSkip.apply(x, a)

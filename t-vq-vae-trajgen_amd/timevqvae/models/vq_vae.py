@@ -19,7 +19,7 @@ import torch.nn as nn
 from ..hip import rng
 from ..hip.conv import conv2d, conv_transpose2d
 from ..hip.linear import linear
-from ..hip.norm import bn_snake, snake
+from ..hip.norm import bn_snake, snake, snake_skip
 from ..hip.signal import istft_decode, stft_encode
 from ..utils import SnakeActivation
 from ..utils.train_utils import band_of
@@ -57,9 +57,10 @@ class ResBlock(nn.Module):
 
     def forward(self, x):
         c = self.convs
-        h = conv2d(snake(x, _a(c[0])), c[1].weight, c[1].bias)
+        s, xs = snake_skip(x, _a(c[0]))  # xs: x, its skip-path gradient summed in Snake bwd
+        h = conv2d(s, c[1].weight, c[1].bias)
         h = bn_snake(h, c[2], _a(c[3]))
-        r = x if isinstance(self.proj, nn.Identity) else conv2d(x, self.proj.weight, self.proj.bias)
+        r = xs if isinstance(self.proj, nn.Identity) else conv2d(xs, self.proj.weight, self.proj.bias)
         p = c[5].p if self.training else 0.0
         return conv2d(h, c[4].weight, c[4].bias, residual=r, drop_p=p, site=self._site)
 
