@@ -148,7 +148,8 @@ int tvq_conv_out_width(int64_t Win, int64_t KW, int64_t SW, int64_t transposed);
  * few gathered channels (whose padded image and weight panel fit in 64 KB of LDS),
  * 2 = halo-tile weight gradient, 4 = halo-tile wherever it fits, 8 = no 32x32-MFMA
  * wide-channel tile, 16 / 32 = its K stage BK = 32 / 16 (default 64), 64 = its 4-wave
- * block (default 12 waves); 0 forces the staged GEMMs; < 0 only queries.  Default 3.
+ * block (default 12 waves), 128 = its 64-channel variant for narrow maps (default off);
+ * 0 forces the staged GEMMs; < 0 only queries.  Default 3.
  * Returns the previous setting. */
 int tvq_conv_config(int64_t halo);
 
@@ -163,6 +164,16 @@ int tvq_conv_config(int64_t halo);
 int tvq_conv_packcache_begin(int64_t id, float* arena, int64_t cap_floats, tvq_stream_t stream);
 int tvq_conv_packcache_end(void);
 int64_t tvq_conv_packcache_entries(void);
+
+/* Deferred weight-gradient reductions: between begin() and flush(stream), the split sums
+ * of tvq_conv2d_wgrad / tvq_convT2d_wgrad (<= 256 splits) are recorded instead of launched,
+ * and flush() runs them all in a few batched launches on `stream` -- bit for bit the same
+ * sums.  Until the flush the callers' workspaces must stay allocated and dw / db are not
+ * final.  Process-wide host state, one scope at a time. */
+int tvq_conv_wgrad_defer_begin(void);
+int tvq_conv_wgrad_defer_flush(tvq_stream_t stream);
+/* paused != 0: calls inside the scope reduce immediately (a gradient needed at once) */
+int tvq_conv_wgrad_defer_pause(int64_t paused);
 /* op: 0 conv2d fwd, 1 convT2d fwd, 2 conv2d dgrad, 3 convT2d dgrad, 4 conv2d wgrad,
  * 5 convT2d wgrad; (Ci, Co, Wi) = the layer's input channels, output channels, input
  * width.  Returns the workspace size in floats (>= 1), -1 for a bad op. */

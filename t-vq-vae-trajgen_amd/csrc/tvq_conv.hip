@@ -454,32 +454,39 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_
                                            0x00020000);
 }
 
-// NW = waves per block: 4 (each wave 32 channels x 96 positions, three accumulators) or
-// 12 (each wave one 32x32 tile, 3 waves per SIMD so one wave's barrier / address work
-// hides behind the others' MFMAs).  Same k order either way.
-template <int MODE, int KH, int KW, int SW, bool REPL, int BK, int NW>
+// TN = channel tile (128, or 64 for the 64-channel LF convs, whose grids are too small
+// for 128 x 96 tiles and otherwise need split-K); NWN = TN / 32 channel tiles.
+// NW = waves per block: NWN (TN = 128 only: each wave 32 channels x 96 positions, three
+// accumulators) or 3 NWN (each wave one 32x32 tile, up to 3 waves per SIMD so one wave's
+// barrier / address work hides behind the others' MFMAs; the first NWN waves stage the
+// weights, the other 2 NWN the input).  Same k order in every variant.
+template <int MODE, int KH, int KW, int SW, bool REPL, int BK, int NW, int TN>
 __global__ __launch_bounds__(NW * 64) void conv_t32_kernel(const float* __restrict__ in,
                                                       const float* __restrict__ wt,
                                                       float* __restrict__ out, ConvGeom g,
                                                       Epi e) {
-  constexpr int TN = 128, TM = 96;
-  // operand staging: NW = 4 -> every thread loads A and B; NW = 12 -> waves 0-3 load A
-  // (weights), waves 4-11 load B (input), so the staging work is spread over all SIMDs
-  constexpr int LB = NW == 12 ? 512 : 256;  // threads loading B
+  constexpr int TM = 96, NWN = TN / 32;
+  constexpr bool SPLIT = NW == 3 * NWN;     // one tile per wave, staging split A | B
+  static_assert(SPLIT || (NW == 4 && TN == 128), "t32 variant");
+  constexpr int ATH = SPLIT ? 64 * NWN : 64 * NW;       // threads loading A
+  constexpr int LB = SPLIT ? 128 * NWN : 64 * NW;       // threads loading B
+  constexpr int ROWF4 = TN / 4;             // dwordx4 per A row (one k)
+  constexpr int APASS = ATH / ROWF4;        // A rows per pass (8)
   constexpr int PSTEP = LB % 96;            // position step between a thread's B rows
   constexpr int KSTEP = 3 * LB / 96;        // k step per 3 B elements
-  constexpr int A4 = TN * BK / 4 / 256;     // dwordx4 A loads per A-loading thread
+  constexpr int A4 = BK / APASS;            // dwordx4 A loads per A-loading thread
   constexpr int BL = TM * BK / LB;          // dword B loads per B-loading thread
+  static_assert(BK % APASS == 0, "A rows");
   constexpr int BAD = 0x40000000;        // offset past any buffer end -> loads 0
   extern __shared__ float smem[];
   float* As = smem;                      // [2][BK][TN]
   float* Bs = smem + 2 * BK * TN;        // [2][BK][TM]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  constexpr int NJ = 12 / NW;  // 32-position tiles per wave
-  const bool aload = NW == 4 || tid < 256;
-  const bool bload = NW == 4 || tid >= 256;
-  const int bt = NW == 4 ? tid : tid - 256;  // index among the B-loading threads
-  const int wch = wid & 3, wpos = (wid >> 2) * NJ;
+  constexpr int NJ = SPLIT ? 1 : 3;  // 32-position tiles per wave
+  const bool aload = !SPLIT || tid < ATH;
+  const bool bload = !SPLIT || tid >= ATH;
+  const int bt = SPLIT ? tid - ATH : tid;  // index among the B-loading threads
+  const int wch = wid % NWN, wpos = (wid / NWN) * NJ;
   const int n0 = blockIdx.y * TN, m0 = blockIdx.x * TM;
   const int csteps = g.C / BK;
   const int nsteps = KH * KW * csteps;
@@ -503,7 +510,7 @@ __global__ __launch_bounds__(NW * 64) void conv_t32_kernel(const float* __restri
     pm_b[u] = (int)fdiv((uint32_t)mc, g.fd_hwo);
     pm_h[u] = (int)bh - pm_b[u] * g.Hout;
   }
-  const int a_k = tid >> 5, a_n = n0 + ((tid & 31) << 2);
+  const int a_k = tid / ROWF4, a_n = n0 + (tid % ROWF4) * 4;
   float4 ra[A4];
   float rb[BL];
   auto load = [&](int step) {
@@ -515,7 +522,7 @@ __global__ __launch_bounds__(NW * 64) void conv_t32_kernel(const float* __restri
 #pragma unroll
       for (int i = 0; i < A4; ++i)
         ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                               rwt, abase, i * 8 * g.N * 4, 0));
+                                               rwt, abase, i * APASS * g.N * 4, 0));
     }
     if (!bload) return;
     int boff[3];
@@ -548,9 +555,9 @@ __global__ __launch_bounds__(NW * 64) void conv_t32_kernel(const float* __restri
   };
   auto store = [&](int buf) {
     if (aload) {
-      float* a = As + buf * BK * TN + a_k * TN + ((tid & 31) << 2);
+      float* a = As + buf * BK * TN + a_k * TN + (tid % ROWF4) * 4;
 #pragma unroll
-      for (int i = 0; i < A4; ++i) *reinterpret_cast<float4*>(a + i * 8 * TN) = ra[i];
+      for (int i = 0; i < A4; ++i) *reinterpret_cast<float4*>(a + i * APASS * TN) = ra[i];
     }
     if (bload) {
       float* bb = Bs + buf * BK * TM;
@@ -640,7 +647,12 @@ __global__ __launch_bounds__(NW * 64) void conv_t32_kernel(const float* __restri
 // concurrent streams' kernels, the two are within 0.5 % (7.29 vs 7.25 ms).
 static int g_t32_bk = 64;  // K-stage depth: 64, or 32 / 16 with tvq_conv_config bit 16 / 32
 static int g_t32_nw = 12;  // waves per block (12, or 4 with tvq_conv_config bit 64)
-static size_t t32_lds(int bk) { return (size_t)2 * bk * (128 + 96) * 4; }
+// 64-channel tile for narrow maps (tvq_conv_config bit 128 turns it on).  Off by default:
+// at the LF band's 64->64 3x3 conv (6144 positions, 64 blocks) it takes 27.5 us against
+// 23.4 us for the split-K tap kernel + epilogue -- 9 K-stages of 32 MFMAs per wave leave
+// each stage's load latency exposed; the grid needs split-K or a deeper prefetch.
+static int g_t32_n64 = 0;
+static size_t t32_lds(int bk, int tn) { return (size_t)2 * bk * (tn + 96) * 4; }
 
 // Weight gradient: rows = n (channels of G), cols = k' = (c, kh, kw), reduction over
 // positions.  blockIdx.z = split index over positions; partial results go to
@@ -1375,6 +1387,9 @@ static std::vector<PackEntry> g_pc;
 static int64_t g_pc_id = -1, g_pc_cap = 0, g_pc_used = 0;
 static float* g_pc_arena = nullptr;
 static bool g_pc_active = false;
+// deferred weight-gradient split sums (see wgrad_finish)
+static std::vector<RrJob> g_rd;
+static bool g_rd_on = false, g_rd_paused = false;
 
 constexpr int PACK_BATCH = 24;
 struct PackBatch {
@@ -1488,33 +1503,44 @@ template <int MODE, int KH, int KW, int SW, bool REPL>
 static void launch_gemm(const float* in, const float* wt, float* out, const ConvGeom& g,
                         const Epi& e, float* slab, hipStream_t st) {
   if (g.C % 16 == 0) {
-    // wide channels on a full grid: 32x32 MFMA tile, no split-K (needs packed weights)
-    const int64_t t32_blocks = (int64_t)((g.Mpos + 95) / 96) * ((g.N + 127) / 128);
-    if (g_conv_t32 && g.C % g_t32_bk == 0 && g.N % 128 == 0 && g.wsn == 1 && g.wsc == g.N &&
-        t32_blocks >= 192 && (int64_t)g.B * g.C * g.Hin * g.Win < (1ll << 29) &&
-        (int64_t)KH * KW * g.C * g.N < (1ll << 29)) {
-      dim3 grid((g.Mpos + 95) / 96, g.N / 128);
+    // wide channels: 32x32 MFMA tile, no split-K (needs packed weights).  128-channel
+    // tiles on a full grid; 64-channel tiles (6 waves) for N % 64 maps too small for it
+    // (the LF band's 64-channel convs), which otherwise run split-K + an epilogue launch.
+    const bool t32_ok = g_conv_t32 && g.wsn == 1 && g.wsc == g.N &&
+                        (int64_t)g.B * g.C * g.Hin * g.Win < (1ll << 29) &&
+                        (int64_t)KH * KW * g.C * g.N < (1ll << 29);
+    const int64_t mt = (g.Mpos + 95) / 96;
+    const bool wide128 = t32_ok && g.C % g_t32_bk == 0 && g.N % 128 == 0 && mt * (g.N / 128) >= 192;
+    const bool wide64 = !wide128 && t32_ok && g_t32_n64 && g.C % 64 == 0 && g.N % 64 == 0 &&
+                        mt >= 32;
+    if (wide128 || wide64) {
       static bool lds_set = false;  // > 64 KB of dynamic LDS must be opted into once
       if (!lds_set) {
         (void)hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&conv_t32_kernel<MODE, KH, KW, SW, REPL, 64, 4>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)t32_lds(64));
+            reinterpret_cast<const void*>(&conv_t32_kernel<MODE, KH, KW, SW, REPL, 64, 4, 128>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)t32_lds(64, 128));
         (void)hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&conv_t32_kernel<MODE, KH, KW, SW, REPL, 64, 12>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)t32_lds(64));
+            reinterpret_cast<const void*>(&conv_t32_kernel<MODE, KH, KW, SW, REPL, 64, 12, 128>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)t32_lds(64, 128));
+        (void)hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&conv_t32_kernel<MODE, KH, KW, SW, REPL, 64, 6, 64>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)t32_lds(64, 64));
         lds_set = true;
       }
-#define TVQ_T32(BKV, NWV)                                                                   \
-  hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, BKV, NWV>), grid, dim3(64 * NWV), \
-                     t32_lds(BKV), st, in, wt, out, g, e)
-      if (g_t32_nw == 12) {
-        if (g_t32_bk == 64) TVQ_T32(64, 12);
-        else if (g_t32_bk == 16) TVQ_T32(16, 12);
-        else TVQ_T32(32, 12);
+#define TVQ_T32(BKV, NWV, TNV)                                                             \
+  hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, BKV, NWV, TNV>),             \
+                     dim3((unsigned)mt, g.N / TNV), dim3(64 * NWV), t32_lds(BKV, TNV), st, in, \
+                     wt, out, g, e)
+      if (wide64) {
+        TVQ_T32(64, 6, 64);
+      } else if (g_t32_nw == 12) {
+        if (g_t32_bk == 64) TVQ_T32(64, 12, 128);
+        else if (g_t32_bk == 16) TVQ_T32(16, 12, 128);
+        else TVQ_T32(32, 12, 128);
       } else {
-        if (g_t32_bk == 64) TVQ_T32(64, 4);
-        else if (g_t32_bk == 16) TVQ_T32(16, 4);
-        else TVQ_T32(32, 4);
+        if (g_t32_bk == 64) TVQ_T32(64, 4, 128);
+        else if (g_t32_bk == 16) TVQ_T32(16, 4, 128);
+        else TVQ_T32(32, 4, 128);
       }
 #undef TVQ_T32
       return;
@@ -1708,14 +1734,36 @@ extern "C" int tvq_conv_packcache_end(void) {
 
 extern "C" int64_t tvq_conv_packcache_entries(void) { return (int64_t)g_pc.size(); }
 
+extern "C" int tvq_conv_wgrad_defer_begin(void) {
+  TVQ_CHECK_ARG(!g_rd_on, "tvq_conv_wgrad_defer_begin: a scope is already open");
+  g_rd.clear();
+  g_rd_on = true;
+  return TVQ_OK;
+}
+
+extern "C" int tvq_conv_wgrad_defer_pause(int64_t paused) {
+  g_rd_paused = paused != 0;
+  return TVQ_OK;
+}
+
+extern "C" int tvq_conv_wgrad_defer_flush(tvq_stream_t stream) {
+  g_rd_on = false;
+  g_rd_paused = false;
+  if (!g_rd.empty()) reduce_rows_batch(g_rd.data(), (int)g_rd.size(), (hipStream_t)stream);
+  g_rd.clear();
+  return launch_status("tvq_conv_wgrad_defer_flush");
+}
+
 extern "C" int tvq_conv_config(int64_t halo) {
   const int prev = g_conv_halo | (g_conv_t32 ? 0 : 8) | (g_t32_bk == 32 ? 16 : 0) |
-                   (g_t32_bk == 16 ? 32 : 0) | (g_t32_nw == 4 ? 64 : 0);
+                   (g_t32_bk == 16 ? 32 : 0) | (g_t32_nw == 4 ? 64 : 0) |
+                   (g_t32_n64 ? 128 : 0);
   if (halo >= 0) {
     g_conv_halo = (int)(halo & 7);
     g_conv_t32 = (halo & 8) ? 0 : 1;
     g_t32_bk = (halo & 16) ? 32 : ((halo & 32) ? 16 : 64);
     g_t32_nw = (halo & 64) ? 4 : 12;
+    g_t32_n64 = (halo & 128) ? 1 : 0;
   }
   return prev;
 }
@@ -1909,11 +1957,20 @@ extern "C" int64_t tvq_conv_workspace(int64_t op, int64_t B, int64_t Ci, int64_t
   return r > 0 ? r : 1;
 }
 
+// Deferred weight-gradient split sums (tvq_conv_wgrad_defer_*): inside a scope the
+// slabs' reductions are recorded and run by a few batched launches at the flush instead
+// of one launch per conv (the caller keeps the workspaces alive until then).
+
 static void wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, float* dw,
                          float* db, int accumulate, hipStream_t st) {
   // deterministic split sum; kcols = Kred+1 splits out the bias column.  The level-1
   // scratch follows the slab in the workspace.
-  reduce_rows(slab, splits, N * kcols, N * kcols, dw, db, kcols > 0 && db ? kcols : 0, accumulate,
+  const int64_t L = kcols > 0 && db ? kcols : 0;
+  if (g_rd_on && !g_rd_paused && splits <= RR_ONE_ROWS) {  // the single-level case: batched at the flush
+    g_rd.push_back({slab, dw, db, splits, N * kcols, L, accumulate});
+    return;
+  }
+  reduce_rows(slab, splits, N * kcols, N * kcols, dw, db, L, accumulate,
               slab + (int64_t)splits * N * kcols, st);
 }
 

@@ -9,6 +9,17 @@ namespace tvq {
 int64_t reduce_rows_scratch(int64_t P, int64_t N);
 void reduce_rows(const float* in, int64_t P, int64_t N, int64_t ld, float* out, float* out2,
                  int64_t L, int accumulate, float* scratch, hipStream_t st);
+// Batched single-level reduce_rows (P <= RR_ONE = 256 rows, ld = N): each job gives the
+// result of the matching reduce_rows call bit for bit, for many slabs in one launch.
+struct RrJob {
+  const float* in;
+  float* out;
+  float* out2;
+  int64_t P, N, L;
+  int accumulate;
+};
+constexpr int RR_ONE_ROWS = 256;
+void reduce_rows_batch(const RrJob* jobs, int n, hipStream_t st);
 // stable group-by of indices in [0,V): offsets[V+1], perm[M]; scratch: group_by_scratch_ints ints
 int64_t group_by_scratch_ints(int64_t M, int64_t V);
 void group_by_i32(const int32_t* idx, int64_t M, int64_t V, int* offsets, int* perm, int* scratch,

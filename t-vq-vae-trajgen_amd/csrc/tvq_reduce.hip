@@ -103,6 +103,39 @@ void reduce_rows(const float* in, int64_t P, int64_t N, int64_t ld, float* out, 
                        out, out2, L, accumulate, 1, nullptr, nullptr);
 }
 
+// Batched single-level column sums: blockIdx.x runs over the jobs' column blocks (cb0 =
+// prefix of column-block counts); each block is exactly reduce_rows_kernel's direct path.
+constexpr int RR_BATCH = 24;
+struct RrBatch {
+  RrJob job[RR_BATCH];
+  int cb0[RR_BATCH + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void reduce_rows_batch_kernel(RrBatch b) {
+  __shared__ float sh[RR_GROUPS][RR_COLS];
+  int j = 0;
+  while (j + 1 < b.n && (int)blockIdx.x >= b.cb0[j + 1]) ++j;
+  const RrJob& jb = b.job[j];
+  const int c = threadIdx.x % RR_COLS, g = threadIdx.x / RR_COLS;
+  const int64_t col = (int64_t)(blockIdx.x - b.cb0[j]) * RR_COLS + c;
+  const float t = rr_colsum<false>(jb.in, 0, jb.P, jb.N, col, jb.N, sh, c, g);
+  if (g == 0 && col < jb.N) rr_store(t, col, jb.out, jb.out2, jb.L, jb.accumulate);
+}
+
+void reduce_rows_batch(const RrJob* jobs, int n, hipStream_t st) {
+  for (int i0 = 0; i0 < n; i0 += RR_BATCH) {
+    RrBatch b;
+    b.n = n - i0 < RR_BATCH ? n - i0 : RR_BATCH;
+    b.cb0[0] = 0;
+    for (int i = 0; i < b.n; ++i) {
+      b.job[i] = jobs[i0 + i];
+      b.cb0[i + 1] = b.cb0[i] + (int)((jobs[i0 + i].N + RR_COLS - 1) / RR_COLS);
+    }
+    hipLaunchKernelGGL(reduce_rows_batch_kernel, dim3((unsigned)b.cb0[b.n]), dim3(256), 0, st, b);
+  }
+}
+
 // ---------------------------------------------------------------- group-by
 constexpr int GB_CHUNK = 256;
 constexpr int SEG_CH = 32;  // rows per segmented-sum chunk (skewed groups split over waves)

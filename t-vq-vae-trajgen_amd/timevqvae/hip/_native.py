@@ -108,6 +108,9 @@ sig("tvq_maskgit_remask", P, I64, I64, I64, F32, P, P, U64, P, I64, P, P, P)
 sig("tvq_conv_packcache_begin", I64, P, I64, P)
 sig("tvq_conv_packcache_end")
 sig("tvq_conv_packcache_entries", restype=I64)
+sig("tvq_conv_wgrad_defer_begin")
+sig("tvq_conv_wgrad_defer_flush", P)
+sig("tvq_conv_wgrad_defer_pause", I64)
 # --- ROCKET features --------------------------------------------------------
 sig("tvq_rocket_apply", P, I64, I64, I64, P, P, P, P, P, P, I64, P, P)
 sig("tvq_codebook_gather_nchw", P, I64, I64, I64, P, P, P)

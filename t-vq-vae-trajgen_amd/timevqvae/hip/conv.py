@@ -6,6 +6,7 @@ conv_transpose2d nn.ConvTranspose2d 3x4 s(1,2) (VQVAEDecBlock, decoder tail)
 Backward: dgrad (T/F gathers), wgrad (split positions, deterministic), bias = channel sum.
 """
 import contextlib
+import os
 
 import torch
 
@@ -29,6 +30,47 @@ def _bias_grad(g, dev, sink=None):
 
 
 USE_WORKSPACE = True  # tests flip this to cover the no-workspace (in-place weight) path
+
+
+_defer_keep = None  # workspaces of deferred weight-gradient reductions (wgrad_deferred)
+
+
+@contextlib.contextmanager
+def wgrad_deferred():
+    """Inside the scope the conv weight-gradient split sums are recorded and run by a few
+    batched launches on the current stream at the exit (tvq_conv_wgrad_defer_*), bit for
+    bit the same sums, instead of one reduction launch per conv.  Wrap a backward pass;
+    gradients are final only after the exit."""
+    global _defer_keep
+    if _defer_keep is not None or os.environ.get("TVQ_WGRAD_DEFER", "1") == "0":
+        yield  # nested (the outer scope flushes) or switched off
+        return
+    call("tvq_conv_wgrad_defer_begin")
+    _defer_keep = []
+    try:
+        yield
+    finally:
+        call("tvq_conv_wgrad_defer_flush", stream_ptr())
+        _defer_keep = None  # freed after the flush is enqueued: stream-ordered reuse
+
+
+def _keep(ws):
+    if _defer_keep is not None and ws is not None:
+        _defer_keep.append(ws)
+
+
+@contextlib.contextmanager
+def _immediate(needed_now):
+    """A weight gradient returned to autograd (not written into a flat sink) is read right
+    away: its reduction must not wait for the deferral scope's flush."""
+    if needed_now and _defer_keep is not None:
+        call("tvq_conv_wgrad_defer_pause", 1)
+        try:
+            yield
+        finally:
+            call("tvq_conv_wgrad_defer_pause", 0)
+    else:
+        yield
 
 
 class PackCache:
@@ -133,8 +175,10 @@ class _Conv2d(torch.autograd.Function):
                 dbt = (sb if direct else torch.empty(Co, device=dev)) if need_b else None
                 ws = _conv_ws(OP_WGRAD, dev, B, Ci, H, Wi, Co, KH, KW, SW, replicate,
                               required=True)
-                call("tvq_conv2d_wgrad", ptr(x4), B, Ci, H, Wi, ptr(gd), Co, Wo, KH, KW, SW,
-                     int(replicate), ptr(dwt), ptr(dbt), int(direct), ptr(ws), stream_ptr())
+                with _immediate(not direct):
+                    call("tvq_conv2d_wgrad", ptr(x4), B, Ci, H, Wi, ptr(gd), Co, Wo, KH, KW, SW,
+                         int(replicate), ptr(dwt), ptr(dbt), int(direct), ptr(ws), stream_ptr())
+                _keep(ws)
             if not direct:
                 dw = (dwt.squeeze(2) if wdim == 3 else dwt) if need_w else None
                 db = dbt
@@ -190,8 +234,10 @@ class _ConvT2d(torch.autograd.Function):
             with (streams.offload(x, g) if sw is not None else contextlib.nullcontext()):
                 dwt = sw if sw is not None else torch.empty_like(w)
                 ws = _conv_ws(OP_T_WGRAD, x.device, B, Ci, H, Wi, Co, KH, KW, SW, required=True)
-                call("tvq_convT2d_wgrad", ptr(x), B, Ci, H, Wi, ptr(g), Co, Wo, KH, KW, SW,
-                     ptr(dwt), int(sw is not None), ptr(ws), stream_ptr())
+                with _immediate(sw is None):
+                    call("tvq_convT2d_wgrad", ptr(x), B, Ci, H, Wi, ptr(g), Co, Wo, KH, KW, SW,
+                         ptr(dwt), int(sw is not None), ptr(ws), stream_ptr())
+                _keep(ws)
             dw = None if sw is not None else dwt
         if ctx.has_b and ctx.needs_input_grad[2]:
             sb = grad_sink(b_p)

@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 
 from ..hip import streams
+from ..hip.conv import wgrad_deferred
 from ..hip.loss import l1_loss, mse_loss
 from ..hip.optim import FusedAdamW
 from ..utils.checkpoint import adapt_state_dict, read_state_dict, save_checkpoint
@@ -101,7 +102,8 @@ class Stage1(nn.Module):
             with streams.branch(x.device, "s1" + band.lower()) as br:
                 br.inputs(s)
                 part = self._band(band, s)
-                (part[1] + part[2]["loss"]).sum().backward()
+                with wgrad_deferred():  # weight-gradient split sums batched at the band's end
+                    (part[1] + part[2]["loss"]).sum().backward()
                 parts[band] = part
                 br.outputs(part)
         if self._sched is not None:

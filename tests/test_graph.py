@@ -129,3 +129,23 @@ def test_pack_cache_matches_per_call_packing(cuda):
     assert lg == ref2[2:]
     for a, b in zip(_state(ref), _state(g)):
         assert torch.equal(a, b)
+
+
+def test_deferred_wgrad_reductions_match_immediate(cuda, monkeypatch):
+    """Batching the conv weight-gradient split sums at the end of each band's backward
+    (hip.conv.wgrad_deferred) gives the same gradients, parameters and optimizer state
+    bit for bit as reducing after every conv, eager and graphed."""
+    import bench
+    batch = _batch(cuda, B=32, C=6, L=256)
+    monkeypatch.setenv("TVQ_WGRAD_DEFER", "0")
+    ref = bench.JointTrainer(cuda, 1, cfg=_cfg(), length=256, channels=6)
+    lr = [tuple(float(o["loss"].detach().sum()) for o in ref.step(batch)) for _ in range(7)]
+    monkeypatch.setenv("TVQ_WGRAD_DEFER", "1")
+    d = bench.JointTrainer(cuda, 1, cfg=_cfg(), length=256, channels=6)
+    ld = [tuple(float(o["loss"].detach().sum()) for o in d.step(batch)) for _ in range(3)]
+    d.capture(batch)  # 2 eager warmup steps (deferral on), then capture
+    ld += [tuple(float(o["loss"].detach().sum()) for o in d.step(batch)) for _ in range(2)]
+    torch.cuda.synchronize()
+    assert lr[:3] == ld[:3] and lr[5:] == ld[3:]
+    for a, b in zip(_state(ref), _state(d)):
+        assert torch.equal(a, b)

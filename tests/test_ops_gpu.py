@@ -321,7 +321,8 @@ def test_conv_paths_same_dropout_mask(Ci, Co, W, cuda):
     torch.testing.assert_close(outs[0], outs[2], rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("op", ["fwd", "dgrad", "conv1d_fwd", "conv1d_dgrad"])
+@pytest.mark.parametrize("op", ["fwd", "dgrad", "conv1d_fwd", "conv1d_dgrad", "fwd64", "dgrad64",
+                                "fwd128n", "dgrad128n"])
 def test_conv_wide_tile_matches_tap(op, cuda):
     """The 32x32-MFMA wide-channel tile (C, N >= 128 on a full grid) computes each output as
     the same k-ordered fma chain as the tap-major kernel's unsplit path: bitwise equal to it,
@@ -330,6 +331,10 @@ def test_conv_wide_tile_matches_tap(op, cuda):
     gen = torch.Generator().manual_seed(11)
     if op.startswith("conv1d"):
         B, Ci, Co, H, W, KH, KW = 256, 128, 256, 1, 96, 1, 3
+    elif op.endswith("64"):  # LF band 64-channel ResBlock conv: the 64-channel tile
+        B, Ci, Co, H, W, KH, KW = 256, 64, 64, 3, 8, 3, 3
+    elif op.endswith("128n"):  # 128 channels on a narrow map: 64-channel tile, 2 column tiles
+        B, Ci, Co, H, W, KH, KW = 256, 128, 128, 3, 8, 3, 3
     else:
         B, Ci, Co, H, W, KH, KW = 192, 128, 128, 3, 32, 3, 3
     x = torch.randn(B, Ci, H, W, generator=gen)
@@ -342,10 +347,14 @@ def test_conv_wide_tile_matches_tap(op, cuda):
     try:
         # wide tile (packed) at K-stage depth BK = 64, 32, 16, with 12 and 4 waves per block
         # | tap, unsplit, raw
-        for cfg, use_ws in ((0, True), (16, True), (32, True), (64, True), (80, True),
-                            (8, False)):
+        # (128: the 64-channel variant, which is what the narrow "64"/"128n" maps exercise;
+        # without it those maps run the split-K tap kernel, a different summation order)
+        cfgs = ((0, True), (16, True), (32, True), (64, True), (80, True), (8, False))
+        if op.endswith(("64", "128n")):
+            cfgs = ((128, True), (8, False))
+        for cfg, use_ws in cfgs:
             value("tvq_conv_config", cfg)
-            if op.endswith("fwd"):
+            if "fwd" in op:
                 y = torch.empty(B, Co, H, W, device=cuda)
                 ws = torch.empty(value("tvq_conv_workspace", 0, B, Ci, H, W, Co, KH, KW, 1, 0),
                                  device=cuda) if use_ws else None
@@ -364,7 +373,7 @@ def test_conv_wide_tile_matches_tap(op, cuda):
     for o in outs[:-1]:
         assert torch.equal(o, outs[-1])
     pad = (KH // 2, (KW - 1) // 2)
-    if op.endswith("fwd"):
+    if "fwd" in op:
         ref = F.conv2d(x, w, bias, padding=pad)
     else:
         ref = torch.nn.grad.conv2d_input(x.shape, w, dy, padding=pad)
