@@ -374,6 +374,39 @@ int tvq_rocket_apply(const double* X, int64_t n, int64_t L, int64_t ldx, const d
                      const int32_t* dilations, const int32_t* paddings, int64_t nk, double* out,
                      tvq_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * FidelityEnhancer / Unet1D eval forward (models/fidelity_enhancer.py:284-498, the
+ * sampler's post-decode refinement, generation/sampler.py:156-169).  (B, C, L) fp32.
+ * tvq_fe_ws_weight: WeightStandardizedConv2d weight (:102-106), per output row of n = Ci*K.
+ * tvq_fe_conv1d: nn.Conv1d(Ci, Co, K, stride S, padding P) (zero, or replicate when
+ *   replicate != 0, :386-392); up2 != 0 reads x nearest-upsampled by 2 (Upsample, :85-89);
+ *   bias and residual (added after the bias) nullable; Lout = tvq_fe_conv1d_out_len(...).
+ * tvq_fe_group_norm_snake: GroupNorm(G, C, eps) -> Snake(a) (+ residual), Block.forward
+ *   (:193-204) and ResnetBlock's skip add (:231).
+ * tvq_fe_channel_layernorm: LayerNorm over C, gamma only (:119-127) (+ residual).
+ * tvq_fe_linear_attention / tvq_fe_attention: LinearAttention (:234-260) / Attention
+ *   (:263-283) core on to_qkv's output (B, 3 H dh, n) -> (B, H dh, n); dh must be 32.
+ * tvq_fe_cat_interp: cat(interp(a -> L), interp(b -> L)) on channels, linear,
+ *   align_corners=False (Unet1D skips :434-452; Cb = 0 interpolates a alone, :495-497). */
+int64_t tvq_fe_conv1d_out_len(int64_t Lin, int64_t K, int64_t S, int64_t P, int64_t up2);
+int tvq_fe_ws_weight(const float* w, int64_t Co, int64_t n, float eps, float* out,
+                     tvq_stream_t stream);
+int tvq_fe_conv1d(const float* x, int64_t B, int64_t Ci, int64_t Lin, const float* w,
+                  const float* bias, int64_t Co, int64_t K, int64_t S, int64_t P, int64_t up2,
+                  int64_t replicate, const float* residual, float* y, int64_t Lout,
+                  tvq_stream_t stream);
+int tvq_fe_group_norm_snake(const float* x, int64_t B, int64_t C, int64_t L, int64_t G,
+                            const float* gamma, const float* beta, const float* a, float eps,
+                            const float* residual, float* y, tvq_stream_t stream);
+int tvq_fe_channel_layernorm(const float* x, int64_t B, int64_t C, int64_t L, const float* g,
+                             float eps, const float* residual, float* y, tvq_stream_t stream);
+int tvq_fe_linear_attention(const float* qkv, int64_t B, int64_t H, int64_t dh, int64_t n,
+                            float* out, tvq_stream_t stream);
+int tvq_fe_attention(const float* qkv, int64_t B, int64_t H, int64_t dh, int64_t n, float* out,
+                     tvq_stream_t stream);
+int tvq_fe_cat_interp(const float* a, int64_t Ca, int64_t La, const float* b, int64_t Cb,
+                      int64_t Lb, int64_t B, int64_t L, float* out, tvq_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -506,3 +506,115 @@ def iterative_decoding_torch(tf_l, tf_h, num, n_l, n_h, mask_l, mask_h, T, temp_
     s_l = _pass_torch(tf_l, s_l, mask_l, T["lf"], temp_l, unk_l)
     s_h = _pass_torch(lambda sh: tf_h(s_l, sh), s_h, mask_h, T["hf"], temp_h, unk_h)
     return s_l, s_h
+
+
+# ----------------------------------------------------------------------------
+# FidelityEnhancer / Unet1D forward (models/fidelity_enhancer.py), eval mode
+# ----------------------------------------------------------------------------
+def fe_ws_conv(x, w, b, stride=1, padding=0):
+    """WeightStandardizedConv2d.forward (fidelity_enhancer.py:96-116): per output channel,
+    (w - mean) * rsqrt(var_biased + 1e-5), then conv1d."""
+    mean = w.mean(dim=(1, 2), keepdim=True)
+    var = w.var(dim=(1, 2), unbiased=False, keepdim=True)
+    return F.conv1d(x, (w - mean) * (var + 1e-5).rsqrt(), b, stride, padding)
+
+
+def fe_layernorm(x, g):
+    """LayerNorm over the channel axis, gamma only (fidelity_enhancer.py:119-127)."""
+    var = torch.var(x, dim=1, unbiased=False, keepdim=True)
+    mean = torch.mean(x, dim=1, keepdim=True)
+    return (x - mean) * (var + 1e-5).rsqrt() * g
+
+
+def fe_block(sd, p, x, groups):
+    """Block.forward (fidelity_enhancer.py:182-204): WS conv3 -> GroupNorm -> Snake ->
+    Dropout (identity in eval); scale_shift is never passed (Unet1D.forward :402-405)."""
+    x = fe_ws_conv(x, sd[p + "proj.weight"], sd[p + "proj.bias"], padding=1)
+    x = F.group_norm(x, groups, sd[p + "norm.weight"], sd[p + "norm.bias"], 1e-5)
+    a = sd[p + "act.a"]
+    return x + (1 / a) * torch.sin(a * x) ** 2
+
+
+def fe_resnet(sd, p, x, groups):
+    """ResnetBlock.forward (fidelity_enhancer.py:219-231) without a time embedding."""
+    h = fe_block(sd, p + "block1.", x, groups)
+    h = fe_block(sd, p + "block2.", h, groups)
+    res = F.conv1d(x, sd[p + "res_conv.weight"], sd[p + "res_conv.bias"]) \
+        if p + "res_conv.weight" in sd else x
+    return h + res
+
+
+def fe_linear_attention(sd, p, x, heads=4, dim_head=32):
+    """Residual(PreNorm(LinearAttention)) (fidelity_enhancer.py:75-82,130-137,234-260)."""
+    b, c, n = x.shape
+    xn = fe_layernorm(x, sd[p + "norm.g"])
+    q, k, v = F.conv1d(xn, sd[p + "fn.to_qkv.weight"]).chunk(3, dim=1)
+    q, k, v = (t.reshape(b, heads, dim_head, n) for t in (q, k, v))
+    q = q.softmax(dim=-2) * dim_head ** -0.5
+    k = k.softmax(dim=-1)
+    context = torch.einsum("bhdn,bhen->bhde", k, v)
+    out = torch.einsum("bhde,bhdn->bhen", context, q).reshape(b, heads * dim_head, n)
+    out = F.conv1d(out, sd[p + "fn.to_out.0.weight"], sd[p + "fn.to_out.0.bias"])
+    return fe_layernorm(out, sd[p + "fn.to_out.1.g"]) + x
+
+
+def fe_attention(sd, p, x, heads=4, dim_head=32):
+    """Residual(PreNorm(Attention)) (fidelity_enhancer.py:263-283)."""
+    b, c, n = x.shape
+    xn = fe_layernorm(x, sd[p + "norm.g"])
+    q, k, v = F.conv1d(xn, sd[p + "fn.to_qkv.weight"]).chunk(3, dim=1)
+    q, k, v = (t.reshape(b, heads, dim_head, n) for t in (q, k, v))
+    attn = torch.einsum("bhdi,bhdj->bhij", q * dim_head ** -0.5, k).softmax(dim=-1)
+    out = torch.einsum("bhij,bhdj->bhid", attn, v)
+    out = out.permute(0, 1, 3, 2).reshape(b, heads * dim_head, n)
+    return F.conv1d(out, sd[p + "fn.to_out.weight"], sd[p + "fn.to_out.bias"]) + x
+
+
+def _fe_upsample(sd, p, x):
+    """Upsample (fidelity_enhancer.py:85-89): nearest x2 then conv3 p1."""
+    x = F.interpolate(x, scale_factor=2, mode="nearest")
+    return F.conv1d(x, sd[p + "1.weight"], sd[p + "1.bias"], padding=1)
+
+
+def fe_forward(sd, x_a, input_length, dim_mults=(1, 2, 4, 8), groups=4):
+    """FidelityEnhancer.forward (fidelity_enhancer.py:484-498) -> Unet1D.forward
+    (:395-455).  `sd` holds the FidelityEnhancer state_dict (keys `unet.*`)."""
+    sd = {k[5:]: v for k, v in sd.items() if k.startswith("unet.")}
+    x = F.interpolate(x_a, size=input_length, mode="linear", align_corners=False)
+    x = F.conv1d(x, sd["init_conv.weight"], sd["init_conv.bias"], padding=3)
+    r = x.clone()
+    h = []
+    n = len(dim_mults)
+    for i in range(n):
+        p = f"downs.{i}."
+        x = fe_resnet(sd, p + "0.", x, groups)
+        h.append(x)
+        x = fe_resnet(sd, p + "1.", x, groups)
+        x = fe_linear_attention(sd, p + "2.fn.", x)
+        h.append(x)
+        if i < n - 1:  # Downsample: conv k4 s2 p1 (:92-93)
+            x = F.conv1d(x, sd[p + "3.weight"], sd[p + "3.bias"], stride=2, padding=1)
+        else:
+            x = F.conv1d(x, sd[p + "3.weight"], sd[p + "3.bias"], padding=1)
+    x = fe_resnet(sd, "mid_block1.", x, groups)
+    x = fe_attention(sd, "mid_attn.fn.", x)
+    x = fe_resnet(sd, "mid_block2.", x, groups)
+    for i in range(n):
+        p = f"ups.{i}."
+        hh = F.interpolate(h.pop(), size=x.shape[-1], mode="linear", align_corners=False)
+        x = fe_resnet(sd, p + "0.", torch.cat((x, hh), dim=1), groups)
+        hh = F.interpolate(h.pop(), size=x.shape[-1], mode="linear", align_corners=False)
+        x = fe_resnet(sd, p + "1.", torch.cat((x, hh), dim=1), groups)
+        x = fe_linear_attention(sd, p + "2.fn.", x)
+        if i < n - 1:
+            x = _fe_upsample(sd, p + "3.", x)
+        else:
+            x = F.conv1d(x, sd[p + "3.weight"], sd[p + "3.bias"], padding=1)
+    x = _fe_upsample(sd, "last_up.", x)
+    x = F.interpolate(x, size=r.shape[-1], mode="linear", align_corners=False)
+    x = fe_resnet(sd, "final_res_block.", torch.cat((x, r), dim=1), groups)
+    x = F.conv1d(x, sd["final_conv.0.weight"], sd["final_conv.0.bias"])
+    for j in (1, 2):  # conv3, replicate padding (:386-392)
+        x = F.conv1d(F.pad(x, (1, 1), mode="replicate"), sd[f"final_conv.{j}.weight"],
+                     sd[f"final_conv.{j}.bias"])
+    return x

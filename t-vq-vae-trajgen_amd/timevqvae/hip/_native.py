@@ -113,6 +113,15 @@ sig("tvq_conv_wgrad_defer_flush", P)
 sig("tvq_conv_wgrad_defer_pause", I64)
 # --- ROCKET features --------------------------------------------------------
 sig("tvq_rocket_apply", P, I64, I64, I64, P, P, P, P, P, P, I64, P, P)
+# --- FidelityEnhancer (Unet1D eval forward) -----------------------------------
+sig("tvq_fe_conv1d_out_len", I64, I64, I64, I64, I64, restype=I64)
+sig("tvq_fe_ws_weight", P, I64, I64, F32, P, P)
+sig("tvq_fe_conv1d", P, I64, I64, I64, P, P, I64, I64, I64, I64, I64, I64, P, P, I64, P)
+sig("tvq_fe_group_norm_snake", P, I64, I64, I64, I64, P, P, P, F32, P, P, P)
+sig("tvq_fe_channel_layernorm", P, I64, I64, I64, P, F32, P, P, P)
+sig("tvq_fe_linear_attention", P, I64, I64, I64, I64, P, P)
+sig("tvq_fe_attention", P, I64, I64, I64, I64, P, P)
+sig("tvq_fe_cat_interp", P, I64, I64, P, I64, I64, I64, I64, P, P)
 sig("tvq_codebook_gather_nchw", P, I64, I64, I64, P, P, P)
 
 

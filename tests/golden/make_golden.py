@@ -13,6 +13,7 @@ files are loaded by file path with minimal import stubs:
 
 G6 (stochastic VQ) alone: python tests/golden/make_golden.py svq
 G7 (ROCKET features, evaluation/rocket_functions.py with a numba stub) alone: ... rocket
+G8 (FidelityEnhancer / Unet1D forward, models/fidelity_enhancer.py) alone: ... fe
 
 Only the .npz outputs are committed (tests/golden/*.npz).  Usage:
 
@@ -362,6 +363,35 @@ def gen_rocket():
     np.savez_compressed(os.path.join(OUT, "g7_rocket.npz"), **d)
 
 
+# --------------------------------------------------------------------------- G8
+FE_CONFIG = {"dim": 8, "dim_mults": [1, 2, 4, 8], "resnet_block_groups": 4, "dropout": 0.5}
+
+
+def gen_fe(ref):
+    """FidelityEnhancer eval forward (fidelity_enhancer.py:458-498, Unet1D :284-455) with
+    configs/config.yaml:69-77 hyper-parameters.  Parameters come from param_init's per-key
+    rule (seed 11), so only inputs and outputs are stored.  Case a: input_length 256 (the
+    sampler's shape); case b: input_length 301 (the file's own __main__ length) with a
+    256-long x_a, so the FE's interpolation and every ragged skip interpolation run."""
+    fe_mod = _load("ref_fidelity_enhancer", f"{REF}/models/fidelity_enhancer.py")
+    d = {}
+    for tag, (B, C, Lx, Lin, seed) in {"a": (4, 6, 256, 256, 11), "b": (3, 6, 256, 301, 12)}.items():
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        fe = fe_mod.FidelityEnhancer(Lin, C, {"fidelity_enhancer": dict(FE_CONFIG)})
+        vals = fill_state_dict(fe.state_dict(), seed)
+        fe.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
+        fe.eval()
+        g = torch.Generator().manual_seed(seed)
+        x = torch.cumsum(0.1 * torch.randn(B, C, Lx, generator=g), -1)
+        with torch.no_grad():
+            y = fe(x)
+        d[f"{tag}_x"], d[f"{tag}_y"] = x.numpy(), y.numpy()
+        d[f"{tag}_meta"] = np.array([B, C, Lx, Lin, seed], dtype=np.int64)
+        d[f"{tag}_keys"] = np.array(sorted(fe.state_dict().keys()))
+    np.savez_compressed(os.path.join(OUT, "g8_fe.npz"), **d)
+
+
 def main():
     torch.set_num_threads(8)
     if sys.argv[1:] == ["rocket"]:  # regenerate only G7
@@ -371,6 +401,9 @@ def main():
     if sys.argv[1:] == ["svq"]:  # regenerate only G6
         gen_svq(ref)
         return
+    if sys.argv[1:] == ["fe"]:  # regenerate only G8
+        gen_fe(ref)
+        return
     gen_vq(ref)
     gen_stft(ref)
     gen_stage1(ref, "small", B=4, C=6, T=128, K=64, init_dim=4, hid_dim=32, seed=3)
@@ -378,6 +411,7 @@ def main():
     gen_maskgit(ref)
     gen_svq(ref)
     gen_rocket()
+    gen_fe(ref)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
