@@ -42,6 +42,9 @@ def config(sync):
                               "emb_dropout": 0.3},
             "cfg_scale": 1.0,
         },
+        "fidelity_enhancer": {"dim": 8, "dim_mults": [1, 2, 4, 8], "resnet_block_groups": 4,
+                              "dropout": 0.5, "tau_search_rng": [0.1, 0.5, 1, 2, 4],
+                              "tau_search_subset_size": 1.0, "percept_loss_weight": 0.0},
     }
 
 
@@ -227,17 +230,27 @@ def sampler_leg(tr, device, num=1024, reps=5):
         return mg.decode_token_ind_to_timeseries(s_l, "lf") + \
             mg.decode_token_ind_to_timeseries(s_h, "hf")
 
-    with torch.no_grad():
-        run()
+    from timevqvae.models import FidelityEnhancer
+    fe = FidelityEnhancer(T, C, config(False)).to(device).eval()
+
+    def timed(fn):
+        fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            run()
+            out = fn()
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / reps
+        return (time.perf_counter() - t0) / reps, out
+
+    with torch.no_grad():
+        dt, x_new = timed(run)
+        dt_fe, _ = timed(lambda: fe(x_new))
     mg.train(was)
+    # the reference's TrainedModelSampler.sample = decode + FidelityEnhancer (sampler.py:141-169)
     return {"num": num, "ms_per_batch": round(dt * 1e3, 3),
-            "trajectories_per_s": round(num / dt, 1), "reps": reps}
+            "trajectories_per_s": round(num / dt, 1), "reps": reps,
+            "fidelity_enhancer_ms": round(dt_fe * 1e3, 3),
+            "with_fe_trajectories_per_s": round(num / (dt + dt_fe), 1)}
 
 
 def cpu_baseline_leg():

@@ -407,6 +407,26 @@ int tvq_fe_attention(const float* qkv, int64_t B, int64_t H, int64_t dh, int64_t
 int tvq_fe_cat_interp(const float* a, int64_t Ca, int64_t La, const float* b, int64_t Cb,
                       int64_t Lb, int64_t B, int64_t L, float* out, tvq_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Trajectory data format (utils/data_utils.py:84-110 get_data; scripts/generate.py:14-20
+ * post_processed_generated_trajectories).  X (N, Fc = L*F) float64, columns [t0 f0, t0 f1,
+ * ...] as np.stack(flight.data[features].values.ravel()) builds them.
+ * tvq_minmax_fit: sklearn MinMaxScaler(feature_range=(lo, hi)).fit, per column (NaN
+ *   skipped): data_min/data_max/scale/min_ (Fc float64 each); workspace of
+ *   tvq_minmax_fit_workspace(Fc) doubles.
+ * tvq_minmax_transform: out (N, F, L) float32 = transpose((X * scale + min_) as (N, L, F)),
+ *   sklearn's float64 arithmetic, then the torch.FloatTensor cast: bit-equal.
+ * tvq_minmax_inverse: out (N, L*F) float32 from x (N, F, L) float32: numpy's in-place
+ *   `X -= min_; X /= scale_` on the float32 array (float64 op, float32 store), bit-equal. */
+int64_t tvq_minmax_fit_workspace(int64_t Fc);
+int tvq_minmax_fit(const double* X, int64_t N, int64_t Fc, double lo, double hi, double* data_min,
+                   double* data_max, double* scale, double* min_, double* workspace,
+                   tvq_stream_t stream);
+int tvq_minmax_transform(const double* X, int64_t N, int64_t L, int64_t F, const double* scale,
+                         const double* min_, float* out, tvq_stream_t stream);
+int tvq_minmax_inverse(const float* x, int64_t N, int64_t L, int64_t F, const double* scale,
+                       const double* min_, float* out, tvq_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -133,3 +133,50 @@ def test_hip_fe_norms_and_attention(cuda):
                       F.interpolate(b2, size=33, mode="linear", align_corners=False)), 1)
     got = ops.cat_interp(a2.to(cuda), b2.to(cuda), 33).cpu()
     assert torch.allclose(got, want, atol=1e-6, rtol=1e-6)
+
+
+def _sampler(tmp_path, device):
+    """TrainedModelSampler from a stage2 checkpoint (test_checkpoint's builder) and a
+    Lightning-shaped stage3.ckpt holding `fidelity_enhancer.*` (sampler.py:94-106)."""
+    from test_checkpoint import _build_stage2, _stage2_cfg
+    from timevqvae.generation import TrainedModelSampler
+    cfg = _stage2_cfg()
+    cfg["fidelity_enhancer"] = dict(CFG["fidelity_enhancer"])
+    s2, p1 = _build_stage2(tmp_path, cfg)
+    p2, p3 = tmp_path / "stage2.ckpt", tmp_path / "stage3.ckpt"
+    torch.save({"state_dict": s2.state_dict()}, p2)
+    fe = _model(6, 64, 4)
+    torch.save({"state_dict": {f"fidelity_enhancer.{k}": v for k, v in fe.state_dict().items()}},
+               p3)
+    smp = TrainedModelSampler(str(p1), str(p2), str(p3), None, input_length=64, in_channels=6,
+                              n_classes=5, batch_size=16, device=device, config=cfg,
+                              do_evaluate=False)
+    return smp, fe
+
+
+def test_sampler_loads_stage3_fidelity_enhancer(tmp_path):
+    smp, fe = _sampler(tmp_path, "cpu")
+    got = smp.fidelity_enhancer.state_dict()
+    for k, v in fe.state_dict().items():
+        assert torch.equal(got[k], v), k
+    assert not smp.fidelity_enhancer.training
+
+
+def test_sampler_evaluation_half_is_refused():
+    from timevqvae.generation import TrainedModelSampler
+    with pytest.raises(NotImplementedError):
+        TrainedModelSampler(None, None, None, None, 64, 6, 5, 16, do_evaluate=True)
+
+
+@pytest.mark.gpu
+def test_sampler_sample_applies_fidelity_enhancer(tmp_path, cuda):
+    smp, _ = _sampler(tmp_path, cuda)
+    torch.manual_seed(0)
+    (x_l, x_h, x), x_r = smp.sample(40, "conditional", class_index=2)
+    assert x.shape == (40, 6, 64) and x_r.shape == (40, 6, 64)
+    assert torch.allclose(x, x_l + x_h)
+    want = torch.cat([smp.fidelity_enhancer(x[i:i + 16].to(cuda)).cpu() for i in range(0, 40, 16)])
+    assert torch.equal(x_r, want)
+    sd = {k: v.detach().cpu() for k, v in smp.fidelity_enhancer.state_dict().items()}
+    ok, err = _close(x_r[:8].numpy(), O.fe_forward(sd, x[:8], 64).numpy())
+    assert ok, err
