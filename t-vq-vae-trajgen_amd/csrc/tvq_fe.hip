@@ -85,6 +85,81 @@ __global__ __launch_bounds__(256) void conv1d_kernel(const float* __restrict__ x
   }
 }
 
+// Register-blocked conv1d (the FidelityEnhancer's shapes: Ci <= 96, K <= 7, S <= 2).
+// Block tile TC = 4 TCY output channels x TP = 4 TPX positions; each thread owns 4
+// channels x 4 positions (positions tx + i TPX, so LDS reads of the input are consecutive
+// across lanes).  Input channels are streamed in chunks of 16: the chunk's input span and
+// its weights (as [c][k][co], read as float4) are staged in LDS, then every (c, k) does
+// 16 FMAs for 4 + 1 LDS reads.  Sum order per output: c ascending, then k (as
+// conv1d_kernel).
+template <int TPX, int TCY>
+__global__ __launch_bounds__(256) void conv1d_rb_kernel(const float* __restrict__ x, int Ci, int Lin,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ bias, int Co,
+                                                        int K, int S, int P, int up2, int replicate,
+                                                        const float* __restrict__ res,
+                                                        float* __restrict__ y, int Lout, int span) {
+  constexpr int RC = 4, RP = 4, CC = 16, TP = TPX * RP, TC = TCY * RC;
+  extern __shared__ float sm[];
+  float* xs = sm;                // CC x span
+  float* wsm = sm + CC * span;   // CC x K x TC
+  const int b = blockIdx.z, o0 = blockIdx.y * TC, l0 = blockIdx.x * TP;
+  const int tx = threadIdx.x % TPX, ty = threadIdx.x / TPX;
+  const int Leff = up2 ? 2 * Lin : Lin;
+  const float* xb = x + (int64_t)b * Ci * Lin;
+  const int start = l0 * S - P;
+  float acc[RC][RP];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int co = o0 + ty * RC + r;
+    const float bv = (bias && co < Co) ? bias[co] : 0.f;
+#pragma unroll
+    for (int i = 0; i < RP; ++i) acc[r][i] = bv;
+  }
+  for (int c0 = 0; c0 < Ci; c0 += CC) {
+    const int cc = min(CC, Ci - c0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < cc * span; i += 256) {
+      const int c = i / span, j = i - c * span;
+      int p = start + j;
+      if (replicate) p = min(max(p, 0), Leff - 1);
+      xs[i] = (p >= 0 && p < Leff) ? xb[(int64_t)(c0 + c) * Lin + (up2 ? (p >> 1) : p)] : 0.f;
+    }
+    for (int i = threadIdx.x; i < cc * K * TC; i += 256) {
+      const int o = i % TC, ck = i / TC;
+      const int c = ck / K, k = ck - c * K;
+      wsm[i] = (o0 + o < Co) ? w[((int64_t)(o0 + o) * Ci + c0 + c) * K + k] : 0.f;
+    }
+    __syncthreads();
+    for (int c = 0; c < cc; ++c) {
+      const float* xr = xs + c * span + tx * S;
+      const float* wr = wsm + c * K * TC + ty * RC;
+      for (int k = 0; k < K; ++k) {
+        const floatx4 wv = *reinterpret_cast<const floatx4*>(wr + k * TC);
+        float xv[RP];
+#pragma unroll
+        for (int i = 0; i < RP; ++i) xv[i] = xr[i * TPX * S + k];
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+#pragma unroll
+          for (int i = 0; i < RP; ++i) acc[r][i] = fmaf(wv[r], xv[i], acc[r][i]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int co = o0 + ty * RC + r;
+    if (co >= Co) continue;
+#pragma unroll
+    for (int i = 0; i < RP; ++i) {
+      const int l = l0 + tx + i * TPX;
+      if (l >= Lout) continue;
+      const int64_t at = ((int64_t)b * Co + co) * Lout + l;
+      y[at] = acc[r][i] + (res ? res[at] : 0.f);
+    }
+  }
+}
+
 // nn.GroupNorm(G, C) (eps) then SnakeActivation (train_utils.py:446-448), + residual:
 // Block.forward + ResnetBlock's `h + res_conv(x)` (fidelity_enhancer.py:193-231).  One
 // block per (b, g); the group's (C/G) x L values are contiguous.
@@ -147,14 +222,18 @@ __global__ __launch_bounds__(256) void chan_ln_kernel(const float* __restrict__ 
 //   ctx[d, e] = sum_n k[d, n] v[e, n],  out[e, n] = sum_d ctx[d, e] q[d, n].
 // qkv (B, 3 H dh, n) as to_qkv writes it (chunk order q, k, v; head-major channels).
 constexpr int FE_DH = 32;
-__global__ __launch_bounds__(256) void linear_attn_kernel(const float* __restrict__ qkv, int H,
-                                                          int n, float scale,
+constexpr int CTX_LD = FE_DH + 4;
+__global__ __launch_bounds__(256) void linear_attn_kernel(const float* __restrict__ qkv,
+                                                          int H, int n, float scale,
                                                           float* __restrict__ out) {
   extern __shared__ float sm[];
   const int ld = n + 1;  // padded row stride: the context loop reads v[e][*] across lanes
   float* ks = sm;
   float* vs = sm + FE_DH * ld;
-  float* ctx = vs + FE_DH * ld;  // FE_DH x (FE_DH + 1)
+  // the j-quarter partials of ctx overlay k/v once both are consumed
+  const int kv = max(2 * FE_DH * ld, 4 * FE_DH * CTX_LD);
+  float* part = sm;
+  float* ctx = sm + kv;  // FE_DH x CTX_LD (float4-aligned rows)
   const int b = blockIdx.x / H, h = blockIdx.x - b * H;
   const int HD = H * FE_DH;
   const float* q = qkv + ((int64_t)b * 3 * HD + h * FE_DH) * n;
@@ -183,18 +262,41 @@ __global__ __launch_bounds__(256) void linear_attn_kernel(const float* __restric
   }
   __syncthreads();
   {
-    const int e = threadIdx.x & 31, d0 = threadIdx.x >> 5;  // 8 x 32 threads, 4 d each
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int j = 0; j < n; ++j) {
-      const float vv = vs[e * ld + j];
+    // ctx partials: 4 quarters of n x (8 d-groups x 8 e-groups), 4 d x 4 e per thread
+    // (16 FMAs per 8 LDS reads); quarters summed in order 0..3 below
+    const int qt = threadIdx.x >> 6, dg = (threadIdx.x >> 3) & 7, eg = threadIdx.x & 7;
+    const int per = (n + 3) / 4, j0 = qt * per, j1 = min(n, j0 + per);
+    float acc[4][4] = {};
+#pragma unroll 2
+    for (int j = j0; j < j1; ++j) {
+      float kd[4], ve[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = fmaf(ks[(d0 + 8 * r) * ld + j], vv, acc[r]);
+      for (int r = 0; r < 4; ++r) {
+        kd[r] = ks[(dg * 4 + r) * ld + j];
+        ve[r] = vs[(eg * 4 + r) * ld + j];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(kd[r], ve[c], acc[r][c]);
     }
+    __syncthreads();  // k and v consumed: the partials overlay them
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ctx[(d0 + 8 * r) * (FE_DH + 1) + e] = acc[r];
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        part[(qt * FE_DH + dg * 4 + r) * CTX_LD + eg * 4 + c] = acc[r][c];
   }
   __syncthreads();
-  float* ob = out + ((int64_t)b * HD + h * FE_DH) * n;
+  for (int i = threadIdx.x; i < FE_DH * FE_DH; i += blockDim.x) {
+    const int d = i >> 5, e = i & 31;
+    float s = part[d * CTX_LD + e];
+#pragma unroll
+    for (int t = 1; t < 4; ++t) s += part[(t * FE_DH + d) * CTX_LD + e];
+    ctx[d * CTX_LD + e] = s;
+  }
+  __syncthreads();
+  // q softmax over d (x scale) per column, into the k rows (k is consumed)
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
     float qd[FE_DH];
     float m = -INFINITY;
@@ -210,14 +312,35 @@ __global__ __launch_bounds__(256) void linear_attn_kernel(const float* __restric
       s += qd[d];
     }
 #pragma unroll
-    for (int d = 0; d < FE_DH; ++d) qd[d] = qd[d] / s * scale;
-#pragma unroll 4
-    for (int e = 0; e < FE_DH; ++e) {
-      float o = 0.f;
+    for (int d = 0; d < FE_DH; ++d) ks[d * ld + j] = qd[d] / s * scale;
+  }
+  __syncthreads();
+  // out[e, j] = sum_d ctx[d, e] q[d, j]: each thread 4 e x 4 j (16 FMAs per 5 LDS reads)
+  float* ob = out + ((int64_t)b * HD + h * FE_DH) * n;
+  const int te = threadIdx.x & 7, tj = threadIdx.x >> 3;
+  for (int jb = 0; jb < n; jb += 128) {
+    float acc[4][4] = {};
+#pragma unroll 2
+    for (int d = 0; d < FE_DH; ++d) {
+      const floatx4 cv = *reinterpret_cast<const floatx4*>(ctx + d * CTX_LD + te * 4);
+      float qv[4];
 #pragma unroll
-      for (int d = 0; d < FE_DH; ++d) o = fmaf(ctx[d * (FE_DH + 1) + e], qd[d], o);
-      ob[(int64_t)e * n + j] = o;
+      for (int i = 0; i < 4; ++i) {
+        const int j = jb + tj + 32 * i;
+        qv[i] = j < n ? ks[d * ld + j] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[r][i] = fmaf(cv[r], qv[i], acc[r][i]);
     }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = jb + tj + 32 * i;
+        if (j < n) ob[(int64_t)(te * 4 + r) * n + j] = acc[r][i];
+      }
   }
 }
 
@@ -343,6 +466,33 @@ int tvq_fe_conv1d(const float* x, int64_t B, int64_t Ci, int64_t Lin, const floa
                 "tvq_fe_conv1d: bad arguments");
   TVQ_CHECK_ARG(Lout == tvq_fe_conv1d_out_len(Lin, K, S, P, up2) && Lout > 0,
                 "tvq_fe_conv1d: Lout %lld does not match the conv geometry", (long long)Lout);
+  if (S <= 2 && K <= 7) {
+    // register-blocked path: pick the tile (TP positions x TC channels) that pads least
+    struct V { int tp, tc; };
+    const V vs[3] = {{256, 16}, {128, 32}, {64, 64}};
+    int best = 0;
+    int64_t best_area = -1;
+    for (int v = 0; v < 3; ++v) {
+      const int64_t area = ((Lout + vs[v].tp - 1) / vs[v].tp) * vs[v].tp *
+                           ((Co + vs[v].tc - 1) / vs[v].tc) * vs[v].tc;
+      if (best_area < 0 || area <= best_area) best = v, best_area = area;
+    }
+    const int64_t span = (vs[best].tp - 1) * S + K;
+    const size_t lds = (size_t)(16 * span + 16 * K * vs[best].tc) * sizeof(float);
+    TVQ_CHECK_ARG(B <= 65535 && (Co + vs[best].tc - 1) / vs[best].tc <= 65535,
+                  "tvq_fe_conv1d: grid too large");
+    dim3 grid((unsigned)((Lout + vs[best].tp - 1) / vs[best].tp),
+              (unsigned)((Co + vs[best].tc - 1) / vs[best].tc), (unsigned)B);
+#define FE_RB_LAUNCH(TPX, TCY)                                                                \
+  hipLaunchKernelGGL((conv1d_rb_kernel<TPX, TCY>), grid, dim3(256), lds, (hipStream_t)stream, x, \
+                     (int)Ci, (int)Lin, w, bias, (int)Co, (int)K, (int)S, (int)P, (int)up2,      \
+                     (int)replicate, residual, y, (int)Lout, (int)span)
+    if (best == 0) FE_RB_LAUNCH(64, 4);
+    else if (best == 1) FE_RB_LAUNCH(32, 8);
+    else FE_RB_LAUNCH(16, 16);
+#undef FE_RB_LAUNCH
+    return launch_status("tvq_fe_conv1d");
+  }
   const int64_t span = (FE_TILE - 1) * S + K;
   const int64_t lds = Ci * span * (int64_t)sizeof(float);
   TVQ_CHECK_ARG(lds <= 160 * 1024, "tvq_fe_conv1d: Ci %lld x span %lld exceeds LDS",
@@ -380,11 +530,13 @@ int tvq_fe_linear_attention(const float* qkv, int64_t B, int64_t H, int64_t dh, 
                             float* out, tvq_stream_t stream) {
   TVQ_CHECK_ARG(qkv && out && B > 0 && H > 0 && n > 0 && dh == FE_DH,
                 "tvq_fe_linear_attention: bad arguments (dim_head must be %d)", FE_DH);
-  const int64_t lds = (2 * FE_DH * (n + 1) + FE_DH * (FE_DH + 1)) * (int64_t)sizeof(float);
+  const int64_t kv = 2 * FE_DH * (n + 1) > 4 * FE_DH * CTX_LD ? 2 * FE_DH * (n + 1) : 4 * FE_DH * CTX_LD;
+  const int64_t lds = (kv + FE_DH * CTX_LD) * (int64_t)sizeof(float);
   TVQ_CHECK_ARG(lds <= 160 * 1024, "tvq_fe_linear_attention: n %lld exceeds LDS", (long long)n);
   fe_lds_attr();
   hipLaunchKernelGGL(linear_attn_kernel, dim3((unsigned)(B * H)), dim3(256), (size_t)lds,
-                     (hipStream_t)stream, qkv, (int)H, (int)n, 1.0f / sqrtf((float)dh), out);
+                     (hipStream_t)stream, qkv, (int)H, (int)n, 1.0f / sqrtf((float)dh),
+                     out);
   return launch_status("tvq_fe_linear_attention");
 }
 

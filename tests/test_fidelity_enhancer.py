@@ -86,7 +86,7 @@ def test_hip_fe_sampler_batch_vs_oracle(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K,S,P,up2,rep", [(7, 1, 3, 0, 0), (4, 2, 1, 0, 0), (3, 1, 1, 1, 0),
+@pytest.mark.parametrize("K,S,P,up2,rep", [(7, 1, 3, 0, 0), (4, 2, 1, 0, 0), (3, 1, 1, 1, 0), (9, 3, 4, 0, 0),
                                           (3, 1, 1, 0, 1), (1, 1, 0, 0, 0)])
 def test_hip_conv1d_geometries(K, S, P, up2, rep, cuda):
     from timevqvae.hip import fe as ops
