@@ -86,20 +86,21 @@ __global__ __launch_bounds__(256) void conv1d_kernel(const float* __restrict__ x
 }
 
 // Register-blocked conv1d (the FidelityEnhancer's shapes: Ci <= 96, K <= 7, S <= 2).
-// Block tile TC = 4 TCY output channels x TP = 4 TPX positions; each thread owns 4
-// channels x 4 positions (positions tx + i TPX, so LDS reads of the input are consecutive
+// Block tile TC = 4 TCY output channels x TP = RP TPX positions; each thread owns 4
+// channels x RP positions (positions tx + i TPX, so LDS reads of the input are consecutive
 // across lanes).  Input channels are streamed in chunks of 16: the chunk's input span and
 // its weights (as [c][k][co], read as float4) are staged in LDS, then every (c, k) does
 // 16 FMAs for 4 + 1 LDS reads.  Sum order per output: c ascending, then k (as
 // conv1d_kernel).
-template <int TPX, int TCY>
+template <int TPX, int TCY, int RP, int KT>
 __global__ __launch_bounds__(256) void conv1d_rb_kernel(const float* __restrict__ x, int Ci, int Lin,
                                                         const float* __restrict__ w,
                                                         const float* __restrict__ bias, int Co,
-                                                        int K, int S, int P, int up2, int replicate,
+                                                        int K_, int S, int P, int up2, int replicate,
                                                         const float* __restrict__ res,
                                                         float* __restrict__ y, int Lout, int span) {
-  constexpr int RC = 4, RP = 4, CC = 16, TP = TPX * RP, TC = TCY * RC;
+  constexpr int RC = 4, CC = 16, TP = TPX * RP, TC = TCY * RC;
+  const int K = KT > 0 ? KT : K_;  // KT: taps known at compile time (k loop unrolled)
   extern __shared__ float sm[];
   float* xs = sm;                // CC x span
   float* wsm = sm + CC * span;   // CC x K x TC
@@ -119,22 +120,28 @@ __global__ __launch_bounds__(256) void conv1d_rb_kernel(const float* __restrict_
   for (int c0 = 0; c0 < Ci; c0 += CC) {
     const int cc = min(CC, Ci - c0);
     __syncthreads();
-    for (int i = threadIdx.x; i < cc * span; i += 256) {
-      const int c = i / span, j = i - c * span;
-      int p = start + j;
-      if (replicate) p = min(max(p, 0), Leff - 1);
-      xs[i] = (p >= 0 && p < Leff) ? xb[(int64_t)(c0 + c) * Lin + (up2 ? (p >> 1) : p)] : 0.f;
+    {  // x span rows of the chunk; (c, j) advanced incrementally (one division per thread)
+      int c = threadIdx.x / span, j = threadIdx.x - (threadIdx.x / span) * span;
+      for (int i = threadIdx.x; i < cc * span; i += 256) {
+        int p = start + j;
+        if (replicate) p = min(max(p, 0), Leff - 1);
+        xs[i] = (p >= 0 && p < Leff) ? xb[(int64_t)(c0 + c) * Lin + (up2 ? (p >> 1) : p)] : 0.f;
+        j += 256;
+        while (j >= span) j -= span, ++c;
+      }
     }
-    for (int i = threadIdx.x; i < cc * K * TC; i += 256) {
-      const int o = i % TC, ck = i / TC;
-      const int c = ck / K, k = ck - c * K;
-      wsm[i] = (o0 + o < Co) ? w[((int64_t)(o0 + o) * Ci + c0 + c) * K + k] : 0.f;
+    {  // weights as [c k][o]: row ck of output channel o is w[o][c0 K + ck]
+      const int o = threadIdx.x % TC;
+      const bool ok = o0 + o < Co;
+      const float* wo = w + ((int64_t)(o0 + o) * Ci + c0) * K;
+      for (int ck = threadIdx.x / TC; ck < cc * K; ck += 256 / TC) wsm[ck * TC + o] = ok ? wo[ck] : 0.f;
     }
     __syncthreads();
     for (int c = 0; c < cc; ++c) {
       const float* xr = xs + c * span + tx * S;
       const float* wr = wsm + c * K * TC + ty * RC;
-      for (int k = 0; k < K; ++k) {
+#pragma unroll
+      for (int k = 0; k < (KT > 0 ? KT : K); ++k) {
         const floatx4 wv = *reinterpret_cast<const floatx4*>(wr + k * TC);
         float xv[RP];
 #pragma unroll
@@ -469,13 +476,14 @@ int tvq_fe_conv1d(const float* x, int64_t B, int64_t Ci, int64_t Lin, const floa
   if (S <= 2 && K <= 7) {
     // register-blocked path: pick the tile (TP positions x TC channels) that pads least
     struct V { int tp, tc; };
-    const V vs[3] = {{256, 16}, {128, 32}, {64, 64}};
+    const V vs[4] = {{256, 16}, {128, 32}, {64, 64}, {32, 64}};
     int best = 0;
     int64_t best_area = -1;
-    for (int v = 0; v < 3; ++v) {
+    for (int v = 0; v < 4; ++v) {
       const int64_t area = ((Lout + vs[v].tp - 1) / vs[v].tp) * vs[v].tp *
                            ((Co + vs[v].tc - 1) / vs[v].tc) * vs[v].tc;
-      if (best_area < 0 || area <= best_area) best = v, best_area = area;
+      // ties go to the later (wider-channel) tile, except the 2-position one (v = 3)
+      if (best_area < 0 || area < best_area || (area == best_area && v < 3)) best = v, best_area = area;
     }
     const int64_t span = (vs[best].tp - 1) * S + K;
     const size_t lds = (size_t)(16 * span + 16 * K * vs[best].tc) * sizeof(float);
@@ -483,14 +491,22 @@ int tvq_fe_conv1d(const float* x, int64_t B, int64_t Ci, int64_t Lin, const floa
                   "tvq_fe_conv1d: grid too large");
     dim3 grid((unsigned)((Lout + vs[best].tp - 1) / vs[best].tp),
               (unsigned)((Co + vs[best].tc - 1) / vs[best].tc), (unsigned)B);
-#define FE_RB_LAUNCH(TPX, TCY)                                                                \
-  hipLaunchKernelGGL((conv1d_rb_kernel<TPX, TCY>), grid, dim3(256), lds, (hipStream_t)stream, x, \
+#define FE_RB_LAUNCH_K(TPX, TCY, RP, KT)                                                      \
+  hipLaunchKernelGGL((conv1d_rb_kernel<TPX, TCY, RP, KT>), grid, dim3(256), lds, (hipStream_t)stream, x, \
                      (int)Ci, (int)Lin, w, bias, (int)Co, (int)K, (int)S, (int)P, (int)up2,      \
                      (int)replicate, residual, y, (int)Lout, (int)span)
-    if (best == 0) FE_RB_LAUNCH(64, 4);
-    else if (best == 1) FE_RB_LAUNCH(32, 8);
-    else FE_RB_LAUNCH(16, 16);
+#define FE_RB_LAUNCH(TPX, TCY, RP)             \
+  do {                                          \
+    if (K == 1) FE_RB_LAUNCH_K(TPX, TCY, RP, 1); \
+    else if (K == 3) FE_RB_LAUNCH_K(TPX, TCY, RP, 3); \
+    else FE_RB_LAUNCH_K(TPX, TCY, RP, 0);       \
+  } while (0)
+    if (best == 0) FE_RB_LAUNCH(64, 4, 4);
+    else if (best == 1) FE_RB_LAUNCH(32, 8, 4);
+    else if (best == 2) FE_RB_LAUNCH(16, 16, 4);
+    else FE_RB_LAUNCH(16, 16, 2);
 #undef FE_RB_LAUNCH
+#undef FE_RB_LAUNCH_K
     return launch_status("tvq_fe_conv1d");
   }
   const int64_t span = (FE_TILE - 1) * S + K;

@@ -37,6 +37,14 @@ def conv1d(x, weight, bias=None, stride=1, padding=0, upsample2=False, replicate
     return y
 
 
+def standardize_weight(weight, eps=1e-5):
+    """WeightStandardizedConv2d's weight (fidelity_enhancer.py:102-106) on the device."""
+    w = _c(weight)
+    out = torch.empty_like(w)
+    call("tvq_fe_ws_weight", ptr(w), w.shape[0], w[0].numel(), float(eps), ptr(out), stream_ptr())
+    return out
+
+
 def group_norm_snake(x, groups, gamma, beta, a, eps=1e-5, residual=None):
     """GroupNorm -> Snake (+ residual): Block.forward + ResnetBlock skip (:193-231)."""
     x = _c(x)

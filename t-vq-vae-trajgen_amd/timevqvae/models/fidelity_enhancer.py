@@ -76,8 +76,13 @@ class WeightStandardizedConv2d(nn.Conv1d):
     """fidelity_enhancer.py:96-116 (the name is the reference's; it is a Conv1d)."""
 
     def forward(self, x):
-        return ops.conv1d(x, self.weight, self.bias, stride=self.stride[0],
-                          padding=self.padding[0], standardize=True, eps=1e-5)
+        # the standardised weight is kept until the parameter changes (its version counter
+        # moves on every in-place update: optimizer steps, load_state_dict, .to())
+        key = (self.weight.data_ptr(), self.weight._version, self.weight.device)
+        if getattr(self, "_ws_key", None) != key:
+            self._ws = ops.standardize_weight(self.weight, 1e-5)
+            self._ws_key = key
+        return ops.conv1d(x, self._ws, self.bias, stride=self.stride[0], padding=self.padding[0])
 
 
 class LayerNorm(nn.Module):

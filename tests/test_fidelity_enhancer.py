@@ -83,6 +83,13 @@ def test_hip_fe_sampler_batch_vs_oracle(cuda):
     assert ok, err
     assert torch.equal(y[1023], y[5])
     assert torch.isfinite(y).all()
+    # the cached standardised weights follow in-place parameter updates
+    w = fe.unet.downs[0][0].block1.proj.weight
+    with torch.no_grad():
+        w.mul_(1.5).add_(0.01)
+    sd = {k: v.detach().cpu() for k, v in fe.state_dict().items()}
+    ok, err = _close(fe(x[:8].to(cuda)).cpu().numpy(), O.fe_forward(sd, x[:8], 256).numpy())
+    assert ok, err
 
 
 @pytest.mark.gpu
