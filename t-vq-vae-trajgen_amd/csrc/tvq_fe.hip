@@ -246,10 +246,24 @@ __global__ __launch_bounds__(256) void linear_attn_kernel(const float* __restric
   const float* q = qkv + ((int64_t)b * 3 * HD + h * FE_DH) * n;
   const float* k = q + (int64_t)HD * n;
   const float* v = k + (int64_t)HD * n;
-  for (int i = threadIdx.x; i < FE_DH * n; i += blockDim.x) {
-    const int d = i / n, j = i - d * n;
-    ks[d * ld + j] = k[i];
-    vs[d * ld + j] = v[i];
+  if ((n & 3) == 0) {  // 16-byte loads (rows of k / v are n floats, 16-byte aligned)
+    const int n4 = n >> 2;
+    for (int i = threadIdx.x; i < FE_DH * n4; i += blockDim.x) {
+      const int d = i / n4, j = (i - d * n4) * 4;
+      const floatx4 kv4 = *reinterpret_cast<const floatx4*>(k + (int64_t)d * n + j);
+      const floatx4 vv4 = *reinterpret_cast<const floatx4*>(v + (int64_t)d * n + j);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        ks[d * ld + j + t] = kv4[t];
+        vs[d * ld + j + t] = vv4[t];
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < FE_DH * n; i += blockDim.x) {
+      const int d = i / n, j = i - d * n;
+      ks[d * ld + j] = k[i];
+      vs[d * ld + j] = v[i];
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;

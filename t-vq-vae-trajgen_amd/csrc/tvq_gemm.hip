@@ -8,6 +8,7 @@
 // Split-K over gridDim.z writes fp32 slabs reduced in split order (deterministic), by
 // the last-arriving split block of each tile (or a separate reduce launch).
 #include <math.h>
+#include <stdlib.h>
 
 #include "tvq_common.h"
 
@@ -245,15 +246,28 @@ static int gemm_splits(int M, int N, int K, int tiles) {
 
 using namespace tvq;
 
-// Largest tile that still gives >= 256 blocks (the step's GEMMs have K <= 512 and a few
-// thousand rows: latency-bound, so filling the 256 CUs matters more than tile reuse);
-// deep-K GEMMs that stay small get split-K instead.
+// Largest tile that still gives >= TVQ_GEMM_MIN_BLOCKS (default 256) blocks: the GEMMs
+// here have K <= 512, so filling the 256 CUs matters more than tile reuse.  (Measured:
+// 1024 / 2048 minimum blocks, i.e. smaller tiles, change neither the sampler's
+// M = 25600, N = 128, K = 128 projections nor the train step.)  Deep-K GEMMs that stay
+// small get split-K instead.  The tile does not change the k order: results are bitwise
+// the same for every tile.
+static int gemm_min_blocks() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("TVQ_GEMM_MIN_BLOCKS");
+    v = e ? atoi(e) : 256;
+    if (v < 1) v = 1;
+  }
+  return v;
+}
 static void choose_tile(int64_t M, int64_t N, int* TM, int* TN) {
   static const int cand[4][2] = {{128, 64}, {64, 64}, {64, 32}, {32, 32}};
+  const int64_t want = gemm_min_blocks();
   for (int i = 0; i < 4; ++i) {
     *TM = cand[i][0];
     *TN = cand[i][1];
-    if (((M + *TM - 1) / *TM) * ((N + *TN - 1) / *TN) >= 256) return;
+    if (((M + *TM - 1) / *TM) * ((N + *TN - 1) / *TN) >= want) return;
   }
 }
 

@@ -47,3 +47,43 @@ def conditional_sample(maskgit, n_samples: int, device, class_index: int, batch_
     """class_index: starting from 0 (sample_utils.py:70-88)."""
     return unconditional_sample(maskgit, n_samples, device, class_index, batch_size,
                                 return_representations)
+
+
+class GraphedSampler:
+    """One sampling batch -- MaskGIT iterative decoding (maskgit.py:413-446), LF/HF decoding
+    (maskgit.py:448-477) and optionally the FidelityEnhancer (sampler.py:156-169) --
+    captured once as a hipGraph and replayed per batch.
+
+    Every step of the batch already runs on the device with fixed shapes (the mask
+    lengths are host constants, sampling noise is the counter hash of the device seed), so
+    the graph holds the whole batch; the device seed advances inside it, so each replay
+    draws a fresh batch, equal to the eager `rng.advance(); iterative_decoding(...)` from
+    the same seed.  `sample()` returns (x_l, x_h, x[, x_R]) device tensors that the next
+    replay overwrites (clone them to keep)."""
+
+    def __init__(self, maskgit, num: int, device, class_index=None, fidelity_enhancer=None,
+                 warmup: int = 2):
+        from ..hip import rng
+        from ..hip.graph import StepGraph
+        self.maskgit, self.num, self.device = maskgit, num, torch.device(device)
+        self.class_index, self.fe = class_index, fidelity_enhancer
+        maskgit.eval()
+        if fidelity_enhancer is not None:
+            fidelity_enhancer.eval()
+
+        def batch():
+            with torch.no_grad():
+                rng.advance(self.device)
+                s_l, s_h = maskgit.iterative_decoding(num=num, device=self.device,
+                                                      class_index=class_index)
+                x_l = maskgit.decode_token_ind_to_timeseries(s_l, "lf")
+                x_h = maskgit.decode_token_ind_to_timeseries(s_h, "hf")
+                out = (x_l, x_h, x_l + x_h)
+                if fidelity_enhancer is not None:
+                    out = out + (fidelity_enhancer(out[2]),)
+                return out
+
+        self.graph = StepGraph([batch], warmup=warmup).capture()
+
+    def sample(self):
+        return self.graph.replay()[0]

@@ -108,3 +108,29 @@ def test_sample_utils_decode(cuda):
     E = mg.vq_model_l._codebook.embed
     want = E[s].transpose(1, 2).reshape(zq.shape)
     assert torch.equal(zq, want)
+
+
+@pytest.mark.gpu
+def test_graphed_sampler_equals_eager(cuda):
+    """A replay of the captured sampling batch equals the eager batch from the same device
+    seed (decode + FidelityEnhancer included), and successive replays differ."""
+    from timevqvae.hip import rng
+    from timevqvae.models import FidelityEnhancer
+    from timevqvae.utils.sample_utils import GraphedSampler
+    mg = _maskgit(cuda)
+    fe = FidelityEnhancer(64, 3, {"fidelity_enhancer": {"dim": 8, "dim_mults": [1, 2, 4, 8],
+                                                        "resnet_block_groups": 4}}).to(cuda)
+    gs = GraphedSampler(mg, 48, cuda, class_index=1, fidelity_enhancer=fe)
+    rng.manual_seed(7)
+    got = [t.clone() for t in gs.sample()]
+    again = [t.clone() for t in gs.sample()]
+    rng.manual_seed(7)
+    with torch.no_grad():
+        rng.advance(cuda)
+        s_l, s_h = mg.iterative_decoding(num=48, device=cuda, class_index=1)
+        x_l = mg.decode_token_ind_to_timeseries(s_l, "lf")
+        x_h = mg.decode_token_ind_to_timeseries(s_h, "hf")
+        want = [x_l, x_h, x_l + x_h, fe(x_l + x_h)]
+    for g, w in zip(got, want):
+        assert torch.equal(g, w)
+    assert not torch.equal(again[2], got[2])
