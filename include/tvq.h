@@ -402,6 +402,11 @@ int tvq_fe_channel_layernorm(const float* x, int64_t B, int64_t C, int64_t L, co
                              float eps, const float* residual, float* y, tvq_stream_t stream);
 int tvq_fe_linear_attention(const float* qkv, int64_t B, int64_t H, int64_t dh, int64_t n,
                             float* out, tvq_stream_t stream);
+/* tvq_fe_linear_attention_fused: the same from the block input x (B, C, n) and the to_qkv
+ * weight (3 H dh, C): q/k/v computed in LDS (bitwise equal to tvq_fe_conv1d + the core). */
+int tvq_fe_linear_attention_fused(const float* x, int64_t B, int64_t C, int64_t n,
+                                  const float* wqkv, int64_t H, int64_t dh, float* out,
+                                  tvq_stream_t stream);
 int tvq_fe_attention(const float* qkv, int64_t B, int64_t H, int64_t dh, int64_t n, float* out,
                      tvq_stream_t stream);
 int tvq_fe_cat_interp(const float* a, int64_t Ca, int64_t La, const float* b, int64_t Cb,

@@ -230,7 +230,46 @@ __global__ __launch_bounds__(256) void chan_ln_kernel(const float* __restrict__ 
 // qkv (B, 3 H dh, n) as to_qkv writes it (chunk order q, k, v; head-major channels).
 constexpr int FE_DH = 32;
 constexpr int CTX_LD = FE_DH + 4;
+// dst[r][j] (row stride ld) = sum_c wl[c][row0 + r] * xs[c][j], r < NR, j < n, c ascending
+// from 0 (the order conv1d_rb_kernel sums a bias-free 1x1 conv in: bitwise equal).  Each
+// thread owns 4 rows x 4 columns: per c one float4 weight read + 4 input reads for 16 FMAs.
+template <int NR>
+__device__ __forceinline__ void la_rows_matmul(const float* __restrict__ wl, int row0,
+                                               const float* __restrict__ xs, int C, int n,
+                                               float* __restrict__ dst, int ld) {
+  constexpr int TCOL = 256 / (NR / 4);  // threads along columns
+  const int tr = threadIdx.x / TCOL, tc = threadIdx.x % TCOL;
+  for (int jb = 0; jb < n; jb += 4 * TCOL) {
+    float acc[4][4] = {};
+    for (int c = 0; c < C; ++c) {
+      const floatx4 w4 = *reinterpret_cast<const floatx4*>(wl + c * 96 + row0 + tr * 4);
+      float xv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = jb + tc + i * TCOL;
+        xv[i] = j < n ? xs[c * n + j] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[r][i] = fmaf(w4[r], xv[i], acc[r][i]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = jb + tc + i * TCOL;
+        if (j < n) dst[(tr * 4 + r) * ld + j] = acc[r][i];
+      }
+  }
+}
+
+// FUSED: `qkv` is the block input x (B, C, n) and wqkv the to_qkv weight (3 H dh, C): the
+// block computes its head's 96 q/k/v rows from x and the weights staged in LDS, so the
+// (B, 3 H dh, n) qkv tensor never goes through HBM.
+template <bool FUSED>
 __global__ __launch_bounds__(256) void linear_attn_kernel(const float* __restrict__ qkv,
+                                                          const float* __restrict__ wqkv, int C,
                                                           int H, int n, float scale,
                                                           float* __restrict__ out) {
   extern __shared__ float sm[];
@@ -244,25 +283,38 @@ __global__ __launch_bounds__(256) void linear_attn_kernel(const float* __restric
   const int b = blockIdx.x / H, h = blockIdx.x - b * H;
   const int HD = H * FE_DH;
   const float* q = qkv + ((int64_t)b * 3 * HD + h * FE_DH) * n;
-  const float* k = q + (int64_t)HD * n;
-  const float* v = k + (int64_t)HD * n;
-  if ((n & 3) == 0) {  // 16-byte loads (rows of k / v are n floats, 16-byte aligned)
-    const int n4 = n >> 2;
-    for (int i = threadIdx.x; i < FE_DH * n4; i += blockDim.x) {
-      const int d = i / n4, j = (i - d * n4) * 4;
-      const floatx4 kv4 = *reinterpret_cast<const floatx4*>(k + (int64_t)d * n + j);
-      const floatx4 vv4 = *reinterpret_cast<const floatx4*>(v + (int64_t)d * n + j);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        ks[d * ld + j + t] = kv4[t];
-        vs[d * ld + j + t] = vv4[t];
-      }
+  float* xs = ctx + FE_DH * CTX_LD;  // FUSED: x[b] (C x n), then wl (C x 96)
+  float* wl = xs + C * n;
+  if (FUSED) {
+    const float* xb = qkv + (int64_t)b * C * n;
+    for (int i = threadIdx.x; i < C * n; i += blockDim.x) xs[i] = xb[i];
+    for (int i = threadIdx.x; i < 96 * C; i += blockDim.x) {
+      const int r = i / C, c = i - r * C;  // r: q 0..31, k 32..63, v 64..95
+      wl[c * 96 + r] = wqkv[((int64_t)(r >> 5) * HD + h * FE_DH + (r & 31)) * C + c];
     }
+    __syncthreads();
+    la_rows_matmul<2 * FE_DH>(wl, FE_DH, xs, C, n, ks, ld);  // k rows then v rows (vs = ks + 32 ld)
   } else {
-    for (int i = threadIdx.x; i < FE_DH * n; i += blockDim.x) {
-      const int d = i / n, j = i - d * n;
-      ks[d * ld + j] = k[i];
-      vs[d * ld + j] = v[i];
+    const float* k = q + (int64_t)HD * n;
+    const float* v = k + (int64_t)HD * n;
+    if ((n & 3) == 0) {  // 16-byte loads (rows of k / v are n floats, 16-byte aligned)
+      const int n4 = n >> 2;
+      for (int i = threadIdx.x; i < FE_DH * n4; i += blockDim.x) {
+        const int d = i / n4, j = (i - d * n4) * 4;
+        const floatx4 kv4 = *reinterpret_cast<const floatx4*>(k + (int64_t)d * n + j);
+        const floatx4 vv4 = *reinterpret_cast<const floatx4*>(v + (int64_t)d * n + j);
+  #pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          ks[d * ld + j + t] = kv4[t];
+          vs[d * ld + j + t] = vv4[t];
+        }
+      }
+    } else {
+      for (int i = threadIdx.x; i < FE_DH * n; i += blockDim.x) {
+        const int d = i / n, j = i - d * n;
+        ks[d * ld + j] = k[i];
+        vs[d * ld + j] = v[i];
+      }
     }
   }
   __syncthreads();
@@ -318,12 +370,16 @@ __global__ __launch_bounds__(256) void linear_attn_kernel(const float* __restric
   }
   __syncthreads();
   // q softmax over d (x scale) per column, into the k rows (k is consumed)
+  if (FUSED) {
+    la_rows_matmul<FE_DH>(wl, 0, xs, C, n, ks, ld);
+    __syncthreads();
+  }
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
     float qd[FE_DH];
     float m = -INFINITY;
 #pragma unroll
     for (int d = 0; d < FE_DH; ++d) {
-      qd[d] = q[(int64_t)d * n + j];
+      qd[d] = FUSED ? ks[d * ld + j] : q[(int64_t)d * n + j];
       m = fmaxf(m, qd[d]);
     }
     float s = 0.f;
@@ -454,7 +510,9 @@ void fe_lds_attr() {
   done = true;
   const int cap = 160 * 1024;
   (void)hipFuncSetAttribute((const void*)conv1d_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap);
-  (void)hipFuncSetAttribute((const void*)linear_attn_kernel,
+  (void)hipFuncSetAttribute((const void*)linear_attn_kernel<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+  (void)hipFuncSetAttribute((const void*)linear_attn_kernel<true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, cap);
   (void)hipFuncSetAttribute((const void*)attn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap);
 }
@@ -564,10 +622,26 @@ int tvq_fe_linear_attention(const float* qkv, int64_t B, int64_t H, int64_t dh, 
   const int64_t lds = (kv + FE_DH * CTX_LD) * (int64_t)sizeof(float);
   TVQ_CHECK_ARG(lds <= 160 * 1024, "tvq_fe_linear_attention: n %lld exceeds LDS", (long long)n);
   fe_lds_attr();
-  hipLaunchKernelGGL(linear_attn_kernel, dim3((unsigned)(B * H)), dim3(256), (size_t)lds,
-                     (hipStream_t)stream, qkv, (int)H, (int)n, 1.0f / sqrtf((float)dh),
-                     out);
+  hipLaunchKernelGGL(linear_attn_kernel<false>, dim3((unsigned)(B * H)), dim3(256), (size_t)lds,
+                     (hipStream_t)stream, qkv, nullptr, 0, (int)H, (int)n,
+                     1.0f / sqrtf((float)dh), out);
   return launch_status("tvq_fe_linear_attention");
+}
+
+int tvq_fe_linear_attention_fused(const float* x, int64_t B, int64_t C, int64_t n,
+                                  const float* wqkv, int64_t H, int64_t dh, float* out,
+                                  tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && wqkv && out && B > 0 && C > 0 && H > 0 && n > 0 && dh == FE_DH,
+                "tvq_fe_linear_attention_fused: bad arguments (dim_head must be %d)", FE_DH);
+  const int64_t kv = 2 * FE_DH * (n + 1) > 4 * FE_DH * CTX_LD ? 2 * FE_DH * (n + 1) : 4 * FE_DH * CTX_LD;
+  const int64_t lds = (kv + FE_DH * CTX_LD + C * n + 96 * C) * (int64_t)sizeof(float);
+  TVQ_CHECK_ARG(lds <= 160 * 1024, "tvq_fe_linear_attention_fused: C %lld x n %lld exceeds LDS",
+                (long long)C, (long long)n);
+  fe_lds_attr();
+  hipLaunchKernelGGL(linear_attn_kernel<true>, dim3((unsigned)(B * H)), dim3(256), (size_t)lds,
+                     (hipStream_t)stream, x, wqkv, (int)C, (int)H, (int)n,
+                     1.0f / sqrtf((float)dh), out);
+  return launch_status("tvq_fe_linear_attention_fused");
 }
 
 int tvq_fe_attention(const float* qkv, int64_t B, int64_t H, int64_t dh, int64_t n, float* out,

@@ -120,6 +120,7 @@ sig("tvq_fe_conv1d", P, I64, I64, I64, P, P, I64, I64, I64, I64, I64, I64, P, P,
 sig("tvq_fe_group_norm_snake", P, I64, I64, I64, I64, P, P, P, F32, P, P, P)
 sig("tvq_fe_channel_layernorm", P, I64, I64, I64, P, F32, P, P, P)
 sig("tvq_fe_linear_attention", P, I64, I64, I64, I64, P, P)
+sig("tvq_fe_linear_attention_fused", P, I64, I64, I64, P, I64, I64, P, P)
 sig("tvq_fe_attention", P, I64, I64, I64, I64, P, P)
 sig("tvq_fe_cat_interp", P, I64, I64, P, I64, I64, I64, I64, P, P)
 # --- trajectory data format (MinMax scaling + layout) -------------------------

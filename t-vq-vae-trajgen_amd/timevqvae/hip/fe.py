@@ -82,6 +82,23 @@ def linear_attention(qkv, heads, dim_head):
     return _attn("tvq_fe_linear_attention", qkv, heads, dim_head)
 
 
+def linear_attention_fused(x, w_qkv, heads, dim_head):
+    """to_qkv (1x1, no bias) + LinearAttention core in one kernel, bitwise equal to
+    conv1d + linear_attention: the (B, 3 H dh, n) qkv tensor stays in LDS."""
+    x, w = _c(x), _c(w_qkv)
+    B, C, n = x.shape
+    if w.shape[0] != 3 * heads * dim_head or w.shape[1] != C or w[0].numel() != C:
+        raise ValueError(f"linear_attention_fused: weight {tuple(w.shape)} vs x {tuple(x.shape)}")
+    kv = max(2 * 32 * (n + 1), 4 * 32 * 36)
+    if (kv + 32 * 36 + C * n + 96 * C) * 4 > 160 * 1024 or dim_head != 32:
+        # x and the head's weights do not fit beside q/k/v in LDS: the two-kernel HIP path
+        return linear_attention(conv1d(x, w), heads, dim_head)
+    out = torch.empty((B, heads * dim_head, n), device=x.device, dtype=torch.float32)
+    call("tvq_fe_linear_attention_fused", ptr(x), B, C, n, ptr(w), heads, dim_head, ptr(out),
+         stream_ptr())
+    return out
+
+
 def attention(qkv, heads, dim_head):
     """Attention core (:273-282) on to_qkv's output."""
     return _attn("tvq_fe_attention", qkv, heads, dim_head)

@@ -188,8 +188,7 @@ class LinearAttention(nn.Module):
         self.to_out = nn.Sequential(nn.Conv1d(hidden_dim, dim, 1), LayerNorm(dim))
 
     def forward(self, x, residual=None):
-        qkv = ops.conv1d(x, self.to_qkv.weight)
-        out = ops.linear_attention(qkv, self.heads, self.dim_head)
+        out = ops.linear_attention_fused(x, self.to_qkv.weight, self.heads, self.dim_head)
         conv, norm = self.to_out
         return norm(ops.conv1d(out, conv.weight, conv.bias), residual=residual)
 

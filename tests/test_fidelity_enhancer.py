@@ -131,6 +131,11 @@ def test_hip_fe_norms_and_attention(cuda):
         want = torch.einsum("bhde,bhdn->bhen", ctx, ql).reshape(3, 128, n)
         got = ops.linear_attention(qkv.to(cuda), 4, 32).cpu()
         assert torch.allclose(got, want, atol=1e-5, rtol=1e-4), n
+        # fused to_qkv: bitwise equal to the 1x1 conv followed by the core
+        for C in (8, 24, 64):
+            xin, wq = torch.randn(3, C, n).to(cuda), torch.randn(384, C, 1).to(cuda)
+            unfused = ops.linear_attention(ops.conv1d(xin, wq), 4, 32)
+            assert torch.equal(ops.linear_attention_fused(xin, wq, 4, 32), unfused), (n, C)
         attn = torch.einsum("bhdi,bhdj->bhij", q * 32 ** -0.5, k).softmax(-1)
         want = torch.einsum("bhij,bhdj->bhid", attn, v).permute(0, 1, 3, 2).reshape(3, 128, n)
         got = ops.attention(qkv.to(cuda), 4, 32).cpu()
