@@ -181,8 +181,8 @@ def roofline_leg(device):
     runs as one conv_t32_kernel launch (128-channel x 96-position tile on the 32x32x2 fp32
     MFMA, no split-K) reading the weight the step's pack cache packed once at the scope's
     begin (hip.conv.PackCache).  The committed rocprofv3 summary
-    (profiles/r01e_roofline_kernel_stats.csv) lists the launches; `traffic` is the
-    PMC-measured HBM bytes per op from profiles/r01e_roofline_traffic.json (FETCH_SIZE x2 +
+    (profiles/r01f_roofline_kernel_stats.csv) lists the launches; `traffic` is the
+    PMC-measured HBM bytes per op from profiles/r01f_roofline_traffic.json (FETCH_SIZE x2 +
     WRITE_SIZE passes)."""
     from timevqvae.hip.conv import PackCache, conv2d
     x = torch.randn(256, 128, 3, 32, device=device)
@@ -205,7 +205,7 @@ def roofline_leg(device):
     flops = 2.0 * (256 * 3 * 32) * 128 * (128 * 9)
     achieved = flops / (ms * 1e-3) / 1e12
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r01e_roofline_traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "r01f_roofline_traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath))["traffic_bytes"]
     return {"bound": "mfma", "kernel": "conv2d 128->128 3x3 @ (256,128,3,32): "
