@@ -170,6 +170,7 @@ __global__ __launch_bounds__(256) void conv1d_rb_kernel(const float* __restrict_
 // nn.GroupNorm(G, C) (eps) then SnakeActivation (train_utils.py:446-448), + residual:
 // Block.forward + ResnetBlock's `h + res_conv(x)` (fidelity_enhancer.py:193-231).  One
 // block per (b, g); the group's (C/G) x L values are contiguous.
+template <int PT>  // PT > 0: the group (<= 256 PT values) is held in registers, one HBM read
 __global__ __launch_bounds__(256) void gn_snake_kernel(const float* __restrict__ x, int C, int L,
                                                        int G, const float* __restrict__ gamma,
                                                        const float* __restrict__ beta,
@@ -180,27 +181,55 @@ __global__ __launch_bounds__(256) void gn_snake_kernel(const float* __restrict__
   const int cg = C / G, n = cg * L;
   const int64_t base = (int64_t)blockIdx.x * n;  // blockIdx.x = b * G + g
   const int c0 = (blockIdx.x % G) * cg;
+  float v[PT > 0 ? PT : 1];
   float s = 0.f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) s += x[base + i];
+  if (PT > 0) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int e = threadIdx.x + i * 256;
+      v[i] = e < n ? x[base + e] : 0.f;
+      s += v[i];
+    }
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s += x[base + i];
+  }
   const float mean = block_sum(s, red) / (float)n;
   float q = 0.f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const float d = x[base + i] - mean;
-    q += d * d;
+  if (PT > 0) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const float d = v[i] - mean;
+      q += threadIdx.x + i * 256 < n ? d * d : 0.f;
+    }
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const float d = x[base + i] - mean;
+      q += d * d;
+    }
   }
   const float rstd = rsqrtf(block_sum(q, red) / (float)n + eps);
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+  auto out = [&](int i, float xv) {
     const int c = c0 + i / L;
     const float sc = rstd * gamma[c];
-    float v = (x[base + i] - mean) * sc + beta[c];
+    float t = (xv - mean) * sc + beta[c];
     const float ac = a[c];
-    v = snake_f(v, ac, 1.0f / ac);
-    y[base + i] = v + (res ? res[base + i] : 0.f);
+    t = snake_f(t, ac, 1.0f / ac);
+    y[base + i] = t + (res ? res[base + i] : 0.f);
+  };
+  if (PT > 0) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int e = threadIdx.x + i * 256;
+      if (e < n) out(e, v[i]);
+    }
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) out(i, x[base + i]);
   }
 }
 
 // LayerNorm over channels, gamma only (fidelity_enhancer.py:119-127), + residual.
 // One thread per (b, l); the channel loop is coalesced across l.
+template <int CT>  // CT > 0: C == CT, the column held in registers (one HBM read)
 __global__ __launch_bounds__(256) void chan_ln_kernel(const float* __restrict__ x, int B, int C,
                                                       int L, const float* __restrict__ g,
                                                       float eps, const float* __restrict__ res,
@@ -209,18 +238,44 @@ __global__ __launch_bounds__(256) void chan_ln_kernel(const float* __restrict__ 
   if (t >= B * L) return;
   const int b = t / L, l = t - b * L;
   const float* xb = x + (int64_t)b * C * L + l;
+  float v[CT > 0 ? CT : 1];
   float s = 0.f;
-  for (int c = 0; c < C; ++c) s += xb[(int64_t)c * L];
+  if (CT > 0) {
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      v[c] = xb[(int64_t)c * L];
+      s += v[c];
+    }
+  } else {
+    for (int c = 0; c < C; ++c) s += xb[(int64_t)c * L];
+  }
   const float mean = s / (float)C;
   float q = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float d = xb[(int64_t)c * L] - mean;
-    q += d * d;
+  if (CT > 0) {
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const float d = v[c] - mean;
+      q += d * d;
+    }
+  } else {
+    for (int c = 0; c < C; ++c) {
+      const float d = xb[(int64_t)c * L] - mean;
+      q += d * d;
+    }
   }
   const float rstd = rsqrtf(q / (float)C + eps);
-  for (int c = 0; c < C; ++c) {
-    const int64_t at = (int64_t)b * C * L + (int64_t)c * L + l;
-    y[at] = (x[at] - mean) * rstd * g[c] + (res ? res[at] : 0.f);
+  const int64_t at0 = (int64_t)b * C * L + l;
+  if (CT > 0) {
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int64_t at = at0 + (int64_t)c * L;
+      y[at] = (v[c] - mean) * rstd * g[c] + (res ? res[at] : 0.f);
+    }
+  } else {
+    for (int c = 0; c < C; ++c) {
+      const int64_t at = at0 + (int64_t)c * L;
+      y[at] = (x[at] - mean) * rstd * g[c] + (res ? res[at] : 0.f);
+    }
   }
 }
 
@@ -600,8 +655,18 @@ int tvq_fe_group_norm_snake(const float* x, int64_t B, int64_t C, int64_t L, int
                             const float* residual, float* y, tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && y && gamma && beta && a && B > 0 && C > 0 && L > 0 && G > 0 && C % G == 0,
                 "tvq_fe_group_norm_snake: bad arguments");
-  hipLaunchKernelGGL(gn_snake_kernel, dim3((unsigned)(B * G)), dim3(256), 0, (hipStream_t)stream,
-                     x, (int)C, (int)L, (int)G, gamma, beta, a, eps, residual, y);
+  const int64_t n = C / G * L;
+  const dim3 grid((unsigned)(B * G));
+  const hipStream_t st = (hipStream_t)stream;
+  if (n <= 256 * 2)
+    hipLaunchKernelGGL(gn_snake_kernel<2>, grid, dim3(256), 0, st, x, (int)C, (int)L, (int)G, gamma,
+                       beta, a, eps, residual, y);
+  else if (n <= 256 * 8)
+    hipLaunchKernelGGL(gn_snake_kernel<8>, grid, dim3(256), 0, st, x, (int)C, (int)L, (int)G, gamma,
+                       beta, a, eps, residual, y);
+  else
+    hipLaunchKernelGGL(gn_snake_kernel<0>, grid, dim3(256), 0, st, x, (int)C, (int)L, (int)G, gamma,
+                       beta, a, eps, residual, y);
   return launch_status("tvq_fe_group_norm_snake");
 }
 
@@ -609,8 +674,16 @@ int tvq_fe_channel_layernorm(const float* x, int64_t B, int64_t C, int64_t L, co
                              float eps, const float* residual, float* y, tvq_stream_t stream) {
   TVQ_CHECK_ARG(x && y && g && B > 0 && C > 0 && L > 0, "tvq_fe_channel_layernorm: bad arguments");
   const int64_t n = B * L;
-  hipLaunchKernelGGL(chan_ln_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, x, (int)B, (int)C, (int)L, g, eps, residual, y);
+  const dim3 grid((unsigned)((n + 255) / 256));
+  const hipStream_t st = (hipStream_t)stream;
+#define FE_LN(CT) \
+  hipLaunchKernelGGL(chan_ln_kernel<CT>, grid, dim3(256), 0, st, x, (int)B, (int)C, (int)L, g, eps, residual, y)
+  if (C == 8) FE_LN(8);
+  else if (C == 16) FE_LN(16);
+  else if (C == 32) FE_LN(32);
+  else if (C == 64) FE_LN(64);
+  else FE_LN(0);
+#undef FE_LN
   return launch_status("tvq_fe_channel_layernorm");
 }
 

@@ -120,6 +120,14 @@ def test_hip_fe_norms_and_attention(cuda):
     got = ops.group_norm_snake(x.to(cuda), 4, gm.to(cuda), bt.to(cuda), a.to(cuda),
                                residual=res.to(cuda)).cpu()
     assert torch.allclose(got, want, atol=1e-5, rtol=1e-5)
+    for shape in [(3, 8, 100), (2, 64, 300)]:  # register-cached (n <= 512) and streamed groups
+        xg = torch.randn(*shape)
+        yg = F.group_norm(xg, 4, gm[:shape[1]], bt[:shape[1]], 1e-5)
+        ag = a[None, :shape[1], None]
+        wg = yg + (1 / ag) * torch.sin(ag * yg) ** 2
+        gg = ops.group_norm_snake(xg.to(cuda), 4, gm[:shape[1]].to(cuda), bt[:shape[1]].to(cuda),
+                                  a[:shape[1]].to(cuda)).cpu()
+        assert torch.allclose(gg, wg, atol=1e-5, rtol=1e-5), shape
     g = torch.randn(1, 64, 1)
     got = ops.channel_layernorm(x.to(cuda), g.to(cuda), residual=res.to(cuda)).cpu()
     assert torch.allclose(got, O.fe_layernorm(x, g) + res, atol=1e-5, rtol=1e-5)
