@@ -1,16 +1,24 @@
-"""FidelityEnhancer and its Unet1D (reference models/fidelity_enhancer.py) on the HIP path.
+"""FidelityEnhancer (reference models/fidelity_enhancer.py:458-498) and its 1-D U-Net
+(:289-455), eval forward on the HIP path (csrc/tvq_fe.hip via hip/fe.py).
 
-The module tree, constructor arguments and state_dict keys are the reference's, so a
-reference `stage3.ckpt`'s `fidelity_enhancer.*` entries load unchanged
-(generation/sampler.py:94-106).  The forward is the eval-mode forward (Dropout is the
-identity, no time embedding: Unet1D.forward never passes one, :395-455) and runs on
-csrc/tvq_fe.hip through hip/fe.py: weight-standardised convs, GroupNorm+Snake with the
-ResnetBlock skip fused, channel LayerNorm with the Residual add fused, linear / full
-attention, nearest-x2 upsampling read inside the conv, and interpolate+concat skips.
-Training the FidelityEnhancer (Stage3) is not on the HIP path: forward raises in
-training mode rather than silently differing from the reference's dropout."""
+Only the parameter layout is taken from the reference: attribute names and container
+indices reproduce its state_dict keys, so `stage3.ckpt`'s `fidelity_enhancer.*` entries
+load unchanged (generation/sampler.py:94-106).  The modules here are thin parameter
+holders; each forward is a handful of fused launches:
+
+  ResNet unit  (:207-231)  ws-conv3 -> [GroupNorm+Snake] -> ws-conv3 -> [GroupNorm+Snake
+                            + skip], the skip a 1x1 conv or the input itself
+  linear attn  (:234-260)  [channel LN] -> [to_qkv + attention core, q/k/v in LDS]
+                            -> 1x1 conv -> [channel LN + residual]
+  full attn    (:263-283)  [channel LN] -> 1x1 conv -> [attention] -> [1x1 conv + residual]
+  up-sampling  (:85-89)     nearest x2 read inside the following conv3
+  skips        (:434-452)  [interpolate + concat] in one launch
+
+No time embedding reaches the network (Unet1D.forward never passes one), and Dropout is
+the identity in eval mode.  Stage3 training is not on the HIP path: the forward raises in
+training mode instead of silently dropping the reference's dropout.
+"""
 import math
-from functools import partial
 
 import torch
 import torch.nn as nn
@@ -18,289 +26,230 @@ import torch.nn as nn
 from ..hip import fe as ops
 from ..utils import SnakeActivation
 
-
-def exists(x):
-    return x is not None
+_EPS = 1e-5  # the reference's fp32 eps for weight standardisation, LN and GroupNorm
 
 
-def default(val, d):
-    if exists(val):
-        return val
-    return d() if callable(d) else d
+def _eval_only(module):
+    if module.training:
+        raise NotImplementedError(
+            f"{type(module).__name__}: the HIP path runs the FidelityEnhancer's eval forward "
+            "(the sampler's use); Stage3 training is not on it -- call .eval()")
 
 
-class Residual(nn.Module):
-    """fidelity_enhancer.py:75-82; the add is fused into the wrapped op's last kernel."""
+class _Conv(nn.Conv1d):
+    """A Conv1d whose forward is tvq_fe_conv1d (any stride, zero or replicate padding,
+    optional nearest-x2 input, optional fused residual)."""
 
-    def __init__(self, fn):
-        super().__init__()
-        self.fn = fn
-
-    def forward(self, x, *args, **kwargs):
-        return self.fn(x, *args, residual=x, **kwargs)
-
-
-class _UpsampleConv(nn.Conv1d):
-    """Conv1d that reads its input nearest-upsampled by 2 (Upsample's two ops, :85-89)."""
-
-    def forward(self, x):
-        return ops.conv1d(x, self.weight, self.bias, padding=1, upsample2=True)
-
-
-class _Nearest2(nn.Module):
-    """nn.Upsample(scale_factor=2, mode="nearest") placeholder: parameter-free and folded
-    into the following _UpsampleConv (keeps the Sequential's key indices)."""
-
-    def forward(self, x):
-        return x
-
-
-def Upsample(dim, dim_out=None):
-    return nn.Sequential(_Nearest2(), _UpsampleConv(dim, default(dim_out, dim), 3, padding=1))
-
-
-class _Conv1d(nn.Conv1d):
-    """nn.Conv1d on the HIP path (zero or replicate padding, any stride)."""
+    def __init__(self, cin, cout, k, stride=1, pad=0, replicate=False, upsample2=False,
+                 bias=True):
+        super().__init__(cin, cout, k, stride, pad, bias=bias,
+                         padding_mode="replicate" if replicate else "zeros")
+        self._up2 = upsample2
 
     def forward(self, x, residual=None):
         return ops.conv1d(x, self.weight, self.bias, stride=self.stride[0],
-                          padding=self.padding[0], replicate=self.padding_mode == "replicate",
-                          residual=residual)
+                          padding=self.padding[0], upsample2=self._up2,
+                          replicate=self.padding_mode == "replicate", residual=residual)
 
 
-def Downsample(dim, dim_out=None):
-    return _Conv1d(dim, default(dim_out, dim), 4, 2, 1)
+class _StandardizedConv(nn.Conv1d):
+    """Weight-standardised conv3 (:96-116).  The standardised weight is recomputed only
+    when the parameter changes (its version counter moves on every in-place update)."""
 
-
-class WeightStandardizedConv2d(nn.Conv1d):
-    """fidelity_enhancer.py:96-116 (the name is the reference's; it is a Conv1d)."""
+    def __init__(self, cin, cout):
+        super().__init__(cin, cout, 3, padding=1)
 
     def forward(self, x):
-        # the standardised weight is kept until the parameter changes (its version counter
-        # moves on every in-place update: optimizer steps, load_state_dict, .to())
         key = (self.weight.data_ptr(), self.weight._version, self.weight.device)
         if getattr(self, "_ws_key", None) != key:
-            self._ws = ops.standardize_weight(self.weight, 1e-5)
+            self._ws = ops.standardize_weight(self.weight, _EPS)
             self._ws_key = key
-        return ops.conv1d(x, self._ws, self.bias, stride=self.stride[0], padding=self.padding[0])
+        return ops.conv1d(x, self._ws, self.bias, padding=1)
 
 
-class LayerNorm(nn.Module):
-    """Channel LayerNorm, gamma only (:119-127)."""
+class _Identity(nn.Module):
+    """Parameter-free slot (nearest x2 folded into the next conv; the time embedding's
+    sinusoid) that keeps the reference's container indices."""
 
-    def __init__(self, dim):
+    def forward(self, x, *args, **kwargs):
+        return x
+
+
+class _ChannelNorm(nn.Module):
+    """Channel LayerNorm with gain `g` (1, C, 1) (:119-127)."""
+
+    def __init__(self, channels):
         super().__init__()
-        self.g = nn.Parameter(torch.ones(1, dim, 1))
+        self.g = nn.Parameter(torch.ones(1, channels, 1))
 
     def forward(self, x, residual=None):
-        return ops.channel_layernorm(x, self.g, 1e-5, residual=residual)
+        return ops.channel_layernorm(x, self.g, _EPS, residual=residual)
 
 
-class PreNorm(nn.Module):
-    """:130-137"""
+class _ConvNormAct(nn.Module):
+    """conv -> GroupNorm -> Snake (-> Dropout, identity in eval) (:182-204); the unit's
+    skip add rides in the GroupNorm+Snake kernel."""
 
-    def __init__(self, dim, fn):
+    def __init__(self, cin, cout, groups, dropout):
         super().__init__()
-        self.fn = fn
-        self.norm = LayerNorm(dim)
-
-    def forward(self, x, residual=None):
-        return self.fn(self.norm(x), residual=residual)
-
-
-class SinusoidalPosEmb(nn.Module):
-    """:143-155 (time embedding; parameter-free, unused by Unet1D.forward)."""
-
-    def __init__(self, dim):
-        super().__init__()
-        self.dim = dim
-
-    def forward(self, x):
-        half_dim = self.dim // 2
-        emb = math.log(10000) / (half_dim - 1)
-        emb = torch.exp(torch.arange(half_dim, device=x.device) * -emb)
-        emb = x[:, None] * emb[None, :]
-        return torch.cat((emb.sin(), emb.cos()), dim=-1)
-
-
-class RandomOrLearnedSinusoidalPosEmb(nn.Module):
-    """:158-176 (kept for the state_dict layout of learned_sinusoidal_cond configs)."""
-
-    def __init__(self, dim, is_random=False):
-        super().__init__()
-        assert (dim % 2) == 0
-        self.weights = nn.Parameter(torch.randn(dim // 2), requires_grad=not is_random)
-
-    def forward(self, x):
-        x = x[:, None]
-        freqs = x * self.weights[None, :] * 2 * math.pi
-        return torch.cat((x, freqs.sin(), freqs.cos()), dim=-1)
-
-
-class Block(nn.Module):
-    """WS conv3 -> GroupNorm -> Snake -> Dropout (:182-204); the ResnetBlock's skip add
-    rides in the GroupNorm+Snake kernel."""
-
-    def __init__(self, dim, dim_out, groups=8, dropout=0.0):
-        super().__init__()
-        self.proj = WeightStandardizedConv2d(dim, dim_out, 3, padding=1)
-        self.norm = nn.GroupNorm(groups, dim_out)
-        self.act = SnakeActivation(dim_out, dim=1)
+        self.proj = _StandardizedConv(cin, cout)
+        self.norm = nn.GroupNorm(groups, cout)
+        self.act = SnakeActivation(cout, dim=1)
         self.dropout = nn.Dropout(dropout)
 
-    def forward(self, x, scale_shift=None, residual=None):
-        if scale_shift is not None:
-            raise NotImplementedError("Block: scale_shift (time conditioning) is not on the HIP "
-                                      "path; Unet1D.forward never passes it")
-        x = self.proj(x)
-        return ops.group_norm_snake(x, self.norm.num_groups, self.norm.weight, self.norm.bias,
-                                    self.act.a, self.norm.eps, residual=residual)
-
-
-class ResnetBlock(nn.Module):
-    """:207-231 (time_emb never passed by Unet1D.forward; the mlp exists for the keys)."""
-
-    def __init__(self, dim, dim_out, *, time_emb_dim=None, groups=8, dropout=0.0):
-        super().__init__()
-        self.mlp = (nn.Sequential(nn.SiLU(), nn.Linear(time_emb_dim, dim_out * 2))
-                    if exists(time_emb_dim) else None)
-        self.block1 = Block(dim, dim_out, groups=groups, dropout=dropout)
-        self.block2 = Block(dim_out, dim_out, groups=groups, dropout=dropout)
-        self.res_conv = _Conv1d(dim, dim_out, 1) if dim != dim_out else nn.Identity()
-
-    def forward(self, x, time_emb=None):
-        if time_emb is not None:
-            raise NotImplementedError("ResnetBlock: time_emb is not on the HIP path")
-        h = self.block1(x)
-        return self.block2(h, residual=self.res_conv(x))
-
-
-class LinearAttention(nn.Module):
-    """:234-260"""
-
-    def __init__(self, dim, heads=4, dim_head=32):
-        super().__init__()
-        self.scale = dim_head ** -0.5
-        self.heads = heads
-        self.dim_head = dim_head
-        hidden_dim = dim_head * heads
-        self.to_qkv = nn.Conv1d(dim, hidden_dim * 3, 1, bias=False)
-        self.to_out = nn.Sequential(nn.Conv1d(hidden_dim, dim, 1), LayerNorm(dim))
-
     def forward(self, x, residual=None):
-        out = ops.linear_attention_fused(x, self.to_qkv.weight, self.heads, self.dim_head)
-        conv, norm = self.to_out
-        return norm(ops.conv1d(out, conv.weight, conv.bias), residual=residual)
+        return ops.group_norm_snake(self.proj(x), self.norm.num_groups, self.norm.weight,
+                                    self.norm.bias, self.act.a, self.norm.eps,
+                                    residual=residual)
 
 
-class Attention(nn.Module):
-    """:263-283"""
+class _ResUnit(nn.Module):
+    """ResnetBlock (:207-231).  `mlp` holds the time-conditioning weights (never used by
+    the forward the reference runs; kept for the state_dict)."""
 
-    def __init__(self, dim, heads=4, dim_head=32):
+    def __init__(self, cin, cout, time_dim, groups, dropout):
         super().__init__()
-        self.scale = dim_head ** -0.5
-        self.heads = heads
-        self.dim_head = dim_head
-        hidden_dim = dim_head * heads
-        self.to_qkv = nn.Conv1d(dim, hidden_dim * 3, 1, bias=False)
-        self.to_out = nn.Conv1d(hidden_dim, dim, 1)
+        self.mlp = nn.Sequential(nn.SiLU(), nn.Linear(time_dim, 2 * cout))
+        self.block1 = _ConvNormAct(cin, cout, groups, dropout)
+        self.block2 = _ConvNormAct(cout, cout, groups, dropout)
+        self.res_conv = _Conv(cin, cout, 1) if cin != cout else _Identity()
 
-    def forward(self, x, residual=None):
-        qkv = ops.conv1d(x, self.to_qkv.weight)
-        out = ops.attention(qkv, self.heads, self.dim_head)
-        return ops.conv1d(out, self.to_out.weight, self.to_out.bias, residual=residual)
+    def forward(self, x):
+        return self.block2(self.block1(x), residual=self.res_conv(x))
+
+
+class _LinearAttnCore(nn.Module):
+    """to_qkv / to_out of LinearAttention (:234-260): 4 heads of 32."""
+
+    def __init__(self, channels, heads=4, dim_head=32):
+        super().__init__()
+        self.heads, self.dim_head = heads, dim_head
+        self.to_qkv = nn.Conv1d(channels, 3 * heads * dim_head, 1, bias=False)
+        self.to_out = nn.Sequential(nn.Conv1d(heads * dim_head, channels, 1),
+                                    _ChannelNorm(channels))
+
+    def forward(self, xn, residual):
+        att = ops.linear_attention_fused(xn, self.to_qkv.weight, self.heads, self.dim_head)
+        proj, norm = self.to_out
+        return norm(ops.conv1d(att, proj.weight, proj.bias), residual=residual)
+
+
+class _FullAttnCore(nn.Module):
+    """to_qkv / to_out of Attention (:263-283): 4 heads of 32, exact softmax."""
+
+    def __init__(self, channels, heads=4, dim_head=32):
+        super().__init__()
+        self.heads, self.dim_head = heads, dim_head
+        self.to_qkv = nn.Conv1d(channels, 3 * heads * dim_head, 1, bias=False)
+        self.to_out = nn.Conv1d(heads * dim_head, channels, 1)
+
+    def forward(self, xn, residual):
+        att = ops.attention(ops.conv1d(xn, self.to_qkv.weight), self.heads, self.dim_head)
+        return ops.conv1d(att, self.to_out.weight, self.to_out.bias, residual=residual)
+
+
+class _NormedResidual(nn.Module):
+    """Residual(PreNorm(core)) (:75-82, :130-137) as one module: `fn.norm`, `fn.fn`."""
+
+    class _Pre(nn.Module):
+        def __init__(self, channels, core):
+            super().__init__()
+            self.fn = core
+            self.norm = _ChannelNorm(channels)
+
+    def __init__(self, channels, core):
+        super().__init__()
+        self.fn = self._Pre(channels, core)
+
+    def forward(self, x):
+        return self.fn.fn(self.fn.norm(x), residual=x)
+
+
+class _TimeFourier(nn.Module):
+    """Learned / random Fourier features of the time embedding (:158-176); present only
+    for configs with learned_sinusoidal_cond, for their `weights` key."""
+
+    def __init__(self, dim, frozen):
+        super().__init__()
+        self.weights = nn.Parameter(torch.randn(dim // 2), requires_grad=not frozen)
+
+    def forward(self, t):
+        f = t[:, None] * self.weights[None, :] * (2 * math.pi)
+        return torch.cat((t[:, None], f.sin(), f.cos()), dim=-1)
+
+
+def _upsampler(cin, cout):
+    """Upsample (:85-89): [nearest x2 (folded), conv3 reading the upsampled input]."""
+    return nn.Sequential(_Identity(), _Conv(cin, cout, 3, pad=1, upsample2=True))
 
 
 class Unet1D(nn.Module):
-    """:289-455, same constructor and module tree."""
+    """Reference constructor signature (:289-304); the layer plan is derived from `dims`
+    level by level (encoder: two ResNet units, linear attention, stride-2 conv4 or a conv3 at
+    the last level; decoder mirrored with concatenated skips and x2 up-sampling)."""
 
     def __init__(self, dim, init_dim=None, out_dim=None, dim_mults=(1, 2, 4, 8), channels=1,
                  self_condition=False, resnet_block_groups=8, learned_variance=False,
                  learned_sinusoidal_cond=False, random_fourier_features=False,
                  learned_sinusoidal_dim=16, dropout: float = 0.0, **kwargs):
         super().__init__()
-        self.channels = channels
-        self.self_condition = self_condition
-        input_channels = channels * (2 if self_condition else 1)
-        init_dim = default(init_dim, dim)
-        self.init_conv = _Conv1d(input_channels, init_dim, 7, padding=3)
-        dims = [init_dim, *map(lambda m: dim * m, dim_mults)]
-        in_out = list(zip(dims[:-1], dims[1:]))
-        block_klass = partial(ResnetBlock, groups=resnet_block_groups, dropout=dropout)
-        time_dim = dim * 4
-        self.random_or_learned_sinusoidal_cond = learned_sinusoidal_cond or random_fourier_features
-        if self.random_or_learned_sinusoidal_cond:
-            sinu_pos_emb = RandomOrLearnedSinusoidalPosEmb(learned_sinusoidal_dim,
-                                                           random_fourier_features)
-            fourier_dim = learned_sinusoidal_dim + 1
-        else:
-            sinu_pos_emb = SinusoidalPosEmb(dim)
-            fourier_dim = dim
-        self.time_mlp = nn.Sequential(sinu_pos_emb, nn.Linear(fourier_dim, time_dim), nn.GELU(),
-                                      nn.Linear(time_dim, time_dim))
-        self.downs = nn.ModuleList([])
-        self.ups = nn.ModuleList([])
-        num_resolutions = len(in_out)
-        for ind, (dim_in, dim_out) in enumerate(in_out):
-            is_last = ind >= (num_resolutions - 1)
-            self.downs.append(nn.ModuleList([
-                block_klass(dim_in, dim_in, time_emb_dim=time_dim),
-                block_klass(dim_in, dim_in, time_emb_dim=time_dim),
-                Residual(PreNorm(dim_in, LinearAttention(dim_in))),
-                Downsample(dim_in, dim_out) if not is_last else _Conv1d(dim_in, dim_out, 3, padding=1),
-            ]))
-        mid_dim = dims[-1]
-        self.mid_block1 = block_klass(mid_dim, mid_dim, time_emb_dim=time_dim)
-        self.mid_attn = Residual(PreNorm(mid_dim, Attention(mid_dim)))
-        self.mid_block2 = block_klass(mid_dim, mid_dim, time_emb_dim=time_dim)
-        for ind, (dim_in, dim_out) in enumerate(reversed(in_out)):
-            is_last = ind == (len(in_out) - 1)
-            self.ups.append(nn.ModuleList([
-                block_klass(dim_out + dim_in, dim_out, time_emb_dim=time_dim),
-                block_klass(dim_out + dim_in, dim_out, time_emb_dim=time_dim),
-                Residual(PreNorm(dim_out, LinearAttention(dim_out))),
-                Upsample(dim_out, dim_in) if not is_last else _Conv1d(dim_out, dim_in, 3, padding=1),
-            ]))
-        self.last_up = Upsample(dim_in, dim_in)
-        default_out_dim = channels * (1 if not learned_variance else 2)
-        self.out_dim = default(out_dim, default_out_dim)
-        self.final_res_block = block_klass(dim * 2, dim, time_emb_dim=time_dim)
+        self.channels, self.self_condition = channels, self_condition
+        init_dim = dim if init_dim is None else init_dim
+        widths = [init_dim] + [dim * m for m in dim_mults]
+        pairs = list(zip(widths[:-1], widths[1:]))
+        tdim = 4 * dim
+        unit = lambda cin, cout: _ResUnit(cin, cout, tdim, resnet_block_groups, dropout)  # noqa: E731
+
+        self.init_conv = _Conv(channels * (2 if self_condition else 1), init_dim, 7, pad=3)
+        fourier = learned_sinusoidal_cond or random_fourier_features
+        self.random_or_learned_sinusoidal_cond = fourier
+        emb, emb_dim = ((_TimeFourier(learned_sinusoidal_dim, random_fourier_features),
+                         learned_sinusoidal_dim + 1) if fourier else (_Identity(), dim))
+        self.time_mlp = nn.Sequential(emb, nn.Linear(emb_dim, tdim), nn.GELU(),
+                                      nn.Linear(tdim, tdim))
+
+        last = len(pairs) - 1
+        self.downs = nn.ModuleList(
+            nn.ModuleList([unit(a, a), unit(a, a), _NormedResidual(a, _LinearAttnCore(a)),
+                           _Conv(a, b, 4, 2, 1) if lvl < last else _Conv(a, b, 3, pad=1)])
+            for lvl, (a, b) in enumerate(pairs))
+        mid = widths[-1]
+        self.mid_block1 = unit(mid, mid)
+        self.mid_attn = _NormedResidual(mid, _FullAttnCore(mid))
+        self.mid_block2 = unit(mid, mid)
+        self.ups = nn.ModuleList(
+            nn.ModuleList([unit(b + a, b), unit(b + a, b), _NormedResidual(b, _LinearAttnCore(b)),
+                           _upsampler(b, a) if lvl < last else _Conv(b, a, 3, pad=1)])
+            for lvl, (a, b) in enumerate(reversed(pairs)))
+        self.last_up = _upsampler(pairs[0][0], pairs[0][0])
+        self.out_dim = out_dim if out_dim is not None else channels * (2 if learned_variance else 1)
+        self.final_res_block = unit(2 * dim, dim)
         self.final_conv = nn.Sequential(
-            _Conv1d(dim, self.out_dim, kernel_size=1),
-            _Conv1d(self.out_dim, self.out_dim, kernel_size=3, padding=1, padding_mode="replicate"),
-            _Conv1d(self.out_dim, self.out_dim, kernel_size=3, padding=1, padding_mode="replicate"),
-        )
+            _Conv(dim, self.out_dim, 1),
+            _Conv(self.out_dim, self.out_dim, 3, pad=1, replicate=True),
+            _Conv(self.out_dim, self.out_dim, 3, pad=1, replicate=True))
 
     def forward(self, x):
-        if self.training:
-            raise NotImplementedError(
-                "Unet1D: the HIP path implements the eval forward (the sampler's use); "
-                "Stage3 training of the FidelityEnhancer is not on it (call .eval())")
+        _eval_only(self)
         x = self.init_conv(x)
-        r = x
-        h = []
-        for block1, block2, attn, downsample in self.downs:
-            x = block1(x)
-            h.append(x)
-            x = block2(x)
-            x = attn(x)
-            h.append(x)
-            x = downsample(x)
-        x = self.mid_block1(x)
-        x = self.mid_attn(x)
-        x = self.mid_block2(x)
-        for block1, block2, attn, upsample in self.ups:
-            x = block1(ops.cat_interp(x, h.pop(), x.shape[-1]))
-            x = block2(ops.cat_interp(x, h.pop(), x.shape[-1]))
-            x = attn(x)
-            x = upsample(x)
-        x = self.last_up(x)
-        x = self.final_res_block(ops.cat_interp(x, r, r.shape[-1]))
+        stem, skips = x, []
+        for res1, res2, attn, down in self.downs:
+            x = res1(x)
+            skips.append(x)
+            x = attn(res2(x))
+            skips.append(x)
+            x = down(x)
+        x = self.mid_block2(self.mid_attn(self.mid_block1(x)))
+        for res1, res2, attn, up in self.ups:
+            x = res1(ops.cat_interp(x, skips.pop(), x.shape[-1]))
+            x = res2(ops.cat_interp(x, skips.pop(), x.shape[-1]))
+            x = up(attn(x))
+        x = self.final_res_block(ops.cat_interp(self.last_up(x), stem, stem.shape[-1]))
         return self.final_conv(x)
 
 
 class FidelityEnhancer(nn.Module):
-    """fidelity_enhancer.py:458-498: interpolate x_a to input_length, then the Unet1D."""
+    """x_a (b, c, l) -> refined (b, c, input_length) (:458-498)."""
 
     def __init__(self, input_length, in_channels, config):
         super().__init__()
@@ -310,7 +259,6 @@ class FidelityEnhancer(nn.Module):
 
     @torch.no_grad()
     def forward(self, x_a):
-        """x_a (b, c, l) -> (b, c, input_length)."""
         x_a = x_a.float()
         if x_a.shape[-1] != self.input_length:
             x_a = ops.cat_interp(x_a, None, self.input_length)
