@@ -29,30 +29,64 @@ def _a(snake_mod):
     return snake_mod.a  # the (1,C,1,1) Parameter: kernels read it flat, grads land in .grad
 
 
+def _no_freq_indep(flag):
+    if flag:
+        raise NotImplementedError("frequency_indepence=True is not on the path (stage1.py:42)")
+
+
+def _conv3x3(cin, cout):
+    return nn.Conv2d(cin, cout, kernel_size=(3, 3), stride=(1, 1), padding=(1, 1))
+
+
+def _strided_block(conv, cout, dropout):
+    """[conv (3x4, stride (1,2)), BN, Snake, Dropout] as EncBlock / DecBlock hold it."""
+    return nn.Sequential(conv, nn.BatchNorm2d(cout), SnakeActivation(cout, 2), nn.Dropout(dropout))
+
+
+def _n_levels(downsample_rate):
+    return int(round(np.log2(downsample_rate)))
+
+
+def _encoder_plan(init_dim, hid_dim, num_channels, downsample_rate, n_res):
+    """(kind, cin, cout) per layer of VQVAEEncoder.encoder (vq_vae.py:143-170): a strided
+    block per octave of the rate, n_res ResBlocks after every one but the first, then the
+    ResBlock into hid_dim."""
+    plan, width = [("down", num_channels, init_dim)], init_dim
+    for _ in range(_n_levels(downsample_rate) - 1):
+        plan.append(("down", width, 2 * width))
+        width *= 2
+        plan += [("res", width, width)] * n_res
+    return plan + [("res", width, hid_dim)]
+
+
+def _decoder_plan(init_dim, hid_dim, num_channels, downsample_rate, n_res):
+    """(kind, cin, cout) per layer of VQVAEDecoder.decoder (vq_vae.py:211-251): ResBlock out
+    of hid_dim, then per octave n_res ResBlocks and a transposed strided block halving the
+    width, then two transposed convs to num_channels."""
+    lv = _n_levels(downsample_rate)
+    width = int(init_dim * 2 ** (lv - 1)) if lv != 0 else int(init_dim)
+    plan = [("res", hid_dim, width)]
+    for _ in range(lv - 1):
+        plan += [("res", width, width)] * n_res
+        plan.append(("up", width, width // 2))
+        width //= 2
+    return plan + [("convT", width, num_channels), ("convT", num_channels, num_channels)]
+
+
 class ResBlock(nn.Module):
     """vq_vae.py:13-62."""
 
     def __init__(self, in_channels, out_channels, frequency_indepence: bool, mid_channels=None,
                  dropout: float = 0.0):
         super().__init__()
-        if frequency_indepence:
-            raise NotImplementedError("frequency_indepence=True is not on the path (stage1.py:42)")
-        if mid_channels is None:
-            mid_channels = out_channels
-        kernel_size, padding = (3, 3), (1, 1)
-        layers = [
-            SnakeActivation(in_channels, 2),
-            nn.Conv2d(in_channels, mid_channels, kernel_size=kernel_size, stride=(1, 1),
-                      padding=padding),
-            nn.BatchNorm2d(out_channels),
-            SnakeActivation(out_channels, 2),
-            nn.Conv2d(mid_channels, out_channels, kernel_size=kernel_size, stride=(1, 1),
-                      padding=padding),
-            nn.Dropout(dropout),
-        ]
-        self.convs = nn.Sequential(*layers)
-        self.proj = (nn.Identity() if in_channels == out_channels
-                     else nn.Conv2d(in_channels, out_channels, kernel_size=1))
+        _no_freq_indep(frequency_indepence)
+        mid = out_channels if mid_channels is None else mid_channels
+        # convs: [Snake(in), conv3x3 in->mid, BN(out), Snake(out), conv3x3 mid->out, Dropout]
+        self.convs = nn.Sequential(
+            SnakeActivation(in_channels, 2), _conv3x3(in_channels, mid), nn.BatchNorm2d(out_channels),
+            SnakeActivation(out_channels, 2), _conv3x3(mid, out_channels), nn.Dropout(dropout))
+        self.proj = (nn.Conv2d(in_channels, out_channels, kernel_size=1)
+                     if in_channels != out_channels else nn.Identity())
         self._site = rng.new_site()
 
     def forward(self, x):
@@ -70,15 +104,10 @@ class VQVAEEncBlock(nn.Module):
 
     def __init__(self, in_channels, out_channels, frequency_indepence: bool, dropout: float = 0.0):
         super().__init__()
-        if frequency_indepence:
-            raise NotImplementedError("frequency_indepence=True is not on the path")
-        self.block = nn.Sequential(
-            nn.Conv2d(in_channels, out_channels, kernel_size=(3, 4), stride=(1, 2),
-                      padding=(1, 1), padding_mode="replicate"),
-            nn.BatchNorm2d(out_channels),
-            SnakeActivation(out_channels, 2),
-            nn.Dropout(dropout),
-        )
+        _no_freq_indep(frequency_indepence)
+        self.block = _strided_block(
+            nn.Conv2d(in_channels, out_channels, (3, 4), (1, 2), (1, 1), padding_mode="replicate"),
+            out_channels, dropout)
 
     def forward(self, x):
         b = self.block
@@ -93,15 +122,9 @@ class VQVAEDecBlock(nn.Module):
 
     def __init__(self, in_channels, out_channels, frequency_indepence: bool, dropout: float = 0.0):
         super().__init__()
-        if frequency_indepence:
-            raise NotImplementedError("frequency_indepence=True is not on the path")
-        self.block = nn.Sequential(
-            nn.ConvTranspose2d(in_channels, out_channels, kernel_size=(3, 4), stride=(1, 2),
-                               padding=(1, 1)),
-            nn.BatchNorm2d(out_channels),
-            SnakeActivation(out_channels, 2),
-            nn.Dropout(dropout),
-        )
+        _no_freq_indep(frequency_indepence)
+        self.block = _strided_block(nn.ConvTranspose2d(in_channels, out_channels, (3, 4), (1, 2), (1, 1)),
+                                    out_channels, dropout)
 
     def forward(self, x):
         b = self.block
@@ -123,16 +146,11 @@ class VQVAEEncoder(nn.Module):
         self.pad_func = pad_func
         self.band = band_of(pad_func)
         self.n_fft = n_fft
-        d = init_dim
-        enc_layers = [VQVAEEncBlock(num_channels, d, frequency_indepence)]
-        d *= 2
-        for _ in range(int(round(np.log2(downsample_rate))) - 1):
-            enc_layers.append(VQVAEEncBlock(d // 2, d, frequency_indepence))
-            for _ in range(n_resnet_blocks):
-                enc_layers.append(ResBlock(d, d, frequency_indepence, dropout=dropout))
-            d *= 2
-        enc_layers.append(ResBlock(d // 2, hid_dim, frequency_indepence, dropout=dropout))
-        self.encoder = nn.Sequential(*enc_layers)
+        self.encoder = nn.Sequential(*(
+            VQVAEEncBlock(cin, cout, frequency_indepence) if kind == "down"
+            else ResBlock(cin, cout, frequency_indepence, dropout=dropout)
+            for kind, cin, cout in _encoder_plan(init_dim, hid_dim, num_channels,
+                                                 downsample_rate, n_resnet_blocks)))
         self.is_num_tokens_updated = False
         self.register_buffer("num_tokens", torch.tensor(0))
         self.register_buffer("H_prime", torch.tensor(0))
@@ -171,21 +189,12 @@ class VQVAEDecoder(nn.Module):
         self.n_fft = n_fft
         self.x_channels = x_channels
         self.input_length = input_length
-        kernel_size, padding = (3, 4), (1, 1)
-        d = int(init_dim * 2 ** (int(round(np.log2(downsample_rate))) - 1))
-        if round(np.log2(downsample_rate)) == 0:
-            d = int(init_dim * 2 ** (int(round(np.log2(downsample_rate)))))
-        dec_layers = [ResBlock(hid_dim, d, frequency_indepence, dropout=dropout)]
-        for _ in range(int(round(np.log2(downsample_rate))) - 1):
-            for _ in range(n_resnet_blocks):
-                dec_layers.append(ResBlock(d, d, frequency_indepence, dropout=dropout))
-            d //= 2
-            dec_layers.append(VQVAEDecBlock(2 * d, d, frequency_indepence))
-        dec_layers.append(nn.ConvTranspose2d(d, num_channels, kernel_size=kernel_size,
-                                             stride=(1, 2), padding=padding))
-        dec_layers.append(nn.ConvTranspose2d(num_channels, num_channels, kernel_size=kernel_size,
-                                             stride=(1, 2), padding=padding))
-        self.decoder = nn.Sequential(*dec_layers)
+        make = {"res": lambda a, b: ResBlock(a, b, frequency_indepence, dropout=dropout),
+                "up": lambda a, b: VQVAEDecBlock(a, b, frequency_indepence),
+                "convT": lambda a, b: nn.ConvTranspose2d(a, b, (3, 4), (1, 2), (1, 1))}
+        self.decoder = nn.Sequential(*(
+            make[kind](cin, cout) for kind, cin, cout in _decoder_plan(
+                init_dim, hid_dim, num_channels, downsample_rate, n_resnet_blocks)))
         self.interp = nn.Upsample(input_length, mode="linear")
         self.linear = nn.Linear(input_length, input_length)
 

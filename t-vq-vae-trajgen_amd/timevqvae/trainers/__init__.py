@@ -1,3 +1,4 @@
+"""Lightning-free Stage1 / Stage2 trainers over the HIP modules (reference trainers/)."""
 from .stage1 import Stage1
 from .stage2 import Stage2
 
