@@ -100,9 +100,14 @@ class JointTrainer:
         self.packs = PackCache(device) if os.environ.get("TVQ_PACK_CACHE", "1") != "0" else None
 
     def _allreduce(self, opt):
+        """DP exchange: mean of the flat gradients; the layer-dropout gates (which
+        parameter segments some replica's forward used) are OR-ed (MAX), so every replica
+        updates the same segments and the replicas stay identical."""
         if self.world > 1:
             dist.all_reduce(opt.flat_grad)
             opt.flat_grad.mul_(1.0 / self.world)
+            if opt.has_gates:
+                dist.all_reduce(opt.gates, op=dist.ReduceOp.MAX)
 
     def _fwd_bwd(self, batch, defer):
         """zero_grad, then stage1's LF and HF bands (forward+backward, one side stream
@@ -132,10 +137,10 @@ class JointTrainer:
         from timevqvae.hip import rng
         rng.advance(self.device)
         out1, out2, _ = self._fwd_bwd(batch, defer=False)
-        self._allreduce(self.opt1)
-        self._allreduce(self.opt2)
-        self.opt1.step()
-        self.opt2.step()
+        for opt in (self.opt1, self.opt2):
+            opt.gather_gates()
+            self._allreduce(opt)
+            opt.step(gates_ready=True)
         return out1, out2
 
     def capture(self, batch):
@@ -154,7 +159,9 @@ class JointTrainer:
 
         def seg1():
             rng.advance(self.device)
-            out1, out2, self._pending = self._fwd_bwd(batch, defer)
+            out1, out2, self._pending = self._fwd_bwd(batch, defer)  # streams joined
+            self.opt1.gather_gates()
+            self.opt2.gather_gates()
             return out1, out2
 
         def between1():
@@ -166,8 +173,8 @@ class JointTrainer:
         def seg2():
             for u in self._pending:
                 u.apply()
-            self.opt1.step(lr_on_device=True)
-            self.opt2.step(lr_on_device=True)
+            self.opt1.step(lr_on_device=True, gates_ready=True)
+            self.opt2.step(lr_on_device=True, gates_ready=True)
 
         self.graph = StepGraph([seg1, seg2], [between1, None], warmup=2, before=before).capture()
 

@@ -39,6 +39,10 @@ int tvq_abi_version(void);
  * zero.  Without a pool, those reductions use a separate finishing launch (same
  * result).  Call before the first launch on that device, outside graph capture. */
 int tvq_counter_pool(int64_t device, int32_t* zeroed, int64_t n);
+/* Bracket a hipGraph capture (begin = 1 / 0): slots taken inside are pinned for the
+ * process lifetime (a graph replays with its capture-time slots), taken from the top
+ * half of the pool, which eager launches never use. */
+int tvq_counter_capture(int64_t begin);
 
 /* ---------------------------------------------------------------- VQ codebook
  * Replaces EuclideanCodebook.forward (timevqvae/models/vq.py:197-251) and the
@@ -267,13 +271,30 @@ int tvq_loss_fwd(const float* input, const float* target, int64_t n, int64_t kin
                  float* workspace, tvq_stream_t stream);
 int tvq_loss_bwd(const float* input, const float* target, int64_t n, int64_t kind,
                  const float* gout, float* dtarget, tvq_stream_t stream);
-/* torch.optim.AdamW step over a flat buffer (stage1.py:230, stage2.py:113);
- * lr_step = device {lr, step}; tvq_adamw_begin increments step and writes lr when
- * lr >= 0 (pass -1 inside a captured graph and set lr[0] before each replay). */
-int tvq_adamw_begin(float* lr_step, float lr, tvq_stream_t stream);
-int tvq_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
-              const float* lr_step, float beta1, float beta2, float eps, float weight_decay,
+/* torch.optim.AdamW step over a flat buffer (stage1.py:230, stage2.py:113) holding
+ * nseg parameter segments.  torch skips a parameter whose .grad is None (Lightning
+ * zero_grad(set_to_none=True); x-transformers layer dropout leaves a skipped branch
+ * without grads, bidirectional_transformer.py:104-108) and keeps state['step'] per
+ * parameter, so each segment has a gate and its own step count:
+ *   tvq_adamw_gates: gates[s] = (*gate_ptrs[s] != 0) (gate_ptrs[s] = 0: always 1);
+ *   tvq_adamw_begin: lr_step = device {lr, step}: writes lr when lr >= 0 (pass -1 inside
+ *     a captured graph and set lr[0] before each replay), counts the step, and
+ *     seg_step[s] += 1 where gates[s] != 0;
+ *   tvq_adamw: chunks = int64 [nchunks][3] {start, len <= tvq_adamw_chunk(), segment};
+ *     segments with gates[s] == 0 are left untouched. */
+int64_t tvq_adamw_chunk(void);
+int tvq_adamw_gates(const int64_t* gate_ptrs, int64_t nseg, float* gates, tvq_stream_t stream);
+int tvq_adamw_begin(float* lr_step, float lr, const float* gates, float* seg_step, int64_t nseg,
+                    tvq_stream_t stream);
+int tvq_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+              const int64_t* chunks, int64_t nchunks, const float* lr_step, const float* gates,
+              const float* seg_step, float beta1, float beta2, float eps, float weight_decay,
               tvq_stream_t stream);
+/* x-transformers layer dropout (random() < p skips a branch) drawn on the device for
+ * n <= 256 branches: keep[i] = U(seed, offset, i) >= p; touched[i] = keep[i], or
+ * max(touched[i], keep[i]) when accumulate (a second pass of the prior in one step). */
+int tvq_layer_drop(const int64_t* seed_ptr, uint64_t offset, float p, int64_t n, float* keep,
+                   float* touched, int64_t accumulate, tvq_stream_t stream);
 
 /* ------------------------------------------------ MaskGIT transformer
  * x-transformers internals used by BidirectionalTransformer
@@ -324,9 +345,10 @@ int tvq_masked_ce_bwd(const float* logits, int64_t ldl, int64_t M, int64_t K,
                       const float* stats, const float* gout, float* dlogits, int64_t ldd,
                       tvq_stream_t stream);
 /* MaskGIT._randomly_mask_tokens (maskgit.py:194-216) on device: cosine schedule,
- * per-row top-k of U[0,1) scores; ratio/rand may be given (testing) or NULL (device RNG). */
+ * per-row top-k of U[0,1) scores; ratio (float64, as np.random.uniform draws it) / rand
+ * may be given (testing) or NULL (device RNG). */
 int tvq_mask_tokens(const int64_t* s, int64_t B, int64_t n, int64_t mask_id,
-                    const int64_t* seed_ptr, uint64_t offset, const float* ratio,
+                    const int64_t* seed_ptr, uint64_t offset, const double* ratio,
                     const float* rand, int64_t* s_M, bool* keep, tvq_stream_t stream);
 /* Upscale's F.interpolate(mode='nearest') (bidirectional_transformer.py:27) and GELU. */
 int tvq_upsample_nearest(const float* x, int64_t R, int64_t Lin, int64_t Lout, float* y,

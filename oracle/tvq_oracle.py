@@ -374,13 +374,15 @@ def sample_step(logits, s, mask_token_id, t, T, unknown0, temperature, u_cat, u_
     """One iteration of first_pass/second_pass (maskgit.py:302-346) with injected noise.
 
     Categorical sampling by inverse CDF of softmax(logits) at u_cat (b,n) (double softmax and
-    prefix: the first code whose CDF reaches u); Gumbel noise -log(-log(u_gumbel)).  The
-    mask length is floor(unknown0 * gamma(ratio)) in float32 as in the reference.  Returns
-    the re-masked token set.
+    prefix: the first code whose CDF exceeds u, so a zero-probability code is never
+    drawn, as torch's Categorical); Gumbel noise -log(-log(u_gumbel)).  The mask length is
+    floor(unknown0 * gamma(ratio)) in float32 as in the reference.  Returns the re-masked
+    token set.
     """
     probs = F.softmax(logits.double(), dim=-1)
     cdf = torch.cumsum(probs, dim=-1)
-    sampled = torch.searchsorted(cdf, u_cat.double().unsqueeze(-1) * cdf[..., -1:]).squeeze(-1)
+    sampled = torch.searchsorted(cdf, u_cat.double().unsqueeze(-1) * cdf[..., -1:],
+                                 right=True).squeeze(-1)
     sampled = sampled.clamp(max=logits.shape[-1] - 1)
     unknown = s == mask_token_id
     sampled = torch.where(unknown, sampled, s)

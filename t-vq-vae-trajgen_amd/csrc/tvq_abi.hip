@@ -18,10 +18,15 @@ void set_error(const char* fmt, ...) {
 }
 
 namespace {
+// Eager launches take slots round robin from [0, lo); slots handed out while a hipGraph
+// is being captured (tvq_counter_capture) come from the top of the pool, [lo, n), and are
+// never handed out again: a captured graph keeps its slots for every replay, so the
+// eager cursor (or another capture) must never share one with a live graph node.
 struct CounterPool {
   int* base = nullptr;
-  int64_t n = 0, cur = 0;
+  int64_t n = 0, cur = 0, lo = 0;
 };
+int g_capture_depth = 0;
 constexpr int kMaxDevices = 64;
 CounterPool g_pools[kMaxDevices];
 std::mutex g_pool_mu;
@@ -49,13 +54,27 @@ int* counters(int64_t k, FinishClass cls) {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
   std::lock_guard<std::mutex> lock(g_pool_mu);
   CounterPool& p = g_pools[dev];
-  if (!p.base || k > p.n) return nullptr;
-  if (p.cur + k > p.n) p.cur = 0;
+  if (!p.base) return nullptr;
+  if (g_capture_depth > 0) {  // pinned for the graph's lifetime
+    if (p.lo - k < p.n / 2) return nullptr;  // keep half the pool for eager launches
+    p.lo -= k;
+    if (p.cur > p.lo) p.cur = 0;
+    return p.base + p.lo;
+  }
+  if (k > p.lo) return nullptr;  // the caller falls back to a separate finishing launch
+  if (p.cur + k > p.lo) p.cur = 0;
   int* r = p.base + p.cur;
   p.cur += k;
   return r;
 }
 }  // namespace tvq
+
+extern "C" int tvq_counter_capture(int64_t begin) {
+  std::lock_guard<std::mutex> lock(tvq::g_pool_mu);
+  tvq::g_capture_depth += begin ? 1 : -1;
+  if (tvq::g_capture_depth < 0) tvq::g_capture_depth = 0;
+  return TVQ_OK;
+}
 
 extern "C" int tvq_counter_pool(int64_t device, int32_t* zeroed, int64_t n) {
   TVQ_CHECK_ARG(device >= 0 && device < tvq::kMaxDevices && (zeroed || n == 0) && n >= 0,
@@ -64,6 +83,7 @@ extern "C" int tvq_counter_pool(int64_t device, int32_t* zeroed, int64_t n) {
   tvq::g_pools[device].base = zeroed;
   tvq::g_pools[device].n = n;
   tvq::g_pools[device].cur = 0;
+  tvq::g_pools[device].lo = n;
   return TVQ_OK;
 }
 

@@ -54,7 +54,8 @@ __global__ __launch_bounds__(256) void maskgit_sample_kernel(
     const double tot = wave_sum_dd(part);
     const float totf = wave_sum(partf);
     // inclusive prefix of the lane chunks (probabilities), then the first chunk whose
-    // running sum reaches v = u * total
+    // running sum exceeds v = u * total (strictly: at u = 0 a leading zero-probability
+    // code must not be drawn; torch's Categorical never samples one)
     double incl = part / tot;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -64,14 +65,14 @@ __global__ __launch_bounds__(256) void maskgit_sample_kernel(
     const double cdf_last = __shfl(incl, 63, 64);
     const float u = u_cat ? u_cat[t] : uniform01(seed, (uint64_t)t);
     const double v = (double)u * cdf_last;
-    const unsigned long long hit = __ballot(incl >= v);
+    const unsigned long long hit = __ballot(incl > v);
     const int src = hit ? __ffsll(hit) - 1 : 63;
     int pick = min(K, j0 + per) - 1;  // rounding fallback: the chunk's last code
     if (lane == src) {
       double acc = incl - part / tot;
       for (int j = j0; j < min(K, j0 + per); ++j) {
         acc += exp((double)l[j] - (double)m) / tot;
-        if (acc >= v) {
+        if (acc > v) {
           pick = j;
           break;
         }

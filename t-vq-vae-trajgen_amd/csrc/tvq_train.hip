@@ -48,20 +48,34 @@ __global__ void loss_bwd_kernel(const float* __restrict__ input, const float* __
   }
 }
 
-__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
-                             float* __restrict__ m, float* __restrict__ v, int64_t n,
-                             const float* __restrict__ lr_step, float b1, float b2, float eps,
-                             float wd) {
+// One block per chunk of one parameter segment (chunk = {start, len, segment}).  A
+// segment whose gate is 0 this step is skipped whole: torch.optim.AdamW leaves a
+// parameter whose .grad is None untouched (no decay, no moment update, no step count),
+// which is what x-transformers' layer dropout produces for a skipped branch.
+constexpr int ADAMW_CHUNK = 4096;
+
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p,
+                                                    const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    const int64_t* __restrict__ chunks,
+                                                    const float* __restrict__ lr_step,
+                                                    const float* __restrict__ gates,
+                                                    const float* __restrict__ seg_step, float b1,
+                                                    float b2, float eps, float wd) {
+  const int64_t start = chunks[3 * blockIdx.x];
+  const int len = (int)chunks[3 * blockIdx.x + 1];
+  const int seg = (int)chunks[3 * blockIdx.x + 2];
+  if (gates[seg] == 0.f) return;
   const double lr = lr_step[0];
-  const double t = lr_step[1];
+  const double t = seg_step[seg];
   const double bc1 = 1.0 - pow((double)b1, t);
   const double bc2 = 1.0 - pow((double)b2, t);
   const float step_size = (float)(lr / bc1);
   const float bc2s = (float)sqrt(bc2);
   const float decay = (float)(1.0 - lr * (double)wd);
   const float w1 = 1.0f - b1, w2 = 1.0f - b2;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  for (int j = threadIdx.x; j < len; j += 256) {
+    const int64_t i = start + j;
     const float gi = g[i];
     float pi = p[i] * decay;
     float mi = m[i];
@@ -75,9 +89,40 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   }
 }
 
-__global__ void adamw_begin_kernel(float* __restrict__ lr_step, float lr) {
-  if (lr >= 0.f) lr_step[0] = lr;
-  lr_step[1] += 1.0f;
+// gates[s] = *gate_ptr[s] (1 where the segment has no gate); then the per-segment step
+// counts advance where the gate is set (torch keeps state['step'] per parameter)
+__global__ void adamw_gates_kernel(const int64_t* __restrict__ gate_ptrs, int64_t nseg,
+                                   float* __restrict__ gates) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < nseg;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const float* gp = (const float*)gate_ptrs[s];
+    gates[s] = gp ? (*gp != 0.f ? 1.f : 0.f) : 1.f;
+  }
+}
+
+__global__ void adamw_begin_kernel(float* __restrict__ lr_step, float lr,
+                                   const float* __restrict__ gates, float* __restrict__ seg_step,
+                                   int64_t nseg) {
+  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (s == 0) {
+    if (lr >= 0.f) lr_step[0] = lr;
+    lr_step[1] += 1.0f;
+  }
+  if (s < nseg && gates[s] != 0.f) seg_step[s] += 1.0f;
+}
+
+// layer-dropout decisions of one x-transformers layer stack (random() < p skips a
+// branch): keep[i] = U(seed, offset, i) >= p; touched[i] = keep[i] (first pass of the
+// step) or max(touched[i], keep[i]) (a later pass: CFG runs the prior twice)
+__global__ void layer_drop_kernel(const int64_t* seed_ptr, uint64_t offset, float p, int n,
+                                  float* __restrict__ keep, float* __restrict__ touched,
+                                  int accumulate) {
+  const int i = threadIdx.x;
+  if (i >= n) return;
+  const uint64_t seed = mix_seed(seed_ptr, offset);
+  const float k = uniform01(seed, (uint64_t)i) >= p ? 1.f : 0.f;
+  keep[i] = k;
+  touched[i] = accumulate ? fmaxf(touched[i], k) : k;
 }
 
 static int blocks_for(int64_t n, int cap) {
@@ -112,21 +157,45 @@ extern "C" int tvq_loss_bwd(const float* input, const float* target, int64_t n, 
   return launch_status("tvq_loss_bwd");
 }
 
-// lr_step: device float[2] = {lr, step}; tvq_adamw_begin sets lr and increments step.
-extern "C" int tvq_adamw_begin(float* lr_step, float lr, tvq_stream_t stream) {
-  TVQ_CHECK_ARG(lr_step, "tvq_adamw_begin: bad arguments");
-  hipLaunchKernelGGL(adamw_begin_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, lr_step, lr);
+extern "C" int64_t tvq_adamw_chunk(void) { return ADAMW_CHUNK; }
+
+extern "C" int tvq_adamw_gates(const int64_t* gate_ptrs, int64_t nseg, float* gates,
+                               tvq_stream_t stream) {
+  TVQ_CHECK_ARG(gate_ptrs && gates && nseg > 0, "tvq_adamw_gates: bad arguments");
+  hipLaunchKernelGGL(adamw_gates_kernel, dim3(blocks_for(nseg, 64)), dim3(256), 0,
+                     (hipStream_t)stream, gate_ptrs, nseg, gates);
+  return launch_status("tvq_adamw_gates");
+}
+
+// lr_step: device float[2] = {lr, step}; sets lr (when >= 0), counts the step, and
+// advances the step count of every segment whose gate is set.
+extern "C" int tvq_adamw_begin(float* lr_step, float lr, const float* gates, float* seg_step,
+                               int64_t nseg, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(lr_step && gates && seg_step && nseg > 0, "tvq_adamw_begin: bad arguments");
+  hipLaunchKernelGGL(adamw_begin_kernel, dim3(blocks_for(nseg, 64)), dim3(256), 0,
+                     (hipStream_t)stream, lr_step, lr, gates, seg_step, nseg);
   return launch_status("tvq_adamw_begin");
 }
 
 extern "C" int tvq_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
-                         int64_t n, const float* lr_step, float beta1, float beta2, float eps,
-                         float weight_decay, tvq_stream_t stream) {
-  TVQ_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && lr_step && n >= 0,
+                         const int64_t* chunks, int64_t nchunks, const float* lr_step,
+                         const float* gates, const float* seg_step, float beta1, float beta2,
+                         float eps, float weight_decay, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && chunks && lr_step && gates &&
+                    seg_step && nchunks >= 0,
                 "tvq_adamw: bad arguments");
-  if (n == 0) return TVQ_OK;
-  hipLaunchKernelGGL(adamw_kernel, dim3(blocks_for(n, 4096)), dim3(256), 0, (hipStream_t)stream,
-                     params, grads, exp_avg, exp_avg_sq, n, lr_step, beta1, beta2, eps,
-                     weight_decay);
+  if (nchunks == 0) return TVQ_OK;
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)stream,
+                     params, grads, exp_avg, exp_avg_sq, chunks, lr_step, gates, seg_step, beta1,
+                     beta2, eps, weight_decay);
   return launch_status("tvq_adamw");
+}
+
+extern "C" int tvq_layer_drop(const int64_t* seed_ptr, uint64_t offset, float p, int64_t n,
+                              float* keep, float* touched, int64_t accumulate,
+                              tvq_stream_t stream) {
+  TVQ_CHECK_ARG(keep && touched && n > 0 && n <= 256, "tvq_layer_drop: bad arguments");
+  hipLaunchKernelGGL(layer_drop_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, seed_ptr,
+                     offset, p, (int)n, keep, touched, (int)accumulate);
+  return launch_status("tvq_layer_drop");
 }

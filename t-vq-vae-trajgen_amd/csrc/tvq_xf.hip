@@ -439,7 +439,7 @@ __global__ void masked_ce_bwd_kernel(const float* __restrict__ logits, int64_t l
 // largest U[0,1) scores (ties -> lower index, like torch.topk).  s_M = keep ? s : mask_id.
 __global__ void mask_tokens_kernel(const int64_t* __restrict__ s, int B, int n, int64_t mask_id,
                                    const int64_t* seed_ptr, uint64_t offset,
-                                   const float* __restrict__ ratio_in,
+                                   const double* __restrict__ ratio_in,
                                    const float* __restrict__ rand_in, int64_t* __restrict__ s_M,
                                    bool* __restrict__ keep) {
   extern __shared__ float sc[];  // [n]
@@ -448,7 +448,7 @@ __global__ void mask_tokens_kernel(const int64_t* __restrict__ s, int B, int n, 
   for (int j = threadIdx.x; j < n; j += blockDim.x)
     sc[j] = rand_in ? rand_in[(int64_t)b * n + j] : uniform01(seed, (uint64_t)b * (n + 1) + 1 + j);
   __syncthreads();
-  const double ratio = ratio_in ? (double)ratio_in[b] : (double)uniform01(seed, (uint64_t)b * (n + 1));
+  const double ratio = ratio_in ? ratio_in[b] : (double)uniform01(seed, (uint64_t)b * (n + 1));
   // numpy float64 in the reference: floor(cos(r*pi/2) * n), clip to [0, n-1]
   double nu = floor(cos(ratio * 3.14159265358979323846 / 2.0) * (double)n);
   nu = fmin(fmax(nu, 0.0), (double)(n - 1));
@@ -695,7 +695,7 @@ extern "C" int tvq_masked_ce_bwd(const float* logits, int64_t ldl, int64_t M, in
 }
 
 extern "C" int tvq_mask_tokens(const int64_t* s, int64_t B, int64_t n, int64_t mask_id,
-                               const int64_t* seed_ptr, uint64_t offset, const float* ratio,
+                               const int64_t* seed_ptr, uint64_t offset, const double* ratio,
                                const float* rand, int64_t* s_M, bool* keep, tvq_stream_t stream) {
   TVQ_CHECK_ARG(s && s_M && keep && B > 0 && n > 0 && n <= 4096, "tvq_mask_tokens: bad arguments");
   hipLaunchKernelGGL(mask_tokens_kernel, dim3((unsigned)B), dim3(128), n * sizeof(float),

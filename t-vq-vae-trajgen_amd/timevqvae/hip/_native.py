@@ -32,6 +32,7 @@ def sig(name, *argtypes, restype=I32):
 
 
 sig("tvq_counter_pool", I64, P, I64)
+sig("tvq_counter_capture", I64)
 # --- VQ codebook -----------------------------------------------------------
 sig("tvq_vq_sqnorm", P, I64, I64, P, P)
 sig("tvq_vq_assign_nblocks", I64, restype=I64)
@@ -79,8 +80,11 @@ sig("tvq_gemm", P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, F32, P, P, I64,
 sig("tvq_loss_workspace", I64, restype=I64)
 sig("tvq_loss_fwd", P, P, I64, I64, P, P, P)
 sig("tvq_loss_bwd", P, P, I64, I64, P, P, P)
-sig("tvq_adamw_begin", P, F32, P)
-sig("tvq_adamw", P, P, P, P, I64, P, F32, F32, F32, F32, P)
+sig("tvq_adamw_chunk", restype=I64)
+sig("tvq_adamw_gates", P, I64, P, P)
+sig("tvq_adamw_begin", P, F32, P, P, I64, P)
+sig("tvq_adamw", P, P, P, P, P, I64, P, P, P, F32, F32, F32, F32, P)
+sig("tvq_layer_drop", P, ctypes.c_uint64, F32, I64, P, P, I64, P)
 
 # --- MaskGIT transformer ---------------------------------------------------------
 sig("tvq_rmsnorm_fwd", P, I64, I64, P, F32, P, P, P)

@@ -14,6 +14,7 @@ drawn on the device under `rng.device_decisions()`), fixed input buffers.
 import torch
 
 from . import rng, streams
+from ._native import call
 
 
 class StepGraph:
@@ -50,14 +51,18 @@ class StepGraph:
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
         self.graphs, self.outputs = [], []
-        with rng.device_decisions():
-            for seg in self.segments:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
-                    out = seg()
-                    streams.join(backward_done=True)  # side-stream branches rejoin the capture
-                self.graphs.append(g)
-                self.outputs.append(out)
+        call("tvq_counter_capture", 1)  # finish-counter slots of the graph stay reserved
+        try:
+            with rng.device_decisions():
+                for seg in self.segments:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pool):
+                        out = seg()
+                        streams.join(backward_done=True)  # side-stream branches rejoin
+                    self.graphs.append(g)
+                    self.outputs.append(out)
+        finally:
+            call("tvq_counter_capture", 0)
         return self
 
     def replay(self):

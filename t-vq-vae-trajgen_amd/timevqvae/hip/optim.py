@@ -4,13 +4,29 @@ The optimizer re-binds every trainable parameter to a view of one contiguous fp3
 buffer and every .grad to a view of one flat gradient buffer, so that
   * zero_grad is one memset, the DP gradient all-reduce is one collective,
   * the update is one kernel launch (tvq_adamw) for the whole model.
-lr and the step counter live on the device ({lr, step}); schedulers keep working
-through param_groups[0]['lr'].
+lr lives on the device ({lr, step}); schedulers keep working through
+param_groups[0]['lr'].
+
+Skipped parameters.  torch.optim.AdamW leaves a parameter whose .grad is None alone
+(no weight decay, no moment update, its own state['step'] not advanced); under
+Lightning's zero_grad(set_to_none=True) that is every parameter of an x-transformers
+branch that layer dropout skipped this step (bidirectional_transformer.py:104-108).
+Each parameter is one segment of the flat buffer with its own step count; a
+parameter tagged `_tvq_gate = (module, i)` (set by the transformer Encoder) is updated
+only when `module._touched[i]` is non-zero after the step's forward passes.
 """
 import torch
 
 from . import streams
-from ._native import call, ptr, stream_ptr
+from ._native import call, ptr, stream_ptr, value
+
+_grad_epoch = [0]
+
+
+def grad_epoch() -> int:
+    """Incremented by every FusedAdamW.zero_grad: a module that records which of its
+    branches ran (Encoder._touched) starts a new record on the first forward of an epoch."""
+    return _grad_epoch[0]
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -30,15 +46,38 @@ class FusedAdamW(torch.optim.Optimizer):
         self.exp_avg = torch.zeros(n, device=dev, dtype=torch.float32)
         self.exp_avg_sq = torch.zeros(n, device=dev, dtype=torch.float32)
         self.lr_step = torch.tensor([lr, 0.0], device=dev, dtype=torch.float32)
+        chunk = int(value("tvq_adamw_chunk"))
+        chunks, gate_ptrs = [], []
+        self._gate_refs = []  # keeps every gate tensor's storage alive
         off = 0
         with torch.no_grad():
-            for p in ps:
+            for s, p in enumerate(ps):
                 k = p.numel()
                 self.flat[off:off + k].copy_(p.reshape(-1))
                 p.data = self.flat[off:off + k].view_as(p)
                 p.grad = self.flat_grad[off:off + k].view_as(p)
                 p._tvq_flat = True
+                for c in range(0, k, chunk):
+                    chunks.append((off + c, min(chunk, k - c), s))
+                gate = getattr(p, "_tvq_gate", None)
+                if gate is not None:
+                    owner, i = gate
+                    t = owner._touched
+                    if t.device != dev:
+                        raise ValueError("FusedAdamW: a gate buffer is not on the parameters' "
+                                         "device (build the optimizer after .to(device))")
+                    self._gate_refs.append(t)
+                    gate_ptrs.append(t.data_ptr() + 4 * i)
+                else:
+                    gate_ptrs.append(0)
                 off += k
+        self.nseg = len(ps)
+        self.chunks = torch.tensor(chunks, dtype=torch.int64, device=dev).reshape(-1)
+        self.nchunks = len(chunks)
+        self.gate_ptrs = torch.tensor(gate_ptrs, dtype=torch.int64, device=dev)
+        self.gates = torch.ones(self.nseg, device=dev, dtype=torch.float32)
+        self.seg_step = torch.zeros(self.nseg, device=dev, dtype=torch.float32)
+        self.has_gates = any(gate_ptrs)
 
     def push_lr(self):
         """Write param_groups[0]['lr'] into the device {lr, step} pair (for graph replays,
@@ -47,17 +86,28 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def zero_grad(self, set_to_none: bool = False):
         # gradients accumulate in place into the flat buffer views
+        _grad_epoch[0] += 1
         self.flat_grad.zero_()
 
+    def gather_gates(self):
+        """gates[s] <- whether segment s's gated branch ran this step (after the forward
+        passes; under DP the trainer then all-reduces `gates` with MAX)."""
+        if self.has_gates:
+            call("tvq_adamw_gates", ptr(self.gate_ptrs), self.nseg, ptr(self.gates), stream_ptr())
+
     @torch.no_grad()
-    def step(self, closure=None, lr_on_device=False):
+    def step(self, closure=None, lr_on_device=False, gates_ready=False):
         loss = closure() if closure is not None else None
         streams.join(self.flat.device, backward_done=True)  # grads written on side streams
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         s = stream_ptr()
-        call("tvq_adamw_begin", ptr(self.lr_step), -1.0 if lr_on_device else float(g["lr"]), s)
+        if not gates_ready:
+            self.gather_gates()
+        call("tvq_adamw_begin", ptr(self.lr_step), -1.0 if lr_on_device else float(g["lr"]),
+             ptr(self.gates), ptr(self.seg_step), self.nseg, s)
         call("tvq_adamw", ptr(self.flat), ptr(self.flat_grad), ptr(self.exp_avg),
-             ptr(self.exp_avg_sq), self.numel, ptr(self.lr_step), float(b1), float(b2),
-             float(g["eps"]), float(g["weight_decay"]), s)
+             ptr(self.exp_avg_sq), ptr(self.chunks), self.nchunks, ptr(self.lr_step),
+             ptr(self.gates), ptr(self.seg_step), float(b1), float(b2), float(g["eps"]),
+             float(g["weight_decay"]), s)
         return loss

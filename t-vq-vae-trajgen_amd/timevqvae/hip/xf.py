@@ -255,7 +255,7 @@ def mask_tokens(s, mask_id, site, ratio=None, rand=None):
     keep = torch.empty((B, n), device=s.device, dtype=torch.bool)
     seed = rng.seed_tensor(s.device)
     call("tvq_mask_tokens", ptr(s), B, n, int(mask_id), ptr(seed), rng.call_offset(site),
-         ptr(ratio.contiguous() if ratio is not None else None),
+         ptr(ratio.to(torch.float64).contiguous() if ratio is not None else None),
          ptr(rand.contiguous() if rand is not None else None), ptr(s_M), ptr(keep), stream_ptr())
     return s_M, keep
 

@@ -98,7 +98,13 @@ class Residual(nn.Module):
 
 
 class Encoder(nn.Module):
-    """x-transformers Encoder(pre_norm=True, ...) restated."""
+    """x-transformers Encoder(pre_norm=True, ...) restated.
+
+    Layer dropout: in training each branch is skipped with probability layer_dropout
+    (x-transformers draws `random() < layer_dropout` per branch).  `_touched[i]` records
+    whether branch i ran in any forward since the optimizer's last zero_grad; its
+    parameters carry `_tvq_gate = (self, i)`, so FusedAdamW leaves a skipped branch's
+    parameters untouched, as torch.optim.AdamW does for parameters whose .grad is None."""
 
     def __init__(self, dim, depth, heads, attn_dim_head=64, use_rmsnorm=True, ff_mult=1,
                  layer_dropout=0.0, attn_dropout=0.0, ff_dropout=0.0):
@@ -113,17 +119,49 @@ class Encoder(nn.Module):
             self.layers.append(nn.ModuleList([nn.ModuleList([norm(), None, None]), block, Residual()]))
         self.layer_dropout = layer_dropout
         self.final_norm = norm()
+        n = len(self.layers)
+        self.register_buffer("_keep", torch.ones(n), persistent=False)
+        self.register_buffer("_touched", torch.ones(n), persistent=False)
+        for i, layer in enumerate(self.layers):
+            for p in layer.parameters():
+                p._tvq_gate = (self, i)
+        self._site = rng.new_site()
+        self._epoch = -1
+        self._touched_host = [1.0] * n
+
+    def _draw_branches(self, device):
+        """Per-branch keep decisions of this forward; updates `_touched`.  Returns the
+        host keep list (eager) or None (device decisions: `_keep` holds them)."""
+        from ..hip.optim import grad_epoch
+        fresh = self._epoch != grad_epoch()
+        self._epoch = grad_epoch()
+        n = len(self.layers)
+        if rng.decisions_on_device():
+            # graph capture: the decisions are re-drawn on every replay
+            call("tvq_layer_drop", ptr(rng.seed_tensor(device)), rng.call_offset(self._site),
+                 float(self.layer_dropout), n, ptr(self._keep), ptr(self._touched),
+                 int(not fresh), stream_ptr())
+            return None
+        keep = [0.0 if random.random() < self.layer_dropout else 1.0 for _ in range(n)]
+        self._touched_host = keep if fresh else [max(a, b) for a, b in zip(self._touched_host, keep)]
+        self._touched.copy_(torch.tensor(self._touched_host))
+        return keep
 
     def forward(self, x):
-        for norms, block, _ in self.layers:
-            if self.training and self.layer_dropout > 0.0:
-                if rng.decisions_on_device():
-                    # graph capture: skip-with-prob-p as a device Bernoulli gate on the branch
-                    keep = (torch.rand((), device=x.device) >= self.layer_dropout).to(x.dtype)
-                    x = torch.addcmul(x, block(norms[0](x), residual=None), keep)
-                    continue
-                if random.random() < self.layer_dropout:
-                    continue
+        keep = None
+        device_gates = False
+        if self.training and self.layer_dropout > 0.0:
+            keep = self._draw_branches(x.device)
+            device_gates = keep is None
+        elif self.training and self._touched_host != [1.0] * len(self.layers):
+            self._touched_host = [1.0] * len(self.layers)
+            self._touched.fill_(1.0)
+        for i, (norms, block, _) in enumerate(self.layers):
+            if device_gates:
+                x = torch.addcmul(x, block(norms[0](x), residual=None), self._keep[i])
+                continue
+            if keep is not None and keep[i] == 0.0:
+                continue
             x = block(norms[0](x), residual=x)
         return self.final_norm(x)
 
@@ -281,14 +319,19 @@ class BidirectionalTransformer(nn.Module):
             self.projector = Upscale(embed_dim, embed_dim, 2 * embed_dim)
         self._site_l = rng.new_site()
         self._site_h = rng.new_site()
+        self._class_rand = None
 
     def class_embedding(self, class_condition: Union[None, torch.Tensor], batch_size: int, device):
-        """bidirectional_transformer.py:124-150."""
+        """bidirectional_transformer.py:124-150.  `_class_rand` (tests only): the uniform
+        draws of the classifier-free-guidance drop, injected instead of torch.rand."""
         if class_condition is None:
             idx = torch.full((batch_size, 1), self.n_classes, dtype=torch.long, device=device)
         else:
             if self.training:
-                ind = torch.rand(class_condition.shape, device=device) > self.p_unconditional
+                u = self._class_rand
+                if u is None:
+                    u = torch.rand(class_condition.shape, device=device)
+                ind = torch.as_tensor(u).to(device).reshape(class_condition.shape) > self.p_unconditional
             else:
                 ind = torch.ones_like(class_condition, dtype=torch.bool)
             idx = torch.where(ind, class_condition.long(), self.n_classes)

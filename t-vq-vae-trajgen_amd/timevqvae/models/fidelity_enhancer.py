@@ -53,14 +53,23 @@ class _Conv(nn.Conv1d):
 
 
 class _StandardizedConv(nn.Conv1d):
-    """Weight-standardised conv3 (:96-116).  The standardised weight is recomputed only
-    when the parameter changes (its version counter moves on every in-place update)."""
+    """Weight-standardised conv3 (:96-116).  Eager: the standardised weight is recomputed
+    only when the parameter changes (its version counter moves on every in-place update
+    through the parameter; writes through `.data` do not move it, so call
+    `invalidate()` after those).  Under hipGraph capture it is always recomputed inside
+    the graph, so replays read the weight as it is at replay time."""
 
     def __init__(self, cin, cout):
         super().__init__(cin, cout, 3, padding=1)
 
+    def invalidate(self):
+        self._ws_key = None
+
     def forward(self, x):
         key = (self.weight.data_ptr(), self.weight._version, self.weight.device)
+        if torch.cuda.is_current_stream_capturing():
+            self._ws_key = None
+            return ops.conv1d(x, ops.standardize_weight(self.weight, _EPS), self.bias, padding=1)
         if getattr(self, "_ws_key", None) != key:
             self._ws = ops.standardize_weight(self.weight, _EPS)
             self._ws_key = key

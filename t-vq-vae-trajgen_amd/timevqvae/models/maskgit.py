@@ -121,29 +121,47 @@ class MaskGIT(nn.Module):
         logits = transformer(*s_in, class_condition=class_condition)
         return logits_null + self.cfg_scale * (logits - logits_null)
 
-    def forward(self, x, y):
-        """maskgit.py:155-192 -> (loss, (loss_l, loss_h))."""
+    def forward(self, x, y, draws=None):
+        """maskgit.py:155-192 -> (loss, (loss_l, loss_h)).
+
+        `draws` (tests only) injects the reference's random draws instead of the device
+        RNG: {"ratio_l", "rand_l", "ratio_h", "rand_h"} for _randomly_mask_tokens
+        (np.random.uniform ratios, torch.rand scores) and {"cls_l", "cls_h"} for the
+        class-drop draws of each transformer (bidirectional_transformer.py:140-143)."""
         self.encoder_l.eval()
         self.vq_model_l.eval()
         self.encoder_h.eval()
         self.vq_model_h.eval()
+        dr = draws or {}
         s_l, s_h = self.encode_tokens(x)
-        s_l_M, keep_l = self._randomly_mask_tokens(s_l, self.mask_token_ids["lf"], x.device)
-        s_h_M, keep_h = self._randomly_mask_tokens(s_h, self.mask_token_ids["hf"], x.device)
-        with streams.branch(x.device) as br:  # HF transformer concurrently with LF
-            br.inputs(y, s_l_M, s_h_M, s_h, keep_h)
-            logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
-            mask_pred_loss_h = masked_cross_entropy(logits_h, s_h, keep_h)
-            br.outputs(mask_pred_loss_h)
-        logits_l = self.masked_prediction(self.transformer_l, y, s_l_M)
-        mask_pred_loss_l = masked_cross_entropy(logits_l, s_l, keep_l)
-        br.join()
+        s_l_M, keep_l = self._randomly_mask_tokens(s_l, self.mask_token_ids["lf"], x.device,
+                                                   dr.get("ratio_l"), dr.get("rand_l"))
+        s_h_M, keep_h = self._randomly_mask_tokens(s_h, self.mask_token_ids["hf"], x.device,
+                                                   dr.get("ratio_h"), dr.get("rand_h"))
+        self.transformer_l._class_rand = dr.get("cls_l")
+        self.transformer_h._class_rand = dr.get("cls_h")
+        try:
+            with streams.branch(x.device) as br:  # HF transformer concurrently with LF
+                br.inputs(y, s_l_M, s_h_M, s_h, keep_h)
+                logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
+                mask_pred_loss_h = masked_cross_entropy(logits_h, s_h, keep_h)
+                br.outputs(mask_pred_loss_h)
+            logits_l = self.masked_prediction(self.transformer_l, y, s_l_M)
+            mask_pred_loss_l = masked_cross_entropy(logits_l, s_l, keep_l)
+            br.join()
+        finally:
+            self.transformer_l._class_rand = self.transformer_h._class_rand = None
         return mask_pred_loss_l + mask_pred_loss_h, (mask_pred_loss_l, mask_pred_loss_h)
 
-    def _randomly_mask_tokens(self, s, mask_token_id, device):
-        """maskgit.py:194-216 on device; returns (s_M, mask) with mask=True for kept tokens."""
+    def _randomly_mask_tokens(self, s, mask_token_id, device, ratio=None, rand=None):
+        """maskgit.py:194-216 on device; returns (s_M, mask) with mask=True for kept tokens.
+        ratio (b,) / rand (b, n): injected draws (tests), else the device RNG."""
         site = self._site_mask_l if s.shape[1] == self.num_tokens_l else self._site_mask_h
-        return mask_tokens(s, mask_token_id, site)
+        if ratio is not None:
+            ratio = torch.as_tensor(ratio, dtype=torch.float64).to(device)
+        if rand is not None:
+            rand = torch.as_tensor(rand, dtype=torch.float32).to(device)
+        return mask_tokens(s, mask_token_id, site, ratio=ratio, rand=rand)
 
     def gamma_func(self, mode="cosine"):
         """maskgit.py:218-228."""

@@ -392,6 +392,290 @@ def gen_fe(ref):
     np.savez_compressed(os.path.join(OUT, "g8_fe.npz"), **d)
 
 
+# --------------------------------------------------------------------------- G9
+def install_x_transformers_stub():
+    """x-transformers (pyproject.toml:21, ^1.31.6) is absent from the image and has no
+    source on disk, so bidirectional_transformer.py:8-9 cannot import it.  This stub
+    registers a module `x_transformers` whose ContinuousTransformerWrapper / Encoder
+    are the T1 restatement (x-transformers 1.3x behaviour, the same arithmetic as
+    oracle/tvq_oracle.py:xf_blocks) with the x-transformers module tree, so the
+    reference file itself runs: Upscale, embeddings, class conditioning, pred_head,
+    tied logits and the MaskGIT loss composition are then the reference's own code.
+    Only T1's arithmetic stays parity-unpinned."""
+    import random
+    import torch.nn.functional as F
+
+    xt = types.ModuleType("x_transformers")
+
+    class RMSNorm(nn.Module):  # F.normalize(x) * sqrt(dim) * g
+        def __init__(self, dim):
+            super().__init__()
+            self.scale = dim ** 0.5
+            self.g = nn.Parameter(torch.ones(dim))
+
+        def forward(self, x):
+            return F.normalize(x, dim=-1) * self.scale * self.g
+
+    class LayerNorm(nn.Module):  # gamma-only LayerNorm (beta is a zero buffer)
+        def __init__(self, dim):
+            super().__init__()
+            self.gamma = nn.Parameter(torch.ones(dim))
+            self.register_buffer("beta", torch.zeros(dim), persistent=False)
+
+        def forward(self, x):
+            return F.layer_norm(x, x.shape[-1:], self.gamma, self.beta)
+
+    class Attention(nn.Module):
+        def __init__(self, dim, heads, dim_head, dropout):
+            super().__init__()
+            self.heads, self.dim_head = heads, dim_head
+            inner = heads * dim_head
+            self.to_q = nn.Linear(dim, inner, bias=False)
+            self.to_k = nn.Linear(dim, inner, bias=False)
+            self.to_v = nn.Linear(dim, inner, bias=False)
+            self.to_out = nn.Linear(inner, dim, bias=False)
+            self.dropout = nn.Dropout(dropout)
+
+        def forward(self, x):
+            B, S, _ = x.shape
+            sh = lambda t: t.view(B, S, self.heads, self.dim_head).transpose(1, 2)
+            q, k, v = sh(self.to_q(x)), sh(self.to_k(x)), sh(self.to_v(x))
+            att = torch.softmax(q @ k.transpose(-1, -2) * self.dim_head ** -0.5, dim=-1)
+            o = (self.dropout(att) @ v).transpose(1, 2).reshape(B, S, -1)
+            return self.to_out(o)
+
+    class FeedForward(nn.Module):
+        def __init__(self, dim, mult, dropout):
+            super().__init__()
+            inner = int(dim * mult)
+            self.ff = nn.Sequential(nn.Sequential(nn.Linear(dim, inner), nn.GELU()),
+                                    nn.Dropout(dropout), nn.Linear(inner, dim))
+
+        def forward(self, x):
+            return self.ff(x)
+
+    class Residual(nn.Module):
+        def forward(self, x, residual):
+            return x + residual
+
+    class Encoder(nn.Module):
+        def __init__(self, dim, depth, heads=8, pre_norm=True, use_rmsnorm=False,
+                     layer_dropout=0.0, **kw):
+            super().__init__()
+            assert pre_norm
+            self.dim = dim
+            norm = (lambda: RMSNorm(dim)) if use_rmsnorm else (lambda: LayerNorm(dim))
+            dim_head = kw.get("attn_dim_head", 64)
+            self.layers = nn.ModuleList()
+            for t in ("a", "f") * depth:
+                block = (Attention(dim, heads, dim_head, kw.get("attn_dropout", 0.0)) if t == "a"
+                         else FeedForward(dim, kw.get("ff_mult", 4), kw.get("ff_dropout", 0.0)))
+                self.layers.append(nn.ModuleList([nn.ModuleList([norm(), None, None]), block,
+                                                  Residual()]))
+            self.layer_dropout = layer_dropout
+            self.final_norm = norm()
+
+        def forward(self, x):
+            for norms, block, residual_fn in self.layers:
+                if self.training and self.layer_dropout > 0.0 and random.random() < self.layer_dropout:
+                    continue
+                x = residual_fn(block(norms[0](x)), x)
+            return self.final_norm(x)
+
+    class ContinuousTransformerWrapper(nn.Module):
+        def __init__(self, *, max_seq_len, attn_layers, dim_in=None, dim_out=None,
+                     use_abs_pos_emb=True, post_emb_norm=False, emb_dropout=0.0, **kw):
+            super().__init__()
+            assert not use_abs_pos_emb
+            dim = attn_layers.dim
+            self.max_seq_len = max_seq_len
+            self.post_emb_norm = LayerNorm(dim) if post_emb_norm else nn.Identity()
+            self.emb_dropout = nn.Dropout(emb_dropout)
+            self.project_in = nn.Linear(dim_in, dim, bias=False) if dim_in is not None else nn.Identity()
+            self.attn_layers = attn_layers
+            self.project_out = nn.Linear(dim, dim_out, bias=False) if dim_out is not None else nn.Identity()
+
+        def forward(self, x):
+            x = self.post_emb_norm(self.project_in(x))
+            x = self.attn_layers(self.emb_dropout(x))
+            return self.project_out(x)
+
+    xt.ContinuousTransformerWrapper = ContinuousTransformerWrapper
+    xt.Encoder = Encoder
+    sys.modules["x_transformers"] = xt
+    return xt
+
+
+def load_reference_stage2(ref):
+    """bidirectional_transformer.py (with the x_transformers stub) + maskgit.py re-loaded
+    against it."""
+    install_x_transformers_stub()
+    bt = _load("ref_bidirectional_transformer", f"{REF}/models/bidirectional_transformer.py")
+    sys.modules["timevqvae.models"].BidirectionalTransformer = bt.BidirectionalTransformer
+    maskgit = _load("ref_maskgit_bt", f"{REF}/models/maskgit.py")
+    return bt, maskgit
+
+
+PRIOR_L = {"hidden_dim": 128, "n_layers": 4, "heads": 2, "ff_mult": 1, "use_rmsnorm": True}
+PRIOR_H = {"hidden_dim": 32, "n_layers": 1, "heads": 1, "ff_mult": 1, "use_rmsnorm": True}
+
+
+def gout(shape, seed):
+    """Upstream gradient for the G9 backward checks (numpy, so tests rebuild it)."""
+    return np.random.default_rng(seed + 200).standard_normal(shape).astype(np.float32)
+
+
+class _Recorder:
+    """Records every torch.rand / np.random.uniform draw the reference makes (in call
+    order), so the HIP path can be fed the same draws."""
+
+    def __init__(self):
+        self.torch_rand, self.np_uniform = [], []
+
+    def __enter__(self):
+        self._tr, self._nu = torch.rand, np.random.uniform
+
+        def tr(*a, **k):
+            t = self._tr(*a, **k)
+            self.torch_rand.append(t.detach().clone())
+            return t
+
+        def nu(*a, **k):
+            v = self._nu(*a, **k)
+            self.np_uniform.append(np.array(v, dtype=np.float64).copy())
+            return v
+        torch.rand, np.random.uniform = tr, nu
+        return self
+
+    def __exit__(self, *exc):
+        torch.rand, np.random.uniform = self._tr, self._nu
+
+
+def gen_stage2(ref):
+    """G9: the reference BidirectionalTransformer (bidirectional_transformer.py:34-251)
+    and MaskGIT forward / CFG (maskgit.py:136-192) run from the reference files, with
+    x-transformers replaced by the restated stub (install_x_transformers_stub).  Params
+    come from param_init (seeded per key); every random draw is recorded and stored."""
+    bt, maskgit = load_reference_stage2(ref)
+    d = {}
+    K, B, emb = 512, 4, 128
+    # ---- (1) transformers alone at the config-B architecture (K=512, hid 128)
+    for kind, pm, seed in (("lf", PRIOR_L, 41), ("hf", PRIOR_H, 42)):
+        torch.manual_seed(seed)
+        m = bt.BidirectionalTransformer(kind, 24 if kind == "lf" else 96, {"lf": K, "hf": K}, emb,
+                                        p_unconditional=0.2, n_classes=5, model_dropout=0.0,
+                                        emb_dropout=0.0, num_tokens_l=24, **pm)
+        vals = fill_state_dict(m.state_dict(), seed)
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()}, strict=True)
+        g = torch.Generator().manual_seed(seed + 100)
+        s_l = torch.randint(0, K + 1, (B, 24), generator=g)
+        s_h = torch.randint(0, K + 1, (B, 96), generator=g)
+        s_l[:, :5] = K  # some mask tokens
+        s_h[:, ::3] = K
+        y = torch.randint(0, 5, (B, 1), generator=g)
+        args = (s_l,) if kind == "lf" else (s_l, s_h)
+        p = f"{kind}_"
+        d[p + "s_l"], d[p + "s_h"], d[p + "y"] = s_l.numpy(), s_h.numpy(), y.numpy()
+        d[p + "keys"] = np.array(sorted(m.state_dict().keys()))
+        m.eval()
+        with torch.no_grad():
+            d[p + "eval_cond"] = m(*args, class_condition=y).numpy()
+            d[p + "eval_uncond"] = m(*args, class_condition=None).numpy()
+        m.train()  # train-mode BN (Upscale), class-drop draws recorded
+        with _Recorder() as rec:
+            logits = m(*args, class_condition=y)
+        d[p + "train_cls_rand"] = rec.torch_rand[0].numpy()
+        d[p + "train_cond"] = logits.detach().numpy()
+        gl = torch.from_numpy(gout(logits.shape, seed))  # regenerated by the tests
+        (logits * gl).sum().backward()
+        for k, prm in m.named_parameters():
+            if prm.grad is not None:
+                d[p + "grad/" + k] = prm.grad.numpy().copy()
+        d.update({p + "post/" + k: v.numpy().copy() for k, v in m.state_dict().items()
+                  if k.endswith(("running_mean", "running_var"))})
+
+    # ---- (2) MaskGIT.forward loss (maskgit.py:155-192) over a stage1 (T=128, K=64, hid 32)
+    T, Ks, hid = 128, 64, 32
+    seed = 3  # the G3-small stage1 weights
+    cfg = _stage1_config(4, hid, Ks)
+    torch.manual_seed(seed)
+    s1 = ref.stage1.Stage1(T, 6, cfg)
+    vals = fill_state_dict(s1.state_dict(), seed)
+    s1.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()}, strict=False)
+    gx = torch.Generator().manual_seed(77)
+    Bm = 8
+    x = torch.cumsum(0.1 * torch.randn(Bm, 6, T, generator=gx), -1)
+    x = 2 * (x - x.amin(0, keepdim=True)) / (x.amax(0, keepdim=True) - x.amin(0, keepdim=True) + 1e-8) - 1
+    y = torch.randint(0, 5, (Bm, 1), generator=gx)
+    s1.eval()
+    with torch.no_grad():
+        s1.encoder_l(x), s1.encoder_h(x)  # sets num_tokens / H' / W' buffers (vq_vae.py:183-187)
+    MG = maskgit.MaskGIT
+    mg = MG.__new__(MG)
+    nn.Module.__init__(mg)
+    mg.choice_temperature_l, mg.choice_temperature_h = 10, 4
+    mg.T = {"lf": 10, "hf": 1}
+    mg.n_classes = 5
+    mg.cfg_scale = 1.0
+    mg.mask_token_ids = {"lf": Ks, "hf": Ks}
+    mg.gamma = mg.gamma_func("cosine")
+    mg.stage1 = s1
+    for n in ("encoder_l", "decoder_l", "vq_model_l", "encoder_h", "decoder_h", "vq_model_h"):
+        setattr(mg, n, getattr(s1, n))
+    mg.num_tokens_l, mg.num_tokens_h = int(s1.encoder_l.num_tokens), int(s1.encoder_h.num_tokens)
+    prior = dict(p_unconditional=0.2, model_dropout=0.0, emb_dropout=0.0)
+    torch.manual_seed(50)
+    mg.transformer_l = bt.BidirectionalTransformer("lf", mg.num_tokens_l, {"lf": Ks, "hf": Ks}, hid,
+                                                   n_classes=5, **PRIOR_L, **prior)
+    mg.transformer_h = bt.BidirectionalTransformer("hf", mg.num_tokens_h, {"lf": Ks, "hf": Ks}, hid,
+                                                   n_classes=5, num_tokens_l=mg.num_tokens_l,
+                                                   **PRIOR_H, **prior)
+    for name in ("transformer_l", "transformer_h"):
+        tm = getattr(mg, name)
+        vals = fill_state_dict(tm.state_dict(), 50)
+        tm.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()}, strict=True)
+    for p_ in s1.parameters():
+        p_.requires_grad_(False)
+    mg.train()
+    np.random.seed(31)
+    torch.manual_seed(32)
+    with _Recorder() as rec:
+        loss, (loss_l, loss_h) = mg(x, y)
+    # draw order (maskgit.py:167-178, bidirectional_transformer.py:140-143):
+    # np ratio_l, torch rand_l, np ratio_h, torch rand_h, cls rand (LF), cls rand (HF)
+    assert len(rec.np_uniform) == 2 and len(rec.torch_rand) == 4, (len(rec.np_uniform), len(rec.torch_rand))
+    d["mg_x"], d["mg_y"] = x.numpy(), y.numpy()
+    d["mg_ratio_l"], d["mg_ratio_h"] = rec.np_uniform
+    d["mg_rand_l"], d["mg_rand_h"] = rec.torch_rand[0].numpy(), rec.torch_rand[1].numpy()
+    d["mg_cls_rand_l"], d["mg_cls_rand_h"] = rec.torch_rand[2].numpy(), rec.torch_rand[3].numpy()
+    d["mg_loss"], d["mg_loss_l"], d["mg_loss_h"] = (np.array(float(v)) for v in (loss, loss_l, loss_h))
+    loss.backward()
+    for name in ("transformer_l", "transformer_h"):
+        for k, prm in getattr(mg, name).named_parameters():
+            if prm.grad is not None:
+                d[f"mg_grad/{name}.{k}"] = prm.grad.numpy().copy()
+        for k, v in getattr(mg, name).state_dict().items():
+            if k.endswith(("running_mean", "running_var")):  # Upscale BN after the forward
+                d[f"mg_post/{name}.{k}"] = v.numpy().copy()
+    with torch.no_grad():
+        _, s_l = mg.encode_to_z_q(x, mg.encoder_l, mg.vq_model_l)
+        _, s_h = mg.encode_to_z_q(x, mg.encoder_h, mg.vq_model_h)
+    d["mg_s_l"], d["mg_s_h"] = s_l.numpy().astype(np.int64), s_h.numpy().astype(np.int64)
+
+    # ---- (3) masked_prediction with classifier-free guidance (maskgit.py:136-153), eval
+    mg.eval()
+    mg.cfg_scale = 2.0
+    gs = torch.Generator().manual_seed(78)
+    s_l_M = torch.randint(0, Ks + 1, s_l.shape, generator=gs)
+    s_h_M = torch.randint(0, Ks + 1, s_h.shape, generator=gs)
+    with torch.no_grad():
+        d["cfg_s_l_M"], d["cfg_s_h_M"] = s_l_M.numpy(), s_h_M.numpy()
+        d["cfg_logits_l"] = mg.masked_prediction(mg.transformer_l, y, s_l_M).numpy()
+        d["cfg_logits_h"] = mg.masked_prediction(mg.transformer_h, y, s_l_M, s_h_M).numpy()
+        d["cfg_logits_h_uncond"] = mg.masked_prediction(mg.transformer_h, None, s_l_M, s_h_M).numpy()
+    np.savez_compressed(os.path.join(OUT, "g9_stage2.npz"), **d)
+
+
 def main():
     torch.set_num_threads(8)
     if sys.argv[1:] == ["rocket"]:  # regenerate only G7
@@ -403,6 +687,9 @@ def main():
         return
     if sys.argv[1:] == ["fe"]:  # regenerate only G8
         gen_fe(ref)
+        return
+    if sys.argv[1:] == ["stage2"]:  # regenerate only G9
+        gen_stage2(ref)
         return
     gen_vq(ref)
     gen_stft(ref)

@@ -23,13 +23,18 @@ def _worker(rank, world, port, q):
         from timevqvae.hip.vq import CodebookUpdate
 
         # flat gradient average (JointTrainer._allreduce)
+        # + layer-dropout gates OR-ed over ranks (a segment some replica used is updated
+        # on every replica)
         class Opt:
             flat_grad = torch.full((5,), float(rank + 1))
+            has_gates = True
+            gates = torch.tensor([1.0, 0.0, 0.0]) if rank == 0 else torch.tensor([0.0, 0.0, 1.0])
         tr = bench.JointTrainer.__new__(bench.JointTrainer)
         tr.world = world
         opt = Opt()
         tr._allreduce(opt)
         ok_grad = torch.allclose(opt.flat_grad, torch.full((5,), (1 + world) / 2.0))
+        ok_grad = ok_grad and torch.equal(opt.gates, torch.tensor([1.0, 0.0, 1.0]))
 
         # sync_codebook statistics: summed over ranks before the EMA
         K, D = 4, 3

@@ -288,6 +288,69 @@ def test_adamw_matches_torch(cuda):
         torch.testing.assert_close(pd.detach().cpu(), pc.detach(), rtol=1e-6, atol=1e-6)
 
 
+def test_adamw_skips_gated_parameters_like_torch(cuda):
+    """A parameter whose branch did not run (gate 0) is left alone, as torch.optim.AdamW
+    leaves a parameter with .grad None: no decay, no moments, no step count."""
+    from timevqvae.hip.optim import FusedAdamW
+
+    class Owner:  # stands in for the transformer Encoder (its _touched buffer)
+        _touched = torch.ones(2, device=cuda)
+
+    gen = torch.Generator().manual_seed(4)
+    shapes = ((5000,), (7, 3), (33,))  # the first spans two chunks
+    ps_c = [torch.randn(s, generator=gen).requires_grad_(True) for s in shapes]
+    ps_d = [p.detach().to(cuda).requires_grad_(True) for p in ps_c]
+    ps_d[0]._tvq_gate = (Owner, 0)
+    ps_d[2]._tvq_gate = (Owner, 1)
+    oc = torch.optim.AdamW(ps_c, lr=1e-2)
+    od = FusedAdamW(ps_d, lr=1e-2)
+    pattern = [(1, 1), (0, 1), (0, 0), (1, 0), (1, 1), (0, 1)]
+    for step, (k0, k2) in enumerate(pattern):
+        grads = [torch.randn(p.shape, generator=gen) for p in ps_c]
+        oc.zero_grad(set_to_none=True)
+        od.zero_grad()
+        Owner._touched.copy_(torch.tensor([float(k0), float(k2)]))
+        for i, (pc, pd, g) in enumerate(zip(ps_c, ps_d, grads)):
+            used = {0: k0, 1: 1, 2: k2}[i]
+            if used:
+                pc.grad = g.clone()
+                pd.grad.copy_(g)
+        oc.step()
+        od.step()
+    for pc, pd in zip(ps_c, ps_d):
+        torch.testing.assert_close(pd.detach().cpu(), pc.detach(), rtol=1e-6, atol=1e-6)
+
+
+def test_layer_dropout_leaves_skipped_branches_untouched(cuda):
+    """x-transformers layer dropout in training (graph-style device decisions): after one
+    optimizer step, every parameter of a skipped branch is bitwise unchanged and every
+    parameter of a branch that ran has moved."""
+    from timevqvae.hip import rng
+    from timevqvae.hip.optim import FusedAdamW
+    from timevqvae.models.bidirectional_transformer import Encoder
+    import contextlib
+    import random
+    random.seed(3)
+    torch.manual_seed(0)
+    enc = Encoder(dim=64, depth=4, heads=1, layer_dropout=0.5).to(cuda).train()
+    opt = FusedAdamW(enc.parameters(), lr=1e-2)
+    x = torch.randn(3, 9, 64, device=cuda)
+    for device_decisions in (True, False):
+        before = {k: p.detach().clone() for k, p in enc.named_parameters()}
+        opt.zero_grad()
+        ctx = rng.device_decisions() if device_decisions else contextlib.nullcontext()
+        with ctx:
+            enc(x).square().sum().backward()
+        opt.step()
+        touched = enc._touched.cpu().tolist()
+        assert 0.0 in touched or device_decisions, touched  # p=0.5 over 8 branches
+        for k, p in enc.named_parameters():
+            if k.startswith("layers."):
+                i = int(k.split(".")[1])
+                moved = not torch.equal(p.detach(), before[k])
+                assert moved == bool(touched[i]), (k, touched)
+
+
 @pytest.mark.parametrize("Ci,Co,W", [(16, 16, 32), (64, 64, 8), (8, 8, 64), (128, 16, 32)])
 def test_conv_paths_same_dropout_mask(Ci, Co, W, cuda):
     """The dropout mask is a function of (seed, offset, output index) only: the halo

@@ -43,11 +43,26 @@ def test_sample_step_vs_oracle(B, n, K, t, T, temp, cuda):
     # categorical draw: exact vs the double-precision inverse CDF
     probs = torch.softmax(logits.double(), -1)
     cdf = torch.cumsum(probs, -1)
-    want = torch.searchsorted(cdf, u_cat.double().unsqueeze(-1) * cdf[..., -1:]).squeeze(-1)
+    want = torch.searchsorted(cdf, u_cat.double().unsqueeze(-1) * cdf[..., -1:],
+                              right=True).squeeze(-1)
     want = torch.where(s == mask_id, want.clamp(max=K - 1), s)
     assert torch.equal(sampled.cpu(), want)
     assert torch.equal(out.cpu(), ref)
     assert int((out == mask_id).sum(1).max()) == k == int((out == mask_id).sum(1).min())
+
+
+def test_sample_never_draws_zero_probability_code(cuda):
+    """u = 0 with leading codes whose probability underflows to 0: the draw is the first
+    code of positive probability (torch's Categorical never samples a 0-probability code)."""
+    from timevqvae.hip.sample import maskgit_sample
+    K = 512
+    logits = torch.zeros(2, 3, K)
+    logits[..., :70] = -1e4  # exp underflows: p = 0 for codes 0..69 (two lanes' chunks)
+    s = torch.full((2, 3), K, dtype=torch.int64)
+    u = torch.zeros(2, 3)
+    sampled, selp = maskgit_sample(logits.to(cuda), s.to(cuda), K, u_cat=u.to(cuda))
+    assert (sampled.cpu() == 70).all()
+    assert (selp.cpu() > 0).all()
 
 
 def test_mask_by_random_topk_exact_k(cuda):
