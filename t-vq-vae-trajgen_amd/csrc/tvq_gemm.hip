@@ -7,35 +7,15 @@
 //   epi: + bias[n], GELU (erf), + R[m*ldr + n], or accumulate into C.
 // Split-K over gridDim.z writes fp32 slabs reduced in split order (deterministic), by
 // the last-arriving split block of each tile (or a separate reduce launch).
+// tvq_gemm first offers the call to the skinny kernels (tvq_gemm_skinny.hip: A rows
+// k-contiguous, K <= 512); this generic kernel takes the rest (the weight gradients).
 #include <math.h>
 #include <stdlib.h>
 
 #include "tvq_common.h"
+#include "tvq_gemm.h"
 
 namespace tvq {
-
-struct GemmArgs {
-  const float* A;
-  const float* B;
-  float* C;
-  int M, N, K;
-  int64_t sam, sak, sbk, sbn, ldc;
-  const float* bias;
-  const float* R;
-  int64_t ldr;
-  int64_t rmod;    // R row = m % rmod when > 0 (per-position bias broadcast over the batch)
-  float* pre;      // optional: pre-activation output (ldc layout), for the GELU backward
-  int act;         // 0 none, 1 GELU(erf)
-  int accumulate;  // C += result
-  float alpha;
-  int kper;        // K range per split
-  float* slab;     // split-K partials [split][M][N] (nullptr: write C directly)
-  int* cnt;        // split-K: one counter per (m, n) tile -> the last split block finishes
-};
-
-__device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
-}
 
 __device__ __forceinline__ float apply_epi(const GemmArgs& g, int m, int n, float v) {
   v *= g.alpha;
@@ -297,6 +277,10 @@ extern "C" int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B
   g.bias = bias; g.R = R; g.ldr = ldr; g.rmod = rmod; g.pre = pre;
   g.act = (int)act; g.accumulate = (int)accumulate;
   g.alpha = alpha;
+  g.kper = (int)K;
+  g.cnt = nullptr;
+  g.slab = nullptr;
+  if (gemm_skinny(g, (hipStream_t)stream)) return launch_status("tvq_gemm(skinny)");
   int TM, TN;
   choose_tile(M, N, &TM, &TN);
   const int tiles = (int)(((M + TM - 1) / TM) * ((N + TN - 1) / TN));

@@ -2,12 +2,7 @@
 //
 //  rmsnorm     x-transformers RMSNorm: F.normalize(x) * sqrt(D) * g
 //  layernorm   LayerNorm over the last dim (gamma [+ beta]), eps given
-//  attention   softmax(Q K^T * scale) [dropout] V for seq <= 104 (the path has 25
-//              and 97: token counts do not depend on T), one workgroup
-//              per (batch, head): Q/K/V tiles and the score matrix live in LDS,
-//              scores/probabilities never touch HBM; backward recomputes P from
-//              the saved row log-sum-exp.  Q/K/V/O are read in the Linear layout
-//              [(b*S + s) * ld + h*Dh + d] so no head transposes are materialised.
+//  (attention: tvq_attn.hip)
 //  embedding   table gather (+ dropout on non-mask tokens) and a deterministic
 //              per-row scatter-add backward (no float atomics)
 //  masked CE   cross_entropy over the masked positions (maskgit.py:183-191)
@@ -173,177 +168,6 @@ __global__ void ln_colsum2_kernel(const float* __restrict__ ws, int P, int D,
   float s = 0.f;
   for (int p = 0; p < P; ++p) s += ws[((int64_t)p * 2 + k) * D + d];
   dst[d] = accumulate ? dst[d] + s : s;
-}
-
-// ---------------------------------------------------------------- attention
-// Q/K/V/O element (b, s, h, d) at base + (b*S + s)*ld + h*DH + d.  One 256-thread
-// workgroup per (b, h).  LDS: Qs, Ks, Vs [S][DH+1], P [S][S+1].
-constexpr int ATT_DH = 64;
-
-struct AttnArgs {
-  const float* q; const float* k; const float* v;
-  int64_t ldq, ldk, ldv;
-  float* o; int64_t ldo;
-  float* lse;  // [B*H*S]
-  int B, H, S;
-  float scale;
-  float drop_p;
-  const int64_t* seed_ptr;
-  uint64_t offset;
-};
-
-__device__ __forceinline__ bool attn_keep(uint64_t seed, int64_t bh, int S, int i, int j, float p) {
-  return uniform01(seed, ((uint64_t)bh * S + i) * S + j) >= p;
-}
-
-__global__ __launch_bounds__(256) void attention_fwd_kernel(AttnArgs a) {
-  extern __shared__ float sm[];
-  const int S = a.S;
-  constexpr int LD = ATT_DH + 1;
-  float* Qs = sm;
-  float* Ks = Qs + S * LD;
-  float* Vs = Ks + S * LD;
-  float* P = Vs + S * LD;  // [S][S+1]
-  const int PL = S + 1;
-  const int bh = blockIdx.x;
-  const int b = bh / a.H, h = bh - b * a.H;
-  const int tid = threadIdx.x;
-  for (int e = tid; e < S * ATT_DH; e += 256) {
-    const int s = e / ATT_DH, d = e - s * ATT_DH;
-    const int64_t r = (int64_t)b * S + s;
-    Qs[s * LD + d] = a.q[r * a.ldq + h * ATT_DH + d];
-    Ks[s * LD + d] = a.k[r * a.ldk + h * ATT_DH + d];
-    Vs[s * LD + d] = a.v[r * a.ldv + h * ATT_DH + d];
-  }
-  __syncthreads();
-  for (int e = tid; e < S * S; e += 256) {
-    const int i = e / S, j = e - i * S;
-    float acc = 0.f;
-#pragma unroll 8
-    for (int d = 0; d < ATT_DH; ++d) acc = fmaf(Qs[i * LD + d], Ks[j * LD + d], acc);
-    P[i * PL + j] = acc * a.scale;
-  }
-  __syncthreads();
-  // row softmax: one wave per row
-  const int lane = tid & 63, wid = tid >> 6;
-  const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
-  const float dscale = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
-  for (int i = wid; i < S; i += 4) {
-    float mx = -INFINITY;
-    for (int j = lane; j < S; j += 64) mx = fmaxf(mx, P[i * PL + j]);
-    mx = wave_max(mx);
-    float sum = 0.f;
-    for (int j = lane; j < S; j += 64) {
-      const float e = expf(P[i * PL + j] - mx);
-      P[i * PL + j] = e;
-      sum += e;
-    }
-    sum = wave_sum(sum);
-    const float inv = 1.0f / sum;
-    for (int j = lane; j < S; j += 64) {
-      float p = P[i * PL + j] * inv;
-      if (a.drop_p > 0.f) p = attn_keep(seed, bh, S, i, j, a.drop_p) ? p * dscale : 0.f;
-      P[i * PL + j] = p;
-    }
-    if (lane == 0) a.lse[(int64_t)bh * S + i] = mx + logf(sum);
-  }
-  __syncthreads();
-  for (int e = tid; e < S * ATT_DH; e += 256) {
-    const int i = e / ATT_DH, d = e - i * ATT_DH;
-    float acc = 0.f;
-    for (int j = 0; j < S; ++j) acc = fmaf(P[i * PL + j], Vs[j * LD + d], acc);
-    a.o[((int64_t)b * S + i) * a.ldo + h * ATT_DH + d] = acc;
-  }
-}
-
-struct AttnBwdArgs {
-  AttnArgs f;
-  const float* out; int64_t ldout;  // forward output O (for D_i = dO_i . O_i)
-  const float* dout; int64_t ldd;
-  float* dq; float* dk; float* dv; int64_t ldg;  // grads in the Q/K/V layout with stride ldg
-};
-
-// LDS: Qs, Ks, Vs, dOs [S][LD], A [S][S+1], Dr [S].  Two phases over one S x S array:
-//   1) A = P_drop (recomputed from lse)          -> dV = A^T dO
-//   2) A = dS = P * (dP - D_i), D_i = dO_i . O_i -> dQ = A K scale, dK = A^T Q scale
-// (sum_j P_ij dP_ij = dO_i . O_i holds with dropout since O = P_drop V).
-__global__ __launch_bounds__(256) void attention_bwd_kernel(AttnBwdArgs ab) {
-  extern __shared__ float sm[];
-  const AttnArgs& a = ab.f;
-  const int S = a.S;
-  constexpr int LD = ATT_DH + 1;
-  const int PL = S + 1;
-  float* Qs = sm;
-  float* Ks = Qs + S * LD;
-  float* Vs = Ks + S * LD;
-  float* dOs = Vs + S * LD;
-  float* A = dOs + S * LD;
-  float* Dr = A + S * PL;
-  const int bh = blockIdx.x;
-  const int b = bh / a.H, h = bh - b * a.H;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int e = tid; e < S * ATT_DH; e += 256) {
-    const int s = e / ATT_DH, d = e - s * ATT_DH;
-    const int64_t r = (int64_t)b * S + s;
-    Qs[s * LD + d] = a.q[r * a.ldq + h * ATT_DH + d];
-    Ks[s * LD + d] = a.k[r * a.ldk + h * ATT_DH + d];
-    Vs[s * LD + d] = a.v[r * a.ldv + h * ATT_DH + d];
-    dOs[s * LD + d] = ab.dout[r * ab.ldd + h * ATT_DH + d];
-  }
-  for (int i = wid; i < S; i += 4) {
-    const int64_t r = (int64_t)b * S + i;
-    float t = 0.f;
-    for (int d = lane; d < ATT_DH; d += 64)
-      t += ab.dout[r * ab.ldd + h * ATT_DH + d] * ab.out[r * ab.ldout + h * ATT_DH + d];
-    t = wave_sum(t);
-    if (lane == 0) Dr[i] = t;
-  }
-  __syncthreads();
-  const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
-  const float dscale = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
-  // phase 1: A = P_drop
-  for (int e = tid; e < S * S; e += 256) {
-    const int i = e / S, j = e - i * S;
-    float s = 0.f;
-#pragma unroll 8
-    for (int d = 0; d < ATT_DH; ++d) s = fmaf(Qs[i * LD + d], Ks[j * LD + d], s);
-    float p = expf(s * a.scale - a.lse[(int64_t)bh * S + i]);
-    if (a.drop_p > 0.f) p = attn_keep(seed, bh, S, i, j, a.drop_p) ? p * dscale : 0.f;
-    A[i * PL + j] = p;
-  }
-  __syncthreads();
-  for (int e = tid; e < S * ATT_DH; e += 256) {
-    const int j = e / ATT_DH, d = e - j * ATT_DH;
-    float dv = 0.f;
-    for (int i = 0; i < S; ++i) dv = fmaf(A[i * PL + j], dOs[i * LD + d], dv);
-    ab.dv[((int64_t)b * S + j) * ab.ldg + h * ATT_DH + d] = dv;
-  }
-  __syncthreads();
-  // phase 2: A = dS
-  for (int e = tid; e < S * S; e += 256) {
-    const int i = e / S, j = e - i * S;
-    float s = 0.f, dp = 0.f;
-#pragma unroll 8
-    for (int d = 0; d < ATT_DH; ++d) {
-      s = fmaf(Qs[i * LD + d], Ks[j * LD + d], s);
-      dp = fmaf(dOs[i * LD + d], Vs[j * LD + d], dp);
-    }
-    const float p = expf(s * a.scale - a.lse[(int64_t)bh * S + i]);
-    if (a.drop_p > 0.f) dp = attn_keep(seed, bh, S, i, j, a.drop_p) ? dp * dscale : 0.f;
-    A[i * PL + j] = p * (dp - Dr[i]);
-  }
-  __syncthreads();
-  for (int e = tid; e < S * ATT_DH; e += 256) {
-    const int i = e / ATT_DH, d = e - i * ATT_DH;
-    float dq = 0.f, dk = 0.f;
-    for (int j = 0; j < S; ++j) {
-      dq = fmaf(A[i * PL + j], Ks[j * LD + d], dq);
-      dk = fmaf(A[j * PL + i], Qs[j * LD + d], dk);
-    }
-    const int64_t r = ((int64_t)b * S + i) * ab.ldg + h * ATT_DH + d;
-    ab.dq[r] = dq * a.scale;
-    ab.dk[r] = dk * a.scale;
-  }
 }
 
 // ---------------------------------------------------------------- embedding
@@ -582,47 +406,6 @@ extern "C" int tvq_layernorm_bwd(const float* dy, const float* x, int64_t M, int
     reduce_rows(workspace + D, nb, D, 2 * D, dbeta, nullptr, 0, (int)accumulate,
                 rs + reduce_rows_scratch(nb, D), st);
   return launch_status("tvq_layernorm_bwd");
-}
-
-extern "C" int tvq_attention_fwd(const float* q, int64_t ldq, const float* k, int64_t ldk,
-                                 const float* v, int64_t ldv, float* o, int64_t ldo, float* lse,
-                                 int64_t B, int64_t H, int64_t S, int64_t Dh, float scale,
-                                 float drop_p, const int64_t* seed_ptr, uint64_t offset,
-                                 tvq_stream_t stream) {
-  TVQ_CHECK_ARG(q && k && v && o && lse && B > 0 && H > 0, "tvq_attention_fwd: bad arguments");
-  TVQ_CHECK_ARG(Dh == ATT_DH && S >= 1 && S <= 104, "tvq_attention_fwd: need Dh=64, S<=104");
-  AttnArgs a;
-  a.q = q; a.k = k; a.v = v; a.ldq = ldq; a.ldk = ldk; a.ldv = ldv;
-  a.o = o; a.ldo = ldo; a.lse = lse;
-  a.B = (int)B; a.H = (int)H; a.S = (int)S; a.scale = scale;
-  a.drop_p = drop_p; a.seed_ptr = seed_ptr; a.offset = offset;
-  const size_t lds = (size_t)(3 * S * (ATT_DH + 1) + S * (S + 1)) * sizeof(float);
-  hipLaunchKernelGGL(attention_fwd_kernel, dim3((unsigned)(B * H)), dim3(256), lds,
-                     (hipStream_t)stream, a);
-  return launch_status("tvq_attention_fwd");
-}
-
-extern "C" int tvq_attention_bwd(const float* q, int64_t ldq, const float* k, int64_t ldk,
-                                 const float* v, int64_t ldv, const float* out, int64_t ldout,
-                                 const float* dout, int64_t ldd,
-                                 const float* lse, int64_t B, int64_t H, int64_t S, int64_t Dh,
-                                 float scale, float drop_p, const int64_t* seed_ptr,
-                                 uint64_t offset, float* dq, float* dk, float* dv, int64_t ldg,
-                                 tvq_stream_t stream) {
-  TVQ_CHECK_ARG(q && k && v && out && dout && lse && dq && dk && dv,
-                "tvq_attention_bwd: bad arguments");
-  TVQ_CHECK_ARG(Dh == ATT_DH && S >= 1 && S <= 104, "tvq_attention_bwd: need Dh=64, S<=104");
-  AttnBwdArgs ab;
-  ab.f.q = q; ab.f.k = k; ab.f.v = v; ab.f.ldq = ldq; ab.f.ldk = ldk; ab.f.ldv = ldv;
-  ab.f.o = nullptr; ab.f.ldo = 0; ab.f.lse = (float*)lse;
-  ab.f.B = (int)B; ab.f.H = (int)H; ab.f.S = (int)S; ab.f.scale = scale;
-  ab.f.drop_p = drop_p; ab.f.seed_ptr = seed_ptr; ab.f.offset = offset;
-  ab.out = out; ab.ldout = ldout;
-  ab.dout = dout; ab.ldd = ldd; ab.dq = dq; ab.dk = dk; ab.dv = dv; ab.ldg = ldg;
-  const size_t lds = (size_t)(4 * S * (ATT_DH + 1) + S * (S + 1) + S) * sizeof(float);
-  hipLaunchKernelGGL(attention_bwd_kernel, dim3((unsigned)(B * H)), dim3(256), lds,
-                     (hipStream_t)stream, ab);
-  return launch_status("tvq_attention_bwd");
 }
 
 extern "C" int tvq_embedding_fwd(const int64_t* idx, int64_t M, int64_t D, const float* table,

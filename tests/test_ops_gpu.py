@@ -259,6 +259,60 @@ def test_linear(M, K, N, res, cuda):
         close(d[i].grad, c[i].grad, what=f"grad{i}")
 
 
+@pytest.mark.parametrize("M,N,K", [(25600, 128, 128), (300, 512, 128), (97, 32, 256), (1000, 64, 32),
+                                   (130, 600, 64), (64, 96, 512), (7, 3, 4), (2000, 384, 128)])
+@pytest.mark.parametrize("epi", ["plain", "bias_gelu_pre", "res_rmod_acc"])
+def test_gemm_nt_epilogues(M, N, K, epi, cuda):
+    """C = epi(alpha A W^T) on the MFMA NT path (A, W k-contiguous) against torch fp32."""
+    from timevqvae.hip.linear import gemm
+    gen = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=gen)
+    W = torch.randn(N, K, generator=gen) / K ** 0.5
+    b = torch.randn(N, generator=gen)
+    R = torch.randn(24, N, generator=gen)
+    C0 = torch.randn(M, N, generator=gen)
+    ref = 0.5 * (A.double() @ W.double().t())
+    kw = {}
+    if epi == "bias_gelu_pre":
+        pre_ref = ref + b.double()
+        ref = F.gelu(pre_ref)
+        pre = torch.empty(M, N, device=cuda)
+        kw = dict(bias=b.to(cuda), act=1, pre=pre)
+    elif epi == "res_rmod_acc":
+        ref = ref + R.double()[torch.arange(M) % 24] + C0.double()
+        kw = dict(R=R.to(cuda), ldr=N, rmod=24, accumulate=True)
+    out = C0.to(cuda) if epi == "res_rmod_acc" else None
+    y = gemm(A.to(cuda), K, 1, W.to(cuda), 1, K, M, N, K, out=out, ldc=N if out is not None else None,
+             alpha=0.5, **kw)
+    err = float((y.cpu().double() - ref).norm() / ref.norm())
+    assert err < 2e-6, err
+    if epi == "bias_gelu_pre":
+        assert float((pre.cpu().double() - pre_ref).norm() / pre_ref.norm()) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K,kind", [(6400, 128, 128, "nn"), (6144, 128, 512, "nn"), (501, 70, 36, "nn"),
+                                        (128, 128, 6400, "tn"), (512, 128, 6144, "tn"),
+                                        (128, 256, 24576, "tn"), (33, 70, 1001, "tn"), (256, 256, 1536, "tn")])
+def test_gemm_nn_tn(M, N, K, kind, cuda):
+    """dX = dY W (nn: B n-contiguous) and dW (+)= dY^T X (tn: split over rows, slabs summed
+    in order) against torch fp64; tn accumulates into an existing buffer (the flat grad)."""
+    from timevqvae.hip.linear import gemm
+    gen = torch.Generator().manual_seed(M * 7 + N + K)
+    C0 = torch.randn(M, N, generator=gen)
+    if kind == "nn":
+        A = torch.randn(M, K, generator=gen)
+        B = torch.randn(K, N, generator=gen) / K ** 0.5
+        y = gemm(A.to(cuda), K, 1, B.to(cuda), N, 1, M, N, K)
+        ref = A.double() @ B.double()
+    else:
+        A = torch.randn(K, M, generator=gen) / K ** 0.5
+        B = torch.randn(K, N, generator=gen)
+        y = gemm(A.to(cuda), 1, M, B.to(cuda), N, 1, M, N, K, out=C0.to(cuda), ldc=N, accumulate=True)
+        ref = A.double().t() @ B.double() + C0.double()
+    err = float((y.cpu().double() - ref).norm() / ref.norm())
+    assert err < 2e-6, err
+
+
 def test_losses(cuda):
     from timevqvae.hip.loss import l1_loss, mse_loss
     for f_hip, f_ref in ((mse_loss, F.mse_loss), (l1_loss, F.l1_loss)):

@@ -73,8 +73,48 @@ def test_rmsnorm_layernorm(cuda):
     assert rel(gd.grad, g.grad) < 1e-5 and rel(bd.grad, b.grad) < 1e-5
 
 
+def _hash_uniform(seed, offset, ctr):
+    """tvq_common.h mix_seed / uniform01 in numpy uint64 (wrapping) arithmetic."""
+    u64 = np.uint64
+    with np.errstate(over="ignore"):
+        s = (u64(seed) * u64(0x9E3779B97F4A7C15)) ^ (u64(offset) * u64(0xC2B2AE3D27D4EB4F)
+                                                    + u64(0x165667B19E3779F9))
+        x = s * u64(0xD1B54A32D192ED03) + ctr.astype(np.uint64)
+        x = x + u64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> u64(30))) * u64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> u64(27))) * u64(0x94D049BB133111EB)
+        x = x ^ (x >> u64(31))
+    return ((x >> u64(32)).astype(np.uint32) >> np.uint32(8)).astype(np.float64) / 16777216.0
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,S,H", [(8, 25, 2), (4, 97, 1), (2, 104, 2), (3, 1, 1)])
+@pytest.mark.parametrize("B,S,H", [(3, 25, 2), (2, 97, 1)])
+def test_attention_dropout_matches_hash_mask(B, S, H, cuda):
+    """Attention dropout: forward and backward both apply the documented counter-hash mask
+    keep(q, k) = U(seed, offset, (bh*S + q)*S + k) >= p, scaled by 1/(1-p)."""
+    from timevqvae.hip import rng
+    from timevqvae.hip.xf import attention
+    p, site = 0.3, 77 << 40
+    (q, k, v), (qd, kd, vd) = _both([(B, S, H * 64)] * 3, cuda, seed=9)
+    seed = int(rng.seed_tensor(cuda).item())
+    offset = (site + rng._calls[0] + 1) & 0xFFFFFFFFFFFFFFFF
+    od = attention(qd, kd, vd, H, drop_p=p, site=site)
+    ctr = np.arange(B * H * S * S, dtype=np.uint64)
+    keep = torch.from_numpy(_hash_uniform(seed, offset, ctr) >= p).reshape(B, H, S, S)
+    sh = lambda t: t.view(B, S, H, 64).transpose(1, 2)
+    a = torch.softmax(sh(q) @ sh(k).transpose(-1, -2) / 8.0, -1) * keep / (1 - p)
+    oc = (a @ sh(v)).transpose(1, 2).reshape(B, S, H * 64)
+    assert rel(od, oc) < 1e-5
+    go = torch.randn(oc.shape)
+    oc.backward(go)
+    od.backward(go.to(cuda))
+    for x, y in ((qd, q), (kd, k), (vd, v)):
+        assert rel(x.grad, y.grad) < 2e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,S,H", [(8, 25, 2), (4, 97, 1), (2, 104, 2), (3, 1, 1), (2, 128, 1),
+                                   (3, 64, 2), (5, 33, 1), (2, 96, 3)])
 def test_attention(B, S, H, cuda):
     from timevqvae.hip.xf import attention
     (q, k, v), (qd, kd, vd) = _both([(B, S, H * 64)] * 3, cuda)

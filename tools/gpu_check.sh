@@ -5,7 +5,7 @@
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 ${TVQ_TEST_TIMEOUT:-900} python -u -m pytest tests -v -m gpu --timeout 120 \
-  --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+  --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 grep -E "FAILED|ERROR|passed|failed" gpurun_out/pytest_gpu.log | tail -30
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
