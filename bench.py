@@ -179,6 +179,83 @@ class JointTrainer:
         self.graph = StepGraph([seg1, seg2], [between1, None], warmup=2, before=before).capture()
 
 
+class Stage1Trainer:
+    """Stage1 alone (BASELINE configs[0]: T=128, K=256, configs/config.yaml widths), one
+    hipGraph per step like JointTrainer: [advance seed, zero_grad, LF | HF fwd+bwd] ->
+    [AdamW]."""
+
+    def __init__(self, device, B_, T_, K_):
+        from timevqvae.trainers import Stage1
+        from timevqvae.hip import rng
+        from timevqvae.hip.conv import PackCache
+        from timevqvae.utils import set_seed
+        set_seed(0)
+        rng.manual_seed(1)
+        cfg = config(False)
+        cfg["VQ-VAE"]["codebook_sizes"] = {"lf": K_, "hf": K_}
+        self.s1 = Stage1(T_, C, cfg).to(device).train()
+        self.opt = self.s1.configure_optimizers()["optimizer"]
+        self.device = device
+        self.packs = PackCache(device)
+        g = torch.Generator().manual_seed(1234)
+        x = torch.cumsum(0.1 * torch.randn(B_, C, T_, generator=g), -1)
+        x = 2 * (x - x.amin(0, keepdim=True)) / (x.amax(0, keepdim=True) - x.amin(0, keepdim=True) + 1e-8) - 1
+        self.batch = (x.to(device), torch.randint(0, N_CLASSES, (B_, 1), generator=g).to(device))
+        self.graph = None
+
+    def capture(self):
+        from timevqvae.hip import rng, streams
+        from timevqvae.hip.graph import StepGraph
+        sched = self.s1._sched
+        self.s1._sched = None
+
+        def before():
+            sched.step()
+            self.opt.push_lr()
+
+        def seg1():
+            rng.advance(self.device)
+            self.opt.zero_grad()
+            with self.packs.scope(), streams.concurrent():
+                hist = self.s1.forward_backward(self.batch, 0)
+            return hist()
+
+        def seg2():
+            self.opt.step(lr_on_device=True)
+
+        self.graph = StepGraph([seg1, seg2], [None, None], warmup=2, before=before).capture()
+
+    def timed(self, steps=20, warmup=3):
+        for _ in range(warmup):
+            self.graph.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.graph.replay()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+
+
+def config0_leg(device, cpu=True):
+    """BASELINE configs[0] (stage1 VQ-VAE, T=128, K=256, config.yaml widths; the
+    reference's CPU-runnable case) on the GPU at the config.yaml batch (32) and at 256,
+    with the CPU port timed beside it (oracle/cpu_baseline.measure_stage1)."""
+    out = {}
+    for b in (32, 256):
+        tr = Stage1Trainer(device, b, 128, 256)
+        tr.capture()
+        out[f"B{b}_ms_per_step"] = round(tr.timed() * 1e3, 3)
+        del tr
+    if cpu:
+        from oracle import cpu_baseline
+        threads = int(os.environ.get("TVQ_CPU_THREADS", min(16, os.cpu_count() or 1)))
+        for b in (32, 256):
+            s = cpu_baseline.measure_stage1(threads, b, 128, 256, steps=2, warmup=1)
+            out[f"cpu_B{b}_ms_per_step"] = round(s * 1e3, 1)
+        out["cpu_cores"] = threads
+    return out
+
+
 def roofline_leg(device):
     """Average duration of the dominant conv op at its step shape, on the stream it runs on
     (HIP events), with its algorithmic FLOPs -> achieved / peak.
@@ -272,8 +349,9 @@ def cpu_baseline_leg():
     s = cpu_baseline.measure(threads, steps=2, warmup=1)
     return {"value": round(1.0 / s, 4), "unit": "steps/s", "cores": threads, "kind": "port",
             "sample": f"2 timed joint steps (after 1 warmup) of oracle/cpu_baseline.py at B=256,C=6,"
-                      f"T=256,K=512 on {threads} torch threads: {s:.3f} s/step; transformer "
-                      f"dropouts off in the restatement"}
+                      f"T=256,K=512 on {threads} torch threads, every reference dropout on: "
+                      f"{s:.3f} s/step (the port runs 0.77x the reference's own stage1 time "
+                      f"and 0.97x its stage2 time at 8 threads, profiles/r02_cpu_ref_compare.json)"}
 
 
 def main():
@@ -284,6 +362,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-sampler", action="store_true")
+    ap.add_argument("--no-config0", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     args = ap.parse_args()
 
@@ -345,6 +424,8 @@ def main():
             res["roofline"] = roofline_leg(device)
         if not args.no_sampler:
             res["sampler"] = sampler_leg(tr, device)
+        if not args.no_config0 and world == 1:
+            res["config0"] = config0_leg(device, cpu=not args.no_cpu_baseline)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline_leg()
         print(json.dumps(res), flush=True)

@@ -3,9 +3,11 @@ restated on torch CPU (the `cpu_baseline` leg of bench.py; "port" kind).
 
 Same work as one product joint step: stage1 forward/backward/AdamW
 (trainers/stage1.py:89-236) then stage2 forward/backward/AdamW with the frozen
-stage1 encoders (trainers/stage2.py:49-68, models/maskgit.py:155-216), dropout
-as in the reference (ResBlock 0.3; transformer dropouts off because the
-x-transformers restatement is inference-exact only — noted in the sample string).
+stage1 encoders (trainers/stage2.py:49-68, models/maskgit.py:155-216), dropouts as
+in the reference: ResBlock 0.3; in the priors token-embedding, attention, FF and layer
+dropout 0.3 and the classifier-free-guidance class drop 0.2
+(configs/config.yaml:48-64).  tools/cpu_ref_compare.py times its stage1 / stage2 halves
+against the reference's own files in the build container (DESIGN.md §CPU baseline).
 """
 import time
 
@@ -128,7 +130,9 @@ class JointStep:
         self.rng = np.random.default_rng(0)
 
     def step(self):
-        # ---- stage1
+        return self.step_stage1(), self.step_stage2()
+
+    def step_stage1(self):
         self.opt1.zero_grad()
         ctx = O.Ctx(True, dropout_p=0.3)
         out = O.stage1_forward(ctx, self.sd1, self.spec, self.x)
@@ -137,7 +141,10 @@ class JointStep:
         with torch.no_grad():
             for k, v in ctx.updates.items():
                 self.sd1[k] = v.detach()
-        # ---- stage2 (frozen stage1 snapshot, eval)
+        return float(out["loss"].detach())
+
+    def step_stage2(self, drop=0.3, p_uncond=0.2):
+        """frozen stage1 snapshot (eval) -> tokens -> masking -> priors -> masked CE."""
         self.opt2.zero_grad()
         with torch.no_grad():
             e = O.Ctx(False)
@@ -149,12 +156,17 @@ class JointStep:
         sMl, kl = O.random_mask_tokens(s_l, self.K, self.rng.uniform(0, 1, B), torch.rand(s_l.shape))
         sMh, kh = O.random_mask_tokens(s_h, self.K, self.rng.uniform(0, 1, B), torch.rand(s_h.shape))
         c = O.Ctx(True)
-        ll = O.transformer_forward(c, self.xl, "lf", sMl, None, self.y, self.K, 2, 4)
-        lh = O.transformer_forward(c, self.xh, "hf", sMl, sMh, self.y, self.K, 1, 1)
+        uncond = torch.full_like(self.y, 5)
+        ll = O.transformer_forward(c, self.xl, "lf", sMl, None,
+                                   torch.where(torch.rand(self.y.shape) > p_uncond, self.y, uncond),
+                                   self.K, 2, 4, drop=drop)
+        lh = O.transformer_forward(c, self.xh, "hf", sMl, sMh,
+                                   torch.where(torch.rand(self.y.shape) > p_uncond, self.y, uncond),
+                                   self.K, 1, 1, drop=drop)
         loss = O.masked_ce(ll, s_l, kl) + O.masked_ce(lh, s_h, kh)
         loss.backward()
         self.opt2.step()
-        return float(out["loss"]), float(loss)
+        return float(loss.detach())
 
 
 def measure(threads, steps=2, warmup=1, B=256):
@@ -166,6 +178,19 @@ def measure(threads, steps=2, warmup=1, B=256):
     t0 = time.perf_counter()
     for _ in range(steps):
         js.step()
+    return (time.perf_counter() - t0) / steps
+
+
+def measure_stage1(threads, B, T, K, steps=2, warmup=1):
+    """Seconds per stage1 train step (BASELINE configs[0]: T=128, K=256, config.yaml
+    widths) of the CPU restatement."""
+    torch.set_num_threads(threads)
+    js = JointStep(B=B, T=T, K=K)
+    for _ in range(warmup):
+        js.step_stage1()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        js.step_stage1()
     return (time.perf_counter() - t0) / steps
 
 

@@ -409,11 +409,16 @@ def xf_rmsnorm(x, g):
     return F.normalize(x, dim=-1) * (x.shape[-1] ** 0.5) * g
 
 
-def xf_blocks(sd, p, x, heads, depth):
-    """ContinuousTransformerWrapper(project_in, post_emb_norm, Encoder(pre_norm), project_out)."""
+def xf_blocks(sd, p, x, heads, depth, drop=0.0):
+    """ContinuousTransformerWrapper(project_in, post_emb_norm, Encoder(pre_norm), project_out).
+    drop > 0 (training): x-transformers' layer dropout (skip a branch with prob `drop`,
+    host random() as the reference), attention-probability and FF dropout at `drop`."""
+    import random
     h = F.linear(x, sd[p + "project_in.weight"])
     h = F.layer_norm(h, h.shape[-1:]) * sd[p + "post_emb_norm.gamma"]
     for i in range(2 * depth):
+        if drop > 0 and random.random() < drop:
+            continue
         q = f"{p}attn_layers.layers.{i}."
         n = xf_rmsnorm(h, sd[q + "0.0.g"])
         if i % 2 == 0:
@@ -422,10 +427,14 @@ def xf_blocks(sd, p, x, heads, depth):
             kk = F.linear(n, sd[q + "1.to_k.weight"]).view(B, S, heads, 64).transpose(1, 2)
             vv = F.linear(n, sd[q + "1.to_v.weight"]).view(B, S, heads, 64).transpose(1, 2)
             att = torch.softmax(qq @ kk.transpose(-1, -2) * 64 ** -0.5, dim=-1)
+            if drop > 0:
+                att = F.dropout(att, drop)
             o = (att @ vv).transpose(1, 2).reshape(B, S, heads * 64)
             out = F.linear(o, sd[q + "1.to_out.weight"])
         else:
             u = F.gelu(F.linear(n, sd[q + "1.ff.0.0.weight"], sd[q + "1.ff.0.0.bias"]))
+            if drop > 0:
+                u = F.dropout(u, drop)
             out = F.linear(u, sd[q + "1.ff.2.weight"], sd[q + "1.ff.2.bias"])
         h = h + out
     h = xf_rmsnorm(h, sd[p + "attn_layers.final_norm.g"])
@@ -442,19 +451,25 @@ def upscale(ctx, sd, p, x, m):
     return x.transpose(1, 2)
 
 
-def transformer_forward(ctx, sd, kind, s_l, s_h, cls_idx, K, heads, depth):
-    """forward_lf / forward_hf (bidirectional_transformer.py:166-236), dropout off;
-    cls_idx (b,1) is the (already drop-resolved) class index (n_classes = uncond)."""
-    tok = F.embedding(s_l, sd["tok_emb_l.weight"])
+def transformer_forward(ctx, sd, kind, s_l, s_h, cls_idx, K, heads, depth, drop=0.0):
+    """forward_lf / forward_hf (bidirectional_transformer.py:166-236); cls_idx (b,1) is the
+    (already drop-resolved) class index (n_classes = uncond).  drop > 0: the reference's
+    training-time dropouts at that rate (token-embedding dropout on non-mask tokens,
+    :152-164, and the encoder's, xf_blocks) with torch's CPU RNG; 0: deterministic."""
+    def tok_drop(s, e, mask_id):
+        if drop <= 0:
+            return e
+        return torch.where((s == mask_id)[:, :, None], e, F.dropout(e, drop))
+    tok = tok_drop(s_l, F.embedding(s_l, sd["tok_emb_l.weight"]), K)
     table = "tok_emb_l.weight"
     if kind == "hf":
-        th = F.embedding(s_h, sd["tok_emb_h.weight"])
+        th = tok_drop(s_h, F.embedding(s_h, sd["tok_emb_h.weight"]), K)
         tok = torch.cat([upscale(ctx, sd, "projector.", tok, th.shape[1]), th], dim=-1)
         table = "tok_emb_h.weight"
     cls = F.embedding(cls_idx, sd["class_condition_emb.weight"])
     n = tok.shape[1]
     x = torch.cat([cls, tok + sd["pos_emb.weight"][:n]], dim=1)
-    x = xf_blocks(sd, "blocks.", x, heads, depth)
+    x = xf_blocks(sd, "blocks.", x, heads, depth, drop)
     x = F.linear(x, sd["pred_head.0.weight"], sd["pred_head.0.bias"])
     x = F.layer_norm(F.gelu(x), x.shape[-1:], sd["pred_head.2.weight"], sd["pred_head.2.bias"], 1e-12)
     x = x[:, 1:, :]

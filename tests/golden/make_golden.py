@@ -691,10 +691,14 @@ def main():
     if sys.argv[1:] == ["stage2"]:  # regenerate only G9
         gen_stage2(ref)
         return
+    if sys.argv[1:] == ["cfgA"]:  # regenerate only G3 at BASELINE configs[0]
+        gen_stage1(ref, "cfgA", B=4, C=6, T=128, K=256, init_dim=4, hid_dim=128, seed=7)
+        return
     gen_vq(ref)
     gen_stft(ref)
     gen_stage1(ref, "small", B=4, C=6, T=128, K=64, init_dim=4, hid_dim=32, seed=3)
     gen_stage1(ref, "cfgB", B=2, C=6, T=256, K=512, init_dim=4, hid_dim=128, seed=5)
+    gen_stage1(ref, "cfgA", B=4, C=6, T=128, K=256, init_dim=4, hid_dim=128, seed=7)
     gen_maskgit(ref)
     gen_svq(ref)
     gen_rocket()

@@ -13,7 +13,7 @@ import torch
 from conftest import golden
 from param_init import fill_state_dict
 
-TAGS = ["small", "cfgB"]
+TAGS = ["small", "cfgB", "cfgA"]  # cfgA: BASELINE configs[0] (T=128, K=256, hid 128)
 
 
 def make_config(K, init_dim, hid_dim):
@@ -83,7 +83,8 @@ def test_stage1_eval_reconstruction(tag, cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tag,flat", [("small", False), ("cfgB", False), ("cfgB", True)])
+@pytest.mark.parametrize("tag,flat", [("small", False), ("cfgB", False), ("cfgB", True),
+                                      ("cfgA", True)])
 def test_stage1_train_step_grads(tag, flat, cuda):
     """flat=True: FusedAdamW owns the gradients (kernels accumulate into the flat buffer)."""
     m, g = build(tag, cuda)

@@ -237,7 +237,7 @@ def test_masked_prediction_cfg_vs_reference(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tag", ["small", "cfgB"])
+@pytest.mark.parametrize("tag", ["small", "cfgB", "cfgA"])
 def test_encode_tokens_vs_reference(tag, cuda):
     """M1: MaskGIT's fused encode (one STFT pass, eval encoders, VQ assign) gives the
     reference's quantize() indices of G3 (encode_to_z_q, maskgit.py:117-134)."""

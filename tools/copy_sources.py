@@ -14,14 +14,26 @@ import bench  # noqa: E402
 
 
 def main():
+    """`python tools/copy_sources.py [sampler]`: the joint step, or one sampling batch."""
     dev = torch.device("cuda", 0)
     tr = bench.JointTrainer(dev, 1)
     batch = bench.synthetic_batch(1234, dev)
+    if sys.argv[1:] == ["sampler"]:
+        mg = tr.s2.maskgit.eval()
+
+        def work():
+            with torch.no_grad():
+                s_l, s_h = mg.iterative_decoding(num=1024, device=dev)
+                mg.decode_token_ind_to_timeseries(s_l, "lf")
+                mg.decode_token_ind_to_timeseries(s_h, "hf")
+    else:
+        def work():
+            tr.step(batch)
     for _ in range(2):
-        tr.step(batch)
+        work()
     torch.cuda.synchronize()
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
-        tr.step(batch)
+        work()
         torch.cuda.synchronize()
     sites = collections.Counter()
     kern = collections.Counter()
