@@ -256,8 +256,87 @@ def config0_leg(device, cpu=True):
     return out
 
 
-def roofline_leg(device):
-    """Average duration of the dominant conv op at its step shape, on the stream it runs on
+# Algorithmic FLOPs of one joint step at B=256 (matmul/conv work of stage1 fwd+bwd and
+# stage2 with every prior branch run): tools/count_step_flops.py over the CPU restatement
+# of the same module tree -> profiles/r02_step_flops.json (169.78 GFLOP).
+STEP_GFLOP = 169.78
+FP32_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0
+
+
+def _graph_time_us(fns, reps):
+    """Average device time per launch of `fns` (each called `reps` times, interleaved),
+    captured in one hipGraph on a side stream and timed with HIP events recorded on that
+    same stream (the host launch cost of the ctypes calls is not in the region)."""
+    st = torch.cuda.Stream(device=torch.cuda.current_device())
+    with torch.cuda.stream(st):
+        for f in fns:
+            f()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            for _ in range(reps):
+                for f in fns:
+                    f()
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(5):
+            g.replay()
+        e1.record(st)
+        torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (5 * reps * len(fns))
+
+
+def dominant_leg(device):
+    """The step's dominant kernel (profiles/r02_step_kernel_stats.csv, first row):
+    conv_halo_kernel<F,3,3,1,...,FN=1,KS=1>, the forward of every ResBlock 3x3 conv with
+    8 or 16 channels (LF/HF encoders + decoders + stage2's frozen encoders: 49 launches per
+    step).  Its two step shapes, (256,8,3,64)x(8,8,3,3) and (256,16,3,32)x(16,16,3,3), move
+    the same algorithmic bytes per launch (input + output + weight + bias, fp32 = 3.15 MB)
+    at 56.6 / 56.6 MFLOP: HBM-class (arithmetic intensity 18 FLOP/B).  Timed here as 2x25
+    graph-replayed launches with HIP events on their stream."""
+    from timevqvae.hip.conv import conv2d
+    fns, byts = [], 0
+    for Ci, W in ((8, 64), (16, 32)):
+        x = torch.randn(B, Ci, 3, W, device=device)
+        w = torch.randn(Ci, Ci, 3, 3, device=device) * 0.1
+        b = torch.zeros(Ci, device=device)
+        fns.append(lambda x=x, w=w, b=b: conv2d(x, w, b))
+        byts += 4 * (2 * x.numel() + w.numel() + b.numel())
+    with torch.no_grad():
+        us = _graph_time_us(fns, 25)
+    per_launch = byts / 2
+    achieved = per_launch / (us * 1e-6) / 1e9
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "r02_dominant_traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath))["traffic_bytes"]
+    return {"bound": "hbm", "kernel": "conv_halo_kernel<0,3,3,1,false,1,1> (ResBlock 3x3 conv "
+                                      "fwd, C=8 @W64 and C=16 @W32, B=256)",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "algorithmic_bytes": per_launch, "avg_launch_us": round(us, 2)}
+
+
+def roofline_leg(device, ms_per_step):
+    """bench JSON `roofline`: the step's dominant kernel (dominant_leg) at top level, the
+    whole step against the fp32 MFMA peak (`step`), and the largest single conv on MFMA
+    (`conv_t32`, conv_t32_leg)."""
+    out = dominant_leg(device)
+    tf = STEP_GFLOP / ms_per_step  # GFLOP / ms = TFLOP/s
+    out["step"] = {"bound": "mfma", "gflop": STEP_GFLOP, "achieved": round(tf, 2),
+                   "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                   "frac": round(tf / FP32_PEAK_TFLOPS, 4),
+                   "source": "tools/count_step_flops.py -> profiles/r02_step_flops.json"}
+    out["step_frac"] = out["step"]["frac"]
+    out["conv_t32"] = conv_t32_leg(device)
+    return out
+
+
+def conv_t32_leg(device):
+    """Average duration of the largest conv op at its step shape, on the stream it runs on
     (HIP events), with its algorithmic FLOPs -> achieved / peak.
 
     The op is the HF encoder ResBlock(16->128) second conv, (256,128,3,32) x (128,128,3,3):
@@ -421,7 +500,7 @@ def main():
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 3),
         }
         if not args.no_roofline:
-            res["roofline"] = roofline_leg(device)
+            res["roofline"] = roofline_leg(device, res["ms_per_step"])
         if not args.no_sampler:
             res["sampler"] = sampler_leg(tr, device)
         if not args.no_config0 and world == 1:

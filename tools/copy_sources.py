@@ -1,5 +1,6 @@
-"""Attribute device copies (aten::copy_ / clone / contiguous) of the joint step to Python
-call sites with torch.profiler.  usage: python tools/copy_sources.py"""
+"""Attribute device copies (aten::copy_ / clone / contiguous) and every other PyTorch-native
+kernel of the joint step to Python call sites with torch.profiler.
+usage: python tools/copy_sources.py [sampler]"""
 import collections
 import os
 import sys
@@ -43,7 +44,7 @@ def main():
             continue
         for k in ks:
             kern[k[:60]] += 1
-        if not any(("opy" in k or "emcpy" in k or "emset" in k) for k in ks):
+        if not any(("opy" in k or "emcpy" in k or "emset" in k or "at::native" in k) for k in ks):
             continue
         stack = [f for f in (ev.stack or []) if "site-packages" not in f and "dist-packages" not in f]
         sites[(ev.name, " | ".join(stack[:3]) if stack else "?", ks[0][:30])] += 1

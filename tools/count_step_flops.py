@@ -1,0 +1,48 @@
+"""Algorithmic FLOPs of one joint train step, counted with torch.utils.flop_counter over the
+CPU restatement of the same module tree (oracle/cpu_baseline.JointStep: config.yaml
+architecture, K=512, T=256, C=6), at a small batch and scaled per trajectory.
+
+Counted: every conv / matmul / bmm / addmm of stage1 forward+backward and of stage2 (frozen
+encoders forward, both priors forward+backward); not counted: FFTs, norms, elementwise work and
+the optimizer.  The VQ distance matmul (2*K*hid per token) is counted; the restatement's
+one-hot EMA matmul (vq.py:229's embed_sum as onehot.T @ x) is subtracted, since the EMA is a
+segmented sum, not a GEMM.  Stage2 is counted
+with layer dropout off (every branch run: the upper bound of the per-step work).
+
+usage: python tools/count_step_flops.py [B] > profiles/r02_step_flops.json"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+from torch.utils.flop_counter import FlopCounterMode  # noqa: E402
+
+from oracle import cpu_baseline  # noqa: E402
+
+
+def count(fn):
+    with FlopCounterMode(display=False) as fc:
+        fn()
+    return fc.get_total_flops(), {str(k): v for k, v in fc.get_flop_counts()["Global"].items()}
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    torch.manual_seed(0)
+    js = cpu_baseline.JointStep(B=B)
+    f1, by1 = count(js.step_stage1)
+    f2, by2 = count(lambda: js.step_stage2(drop=0.0))
+    K, hid = 512, 128
+    tokens = B * (3 * 8 + 3 * 32)  # LF 3x8 and HF 3x32 token grids
+    f1 -= 2 * hid * tokens * K  # one-hot EMA matmul of the restatement (stage1 only)
+    out = {"batch_counted": B,
+           "stage1_gflop_per_traj": f1 / B / 1e9, "stage2_gflop_per_traj": f2 / B / 1e9,
+           "step_gflop_at_B256": (f1 + f2) / B * 256 / 1e9,
+           "stage1_by_op": by1, "stage2_by_op": by2}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,4 +1,5 @@
-"""Run only bench.roofline_leg (for rocprofv3 --pmc passes on the dominant kernel)."""
+"""Run only one roofline leg of bench.py (for rocprofv3 --pmc passes on that kernel).
+usage: python tools/roofline_only.py [dominant|t32]"""
 import json
 import os
 import sys
@@ -11,4 +12,6 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 if __name__ == "__main__":
-    print(json.dumps(bench.roofline_leg(torch.device("cuda", 0))))
+    leg = sys.argv[1] if len(sys.argv) > 1 else "dominant"
+    fn = bench.dominant_leg if leg == "dominant" else bench.conv_t32_leg
+    print(json.dumps(fn(torch.device("cuda", 0))))
