@@ -8,6 +8,7 @@ EMA all-reduce), weak scaling (global batch 256*N).  Rank 0 prints ONE JSON line
 """
 import argparse
 import copy
+import gc
 import json
 import os
 import sys
@@ -274,10 +275,15 @@ def _graph_time_us(fns, reps):
             f()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=st):
-            for _ in range(reps):
-                for f in fns:
-                    f()
+        gc.collect()
+        gc.disable()  # see timevqvae.hip.graph.StepGraph.capture
+        try:
+            with torch.cuda.graph(g, stream=st):
+                for _ in range(reps):
+                    for f in fns:
+                        f()
+        finally:
+            gc.enable()
         g.replay()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -286,7 +292,10 @@ def _graph_time_us(fns, reps):
             g.replay()
         e1.record(st)
         torch.cuda.synchronize()
-    return e0.elapsed_time(e1) * 1e3 / (5 * reps * len(fns))
+    us = e0.elapsed_time(e1) * 1e3 / (5 * reps * len(fns))
+    del g
+    torch.cuda.synchronize()
+    return us
 
 
 def dominant_leg(device):

@@ -244,6 +244,39 @@ int tvq_snake_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t
 int tvq_dropout_bwd(const float* dy, int64_t n, float p, const int64_t* seed_ptr,
                     uint64_t offset, float* dx, tvq_stream_t stream);
 
+/* ---- fused small-channel ResBlock (vq_vae.py:13-62), C_in == C_out = C in {8,16,32}, H = 3,
+ * W in {16,32,64}, C*W <= 1024 (csrc/tvq_resblock.hip):
+ *   y = x + Dropout_p(conv2(Snake_a2(BN(conv1(Snake_a1(x)) + b1))) + b2)
+ * replaces tvq_snake_fwd + tvq_conv2d_fwd + tvq_bn_train_fwd + tvq_conv2d_fwd(residual,
+ * dropout) and their backward.  Weights (C,C,3,3), a1/a2/biases/BN params (C,). */
+/* bytes of workspace for B images, or -1 when the shape is not supported */
+int64_t tvq_resblock_workspace(int64_t B, int64_t C, int64_t H, int64_t W);
+/* training forward: h (B,C,3,W) = conv1 output (kept for backward), y (B,C,3,W), save
+ * (4C floats) = batch mean | invstd | BN scale | BN shift; running stats updated in place
+ * (momentum, unbiased var, num_batches_tracked += 1) */
+int tvq_resblock_train_fwd(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
+                           const float* a1, const float* w1, const float* b1, const float* bn_w,
+                           const float* bn_b, float* running_mean, float* running_var,
+                           int64_t* num_batches_tracked, float momentum, float eps,
+                           const float* a2, const float* w2, const float* b2, float drop_p,
+                           const int64_t* seed_ptr, uint64_t offset, float* h, float* y,
+                           float* save, void* workspace, tvq_stream_t stream);
+/* eval forward (BN from the running statistics, no dropout), one launch */
+int tvq_resblock_eval_fwd(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
+                          const float* a1, const float* w1, const float* b1, const float* bn_w,
+                          const float* bn_b, const float* running_mean,
+                          const float* running_var, float eps, const float* a2, const float* w2,
+                          const float* b2, float* y, tvq_stream_t stream);
+/* backward from dy: dx and every parameter gradient (written, or added when accumulate);
+ * dbn_w / dbn_b may be NULL.  The workspace must stay alive until an open
+ * tvq_conv_wgrad_defer scope is flushed (the weight-gradient slab sums are batched there). */
+int tvq_resblock_bwd(const float* dy, const float* x, const float* h, int64_t B, int64_t C,
+                     int64_t H, int64_t W, const float* a1, const float* w1, const float* bn_w,
+                     const float* save, const float* a2, const float* w2, float drop_p,
+                     const int64_t* seed_ptr, uint64_t offset, float* dx, float* da1, float* dw1,
+                     float* db1, float* dbn_w, float* dbn_b, float* da2, float* dw2, float* db2,
+                     int64_t accumulate, void* workspace, tvq_stream_t stream);
+
 /* deterministic column sums of a P x N slab: out[j] (+)= sum_p in[p*ld + j]
  * (workspace: tvq_reduce_rows_workspace floats, may be 0). */
 int64_t tvq_reduce_rows_workspace(int64_t P, int64_t N);

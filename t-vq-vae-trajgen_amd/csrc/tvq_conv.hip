@@ -20,6 +20,7 @@
 // flight during the current step's MFMAs.
 #include "tvq_common.h"
 #include "tvq_reduce.h"
+#include "tvq_conv_internal.h"
 
 #include <stdlib.h>
 
@@ -1976,6 +1977,11 @@ static void wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, floa
   }
   reduce_rows(slab, splits, N * kcols, N * kcols, dw, db, L, accumulate,
               slab + (int64_t)splits * N * kcols, st);
+}
+
+void tvq::conv_wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, float* dw, float* db,
+                       int accumulate, hipStream_t st) {
+  wgrad_finish(slab, splits, N, kcols, dw, db, accumulate, st);
 }
 
 // Conv2d weight (+bias) gradient: dW[co,ci,kh,kw] (+)= sum dY[b,co,h,wo] X[b,ci,h+kh-PH, wo*SW+kw-PW],

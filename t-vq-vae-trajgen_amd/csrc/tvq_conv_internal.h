@@ -1,0 +1,13 @@
+// Internal (non-ABI) entry points of the conv engine used by other kernel files.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tvq {
+// Deterministic split sum of a weight-gradient slab slab[s][n][kcols] (s < splits) into
+// dw[n][kcols-1] (+ db[n] from the last column when db != null); batched into the open
+// tvq_conv_wgrad_defer scope when there is one.  reduce_rows_scratch(splits, N*kcols)
+// floats of scratch must follow the slab.
+void conv_wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, float* dw, float* db,
+                       int accumulate, hipStream_t st);
+}  // namespace tvq

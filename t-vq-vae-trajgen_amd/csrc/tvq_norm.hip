@@ -10,6 +10,7 @@
 // Backward recomputes the BN output from x and (mean, invstd); reductions are
 // fixed-order (deterministic).
 #include "tvq_common.h"
+#include "tvq_bn.h"
 
 namespace tvq {
 
@@ -27,63 +28,6 @@ static int bn_chunks(int64_t B, int64_t HW) {
 __device__ __forceinline__ int64_t chan_off(int i, int C, int c, int HW, const Div16& dhw) {
   const int b = div16(i, dhw);
   return ((int64_t)b * C + c) * HW + (i - b * HW);
-}
-
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-__device__ __forceinline__ double block_sum_d(double v, double* red) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  __syncthreads();
-  if (lane == 0) red[wid] = v;
-  __syncthreads();
-  double t = 0.0;
-  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
-  return t;
-}
-
-struct BNFinal {  // per-channel finalize of the training statistics
-  int C, chunks;
-  int64_t N;
-  float eps, momentum;
-  const float *w, *b;
-  float *rmean, *rvar;
-  int64_t* nbt;
-  float *save_mean, *save_invstd, *scale, *shift;
-};
-
-// one wave (lane 0..63) finalizes channel c: lanes stride the chunk partials, fixed
-// xor-tree combine; running stats with momentum, unbiased running var
-__device__ __forceinline__ void bn_final_channel(const double* part, int c, int lane,
-                                                 const BNFinal& f) {
-  if (c == 0 && lane == 0 && f.nbt) f.nbt[0] += 1;
-  double s1 = 0.0, s2 = 0.0;
-  for (int i = lane; i < f.chunks; i += 64) {
-    s1 += ld_wt(part + ((int64_t)c * f.chunks + i) * 2 + 0);
-    s2 += ld_wt(part + ((int64_t)c * f.chunks + i) * 2 + 1);
-  }
-  s1 = wave_sum_d(s1);
-  s2 = wave_sum_d(s2);
-  if (lane != 0) return;
-  const double mean = s1 / (double)f.N;
-  double var = s2 / (double)f.N - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const double invstd = 1.0 / sqrt(var + (double)f.eps);
-  if (f.rmean) {
-    const double unb = f.N > 1 ? var * (double)f.N / (double)(f.N - 1) : var;
-    f.rmean[c] = (float)((1.0 - f.momentum) * f.rmean[c] + f.momentum * mean);
-    f.rvar[c] = (float)((1.0 - f.momentum) * f.rvar[c] + f.momentum * unb);
-  }
-  const float sc = (float)((double)(f.w ? f.w[c] : 1.f) * invstd);
-  f.save_mean[c] = (float)mean;
-  f.save_invstd[c] = (float)invstd;
-  f.scale[c] = sc;
-  f.shift[c] = (f.b ? f.b[c] : 0.f) - (float)mean * sc;
 }
 
 // partial [c][chunk][2] = (sum x, sum x^2); with `cnt`, the last block of channel c
@@ -161,33 +105,6 @@ __global__ __launch_bounds__(256) void affine_snake_kernel(const float* __restri
     if (a) s = snake_fwd(s, a[c]);
     y[i] = s;
   }
-}
-
-struct BNBwdFinal {
-  int C, chunks;
-  float *coef, *dw, *db, *da;
-  int accumulate;
-};
-
-// coef[c] = (sum ds, sum ds*xhat) and the parameter grads of channel c (one wave)
-__device__ __forceinline__ void bn_bwd_final_channel(const double* part, int c, int lane,
-                                                     const BNBwdFinal& f) {
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  for (int i = lane; i < f.chunks; i += 64) {
-    const double* pp = part + ((int64_t)c * f.chunks + i) * 3;
-    s0 += ld_wt(pp + 0);
-    s1 += ld_wt(pp + 1);
-    s2 += ld_wt(pp + 2);
-  }
-  s0 = wave_sum_d(s0);
-  s1 = wave_sum_d(s1);
-  s2 = wave_sum_d(s2);
-  if (lane != 0) return;
-  f.coef[2 * c] = (float)s0;
-  f.coef[2 * c + 1] = (float)s1;
-  if (f.dw) f.dw[c] = f.accumulate ? f.dw[c] + (float)s1 : (float)s1;
-  if (f.db) f.db[c] = f.accumulate ? f.db[c] + (float)s0 : (float)s0;
-  if (f.da) f.da[c] = f.accumulate ? f.da[c] + (float)s2 : (float)s2;
 }
 
 // backward partials: [c][chunk][3] = (sum ds, sum ds*xhat, sum da-term); with `cnt`
@@ -283,14 +200,6 @@ __global__ __launch_bounds__(256) void snake_fwd_kernel(const float* __restrict_
     y[i] = snake_fwd(x[i], a[div16(i, dhw) % C]);
 }
 
-__device__ __forceinline__ void snake_bwd_final_channel(const double* part, int C, int chunks,
-                                                        int c, float* da, int accumulate) {
-  double s = 0.0;
-  for (int i = threadIdx.x; i < chunks; i += 64) s += ld_wt(part + (int64_t)c * chunks + i);
-  s = wave_sum_d(s);
-  if (threadIdx.x == 0) da[c] = accumulate ? da[c] + (float)s : (float)s;
-}
-
 // dx (elementwise) and per-(channel, chunk) partials of da; with `cnt` the last block
 // of channel c sums them into da[c]
 __global__ __launch_bounds__(256) void snake_bwd_kernel(const float* __restrict__ dy,
@@ -350,6 +259,18 @@ __global__ void dropout_bwd_kernel(const float* __restrict__ dy, int64_t n, floa
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     dx[i] = (uniform01(seed, (uint64_t)i) >= p) ? dy[i] * scale : 0.f;
+}
+
+void bn_stats_final_launch(const double* part, const BNFinal& f, hipStream_t st) {
+  hipLaunchKernelGGL(bn_stats_final_kernel, dim3(f.C), dim3(64), 0, st, part, f);
+}
+void bn_bwd_final_launch(const double* part, const BNBwdFinal& f, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(f.C), dim3(64), 0, st, part, f);
+}
+void snake_da_final_launch(const double* part, int C, int chunks, float* da, int accumulate,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(snake_bwd_final_kernel, dim3(C), dim3(64), 0, st, part, C, chunks, da,
+                     accumulate);
 }
 
 static dim3 ew_grid(int64_t n) {

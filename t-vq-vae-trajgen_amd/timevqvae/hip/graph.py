@@ -11,6 +11,8 @@ Everything inside a segment must be capturable: no host synchronisation, device-
 randomness only (the dropout seed advances on the device, layer-dropout decisions are
 drawn on the device under `rng.device_decisions()`), fixed input buffers.
 """
+import gc
+
 import torch
 
 from . import rng, streams
@@ -52,6 +54,12 @@ class StepGraph:
         pool = torch.cuda.graph_pool_handle()
         self.graphs, self.outputs = [], []
         call("tvq_counter_capture", 1)  # finish-counter slots of the graph stay reserved
+        # no garbage collection inside a capture: collecting an unreachable graph of an
+        # earlier capture (reference cycles) destroys it, which HIP refuses while a stream
+        # is capturing
+        gc_on = gc.isenabled()
+        gc.collect()
+        gc.disable()
         try:
             with rng.device_decisions():
                 for seg in self.segments:
@@ -63,6 +71,8 @@ class StepGraph:
                     self.outputs.append(out)
         finally:
             call("tvq_counter_capture", 0)
+            if gc_on:
+                gc.enable()
         return self
 
     def replay(self):

@@ -16,7 +16,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..hip import rng
+from ..hip import resblock, rng
 from ..hip.conv import conv2d, conv_transpose2d
 from ..hip.linear import linear
 from ..hip.norm import bn_snake, snake, snake_skip
@@ -91,6 +91,16 @@ class ResBlock(nn.Module):
 
     def forward(self, x):
         c = self.convs
+        if isinstance(self.proj, nn.Identity) and resblock.supported(x, c[1].in_channels,
+                                                                     c[4].out_channels):
+            # the whole block as 2 (eval: 1) fused launches, csrc/tvq_resblock.hip
+            if c[2].training:
+                p = c[5].p if self.training else 0.0
+                return resblock.resblock_train(x, _a(c[0]), c[1], c[2], _a(c[3]), c[4], p,
+                                               self._site)
+            if not (torch.is_grad_enabled() and x.requires_grad) and not (
+                    self.training and c[5].p > 0):
+                return resblock.resblock_eval(x, _a(c[0]), c[1], c[2], _a(c[3]), c[4])
         s, xs = snake_skip(x, _a(c[0]))  # xs: x, its skip-path gradient summed in Snake bwd
         h = conv2d(s, c[1].weight, c[1].bias)
         h = bn_snake(h, c[2], _a(c[3]))

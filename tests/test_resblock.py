@@ -1,0 +1,106 @@
+"""Fused small-channel ResBlock (csrc/tvq_resblock.hip) against the per-op HIP path it
+replaces (Snake -> conv -> BN+Snake -> conv+dropout+residual kernels, which the G3 goldens
+pin to the reference): training forward (y, BN running stats), every gradient, the same
+dropout mask, and the eval forward.  Tolerance: rel 2e-5 of each tensor's max (different
+summation order of the same fp32 arithmetic)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(8, 8, 64), (8, 16, 32), (4, 16, 16), (16, 8, 32), (3, 32, 16), (2, 32, 32),
+          (2, 16, 64), (5, 8, 16)]
+
+
+def _block(C, drop, seed=0):
+    from timevqvae.models.vq_vae import ResBlock
+    torch.manual_seed(seed)
+    m = ResBlock(C, C, False, dropout=drop)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn_like(p) * (0.3 if p.dim() > 1 else 0.5))
+        m.convs[0].a.uniform_(0.3, 0.8)
+        m.convs[3].a.uniform_(0.3, 0.8)
+        m.convs[2].running_mean.normal_()
+        m.convs[2].running_var.uniform_(0.5, 2.0)
+    return m.cuda()
+
+
+def _run(m, x, fused, train=True):
+    from timevqvae.hip import resblock, rng
+    prev = resblock.ENABLED
+    resblock.ENABLED = fused
+    try:
+        rng._calls[0] = 0
+        m.train(train)
+        for p in m.parameters():
+            p.grad = None
+        xx = x.clone().requires_grad_(train)
+        if train:
+            y = m(xx)
+            gy = torch.cos(torch.arange(y.numel(), device=y.device, dtype=torch.float32)).view_as(y)
+            y.backward(gy)
+            grads = {n: p.grad.clone() for n, p in m.named_parameters()}
+            grads["x"] = xx.grad.clone()
+        else:
+            with torch.no_grad():
+                y = m(xx)
+            grads = {}
+        bufs = {n: b.clone() for n, b in m.named_buffers()}
+        return y.detach(), grads, bufs
+    finally:
+        resblock.ENABLED = prev
+
+
+def _close(a, b, name, rel=2e-5):
+    scale = b.abs().max().item() + 1e-6
+    err = (a - b).abs().max().item()
+    assert err <= rel * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+@pytest.mark.parametrize("B,C,W", SHAPES)
+@pytest.mark.parametrize("drop", [0.0, 0.3])
+def test_fused_resblock_train_matches_per_op(B, C, W, drop):
+    from timevqvae.hip import resblock
+    x = torch.randn(B, C, 3, W, device="cuda")
+    assert resblock.supported(x, C, C)
+    m1 = _block(C, drop)
+    m2 = _block(C, drop)
+    m2._site = m1._site  # same dropout call site -> same mask stream
+    y1, g1, b1 = _run(m1, x, fused=False)
+    y2, g2, b2 = _run(m2, x, fused=True)
+    _close(y2, y1, "y")
+    for k in g1:
+        if k == "convs.1.bias":
+            # conv1's bias feeds a BatchNorm: its true gradient is 0 (rounding noise only)
+            tol = 2e-5 * g1["convs.1.weight"].abs().max().item()
+            assert (g2[k] - g1[k]).abs().max().item() <= tol, k
+            continue
+        _close(g2[k], g1[k], k)
+    for k in b1:
+        if b1[k].is_floating_point():
+            _close(b2[k], b1[k], k)
+        else:
+            assert torch.equal(b2[k], b1[k]), k
+    if drop > 0:  # the dropout really dropped, identically: zero pattern of y - x agrees
+        assert torch.equal((y1 - x) == 0, (y2 - x) == 0)
+        assert ((y2 - x) == 0).float().mean().item() > 0.2
+
+
+@pytest.mark.parametrize("B,C,W", SHAPES)
+def test_fused_resblock_eval_matches_per_op(B, C, W):
+    x = torch.randn(B, C, 3, W, device="cuda")
+    m = _block(C, 0.3)
+    y1, _, _ = _run(m, x, fused=False, train=False)
+    y2, _, _ = _run(m, x, fused=True, train=False)
+    _close(y2, y1, "y eval")
+
+
+def test_fused_resblock_declines_unsupported_shapes():
+    from timevqvae.hip import resblock
+    assert not resblock.supported(torch.empty(2, 64, 3, 8, device="cuda"), 64, 64)
+    assert not resblock.supported(torch.empty(2, 32, 3, 64, device="cuda"), 32, 32)
+    assert not resblock.supported(torch.empty(2, 4, 3, 32, device="cuda"), 4, 4)
+    assert not resblock.supported(torch.empty(2, 8, 3, 20, device="cuda"), 8, 8)
+    assert not resblock.supported(torch.empty(2, 8, 3, 128, device="cuda"), 8, 8)
+    assert not resblock.supported(torch.empty(2, 8, 3, 32, device="cuda"), 8, 16)
