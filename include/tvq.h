@@ -429,6 +429,13 @@ int tvq_rocket_apply(const double* X, int64_t n, int64_t L, int64_t ldx, const d
                      const int32_t* dilations, const int32_t* paddings, int64_t nk, double* out,
                      tvq_stream_t stream);
 
+/* ---- FID feature statistics (evaluation/eval_utils.py:56-81 calculate_fid; csrc/tvq_fid.hip):
+ * mu (D) = z.mean(0) and cov (D x D) = np.cov(z, rowvar=False) (divisor N-1) of the rows of
+ * z (N x D, float64, row-major), fixed summation order.  The matrix square root of
+ * cov1 @ cov2 stays on the host (float64 scipy.linalg.sqrtm, as the reference). */
+int tvq_fid_moments(const double* z, int64_t N, int64_t D, double* mu, double* cov,
+                    tvq_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * FidelityEnhancer / Unet1D eval forward (models/fidelity_enhancer.py:284-498, the
  * sampler's post-decode refinement, generation/sampler.py:156-169).  (B, C, L) fp32.

@@ -635,3 +635,22 @@ def fe_forward(sd, x_a, input_length, dim_mults=(1, 2, 4, 8), groups=4):
         x = F.conv1d(F.pad(x, (1, 1), mode="replicate"), sd[f"final_conv.{j}.weight"],
                      sd[f"final_conv.{j}.bias"])
     return x
+
+
+# ----------------------------------------------------------------------------
+# FID (evaluation/eval_utils.py:56-81)
+# ----------------------------------------------------------------------------
+def fid_moments(z):
+    """z.mean(0) (in z's dtype, as numpy does) and np.cov(z, rowvar=False) (float64)."""
+    return z.mean(axis=0), np.cov(z, rowvar=False)
+
+
+def fid(z1, z2):
+    """calculate_fid: |mu1 - mu2|^2 + tr(s1 + s2 - 2 sqrtm(s1 s2)), real part of sqrtm."""
+    from scipy.linalg import sqrtm
+    mu1, s1 = fid_moments(z1)
+    mu2, s2 = fid_moments(z2)
+    cm = sqrtm(s1.dot(s2))
+    if np.iscomplexobj(cm):
+        cm = cm.real
+    return ((mu1 - mu2) ** 2.0).sum() + np.trace(s1 + s2 - 2.0 * cm)

@@ -137,6 +137,7 @@ sig("tvq_fe_cat_interp", P, I64, I64, P, I64, I64, I64, I64, P, P)
 F64 = ctypes.c_double
 sig("tvq_minmax_fit_workspace", I64, restype=I64)
 sig("tvq_minmax_fit", P, I64, I64, F64, F64, P, P, P, P, P, P)
+sig("tvq_fid_moments", P, I64, I64, P, P, P)
 sig("tvq_minmax_transform", P, I64, I64, I64, P, P, P, P)
 sig("tvq_minmax_inverse", P, I64, I64, I64, P, P, P, P)
 sig("tvq_codebook_gather_nchw", P, I64, I64, I64, P, P, P)

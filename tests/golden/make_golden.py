@@ -14,6 +14,7 @@ files are loaded by file path with minimal import stubs:
 G6 (stochastic VQ) alone: python tests/golden/make_golden.py svq
 G7 (ROCKET features, evaluation/rocket_functions.py with a numba stub) alone: ... rocket
 G8 (FidelityEnhancer / Unet1D forward, models/fidelity_enhancer.py) alone: ... fe
+G10 (calculate_fid, evaluation/eval_utils.py) alone: ... fid
 
 Only the .npz outputs are committed (tests/golden/*.npz).  Usage:
 
@@ -676,6 +677,34 @@ def gen_stage2(ref):
     np.savez_compressed(os.path.join(OUT, "g9_stage2.npz"), **d)
 
 
+def gen_fid(ref):
+    """G10: calculate_fid (evaluation/eval_utils.py:56-81), loaded by file path (its
+    FCNBaseline import is stubbed: the function never uses it).  Case a: float64 Gaussian
+    features, D=32; b: ROCKET-like float64 features (ppv in [0,1] | max), D=160; c: float32
+    FCN-like features, D=128 (the reference takes the mean in float32, the cov in float64)."""
+    sys.modules["timevqvae.models"].FCNBaseline = object
+    eu = _load("ref_eval_utils", f"{REF}/evaluation/eval_utils.py")
+    rng = np.random.default_rng(10)
+    d = {}
+    A = rng.standard_normal((32, 32)) / 6
+    Bm = rng.standard_normal((32, 32)) / 5
+    cases = {
+        "a": (rng.standard_normal((600, 32)) @ A, 0.3 + rng.standard_normal((500, 32)) @ Bm),
+        "b": (np.concatenate([rng.uniform(0, 1, (700, 80)), rng.normal(1.0, 2.0, (700, 80))], 1),
+              np.concatenate([rng.uniform(0.1, 1, (600, 80)), rng.normal(1.2, 1.8, (600, 80))], 1)),
+        "c": (rng.standard_normal((700, 128)).astype(np.float32),
+              (0.1 + 1.1 * rng.standard_normal((650, 128))).astype(np.float32)),
+    }
+    for k, (z1, z2) in cases.items():
+        d[f"{k}_z1"], d[f"{k}_z2"] = z1, z2
+        d[f"{k}_fid"] = np.float64(eu.calculate_fid(z1, z2))
+        for i, z in ((1, z1), (2, z2)):
+            d[f"{k}_mu{i}"] = np.asarray(z.mean(axis=0), np.float64)
+            d[f"{k}_sigma{i}"] = np.cov(z, rowvar=False)
+        print("fid", k, d[f"{k}_fid"])
+    np.savez_compressed(os.path.join(OUT, "g10_fid.npz"), **d)
+
+
 def main():
     torch.set_num_threads(8)
     if sys.argv[1:] == ["rocket"]:  # regenerate only G7
@@ -691,6 +720,9 @@ def main():
     if sys.argv[1:] == ["stage2"]:  # regenerate only G9
         gen_stage2(ref)
         return
+    if sys.argv[1:] == ["fid"]:  # regenerate only G10
+        gen_fid(ref)
+        return
     if sys.argv[1:] == ["cfgA"]:  # regenerate only G3 at BASELINE configs[0]
         gen_stage1(ref, "cfgA", B=4, C=6, T=128, K=256, init_dim=4, hid_dim=128, seed=7)
         return
@@ -703,6 +735,7 @@ def main():
     gen_svq(ref)
     gen_rocket()
     gen_fe(ref)
+    gen_fid(ref)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
