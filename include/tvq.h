@@ -474,6 +474,39 @@ int tvq_fe_attention(const float* qkv, int64_t B, int64_t H, int64_t dh, int64_t
 int tvq_fe_cat_interp(const float* a, int64_t Ca, int64_t La, const float* b, int64_t Cb,
                       int64_t Lb, int64_t B, int64_t L, float* out, tvq_stream_t stream);
 
+/* ---- FidelityEnhancer training (Stage3, trainers/stage3.py:197-231; csrc/tvq_fe_train.hip).
+ * The Unet1D convolutions train on the conv engine (tvq_conv2d_* with H = 1; kinds k7 and
+ * k4/s2 for the init conv and Downsample, k3 replicate for the final convs). */
+/* WeightStandardizedConv2d backward: w (O, n) rows, g = dL/d(standardised w) -> dw */
+int tvq_fe_ws_weight_bwd(const float* w, int64_t O, int64_t n, float eps, const float* g,
+                         float* dw, int64_t accumulate, tvq_stream_t stream);
+/* y = Dropout_p(Snake_a(GroupNorm_G(x))) (+ residual); mean / rstd (B*G) saved */
+int tvq_fe_gn_snake_train_fwd(const float* x, int64_t B, int64_t C, int64_t L, int64_t G,
+                              const float* gamma, const float* beta, const float* a, float eps,
+                              float drop_p, const int64_t* seed_ptr, uint64_t offset,
+                              const float* residual, float* y, float* mean, float* rstd,
+                              tvq_stream_t stream);
+/* backward from dy: dx, and per element (B, C, L) terms whose channel sums are dgamma
+ * (tgam), dbeta (tbet) and da (tda) */
+int tvq_fe_gn_snake_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t L,
+                        int64_t G, const float* gamma, const float* beta, const float* a,
+                        const float* mean, const float* rstd, float drop_p,
+                        const int64_t* seed_ptr, uint64_t offset, float* dx, float* tgam,
+                        float* tbet, float* tda, tvq_stream_t stream);
+/* channel LayerNorm backward: dx and tg = dy * xhat (channel sums = dg) */
+int tvq_fe_channel_layernorm_bwd(const float* dy, const float* x, int64_t B, int64_t C,
+                                 int64_t L, const float* g, float eps, float* dx, float* tg,
+                                 tvq_stream_t stream);
+/* attention cores backward: qkv (B, 3 H dh, n) as to_qkv wrote it, dout (B, H dh, n) ->
+ * dqkv (B, 3 H dh, n); dh = 32; full attention n <= ~70 (LDS) */
+int tvq_fe_linear_attention_bwd(const float* qkv, const float* dout, int64_t B, int64_t H,
+                                int64_t dh, int64_t n, float* dqkv, tvq_stream_t stream);
+int tvq_fe_attention_bwd(const float* qkv, const float* dout, int64_t B, int64_t H, int64_t dh,
+                         int64_t n, float* dqkv, tvq_stream_t stream);
+/* tvq_fe_cat_interp backward: gout (B, Ca + Cb, L) -> da (B, Ca, La), db (B, Cb, Lb) */
+int tvq_fe_cat_interp_bwd(const float* gout, int64_t Ca, int64_t La, int64_t Cb, int64_t Lb,
+                          int64_t B, int64_t L, float* da, float* db, tvq_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * Trajectory data format (utils/data_utils.py:84-110 get_data; scripts/generate.py:14-20
  * post_processed_generated_trajectories).  X (N, Fc = L*F) float64, columns [t0 f0, t0 f1,

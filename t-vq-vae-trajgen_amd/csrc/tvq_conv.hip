@@ -1660,7 +1660,9 @@ static void launch_wgrad(const float* G, const float* in, float* slab, int split
     case 0: if (repl) { MACRO(3, 4, 2, true) } else { MACRO(3, 4, 2, false) } break; \
     case 1: MACRO(3, 3, 1, false) break;                                      \
     case 2: MACRO(1, 1, 1, false) break;                                      \
-    case 3: MACRO(1, 3, 1, false) break;                                      \
+    case 3: if (repl) { MACRO(1, 3, 1, true) } else { MACRO(1, 3, 1, false) } break; \
+    case 4: MACRO(1, 7, 1, false) break;                                      \
+    case 5: MACRO(1, 4, 2, false) break;                                      \
     default: set_error("conv: unsupported kernel kind %d", kind); return TVQ_ERR_ARG; \
   }
 
@@ -1669,6 +1671,8 @@ static int kind_of(int KH, int KW, int SW) {
   if (KH == 3 && KW == 3 && SW == 1) return 1;
   if (KH == 1 && KW == 1 && SW == 1) return 2;
   if (KH == 1 && KW == 3 && SW == 1) return 3;
+  if (KH == 1 && KW == 7 && SW == 1) return 4;  // FidelityEnhancer init conv (k7, pad 3)
+  if (KH == 1 && KW == 4 && SW == 2) return 5;  // FidelityEnhancer Downsample (k4, s2, pad 1)
   return -1;
 }
 

@@ -133,6 +133,13 @@ sig("tvq_fe_linear_attention", P, I64, I64, I64, I64, P, P)
 sig("tvq_fe_linear_attention_fused", P, I64, I64, I64, P, I64, I64, P, P)
 sig("tvq_fe_attention", P, I64, I64, I64, I64, P, P)
 sig("tvq_fe_cat_interp", P, I64, I64, P, I64, I64, I64, I64, P, P)
+sig("tvq_fe_ws_weight_bwd", P, I64, I64, F32, P, P, I64, P)
+sig("tvq_fe_gn_snake_train_fwd", P, I64, I64, I64, I64, P, P, P, F32, F32, P, U64, P, P, P, P, P)
+sig("tvq_fe_gn_snake_bwd", P, P, I64, I64, I64, I64, P, P, P, P, P, F32, P, U64, P, P, P, P, P)
+sig("tvq_fe_channel_layernorm_bwd", P, P, I64, I64, I64, P, F32, P, P, P)
+sig("tvq_fe_linear_attention_bwd", P, P, I64, I64, I64, I64, P, P)
+sig("tvq_fe_attention_bwd", P, P, I64, I64, I64, I64, P, P)
+sig("tvq_fe_cat_interp_bwd", P, I64, I64, I64, I64, I64, I64, P, P, P)
 # --- trajectory data format (MinMax scaling + layout) -------------------------
 F64 = ctypes.c_double
 sig("tvq_minmax_fit_workspace", I64, restype=I64)

@@ -15,8 +15,13 @@ holders; each forward is a handful of fused launches:
   skips        (:434-452)  [interpolate + concat] in one launch
 
 No time embedding reaches the network (Unet1D.forward never passes one), and Dropout is
-the identity in eval mode.  Stage3 training is not on the HIP path: the forward raises in
-training mode instead of silently dropping the reference's dropout.
+the identity in eval mode.
+
+Training mode (Stage3, trainers/stage3.py:197-231) runs the same graph through
+differentiable ops (hip/fe_train.py): the convolutions on the conv engine (H = 1, fused
+bias / residual, deterministic weight gradients), the weight standardisation, GroupNorm +
+Snake + the Block's Dropout (counter-hash mask, site per Block), channel LayerNorm, both
+attention cores and the interpolate+concat skips, each with a HIP backward.
 """
 import math
 
@@ -24,16 +29,18 @@ import torch
 import torch.nn as nn
 
 from ..hip import fe as ops
+from ..hip import fe_train as tops
+from ..hip import rng
+from ..hip.conv import conv2d
+from ..hip.xf import upsample_nearest
 from ..utils import SnakeActivation
 
 _EPS = 1e-5  # the reference's fp32 eps for weight standardisation, LN and GroupNorm
 
 
-def _eval_only(module):
-    if module.training:
-        raise NotImplementedError(
-            f"{type(module).__name__}: the HIP path runs the FidelityEnhancer's eval forward "
-            "(the sampler's use); Stage3 training is not on it -- call .eval()")
+def _train(module):
+    """Training graph: the module is in training mode and autograd is recording."""
+    return module.training and torch.is_grad_enabled()
 
 
 class _Conv(nn.Conv1d):
@@ -47,9 +54,20 @@ class _Conv(nn.Conv1d):
         self._up2 = upsample2
 
     def forward(self, x, residual=None):
+        if _train(self):
+            return self._train_forward(x, self.weight, residual)
         return ops.conv1d(x, self.weight, self.bias, stride=self.stride[0],
                           padding=self.padding[0], upsample2=self._up2,
                           replicate=self.padding_mode == "replicate", residual=residual)
+
+    def _train_forward(self, x, w, residual=None):
+        k = self.kernel_size[0]
+        if self.padding[0] != (k - 1) // 2:
+            raise NotImplementedError(f"conv1d k{k} pad {self.padding[0]} is not on the path")
+        if self._up2:
+            x = upsample_nearest(x, 2 * x.shape[-1])
+        return conv2d(x, w, self.bias, stride_w=self.stride[0],
+                      replicate=self.padding_mode == "replicate", residual=residual)
 
 
 class _StandardizedConv(nn.Conv1d):
@@ -66,6 +84,9 @@ class _StandardizedConv(nn.Conv1d):
         self._ws_key = None
 
     def forward(self, x):
+        if _train(self):
+            self._ws_key = None
+            return conv2d(x, tops.standardize_weight(self.weight, _EPS), self.bias)
         key = (self.weight.data_ptr(), self.weight._version, self.weight.device)
         if torch.cuda.is_current_stream_capturing():
             self._ws_key = None
@@ -92,6 +113,8 @@ class _ChannelNorm(nn.Module):
         self.g = nn.Parameter(torch.ones(1, channels, 1))
 
     def forward(self, x, residual=None):
+        if _train(self):
+            return tops.channel_layernorm(x, self.g, _EPS, residual=residual)
         return ops.channel_layernorm(x, self.g, _EPS, residual=residual)
 
 
@@ -105,8 +128,14 @@ class _ConvNormAct(nn.Module):
         self.norm = nn.GroupNorm(groups, cout)
         self.act = SnakeActivation(cout, dim=1)
         self.dropout = nn.Dropout(dropout)
+        self._site = rng.new_site()
 
     def forward(self, x, residual=None):
+        if _train(self):
+            return tops.group_norm_snake(self.proj(x), self.norm.num_groups, self.norm.weight,
+                                         self.norm.bias, self.act.a, self.norm.eps,
+                                         residual=residual, drop_p=self.dropout.p,
+                                         site=self._site)
         return ops.group_norm_snake(self.proj(x), self.norm.num_groups, self.norm.weight,
                                     self.norm.bias, self.act.a, self.norm.eps,
                                     residual=residual)
@@ -138,8 +167,11 @@ class _LinearAttnCore(nn.Module):
                                     _ChannelNorm(channels))
 
     def forward(self, xn, residual):
-        att = ops.linear_attention_fused(xn, self.to_qkv.weight, self.heads, self.dim_head)
         proj, norm = self.to_out
+        if _train(self):
+            att = tops.linear_attention(conv2d(xn, self.to_qkv.weight), self.heads, self.dim_head)
+            return norm(conv2d(att, proj.weight, proj.bias), residual=residual)
+        att = ops.linear_attention_fused(xn, self.to_qkv.weight, self.heads, self.dim_head)
         return norm(ops.conv1d(att, proj.weight, proj.bias), residual=residual)
 
 
@@ -153,6 +185,9 @@ class _FullAttnCore(nn.Module):
         self.to_out = nn.Conv1d(heads * dim_head, channels, 1)
 
     def forward(self, xn, residual):
+        if _train(self):
+            att = tops.attention(conv2d(xn, self.to_qkv.weight), self.heads, self.dim_head)
+            return conv2d(att, self.to_out.weight, self.to_out.bias, residual=residual)
         att = ops.attention(ops.conv1d(xn, self.to_qkv.weight), self.heads, self.dim_head)
         return ops.conv1d(att, self.to_out.weight, self.to_out.bias, residual=residual)
 
@@ -239,7 +274,7 @@ class Unet1D(nn.Module):
             _Conv(self.out_dim, self.out_dim, 3, pad=1, replicate=True))
 
     def forward(self, x):
-        _eval_only(self)
+        cat = tops.cat_interp if _train(self) else ops.cat_interp
         x = self.init_conv(x)
         stem, skips = x, []
         for res1, res2, attn, down in self.downs:
@@ -250,10 +285,10 @@ class Unet1D(nn.Module):
             x = down(x)
         x = self.mid_block2(self.mid_attn(self.mid_block1(x)))
         for res1, res2, attn, up in self.ups:
-            x = res1(ops.cat_interp(x, skips.pop(), x.shape[-1]))
-            x = res2(ops.cat_interp(x, skips.pop(), x.shape[-1]))
+            x = res1(cat(x, skips.pop(), x.shape[-1]))
+            x = res2(cat(x, skips.pop(), x.shape[-1]))
             x = up(attn(x))
-        x = self.final_res_block(ops.cat_interp(self.last_up(x), stem, stem.shape[-1]))
+        x = self.final_res_block(cat(self.last_up(x), stem, stem.shape[-1]))
         return self.final_conv(x)
 
 
@@ -266,9 +301,15 @@ class FidelityEnhancer(nn.Module):
         self.unet = Unet1D(channels=in_channels, **config["fidelity_enhancer"])
         self.register_buffer("tau", torch.tensor(0.0).float())
 
-    @torch.no_grad()
     def forward(self, x_a):
+        """Eval: no autograd (the sampler's use).  Training: differentiable in the FE's
+        parameters (Stage3)."""
         x_a = x_a.float()
-        if x_a.shape[-1] != self.input_length:
-            x_a = ops.cat_interp(x_a, None, self.input_length)
-        return self.unet(x_a)
+        if _train(self):
+            if x_a.shape[-1] != self.input_length:
+                x_a = tops.cat_interp(x_a, None, self.input_length)
+            return self.unet(x_a)
+        with torch.no_grad():
+            if x_a.shape[-1] != self.input_length:
+                x_a = ops.cat_interp(x_a, None, self.input_length)
+            return self.unet(x_a)

@@ -146,3 +146,11 @@ def linear_warmup_cosine_annealingLR(optimizer: torch.optim.Optimizer, max_steps
     warmup = LambdaLR(optimizer, lr_lambda=warmup_lambda)
     cosine = CosineAnnealingLR(optimizer, max_steps - warmup_steps, eta_min=min_lr)
     return SequentialLR(optimizer, schedulers=[warmup, cosine], milestones=[warmup_steps])
+
+
+def remove_outliers(data: np.ndarray):
+    """train_utils.py:486-493: keep the rows an IsolationForest (max_samples 0.9,
+    contamination 0.1, random_state 0) labels inliers -- host sklearn, as the reference."""
+    from sklearn.ensemble import IsolationForest
+    keep = IsolationForest(max_samples=0.9, contamination=0.1, random_state=0).fit_predict(data) == 1
+    return data[keep]

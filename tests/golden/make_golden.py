@@ -15,6 +15,7 @@ G6 (stochastic VQ) alone: python tests/golden/make_golden.py svq
 G7 (ROCKET features, evaluation/rocket_functions.py with a numba stub) alone: ... rocket
 G8 (FidelityEnhancer / Unet1D forward, models/fidelity_enhancer.py) alone: ... fe
 G10 (calculate_fid, evaluation/eval_utils.py) alone: ... fid
+G11 (Stage3 FE training loss + gradients, trainers/stage3.py) alone: ... fetrain
 
 Only the .npz outputs are committed (tests/golden/*.npz).  Usage:
 
@@ -28,6 +29,7 @@ import types
 import numpy as np
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from param_init import fill_state_dict  # noqa: E402
@@ -393,6 +395,84 @@ def gen_fe(ref):
     np.savez_compressed(os.path.join(OUT, "g8_fe.npz"), **d)
 
 
+def _ref_fe(fe_mod, Lin, C, seed):
+    """Reference FidelityEnhancer with dropout 0 (config.yaml's other FE settings) and
+    param_init weights (seed), in training mode."""
+    cfg = dict(FE_CONFIG)
+    cfg["dropout"] = 0.0
+    torch.manual_seed(seed)
+    fe = fe_mod.FidelityEnhancer(Lin, C, {"fidelity_enhancer": cfg})
+    vals = fill_state_dict(fe.state_dict(), seed)
+    fe.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
+    return fe.train()
+
+
+def gen_fe_train(ref):
+    """G11: Stage3 training (trainers/stage3.py:197-231) with dropout 0.
+    Cases a / b: FidelityEnhancer forward + L1 loss + backward (fidelity_enhancer.py:458-498,
+    stage3.py:206-209) at input_length 256 and 301 (ragged skips).  Case s3: the reference
+    Stage3._fidelity_enhancer_loss_fn itself (stage3.py:193-210) -- decode LF / HF token
+    indices with the reference MaskGIT over the G3-small stage1 (seed 3), FE, L1 -- loaded
+    from the file with stubs for its plotting / evaluation imports; the stochastic-VQ
+    encoding that produces the indices (svq_temp = tau) is pinned by G6."""
+    fe_mod = _load("ref_fidelity_enhancer_t", f"{REF}/models/fidelity_enhancer.py")
+    d = {}
+    for tag, (B, C, Lx, Lin, seed) in {"a": (3, 6, 256, 256, 21), "b": (2, 6, 256, 301, 22)}.items():
+        fe = _ref_fe(fe_mod, Lin, C, seed)
+        g = torch.Generator().manual_seed(seed + 1)
+        xp = torch.cumsum(0.1 * torch.randn(B, C, Lx, generator=g), -1)
+        x = torch.cumsum(0.1 * torch.randn(B, C, Lin, generator=g), -1)
+        xhat = fe(xp)
+        loss = F.l1_loss(xhat, x)
+        loss.backward()
+        d[f"{tag}_xprime"], d[f"{tag}_x"] = xp.numpy(), x.numpy()
+        d[f"{tag}_xhat"], d[f"{tag}_loss"] = xhat.detach().numpy(), np.array(float(loss))
+        d[f"{tag}_meta"] = np.array([B, C, Lx, Lin, seed], dtype=np.int64)
+        for k, prm in fe.named_parameters():
+            if prm.grad is not None:
+                d[f"{tag}_grad/{k}"] = prm.grad.numpy().copy()
+    # ---- s3: the reference Stage3 loss function
+    for name in ("timevqvae.evaluation", "timevqvae.trainers"):
+        m = types.ModuleType(name)
+        m.Metrics = m.MiniRocketTransform = m.Stage2 = object
+        sys.modules[name] = m
+    sys.modules["timevqvae.models"].FidelityEnhancer = fe_mod.FidelityEnhancer
+    st3 = _load("ref_stage3", f"{REF}/trainers/stage3.py")
+    T, Ks, hid, seed = 128, 64, 32, 3
+    torch.manual_seed(seed)
+    s1 = ref.stage1.Stage1(T, 6, _stage1_config(4, hid, Ks))
+    vals = fill_state_dict(s1.state_dict(), seed)
+    s1.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()}, strict=False)
+    s1.eval()
+    gx = torch.Generator().manual_seed(81)
+    B = 4
+    x = torch.cumsum(0.1 * torch.randn(B, 6, T, generator=gx), -1)
+    with torch.no_grad():
+        s1.encoder_l(x), s1.encoder_h(x)  # num_tokens / H' / W' buffers
+    MG = ref.maskgit.MaskGIT
+    mg = MG.__new__(MG)
+    nn.Module.__init__(mg)
+    for n in ("encoder_l", "decoder_l", "vq_model_l", "encoder_h", "decoder_h", "vq_model_h"):
+        setattr(mg, n, getattr(s1, n))
+    mg.H_prime_l, mg.W_prime_l = int(s1.encoder_l.H_prime), int(s1.encoder_l.W_prime)
+    mg.H_prime_h, mg.W_prime_h = int(s1.encoder_h.H_prime), int(s1.encoder_h.W_prime)
+    n_l, n_h = int(s1.encoder_l.num_tokens), int(s1.encoder_h.num_tokens)
+    s_l = torch.randint(0, Ks, (B, n_l), generator=gx)
+    s_h = torch.randint(0, Ks, (B, n_h), generator=gx)
+    fe = _ref_fe(fe_mod, T, 6, 23)
+    this = types.SimpleNamespace(maskgit=mg, fidelity_enhancer=fe)
+    loss, (xprime, xhat) = st3.Stage3._fidelity_enhancer_loss_fn(this, x, s_l, s_h)
+    loss.backward()
+    d["s3_x"], d["s3_s_l"], d["s3_s_h"] = x.numpy(), s_l.numpy(), s_h.numpy()
+    d["s3_xprime"], d["s3_xhat"] = xprime.numpy(), xhat.detach().numpy()
+    d["s3_loss"] = np.array(float(loss))
+    for k, prm in fe.named_parameters():
+        if prm.grad is not None:
+            d[f"s3_grad/{k}"] = prm.grad.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "g11_fe_train.npz"), **d)
+    print("g11", {k: float(d[k]) for k in ("a_loss", "b_loss", "s3_loss")})
+
+
 # --------------------------------------------------------------------------- G9
 def install_x_transformers_stub():
     """x-transformers (pyproject.toml:21, ^1.31.6) is absent from the image and has no
@@ -720,6 +800,9 @@ def main():
     if sys.argv[1:] == ["stage2"]:  # regenerate only G9
         gen_stage2(ref)
         return
+    if sys.argv[1:] == ["fetrain"]:  # regenerate only G11
+        gen_fe_train(ref)
+        return
     if sys.argv[1:] == ["fid"]:  # regenerate only G10
         gen_fid(ref)
         return
@@ -736,6 +819,7 @@ def main():
     gen_rocket()
     gen_fe(ref)
     gen_fid(ref)
+    gen_fe_train(ref)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

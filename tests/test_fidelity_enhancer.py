@@ -50,12 +50,6 @@ def test_oracle_fe_matches_reference_golden(tag):
     assert ok, err
 
 
-def test_training_mode_raises():
-    fe = _model(6, 256, 11).train()
-    with pytest.raises(NotImplementedError):
-        fe.unet(torch.zeros(1, 6, 256))
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("tag", ["a", "b"])
 def test_hip_fe_matches_reference_golden(tag, cuda):
