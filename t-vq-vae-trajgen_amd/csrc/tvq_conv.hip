@@ -808,8 +808,10 @@ __global__ void replicate_fold_kernel(const float* __restrict__ dpad, int B, int
 }
 
 // Per-channel sum over (B, HW) of a (B, C, HW) tensor: out[c] (+)= sum, deterministic.
-// Stage 1: partial[c][chunk]; stage 2 (fixed-order sum) in the last block of channel c
-// when `cnt` is given, else chan_sum_final_kernel.
+// Stage 1: partial[c][chunk], chunk = `ipc` whole images of channel c (contiguous HW rows,
+// float4 loads, 4 in flight per thread); stage 2 (fixed xor tree over <= 64 partials, one
+// load per lane) in the last block of channel c when `cnt` is given, else
+// chan_sum_final_kernel.
 __device__ __forceinline__ void chan_sum_final_one(const float* part, int chunks, int c,
                                                    float* out, int accumulate) {
   float s = 0.f;
@@ -817,24 +819,43 @@ __device__ __forceinline__ void chan_sum_final_one(const float* part, int chunks
   out[c] = accumulate ? out[c] + s : s;
 }
 __global__ __launch_bounds__(256) void chan_sum_partial_kernel(const float* __restrict__ x, int B,
-                                                               int C, int HW, int chunks,
-                                                               float* __restrict__ part,
+                                                               int C, int HW, int ipc, int chunks,
+                                                               int vec, float* __restrict__ part,
                                                                int* __restrict__ cnt,
                                                                float* __restrict__ out,
                                                                int accumulate) {
   __shared__ float red[4];
   const int c = blockIdx.x, ch = blockIdx.y;
-  const int64_t per = ((int64_t)B * HW + chunks - 1) / chunks;
-  const int64_t lo = ch * per, hi = min((int64_t)B * HW, lo + per);
+  const int b0 = ch * ipc, b1 = min(B, b0 + ipc);
   float s = 0.f;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
-    const int64_t b = i / HW, p = i - b * HW;
-    s += x[(b * C + c) * HW + p];
+  if (vec) {
+    const int hw4 = HW >> 2, n4 = (b1 - b0) * hw4;
+    for (int i0 = threadIdx.x; i0 < n4; i0 += 256 * 4) {
+      floatx4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256;
+        const int bb = b0 + (i < n4 ? i : 0) / hw4, q = (i < n4 ? i : 0) % hw4;
+        v[u] = *reinterpret_cast<const floatx4*>(x + ((int64_t)bb * C + c) * HW + 4 * q);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + u * 256 < n4) s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
+    }
+  } else {
+    const int n = (b1 - b0) * HW;
+    for (int i = threadIdx.x; i < n; i += 256) {
+      const int bb = b0 + i / HW, p = i % HW;
+      s += x[((int64_t)bb * C + c) * HW + p];
+    }
   }
   s = block_sum(s, red);
   if (threadIdx.x == 0) st_wt(part + (int64_t)c * chunks + ch, s);
-  if (cnt && last_block(cnt + c, chunks) && threadIdx.x == 0)
-    chan_sum_final_one(part, chunks, c, out, accumulate);
+  if (cnt && last_block(cnt + c, chunks) && threadIdx.x < 64) {
+    float t = threadIdx.x < chunks ? ld_wt(part + (int64_t)c * chunks + threadIdx.x) : 0.f;
+    t = wave_sum(t);
+    if (threadIdx.x == 0) out[c] = accumulate ? out[c] + t : t;
+  }
 }
 __global__ void chan_sum_final_kernel(const float* __restrict__ part, int C, int chunks,
                                       float* __restrict__ out, int accumulate) {
@@ -1091,6 +1112,107 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const float* __restrict_
     }
   }
 }
+
+// Direct convolution for few channels on both sides (C, N <= 16): the stride-2 encoder /
+// decoder convs and the decoders' ConvTranspose tail (12 <-> 4 / 12 channels at W up to
+// 512), where an MFMA tile would be mostly padding and the staged GEMMs are latency-bound.
+// One thread owns two adjacent output positions for all N channels (32 fp32 accumulators),
+// the weights sit in LDS as [c][tap][16 n] (float4 broadcast reads), the input is read
+// through L1/L2; for the T gather (stride-2 transposed) the taps whose source is fractional
+// are skipped per output parity with wave-uniform branches.  Same epilogue as epi_store.
+constexpr int SMALL_NB = 16;
+template <int MODE, int KH, int KW, int SW, bool REPL>
+__global__ __launch_bounds__(256) void conv_small_kernel(const float* __restrict__ in,
+                                                         const float* __restrict__ wt,
+                                                         float* __restrict__ out, ConvGeom g,
+                                                         Epi e) {
+  constexpr int KK = KH * KW;
+  __shared__ floatx4 ws4[SMALL_NB * KK * SMALL_NB / 4];  // [c][t][n]
+  float* ws = reinterpret_cast<float*>(ws4);
+  for (int i = threadIdx.x; i < g.C * KK * SMALL_NB; i += 256) {
+    const int n = i % SMALL_NB, ct = i / SMALL_NB;
+    const int c = ct / KK, t = ct - c * KK;
+    ws[i] = n < g.N ? wt[(int64_t)n * g.wsn + (int64_t)c * g.wsc + t] : 0.f;
+  }
+  __syncthreads();
+  const int wo2 = (g.Wo + 1) >> 1;
+  const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (tid >= (int64_t)g.B * g.Hout * wo2) return;
+  const int j = (int)(tid % wo2);
+  const int64_t bh = tid / wo2;
+  const int h = (int)(bh % g.Hout), b = (int)(bh / g.Hout);
+  const int wo0 = 2 * j;
+  float acc[2][SMALL_NB];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int n = 0; n < SMALL_NB; ++n) acc[p][n] = 0.f;
+  const float* inb = in + (int64_t)b * g.C * g.Hin * g.Win;
+  for (int c = 0; c < g.C; ++c) {
+    const float* inc = inb + (int64_t)c * g.Hin * g.Win;
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh) {
+      int hi = MODE == GATHER_F ? h + kh - g.oph : h - kh + g.oph;
+      bool hv = hi >= 0 && hi < g.Hin;
+      if (REPL) {
+        hi = hi < 0 ? 0 : (hi >= g.Hin ? g.Hin - 1 : hi);
+        hv = true;
+      }
+      const float* row = inc + (int64_t)(hv ? hi : 0) * g.Win;
+#pragma unroll
+      for (int kw = 0; kw < KW; ++kw) {
+        const floatx4* w4 = ws4 + ((c * KK + kh * KW + kw) * SMALL_NB) / 4;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int wo = wo0 + p;
+          int wi;
+          bool ok;
+          if (MODE == GATHER_F) {
+            wi = wo * SW + kw - g.opw;
+            ok = wi >= 0 && wi < g.Win;
+            if (REPL) {
+              wi = wi < 0 ? 0 : (wi >= g.Win ? g.Win - 1 : wi);
+              ok = true;
+            }
+          } else {
+            const int wn = wo - kw + g.opw;
+            if (SW == 2 && ((wn & 1) != 0)) continue;  // parity: uniform per (p, kw)
+            wi = wn / SW;
+            ok = wn >= 0 && wi < g.Win;
+          }
+          ok = ok && hv && wo < g.Wo;
+          const float v = ok ? row[ok ? wi : 0] : 0.f;
+#pragma unroll
+          for (int q = 0; q < SMALL_NB / 4; ++q) {
+            const floatx4 w = w4[q];
+            acc[p][4 * q + 0] = fmaf(w[0], v, acc[p][4 * q + 0]);
+            acc[p][4 * q + 1] = fmaf(w[1], v, acc[p][4 * q + 1]);
+            acc[p][4 * q + 2] = fmaf(w[2], v, acc[p][4 * q + 2]);
+            acc[p][4 * q + 3] = fmaf(w[3], v, acc[p][4 * q + 3]);
+          }
+        }
+      }
+    }
+  }
+  const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
+  const int64_t hw = (int64_t)g.Hout * g.Wo;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int wo = wo0 + p;
+    if (wo >= g.Wo) continue;
+#pragma unroll
+    for (int n = 0; n < SMALL_NB; ++n) {
+      if (n >= g.N) continue;
+      const int64_t o = ((int64_t)b * g.N + n) * hw + (int64_t)h * g.Wo + wo;
+      float v = acc[p][n] + (e.bias ? e.bias[n] : 0.f);
+      if (e.drop_p > 0.f) v = uniform01(seed, (uint64_t)o) >= e.drop_p ? v * e.drop_scale : 0.f;
+      if (e.residual) v += e.residual[o];
+      out[o] = v;
+    }
+  }
+}
+
+static int g_conv_small = 1;  // conv_small_kernel enabled (tvq_conv_config bit 256 turns it off)
 
 static constexpr int HALO_LDS_MAX = 64 * 1024;
 
@@ -1616,6 +1738,16 @@ static bool halo_preferred(int mode, int C, int KK, int SW) {
 template <int MODE, int KH, int KW, int SW, bool REPL>
 static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g, float* ws,
                         const Epi& e, hipStream_t st) {
+  // measured per shape (tools/conv_shapes_bench.py, r02): the direct kernel wins for the
+  // stride-2 transposed gathers with <= 12 channels on both sides (the decoders' ConvT tail
+  // and DecBlocks 8->4, the EncBlocks' data gradients), loses to the halo / staged paths
+  // elsewhere
+  if (g_conv_small && MODE == GATHER_T && SW == 2 && g.C <= 12 && g.N <= 12) {
+    const int64_t th = (int64_t)g.B * g.Hout * ((g.Wo + 1) / 2);
+    hipLaunchKernelGGL((conv_small_kernel<MODE, KH, KW, SW, REPL>), dim3((unsigned)((th + 255) / 256)),
+                       dim3(256), 0, st, in, wt, out, g, e);
+    return;
+  }
   HaloPlan pl;
   const int oh = MODE == GATHER_F ? g.oph : KH - 1 - g.oph;
   const int ow = MODE == GATHER_F ? g.opw : KW - 1 - g.opw;
@@ -1766,13 +1898,14 @@ extern "C" int tvq_conv_wgrad_defer_flush(tvq_stream_t stream) {
 extern "C" int tvq_conv_config(int64_t halo) {
   const int prev = g_conv_halo | (g_conv_t32 ? 0 : 8) | (g_t32_bk == 32 ? 16 : 0) |
                    (g_t32_bk == 16 ? 32 : 0) | (g_t32_nw == 4 ? 64 : 0) |
-                   (g_t32_n64 ? 128 : 0);
+                   (g_t32_n64 ? 128 : 0) | (g_conv_small ? 0 : 256);
   if (halo >= 0) {
     g_conv_halo = (int)(halo & 7);
     g_conv_t32 = (halo & 8) ? 0 : 1;
     g_t32_bk = (halo & 16) ? 32 : ((halo & 32) ? 16 : 64);
     g_t32_nw = (halo & 64) ? 4 : 12;
     g_t32_n64 = (halo & 128) ? 1 : 0;
+    g_conv_small = (halo & 256) ? 0 : 1;
   }
   return prev;
 }
@@ -2073,11 +2206,17 @@ extern "C" int tvq_channel_sum(const float* x, int64_t B, int64_t C, int64_t HW,
   const int64_t chunks = tvq_channel_sum_workspace(B, C, HW) / C;
   hipStream_t st = (hipStream_t)stream;
   int* cnt = counters(C, FIN_REDUCE);
-  hipLaunchKernelGGL(chan_sum_partial_kernel, dim3((int)C, (int)chunks), dim3(256), 0, st, x,
-                     (int)B, (int)C, (int)HW, (int)chunks, workspace, cnt, out, (int)accumulate);
+  // whole images per chunk (at most the workspace's `chunks`, which is <= 64)
+  const int64_t ipc = (B + chunks - 1) / chunks;
+  const int64_t nch = (B + ipc - 1) / ipc;
+  TVQ_CHECK_ARG(ipc * HW < (1ll << 31), "tvq_channel_sum: bad geometry");
+  const int vec = (HW & 3) == 0 && ((uintptr_t)x & 15) == 0;
+  hipLaunchKernelGGL(chan_sum_partial_kernel, dim3((int)C, (int)nch), dim3(256), 0, st, x,
+                     (int)B, (int)C, (int)HW, (int)ipc, (int)nch, vec, workspace, cnt, out,
+                     (int)accumulate);
   if (!cnt)
     hipLaunchKernelGGL(chan_sum_final_kernel, dim3((int)((C + 127) / 128)), dim3(128), 0, st,
-                       workspace, (int)C, (int)chunks, out, (int)accumulate);
+                       workspace, (int)C, (int)nch, out, (int)accumulate);
   return launch_status("tvq_channel_sum");
 }
 

@@ -24,9 +24,9 @@ SHAPES = [
     (1, 128, 16, 3, 32, 3, 3, 1, 0, 0), (1, 128, 64, 3, 8, 1, 1, 1, 0, 0),
     (1, 128, 64, 3, 8, 3, 3, 1, 0, 0), (2, 128, 128, 3, 8, 3, 3, 1, 0, 0),
     (2, 128, 128, 3, 32, 3, 3, 1, 0, 0),
-    (2, 4, 3, 3, 128, 3, 4, 2, 0, 1), (2, 8, 3, 3, 64, 3, 4, 2, 0, 1),
-    (2, 12, 3, 3, 256, 3, 4, 2, 0, 1), (2, 16, 3, 3, 32, 3, 4, 2, 0, 1),
-    (1, 32, 3, 3, 16, 3, 4, 2, 0, 1), (1, 64, 3, 3, 8, 3, 4, 2, 0, 1),
+    (2, 4, 12, 3, 128, 3, 4, 2, 0, 1), (2, 8, 4, 3, 64, 3, 4, 2, 0, 1),
+    (2, 12, 12, 3, 256, 3, 4, 2, 0, 1), (2, 16, 8, 3, 32, 3, 4, 2, 0, 1),
+    (1, 32, 16, 3, 16, 3, 4, 2, 0, 1), (1, 64, 32, 3, 8, 3, 4, 2, 0, 1),
     (1, 128, 256, 1, 96, 1, 3, 1, 0, 0), (1, 256, 128, 1, 96, 1, 3, 1, 0, 0),
 ]
 B = 256
@@ -57,7 +57,7 @@ def timeit(fn, reps=20):
 def main():
     only = {int(a) for a in sys.argv[1].split(",")} if len(sys.argv) > 1 else None
     dev = torch.device("cuda", 0)
-    if "TVQ_CONV_HALO" in os.environ:  # 0: staged GEMM only, 1: halo fwd/dgrad, 2: halo wgrad
+    if "TVQ_CONV_HALO" in os.environ:  # tvq_conv_config bits (1/2 halo, 256: no small direct)
         value("tvq_conv_config", int(os.environ["TVQ_CONV_HALO"]))
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "floor": 0.0}
     print(f"{'n':>3} {'Ci':>4} {'Co':>4} {'W':>4} k    {'fwd':>7} {'dgrad':>7} {'wgrad':>7}  floor(us)")
