@@ -260,7 +260,9 @@ extern "C" int64_t tvq_gemm_workspace(int64_t M, int64_t N, int64_t K) {
   int TM, TN;
   choose_tile(M, N, &TM, &TN);
   const int tiles = (int)(((M + TM - 1) / TM) * ((N + TN - 1) / TN));
-  const int s = gemm_splits((int)M, (int)N, (int)K, tiles);
+  int s = gemm_splits((int)M, (int)N, (int)K, tiles);
+  const int sd = gemm_direct_splits(M, N, K);  // the direct weight-gradient form
+  if (sd > s) s = sd;
   return s > 1 ? (int64_t)s * M * N : 0;
 }
 
@@ -280,6 +282,7 @@ extern "C" int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B
   g.kper = (int)K;
   g.cnt = nullptr;
   g.slab = nullptr;
+  if (gemm_direct(g, workspace, (hipStream_t)stream)) return launch_status("tvq_gemm(direct)");
   if (gemm_skinny(g, (hipStream_t)stream)) return launch_status("tvq_gemm(skinny)");
   int TM, TN;
   choose_tile(M, N, &TM, &TN);

@@ -134,13 +134,18 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g) {
 // MFMAs and stores (measured the fastest of the forms in this file at the transformer
 // shapes; tools/mfma_probe.hip).
 template <int KH, bool B_KCONTIG>
-__global__ __launch_bounds__(256) void gemm_rb2_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256) void gemm_rb2_kernel(GemmArgs g, int nblk, int xcd) {
   constexpr int KP = 2 * KH;
   constexpr int P = KP + 4;
   __shared__ float Bs[32 * P];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r32 = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.y * 32;
+  int mblk = (int)blockIdx.x, nb = (int)blockIdx.y;
+  if (xcd) {  // 1-D grid: the column blocks of one row block share an XCD (tvq_gemm.h)
+    xcd_tile((int)blockIdx.x, nblk, &mblk, &nb);
+    if (mblk * 128 >= g.M) return;
+  }
+  const int n0 = nb * 32;
   if (B_KCONTIG) {
     for (int e = tid; e < 32 * KP / 4; e += 256) {
       const int n = e / (KP / 4), k = (e - n * (KP / 4)) * 4;
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(256) void gemm_rb2_kernel(GemmArgs g) {
     const float4 v = *(const float4*)(Bs + r32 * P + h * KH + t);
     b[t] = v.x; b[t + 1] = v.y; b[t + 2] = v.z; b[t + 3] = v.w;
   }
-  const int mt = blockIdx.x * 4 + wid;
+  const int mt = mblk * 4 + wid;
   if (mt * 32 >= g.M) return;
   int row = mt * 32 + r32;
   row = row < g.M ? row : g.M - 1;
@@ -197,8 +202,15 @@ __global__ __launch_bounds__(256) void gemm_rb2_kernel(GemmArgs g) {
 
 template <int KH, bool BKC>
 static void launch_rb2(const GemmArgs& g, hipStream_t st) {
+  static const int xcd = [] {  // TVQ_GEMM_XCD=0: row-major 2-D grid (comparisons)
+    const char* e = getenv("TVQ_GEMM_XCD");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
   const int mb = (g.M + 127) / 128, nb = (g.N + 31) / 32;
-  hipLaunchKernelGGL((gemm_rb2_kernel<KH, BKC>), dim3(mb, nb), dim3(256), 0, st, g);
+  if (xcd)
+    hipLaunchKernelGGL((gemm_rb2_kernel<KH, BKC>), dim3(xcd_grid(mb, nb)), dim3(256), 0, st, g, nb, 1);
+  else
+    hipLaunchKernelGGL((gemm_rb2_kernel<KH, BKC>), dim3(mb, nb), dim3(256), 0, st, g, nb, 0);
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }

@@ -27,6 +27,9 @@ SHAPES = [
     ("lf_logits_dx_train", 6144, 128, 512, "nn"),
     ("lf_logits_dw_train", 512, 128, 6144, "tn"),
     ("hf_head_dw_train", 128, 256, 24576, "tn"),
+    ("hf_dx_train", 24832, 32, 64, "nn"),
+    ("hf_dw_train", 32, 32, 24832, "tn"),
+    ("hf_ff_dw_train", 64, 32, 24832, "tn"),
 ]
 
 
