@@ -287,14 +287,15 @@ int tvq_reduce_rows(const float* in, int64_t P, int64_t N, int64_t ld, float* ou
  * nn.Linear and friends: C[m,n] = epi(alpha * sum_k A(m,k) B(k,n)),
  * A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn]; epi: + bias[n]
  * (pre-activation copy to `pre` if non-NULL), act (0 none, 1 GELU-erf),
- * + R[(rmod ? m % rmod : m)*ldr + n] (residual, or the per-position logits bias
+ * times *gate (device scalar, if non-NULL: x-transformers layer dropout fused into
+ * the branch's output Linear), + R[(rmod ? m % rmod : m)*ldr + n] (residual, or the per-position logits bias
  * of bidirectional_transformer.py:187), accumulate (C +=).  Workspace
  * (tvq_gemm_workspace floats) enables deterministic split-K. */
 int64_t tvq_gemm_workspace(int64_t M, int64_t N, int64_t K);
 int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
              float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha,
              const float* bias, const float* R, int64_t ldr, int64_t rmod, int64_t act, float* pre,
-             int64_t accumulate, float* workspace, tvq_stream_t stream);
+             int64_t accumulate, const float* gate, float* workspace, tvq_stream_t stream);
 
 /* ------------------------------------------------------ losses, optimizer
  * F.mse_loss (kind 0) / F.l1_loss (kind 1) means (stage1.py:129,133); backward
@@ -340,8 +341,10 @@ int tvq_rmsnorm_fwd(const float* x, int64_t M, int64_t D, const float* g, float 
                     float* inv_norm, tvq_stream_t stream);
 int64_t tvq_norm_bwd_workspace(int64_t M, int64_t D);
 int tvq_rmsnorm_bwd(const float* dy, const float* x, int64_t M, int64_t D, const float* g,
-                    float scale, const float* inv_norm, float* dx, float* dg, int64_t accumulate,
-                    float* workspace, tvq_stream_t stream);
+                    float scale, const float* inv_norm, const float* dres, float* dx, float* dg,
+                    int64_t accumulate, float* workspace, tvq_stream_t stream);
+/* y[i] = x[i] * s[0] (s a device scalar; the gradient of a layer-dropout-gated branch). */
+int tvq_scale_by(const float* x, int64_t n, const float* s, float* y, tvq_stream_t stream);
 int tvq_layernorm_fwd(const float* x, int64_t M, int64_t D, const float* gamma, const float* beta,
                       float eps, float* y, float* mean, float* rstd, tvq_stream_t stream);
 int tvq_layernorm_bwd(const float* dy, const float* x, int64_t M, int64_t D, const float* gamma,

@@ -17,6 +17,8 @@ struct GemmArgs {
   int64_t rmod;    // R row = m % rmod when > 0 (per-position bias broadcast over the batch)
   float* pre;      // optional: pre-activation output (ldc layout), for the GELU backward
   int act;         // 0 none, 1 GELU(erf)
+  const float* gate;  // optional device scalar: the (activated) result times *gate, before
+                      // R / accumulate (x-transformers layer dropout: keep = 0 or 1)
   int accumulate;  // C += result
   float alpha;
   int kper;        // K range per split

@@ -22,6 +22,7 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& g, int m, int n, floa
   if (g.bias) v += g.bias[n];
   if (g.pre) g.pre[(int64_t)m * g.ldc + n] = v;
   if (g.act == 1) v = gelu_erf(v);
+  if (g.gate) v *= *g.gate;
   if (g.R) v += g.R[(int64_t)(g.rmod > 0 ? m % g.rmod : m) * g.ldr + n];
   if (g.accumulate) v += g.C[(int64_t)m * g.ldc + n];
   return v;
@@ -174,6 +175,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) v[r][j] = gelu_erf(v[r][j]);
     }
+    if (g.gate) {
+      const float gt = *g.gate;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) v[r][j] *= gt;
+    }
     if (g.R) {
       float rv[4][FN];
 #pragma unroll
@@ -269,15 +277,15 @@ extern "C" int64_t tvq_gemm_workspace(int64_t M, int64_t N, int64_t K) {
 extern "C" int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
                         int64_t sbn, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
                         float alpha, const float* bias, const float* R, int64_t ldr, int64_t rmod,
-                        int64_t act, float* pre, int64_t accumulate, float* workspace,
-                        tvq_stream_t stream) {
+                        int64_t act, float* pre, int64_t accumulate, const float* gate,
+                        float* workspace, tvq_stream_t stream) {
   TVQ_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0, "tvq_gemm: bad arguments");
   GemmArgs g;
   g.A = A; g.B = B; g.C = C;
   g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.sam = sam; g.sak = sak; g.sbk = sbk; g.sbn = sbn; g.ldc = ldc;
   g.bias = bias; g.R = R; g.ldr = ldr; g.rmod = rmod; g.pre = pre;
-  g.act = (int)act; g.accumulate = (int)accumulate;
+  g.act = (int)act; g.accumulate = (int)accumulate; g.gate = gate;
   g.alpha = alpha;
   g.kper = (int)K;
   g.cnt = nullptr;

@@ -42,6 +42,7 @@ __device__ __forceinline__ float epi_value(const GemmArgs& g, int m, int n, floa
   const int64_t ci = (int64_t)m * g.ldc + n;
   if (g.pre) g.pre[ci] = v;
   if (g.act == 1) v = gelu_erf(v);
+  if (g.gate) v *= *g.gate;
   if (g.R) v += g.R[(int64_t)(g.rmod > 0 ? m % g.rmod : m) * g.ldr + n];
   if (g.accumulate) v += g.C[ci];
   return v;
@@ -181,6 +182,7 @@ __global__ __launch_bounds__(256) void gemm_dk_kernel(GemmArgs g, int kw, int nb
         const int64_t ci = (int64_t)m * g.ldc + n;
         if (g.pre) g.pre[ci] = v;
         if (g.act == 1) v = gelu_erf(v);
+        if (g.gate) v *= *g.gate;
         if (g.R) v += g.R[(int64_t)(g.rmod > 0 ? m % g.rmod : m) * g.ldr + n];
         if (g.accumulate) v += g.C[ci];
         g.C[ci] = v;

@@ -111,6 +111,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g) {
       const int64_t ci = (int64_t)m * g.ldc + ncol;
       if (g.pre) g.pre[ci] = v;
       if (g.act == 1) v = gelu_erf(v);
+      if (g.gate) v *= *g.gate;
       if (g.R) v += g.R[(int64_t)(g.rmod > 0 ? m % g.rmod : m) * g.ldr + ncol];
       if (g.accumulate) v += g.C[ci];
       g.C[ci] = v;
@@ -194,6 +195,7 @@ __global__ __launch_bounds__(256) void gemm_rb2_kernel(GemmArgs g, int nblk, int
     const int64_t ci = (int64_t)m * g.ldc + ncol;
     if (g.pre) g.pre[ci] = v;
     if (g.act == 1) v = gelu_erf(v);
+    if (g.gate) v *= *g.gate;
     if (g.R) v += g.R[(int64_t)(g.rmod > 0 ? m % g.rmod : m) * g.ldr + ncol];
     if (g.accumulate) v += g.C[ci];
     g.C[ci] = v;

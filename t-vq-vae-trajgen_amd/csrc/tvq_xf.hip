@@ -46,7 +46,8 @@ __global__ void rmsnorm_fwd_kernel(const float* __restrict__ x, int64_t M, int D
 // dx; and per-block partial dg (deterministic, reduced by colsum_kernel)
 __global__ void rmsnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                    int64_t M, int D, const float* __restrict__ g, float scale,
-                                   const float* __restrict__ inv_norm, float* __restrict__ dx,
+                                   const float* __restrict__ inv_norm,
+                                   const float* __restrict__ dres, float* __restrict__ dx,
                                    float* __restrict__ dg_part, int rows_per_block) {
   extern __shared__ float sh[];  // [waves][D] partial dg
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -63,7 +64,8 @@ __global__ void rmsnorm_bwd_kernel(const float* __restrict__ dy, const float* __
     dot = wave_sum(dot);
     const float c = dot * scale * inv * inv * inv;
     for (int d = lane; d < D; d += 64) {
-      dx[row * D + d] = gr[d] * g[d] * scale * inv - xr[d] * c;
+      const float v = gr[d] * g[d] * scale * inv - xr[d] * c;
+      dx[row * D + d] = dres ? v + dres[row * D + d] : v;  // + the residual path's gradient
       sh[wid * D + d] += gr[d] * xr[d] * inv * scale;
     }
   }
@@ -347,9 +349,31 @@ static int norm_rows_per_block(int64_t M) {
   return (int)(r < 4 ? 4 : r);
 }
 
+__global__ void scale_by_kernel(const float4* __restrict__ x, int64_t n4, const float* __restrict__ s,
+                                float4* __restrict__ y) {
+  const float f = *s;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = x[i];
+    y[i] = make_float4(v.x * f, v.y * f, v.z * f, v.w * f);
+  }
+}
+
 }  // namespace tvq
 
 using namespace tvq;
+
+extern "C" int tvq_scale_by(const float* x, int64_t n, const float* s, float* y,
+                            tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && s && y && n > 0 && n % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
+                    ((uintptr_t)y & 15) == 0,
+                "tvq_scale_by: bad arguments");
+  const int64_t n4 = n / 4;
+  const int blocks = (int)((n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048);
+  hipLaunchKernelGGL(scale_by_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const float4*)x, n4, s, (float4*)y);
+  return launch_status("tvq_scale_by");
+}
 
 extern "C" int tvq_rmsnorm_fwd(const float* x, int64_t M, int64_t D, const float* g, float scale,
                                float* y, float* inv_norm, tvq_stream_t stream) {
@@ -366,15 +390,15 @@ extern "C" int64_t tvq_norm_bwd_workspace(int64_t M, int64_t D) {
 }
 
 extern "C" int tvq_rmsnorm_bwd(const float* dy, const float* x, int64_t M, int64_t D,
-                               const float* g, float scale, const float* inv_norm, float* dx,
-                               float* dg, int64_t accumulate, float* workspace,
-                               tvq_stream_t stream) {
+                               const float* g, float scale, const float* inv_norm,
+                               const float* dres, float* dx, float* dg, int64_t accumulate,
+                               float* workspace, tvq_stream_t stream) {
   TVQ_CHECK_ARG(dy && x && g && inv_norm && dx && dg && workspace, "tvq_rmsnorm_bwd: bad args");
   const int rpb = norm_rows_per_block(M);
   const int nb = (int)((M + rpb - 1) / rpb);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(nb), dim3(256), 4 * D * sizeof(float), st, dy, x, M,
-                     (int)D, g, scale, inv_norm, dx, workspace, rpb);
+                     (int)D, g, scale, inv_norm, dres, dx, workspace, rpb);
   reduce_rows(workspace, nb, D, D, dg, nullptr, 0, (int)accumulate, workspace + (int64_t)nb * 2 * D,
               st);
   return launch_status("tvq_rmsnorm_bwd");

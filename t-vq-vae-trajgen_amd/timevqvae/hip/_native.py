@@ -81,7 +81,7 @@ sig("tvq_reduce_rows_workspace", I64, I64, restype=I64)
 sig("tvq_reduce_rows", P, I64, I64, I64, P, I64, P, P)
 # --- dense GEMM --------------------------------------------------------------
 sig("tvq_gemm_workspace", I64, I64, I64, restype=I64)
-sig("tvq_gemm", P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, F32, P, P, I64, I64, I64, P, I64, P, P)
+sig("tvq_gemm", P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, F32, P, P, I64, I64, I64, P, I64, P, P, P)
 # --- losses / optimizer --------------------------------------------------------
 sig("tvq_loss_workspace", I64, restype=I64)
 sig("tvq_loss_fwd", P, P, I64, I64, P, P, P)
@@ -95,7 +95,8 @@ sig("tvq_layer_drop", P, ctypes.c_uint64, F32, I64, P, P, I64, P)
 # --- MaskGIT transformer ---------------------------------------------------------
 sig("tvq_rmsnorm_fwd", P, I64, I64, P, F32, P, P, P)
 sig("tvq_norm_bwd_workspace", I64, I64, restype=I64)
-sig("tvq_rmsnorm_bwd", P, P, I64, I64, P, F32, P, P, P, I64, P, P)
+sig("tvq_rmsnorm_bwd", P, P, I64, I64, P, F32, P, P, P, P, I64, P, P)
+sig("tvq_scale_by", P, I64, P, P, P)
 sig("tvq_layernorm_fwd", P, I64, I64, P, P, F32, P, P, P, P)
 sig("tvq_layernorm_bwd", P, P, I64, I64, P, P, P, P, P, P, I64, P, P)
 sig("tvq_attention_fwd", P, I64, P, I64, P, I64, P, I64, P, I64, I64, I64, I64, F32, F32, P, U64, P)

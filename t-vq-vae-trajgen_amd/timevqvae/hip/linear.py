@@ -6,7 +6,7 @@ from ._native import call, grad_sink, ptr, stream_ptr, value
 
 
 def gemm(A, sam, sak, B, sbk, sbn, M, N, K, out=None, ldc=None, alpha=1.0, bias=None, R=None,
-         ldr=0, rmod=0, act=0, pre=None, accumulate=False):
+         ldr=0, rmod=0, act=0, pre=None, accumulate=False, gate=None):
     dev = A.device
     if out is None:
         out = torch.empty((M, N), device=dev, dtype=torch.float32)
@@ -14,8 +14,8 @@ def gemm(A, sam, sak, B, sbk, sbn, M, N, K, out=None, ldc=None, alpha=1.0, bias=
     wsz = value("tvq_gemm_workspace", M, N, K)
     ws = torch.empty(wsz, device=dev, dtype=torch.float32) if wsz > 0 else None
     call("tvq_gemm", ptr(A), sam, sak, ptr(B), sbk, sbn, ptr(out), ldc, M, N, K, float(alpha),
-         ptr(bias), ptr(R), ldr, int(rmod), int(act), ptr(pre), int(bool(accumulate)), ptr(ws),
-         stream_ptr())
+         ptr(bias), ptr(R), ldr, int(rmod), int(act), ptr(pre), int(bool(accumulate)), ptr(gate),
+         ptr(ws), stream_ptr())
     return out
 
 
@@ -43,9 +43,17 @@ def weight_grad(g, x2, w_param, M, N, K):
     return gemm(g, 1, N, x2, K, 1, N, K, M)
 
 
+def scale_by(x, s):
+    """x * s[0] (s: a one-element device tensor) in one kernel."""
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    call("tvq_scale_by", ptr(x), x.numel(), ptr(s), ptr(y), stream_ptr())
+    return y
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, residual):
+    def forward(ctx, x, w, b, residual, gate):
         shp = x.shape
         K = shp[-1]
         N = w.shape[0]
@@ -53,11 +61,12 @@ class _Linear(torch.autograd.Function):
         w = w.contiguous()
         M = x2.shape[0]
         R = residual.reshape(M, N).contiguous() if residual is not None else None
-        y = gemm(x2, K, 1, w, 1, K, M, N, K, bias=b, R=R, ldr=N)
+        y = gemm(x2, K, 1, w, 1, K, M, N, K, bias=b, R=R, ldr=N, gate=gate)
         ctx.save_for_backward(x2, w)
         ctx.has = (b is not None, residual is not None)
         ctx.shp = shp
         ctx.params = (w, b)
+        ctx.gate = gate
         return y.reshape(*shp[:-1], N)
 
     @staticmethod
@@ -65,19 +74,21 @@ class _Linear(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         M, K = x2.shape
         N = w.shape[0]
-        g = gy.reshape(M, N).contiguous()
-        dx = dw = db = dres = None
+        dres = gy if ctx.has[1] and ctx.needs_input_grad[3] else None
+        # gated branch (layer dropout): the branch's gradient is gate * gy
+        g = scale_by(gy, ctx.gate) if ctx.gate is not None else gy
+        g = g.reshape(M, N).contiguous()
+        dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = gemm(g, N, 1, w, K, 1, M, K, N).reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
             dw = weight_grad(g, x2, ctx.params[0], M, N, K)
         if ctx.has[0] and ctx.needs_input_grad[2]:
             db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
-        if ctx.has[1] and ctx.needs_input_grad[3]:
-            dres = gy
-        return dx, dw, db, dres
+        return dx, dw, db, dres, None
 
 
-def linear(x, weight, bias=None, residual=None):
-    """residual + x @ weight^T + bias over the last dim (nn.Linear; vq_vae.py:255,263)."""
-    return _Linear.apply(x, weight, bias, residual)
+def linear(x, weight, bias=None, residual=None, gate=None):
+    """residual + gate * (x @ weight^T + bias) over the last dim (nn.Linear; vq_vae.py:255,263;
+    `gate`: optional one-element device tensor, the x-transformers layer-dropout keep flag)."""
+    return _Linear.apply(x, weight, bias, residual, gate)

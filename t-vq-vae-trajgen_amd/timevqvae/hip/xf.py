@@ -37,14 +37,55 @@ class _RMSNorm(torch.autograd.Function):
         sink = grad_sink(ctx.g_param)
         dg = sink if sink is not None else torch.empty(D, device=x2.device)
         ws = torch.empty(value("tvq_norm_bwd_workspace", M, D), device=x2.device)
-        call("tvq_rmsnorm_bwd", ptr(dy), ptr(x2), M, D, ptr(g), float(ctx.scale), ptr(inv), ptr(dx),
-             ptr(dg), int(sink is not None), ptr(ws), stream_ptr())
+        call("tvq_rmsnorm_bwd", ptr(dy), ptr(x2), M, D, ptr(g), float(ctx.scale), ptr(inv), None,
+             ptr(dx), ptr(dg), int(sink is not None), ptr(ws), stream_ptr())
         return dx.reshape(ctx.shape), (None if sink is not None else dg), None
 
 
 def rmsnorm(x, g):
     """x-transformers RMSNorm: F.normalize(x, dim=-1) * sqrt(D) * g."""
     return _RMSNorm.apply(x, g, math.sqrt(x.shape[-1]))
+
+
+class _RMSNormRes(torch.autograd.Function):
+    """(RMSNorm(x), x) for a pre-norm residual layer x + f(RMSNorm(x)): the second output
+    (the residual stream) is what the branch's output Linear adds, so x has a single
+    autograd consumer and dx = RMSNorm'(dn) + dres comes out of one kernel instead of an
+    autograd accumulation add."""
+
+    @staticmethod
+    def forward(ctx, x, g, scale):
+        x2, M, D = _rows(x.contiguous())
+        y = torch.empty_like(x2)
+        inv = torch.empty(M, device=x.device, dtype=torch.float32)
+        call("tvq_rmsnorm_fwd", ptr(x2), M, D, ptr(g), float(scale), ptr(y), ptr(inv), stream_ptr())
+        ctx.save_for_backward(x2, g, inv)
+        ctx.g_param = g
+        ctx.scale = scale
+        ctx.shape = x.shape
+        return y.reshape(x.shape), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, gy, gr):
+        x2, g, inv = ctx.saved_tensors
+        M, D = x2.shape
+        dx = torch.empty_like(x2)
+        if gy is None:  # the normalised output unused: only the residual path
+            return gr, None, None
+        dy = gy.reshape(M, D).contiguous()
+        dres = gr.reshape(M, D).contiguous() if gr is not None else None
+        sink = grad_sink(ctx.g_param)
+        dg = sink if sink is not None else torch.empty(D, device=x2.device)
+        ws = torch.empty(value("tvq_norm_bwd_workspace", M, D), device=x2.device)
+        call("tvq_rmsnorm_bwd", ptr(dy), ptr(x2), M, D, ptr(g), float(ctx.scale), ptr(inv),
+             ptr(dres), ptr(dx), ptr(dg), int(sink is not None), ptr(ws), stream_ptr())
+        return dx.reshape(ctx.shape), (None if sink is not None else dg), None
+
+
+def rmsnorm_res(x, g):
+    """(RMSNorm(x), residual stream x) with the residual gradient summed in the norm's
+    backward kernel (see _RMSNormRes)."""
+    return _RMSNormRes.apply(x, g, math.sqrt(x.shape[-1]))
 
 
 # ---------------------------------------------------------------- LayerNorm
@@ -170,6 +211,86 @@ class _Attention(torch.autograd.Function):
 def attention(q, k, v, heads, drop_p=0.0, site=0):
     """softmax(q k^T / sqrt(64)) [dropout] v per head; q/k/v (B, S, heads*64)."""
     return _Attention.apply(q, k, v, int(heads), float(drop_p), int(site))
+
+
+def _stacked(ws, shape):
+    """The row-stacked matrix of `ws` as one view when they are consecutive in memory
+    (FusedAdamW's flat buffers keep to_q, to_k, to_v adjacent), else None."""
+    p0 = ws[0]
+    if any(w is None or not w.is_contiguous() for w in ws):
+        return None
+    step = p0.numel() * p0.element_size()
+    base = p0.untyped_storage().data_ptr()
+    if any(w.untyped_storage().data_ptr() != base or w.data_ptr() != p0.data_ptr() + i * step
+           for i, w in enumerate(ws)):
+        return None  # separate storages (adjacent allocations are not one buffer)
+    return torch.as_strided(p0, shape, (shape[1], 1))
+
+
+class _QKVAttention(torch.autograd.Function):
+    """o = attention(x Wq^T, x Wk^T, x Wv^T): the three projections as ONE GEMM against the
+    row-stacked [Wq; Wk; Wv] (a view of the flat parameters when they are adjacent), the
+    attention reading q / k / v as strided column blocks of its output; the backward
+    writes dq | dk | dv into one buffer, then one input-gradient GEMM and one weight-
+    gradient GEMM (straight into the stacked flat-gradient view) replace three of each
+    and their two accumulation adds."""
+
+    @staticmethod
+    def forward(ctx, x, wq, wk, wv, heads, drop_p, site):
+        B, S, D = x.shape
+        HD = wq.shape[0]
+        x2 = x.reshape(B * S, D).contiguous()
+        M = B * S
+        W = _stacked([wq, wk, wv], (3 * HD, D))
+        if W is None:
+            W = torch.cat([wq, wk, wv], 0).contiguous()
+        qkv = gemm(x2, D, 1, W, 1, D, M, 3 * HD, D)
+        Dh = HD // heads
+        o = torch.empty((M, HD), device=x.device)
+        lse = torch.empty(B * heads * S, device=x.device)
+        seed = rng.seed_tensor(x.device) if drop_p > 0 else None
+        off = rng.call_offset(site) if drop_p > 0 else 0
+        scale = Dh ** -0.5
+        L = 3 * HD
+        call("tvq_attention_fwd", ptr(qkv), L, ptr(qkv[:, HD:]), L, ptr(qkv[:, 2 * HD:]), L, ptr(o),
+             HD, ptr(lse), B, heads, S, Dh, float(scale), float(drop_p), ptr(seed), off,
+             stream_ptr())
+        ctx.save_for_backward(x2, W, qkv, o, lse)
+        ctx.params = (wq, wk, wv)
+        ctx.cfg = (B, S, D, HD, heads, drop_p, off, scale)
+        ctx.seed = seed
+        return o.reshape(B, S, HD)
+
+    @staticmethod
+    def backward(ctx, go):
+        x2, W, qkv, o, lse = ctx.saved_tensors
+        B, S, D, HD, heads, drop_p, off, scale = ctx.cfg
+        M, L, Dh = B * S, 3 * HD, HD // heads
+        go = go.reshape(M, HD).contiguous()
+        dqkv = torch.empty((M, L), device=go.device)
+        call("tvq_attention_bwd", ptr(qkv), L, ptr(qkv[:, HD:]), L, ptr(qkv[:, 2 * HD:]), L, ptr(o),
+             HD, ptr(go), HD, ptr(lse), B, heads, S, Dh, float(scale), float(drop_p),
+             ptr(ctx.seed), off, ptr(dqkv), ptr(dqkv[:, HD:]), ptr(dqkv[:, 2 * HD:]), L,
+             stream_ptr())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(dqkv, L, 1, W, D, 1, M, D, L).reshape(B, S, D)
+        dws = [None, None, None]
+        if any(ctx.needs_input_grad[1:4]):
+            sinks = [grad_sink(p) for p in ctx.params]
+            sink = _stacked(sinks, (L, D)) if all(s is not None for s in sinks) else None
+            if sink is not None:  # into the flat gradient (stacked view)
+                with streams.offload(dqkv, x2):
+                    gemm(dqkv, 1, L, x2, D, 1, L, D, M, out=sink, ldc=D, accumulate=True)
+            else:
+                dW = gemm(dqkv, 1, L, x2, D, 1, L, D, M)
+                dws = [dW[i * HD:(i + 1) * HD] for i in range(3)]
+        return (dx, *dws, None, None, None)
+
+
+def qkv_attention(x, wq, wk, wv, heads, drop_p=0.0, site=0):
+    """attention(x Wq^T, x Wk^T, x Wv^T) with the projections fused (_QKVAttention)."""
+    return _QKVAttention.apply(x, wq, wk, wv, int(heads), float(drop_p), int(site))
 
 
 # ---------------------------------------------------------------- embedding

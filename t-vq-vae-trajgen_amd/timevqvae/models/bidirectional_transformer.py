@@ -27,8 +27,8 @@ from ..hip import rng, streams
 from ..hip.conv import conv2d
 from ..hip.linear import _bias_grad_rows, gemm, linear
 from ..hip.norm import bn_snake
-from ..hip.xf import (attention, embedding, gelu, layer_norm, linear_act, rmsnorm,
-                      upsample_nearest)
+from ..hip.xf import (embedding, gelu, layer_norm, linear_act, qkv_attention, rmsnorm,
+                      rmsnorm_res, upsample_nearest)
 from ..hip._native import call, grad_sink, ptr, stream_ptr
 
 
@@ -66,12 +66,10 @@ class Attention(nn.Module):
         self.dropout = dropout
         self._site = rng.new_site()
 
-    def forward(self, x, residual):
-        q = linear(x, self.to_q.weight)
-        k = linear(x, self.to_k.weight)
-        v = linear(x, self.to_v.weight)
-        o = attention(q, k, v, self.heads, self.dropout if self.training else 0.0, self._site)
-        return linear(o, self.to_out.weight, None, residual=residual)
+    def forward(self, x, residual, gate=None):
+        o = qkv_attention(x, self.to_q.weight, self.to_k.weight, self.to_v.weight, self.heads,
+                          self.dropout if self.training else 0.0, self._site)
+        return linear(o, self.to_out.weight, None, residual=residual, gate=gate)
 
 
 class FeedForward(nn.Module):
@@ -82,14 +80,14 @@ class FeedForward(nn.Module):
                                 nn.Linear(inner, dim))
         self._site = rng.new_site()
 
-    def forward(self, x, residual):
+    def forward(self, x, residual, gate=None):
         lin1 = self.ff[0][0]
         h = linear_act(x, lin1.weight, lin1.bias, gelu=True)
         p = self.ff[1].p if self.training else 0.0
         if p > 0:
             h = dropout(h, p, self._site)
         lin2 = self.ff[2]
-        return linear(h, lin2.weight, lin2.bias, residual=residual)
+        return linear(h, lin2.weight, lin2.bias, residual=residual, gate=gate)
 
 
 class Residual(nn.Module):
@@ -157,12 +155,16 @@ class Encoder(nn.Module):
             self._touched_host = [1.0] * len(self.layers)
             self._touched.fill_(1.0)
         for i, (norms, block, _) in enumerate(self.layers):
-            if device_gates:
-                x = torch.addcmul(x, block(norms[0](x), residual=None), self._keep[i])
-                continue
             if keep is not None and keep[i] == 0.0:
                 continue
-            x = block(norms[0](x), residual=x)
+            # device gates (graph capture): x + keep_i * branch, the gate applied in the
+            # branch's output-Linear epilogue (its backward scales the branch gradient)
+            gate = self._keep[i:i + 1] if device_gates else None
+            if isinstance(norms[0], RMSNorm):
+                n, r = rmsnorm_res(x, norms[0].g)  # residual gradient summed in the norm bwd
+                x = block(n, residual=r, gate=gate)
+            else:
+                x = block(norms[0](x), residual=x, gate=gate)
         return self.final_norm(x)
 
 
