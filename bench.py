@@ -299,34 +299,35 @@ def _graph_time_us(fns, reps):
 
 
 def dominant_leg(device):
-    """The step's dominant kernel (profiles/r02_step_kernel_stats.csv, first row):
-    conv_halo_kernel<F,3,3,1,...,FN=1,KS=1>, the forward of every ResBlock 3x3 conv with
-    8 or 16 channels (LF/HF encoders + decoders + stage2's frozen encoders: 49 launches per
-    step).  Its two step shapes, (256,8,3,64)x(8,8,3,3) and (256,16,3,32)x(16,16,3,3), move
-    the same algorithmic bytes per launch (input + output + weight + bias, fp32 = 3.15 MB)
-    at 56.6 / 56.6 MFLOP: HBM-class (arithmetic intensity 18 FLOP/B).  Timed here as 2x25
-    graph-replayed launches with HIP events on their stream."""
-    from timevqvae.hip.conv import conv2d
-    fns, byts = [], 0
-    for Ci, W in ((8, 64), (16, 32)):
-        x = torch.randn(B, Ci, 3, W, device=device)
-        w = torch.randn(Ci, Ci, 3, 3, device=device) * 0.1
-        b = torch.zeros(Ci, device=device)
-        fns.append(lambda x=x, w=w, b=b: conv2d(x, w, b))
-        byts += 4 * (2 * x.numel() + w.numel() + b.numel())
+    """The step's dominant kernel (profiles/r02c_step_kernel_stats.csv, first row):
+    gemm_kt_kernel, the weight-gradient GEMM dW (+)= dY^T X of every transformer Linear
+    (direct-operand 32x32x2 fp32 MFMA, K = tokens split over 4 waves x `splits` blocks) with
+    its slab sum gemm_direct_reduce_kernel (one op = these 2 launches).  Timed at its
+    commonest step shape, the LF prior's Linear(128 -> 128) over 6400 tokens (B=256 x 25),
+    accumulating into a flat-gradient view as the step does: 2*6400*128*128 = 209.7 MFLOP
+    and 4*(2*6400*128 + 2*128*128) = 6.68 MB algorithmic per op (AI 31 FLOP/B: fp32 MFMA
+    bound).  50 graph-replayed ops timed with HIP events on their stream."""
+    from timevqvae.hip.linear import gemm
+    M, N, K = 6400, 128, 128  # tokens, out features, in features
+    g = torch.randn(M, N, device=device)
+    x = torch.randn(M, K, device=device)
+    dw = torch.zeros(N, K, device=device)
+    fn = (lambda: gemm(g, 1, N, x, K, 1, N, K, M, out=dw, ldc=K, accumulate=True))
     with torch.no_grad():
-        us = _graph_time_us(fns, 25)
-    per_launch = byts / 2
-    achieved = per_launch / (us * 1e-6) / 1e9
+        us = _graph_time_us([fn], 50)
+    flops = 2.0 * M * N * K
+    byts = 4.0 * (M * N + M * K + 2 * N * K)
+    tf = flops / (us * 1e-6) / 1e12
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "r02_dominant_traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath))["traffic_bytes"]
-    return {"bound": "hbm", "kernel": "conv_halo_kernel<0,3,3,1,false,1,1> (ResBlock 3x3 conv "
-                                      "fwd, C=8 @W64 and C=16 @W32, B=256)",
-            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "algorithmic_bytes": per_launch, "avg_launch_us": round(us, 2)}
+    return {"bound": "mfma", "kernel": "gemm_kt_kernel + gemm_direct_reduce_kernel (weight-gradient "
+                                       "GEMM dW += dY^T X, 128x128 over 6400 tokens, fp32 MFMA)",
+            "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def roofline_leg(device, ms_per_step):
