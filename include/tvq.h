@@ -343,6 +343,22 @@ int64_t tvq_norm_bwd_workspace(int64_t M, int64_t D);
 int tvq_rmsnorm_bwd(const float* dy, const float* x, int64_t M, int64_t D, const float* g,
                     float scale, const float* inv_norm, const float* dres, float* dx, float* dg,
                     int64_t accumulate, float* workspace, tvq_stream_t stream);
+/* Token-embedding assembly (bidirectional_transformer.py:185,229-231): out (B, n+1, D1+D2)
+ * = cat(cls (B, D1+D2), [t1 | t2] + pos[:n], dim=1), t1/t2 read through (b, j, d) strides
+ * (t2 NULL with D2 = 0 for the LF prior).  Backward: dcls / dt1 / dt2 (same strides, each
+ * NULL to skip) = the matching slices of dout; dpos (n, D1+D2) (+)= sum over b in order. */
+int tvq_embed_assemble(const float* cls, const float* t1, int64_t s1b, int64_t s1n, int64_t s1d,
+                       int64_t D1, const float* t2, int64_t s2b, int64_t s2n, int64_t s2d,
+                       int64_t D2, const float* pos, int64_t B, int64_t n, float* out,
+                       tvq_stream_t stream);
+int tvq_embed_assemble_bwd(const float* dout, int64_t B, int64_t n, int64_t D1, int64_t D2,
+                           float* dcls, float* dt1, int64_t s1b, int64_t s1n, int64_t s1d,
+                           float* dt2, int64_t s2b, int64_t s2n, int64_t s2d, float* dpos,
+                           int64_t accumulate, tvq_stream_t stream);
+/* Training class conditioning (bidirectional_transformer.py:124-150): idx[b] = y[b] if
+ * u_b > p else null_id; u_b = rnd[b] (injected) or the device counter RNG at (seed, offset). */
+int tvq_class_index(const int64_t* y, int64_t B, float p, int64_t null_id, const int64_t* seed_ptr,
+                    uint64_t offset, const float* rnd, int64_t* idx, tvq_stream_t stream);
 /* y[i] = x[i] * s[0] (s a device scalar; the gradient of a layer-dropout-gated branch). */
 int tvq_scale_by(const float* x, int64_t n, const float* s, float* y, tvq_stream_t stream);
 int tvq_layernorm_fwd(const float* x, int64_t M, int64_t D, const float* gamma, const float* beta,

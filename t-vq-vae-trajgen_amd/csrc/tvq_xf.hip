@@ -349,6 +349,90 @@ static int norm_rows_per_block(int64_t M) {
   return (int)(r < 4 ? 4 : r);
 }
 
+
+// ------------------------------------------------------- embedding assembly
+// bidirectional_transformer.py:185,229-231: embed = cat(cls_emb, tok + pos_emb[:n], dim=1)
+// with tok = [t1 | t2] along features (HF: Upscale(LF emb) | HF emb; LF: t1 only).
+// Token inputs are read through strides (the Upscale output is a (b, m, d) view of a
+// (b, d, m) tensor); the backward writes their gradients with the same strides.
+struct AsmTok {
+  const float* p;
+  float* g;
+  int64_t sb, sn, sd;
+  int D;
+};
+
+__global__ void embed_assemble_kernel(const float* __restrict__ cls, AsmTok t1, AsmTok t2,
+                                      const float* __restrict__ pos, int B, int n,
+                                      float* __restrict__ out) {
+  const int Dt = t1.D + t2.D;
+  const int64_t tot = (int64_t)B * (n + 1) * Dt;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(e % Dt);
+    const int64_t r = e / Dt;
+    const int i = (int)(r % (n + 1));
+    const int b = (int)(r / (n + 1));
+    float v;
+    if (i == 0) {
+      v = cls[(int64_t)b * Dt + d];
+    } else {
+      const int j = i - 1;
+      const float tv = d < t1.D ? t1.p[b * t1.sb + j * t1.sn + d * t1.sd]
+                                : t2.p[b * t2.sb + j * t2.sn + (d - t1.D) * t2.sd];
+      v = tv + pos[(int64_t)j * Dt + d];
+    }
+    out[e] = v;
+  }
+}
+
+// dcls[b, d] = dout[b, 0, d]; dt[b, j, d] = dout[b, 1 + j, d] (through the tokens' strides)
+__global__ void embed_assemble_split_kernel(const float* __restrict__ dout, int B, int n,
+                                            float* __restrict__ dcls, AsmTok t1, AsmTok t2) {
+  const int Dt = t1.D + t2.D;
+  const int64_t tot = (int64_t)B * (n + 1) * Dt;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(e % Dt);
+    const int64_t r = e / Dt;
+    const int i = (int)(r % (n + 1));
+    const int b = (int)(r / (n + 1));
+    const float v = dout[e];
+    if (i == 0) {
+      if (dcls) dcls[(int64_t)b * Dt + d] = v;
+    } else if (d < t1.D) {
+      if (t1.g) t1.g[b * t1.sb + (i - 1) * t1.sn + d * t1.sd] = v;
+    } else if (t2.g) {
+      t2.g[b * t2.sb + (i - 1) * t2.sn + (d - t1.D) * t2.sd] = v;
+    }
+  }
+}
+
+// dpos[j, d] (+)= sum_b dout[b, 1 + j, d], b in order (one thread per (j, d))
+__global__ void embed_pos_grad_kernel(const float* __restrict__ dout, int B, int n, int Dt,
+                                      float* __restrict__ dpos, int accumulate) {
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e >= (int64_t)n * Dt) return;
+  const int64_t bs = (int64_t)(n + 1) * Dt;
+  const float* p = dout + Dt + e;
+  float s = 0.f;
+#pragma unroll 8
+  for (int b = 0; b < B; ++b) s += p[b * bs];
+  dpos[e] = accumulate ? dpos[e] + s : s;
+}
+
+// bidirectional_transformer.py:124-150 class conditioning in training: idx[b] = y[b] where
+// u_b > p_unconditional, else the null class; u_b injected (tests) or drawn from the
+// device counter RNG
+__global__ void class_index_kernel(const int64_t* __restrict__ y, int B, float p, int64_t null_id,
+                                   const int64_t* __restrict__ seed_ptr, uint64_t offset,
+                                   const float* __restrict__ rnd, int64_t* __restrict__ idx) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float u = rnd ? rnd[b] : uniform01(mix_seed(seed_ptr, offset), (uint64_t)b);
+  idx[b] = u > p ? y[b] : null_id;
+}
+
 __global__ void scale_by_kernel(const float4* __restrict__ x, int64_t n4, const float* __restrict__ s,
                                 float4* __restrict__ y) {
   const float f = *s;
@@ -362,6 +446,49 @@ __global__ void scale_by_kernel(const float4* __restrict__ x, int64_t n4, const 
 }  // namespace tvq
 
 using namespace tvq;
+
+extern "C" int tvq_embed_assemble(const float* cls, const float* t1, int64_t s1b, int64_t s1n,
+                                  int64_t s1d, int64_t D1, const float* t2, int64_t s2b,
+                                  int64_t s2n, int64_t s2d, int64_t D2, const float* pos,
+                                  int64_t B, int64_t n, float* out, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(cls && t1 && pos && out && B > 0 && n > 0 && D1 > 0 && D2 >= 0 &&
+                    (D2 == 0 || t2),
+                "tvq_embed_assemble: bad arguments");
+  const AsmTok a1 = {t1, nullptr, s1b, s1n, s1d, (int)D1};
+  const AsmTok a2 = {t2, nullptr, s2b, s2n, s2d, (int)D2};
+  hipLaunchKernelGGL(embed_assemble_kernel, dim3(grid_for(B * (n + 1) * (D1 + D2))), dim3(256), 0,
+                     (hipStream_t)stream, cls, a1, a2, pos, (int)B, (int)n, out);
+  return launch_status("tvq_embed_assemble");
+}
+
+extern "C" int tvq_embed_assemble_bwd(const float* dout, int64_t B, int64_t n, int64_t D1,
+                                      int64_t D2, float* dcls, float* dt1, int64_t s1b, int64_t s1n,
+                                      int64_t s1d, float* dt2, int64_t s2b, int64_t s2n,
+                                      int64_t s2d, float* dpos, int64_t accumulate,
+                                      tvq_stream_t stream) {
+  TVQ_CHECK_ARG(dout && B > 0 && n > 0 && D1 > 0 && D2 >= 0, "tvq_embed_assemble_bwd: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  const AsmTok a1 = {nullptr, dt1, s1b, s1n, s1d, (int)D1};
+  const AsmTok a2 = {nullptr, dt2, s2b, s2n, s2d, (int)D2};
+  if (dcls || dt1 || dt2)
+    hipLaunchKernelGGL(embed_assemble_split_kernel, dim3(grid_for(B * (n + 1) * (D1 + D2))),
+                       dim3(256), 0, st, dout, (int)B, (int)n, dcls, a1, a2);
+  if (dpos) {
+    const int64_t m = n * (D1 + D2);
+    hipLaunchKernelGGL(embed_pos_grad_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st,
+                       dout, (int)B, (int)n, (int)(D1 + D2), dpos, (int)accumulate);
+  }
+  return launch_status("tvq_embed_assemble_bwd");
+}
+
+extern "C" int tvq_class_index(const int64_t* y, int64_t B, float p, int64_t null_id,
+                               const int64_t* seed_ptr, uint64_t offset, const float* rnd,
+                               int64_t* idx, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(y && idx && B > 0 && (rnd || seed_ptr), "tvq_class_index: bad arguments");
+  hipLaunchKernelGGL(class_index_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, y, (int)B, p, null_id, seed_ptr, offset, rnd, idx);
+  return launch_status("tvq_class_index");
+}
 
 extern "C" int tvq_scale_by(const float* x, int64_t n, const float* s, float* y,
                             tvq_stream_t stream) {

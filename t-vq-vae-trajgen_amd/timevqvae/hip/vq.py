@@ -168,6 +168,7 @@ class _VQStraightThrough(torch.autograd.Function):
             eps=eps, sync=sync, svq_temp=svq_temp)
         ctx.save_for_backward(x, out)
         ctx.mark_non_differentiable(idx, perp)
+        ctx.set_materialize_grads(False)  # no zero-filled grads for idx / perp (None handled)
         return out, idx, commit, perp
 
     @staticmethod

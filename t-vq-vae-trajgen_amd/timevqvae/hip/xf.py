@@ -334,6 +334,52 @@ def embedding(idx, table, mask_id=-1, drop_p=0.0, site=0):
     return _Embedding.apply(idx, table, int(mask_id), float(drop_p), int(site))
 
 
+# ------------------------------------------------------- embedding assembly
+class _EmbedAssemble(torch.autograd.Function):
+    """cat(cls_emb, [t1 | t2] + pos[:n], dim=1) in one kernel (bidirectional_transformer.py:
+    185,229-231); the backward splits the gradient back into the inputs' own layouts (the
+    Upscale output is a transposed view) and sums the position-table gradient over the
+    batch in order into its flat-gradient rows."""
+
+    @staticmethod
+    def forward(ctx, cls_emb, t1, t2, pos_w, n):
+        B, _, D1 = t1.shape
+        D2 = t2.shape[-1] if t2 is not None else 0
+        Dt = D1 + D2
+        cls2 = cls_emb.reshape(B, Dt).contiguous()
+        out = torch.empty((B, n + 1, Dt), device=t1.device)
+        s2 = t2.stride() if t2 is not None else (0, 0, 0)
+        call("tvq_embed_assemble", ptr(cls2), ptr(t1), *t1.stride(), D1, ptr(t2), *s2, D2,
+             ptr(pos_w), B, n, ptr(out), stream_ptr())
+        ctx.meta = (B, n, D1, D2, tuple(t1.shape), t1.stride(),
+                    None if t2 is None else (tuple(t2.shape), t2.stride()), tuple(cls_emb.shape))
+        ctx.pos_w = pos_w
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        B, n, D1, D2, sh1, st1, m2, shc = ctx.meta
+        g = g.contiguous()
+        dev = g.device
+        need = ctx.needs_input_grad
+        dcls = torch.empty(shc, device=dev) if need[0] else None
+        dt1 = torch.empty_strided(sh1, st1, device=dev) if need[1] else None
+        dt2 = torch.empty_strided(m2[0], m2[1], device=dev) if (m2 is not None and need[2]) else None
+        s2 = m2[1] if m2 is not None else (0, 0, 0)
+        sink = grad_sink(ctx.pos_w) if need[3] else None
+        dpos = None
+        if need[3]:
+            dpos = sink if sink is not None else torch.zeros_like(ctx.pos_w)
+        call("tvq_embed_assemble_bwd", ptr(g), B, n, D1, D2, ptr(dcls), ptr(dt1), *st1, ptr(dt2),
+             *s2, ptr(dpos), int(sink is not None), stream_ptr())
+        return dcls, dt1, dt2, (None if sink is not None else dpos), None
+
+
+def embed_assemble(cls_emb, t1, t2, pos_w, n):
+    """cat(cls_emb (B,1,D), [t1 | t2] + pos_w[:n], dim=1) -> (B, n+1, D) (t2 may be None)."""
+    return _EmbedAssemble.apply(cls_emb, t1, t2, pos_w, int(n))
+
+
 # ---------------------------------------------------------------- masked CE
 class _MaskedCE(torch.autograd.Function):
     @staticmethod

@@ -27,8 +27,8 @@ from ..hip import rng, streams
 from ..hip.conv import conv2d
 from ..hip.linear import _bias_grad_rows, gemm, linear
 from ..hip.norm import bn_snake
-from ..hip.xf import (embedding, gelu, layer_norm, linear_act, qkv_attention, rmsnorm,
-                      rmsnorm_res, upsample_nearest)
+from ..hip.xf import (embed_assemble, embedding, gelu, layer_norm, linear_act, qkv_attention,
+                      rmsnorm, rmsnorm_res, upsample_nearest)
 from ..hip._native import call, grad_sink, ptr, stream_ptr
 
 
@@ -328,15 +328,21 @@ class BidirectionalTransformer(nn.Module):
         draws of the classifier-free-guidance drop, injected instead of torch.rand."""
         if class_condition is None:
             idx = torch.full((batch_size, 1), self.n_classes, dtype=torch.long, device=device)
+        elif self.training:
+            # drop to the null class where u > p fails, u ~ U[0,1) per sample: one kernel
+            # (the device counter RNG; the reference's torch.rand draws can be injected)
+            y = class_condition.long().reshape(-1).contiguous()
+            idx = torch.empty_like(y)
+            u = self._class_rand
+            rnd = (torch.as_tensor(u).to(device=device, dtype=torch.float32).reshape(-1).contiguous()
+                   if u is not None else None)
+            seed = rng.seed_tensor(device) if rnd is None else None
+            off = rng.call_offset(self._site_l) if rnd is None else 0
+            call("tvq_class_index", ptr(y), y.numel(), float(self.p_unconditional), self.n_classes,
+                 ptr(seed), off, ptr(rnd), ptr(idx), stream_ptr())
+            idx = idx.reshape(class_condition.shape)
         else:
-            if self.training:
-                u = self._class_rand
-                if u is None:
-                    u = torch.rand(class_condition.shape, device=device)
-                ind = torch.as_tensor(u).to(device).reshape(class_condition.shape) > self.p_unconditional
-            else:
-                ind = torch.ones_like(class_condition, dtype=torch.bool)
-            idx = torch.where(ind, class_condition.long(), self.n_classes)
+            idx = class_condition.long()
         return embedding(idx, self.class_condition_emb.weight)  # (b 1 dim)
 
     def _tok(self, s, table, kind, site):
@@ -354,7 +360,7 @@ class BidirectionalTransformer(nn.Module):
         tok = self._tok(s_M_l, self.tok_emb_l.weight, "lf", self._site_l)
         cls_emb = self.class_embedding(class_condition, s_M_l.shape[0], device)
         n = tok.shape[1]
-        embed = torch.cat((cls_emb, tok + self.pos_emb.weight[:n, :]), dim=1)
+        embed = embed_assemble(cls_emb, tok, None, self.pos_emb.weight, n)  # cat(cls, tok + pos)
         embed = self.blocks(embed)
         embed = self._head(embed[:, 1:, :])
         return _TiedLogits.apply(embed, self.tok_emb_l.weight, self.bias, self.codebook_size)
@@ -365,10 +371,10 @@ class BidirectionalTransformer(nn.Module):
         tl = self._tok(s_M_l, self.tok_emb_l.weight, "lf", self._site_l)
         th = self._tok(s_M_h, self.tok_emb_h.weight, "hf", self._site_h)
         tl = self.projector(tl, upscale_size=th.shape[1])
-        tok = torch.cat((tl, th), dim=-1)
         cls_emb = self.class_embedding(class_condition, s_M_l.shape[0], device)
-        n = tok.shape[1]
-        embed = torch.cat((cls_emb, tok + self.pos_emb.weight[:n, :]), dim=1)
+        n = th.shape[1]
+        # cat(cls, cat(tl, th, -1) + pos) in one kernel
+        embed = embed_assemble(cls_emb, tl, th, self.pos_emb.weight, n)
         embed = self.blocks(embed)
         embed = self._head(embed[:, 1:, :])
         return _TiedLogits.apply(embed, self.tok_emb_h.weight, self.bias, self.codebook_size)

@@ -131,11 +131,7 @@ class VectorQuantize(nn.Module):
         """x: (B,N,D) -> (quantize, embed_ind (B,N), vq_loss dict, perplexity)."""
         cb = self._codebook
         device = x.device
-        vq_loss = {
-            "loss": torch.zeros(1, device=device).requires_grad_(self.training),
-            "commit_loss": 0.0,
-            "orthogonal_reg_loss": 0.0,
-        }
+        vq_loss = {"loss": None, "commit_loss": 0.0, "orthogonal_reg_loss": 0.0}
         if self.accept_image_fmap:
             height, width = x.shape[-2:]
             x = x.flatten(2).transpose(1, 2)
@@ -149,13 +145,18 @@ class VectorQuantize(nn.Module):
                 sync=cb._sync(), svq_temp=svq_temp)
             if self.commitment_weight > 0:
                 vq_loss["commit_loss"] = commit
-                vq_loss["loss"] = vq_loss["loss"] + commit * self.commitment_weight
+                # vq.py:364's [0.] + commit * w, shape (1,): at w == 1 that is commit itself
+                # (bit for bit), so no zeros / mul / add launches
+                vq_loss["loss"] = (commit.reshape(1) if self.commitment_weight == 1.0
+                                   else commit.reshape(1) * self.commitment_weight)
         else:
             with torch.no_grad():
                 quantize, embed_ind, _, perp, counts = vq_codebook_pass(
                     x, cb.embed, cb.cluster_size, cb.embed_avg, straight_through=False,
                     ema=False, decay=cb.decay, eps=cb.eps, svq_temp=svq_temp)
             cb.counts = counts
+        if vq_loss["loss"] is None:
+            vq_loss["loss"] = torch.zeros(1, device=device).requires_grad_(self.training)
         cb.perplexity = perp.detach()
         if not self.channel_last and not self.accept_image_fmap:
             quantize = quantize.transpose(1, 2)

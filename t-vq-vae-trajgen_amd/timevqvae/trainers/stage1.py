@@ -82,6 +82,14 @@ class Stage1(nn.Module):
         rec = None if return_x_rec else loss_fn(s[tgt], xhat)
         return xhat, rec, vq_loss, perplexity
 
+    def _ones(self, t):
+        """A cached ones tensor of t's shape (made outside graph capture, reused)."""
+        cache = self.__dict__.setdefault("_ones_cache", {})
+        key = (tuple(t.shape), t.device)
+        if key not in cache:
+            cache[key] = torch.ones(t.shape, device=t.device, dtype=t.dtype)
+        return cache[key]
+
     @staticmethod
     def _assemble(parts):
         recons_loss = {"LF.time": parts["LF"][1], "HF.time": parts["HF"][1]}
@@ -103,7 +111,10 @@ class Stage1(nn.Module):
                 br.inputs(s)
                 part = self._band(band, s)
                 with wgrad_deferred():  # weight-gradient split sums batched at the band's end
-                    (part[1] + part[2]["loss"]).sum().backward()
+                    # d(recons + vq_loss).sum() = 1 for both roots: backward from the two
+                    # roots with cached ones (no add / sum / ones_like launches)
+                    torch.autograd.backward((part[1], part[2]["loss"]),
+                                            (self._ones(part[1]), self._ones(part[2]["loss"])))
                 parts[band] = part
                 br.outputs(part)
         if self._sched is not None:
