@@ -95,6 +95,7 @@ class JointTrainer:
                     if b.is_floating_point():
                         dist.broadcast(b, 0)
         self.device = device
+        self._one = torch.ones((), device=device)
         self.graph = None
         self._pending = []
         from timevqvae.hip.conv import PackCache
@@ -127,7 +128,7 @@ class JointTrainer:
                 hist1 = self.s1.forward_backward(batch, 0) if only != "stage2" else None
             if only != "stage1":
                 out2 = self.s2.training_step(batch, 0)
-                out2["loss"].backward()
+                out2["loss"].backward(self._one)  # cached ones: no fill launch per step
             else:
                 out2 = {"loss": torch.zeros(())}
         return (hist1() if hist1 else {"loss": torch.zeros(())}), out2, pend

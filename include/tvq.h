@@ -359,6 +359,16 @@ int tvq_embed_assemble_bwd(const float* dout, int64_t B, int64_t n, int64_t D1, 
  * u_b > p else null_id; u_b = rnd[b] (injected) or the device counter RNG at (seed, offset). */
 int tvq_class_index(const int64_t* y, int64_t B, float p, int64_t null_id, const int64_t* seed_ptr,
                     uint64_t offset, const float* rnd, int64_t* idx, tvq_stream_t stream);
+/* Upscale's layout change fused into the nearest upsample (bidirectional_transformer.py:
+ * 25-27): x (B, Lin, D) -> y (B, D, Lout), and its backward dy (B, D, Lout) -> dx (B, Lin, D). */
+int tvq_upsample_nearest_t(const float* x, int64_t B, int64_t Lin, int64_t D, int64_t Lout,
+                           float* y, tvq_stream_t stream);
+int tvq_upsample_nearest_t_bwd(const float* dy, int64_t B, int64_t Lin, int64_t D, int64_t Lout,
+                               float* dx, tvq_stream_t stream);
+/* out[j*ldo + d] (+)= sum_b in[b*sb + j*sj + d] (j < n, d < D; b in order): batch sums of
+ * per-position tables, e.g. the tied-logits bias gradient (bidirectional_transformer.py:187). */
+int tvq_batch_colsum(const float* in, int64_t B, int64_t sb, int64_t n, int64_t sj, int64_t D,
+                     float* out, int64_t ldo, int64_t accumulate, tvq_stream_t stream);
 /* y[i] = x[i] * s[0] (s a device scalar; the gradient of a layer-dropout-gated branch). */
 int tvq_scale_by(const float* x, int64_t n, const float* s, float* y, tvq_stream_t stream);
 int tvq_layernorm_fwd(const float* x, int64_t M, int64_t D, const float* gamma, const float* beta,

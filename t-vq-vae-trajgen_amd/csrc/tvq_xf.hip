@@ -408,19 +408,6 @@ __global__ void embed_assemble_split_kernel(const float* __restrict__ dout, int 
   }
 }
 
-// dpos[j, d] (+)= sum_b dout[b, 1 + j, d], b in order (one thread per (j, d))
-__global__ void embed_pos_grad_kernel(const float* __restrict__ dout, int B, int n, int Dt,
-                                      float* __restrict__ dpos, int accumulate) {
-  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (e >= (int64_t)n * Dt) return;
-  const int64_t bs = (int64_t)(n + 1) * Dt;
-  const float* p = dout + Dt + e;
-  float s = 0.f;
-#pragma unroll 8
-  for (int b = 0; b < B; ++b) s += p[b * bs];
-  dpos[e] = accumulate ? dpos[e] + s : s;
-}
-
 // bidirectional_transformer.py:124-150 class conditioning in training: idx[b] = y[b] where
 // u_b > p_unconditional, else the null class; u_b injected (tests) or drawn from the
 // device counter RNG
@@ -431,6 +418,62 @@ __global__ void class_index_kernel(const int64_t* __restrict__ y, int B, float p
   if (b >= B) return;
   const float u = rnd ? rnd[b] : uniform01(mix_seed(seed_ptr, offset), (uint64_t)b);
   idx[b] = u > p ? y[b] : null_id;
+}
+
+// Upscale's transpose + nearest upsample in one pass: x (B, Lin, D) (the token layout)
+// -> y (B, D, Lout); backward dy (B, D, Lout) -> dx (B, Lin, D)
+__global__ void upsample_nearest_t_kernel(const float* __restrict__ x, int B, int Lin, int D,
+                                          int Lout, float scale, float* __restrict__ y) {
+  const int64_t tot = (int64_t)B * D * Lout;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e % Lout);
+    const int64_t r = e / Lout;
+    const int d = (int)(r % D);
+    const int b = (int)(r / D);
+    int src = (int)floorf((float)j * scale);
+    if (src > Lin - 1) src = Lin - 1;
+    y[e] = x[((int64_t)b * Lin + src) * D + d];
+  }
+}
+
+__global__ void upsample_nearest_t_bwd_kernel(const float* __restrict__ dy, int B, int Lin, int D,
+                                              int Lout, float scale, float* __restrict__ dx) {
+  const int64_t tot = (int64_t)B * Lin * D;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(e % D);
+    const int64_t r = e / D;
+    const int i = (int)(r % Lin);
+    const int b = (int)(r / Lin);
+    const float* row = dy + ((int64_t)b * D + d) * Lout;
+    float s = 0.f;
+    int j0 = (int)floorf((float)i / scale) - 2;  // outputs j with floor(j*scale) == i
+    if (j0 < 0) j0 = 0;
+    for (int j = j0; j < Lout; ++j) {
+      int src = (int)floorf((float)j * scale);
+      if (src > Lin - 1) src = Lin - 1;
+      if (src > i) break;
+      if (src == i) s += row[j];
+    }
+    dx[e] = s;
+  }
+}
+
+// out[j*ldo + d] (+)= sum_b in[b*sb + j*sj + d], b in order (one thread per (j, d)): batch
+// sums of position tables (the tied-logits bias (n, K+1), the position embedding)
+__global__ void batch_colsum_kernel(const float* __restrict__ in, int B, int64_t sb, int n,
+                                    int64_t sj, int D, float* __restrict__ out, int64_t ldo,
+                                    int accumulate) {
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e >= (int64_t)n * D) return;
+  const int j = (int)(e / D), d = (int)(e - (int64_t)j * D);
+  const float* p = in + j * sj + d;
+  float s = 0.f;
+#pragma unroll 8
+  for (int b = 0; b < B; ++b) s += p[b * sb];
+  float* o = out + j * ldo + d;
+  *o = accumulate ? *o + s : s;
 }
 
 __global__ void scale_by_kernel(const float4* __restrict__ x, int64_t n4, const float* __restrict__ s,
@@ -474,9 +517,10 @@ extern "C" int tvq_embed_assemble_bwd(const float* dout, int64_t B, int64_t n, i
     hipLaunchKernelGGL(embed_assemble_split_kernel, dim3(grid_for(B * (n + 1) * (D1 + D2))),
                        dim3(256), 0, st, dout, (int)B, (int)n, dcls, a1, a2);
   if (dpos) {
-    const int64_t m = n * (D1 + D2);
-    hipLaunchKernelGGL(embed_pos_grad_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st,
-                       dout, (int)B, (int)n, (int)(D1 + D2), dpos, (int)accumulate);
+    const int64_t Dt = D1 + D2;
+    hipLaunchKernelGGL(batch_colsum_kernel, dim3((unsigned)((n * Dt + 255) / 256)), dim3(256), 0, st,
+                       dout + Dt, (int)B, (n + 1) * Dt, (int)n, Dt, (int)Dt, dpos, Dt,
+                       (int)accumulate);
   }
   return launch_status("tvq_embed_assemble_bwd");
 }
@@ -488,6 +532,35 @@ extern "C" int tvq_class_index(const int64_t* y, int64_t B, float p, int64_t nul
   hipLaunchKernelGGL(class_index_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, y, (int)B, p, null_id, seed_ptr, offset, rnd, idx);
   return launch_status("tvq_class_index");
+}
+
+extern "C" int tvq_upsample_nearest_t(const float* x, int64_t B, int64_t Lin, int64_t D,
+                                      int64_t Lout, float* y, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && y && B > 0 && Lin > 0 && D > 0 && Lout > 0, "tvq_upsample_nearest_t: bad args");
+  hipLaunchKernelGGL(upsample_nearest_t_kernel, dim3(grid_for(B * D * Lout)), dim3(256), 0,
+                     (hipStream_t)stream, x, (int)B, (int)Lin, (int)D, (int)Lout,
+                     (float)Lin / (float)Lout, y);
+  return launch_status("tvq_upsample_nearest_t");
+}
+
+extern "C" int tvq_upsample_nearest_t_bwd(const float* dy, int64_t B, int64_t Lin, int64_t D,
+                                          int64_t Lout, float* dx, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(dy && dx && B > 0 && Lin > 0 && D > 0 && Lout > 0,
+                "tvq_upsample_nearest_t_bwd: bad args");
+  hipLaunchKernelGGL(upsample_nearest_t_bwd_kernel, dim3(grid_for(B * Lin * D)), dim3(256), 0,
+                     (hipStream_t)stream, dy, (int)B, (int)Lin, (int)D, (int)Lout,
+                     (float)Lin / (float)Lout, dx);
+  return launch_status("tvq_upsample_nearest_t_bwd");
+}
+
+extern "C" int tvq_batch_colsum(const float* in, int64_t B, int64_t sb, int64_t n, int64_t sj,
+                                int64_t D, float* out, int64_t ldo, int64_t accumulate,
+                                tvq_stream_t stream) {
+  TVQ_CHECK_ARG(in && out && B > 0 && n > 0 && D > 0, "tvq_batch_colsum: bad arguments");
+  hipLaunchKernelGGL(batch_colsum_kernel, dim3((unsigned)((n * D + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, in, (int)B, sb, (int)n, sj, (int)D, out, ldo,
+                     (int)accumulate);
+  return launch_status("tvq_batch_colsum");
 }
 
 extern "C" int tvq_scale_by(const float* x, int64_t n, const float* s, float* y,

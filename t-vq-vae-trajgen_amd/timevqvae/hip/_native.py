@@ -97,6 +97,9 @@ sig("tvq_rmsnorm_fwd", P, I64, I64, P, F32, P, P, P)
 sig("tvq_norm_bwd_workspace", I64, I64, restype=I64)
 sig("tvq_rmsnorm_bwd", P, P, I64, I64, P, F32, P, P, P, P, I64, P, P)
 sig("tvq_scale_by", P, I64, P, P, P)
+sig("tvq_upsample_nearest_t", P, I64, I64, I64, I64, P, P)
+sig("tvq_upsample_nearest_t_bwd", P, I64, I64, I64, I64, P, P)
+sig("tvq_batch_colsum", P, I64, I64, I64, I64, I64, P, I64, I64, P)
 sig("tvq_class_index", P, I64, F32, I64, P, U64, P, P, P)
 sig("tvq_embed_assemble", P, P, I64, I64, I64, I64, P, I64, I64, I64, I64, P, I64, I64, P, P)
 sig("tvq_embed_assemble_bwd", P, I64, I64, I64, I64, P, P, I64, I64, I64, P, I64, I64, I64, P, I64, P)

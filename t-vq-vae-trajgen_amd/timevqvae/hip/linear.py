@@ -88,7 +88,40 @@ class _Linear(torch.autograd.Function):
         return dx, dw, db, dres, None
 
 
+class _LinearSelfRes(torch.autograd.Function):
+    """y = x + x W^T + b (vq_vae.py:263 `out + self.linear(out)`, W square): x has one
+    autograd consumer and dx = dy W + dy comes out of one GEMM (residual epilogue)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        shp = x.shape
+        K = shp[-1]
+        x2 = x.reshape(-1, K).contiguous()
+        M = x2.shape[0]
+        y = gemm(x2, K, 1, w.contiguous(), 1, K, M, K, K, bias=b, R=x2, ldr=K)
+        ctx.save_for_backward(x2, w)
+        ctx.params = (w, b)
+        ctx.shp = shp
+        return y.reshape(shp)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w = ctx.saved_tensors
+        M, K = x2.shape
+        g = gy.reshape(M, K).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(g, K, 1, w.contiguous(), K, 1, M, K, K, R=g, ldr=K).reshape(ctx.shp)
+        if ctx.needs_input_grad[1]:
+            dw = weight_grad(g, x2, ctx.params[0], M, K, K)
+        if ctx.params[1] is not None and ctx.needs_input_grad[2]:
+            db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
+        return dx, dw, db
+
+
 def linear(x, weight, bias=None, residual=None, gate=None):
     """residual + gate * (x @ weight^T + bias) over the last dim (nn.Linear; vq_vae.py:255,263;
     `gate`: optional one-element device tensor, the x-transformers layer-dropout keep flag)."""
+    if residual is x and gate is None and weight.shape[0] == weight.shape[1]:
+        return _LinearSelfRes.apply(x, weight, bias)
     return _Linear.apply(x, weight, bias, residual, gate)

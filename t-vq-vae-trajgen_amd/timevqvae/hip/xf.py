@@ -452,6 +452,39 @@ def upsample_nearest(x, size):
     return _UpNearest.apply(x, int(size))
 
 
+class _UpNearestT(torch.autograd.Function):
+    """(b, n, d) -> transpose -> nearest upsample to m -> (b, d, m), one pass each way."""
+
+    @staticmethod
+    def forward(ctx, x, Lout):
+        x = x.contiguous()
+        B, Lin, D = x.shape
+        y = torch.empty((B, D, Lout), device=x.device)
+        call("tvq_upsample_nearest_t", ptr(x), B, Lin, D, Lout, ptr(y), stream_ptr())
+        ctx.cfg = (B, Lin, D, Lout)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        B, Lin, D, Lout = ctx.cfg
+        g = gy.contiguous()
+        dx = torch.empty((B, Lin, D), device=g.device)
+        call("tvq_upsample_nearest_t_bwd", ptr(g), B, Lin, D, Lout, ptr(dx), stream_ptr())
+        return dx, None
+
+
+def upsample_nearest_t(x, size):
+    """F.interpolate(x.transpose(1, 2), size, mode='nearest') for x (b, n, d) -> (b, d, size)."""
+    return _UpNearestT.apply(x, int(size))
+
+
+def batch_colsum(x, out, ldo, accumulate):
+    """out[j*ldo + d] (+)= sum_b x[b, j, d] for x (B, n, D) contiguous (tvq_batch_colsum)."""
+    B, n, D = x.shape
+    call("tvq_batch_colsum", ptr(x), B, n * D, n, D, D, ptr(out), ldo, int(bool(accumulate)),
+         stream_ptr())
+
+
 class _GELU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):

@@ -25,10 +25,10 @@ import torch.nn as nn
 
 from ..hip import rng, streams
 from ..hip.conv import conv2d
-from ..hip.linear import _bias_grad_rows, gemm, linear
+from ..hip.linear import gemm, linear
 from ..hip.norm import bn_snake
-from ..hip.xf import (embed_assemble, embedding, gelu, layer_norm, linear_act, qkv_attention,
-                      rmsnorm, rmsnorm_res, upsample_nearest)
+from ..hip.xf import (batch_colsum, embed_assemble, embedding, gelu, layer_norm, linear_act,
+                      qkv_attention, rmsnorm, rmsnorm_res, upsample_nearest_t)
 from ..hip._native import call, grad_sink, ptr, stream_ptr
 
 
@@ -248,15 +248,14 @@ class _TiedLogits(torch.autograd.Function):
                 dW = torch.zeros_like(W)
                 gemm(g2, 1, K, h2, D, 1, K, D, M, out=dW, ldc=D)
         if ctx.needs_input_grad[2]:
+            # sum over the batch into the (n, K+1) table's first K columns, in order
             sink = grad_sink(ctx.bias)
             if sink is not None:
                 with streams.offload(g2):
-                    s = _bias_grad_rows(g2.reshape(B, n * K)).reshape(n, K)  # sum over the batch
-                    sink[:, :K] += s
+                    batch_colsum(g2.reshape(B, n, K), sink, bshape[1], True)
             else:
-                s = _bias_grad_rows(g2.reshape(B, n * K)).reshape(n, K)
                 dbias = torch.zeros(bshape, device=g.device)
-                dbias[:, :K] = s
+                batch_colsum(g2.reshape(B, n, K), dbias, bshape[1], False)
         return dh, dW, dbias, None
 
 
@@ -274,8 +273,7 @@ class Upscale(nn.Module):
 
     def forward(self, x, upscale_size: int):
         """x: (b n d) -> (b m d)."""
-        x = x.transpose(1, 2).contiguous()               # b d n
-        x = upsample_nearest(x, upscale_size)            # b d m
+        x = upsample_nearest_t(x, upscale_size)          # b n d -> b d m, one kernel
         c = self.conv
         x = gelu(conv2d(x, c[0].weight, c[0].bias))
         x = bn_snake(x, c[2], None)

@@ -92,6 +92,19 @@ class EuclideanCodebook(nn.Module):
         return q.reshape(shape), idx.reshape(shape[:-1])
 
 
+_ZEROS = {}
+
+
+def _eval_zero(device):
+    key = torch.device(device)
+    z = _ZEROS.get(key)
+    if z is None:
+        z = torch.zeros(1, device=key)
+        if not (key.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            _ZEROS[key] = z  # not from a graph's private pool (freed with the graph)
+    return z
+
+
 class VectorQuantize(nn.Module):
     """vq.py:255-407 (heads=1, codebook_dim=dim, channel_last, no orthogonal reg)."""
 
@@ -156,7 +169,10 @@ class VectorQuantize(nn.Module):
                     ema=False, decay=cb.decay, eps=cb.eps, svq_temp=svq_temp)
             cb.counts = counts
         if vq_loss["loss"] is None:
-            vq_loss["loss"] = torch.zeros(1, device=device).requires_grad_(self.training)
+            if self.training:
+                vq_loss["loss"] = torch.zeros(1, device=device).requires_grad_(True)
+            else:  # eval: a shared constant zero (no fill launch per call; never written)
+                vq_loss["loss"] = _eval_zero(device)
         cb.perplexity = perp.detach()
         if not self.channel_last and not self.accept_image_fmap:
             quantize = quantize.transpose(1, 2)
