@@ -735,14 +735,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
       rb[j] = v;
     }
   };
-  // rows of 16 positions, columns XOR-swizzled by (row & 12) as in gemm_kernel: the row
-  // pitches are 16 / 48 mod 64 banks, so unswizzled a wave's stores land on 16 banks.
-  // Layout only (same k order, same results).
+  // rows of 16 positions, columns XOR-swizzled by (row & 14) as in gemm_kernel: the row
+  // pitches are 16 mod 32 store banks, so unswizzled a half-wave's stores land on 16
+  // banks (and with (row & 12) still 2-way).  Layout only (same k order, same results).
   auto store_tile = [&]() {
 #pragma unroll
-    for (int j = 0; j < A_PER; ++j) As[kk_t * SA + ((a_nbase + j * 16) ^ (kk_t & 12))] = ra[j];
+    for (int j = 0; j < A_PER; ++j) As[kk_t * SA + ((a_nbase + j * 16) ^ (kk_t & 14))] = ra[j];
 #pragma unroll
-    for (int j = 0; j < B_PER; ++j) Bs[kk_t * SB + ((b_kbase + j * 16) ^ (kk_t & 12))] = rb[j];
+    for (int j = 0; j < B_PER; ++j) Bs[kk_t * SB + ((b_kbase + j * 16) ^ (kk_t & 14))] = rb[j];
   };
 
   floatx4 acc[FN][FK];
@@ -761,7 +761,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 4) {
         float af[FN], bf[FK];
-        const int swz = r16 ^ (kk & 12);
+        const int swz = r16 ^ ((kk & 12) | (g4 & 2));  // sw(kk + g4)
 #pragma unroll
         for (int i = 0; i < FN; ++i) af[i] = As[(kk + g4) * SA + (wn * FN + i) * 16 + swz];
 #pragma unroll

@@ -70,15 +70,16 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       rb[j] = (n < g.N && k < ke) ? g.B[(int64_t)k * g.sbk + (int64_t)n * g.sbn] : 0.f;
     }
   };
-  // Panels are stored [k][m] / [k][n] with m (n) XOR-swizzled by sw(k) = 4 ((k >> 2) & 3):
-  // the row pitches are 16 (or 48) mod 64 banks, so without it a wave's stores of 16 k
-  // rows hit 4 banks; with it both the stores and the fragment reads are conflict-free.
-  // Layout only: the MFMA k order, and so every result, is unchanged.
+  // Panels are stored [k][m] / [k][n] with m (n) XOR-swizzled by sw(k) = k & 14: the row
+  // pitches are 16 mod 32 banks (ds_write banks are (a/4) mod 32), so a half-wave's stores
+  // of 16 k rows x 2 columns land on 32 distinct banks, and each fragment read (rows kk,
+  // kk+1 per half-wave, 16 consecutive columns each) is conflict-free too.  Layout only:
+  // the MFMA k order, and so every result, is unchanged.
   auto store = [&]() {
 #pragma unroll
-    for (int j = 0; j < A_PER; ++j) As[a_k[j] * SA + (a_m[j] ^ ((a_k[j] & 12)))] = ra[j];
+    for (int j = 0; j < A_PER; ++j) As[a_k[j] * SA + (a_m[j] ^ ((a_k[j] & 14)))] = ra[j];
 #pragma unroll
-    for (int j = 0; j < B_PER; ++j) Bs[b_k[j] * SB + (b_n[j] ^ ((b_k[j] & 12)))] = rb[j];
+    for (int j = 0; j < B_PER; ++j) Bs[b_k[j] * SB + (b_n[j] ^ ((b_k[j] & 14)))] = rb[j];
   };
   floatx4 acc[FM][FN];
 #pragma unroll
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 4) {
         float af[FM], bf[FN];
-        const int swz = r16 ^ (kk & 12);  // sw(kk + g4) = kk & 12 (g4 < 4, kk % 4 == 0)
+        const int swz = r16 ^ ((kk & 12) | (g4 & 2));  // sw(kk + g4) (g4 < 4, kk % 4 == 0)
 #pragma unroll
         for (int i = 0; i < FM; ++i) af[i] = As[(kk + g4) * SA + (wm * FM + i) * 16 + swz];
 #pragma unroll
