@@ -1415,6 +1415,45 @@ static void whalo_blocking(int64_t N, int64_t C, int KK, int* FN, int* CB) {
   *CB = cb;
 }
 
+// Halo-plane stride of conv_wgrad_halo_kernel's image (>= hw): the B-operand read of a
+// half-wave (lanes j = 0..15 over 16 consecutive reduction columns (c, tap), kq = 0..1 over
+// 2 positions) is Hs[c*PS + toff(tap) + kq*SW + base]; its 32 addresses should fall on 32
+// distinct (a/4) mod 32 banks.  The stride residue mod 32 that minimises the extra bank
+// cycles over the kernel's column tiles is chosen on the host (layout only: same sums).
+static int whalo_plane_stride(int hw, int KK, int KW, int WP, int SW, int CB) {
+  int best = hw + ((16 - hw % 32) + 32) % 32, best_cost = 1 << 30;
+  const int ncols = CB * KK;
+  for (int pad = 0; pad < 32; ++pad) {
+    const int PS = hw + pad;
+    int cost = 0;
+    for (int t0 = 0; t0 < ncols; t0 += 16) {
+      int hits[32][2];  // per bank: distinct addresses seen (up to 2 tracked) and count
+      int cnt[32] = {0};
+      for (int l = 0; l < 32; ++l) {
+        const int j = l & 15, kq = l >> 4;
+        const int kl = t0 + j;
+        if (kl >= ncols) continue;
+        const int c = kl / KK, tap = kl - c * KK;
+        const int a = c * PS + (tap / KW) * WP + (tap % KW) + kq * SW;
+        const int bank = ((a % 32) + 32) % 32;
+        bool dup = false;
+        for (int q = 0; q < cnt[bank] && q < 2; ++q) dup |= hits[bank][q] == a;
+        if (dup) continue;
+        if (cnt[bank] < 2) hits[bank][cnt[bank]] = a;
+        ++cnt[bank];
+      }
+      int worst = 0;
+      for (int b = 0; b < 32; ++b) worst = cnt[b] > worst ? cnt[b] : worst;
+      cost += worst > 1 ? worst - 1 : 0;
+    }
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = PS;
+    }
+  }
+  return best;
+}
+
 static bool whalo_plan(int B, int C, int Hin, int Win, int N, int Hout, int Wo, int KH, int KW,
                        int SW, int oh, int ow, int kcols, WHaloPlan* pl) {
   if (Wo % 4 != 0) return false;
@@ -1428,7 +1467,6 @@ static bool whalo_plan(int B, int C, int Hin, int Win, int N, int Hout, int Wo, 
   g.HP = Hout + KH - 1;
   g.WP = (Wo - 1) * SW + KW;
   const int hw = g.HP * g.WP;
-  g.PS = hw + ((16 - hw % 32) + 32) % 32;
   g.P = Hout * Wo;
   g.GST = g.P + ((2 - g.P % 32) + 32) % 32;
   if (g.WP < 2 || g.P >= (1 << 16)) return false;
@@ -1438,6 +1476,7 @@ static bool whalo_plan(int B, int C, int Hin, int Win, int N, int Hout, int Wo, 
   const int KK = KH * KW;
   int FN, CB;
   whalo_blocking(N, C, KK, &FN, &CB);
+  g.PS = whalo_plane_stride(hw, KK, KW, g.WP, SW, CB);
   g.CB = CB;
   g.Kred = C * KK;
   g.kcols = kcols;
