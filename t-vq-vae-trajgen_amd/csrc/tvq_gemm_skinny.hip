@@ -34,7 +34,11 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g) {
   constexpr int T4 = HK / 4;
   constexpr int BN = 32 * WN;
   constexpr int TM = 32 * WM;
-  extern __shared__ float Ws[];  // [chunk][wn][t4][lane][4]: B fragments, ds_read_b128 order
+  // [chunk][wn][t4][lane][4]: B fragments, ds_read_b128 order; declared float4 so the
+  // staging stores are ds_write_b128 (as float, hipcc split them into 4-way-conflicted
+  // ds_write2_b32 pairs at a 16-B lane stride)
+  extern __shared__ float4 Wsv[];
+  float* Ws = reinterpret_cast<float*>(Wsv);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r32 = lane & 31, h = lane >> 5;
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
@@ -60,7 +64,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g) {
           v.w = p[3 * g.sbk];
         }
       }
-      *(float4*)(Ws + 4 * e) = v;
+      Wsv[e] = v;
     }
   }
   __syncthreads();
