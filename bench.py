@@ -300,7 +300,7 @@ def _graph_time_us(fns, reps):
 
 
 def dominant_leg(device):
-    """The step's dominant kernel (profiles/r02c_step_kernel_stats.csv, first row):
+    """The step's dominant kernel (profiles/r02d_step_kernel_stats.csv, first row):
     gemm_kt_kernel, the weight-gradient GEMM dW (+)= dY^T X of every transformer Linear
     (direct-operand 32x32x2 fp32 MFMA, K = tokens split over 4 waves x `splits` blocks) with
     its slab sum gemm_direct_reduce_kernel (one op = these 2 launches).  Timed at its

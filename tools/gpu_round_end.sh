@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-end evidence: every -m gpu test, smoke(), the full bench line (all legs), a step-only
+# rocprofv3 kernel table, and the dominant-kernel roofline evidence (PMC traffic).
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 600 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+grep "smoke ok" gpurun_out/smoke.log
+timeout -k 10 600 python bench.py > gpurun_out/bench_full.log 2>&1 || { tail -20 gpurun_out/bench_full.log; exit 1; }
+tail -1 gpurun_out/bench_full.log > gpurun_out/bench_full.json
+bash tools/gpu_step_prof.sh > gpurun_out/step_prof_out.txt 2>&1 || { tail -20 gpurun_out/step_prof_out.txt; exit 1; }
+grep "launches/step" gpurun_out/step_prof_out.txt
+LEG=dominant bash tools/gpu_roofline.sh > gpurun_out/roof_out.txt 2>&1 || { tail -20 gpurun_out/roof_out.txt; exit 1; }
+echo round-end-done
