@@ -26,8 +26,22 @@ __device__ __forceinline__ float rr_colsum(const float* __restrict__ in, int64_t
                                            int c, int g) {
   float s = 0.f;
   if (j < N) {
-#pragma unroll 4
-    for (int64_t p = p0 + g; p < p1; p += RR_GROUPS) s += WT ? ld_wt(in + p * ld + j) : in[p * ld + j];
+    // 16 rows' loads in flight per thread (the adds stay in row order): the slabs here are
+    // 64-256 rows tall, and 4 in flight left the sum bound by load latency (42 us for the
+    // band-end batch of the fused ResBlocks' 256-row weight-gradient slabs, now 22 us).
+    // (32 in flight, or a masked 16-row tail, measured slower.)
+    int64_t p = p0 + g;
+    for (; p + 15 * RR_GROUPS < p1; p += 16 * RR_GROUPS) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float* a = in + (p + u * RR_GROUPS) * ld + j;
+        v[u] = WT ? ld_wt(a) : *a;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    for (; p < p1; p += RR_GROUPS) s += WT ? ld_wt(in + p * ld + j) : in[p * ld + j];
   }
   sh[g][c] = s;
   __syncthreads();
