@@ -117,7 +117,7 @@ class JointTrainer:
         streams); every stream is joined when the region ends.
         Returns (out1, out2, deferred codebook updates)."""
         import contextlib
-        from timevqvae.hip import streams
+        from timevqvae.hip import streams, wgrad
         from timevqvae.hip.vq import deferred_codebook_updates
         self.opt1.zero_grad()
         self.opt2.zero_grad()
@@ -128,7 +128,8 @@ class JointTrainer:
                 hist1 = self.s1.forward_backward(batch, 0) if only != "stage2" else None
             if only != "stage1":
                 out2 = self.s2.training_step(batch, 0)
-                out2["loss"].backward(self._one)  # cached ones: no fill launch per step
+                with wgrad.grouped():  # Linear weight gradients: one grouped launch per stream
+                    out2["loss"].backward(self._one)  # cached ones: no fill launch per step
             else:
                 out2 = {"loss": torch.zeros(())}
         return (hist1() if hist1 else {"loss": torch.zeros(())}), out2, pend
@@ -300,31 +301,38 @@ def _graph_time_us(fns, reps):
 
 
 def dominant_leg(device):
-    """The step's dominant kernel (profiles/r02d_step_kernel_stats.csv, first row):
-    gemm_kt_kernel, the weight-gradient GEMM dW (+)= dY^T X of every transformer Linear
-    (direct-operand 32x32x2 fp32 MFMA, K = tokens split over 4 waves x `splits` blocks) with
-    its slab sum gemm_direct_reduce_kernel (one op = these 2 launches).  Timed at its
-    commonest step shape, the LF prior's Linear(128 -> 128) over 6400 tokens (B=256 x 25),
-    accumulating into a flat-gradient view as the step does: 2*6400*128*128 = 209.7 MFLOP
-    and 4*(2*6400*128 + 2*128*128) = 6.68 MB algorithmic per op (AI 31 FLOP/B: fp32 MFMA
-    bound).  50 graph-replayed ops timed with HIP events on their stream."""
-    from timevqvae.hip.linear import gemm
-    M, N, K = 6400, 128, 128  # tokens, out features, in features
-    g = torch.randn(M, N, device=device)
-    x = torch.randn(M, K, device=device)
-    dw = torch.zeros(N, K, device=device)
-    fn = (lambda: gemm(g, 1, N, x, K, 1, N, K, M, out=dw, ldc=K, accumulate=True))
+    """The step's dominant kernel (profiles/r02e_step_kernel_stats.csv): wgrad_group_kernel,
+    the grouped weight gradient dW_i += dY_i^T X_i of every Linear of a prior, issued once
+    at the end of its backward (timevqvae.hip.wgrad; 32x32x2 fp32 MFMA, 64x64 tiles, K =
+    tokens split over 4 waves x S blocks) with its ordered slab sum wgrad_group_reduce_kernel
+    (one op = these 2 launches).  Timed on the LF prior's set, accumulating into one flat
+    gradient buffer as the step does: 4 layers x [q|k|v 384x128, out, ff1, ff2 128x128]
+    over 6400 tokens (B=256 x 25) = 5.03 GFLOP and 4 * sum(K (M + N) + 2 M N) = 134.6 MB
+    algorithmic per op (AI 37 FLOP/B: fp32 MFMA bound).  20 graph-replayed ops timed with
+    HIP events on their stream."""
+    from timevqvae.hip import wgrad
+    K = 6400
+    shapes = [(384, 128), (128, 128), (128, 128), (128, 128)] * 4
+    flat = torch.zeros(sum(m * n for m, n in shapes), device=device)
+    recs, off = [], 0
+    for M, N in shapes:
+        dy = torch.randn(K, M, device=device)
+        x = torch.randn(K, N, device=device)
+        recs.append((dy, M, x, N, flat[off:off + M * N], N, M, N, K))
+        off += M * N
+    fn = (lambda: wgrad.launch(recs))
     with torch.no_grad():
-        us = _graph_time_us([fn], 50)
-    flops = 2.0 * M * N * K
-    byts = 4.0 * (M * N + M * K + 2 * N * K)
+        us = _graph_time_us([fn], 20)
+    flops = sum(2.0 * K * M * N for M, N in shapes)
+    byts = sum(4.0 * (K * (M + N) + 2 * M * N) for M, N in shapes)
     tf = flops / (us * 1e-6) / 1e12
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r02_dominant_traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "r02e_dominant_traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath))["traffic_bytes"]
-    return {"bound": "mfma", "kernel": "gemm_kt_kernel + gemm_direct_reduce_kernel (weight-gradient "
-                                       "GEMM dW += dY^T X, 128x128 over 6400 tokens, fp32 MFMA)",
+    return {"bound": "mfma", "kernel": "wgrad_group_kernel + wgrad_group_reduce_kernel (grouped "
+                                       "weight gradients of the LF prior's 16 Linears, "
+                                       "dW_i += dY_i^T X_i over 6400 tokens, fp32 MFMA)",
             "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),

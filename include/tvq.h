@@ -296,6 +296,17 @@ int tvq_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t s
              float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha,
              const float* bias, const float* R, int64_t ldr, int64_t rmod, int64_t act, float* pre,
              int64_t accumulate, const float* gate, float* workspace, tvq_stream_t stream);
+/* Grouped weight gradients of n Linear layers (the dW part of nn.Linear's backward,
+ * issued together at the end of a backward instead of one tvq_gemm per layer):
+ *   dW_i[m*ldw_i + n] (+)= sum_k dY_i[k*ldy_i + m] X_i[k*ldx_i + n],
+ * m < M_i (out features), n < N_i (in features), k < K_i (tokens).  Host arrays of
+ * length n (device pointers in dY / X / dW).  Each sum has a fixed order (results are
+ * run-to-run bitwise identical).  Workspace: tvq_wgrad_group_workspace floats. */
+int64_t tvq_wgrad_group_workspace(int64_t n, const int64_t* M, const int64_t* N, const int64_t* K);
+int tvq_wgrad_group(int64_t n, const float* const* dY, const int64_t* ldy, const float* const* X,
+                    const int64_t* ldx, float* const* dW, const int64_t* ldw, const int64_t* M,
+                    const int64_t* N, const int64_t* K, int64_t accumulate, float* workspace,
+                    tvq_stream_t stream);
 
 /* ------------------------------------------------------ losses, optimizer
  * F.mse_loss (kind 0) / F.l1_loss (kind 1) means (stage1.py:129,133); backward

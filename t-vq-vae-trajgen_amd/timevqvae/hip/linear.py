@@ -1,7 +1,7 @@
 """Dense GEMM ops (nn.Linear over the last dim) on the HIP path."""
 import torch
 
-from . import streams
+from . import streams, wgrad
 from ._native import call, grad_sink, ptr, stream_ptr, value
 
 
@@ -37,6 +37,8 @@ def weight_grad(g, x2, w_param, M, N, K):
     """dW = g^T x (N x K): accumulated into the flat grad view when available."""
     sink = grad_sink(w_param)
     if sink is not None:  # into the flat gradient: off the critical path
+        if wgrad.defer(g, N, x2, K, sink, K, N, K, M):  # grouped at the backward's end
+            return None
         with streams.offload(g, x2):
             gemm(g, 1, N, x2, K, 1, N, K, M, out=sink, ldc=K, accumulate=True)
         return None

@@ -1,0 +1,87 @@
+"""Deferred, grouped weight gradients (tvq_wgrad_group).
+
+nn.Linear's backward is dX = dY W (needed at once: the backward chain continues through
+it) and dW = dY^T X (read by nothing until the optimizer step).  Inside a `grouped()`
+scope, `weight_grad` records dW (+)= dY^T X instead of launching it; at the scope's exit
+each stream's records go out as ONE grouped launch (+ one ordered slab sum) on the stream
+that produced them.  For the LF prior that is 16 weight gradients (5.03 GFLOP) in one
+launch that fills the chip, against 16 latency-bound split-K launch pairs.
+
+Records keep their dY / X tensors alive until the flush is enqueued on their stream
+(stream-ordered reuse afterwards, as for any tensor freed after its last kernel).  A
+record whose output overlaps one already pending on its stream flushes the pending ones
+first, so accumulations into one buffer keep their backward order.  The autograd engine
+runs CUDA backward nodes on its device thread; the scope is process-global and the
+issuing thread blocks in backward() meanwhile, so the records are complete at exit.
+"""
+import contextlib
+import ctypes
+import os
+
+import torch
+
+from ._native import call, ptr, value
+
+ENABLED = os.environ.get("TVQ_WGRAD_GROUP", "1") != "0"
+
+_pending = None  # stream -> list of records while a scope is active
+
+
+@contextlib.contextmanager
+def grouped():
+    """Defer weight gradients issued in the body; flush them per stream at exit."""
+    global _pending
+    if _pending is not None or not ENABLED:
+        yield
+        return
+    _pending = {}
+    try:
+        yield
+    finally:
+        pend, _pending = _pending, None
+        for st, recs in pend.items():
+            if recs:
+                with torch.cuda.stream(st):
+                    launch(recs)
+
+
+def launch(recs):
+    """dW (+)= dY^T X for each record (dy, ldy, x, ldx, dw, ldw, M, N, K, keep) in one
+    tvq_wgrad_group call on the current stream."""
+    n = len(recs)
+    dev = recs[0][0].device
+    I64s = ctypes.c_int64 * n
+    Ps = ctypes.c_void_p * n
+    M, N, K = I64s(*[r[6] for r in recs]), I64s(*[r[7] for r in recs]), I64s(*[r[8] for r in recs])
+    wsz = value("tvq_wgrad_group_workspace", n, ctypes.addressof(M), ctypes.addressof(N),
+                ctypes.addressof(K))
+    ws = torch.empty(wsz, device=dev, dtype=torch.float32) if wsz > 0 else None
+    dy, x, dw = Ps(*[ptr(r[0]) for r in recs]), Ps(*[ptr(r[2]) for r in recs]), Ps(*[ptr(r[4]) for r in recs])
+    ldy, ldx, ldw = I64s(*[r[1] for r in recs]), I64s(*[r[3] for r in recs]), I64s(*[r[5] for r in recs])
+    call("tvq_wgrad_group", n, ctypes.addressof(dy), ctypes.addressof(ldy), ctypes.addressof(x),
+         ctypes.addressof(ldx), ctypes.addressof(dw), ctypes.addressof(ldw), ctypes.addressof(M),
+         ctypes.addressof(N), ctypes.addressof(K), 1, ptr(ws),
+         torch.cuda.current_stream().cuda_stream)
+
+
+def _span(t, rows, ld, cols):
+    a = t.data_ptr()
+    return a, a + 4 * ((rows - 1) * ld + cols)
+
+
+def defer(dy, ldy, x, ldx, dw, ldw, M, N, K):
+    """Record dW[m*ldw + n] += sum_k dY[k*ldy + m] X[k*ldx + n] (m < M, n < N, k < K)
+    when a grouped() scope is active (returns True); else returns False and the caller
+    launches it.  The flat-gradient view `dw` must not be read or written by anything
+    else before the scope's exit (Linear weight gradients: read by the optimizer only)."""
+    if _pending is None:
+        return False
+    rec = (dy, ldy, x, ldx, dw, ldw, M, N, K)
+    st = torch.cuda.current_stream()
+    recs = _pending.setdefault(st, [])
+    lo, hi = _span(dw, M, ldw, N)
+    if any(lo < h and l < hi for l, h in (_span(r[4], r[6], r[5], r[7]) for r in recs)):
+        launch(recs)  # same output: keep the accumulation order
+        recs.clear()
+    recs.append(rec)
+    return True

@@ -4,7 +4,7 @@ import math
 
 import torch
 
-from . import rng, streams
+from . import rng, streams, wgrad
 from ._native import call, grad_sink, ptr, stream_ptr, value
 from .linear import _bias_grad_rows, gemm, weight_grad
 
@@ -280,8 +280,9 @@ class _QKVAttention(torch.autograd.Function):
             sinks = [grad_sink(p) for p in ctx.params]
             sink = _stacked(sinks, (L, D)) if all(s is not None for s in sinks) else None
             if sink is not None:  # into the flat gradient (stacked view)
-                with streams.offload(dqkv, x2):
-                    gemm(dqkv, 1, L, x2, D, 1, L, D, M, out=sink, ldc=D, accumulate=True)
+                if not wgrad.defer(dqkv, L, x2, D, sink, D, L, D, M):  # else grouped later
+                    with streams.offload(dqkv, x2):
+                        gemm(dqkv, 1, L, x2, D, 1, L, D, M, out=sink, ldc=D, accumulate=True)
             else:
                 dW = gemm(dqkv, 1, L, x2, D, 1, L, D, M)
                 dws = [dW[i * HD:(i + 1) * HD] for i in range(3)]

@@ -10,7 +10,7 @@ One fused STFT kernel produces both encoder inputs and both targets
 import torch
 import torch.nn as nn
 
-from ..hip import streams
+from ..hip import streams, wgrad
 from ..hip.conv import wgrad_deferred
 from ..hip.loss import l1_loss, mse_loss
 from ..hip.optim import FusedAdamW
@@ -110,7 +110,9 @@ class Stage1(nn.Module):
             with streams.branch(x.device, "s1" + band.lower()) as br:
                 br.inputs(s)
                 part = self._band(band, s)
-                with wgrad_deferred():  # weight-gradient split sums batched at the band's end
+                # conv weight-gradient split sums and Linear weight gradients batched at
+                # the band's end
+                with wgrad_deferred(), wgrad.grouped():
                     # d(recons + vq_loss).sum() = 1 for both roots: backward from the two
                     # roots with cached ones (no add / sum / ones_like launches)
                     torch.autograd.backward((part[1], part[2]["loss"]),

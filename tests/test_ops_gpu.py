@@ -313,6 +313,70 @@ def test_gemm_nn_tn(M, N, K, kind, cuda):
     assert err < 2e-6, err
 
 
+@pytest.mark.parametrize("case", ["lf_prior", "hf_prior", "ragged_chunked"])
+def test_wgrad_group(case, cuda):
+    """tvq_wgrad_group: dW_i += dY_i^T X_i for a list of Linear layers in one launch, the
+    outputs being views into one flat gradient buffer (as FusedAdamW keeps them), against
+    torch fp64; run twice from the same start, bitwise equal (fixed-order sums).
+    lf_prior: the LF prior's 16 weight gradients (4 layers x [q|k|v 384x128, out, ff1,
+    ff2 128x128], 6400 tokens, 64x64 tiles); hf_prior: the HF prior's (dim 32: 32x32 tiles,
+    24832 tokens); ragged_chunked: 30 odd shapes (two chunks of <= 24 descriptors), mixed
+    token counts and padded leading dimensions."""
+    from timevqvae.hip import wgrad
+    gen = torch.Generator().manual_seed(7)
+    if case == "lf_prior":
+        shapes = [(384, 128, 6400), (128, 128, 6400), (128, 128, 6400), (128, 128, 6400)] * 4
+    elif case == "hf_prior":
+        shapes = [(192, 32, 24832), (32, 64, 24832), (32, 32, 24832), (32, 32, 24832)]
+    else:
+        shapes = [(33 + 7 * i, 70 - 2 * i, 1001 + 97 * i) for i in range(30)]
+    flat = torch.randn(sum(m * n for m, n, _ in shapes), generator=gen)
+    recs, refs, off = [], [], 0
+    for i, (M, N, K) in enumerate(shapes):
+        pad = 3 if case == "ragged_chunked" and i % 2 else 0
+        dy = torch.randn(K, M + pad, generator=gen) / K ** 0.5
+        x = torch.randn(K, N + pad, generator=gen)
+        c0 = flat[off:off + M * N].view(M, N)
+        refs.append(dy[:, :M].double().t() @ x[:, :N].double() + c0.double())
+        recs.append((dy.to(cuda), M + pad, x.to(cuda), N + pad, (off, M * N), N, M, N, K))
+        off += M * N
+    outs = []
+    for _ in range(2):
+        fd = flat.to(cuda)
+        wgrad.launch([r[:4] + (fd[r[4][0]:r[4][0] + r[4][1]],) + r[5:] for r in recs])
+        outs.append(fd.cpu())
+    assert torch.equal(outs[0], outs[1])
+    off = 0
+    for (M, N, K), ref in zip(shapes, refs):
+        y = outs[0][off:off + M * N].view(M, N).double()
+        off += M * N
+        err = float((y - ref).norm() / ref.norm())
+        assert err < 2e-6, (M, N, K, err)
+
+
+def test_wgrad_group_deferral_keeps_order(cuda):
+    """Inside wgrad.grouped(), weight_grad records are issued at the scope's exit; a record
+    whose output overlaps a pending one flushes the pending ones first, so two
+    accumulations into one buffer keep their order (result equals back-to-back tvq_gemm)."""
+    from timevqvae.hip import wgrad
+    gen = torch.Generator().manual_seed(3)
+    M, N, K = 128, 128, 6400
+    dys = [torch.randn(K, M, generator=gen).to(cuda) for _ in range(3)]
+    xs = [torch.randn(K, N, generator=gen).to(cuda) for _ in range(3)]
+    dw = torch.zeros(2, M, N, device=cuda)
+    with wgrad.grouped():
+        assert wgrad.defer(dys[0], M, xs[0], N, dw[0], N, M, N, K)
+        assert wgrad.defer(dys[1], M, xs[1], N, dw[1], N, M, N, K)
+        assert wgrad.defer(dys[2], M, xs[2], N, dw[0], N, M, N, K)  # overlaps record 0
+        torch.cuda.synchronize()
+        assert float(dw[0].abs().sum()) != 0.0  # records 0 and 1 went out before record 2
+    assert not wgrad.defer(dys[0], M, xs[0], N, dw[0], N, M, N, K)  # no scope
+    ref = (dys[0].double().t() @ xs[0].double() + dys[2].double().t() @ xs[2].double())
+    assert float((dw[0].double() - ref).norm() / ref.norm()) < 2e-6
+    ref1 = dys[1].double().t() @ xs[1].double()
+    assert float((dw[1].double() - ref1).norm() / ref1.norm()) < 2e-6
+
+
 def test_losses(cuda):
     from timevqvae.hip.loss import l1_loss, mse_loss
     for f_hip, f_ref in ((mse_loss, F.mse_loss), (l1_loss, F.l1_loss)):
