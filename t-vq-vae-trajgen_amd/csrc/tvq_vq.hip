@@ -24,13 +24,27 @@ __device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
   return v < bv || (v == bv && i < bi);
 }
 
-__global__ void vq_sqnorm_kernel(const float* __restrict__ E, int K, int D, float* __restrict__ ee) {
-  int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  const float* e = E + (int64_t)k * D;
+// ||E_k||^2 as one fmaf chain over d in order (the same value the reference's CPU sum
+// rounds to here, and bitwise what the assign kernel has always used).  A block stages
+// SQ_CODES codebook rows into LDS with coalesced loads, then thread k runs code k's chain
+// from LDS (row stride D + 1: the threads' reads at one d hit distinct banks).  Reading
+// the rows straight from HBM one element per thread step took 19 us per codebook.
+constexpr int SQ_CODES = 32;
+__global__ __launch_bounds__(256) void vq_sqnorm_kernel(const float* __restrict__ E, int K, int D,
+                                                        float* __restrict__ ee) {
+  extern __shared__ float es[];  // [SQ_CODES][D + 1]
+  const int k0 = blockIdx.x * SQ_CODES;
+  const int nk = min(SQ_CODES, K - k0);
+  for (int e = threadIdx.x; e < nk * D; e += 256) {
+    const int c = e / D, d = e - c * D;
+    es[c * (D + 1) + d] = E[(int64_t)k0 * D + e];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x >= nk) return;
+  const float* r = es + threadIdx.x * (D + 1);
   float s = 0.f;
-  for (int d = 0; d < D; ++d) s = fmaf(e[d], e[d], s);
-  ee[k] = s;
+  for (int d = 0; d < D; ++d) s = fmaf(r[d], r[d], s);
+  ee[k0 + threadIdx.x] = s;
 }
 
 // Stochastic assignment (svq_temp > 0, vq.py:51-56 softmax_sample): idx ~
@@ -274,8 +288,10 @@ using namespace tvq;
 
 extern "C" int tvq_vq_sqnorm(const float* E, int64_t K, int64_t D, float* ee, tvq_stream_t stream) {
   TVQ_CHECK_ARG(E && ee && K > 0 && D > 0, "tvq_vq_sqnorm: bad arguments");
-  hipLaunchKernelGGL(vq_sqnorm_kernel, dim3((K + 255) / 256), dim3(256), 0, (hipStream_t)stream, E,
-                     (int)K, (int)D, ee);
+  TVQ_CHECK_ARG(D <= 1024, "tvq_vq_sqnorm: D > 1024");
+  hipLaunchKernelGGL(vq_sqnorm_kernel, dim3((unsigned)((K + SQ_CODES - 1) / SQ_CODES)), dim3(256),
+                     (size_t)SQ_CODES * (D + 1) * sizeof(float), (hipStream_t)stream, E, (int)K,
+                     (int)D, ee);
   return launch_status("tvq_vq_sqnorm");
 }
 

@@ -13,14 +13,22 @@
 // of `kper`; its 4 waves split the span and each computes the whole tile on
 // v_mfma_f32_32x32x2_f32 (TW x TW accumulators: lane l supplies A[m0 + 32 i + (l & 31)]
 // [k = l >> 5], i.e. each operand load is two 128-byte token rows of dY / X).  A wave
-// issues a chunk's loads (KC steps) before multiplying, with the next chunk in flight.
-// The 4 partial tiles are added through LDS in wave order; split tiles go to slab z of
-// the workspace and wgrad_group_reduce sums slabs 0..S-1 in order, then adds C.
-// Deterministic: every sum has a fixed order independent of scheduling.
+// issues a chunk's loads (KC steps) before multiplying, with the next chunk in flight; the
+// chunk loop has no branches (past the span: address clamped, A zeroed by a select), so
+// the loads of the next chunk stay in flight across it.  The 4 partial tiles are added
+// through LDS in wave order; split tiles go to the descriptor's slab z and
+// wgrad_group_reduce sums slabs 0..S-1 in order, then adds C.
+//
+// Every descriptor's plan (tile width, k span, split count) depends on its own shape only,
+// so a weight gradient's bits do not depend on what it was grouped with (a one-stream step
+// groups the LF and HF priors' records together, a multi-stream step does not).  Every
+// sum has a fixed order independent of scheduling: results are run-to-run identical.
 //
 // XCD map: block b runs on XCD b % 8; logical index L = (b % 8) * per + b / 8 walks
-// (split, tile) split-major, so one XCD holds whole splits: a split's dY / X token rows are
-// fetched into one L2 and re-read from it by every tile of that split.
+// (descriptor, split, tile), so one XCD holds whole splits: a split's dY / X token rows
+// are fetched into one L2 and re-read from it by every tile of that split.
+#include <alloca.h>
+#include <stdint.h>
 #include <stdlib.h>
 
 #include "tvq_common.h"
@@ -35,26 +43,29 @@ struct WgDesc {
   float* C;        // dW: C[m * ldc + n]
   int lda, ldb, ldc;
   int M, N, K;
-  int kper;        // k span of one split (multiple of 8)
-  int tiles_n;     // output tiles along n
-  int tile0;       // first tile of this descriptor in the group's tile space
+  int kper;        // k span of one split (multiple of 8 KC)
+  int S;           // splits
+  int tiles, tiles_n;
+  int blk0;        // first logical block of this descriptor (tiles * S of them)
   int rb0;         // first block of this descriptor in the reduce launch
   int accumulate;  // C += result
-  int64_t slab;    // offset of this descriptor's M x N partials inside one slab
+  int64_t slab;    // its S slabs of M x N partials in the workspace
 };
 
 struct WgGroup {
   WgDesc d[WG_MAXD];
-  float* ws;    // S slabs of `tot` floats
-  int64_t tot;
-  int n, S, tiles, per;
+  float* ws;
+  int n, per, blocks;
 };
 
-__device__ __forceinline__ int wg_find_tile(const WgGroup& G, int t) {
-  int di = 0;
-  for (int i = 1; i < G.n; ++i) di = G.d[i].tile0 <= t ? i : di;
-  return di;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wg_rsrc(const float* p, int64_t floats) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)(floats * 4), 0x00020000);
 }
+
+// Byte offset of token row k (wave-uniform; each lane adds its row h and column through
+// its base voffset).  It goes into the range-checked voffset, so rows past K load as 0;
+// rows past the wave's span (inside the tensor) are zeroed at use.
+__device__ __forceinline__ int wg_row(int k, int ld) { return k * ld * 4; }
 
 template <int TW, int KC>
 __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(WgGroup G) {
@@ -62,26 +73,31 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(WgGroup G) {
   __shared__ float red[4 * WSZ];
   const int b = (int)blockIdx.x;
   const int L = (b & 7) * G.per + (b >> 3);
-  const int z = L / G.tiles, t = L - z * G.tiles;
-  if (z >= G.S) return;  // padding block of the XCD map (whole block)
-  const WgDesc& d = G.d[wg_find_tile(G, t)];
-  const int lt = t - d.tile0;
-  const int tm = lt / d.tiles_n, tn = lt - tm * d.tiles_n;
+  if (L >= G.blocks) return;  // padding block of the XCD map (whole block)
+  int di = 0;
+  for (int i = 1; i < G.n; ++i) di = G.d[i].blk0 <= L ? i : di;
+  const WgDesc& d = G.d[di];
+  const int l = L - d.blk0;
+  const int z = l / d.tiles, t = l - z * d.tiles;
+  const int tm = t / d.tiles_n, tn = t - tm * d.tiles_n;
   const int m0 = tm * 32 * TW, n0 = tn * 32 * TW;
-  const int tid = (int)threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar k bounds
   const int r32 = lane & 31, h = lane >> 5;
   const int kq = d.kper >> 2;
   const int kb = z * d.kper + wid * kq;
   const int ke = min(d.K, kb + kq);
   const int steps = kb < ke ? (ke - kb + 1) >> 1 : 0;
-  const int64_t lda = d.lda, ldb = d.ldb;
-  // clamped row / column pointers (rows past M and columns past N are never stored)
-  const float* pa[TW];
-  const float* pb[TW];
+  const int nch = (steps + KC - 1) / KC;
+  const int lda = d.lda, ldb = d.ldb, K = d.K;
+  const auto ra = wg_rsrc(d.A, (int64_t)K * lda), rb = wg_rsrc(d.B, (int64_t)K * ldb);
+  // per-lane byte offsets (row h, clamped column): rows past M / columns past N are never
+  // stored
+  int va[TW], vb[TW];
 #pragma unroll
   for (int i = 0; i < TW; ++i) {
-    pa[i] = d.A + min(m0 + 32 * i + r32, d.M - 1);
-    pb[i] = d.B + min(n0 + 32 * i + r32, d.N - 1);
+    va[i] = (h * lda + min(m0 + 32 * i + r32, d.M - 1)) * 4;
+    vb[i] = (h * ldb + min(n0 + 32 * i + r32, d.N - 1)) * 4;
   }
   floatx16 acc[TW][TW];
 #pragma unroll
@@ -91,49 +107,53 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(WgGroup G) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // step s: k = kb + 2 s + h; steps past `steps` are skipped (wave-uniform branch); a
-  // lane's k past ke (odd span) -> address kb and A zeroed by a select at use
+  // step s: this lane's k = kb + 2 s + h; past ke: A zeroed by a select.  The chunk loop
+  // has no data-dependent branch: the next chunk's loads are always in flight while this
+  // one multiplies (the one past the last chunk is clamped and never used).
   float a0[KC][TW], b0[KC][TW], a1[KC][TW], b1[KC][TW];
   auto load = [&](float(&ad)[KC][TW], float(&bd)[KC][TW], int s0) {
 #pragma unroll
     for (int u = 0; u < KC; ++u) {
-      if (s0 + u < steps) {
-        int k = kb + 2 * (s0 + u) + h;
-        k = k < ke ? k : kb;
+      const int k = kb + 2 * (s0 + u);
+      const int oa = wg_row(k, lda), ob = wg_row(k, ldb);
 #pragma unroll
-        for (int i = 0; i < TW; ++i) {
-          ad[u][i] = pa[i][k * lda];
-          bd[u][i] = pb[i][k * ldb];
-        }
+      for (int i = 0; i < TW; ++i) {
+        ad[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, va[i] + oa, 0, 0));
+        bd[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, vb[i] + ob, 0, 0));
       }
     }
   };
   auto mul = [&](const float(&ad)[KC][TW], const float(&bd)[KC][TW], int s0) {
 #pragma unroll
     for (int u = 0; u < KC; ++u) {
-      if (s0 + u < steps) {
-        const bool ok = kb + 2 * (s0 + u) + h < ke;
+      const bool ok = kb + 2 * (s0 + u) + h < ke;
 #pragma unroll
-        for (int i = 0; i < TW; ++i) {
-          const float av = ok ? ad[u][i] : 0.f;
+      for (int i = 0; i < TW; ++i) {
+        const float av = ok ? ad[u][i] : 0.f;
 #pragma unroll
-          for (int j = 0; j < TW; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bd[u][j], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < TW; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bd[u][j], acc[i][j], 0, 0, 0);
       }
     }
   };
-  if (steps > 0) load(a0, b0, 0);
-  for (int s = 0; s < steps; s += 2 * KC) {
-    if (s + KC < steps) load(a1, b1, s + KC);
-    mul(a0, b0, s);
-    if (s + KC >= steps) break;
-    if (s + 2 * KC < steps) load(a0, b0, s + 2 * KC);
-    mul(a1, b1, s + KC);
+  // sched_barrier: keeps each chunk's loads together ahead of the previous chunk's MFMAs
+  // (left alone, the scheduler sinks every load next to its use: one load round trip per
+  // step)
+  if (nch > 0) load(a0, b0, 0);
+  for (int c = 0; c < nch; c += 2) {
+    load(a1, b1, (c + 1) * KC);
+    __builtin_amdgcn_sched_barrier(0);
+    mul(a0, b0, c * KC);
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 >= nch) break;
+    load(a0, b0, (c + 2) * KC);
+    __builtin_amdgcn_sched_barrier(0);
+    mul(a1, b1, (c + 1) * KC);
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   // the 4 waves' partial tiles -> LDS; thread e then owns tile elements e, e + 256, ...
-  // (row-major, so the global stores coalesce): ((w0 + w1) + w2) + w3
+  // (row-major, so the global stores coalesce): (w0 + w2) + (w1 + w3), the wide form's order
 #pragma unroll
   for (int i = 0; i < TW; ++i)
 #pragma unroll
@@ -142,7 +162,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(WgGroup G) {
       for (int r = 0; r < 16; ++r) red[wid * WSZ + ((i * TW + j) * 16 + r) * 64 + lane] = acc[i][j][r];
   __syncthreads();
   const int64_t ldc = d.ldc;
-  float* slab = G.S > 1 ? G.ws + (int64_t)z * G.tot + d.slab : nullptr;
+  float* slab = d.S > 1 ? G.ws + d.slab + (int64_t)z * d.M * d.N : nullptr;
 #pragma unroll
   for (int q = 0; q < TW * TW * 4; ++q) {
     const int e = tid + 256 * q;
@@ -150,7 +170,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(WgGroup G) {
     const int i = row >> 5, j = col >> 5, rr = row & 31, cc = col & 31;
     const int ln = cc + 32 * ((rr >> 2) & 1), r = (rr & 3) + 4 * (rr >> 3);
     const int o = ((i * TW + j) * 16 + r) * 64 + ln;
-    const float v = ((red[o] + red[WSZ + o]) + red[2 * WSZ + o]) + red[3 * WSZ + o];
+    const float v = (red[o] + red[2 * WSZ + o]) + (red[WSZ + o] + red[3 * WSZ + o]);
     const int m = m0 + row, n = n0 + col;
     if (m < d.M && n < d.N) {
       if (slab) {
@@ -163,19 +183,146 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(WgGroup G) {
   }
 }
 
-// slabs 0..S-1 summed in order, then C (+)= sum; one 256-element chunk of one descriptor
-// per block
+// Wide form for 16-byte-aligned outputs of at least 64 x 64: a 128 (m) x 64 (n) tile from
+// ONE float4 of dY and ONE float2 of X per lane and step (lane l = (h, r): dY row k at
+// m0 + 4 r, X row k at n0 + 2 r): 8 MFMAs per 2 loads, 32 FLOP per loaded byte (the TW
+// form: 16).  MFMA j x jj multiplies the rows {m0 + 4 r + j} by the columns {n0 + 2 r + jj},
+// a permutation of the tile that the store undoes.
+template <int KC>
+__global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WgGroup G) {
+  constexpr int WSZ = 8 * 16 * 64;  // one wave's partial tile in LDS
+  __shared__ float red[2 * WSZ];
+  const int b = (int)blockIdx.x;
+  const int L = (b & 7) * G.per + (b >> 3);
+  if (L >= G.blocks) return;  // padding block of the XCD map (whole block)
+  int di = 0;
+  for (int i = 1; i < G.n; ++i) di = G.d[i].blk0 <= L ? i : di;
+  const WgDesc& d = G.d[di];
+  const int l = L - d.blk0;
+  const int z = l / d.tiles, t = l - z * d.tiles;
+  const int tm = t / d.tiles_n, tn = t - tm * d.tiles_n;
+  const int m0 = tm * 128, n0 = tn * 64;
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar k bounds
+  const int r32 = lane & 31, h = lane >> 5;
+  const int kq = d.kper >> 2;
+  const int kb = z * d.kper + wid * kq;
+  const int ke = min(d.K, kb + kq);
+  const int steps = kb < ke ? (ke - kb + 1) >> 1 : 0;
+  const int nch = (steps + KC - 1) / KC;
+  const int lda = d.lda, ldb = d.ldb, K = d.K;
+  const auto ra = wg_rsrc(d.A, (int64_t)K * lda), rb = wg_rsrc(d.B, (int64_t)K * ldb);
+  // clamped (M % 4 == 0, N % 2 == 0): rows past M / columns past N are never stored
+  const int va = (h * lda + min(m0 + 4 * r32, d.M - 4)) * 4;
+  const int vb = (h * ldb + min(n0 + 2 * r32, d.N - 2)) * 4;
+  floatx16 acc[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][jj][e] = 0.f;
+  float4 a0[KC], a1[KC];
+  float2 b0[KC], b1[KC];
+  auto load = [&](float4(&ad)[KC], float2(&bd)[KC], int s0) {
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+      const int k = kb + 2 * (s0 + u);
+      ad[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, va + wg_row(k, lda), 0, 0));
+      bd[u] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rb, vb + wg_row(k, ldb), 0, 0));
+    }
+  };
+  auto mul = [&](const float4(&ad)[KC], const float2(&bd)[KC], int s0) {
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+      const bool ok = kb + 2 * (s0 + u) + h < ke;
+      const float av[4] = {ok ? ad[u].x : 0.f, ok ? ad[u].y : 0.f, ok ? ad[u].z : 0.f,
+                           ok ? ad[u].w : 0.f};
+      const float bv[2] = {bd[u].x, bd[u].y};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          acc[j][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[jj], acc[j][jj], 0, 0, 0);
+    }
+  };
+  // sched_barrier: keeps each chunk's loads together ahead of the previous chunk's MFMAs
+  // (left alone, the scheduler sinks every load next to its use: one load round trip per
+  // step)
+  if (nch > 0) load(a0, b0, 0);
+  for (int c = 0; c < nch; c += 2) {
+    load(a1, b1, (c + 1) * KC);
+    __builtin_amdgcn_sched_barrier(0);
+    mul(a0, b0, c * KC);
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 >= nch) break;
+    load(a0, b0, (c + 2) * KC);
+    __builtin_amdgcn_sched_barrier(0);
+    mul(a1, b1, (c + 1) * KC);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // (w0 + w2) + (w1 + w3): waves 2, 3 -> LDS, waves 0, 1 add; wave 1 -> LDS, wave 0 adds
+  float* slot = red + (wid & 1) * WSZ + lane;
+  if (wid >= 2) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) slot[(q * 16 + e) * 64] = acc[q >> 1][q & 1][e];
+  }
+  __syncthreads();
+  if (wid < 2) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[q >> 1][q & 1][e] += slot[(q * 16 + e) * 64];
+  }
+  __syncthreads();
+  if (wid == 1) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) slot[(q * 16 + e) * 64] = acc[q >> 1][q & 1][e];
+  }
+  __syncthreads();
+  if (wid != 0) return;
+  const float* o1 = red + WSZ + lane;
+  // acc e of lane (h, r): MFMA row 8 (e / 4) + 4 h + e % 4, column r -> tile row
+  // 4 (MFMA row) + j, columns 2 r + {0, 1}
+  const int n = n0 + 2 * r32;
+  float* slab = d.S > 1 ? G.ws + d.slab + (int64_t)z * d.M * d.N : nullptr;
+  const int64_t ldc = d.ldc;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float v0 = acc[j][0][e] + o1[((2 * j) * 16 + e) * 64];
+      const float v1 = acc[j][1][e] + o1[((2 * j + 1) * 16 + e) * 64];
+      const int m = m0 + 4 * (8 * (e >> 2) + 4 * h + (e & 3)) + j;
+      if (m >= d.M || n >= d.N) continue;
+      if (slab) {
+        *reinterpret_cast<float2*>(slab + (int64_t)m * d.N + n) = make_float2(v0, v1);
+      } else {
+        float* c = d.C + m * ldc + n;
+        c[0] = d.accumulate ? v0 + c[0] : v0;
+        c[1] = d.accumulate ? v1 + c[1] : v1;
+      }
+    }
+}
+
+// slabs 0..S-1 summed in order, then C (+)= sum; one 256-element chunk of one split
+// descriptor per block
 __global__ __launch_bounds__(256) void wgrad_group_reduce_kernel(WgGroup G) {
   const int b = (int)blockIdx.x;
   int di = 0;
   for (int i = 1; i < G.n; ++i) di = G.d[i].rb0 <= b ? i : di;
   const WgDesc& d = G.d[di];
   const int64_t e = (int64_t)(b - d.rb0) * 256 + threadIdx.x;
-  if (e >= (int64_t)d.M * d.N) return;
+  if (d.S <= 1 || e >= (int64_t)d.M * d.N) return;
   const float* p = G.ws + d.slab + e;
+  const int64_t tot = (int64_t)d.M * d.N;
   float s = 0.f;
 #pragma unroll 8
-  for (int z = 0; z < G.S; ++z) s += p[(int64_t)z * G.tot];
+  for (int z = 0; z < d.S; ++z) s += p[z * tot];
   const int m = (int)(e / d.N), n = (int)(e - (int64_t)m * d.N);
   float* c = d.C + (int64_t)m * d.ldc + n;
   *c = d.accumulate ? s + *c : s;
@@ -187,52 +334,51 @@ static int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
+// Tile classes: 4 = the wide 128 x 64 form, 2 = 64 x 64, 1 = 32 x 32.  MFMA steps per
+// chunk: 8 at 64 x 64 and 128 x 64 (2 waves per SIMD without spills), 16 at 32 x 32.
+__host__ __device__ constexpr int wg_kc(int tw) { return tw == 1 ? 16 : 8; }
+
+// The plan of one descriptor, from its own shape only: 64 x 64 tiles unless the output is
+// <= 32 wide; a k span near TVQ_WG_KSPAN (default 640 tokens: the LF prior's 48 wide tiles x 10 splits
+// = 480 blocks, one round at 2 per CU; 256 -> 1200 blocks: 86 us, 640: 67 us, 1280: 69 us) rounded to whole chunks of
+// the 4 waves (multiples of 8 KC), at most 64 splits.
 struct WgPlan {
-  int TW, S, kper, tiles;
-  int64_t tot;
+  int TW, S, kper, tiles, tiles_n;
 };
 
-// Tile width, split count and k span for descriptors [0, n): 64 x 64 tiles unless some
-// output is <= 32 wide; about TVQ_WG_BLOCKS (default 2048: 4 rounds of the 2 blocks per
-// CU the 64 KB LDS / ~200 VGPR footprint allows) blocks, at most 64 slabs, k spans of at
-// least 64 (16 MFMA steps per wave).
-static WgPlan wg_plan(int64_t n, const int64_t* M, const int64_t* N, const int64_t* K) {
+static WgPlan wg_plan(int64_t M, int64_t N, int64_t K, bool wide_ok) {
+  static const int kspan = env_int("TVQ_WG_KSPAN", 640);
+  static const bool wide_on = env_int("TVQ_WG_WIDE", 1) != 0;
   WgPlan p;
-  p.TW = 2;
-  int64_t kmax = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    if (M[i] <= 32 || N[i] <= 32) p.TW = 1;
-    if (K[i] > kmax) kmax = K[i];
-  }
-  const int ts = 32 * p.TW;
-  p.tiles = 0;
-  p.tot = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    p.tiles += (int)(((M[i] + ts - 1) / ts) * ((N[i] + ts - 1) / ts));
-    p.tot += M[i] * N[i];
-  }
-  const int target = env_int("TVQ_WG_BLOCKS", p.TW == 2 ? 2048 : 4096);
-  int64_t s = (target + p.tiles / 2) / p.tiles;
+  p.TW = (M <= 32 || N <= 32) ? 1 : 2;
+  if (p.TW == 2 && wide_on && wide_ok && M % 4 == 0 && N % 2 == 0) p.TW = 4;
+  const int tsm = 32 * p.TW, tsn = p.TW == 4 ? 64 : 32 * p.TW;
+  p.tiles_n = (int)((N + tsn - 1) / tsn);
+  p.tiles = (int)((M + tsm - 1) / tsm) * p.tiles_n;
+  int64_t s = (K + kspan / 2) / kspan;
   if (s > 64) s = 64;
   if (s < 1) s = 1;
-  int64_t kper = (kmax + s - 1) / s;
-  kper = (kper + 7) / 8 * 8;
-  if (kper < 64) kper = 64;
+  const int q = 8 * wg_kc(p.TW);
+  int64_t kper = (K + s - 1) / s;
+  kper = (kper + q - 1) / q * q;
   p.kper = (int)kper;
-  p.S = (int)((kmax + kper - 1) / kper);
+  p.S = (int)((K + kper - 1) / kper);
   return p;
 }
 
+static bool wide_aligned(const float* A, int64_t lda, const float* B, int64_t ldb) {
+  return ((uintptr_t)A & 15) == 0 && lda % 4 == 0 && ((uintptr_t)B & 7) == 0 && ldb % 2 == 0;
+}
+
+// each descriptor with S > 1 owns S slabs of M x N floats (no reuse between launches)
 extern "C" int64_t tvq_wgrad_group_workspace(int64_t n, const int64_t* M, const int64_t* N,
                                              const int64_t* K) {
-  int64_t best = 0;
-  for (int64_t c0 = 0; c0 < n; c0 += WG_MAXD) {
-    const int64_t c = n - c0 < WG_MAXD ? n - c0 : WG_MAXD;
-    const WgPlan p = wg_plan(c, M + c0, N + c0, K + c0);
-    const int64_t need = p.S > 1 ? p.S * p.tot : 0;
-    if (need > best) best = need;
+  int64_t need = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const WgPlan p = wg_plan(M[i], N[i], K[i], false);  // S does not depend on the form
+    if (p.S > 1) need += (int64_t)p.S * M[i] * N[i];
   }
-  return best;
+  return need;
 }
 
 extern "C" int tvq_wgrad_group(int64_t n, const float* const* dY, const int64_t* ldy,
@@ -243,55 +389,66 @@ extern "C" int tvq_wgrad_group(int64_t n, const float* const* dY, const int64_t*
   TVQ_CHECK_ARG(n >= 0 && dY && ldy && X && ldx && dW && ldw && M && N && K,
                 "tvq_wgrad_group: bad arguments");
   hipStream_t st = (hipStream_t)stream;
-  for (int64_t c0 = 0; c0 < n; c0 += WG_MAXD) {  // chunks run in order on `stream`
-    const int64_t c = n - c0 < WG_MAXD ? n - c0 : WG_MAXD;
-    const WgPlan p = wg_plan(c, M + c0, N + c0, K + c0);
-    TVQ_CHECK_ARG(p.S == 1 || workspace, "tvq_wgrad_group: workspace required");
-    WgGroup G;
-    G.n = (int)c;
-    G.S = p.S;
-    G.tiles = p.tiles;
-    G.tot = p.tot;
-    G.ws = workspace;
-    const int ts = 32 * p.TW;
-    int tile0 = 0, rb0 = 0;
-    int64_t off = 0;
-    for (int64_t i = 0; i < c; ++i) {
-      const int64_t j = c0 + i;
-      TVQ_CHECK_ARG(dY[j] && X[j] && dW[j] && M[j] > 0 && N[j] > 0 && K[j] > 0 &&
-                        ldy[j] >= M[j] && ldx[j] >= N[j] && ldw[j] >= N[j] &&
-                        K[j] * (ldy[j] > ldx[j] ? ldy[j] : ldx[j]) < ((int64_t)1 << 31) &&
-                        M[j] * ldw[j] < ((int64_t)1 << 31),
-                    "tvq_wgrad_group: bad descriptor %lld", (long long)j);
-      WgDesc& d = G.d[i];
-      d.A = dY[j];
-      d.B = X[j];
-      d.C = dW[j];
-      d.lda = (int)ldy[j];
-      d.ldb = (int)ldx[j];
-      d.ldc = (int)ldw[j];
-      d.M = (int)M[j];
-      d.N = (int)N[j];
-      d.K = (int)K[j];
-      d.kper = p.kper;
-      d.tiles_n = (int)((N[j] + ts - 1) / ts);
-      d.tile0 = tile0;
-      d.rb0 = rb0;
-      d.accumulate = (int)accumulate;
-      d.slab = off;
-      tile0 += (int)((M[j] + ts - 1) / ts) * d.tiles_n;
-      rb0 += (int)((M[j] * N[j] + 255) / 256);
-      off += M[j] * N[j];
+  for (int64_t j = 0; j < n; ++j)
+    TVQ_CHECK_ARG(dY[j] && X[j] && dW[j] && M[j] > 0 && N[j] > 0 && K[j] > 0 && ldy[j] >= M[j] &&
+                      ldx[j] >= N[j] && ldw[j] >= N[j] &&
+                      (K[j] + 64) * (ldy[j] > ldx[j] ? ldy[j] : ldx[j]) < ((int64_t)1 << 29) &&
+                      M[j] * ldw[j] < ((int64_t)1 << 31),
+                  "tvq_wgrad_group: bad descriptor %lld", (long long)j);
+  // one launch pair per chunk of <= WG_MAXD descriptors of one tile class, in order on
+  // `stream` (the outputs are disjoint and every descriptor's sums have the same order in
+  // every form, so neither the classes nor the chunking change a result)
+  int64_t slab0 = 0;
+  int64_t* slab_of = (int64_t*)alloca(sizeof(int64_t) * (n > 0 ? n : 1));
+  for (int64_t j = 0; j < n; ++j) {
+    slab_of[j] = slab0;
+    const WgPlan p = wg_plan(M[j], N[j], K[j], false);
+    if (p.S > 1) slab0 += (int64_t)p.S * M[j] * N[j];
+  }
+  TVQ_CHECK_ARG(slab0 == 0 || workspace, "tvq_wgrad_group: workspace required");
+  for (int tw : {4, 2, 1}) {
+    int64_t j = 0;
+    while (true) {
+      WgGroup G;
+      G.n = 0;
+      G.ws = workspace;
+      int blk = 0, rb = 0;
+      for (; j < n && G.n < WG_MAXD; ++j) {
+        const WgPlan p = wg_plan(M[j], N[j], K[j], wide_aligned(dY[j], ldy[j], X[j], ldx[j]));
+        if (p.TW != tw) continue;
+        WgDesc& d = G.d[G.n++];
+        d.A = dY[j];
+        d.B = X[j];
+        d.C = dW[j];
+        d.lda = (int)ldy[j];
+        d.ldb = (int)ldx[j];
+        d.ldc = (int)ldw[j];
+        d.M = (int)M[j];
+        d.N = (int)N[j];
+        d.K = (int)K[j];
+        d.kper = p.kper;
+        d.S = p.S;
+        d.tiles = p.tiles;
+        d.tiles_n = p.tiles_n;
+        d.blk0 = blk;
+        d.rb0 = rb;
+        d.accumulate = (int)accumulate;
+        d.slab = slab_of[j];
+        blk += p.tiles * p.S;
+        if (p.S > 1) rb += (int)((M[j] * N[j] + 255) / 256);
+      }
+      if (G.n == 0) break;
+      G.blocks = blk;
+      G.per = (blk + 7) / 8;
+      const unsigned grid = (unsigned)(8 * G.per);
+      if (tw == 4)
+        hipLaunchKernelGGL((wgrad_wide_kernel<wg_kc(4)>), dim3(grid), dim3(256), 0, st, G);
+      else if (tw == 2)
+        hipLaunchKernelGGL((wgrad_group_kernel<2, wg_kc(2)>), dim3(grid), dim3(256), 0, st, G);
+      else
+        hipLaunchKernelGGL((wgrad_group_kernel<1, wg_kc(1)>), dim3(grid), dim3(256), 0, st, G);
+      if (rb > 0) hipLaunchKernelGGL(wgrad_group_reduce_kernel, dim3((unsigned)rb), dim3(256), 0, st, G);
     }
-    const int64_t logical = (int64_t)p.tiles * p.S;
-    G.per = (int)((logical + 7) / 8);
-    const unsigned grid = (unsigned)(8 * G.per);
-    if (p.TW == 2)
-      hipLaunchKernelGGL((wgrad_group_kernel<2, 16>), dim3(grid), dim3(256), 0, st, G);
-    else
-      hipLaunchKernelGGL((wgrad_group_kernel<1, 16>), dim3(grid), dim3(256), 0, st, G);
-    if (p.S > 1)
-      hipLaunchKernelGGL(wgrad_group_reduce_kernel, dim3((unsigned)rb0), dim3(256), 0, st, G);
   }
   return launch_status("tvq_wgrad_group");
 }

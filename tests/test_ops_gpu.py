@@ -354,6 +354,26 @@ def test_wgrad_group(case, cuda):
         assert err < 2e-6, (M, N, K, err)
 
 
+def test_wgrad_group_forms_bitwise_equal(cuda):
+    """The wide 128x64 form (16-byte-aligned operands) and the 64x64 form (the same data
+    one float off alignment) sum every element in the same order: equal bit for bit, so a
+    weight gradient does not depend on the allocator's alignment or on its group."""
+    from timevqvae.hip import wgrad
+    gen = torch.Generator().manual_seed(11)
+    M, N, K = 384, 128, 6400
+    dy = torch.randn(K, M, generator=gen).to(cuda)
+    x = torch.randn(K, N, generator=gen).to(cuda)
+    buf = torch.empty(K * M + 1, device=cuda)
+    dy_off = buf[1:].view(K, M)
+    dy_off.copy_(dy)
+    outs = []
+    for a in (dy, dy_off):
+        dw = torch.zeros(M, N, device=cuda)
+        wgrad.launch([(a, M, x, N, dw, N, M, N, K)])
+        outs.append(dw)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_wgrad_group_deferral_keeps_order(cuda):
     """Inside wgrad.grouped(), weight_grad records are issued at the scope's exit; a record
     whose output overlaps a pending one flushes the pending ones first, so two

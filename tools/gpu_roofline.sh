@@ -13,6 +13,6 @@ timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o
 timeout -s KILL 90 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES --output-format csv -d $O/sq -o roof -- python tools/roofline_only.py $LEG > $O/sq.log 2>&1 || exit 1
 
 if [ "$LEG" = dominant ]; then
-  python tools/roof_traffic.py $O $O/traffic.json "weight-gradient GEMM dW += dY^T X, 128x128 over 6400 tokens: gemm_kt_kernel + gemm_direct_reduce_kernel" gemm_kt_kernel gemm_direct_reduce_kernel
+  python tools/roof_traffic.py $O $O/traffic.json "grouped weight gradients of the LF prior (16 Linears, 6400 tokens): wgrad_wide_kernel + wgrad_group_reduce_kernel" wgrad_wide_kernel wgrad_group_reduce_kernel
 fi
 echo roofline-done

@@ -7,9 +7,9 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py -x -q -m gpu -k "wgrad or gemm" \
   --timeout 120 --timeout-method thread > gpurun_out/wg_tests.log 2>&1 || { tail -30 gpurun_out/wg_tests.log; exit 1; }
 tail -2 gpurun_out/wg_tests.log
-for b in ${WG_BLOCKS:-1024 2048 3072}; do
-  TVQ_WG_BLOCKS=$b timeout -k 10 120 python tools/roofline_only.py dominant > gpurun_out/wg_dom_$b.json 2>&1 || { tail -20 gpurun_out/wg_dom_$b.json; exit 1; }
-  echo "blocks $b: $(cut -c1-400 gpurun_out/wg_dom_$b.json | grep -o '"achieved[^,]*,\|"avg_launch_us[^,]*' | tr '\n' ' ')"
+for b in ${WG_KSPAN:-256 512 1024}; do
+  TVQ_WG_KSPAN=$b timeout -k 10 120 python tools/roofline_only.py dominant > gpurun_out/wg_dom_$b.json 2>&1 || { tail -20 gpurun_out/wg_dom_$b.json; exit 1; }
+  echo "kspan $b: $(cut -c1-400 gpurun_out/wg_dom_$b.json | grep -o '"achieved[^,]*,\|"avg_launch_us[^,]*' | tr '\n' ' ')"
 done
 timeout -k 10 400 python -u -m pytest tests/test_graph.py tests/test_stage2.py tests/test_stage2_golden.py tests/test_stage1.py tests/test_dp_gpu.py -x -q -m gpu \
   --timeout 120 --timeout-method thread > gpurun_out/wg_step_tests.log 2>&1 || { tail -30 gpurun_out/wg_step_tests.log; exit 1; }
