@@ -19,10 +19,9 @@
 // through LDS in wave order; split tiles go to the descriptor's slab z and
 // wgrad_group_reduce sums slabs 0..S-1 in order, then adds C.
 //
-// Every descriptor's plan (tile width, k span, split count) depends on its own shape only,
-// so a weight gradient's bits do not depend on what it was grouped with (a one-stream step
-// groups the LF and HF priors' records together, a multi-stream step does not).  Every
-// sum has a fixed order independent of scheduling: results are run-to-run identical.
+// A launch's plan depends on the descriptors it holds (see wg_splits); the caller groups
+// records the same way whatever the streams (timevqvae.hip.wgrad tags).  Every sum has a
+// fixed order independent of scheduling: results are run-to-run identical.
 //
 // XCD map: block b runs on XCD b % 8; logical index L = (b % 8) * per + b / 8 walks
 // (descriptor, split, tile), so one XCD holds whole splits: a split's dY / X token rows
@@ -338,45 +337,53 @@ static int env_int(const char* name, int dflt) {
 // chunk: 8 at 64 x 64 and 128 x 64 (2 waves per SIMD without spills), 16 at 32 x 32.
 __host__ __device__ constexpr int wg_kc(int tw) { return tw == 1 ? 16 : 8; }
 
-// The plan of one descriptor, from its own shape only: 64 x 64 tiles unless the output is
-// <= 32 wide; a k span near TVQ_WG_KSPAN (default 640 tokens: the LF prior's 48 wide tiles x 10 splits
-// = 480 blocks, one round at 2 per CU; 256 -> 1200 blocks: 86 us, 640: 67 us, 1280: 69 us) rounded to whole chunks of
-// the 4 waves (multiples of 8 KC), at most 64 splits.
-struct WgPlan {
-  int TW, S, kper, tiles, tiles_n;
-};
+// Plans are made per launch: a launch holds one tile class (wide 128 x 64 = 4, 64 x 64 = 2,
+// 32 x 32 = 1) and at most WG_MAXD descriptors, in the caller's order.  Its split count S
+// is chosen from the launch's work units (64 x 64 tiles for classes 4 and 2, 32 x 32 for
+// class 1) so that it has about TVQ_WG_UNITS (default 1000, resp. 1024) unit-splits: the
+// LF prior's 16 Linears + its head (100 units) get S = 10, i.e. 500 wide blocks, one round
+// at 2 per CU; a lone 256 x 256 Linear gets short spans over many blocks.  Every
+// descriptor of the launch uses S (its k span: K / S rounded up to whole chunks of the 4
+// waves, 8 KC).  Classes 4 and 2 count the same units and sum in the same order, so a
+// descriptor's bits do not depend on which of the two its alignment selects.
+static int wg_units(int64_t M, int64_t N, int tw) {
+  const int u = tw == 1 ? 32 : 64;
+  return (int)(((M + u - 1) / u) * ((N + u - 1) / u));
+}
 
-static WgPlan wg_plan(int64_t M, int64_t N, int64_t K, bool wide_ok) {
-  static const int kspan = env_int("TVQ_WG_KSPAN", 640);
+static int wg_class(int64_t M, int64_t N, bool wide_ok) {
   static const bool wide_on = env_int("TVQ_WG_WIDE", 1) != 0;
-  WgPlan p;
-  p.TW = (M <= 32 || N <= 32) ? 1 : 2;
-  if (p.TW == 2 && wide_on && wide_ok && M % 4 == 0 && N % 2 == 0) p.TW = 4;
-  const int tsm = 32 * p.TW, tsn = p.TW == 4 ? 64 : 32 * p.TW;
-  p.tiles_n = (int)((N + tsn - 1) / tsn);
-  p.tiles = (int)((M + tsm - 1) / tsm) * p.tiles_n;
-  int64_t s = (K + kspan / 2) / kspan;
-  if (s > 64) s = 64;
-  if (s < 1) s = 1;
-  const int q = 8 * wg_kc(p.TW);
-  int64_t kper = (K + s - 1) / s;
-  kper = (kper + q - 1) / q * q;
-  p.kper = (int)kper;
-  p.S = (int)((K + kper - 1) / kper);
-  return p;
+  if (M <= 32 || N <= 32) return 1;
+  return (wide_on && wide_ok && M % 4 == 0 && N % 2 == 0) ? 4 : 2;
+}
+
+static int wg_splits(int units, int tw) {
+  static const int t2 = env_int("TVQ_WG_UNITS", 1000);
+  static const int t1 = env_int("TVQ_WG_UNITS1", 1024);
+  int64_t s = ((tw == 1 ? t1 : t2) + units / 2) / (units > 0 ? units : 1);
+  return (int)(s < 1 ? 1 : (s > 64 ? 64 : s));
+}
+
+static void wg_span(int64_t K, int S, int tw, int* kper, int* splits) {
+  const int q = 8 * wg_kc(tw);
+  int64_t kp = (K + S - 1) / S;
+  kp = (kp + q - 1) / q * q;
+  *kper = (int)kp;
+  *splits = (int)((K + kp - 1) / kp);
 }
 
 static bool wide_aligned(const float* A, int64_t lda, const float* B, int64_t ldb) {
   return ((uintptr_t)A & 15) == 0 && lda % 4 == 0 && ((uintptr_t)B & 7) == 0 && ldb % 2 == 0;
 }
 
-// each descriptor with S > 1 owns S slabs of M x N floats (no reuse between launches)
+// an upper bound (the alignment that picks a class is not known here): S <= 64 and
+// S <= ceil(K / 64) for every descriptor
 extern "C" int64_t tvq_wgrad_group_workspace(int64_t n, const int64_t* M, const int64_t* N,
                                              const int64_t* K) {
   int64_t need = 0;
   for (int64_t i = 0; i < n; ++i) {
-    const WgPlan p = wg_plan(M[i], N[i], K[i], false);  // S does not depend on the form
-    if (p.S > 1) need += (int64_t)p.S * M[i] * N[i];
+    const int64_t s = (K[i] + 63) / 64 < 64 ? (K[i] + 63) / 64 : 64;
+    if (s > 1) need += s * M[i] * N[i];
   }
   return need;
 }
@@ -395,49 +402,57 @@ extern "C" int tvq_wgrad_group(int64_t n, const float* const* dY, const int64_t*
                       (K[j] + 64) * (ldy[j] > ldx[j] ? ldy[j] : ldx[j]) < ((int64_t)1 << 29) &&
                       M[j] * ldw[j] < ((int64_t)1 << 31),
                   "tvq_wgrad_group: bad descriptor %lld", (long long)j);
-  // one launch pair per chunk of <= WG_MAXD descriptors of one tile class, in order on
-  // `stream` (the outputs are disjoint and every descriptor's sums have the same order in
-  // every form, so neither the classes nor the chunking change a result)
-  int64_t slab0 = 0;
   int64_t* slab_of = (int64_t*)alloca(sizeof(int64_t) * (n > 0 ? n : 1));
-  for (int64_t j = 0; j < n; ++j) {
+  int* cls = (int*)alloca(sizeof(int) * (n > 0 ? n : 1));
+  int64_t slab0 = 0;
+  for (int64_t j = 0; j < n; ++j) {  // each descriptor's slabs at its workspace-bound offset
     slab_of[j] = slab0;
-    const WgPlan p = wg_plan(M[j], N[j], K[j], false);
-    if (p.S > 1) slab0 += (int64_t)p.S * M[j] * N[j];
+    const int64_t s = (K[j] + 63) / 64 < 64 ? (K[j] + 63) / 64 : 64;
+    if (s > 1) slab0 += s * M[j] * N[j];
+    cls[j] = wg_class(M[j], N[j], wide_aligned(dY[j], ldy[j], X[j], ldx[j]));
   }
   TVQ_CHECK_ARG(slab0 == 0 || workspace, "tvq_wgrad_group: workspace required");
+  // one launch pair per chunk of <= WG_MAXD descriptors of one class, in order on `stream`
+  // (the outputs are disjoint: the launches may run in any order)
   for (int tw : {4, 2, 1}) {
     int64_t j = 0;
     while (true) {
+      int64_t idx[WG_MAXD];
+      int cnt = 0, units = 0;
+      for (; j < n && cnt < WG_MAXD; ++j)
+        if (cls[j] == tw) {
+          idx[cnt++] = j;
+          units += wg_units(M[j], N[j], tw);
+        }
+      if (cnt == 0) break;
+      const int S0 = wg_splits(units, tw);
       WgGroup G;
-      G.n = 0;
+      G.n = cnt;
       G.ws = workspace;
       int blk = 0, rb = 0;
-      for (; j < n && G.n < WG_MAXD; ++j) {
-        const WgPlan p = wg_plan(M[j], N[j], K[j], wide_aligned(dY[j], ldy[j], X[j], ldx[j]));
-        if (p.TW != tw) continue;
-        WgDesc& d = G.d[G.n++];
-        d.A = dY[j];
-        d.B = X[j];
-        d.C = dW[j];
-        d.lda = (int)ldy[j];
-        d.ldb = (int)ldx[j];
-        d.ldc = (int)ldw[j];
-        d.M = (int)M[j];
-        d.N = (int)N[j];
-        d.K = (int)K[j];
-        d.kper = p.kper;
-        d.S = p.S;
-        d.tiles = p.tiles;
-        d.tiles_n = p.tiles_n;
+      const int tsm = 32 * tw, tsn = tw == 4 ? 64 : 32 * tw;
+      for (int i = 0; i < cnt; ++i) {
+        const int64_t q = idx[i];
+        WgDesc& d = G.d[i];
+        d.A = dY[q];
+        d.B = X[q];
+        d.C = dW[q];
+        d.lda = (int)ldy[q];
+        d.ldb = (int)ldx[q];
+        d.ldc = (int)ldw[q];
+        d.M = (int)M[q];
+        d.N = (int)N[q];
+        d.K = (int)K[q];
+        wg_span(K[q], S0, tw, &d.kper, &d.S);
+        d.tiles_n = (int)((N[q] + tsn - 1) / tsn);
+        d.tiles = (int)((M[q] + tsm - 1) / tsm) * d.tiles_n;
         d.blk0 = blk;
         d.rb0 = rb;
         d.accumulate = (int)accumulate;
-        d.slab = slab_of[j];
-        blk += p.tiles * p.S;
-        if (p.S > 1) rb += (int)((M[j] * N[j] + 255) / 256);
+        d.slab = slab_of[q];
+        blk += d.tiles * d.S;
+        if (d.S > 1) rb += (int)((M[q] * N[q] + 255) / 256);
       }
-      if (G.n == 0) break;
       G.blocks = blk;
       G.per = (blk + 7) / 8;
       const unsigned grid = (unsigned)(8 * G.per);

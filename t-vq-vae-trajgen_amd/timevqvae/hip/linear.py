@@ -33,11 +33,12 @@ def _bias_grad_rows(g2, sink=None):
     return out
 
 
-def weight_grad(g, x2, w_param, M, N, K):
-    """dW = g^T x (N x K): accumulated into the flat grad view when available."""
+def weight_grad(g, x2, w_param, M, N, K, tag=None):
+    """dW = g^T x (N x K): accumulated into the flat grad view when available (deferred to
+    the grouped launch inside a wgrad.grouped() scope; `tag`: the forward's wgrad tag)."""
     sink = grad_sink(w_param)
     if sink is not None:  # into the flat gradient: off the critical path
-        if wgrad.defer(g, N, x2, K, sink, K, N, K, M):  # grouped at the backward's end
+        if wgrad.defer(g, N, x2, K, sink, K, N, K, M, tag):  # grouped at the backward's end
             return None
         with streams.offload(g, x2):
             gemm(g, 1, N, x2, K, 1, N, K, M, out=sink, ldc=K, accumulate=True)
@@ -68,6 +69,7 @@ class _Linear(torch.autograd.Function):
         ctx.has = (b is not None, residual is not None)
         ctx.shp = shp
         ctx.params = (w, b)
+        ctx.wg_tag = wgrad.current_tag()
         ctx.gate = gate
         return y.reshape(*shp[:-1], N)
 
@@ -84,7 +86,7 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = gemm(g, N, 1, w, K, 1, M, K, N).reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
-            dw = weight_grad(g, x2, ctx.params[0], M, N, K)
+            dw = weight_grad(g, x2, ctx.params[0], M, N, K, ctx.wg_tag)
         if ctx.has[0] and ctx.needs_input_grad[2]:
             db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
         return dx, dw, db, dres, None
@@ -103,6 +105,7 @@ class _LinearSelfRes(torch.autograd.Function):
         y = gemm(x2, K, 1, w.contiguous(), 1, K, M, K, K, bias=b, R=x2, ldr=K)
         ctx.save_for_backward(x2, w)
         ctx.params = (w, b)
+        ctx.wg_tag = wgrad.current_tag()
         ctx.shp = shp
         return y.reshape(shp)
 
@@ -115,7 +118,7 @@ class _LinearSelfRes(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = gemm(g, K, 1, w.contiguous(), K, 1, M, K, K, R=g, ldr=K).reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
-            dw = weight_grad(g, x2, ctx.params[0], M, K, K)
+            dw = weight_grad(g, x2, ctx.params[0], M, K, K, ctx.wg_tag)
         if ctx.params[1] is not None and ctx.needs_input_grad[2]:
             db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
         return dx, dw, db

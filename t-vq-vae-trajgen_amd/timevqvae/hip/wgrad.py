@@ -23,8 +23,27 @@ import torch
 from ._native import call, ptr, value
 
 ENABLED = os.environ.get("TVQ_WGRAD_GROUP", "1") != "0"
+_DEBUG = os.environ.get("TVQ_WGRAD_DEBUG", "0") != "0"  # print each launch's shapes
 
-_pending = None  # stream -> list of records while a scope is active
+_pending = None  # (stream, tag) -> list of records while a scope is active
+_tag = [None]
+
+
+@contextlib.contextmanager
+def tag(name):
+    """Records of the Linear layers whose forward runs in the body form their own launch
+    (e.g. one per prior): the launch plan is made per launch, so the grouping must not
+    depend on the streams (a one-stream step puts both priors on one stream)."""
+    prev = _tag[0]
+    _tag[0] = name
+    try:
+        yield
+    finally:
+        _tag[0] = prev
+
+
+def current_tag():
+    return _tag[0]
 
 
 @contextlib.contextmanager
@@ -39,7 +58,7 @@ def grouped():
         yield
     finally:
         pend, _pending = _pending, None
-        for st, recs in pend.items():
+        for (st, _), recs in pend.items():
             if recs:
                 with torch.cuda.stream(st):
                     launch(recs)
@@ -50,6 +69,9 @@ def launch(recs):
     tvq_wgrad_group call on the current stream."""
     n = len(recs)
     dev = recs[0][0].device
+    if _DEBUG:
+        print("tvq_wgrad_group", torch.cuda.current_stream().stream_id,
+              [(r[6], r[7], r[8]) for r in recs], flush=True)
     I64s = ctypes.c_int64 * n
     Ps = ctypes.c_void_p * n
     M, N, K = I64s(*[r[6] for r in recs]), I64s(*[r[7] for r in recs]), I64s(*[r[8] for r in recs])
@@ -69,19 +91,21 @@ def _span(t, rows, ld, cols):
     return a, a + 4 * ((rows - 1) * ld + cols)
 
 
-def defer(dy, ldy, x, ldx, dw, ldw, M, N, K):
+def defer(dy, ldy, x, ldx, dw, ldw, M, N, K, tag=None):
     """Record dW[m*ldw + n] += sum_k dY[k*ldy + m] X[k*ldx + n] (m < M, n < N, k < K)
     when a grouped() scope is active (returns True); else returns False and the caller
     launches it.  The flat-gradient view `dw` must not be read or written by anything
-    else before the scope's exit (Linear weight gradients: read by the optimizer only)."""
+    else before the scope's exit (Linear weight gradients: read by the optimizer only).
+    `tag`: the current_tag() of the layer's forward (records group per stream and tag)."""
     if _pending is None:
         return False
     rec = (dy, ldy, x, ldx, dw, ldw, M, N, K)
     st = torch.cuda.current_stream()
-    recs = _pending.setdefault(st, [])
+    recs = _pending.setdefault((st, tag), [])
     lo, hi = _span(dw, M, ldw, N)
-    if any(lo < h and l < hi for l, h in (_span(r[4], r[6], r[5], r[7]) for r in recs)):
-        launch(recs)  # same output: keep the accumulation order
-        recs.clear()
+    for other in [v for (s_, _), v in _pending.items() if s_ == st]:
+        if any(lo < h and l < hi for l, h in (_span(r[4], r[6], r[5], r[7]) for r in other)):
+            launch(other)  # same output: keep the accumulation order
+            other.clear()
     recs.append(rec)
     return True

@@ -144,6 +144,7 @@ class _LinearAct(torch.autograd.Function):
         y = gemm(x2, K, 1, w, 1, K, M, N, K, bias=b, act=act, pre=pre)
         ctx.save_for_backward(x2, w, pre)
         ctx.params = (w, b)
+        ctx.wg_tag = wgrad.current_tag()
         ctx.act = act
         ctx.has_b = b is not None
         ctx.shape = x.shape
@@ -163,7 +164,7 @@ class _LinearAct(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = gemm(g, N, 1, w, K, 1, M, K, N).reshape(ctx.shape)
         if ctx.needs_input_grad[1]:
-            dw = weight_grad(g, x2, ctx.params[0], M, N, K)
+            dw = weight_grad(g, x2, ctx.params[0], M, N, K, ctx.wg_tag)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
         return dx, dw, db, None
@@ -257,6 +258,7 @@ class _QKVAttention(torch.autograd.Function):
              stream_ptr())
         ctx.save_for_backward(x2, W, qkv, o, lse)
         ctx.params = (wq, wk, wv)
+        ctx.wg_tag = wgrad.current_tag()
         ctx.cfg = (B, S, D, HD, heads, drop_p, off, scale)
         ctx.seed = seed
         return o.reshape(B, S, HD)
@@ -280,7 +282,7 @@ class _QKVAttention(torch.autograd.Function):
             sinks = [grad_sink(p) for p in ctx.params]
             sink = _stacked(sinks, (L, D)) if all(s is not None for s in sinks) else None
             if sink is not None:  # into the flat gradient (stacked view)
-                if not wgrad.defer(dqkv, L, x2, D, sink, D, L, D, M):  # else grouped later
+                if not wgrad.defer(dqkv, L, x2, D, sink, D, L, D, M, ctx.wg_tag):  # else grouped later
                     with streams.offload(dqkv, x2):
                         gemm(dqkv, 1, L, x2, D, 1, L, D, M, out=sink, ldc=D, accumulate=True)
             else:

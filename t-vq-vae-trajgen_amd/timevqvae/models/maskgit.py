@@ -13,7 +13,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..hip import rng, streams
+from ..hip import rng, streams, wgrad
 from ..hip.sample import codebook_gather_nchw, mask_len, maskgit_remask, maskgit_sample
 from ..hip.signal import stft_encode
 from ..hip.xf import mask_tokens, masked_cross_entropy
@@ -143,10 +143,12 @@ class MaskGIT(nn.Module):
         try:
             with streams.branch(x.device) as br:  # HF transformer concurrently with LF
                 br.inputs(y, s_l_M, s_h_M, s_h, keep_h)
-                logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
+                with wgrad.tag("prior_h"):  # its weight gradients: one grouped launch
+                    logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
                 mask_pred_loss_h = masked_cross_entropy(logits_h, s_h, keep_h)
                 br.outputs(mask_pred_loss_h)
-            logits_l = self.masked_prediction(self.transformer_l, y, s_l_M)
+            with wgrad.tag("prior_l"):
+                logits_l = self.masked_prediction(self.transformer_l, y, s_l_M)
             mask_pred_loss_l = masked_cross_entropy(logits_l, s_l, keep_l)
             br.join()
         finally:
