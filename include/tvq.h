@@ -80,6 +80,15 @@ int tvq_vq_assign_svq(const float* x, int64_t B, int64_t N, int64_t D, int64_t s
                       float temp, const float* gumbel, const int64_t* seed_ptr, uint64_t offset,
                       float* quant, int64_t* idx, int32_t* idx32, float* commit_partial,
                       tvq_stream_t stream);
+/* tvq_vq_assign_svq that, when training, also writes x token-major to token_rows
+ * (M x D floats, row m = x[m / N, m % N, :]; NULL: not written), so that tvq_vq_stats
+ * can read contiguous rows (pass token_rows with B = 1, N = M, sN = D, sD = 1) instead of
+ * gathering D-strided elements of an NCHW latent. */
+int tvq_vq_assign_rows(const float* x, int64_t B, int64_t N, int64_t D, int64_t sB, int64_t sN,
+                       int64_t sD, const float* E, const float* ee, int64_t K, int training,
+                       float temp, const float* gumbel, const int64_t* seed_ptr, uint64_t offset,
+                       float* quant, int64_t* idx, int32_t* idx32, float* commit_partial,
+                       float* token_rows, tvq_stream_t stream);
 
 /* Per-code batch statistics, deterministic (no float atomics): a stable group-by
  * (counting sort) of idx32, then per-code row sums in row order.

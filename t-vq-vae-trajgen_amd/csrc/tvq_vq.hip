@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256, 2) void vq_assign_kernel(
     const float* __restrict__ x, int64_t M, int64_t N, int64_t sB, int64_t sN, int64_t sD,
     const float* __restrict__ E, const float* __restrict__ ee, int K, int training,
     float* __restrict__ quant, int64_t* __restrict__ idx, int32_t* __restrict__ idx32,
-    float* __restrict__ commit_partial, Svq sv) {
+    float* __restrict__ commit_partial, Svq sv, float* __restrict__ xt) {
   constexpr int S = D + 8;  // LDS row stride (floats): conflict-free ds_read_b128 B-fragments
   constexpr int NQ = D / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -206,8 +206,18 @@ __global__ __launch_bounds__(256, 2) void vq_assign_kernel(
       const float df = st - xv;
       csum = fmaf(df, df, csum);
       quant[off] = st;
+      if (xt) es[r * (D + 1) + d] = xv;  // the chunk buffer is free after the last barrier
     } else {
       quant[off] = qv;
+    }
+  }
+  if (training && xt) {
+    // token-major copy of the block's rows (row m at xt + m * D): the codebook statistics
+    // then sum contiguous rows instead of gathering D-strided NCHW elements
+    __syncthreads();
+    for (int e = tid; e < VQ_BM * D; e += 256) {
+      const int r = e / D, d = e - r * D;
+      if (row0 + r < M) xt[(row0 + r) * D + d] = es[r * (D + 1) + d];
     }
   }
   if (training && commit_partial) {
@@ -311,6 +321,17 @@ extern "C" int tvq_vq_assign_svq(const float* x, int64_t B, int64_t N, int64_t D
                                  const int64_t* seed_ptr, uint64_t offset, float* quant,
                                  int64_t* idx, int32_t* idx32, float* commit_partial,
                                  tvq_stream_t stream) {
+  return tvq_vq_assign_rows(x, B, N, D, sB, sN, sD, E, ee, K, training, temp, gumbel, seed_ptr,
+                            offset, quant, idx, idx32, commit_partial, nullptr, stream);
+}
+
+extern "C" int tvq_vq_assign_rows(const float* x, int64_t B, int64_t N, int64_t D, int64_t sB,
+                                  int64_t sN, int64_t sD, const float* E, const float* ee,
+                                  int64_t K, int training, float temp, const float* gumbel,
+                                  const int64_t* seed_ptr, uint64_t offset, float* quant,
+                                  int64_t* idx, int32_t* idx32, float* commit_partial,
+                                  float* token_rows, tvq_stream_t stream) {
+  float* xt = training ? token_rows : nullptr;
   TVQ_CHECK_ARG(x && E && ee && quant && idx && idx32 && B > 0 && N > 0 && K > 0,
                 "tvq_vq_assign: bad arguments");
   TVQ_CHECK_ARG(temp >= 0.f && (temp == 0.f || gumbel || seed_ptr),
@@ -328,11 +349,11 @@ extern "C" int tvq_vq_assign_svq(const float* x, int64_t B, int64_t N, int64_t D
     if (sv.temp > 0.f)                                                                       \
       hipLaunchKernelGGL((vq_assign_kernel<DD, true>), dim3(nb), dim3(256), lds, st, x, M, N,  \
                          sB, sN, sD, E, ee, (int)K, training, quant, idx, idx32,             \
-                         commit_partial, sv);                                                \
+                         commit_partial, sv, xt);                                            \
     else                                                                                     \
       hipLaunchKernelGGL((vq_assign_kernel<DD, false>), dim3(nb), dim3(256), lds, st, x, M, N, \
                          sB, sN, sD, E, ee, (int)K, training, quant, idx, idx32,             \
-                         commit_partial, sv);                                                \
+                         commit_partial, sv, xt);                                            \
     break;                                                                                   \
   }
   switch (D) {

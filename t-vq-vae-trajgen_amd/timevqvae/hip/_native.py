@@ -46,6 +46,8 @@ sig("tvq_vq_backward", P, P, P, P, I64, I64, P, P)
 U64 = ctypes.c_uint64
 sig("tvq_vq_assign_svq", P, I64, I64, I64, I64, I64, I64, P, P, I64, I32, F32, P, P, U64, P, P, P,
     P, P)
+sig("tvq_vq_assign_rows", P, I64, I64, I64, I64, I64, I64, P, P, I64, I32, F32, P, P, U64, P, P, P,
+    P, P, P)
 # --- STFT / iSTFT ------------------------------------------------------------
 sig("tvq_stft_encode", P, I64, I64, I64, P, P, P, P, P, P)
 sig("tvq_istft_decode", P, I64, I64, I64, I64, I64, P, P)

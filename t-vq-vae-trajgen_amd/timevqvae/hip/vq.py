@@ -99,17 +99,19 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
     nb = value("tvq_vq_assign_nblocks", M)
     partial = torch.empty(nb, device=dev, dtype=torch.float32) if straight_through else None
     sB, sN, sD = x.stride()
+    # EMA statistics sum token rows per code: with an NCHW latent (sD > 1) the assign pass
+    # also writes x token-major so that those sums read contiguous rows
+    rows = (torch.empty((M, D), device=dev, dtype=torch.float32)
+            if ema and straight_through and sD != 1 else None)
+    seed, off = None, 0
     if svq_temp:
         if gumbel is not None and (gumbel.shape != (M, K) or not gumbel.is_contiguous()):
             raise ValueError("vq: injected gumbel noise must be a contiguous (M, K) tensor")
         seed = rng.seed_tensor(dev) if gumbel is None else None
         off = rng.call_offset(_SVQ_SITE) if gumbel is None else 0
-        call("tvq_vq_assign_svq", ptr(x), B, N, D, sB, sN, sD, ptr(embed), ptr(ee), K,
-             int(bool(straight_through)), float(svq_temp), ptr(gumbel), ptr(seed), off,
-             ptr(out), ptr(idx), ptr(idx32), ptr(partial), s)
-    else:
-        call("tvq_vq_assign", ptr(x), B, N, D, sB, sN, sD, ptr(embed), ptr(ee), K,
-             int(bool(straight_through)), ptr(out), ptr(idx), ptr(idx32), ptr(partial), s)
+    call("tvq_vq_assign_rows", ptr(x), B, N, D, sB, sN, sD, ptr(embed), ptr(ee), K,
+         int(bool(straight_through)), float(svq_temp or 0.0), ptr(gumbel), ptr(seed), off,
+         ptr(out), ptr(idx), ptr(idx32), ptr(partial), ptr(rows), s)
     commit = None
     if straight_through:  # the loss reads it: stays on the current stream
         commit = torch.empty((), device=dev, dtype=torch.float32)
@@ -118,8 +120,9 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
     # per-code statistics, EMA and perplexity: nothing downstream of the quantised output
     # waits for them (inside streams.concurrent() they run on the aux stream; the region's
     # join completes them before anyone reads the perplexity or the codebook)
-    with streams.offload(x, idx32, kind="vq"):
-        counts, perp = _codebook_stats(x, idx32, embed, cluster_size, embed_avg, ema, decay,
+    src = rows.view(1, M, D) if rows is not None else x
+    with streams.offload(src, idx32, kind="vq"):
+        counts, perp = _codebook_stats(src, idx32, embed, cluster_size, embed_avg, ema, decay,
                                        eps, sync)
     return out, idx, commit, perp, counts
 
