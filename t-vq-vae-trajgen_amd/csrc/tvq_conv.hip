@@ -1664,6 +1664,135 @@ static void launch_tap(const float* in, const float* wt, float* out, const ConvG
 
 static int g_conv_t32 = 1;  // conv_t32_kernel enabled (tvq_conv_config bit 8 turns it off)
 
+// ---------------------------------------------------------------- direct 3x3 path
+// 3x3 stride-1 convolutions of narrow maps with >= 32 channels on both sides -- the LF
+// band's 64 / 128-channel convs on (256, C, 3, 8), 6,144 positions: the staged paths give
+// them 48-96 blocks (so split-K + an epilogue launch, 21 + 5 us per conv at 0.13 of the
+// fp32 MFMA peak).  Here a block owns a 32-channel x 32-position output tile and its 4
+// waves split the reduction by input-channel quarters (each wave: its C/4 channels for all
+// 9 taps), so the LF 64-channel convs run as 384 blocks of short MFMA chains with no LDS
+// staging: every operand goes global (L2) -> registers.  Per step a lane supplies one
+// packed weight w[tap][c][n0 + l % 32] (coalesced) and one gathered input value at its
+// position (zero outside the map); the wave runs one v_mfma_f32_32x32x2_f32 per 2
+// channels.  A tap's 2 * (C/8) loads are issued as one chunk ahead of the previous tap's
+// MFMAs.  The 4 partial tiles are added in LDS in the fixed order (w0 + w1) + (w2 + w3);
+// bias, dropout (the same counter hash) and residual as epi_store.  F: forward gather;
+// T: the data gradient of a stride-1 conv (flipped taps through the gather offsets).
+constexpr int D32_CPW = 32;  // max channels per wave (C <= 128)
+
+template <int MODE, int CW>
+__global__ __launch_bounds__(256) void conv_d32_kernel(const float* __restrict__ in,
+                                                       const float* __restrict__ wt,
+                                                       float* __restrict__ out, ConvGeom g,
+                                                       Epi e, int mtiles) {
+  __shared__ float red[4][16][64];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hl = lane >> 5;
+  const int mt = (int)blockIdx.x % mtiles, nt = (int)blockIdx.x / mtiles;
+  const int m0 = mt * 32, n0 = nt * 32;
+  // this lane's output position (B operand column) and output channel (A operand row)
+  const int m = m0 + r32;
+  const bool pv = m < g.Mpos;
+  const int mc = pv ? m : 0;
+  const uint32_t bh = fdiv((uint32_t)mc, g.fd_wo);
+  const int ww = mc - (int)bh * g.Wo;
+  const int b = (int)fdiv((uint32_t)mc, g.fd_hwo);
+  const int hh = (int)bh - b * g.Hout;
+  const int HW = g.Hin * g.Win;
+  const int c0 = wid * CW;  // this wave's input channels [c0, c0 + CW)
+  const float* inb = in + ((int64_t)b * g.C + c0 + hl) * HW;
+  const float* wl = wt + (int64_t)(c0 + hl) * g.wsc + min(n0 + r32, g.N - 1);
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  constexpr int ST = CW / 2;  // MFMA steps per tap
+  float fa[2][ST], fb[2][ST];
+  auto load = [&](int buf, int tap) {
+    const int kh = tap / 3, kw = tap - 3 * kh;
+    int hi, wi;
+    if (MODE == GATHER_F) {
+      hi = hh + kh - g.oph;
+      wi = ww + kw - g.opw;
+    } else {
+      hi = hh - kh + g.oph;
+      wi = ww - kw + g.opw;
+    }
+    const bool ok = pv && hi >= 0 && hi < g.Hin && wi >= 0 && wi < g.Win;
+    const int o = ok ? hi * g.Win + wi : 0;
+    const float* wtap = wl + (int64_t)tap * g.wst;
+#pragma unroll
+    for (int u = 0; u < ST; ++u) {
+      fa[buf][u] = wtap[(int64_t)(2 * u) * g.wsc];
+      const float v = inb[(int64_t)(2 * u) * HW + o];
+      fb[buf][u] = ok ? v : 0.f;
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    if (tap + 1 < 9) load((tap + 1) & 1, tap + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < ST; ++u)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tap & 1][u], fb[tap & 1][u], acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // partial tiles -> LDS; (w0 + w1) + (w2 + w3); thread t then owns tile elements
+  // t, t + 256, ... with the channel slowest (row-major [n][m]: the stores coalesce along m)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wid][r][lane] = acc[r];
+  __syncthreads();
+  const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
+  const int64_t hw = (int64_t)g.Hout * g.Wo;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int el = tid + 256 * q, nr = el >> 5, mr = el & 31;
+    // acc r of lane l: row (n) 8 (r / 4) + 4 (l / 32) + r % 4, column (m) l % 32
+    const int ln = mr + 32 * ((nr >> 2) & 1), r = (nr & 3) + 4 * (nr >> 3);
+    const float v0 = (red[0][r][ln] + red[1][r][ln]) + (red[2][r][ln] + red[3][r][ln]);
+    const int n = n0 + nr, mm = m0 + mr;
+    if (n >= g.N || mm >= g.Mpos) continue;
+    const uint32_t bh2 = fdiv((uint32_t)mm, g.fd_wo);
+    const int w2 = mm - (int)bh2 * g.Wo;
+    const int b2 = (int)fdiv((uint32_t)mm, g.fd_hwo);
+    const int h2 = (int)bh2 - b2 * g.Hout;
+    const int64_t o = (((int64_t)b2 * g.N + n) * g.Hout + h2) * g.Wo + w2;
+    float v = v0 + (e.bias ? e.bias[n] : 0.f);
+    if (e.drop_p > 0.f) v = uniform01(seed, (uint64_t)o) >= e.drop_p ? v * e.drop_scale : 0.f;
+    if (e.residual) v += e.residual[o];
+    out[o] = v;
+  }
+}
+
+// TVQ_CONV_D32=0 turns the direct 3x3 path off
+static int d32_on() {
+  static const int v = [] {
+    const char* s = getenv("TVQ_CONV_D32");
+    return s ? atoi(s) : 1;
+  }();
+  return v;
+}
+
+template <int MODE, int KH, int KW, int SW, bool REPL>
+static bool launch_d32(const float* in, const float* wt, float* out, const ConvGeom& g,
+                       const Epi& e, hipStream_t st) {
+  // off with the 32x32-MFMA tiles (tvq_conv_config bit 8: the tap kernel alone)
+  if (!(KH == 3 && KW == 3 && SW == 1 && !REPL) || !d32_on() || !g_conv_t32) return false;
+  if (g.wsn != 1 || g.N < 32 || g.C < 32 || g.C % 8 != 0 || g.C > 4 * D32_CPW) return false;
+  if (g.Hin != g.Hout || g.Win != g.Wo) return false;  // same-size maps (pad 1)
+  const int mtiles = (g.Mpos + 31) / 32, ntiles = (g.N + 31) / 32;
+  if ((int64_t)mtiles * ntiles > 4096) return false;  // wide maps: the staged / t32 paths
+  const unsigned grid = (unsigned)(mtiles * ntiles);
+  switch (g.C / 4) {
+    case 8: hipLaunchKernelGGL((conv_d32_kernel<MODE, 8>), dim3(grid), dim3(256), 0, st, in, wt, out, g, e, mtiles); return true;
+    case 16: hipLaunchKernelGGL((conv_d32_kernel<MODE, 16>), dim3(grid), dim3(256), 0, st, in, wt, out, g, e, mtiles); return true;
+    case 24: hipLaunchKernelGGL((conv_d32_kernel<MODE, 24>), dim3(grid), dim3(256), 0, st, in, wt, out, g, e, mtiles); return true;
+    case 32: hipLaunchKernelGGL((conv_d32_kernel<MODE, 32>), dim3(grid), dim3(256), 0, st, in, wt, out, g, e, mtiles); return true;
+    default: return false;
+  }
+}
+
 // staged GEMM; `slab` (nullable) enables split-K with splits*N*Mpos floats of partials
 template <int MODE, int KH, int KW, int SW, bool REPL>
 static void launch_gemm(const float* in, const float* wt, float* out, const ConvGeom& g,
@@ -1711,6 +1840,7 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
 #undef TVQ_T32
       return;
     }
+    if (launch_d32<MODE, KH, KW, SW, REPL>(in, wt, out, g, e, st)) return;
     int sps;
     const int splits = slab ? tap_splits(g, KH * KW, &sps) : 1;
     if (!slab) sps = KH * KW * ((g.C + 31) / 16);  // >= all K-steps
