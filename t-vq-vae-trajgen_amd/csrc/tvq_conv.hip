@@ -1664,28 +1664,28 @@ static void launch_tap(const float* in, const float* wt, float* out, const ConvG
 
 static int g_conv_t32 = 1;  // conv_t32_kernel enabled (tvq_conv_config bit 8 turns it off)
 
-// ---------------------------------------------------------------- direct 3x3 path
-// 3x3 stride-1 convolutions of narrow maps with >= 32 channels on both sides -- the LF
-// band's 64 / 128-channel convs on (256, C, 3, 8), 6,144 positions: the staged paths give
-// them 48-96 blocks (so split-K + an epilogue launch, 21 + 5 us per conv at 0.13 of the
-// fp32 MFMA peak).  Here a block owns a 32-channel x 32-position output tile and its 4
-// waves split the reduction by input-channel quarters (each wave: its C/4 channels for all
-// 9 taps), so the LF 64-channel convs run as 384 blocks of short MFMA chains with no LDS
+// ---------------------------------------------------------------- direct path
+// Convolutions of narrow maps with >= 32 channels on both sides -- the LF band's 64 /
+// 128-channel convs on (256, C, 3, 8), 6,144 positions, and their neighbours (the 1x1
+// projections, the 32 -> 64 EncBlock, the 64 -> 32 DecBlock): the staged paths give them
+// 48-96 blocks (so split-K + an epilogue launch, 21 + 5 us per 3x3 64-channel conv at 0.13
+// of the fp32 MFMA peak).  Here a block owns a 32-channel x 32-position output tile and its
+// NW waves split the reduction by input-channel ranges (each wave: its C / NW channels for
+// every tap), so the LF 64-channel convs run as 384 blocks of short MFMA chains with no LDS
 // staging: every operand goes global (L2) -> registers.  Per step a lane supplies one
 // packed weight w[tap][c][n0 + l % 32] (coalesced) and one gathered input value at its
-// position (zero outside the map); the wave runs one v_mfma_f32_32x32x2_f32 per 2
-// channels.  A tap's 2 * (C/8) loads are issued as one chunk ahead of the previous tap's
-// MFMAs.  The 4 partial tiles are added in LDS in the fixed order (w0 + w1) + (w2 + w3);
-// bias, dropout (the same counter hash) and residual as epi_store.  F: forward gather;
-// T: the data gradient of a stride-1 conv (flipped taps through the gather offsets).
-constexpr int D32_CPW = 32;  // max channels per wave (C <= 128)
-
-template <int MODE, int CW>
-__global__ __launch_bounds__(256) void conv_d32_kernel(const float* __restrict__ in,
-                                                       const float* __restrict__ wt,
-                                                       float* __restrict__ out, ConvGeom g,
-                                                       Epi e, int mtiles) {
-  __shared__ float red[4][16][64];
+// position (gather_in's index rules: zero / replicate padding, the stride-2 transposed
+// parity skip); the wave runs one v_mfma_f32_32x32x2_f32 per 2 channels.  A tap's loads are
+// issued as one chunk ahead of the previous tap's MFMAs.  The partial tiles are added in
+// LDS in a fixed pairwise order; bias, dropout (the same counter hash) and residual as
+// epi_store.  Replaced: split-K tap + epilogue, 6.12 -> 5.92 ms per joint step.
+template <int MODE, int KH, int KW, int SW, bool REPL, int CW, int NW>
+__global__ __launch_bounds__(64 * NW) void conv_d32_kernel(const float* __restrict__ in,
+                                                          const float* __restrict__ wt,
+                                                          float* __restrict__ out, ConvGeom g,
+                                                          Epi e, int mtiles) {
+  constexpr int KK = KH * KW;
+  __shared__ float red[NW][16][64];
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hl = lane >> 5;
@@ -1709,16 +1709,25 @@ __global__ __launch_bounds__(256) void conv_d32_kernel(const float* __restrict__
   constexpr int ST = CW / 2;  // MFMA steps per tap
   float fa[2][ST], fb[2][ST];
   auto load = [&](int buf, int tap) {
-    const int kh = tap / 3, kw = tap - 3 * kh;
+    const int kh = tap / KW, kw = tap - KW * kh;
     int hi, wi;
+    bool ok = pv;
     if (MODE == GATHER_F) {
       hi = hh + kh - g.oph;
-      wi = ww + kw - g.opw;
+      wi = ww * SW + kw - g.opw;
+      if (REPL) {
+        hi = hi < 0 ? 0 : (hi >= g.Hin ? g.Hin - 1 : hi);
+        wi = wi < 0 ? 0 : (wi >= g.Win ? g.Win - 1 : wi);
+      } else {
+        ok = ok && hi >= 0 && hi < g.Hin && wi >= 0 && wi < g.Win;
+      }
     } else {
       hi = hh - kh + g.oph;
-      wi = ww - kw + g.opw;
+      const int wn = ww - kw + g.opw;
+      ok = ok && hi >= 0 && hi < g.Hin && wn >= 0 && (SW == 1 || (wn & 1) == 0);
+      wi = wn / SW;
+      ok = ok && wi < g.Win;
     }
-    const bool ok = pv && hi >= 0 && hi < g.Hin && wi >= 0 && wi < g.Win;
     const int o = ok ? hi * g.Win + wi : 0;
     const float* wtap = wl + (int64_t)tap * g.wst;
 #pragma unroll
@@ -1730,27 +1739,33 @@ __global__ __launch_bounds__(256) void conv_d32_kernel(const float* __restrict__
   };
   load(0, 0);
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
-    if (tap + 1 < 9) load((tap + 1) & 1, tap + 1);
+  for (int tap = 0; tap < KK; ++tap) {
+    if (tap + 1 < KK) load((tap + 1) & 1, tap + 1);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < ST; ++u)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tap & 1][u], fb[tap & 1][u], acc, 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
-  // partial tiles -> LDS; (w0 + w1) + (w2 + w3); thread t then owns tile elements
-  // t, t + 256, ... with the channel slowest (row-major [n][m]: the stores coalesce along m)
+  // partial tiles -> LDS, summed pairwise ((w0 + w1) + (w2 + w3)) + ...; thread t then owns
+  // tile elements t, t + 64 NW, ... with the channel slowest (row-major [n][m]: the stores
+  // coalesce along m)
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[wid][r][lane] = acc[r];
   __syncthreads();
   const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
-  const int64_t hw = (int64_t)g.Hout * g.Wo;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int el = tid + 256 * q, nr = el >> 5, mr = el & 31;
+  for (int q = 0; q < 1024 / (64 * NW); ++q) {
+    const int el = tid + 64 * NW * q, nr = el >> 5, mr = el & 31;
     // acc r of lane l: row (n) 8 (r / 4) + 4 (l / 32) + r % 4, column (m) l % 32
     const int ln = mr + 32 * ((nr >> 2) & 1), r = (nr & 3) + 4 * (nr >> 3);
-    const float v0 = (red[0][r][ln] + red[1][r][ln]) + (red[2][r][ln] + red[3][r][ln]);
+    float part[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) part[w] = red[w][r][ln];
+#pragma unroll
+    for (int span = 1; span < NW; span *= 2)
+#pragma unroll
+      for (int w = 0; w + span < NW; w += 2 * span) part[w] += part[w + span];
     const int n = n0 + nr, mm = m0 + mr;
     if (n >= g.N || mm >= g.Mpos) continue;
     const uint32_t bh2 = fdiv((uint32_t)mm, g.fd_wo);
@@ -1758,39 +1773,60 @@ __global__ __launch_bounds__(256) void conv_d32_kernel(const float* __restrict__
     const int b2 = (int)fdiv((uint32_t)mm, g.fd_hwo);
     const int h2 = (int)bh2 - b2 * g.Hout;
     const int64_t o = (((int64_t)b2 * g.N + n) * g.Hout + h2) * g.Wo + w2;
-    float v = v0 + (e.bias ? e.bias[n] : 0.f);
+    float v = part[0] + (e.bias ? e.bias[n] : 0.f);
     if (e.drop_p > 0.f) v = uniform01(seed, (uint64_t)o) >= e.drop_p ? v * e.drop_scale : 0.f;
     if (e.residual) v += e.residual[o];
     out[o] = v;
   }
 }
 
-// TVQ_CONV_D32=0 turns the direct 3x3 path off
-static int d32_on() {
+// TVQ_CONV_D32: 0 off; otherwise the largest position count it takes (default 8192:
+// the narrow LF maps, 6,144 positions); TVQ_CONV_D32_NW: waves per block (4 or 8)
+static int d32_max_pos() {
   static const int v = [] {
     const char* s = getenv("TVQ_CONV_D32");
-    return s ? atoi(s) : 1;
+    return s ? (atoi(s) == 1 ? 8192 : atoi(s)) : 8192;
   }();
   return v;
+}
+static int d32_nw() {
+  static const int v = [] {
+    const char* s = getenv("TVQ_CONV_D32_NW");
+    return s ? atoi(s) : 4;
+  }();
+  return v;
+}
+
+template <int MODE, int KH, int KW, int SW, bool REPL, int NW>
+static bool launch_d32_nw(const float* in, const float* wt, float* out, const ConvGeom& g,
+                          const Epi& e, int mtiles, unsigned grid, hipStream_t st) {
+#define TVQ_D32(CWV)                                                                         \
+  hipLaunchKernelGGL((conv_d32_kernel<MODE, KH, KW, SW, REPL, CWV, NW>), dim3(grid),        \
+                     dim3(64 * NW), 0, st, in, wt, out, g, e, mtiles);                        \
+  return true;
+  switch (g.C / NW) {
+    case 4: if (NW == 8) { TVQ_D32(4) } return false;
+    case 8: TVQ_D32(8)
+    case 16: TVQ_D32(16)
+    case 24: TVQ_D32(24)
+    case 32: TVQ_D32(32)
+    default: return false;
+  }
+#undef TVQ_D32
 }
 
 template <int MODE, int KH, int KW, int SW, bool REPL>
 static bool launch_d32(const float* in, const float* wt, float* out, const ConvGeom& g,
                        const Epi& e, hipStream_t st) {
   // off with the 32x32-MFMA tiles (tvq_conv_config bit 8: the tap kernel alone)
-  if (!(KH == 3 && KW == 3 && SW == 1 && !REPL) || !d32_on() || !g_conv_t32) return false;
-  if (g.wsn != 1 || g.N < 32 || g.C < 32 || g.C % 8 != 0 || g.C > 4 * D32_CPW) return false;
-  if (g.Hin != g.Hout || g.Win != g.Wo) return false;  // same-size maps (pad 1)
+  if (!g_conv_t32 || g.Mpos > d32_max_pos()) return false;
+  if (g.wsn != 1 || g.N < 32 || g.C < 32 || g.C > 128) return false;
+  const int nw = d32_nw() == 8 ? 8 : 4;
+  if (g.C % (2 * nw) != 0) return false;
   const int mtiles = (g.Mpos + 31) / 32, ntiles = (g.N + 31) / 32;
-  if ((int64_t)mtiles * ntiles > 4096) return false;  // wide maps: the staged / t32 paths
   const unsigned grid = (unsigned)(mtiles * ntiles);
-  switch (g.C / 4) {
-    case 8: hipLaunchKernelGGL((conv_d32_kernel<MODE, 8>), dim3(grid), dim3(256), 0, st, in, wt, out, g, e, mtiles); return true;
-    case 16: hipLaunchKernelGGL((conv_d32_kernel<MODE, 16>), dim3(grid), dim3(256), 0, st, in, wt, out, g, e, mtiles); return true;
-    case 24: hipLaunchKernelGGL((conv_d32_kernel<MODE, 24>), dim3(grid), dim3(256), 0, st, in, wt, out, g, e, mtiles); return true;
-    case 32: hipLaunchKernelGGL((conv_d32_kernel<MODE, 32>), dim3(grid), dim3(256), 0, st, in, wt, out, g, e, mtiles); return true;
-    default: return false;
-  }
+  return nw == 8 ? launch_d32_nw<MODE, KH, KW, SW, REPL, 8>(in, wt, out, g, e, mtiles, grid, st)
+                 : launch_d32_nw<MODE, KH, KW, SW, REPL, 4>(in, wt, out, g, e, mtiles, grid, st);
 }
 
 // staged GEMM; `slab` (nullable) enables split-K with splits*N*Mpos floats of partials

@@ -522,6 +522,61 @@ def test_conv_paths_same_dropout_mask(Ci, Co, W, cuda):
     torch.testing.assert_close(outs[0], outs[2], rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("Ci,Co,KH,KW,SW,rep,W", [
+    (64, 64, 3, 3, 1, False, 8), (64, 128, 3, 3, 1, False, 8), (128, 128, 3, 3, 1, False, 8),
+    (128, 64, 3, 3, 1, False, 8), (64, 128, 1, 1, 1, False, 8), (128, 64, 1, 1, 1, False, 8),
+    (32, 64, 3, 4, 2, True, 16), (64, 32, 3, 3, 1, False, 8)])
+def test_conv_direct_narrow_maps(Ci, Co, KH, KW, SW, rep, W, cuda):
+    """The direct path (conv_d32_kernel) on the LF band's narrow-map shapes (B=64 of the
+    (256, C, 3, 8) maps): forward with bias, dropout and residual, and the data / weight
+    gradients, against torch fp32 on the CPU; the dropout mask equals the tap kernel's
+    (same counter hash at the same output index)."""
+    from timevqvae.hip.conv import conv2d
+    from timevqvae.hip._native import value
+    gen = torch.Generator().manual_seed(Ci * 7 + Co + KW)
+    B = 64
+    x = torch.randn(B, Ci, 3, W, generator=gen)
+    w = torch.randn(Co, Ci, KH, KW, generator=gen) * (Ci * KH * KW) ** -0.5
+    bias = torch.randn(Co, generator=gen)
+    pad = (0, 0) if rep else (KH // 2, (KW - 1) // 2)
+    xc = x.clone().requires_grad_(True)
+    wc = w.clone().requires_grad_(True)
+    bc = bias.clone().requires_grad_(True)
+    xpc = torch.nn.functional.pad(xc, (1, 1, 1, 1), mode="replicate") if rep else xc
+    yc = F.conv2d(xpc, wc, bc, stride=(1, SW), padding=pad)
+    g = torch.randn(yc.shape, generator=gen)
+    res = torch.randn(yc.shape, generator=gen)
+    yc.backward(g)
+    xd, wd, bd = (t.to(cuda).requires_grad_(True) for t in (x, w, bias))
+    yd = conv2d(xd, wd, bd, stride_w=SW, replicate=rep)
+    yd.backward(g.to(cuda))
+    close(yd, yc, what="fwd")
+    close(xd.grad, xc.grad, what="dx")
+    close(wd.grad, wc.grad, what="dw")
+    close(bd.grad, bc.grad, what="db")
+    # dropout + residual epilogue: same mask as the tap kernel (tvq_conv_config 8) at the
+    # same (seed, offset)
+    from timevqvae.hip._native import call, ptr, stream_ptr
+    seed = torch.tensor([4321], dtype=torch.int64, device=cuda)
+    nws = value("tvq_conv_workspace", 0, B, Ci, 3, W, Co, KH, KW, SW, int(rep))
+    ws = torch.empty(nws, device=cuda)
+    xg, wg, bg, rg = x.to(cuda), w.to(cuda), bias.to(cuda), res.to(cuda)
+    outs = []
+    prev = value("tvq_conv_config", -1)
+    try:
+        for cfg in (prev, 8):
+            value("tvq_conv_config", cfg)
+            y = torch.empty(res.shape, device=cuda)
+            call("tvq_conv2d_fwd", ptr(xg), B, Ci, 3, W, ptr(wg), ptr(bg), Co, KH, KW, SW, int(rep),
+                 ptr(y), ptr(rg), 0.3, ptr(seed), 99, ptr(ws), stream_ptr())
+            outs.append(y)
+    finally:
+        value("tvq_conv_config", prev)
+    r0 = res.to(cuda)
+    assert torch.equal(outs[0] == r0, outs[1] == r0)
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("op", ["fwd", "dgrad", "conv1d_fwd", "conv1d_dgrad", "fwd64", "dgrad64",
                                 "fwd128n", "dgrad128n"])
 def test_conv_wide_tile_matches_tap(op, cuda):

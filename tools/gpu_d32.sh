@@ -1,5 +1,5 @@
 #!/bin/bash
-# direct 3x3 conv: conv tests, step bench with / without it.
+# direct conv: conv tests, step bench A/B over TVQ_CONV_D32 (max positions) / _NW.
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -7,7 +7,7 @@ timeout -k 10 400 python -u -m pytest tests/test_ops_gpu.py tests/test_resblock.
   --timeout 120 --timeout-method thread > gpurun_out/d32_tests.log 2>&1 || { tail -30 gpurun_out/d32_tests.log; exit 1; }
 tail -2 gpurun_out/d32_tests.log
 STEPARGS="--no-sampler --no-roofline --no-config0 --no-cpu-baseline"
-for v in 1 0 1; do
-  TVQ_CONV_D32=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 $STEPARGS > gpurun_out/bench_d32_$v.log 2>&1 || { tail -20 gpurun_out/bench_d32_$v.log; exit 1; }
-  echo "d32=$v $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_d32_$v.log)"
+for v in ${D32_CASES:-"8192:4" "0:4" "8192:8" "32768:4"}; do
+  TVQ_CONV_D32=${v%%:*} TVQ_CONV_D32_NW=${v##*:} timeout -k 10 300 python bench.py --steps 30 --warmup 5 $STEPARGS > gpurun_out/bench_d32.log 2>&1 || { tail -20 gpurun_out/bench_d32.log; exit 1; }
+  echo "d32=$v $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_d32.log)"
 done
