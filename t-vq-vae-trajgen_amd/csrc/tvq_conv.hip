@@ -1675,8 +1675,8 @@ static int g_conv_t32 = 1;  // conv_t32_kernel enabled (tvq_conv_config bit 8 tu
 // staging: every operand goes global (L2) -> registers.  Per step a lane supplies one
 // packed weight w[tap][c][n0 + l % 32] (coalesced) and one gathered input value at its
 // position (gather_in's index rules: zero / replicate padding, the stride-2 transposed
-// parity skip); the wave runs one v_mfma_f32_32x32x2_f32 per 2 channels.  A tap's loads are
-// issued as one chunk ahead of the previous tap's MFMAs.  The partial tiles are added in
+// parity skip); the wave runs one v_mfma_f32_32x32x2_f32 per 2 channels.  Up to ~144
+// floats of loads (every tap of a 64-channel 3x3 conv) are in flight before the first MFMA.  The partial tiles are added in
 // LDS in a fixed pairwise order; bias, dropout (the same counter hash) and residual as
 // epi_store.  Replaced: split-K tap + epilogue, 6.12 -> 5.92 ms per joint step.
 template <int MODE, int KH, int KW, int SW, bool REPL, int CW, int NW>
@@ -1707,7 +1707,11 @@ __global__ __launch_bounds__(64 * NW) void conv_d32_kernel(const float* __restri
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   constexpr int ST = CW / 2;  // MFMA steps per tap
-  float fa[2][ST], fb[2][ST];
+  // PD taps' loads in flight (a ring of PD register buffers, ~144 floats): every tap of a
+  // 64-channel conv is requested before the first MFMA, so the block pays one L2 round
+  // trip instead of one per tap (9 x ~1 us with one tap of prefetch)
+  constexpr int PD0 = 144 / CW, PD = PD0 < 1 ? 1 : (PD0 > KK ? KK : PD0);
+  float fa[PD][ST], fb[PD][ST];
   auto load = [&](int buf, int tap) {
     const int kh = tap / KW, kw = tap - KW * kh;
     int hi, wi;
@@ -1737,15 +1741,16 @@ __global__ __launch_bounds__(64 * NW) void conv_d32_kernel(const float* __restri
       fb[buf][u] = ok ? v : 0.f;
     }
   };
-  load(0, 0);
+#pragma unroll
+  for (int t = 0; t < PD; ++t) load(t, t);
 #pragma unroll
   for (int tap = 0; tap < KK; ++tap) {
-    if (tap + 1 < KK) load((tap + 1) & 1, tap + 1);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < ST; ++u)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tap & 1][u], fb[tap & 1][u], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tap % PD][u], fb[tap % PD][u], acc, 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
+    if (tap + PD < KK) load(tap % PD, tap + PD);
   }
   // partial tiles -> LDS, summed pairwise ((w0 + w1) + (w2 + w3)) + ...; thread t then owns
   // tile elements t, t + 64 NW, ... with the channel slowest (row-major [n][m]: the stores
