@@ -1834,6 +1834,122 @@ static bool launch_d32(const float* in, const float* wt, float* out, const ConvG
                  : launch_d32_nw<MODE, KH, KW, SW, REPL, 4>(in, wt, out, g, e, mtiles, grid, st);
 }
 
+// Weight (+ bias) gradient of the same narrow-map convs (conv2d only): slab[z][n][k'] =
+// sum over split z's positions of dY[n][pos] X[c][pos + tap] (k' = c KK + tap; k' = Kred:
+// the bias column, X = 1).  A block owns a 32 (n) x 32 (k') tile of one split; its 4 waves
+// take quarters of the split's positions, each position pair one 32x32x2 MFMA step (lane
+// l: dY at channel n0 + l % 32 and X gathered at column k0 + l % 32, position 2 s + l / 32),
+// 16 steps' loads in flight ahead of the previous 16 steps' MFMAs.  Quarter tiles added in
+// LDS in the order (w0 + w1) + (w2 + w3); slabs summed in split order by wgrad_finish.
+// Measured slower than conv_wgrad_halo_kernel in the step (see tvq_conv2d_wgrad): off by
+// default, kept for A/B (TVQ_CONV_WD32=1).
+constexpr int WD32_KC = 16;
+
+template <int KH, int KW, int SW, bool REPL>
+__global__ __launch_bounds__(256) void conv_wgrad_d32_kernel(const float* __restrict__ dy,
+                                                             const float* __restrict__ x,
+                                                             float* __restrict__ slab, ConvGeom g,
+                                                             int pps, int kcols, int ntiles,
+                                                             int ctiles) {
+  constexpr int KK = KH * KW;
+  __shared__ float red[4][16][64];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hl = lane >> 5;
+  int bid = (int)blockIdx.x;
+  const int tc = bid % ctiles;
+  bid /= ctiles;
+  const int tn = bid % ntiles, z = bid / ntiles;
+  const int n0 = tn * 32, k0 = tc * 32;
+  // this lane's A row (output channel) and B column (c, tap) / bias / padding column
+  const int n = min(n0 + r32, g.N - 1);
+  const int col = k0 + r32;
+  const bool bias_col = col == g.Kred, real_col = col < g.Kred;
+  const int c = real_col ? col / KK : 0, tap = real_col ? col - (col / KK) * KK : 0;
+  const int dh = tap / KW - g.oph, dw = tap - (tap / KW) * KW - g.opw;
+  const int64_t HWo = (int64_t)g.Hout * g.Wo, HWi = (int64_t)g.Hin * g.Win;
+  const int q = pps >> 2;  // positions per wave (even)
+  const int pb = z * pps + wid * q, pe = min(g.Mpos, pb + q);
+  const int steps = pb < pe ? (pe - pb + 1) >> 1 : 0;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float fa[2][WD32_KC], fb[2][WD32_KC];
+  auto load = [&](int buf, int s0) {
+#pragma unroll
+    for (int u = 0; u < WD32_KC; ++u) {
+      const int pos = pb + 2 * (s0 + u) + hl;
+      const bool pv = pos < pe;
+      const int pc = pv ? pos : pb;
+      const uint32_t bh = fdiv((uint32_t)pc, g.fd_wo);
+      const int wo = pc - (int)bh * g.Wo;
+      const int b = (int)fdiv((uint32_t)pc, g.fd_hwo);
+      const int h = (int)bh - b * g.Hout;
+      const float av = dy[((int64_t)b * g.N + n) * HWo + (int64_t)h * g.Wo + wo];
+      int hi = h + dh, wi = wo * SW + dw;
+      bool ok = real_col;
+      if (REPL) {
+        hi = hi < 0 ? 0 : (hi >= g.Hin ? g.Hin - 1 : hi);
+        wi = wi < 0 ? 0 : (wi >= g.Win ? g.Win - 1 : wi);
+      } else {
+        ok = ok && hi >= 0 && hi < g.Hin && wi >= 0 && wi < g.Win;
+      }
+      const float xv = x[((int64_t)b * g.C + c) * HWi + (ok ? hi * g.Win + wi : 0)];
+      fa[buf][u] = pv ? av : 0.f;
+      fb[buf][u] = ok ? xv : (bias_col ? 1.f : 0.f);
+    }
+  };
+  const int nch = (steps + WD32_KC - 1) / WD32_KC;
+  if (nch > 0) load(0, 0);
+  for (int ch = 0; ch < nch; ch += 2) {
+    load(1, (ch + 1) * WD32_KC);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < WD32_KC; ++u)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[0][u], fb[0][u], acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (ch + 1 >= nch) break;
+    load(0, (ch + 2) * WD32_KC);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < WD32_KC; ++u)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[1][u], fb[1][u], acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wid][r][lane] = acc[r];
+  __syncthreads();
+  float* sz = slab + (int64_t)z * g.N * kcols;
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    const int el = tid + 256 * qq, nr = el >> 5, cr = el & 31;
+    const int ln = cr + 32 * ((nr >> 2) & 1), r = (nr & 3) + 4 * (nr >> 3);
+    const float v = (red[0][r][ln] + red[1][r][ln]) + (red[2][r][ln] + red[3][r][ln]);
+    const int nn = n0 + nr, cc = k0 + cr;
+    if (nn < g.N && cc < kcols) sz[(int64_t)nn * kcols + cc] = v;
+  }
+}
+
+static bool wd32_on() {
+  static const bool v = [] {
+    const char* e = getenv("TVQ_CONV_WD32");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
+// the direct weight gradient's split count (<= max_s, the workspace's slab count)
+static int wd32_splits(const ConvGeom& g, int kcols, int max_s, int* pps) {
+  const int tiles = ((g.N + 31) / 32) * ((kcols + 31) / 32);
+  int s = (768 + tiles / 2) / tiles;
+  if (s > max_s) s = max_s;
+  if (s < 1) s = 1;
+  int p = (g.Mpos + s - 1) / s;
+  p = (p + 7) / 8 * 8;
+  *pps = p;
+  return (g.Mpos + p - 1) / p;
+}
+
 // staged GEMM; `slab` (nullable) enables split-K with splits*N*Mpos floats of partials
 template <int MODE, int KH, int KW, int SW, bool REPL>
 static void launch_gemm(const float* in, const float* wt, float* out, const ConvGeom& g,
@@ -2345,9 +2461,31 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
   const int kcols = g.Kred + (db ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
   WHaloPlan pl;
-  if ((g_conv_halo & 2) && whalo_plan((int)B, (int)Ci, (int)H, (int)Wi, (int)Co, (int)H, (int)Wo,
-                                      (int)KH, (int)KW, (int)SW, PH_OF(KH), PW_OF(KW), kcols,
-                                      &pl)) {
+  const bool halo = (g_conv_halo & 2) && whalo_plan((int)B, (int)Ci, (int)H, (int)Wi, (int)Co,
+                                                    (int)H, (int)Wo, (int)KH, (int)KW, (int)SW,
+                                                    PH_OF(KH), PW_OF(KW), kcols, &pl);
+  // narrow maps with >= 32 channels: the direct kernel, into the slabs of the halo plan or
+  // of the split GEMM (the workspace holds either)
+  // (off by default: measured 6.06 vs 5.84 ms per joint step -- the per-step position
+  // decode and gather address math of every lane outweigh the MFMA; the halo kernel stages
+  // the image in LDS instead.  TVQ_CONV_WD32=1 turns it on.)
+  if (wd32_on() && g_conv_t32 && g.Mpos <= d32_max_pos() && Co >= 32 && Ci >= 8 &&
+      g.Kred >= 32) {
+    int gs, gpps;
+    wgrad_ws(Co, g.Kred, g.Mpos, &gs, &gpps);
+    int pps;
+    const int S = wd32_splits(g, kcols, halo && pl.S > gs ? pl.S : gs, &pps);
+    const int ntiles = (int)((Co + 31) / 32), ctiles = (kcols + 31) / 32;
+    const unsigned grid = (unsigned)(S * ntiles * ctiles);
+#define M_(a, b_, c, d)                                                                        \
+  hipLaunchKernelGGL((conv_wgrad_d32_kernel<a, b_, c, d>), dim3(grid), dim3(256), 0, st, dy, x, \
+                     workspace, g, pps, kcols, ntiles, ctiles);
+    TVQ_DISPATCH_KIND(kind, replicate, M_)
+#undef M_
+    wgrad_finish(workspace, S, Co, kcols, dw, db, (int)accumulate, st);
+    return launch_status("tvq_conv2d_wgrad(direct)");
+  }
+  if (halo) {
 #define M_(a, b_, c, d) launch_wgrad_halo<a, b_, c, d>(dy, x, workspace, pl, st);
     TVQ_DISPATCH_KIND(kind, replicate, M_)
 #undef M_
