@@ -306,6 +306,10 @@ __device__ __forceinline__ int value_of_chunk(const int* __restrict__ seg_start,
   return lo;
 }
 
+// The chunk's row indices are read once (lane r holds perm[r0 + r]) and broadcast by
+// shuffles, and 8 rows' loads are issued before any is added (in row order), so a chunk
+// costs ~4 memory round trips instead of 2 per row (perm -> row): 40 -> few us per call.
+template <int ND>
 __global__ __launch_bounds__(256) void seg_chunk_kernel(SegRows s, const int* __restrict__ offsets,
                                                         const int* __restrict__ perm,
                                                         const int* __restrict__ seg_start, int V,
@@ -316,28 +320,43 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegRows s, const int* __
   const int v = value_of_chunk(seg_start, V, c);
   const int r0 = offsets[v] + (c - seg_start[v]) * SEG_CH;
   const int r1 = min(offsets[v + 1], r0 + SEG_CH);
-  float acc[8];
+  const int n = r1 - r0;  // <= SEG_CH = 32 rows
+  const int pm = lane < n ? perm[r0 + lane] : 0;
+  float acc[ND];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  for (int i = 0; i < ND; ++i) acc[i] = 0.f;
   const bool drop = s.drop_p > 0.f && (int64_t)v != s.mask_id;
   const uint64_t seed = drop ? mix_seed(s.seed_ptr, s.offset) : 0ull;
   const float sc = drop ? 1.0f / (1.0f - s.drop_p) : 1.0f;
-  for (int r = r0; r < r1; ++r) {
-    const int64_t m = perm[r];
-    const int64_t b = m / s.N, n = m - b * s.N;
-    const float* row = s.src + b * s.sB + n * s.sN;
+  for (int rb = 0; rb < n; rb += 8) {
+    float x[8][ND];
+    int64_t mm[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int d = lane + 64 * i;
-      if (d < s.D) {
-        float x = row[(int64_t)d * s.sD];
-        if (drop) x = uniform01(seed, (uint64_t)(m * s.D + d)) >= s.drop_p ? x * sc : 0.f;
-        acc[i] += x;
+    for (int u = 0; u < 8; ++u) {
+      const int m = __shfl(pm, rb + u < n ? rb + u : 0, 64);
+      mm[u] = m;
+      const int64_t b = m / s.N, nn = m - b * s.N;
+      const float* row = s.src + b * s.sB + nn * s.sN;
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        const int d = lane + 64 * i;
+        x[u][i] = row[(int64_t)(d < s.D ? d : 0) * s.sD];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (rb + u >= n) break;
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        const int d = lane + 64 * i;
+        float xv = x[u][i];
+        if (drop) xv = uniform01(seed, (uint64_t)(mm[u] * s.D + d)) >= s.drop_p ? xv * sc : 0.f;
+        acc[i] += xv;
       }
     }
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < ND; ++i) {
     const int d = lane + 64 * i;
     if (d < s.D) part[(int64_t)c * s.D + d] = acc[i];
   }
@@ -383,8 +402,16 @@ int64_t seg_rowsum_scratch_floats(int64_t M, int64_t V, int64_t D) {
 void seg_rowsum(const SegRows& s, const int* offsets, const int* perm, const int* seg_start,
                 int64_t M, int64_t V, float* out, int accumulate, float* part, hipStream_t st) {
   const int max_chunks = (int)((M + SEG_CH - 1) / SEG_CH + V);
-  hipLaunchKernelGGL(seg_chunk_kernel, dim3((unsigned)((max_chunks + 3) / 4)), dim3(256), 0, st, s,
-                     offsets, perm, seg_start, (int)V, max_chunks, part);
+  const dim3 grid((unsigned)((max_chunks + 3) / 4));
+  if (s.D <= 64)
+    hipLaunchKernelGGL(seg_chunk_kernel<1>, grid, dim3(256), 0, st, s, offsets, perm, seg_start,
+                       (int)V, max_chunks, part);
+  else if (s.D <= 128)
+    hipLaunchKernelGGL(seg_chunk_kernel<2>, grid, dim3(256), 0, st, s, offsets, perm, seg_start,
+                       (int)V, max_chunks, part);
+  else
+    hipLaunchKernelGGL(seg_chunk_kernel<8>, grid, dim3(256), 0, st, s, offsets, perm, seg_start,
+                       (int)V, max_chunks, part);
   hipLaunchKernelGGL(seg_combine_kernel, dim3((unsigned)V), dim3(256), 0, st, part, seg_start, (int)V,
                      s.D, out, accumulate);
 }
