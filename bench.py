@@ -301,8 +301,8 @@ def _graph_time_us(fns, reps):
 
 
 def dominant_leg(device):
-    """The step's dominant kernel (profiles/r02e_step_kernel_stats.csv): wgrad_group_kernel,
-    the grouped weight gradient dW_i += dY_i^T X_i of every Linear of a prior, issued once
+    """The step's largest single launch (profiles/r02e_step_kernel_stats.csv): the grouped
+    weight gradient dW_i += dY_i^T X_i of every Linear of a prior, issued once
     at the end of its backward (timevqvae.hip.wgrad; 32x32x2 fp32 MFMA, 64x64 tiles, K =
     tokens split over 4 waves x S blocks) with its ordered slab sum wgrad_group_reduce_kernel
     (one op = these 2 launches).  Timed on the LF prior's set, accumulating into one flat
@@ -330,7 +330,7 @@ def dominant_leg(device):
     tpath = os.path.join(ROOT, "profiles", "r02e_dominant_traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath))["traffic_bytes"]
-    return {"bound": "mfma", "kernel": "wgrad_group_kernel + wgrad_group_reduce_kernel (grouped "
+    return {"bound": "mfma", "kernel": "wgrad_wide_kernel + wgrad_group_reduce_kernel (grouped "
                                        "weight gradients of the LF prior's 16 Linears, "
                                        "dW_i += dY_i^T X_i over 6400 tokens, fp32 MFMA)",
             "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -339,11 +339,48 @@ def dominant_leg(device):
             "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def conv_wgrad_leg(device):
+    """The step's top kernel by summed time (profiles/r02e_step_kernel_stats.csv:
+    conv_wgrad_halo_kernel<3,3,1>, 12 launches per step): the LF band's 64 -> 64 3x3 conv
+    weight (+ bias) gradient on (256, 64, 3, 8), dW[64][577] = sum over 6144 positions of
+    dY x im2col(X) -> 2 * 6144 * 64 * 577 = 453.8 MFLOP and 4 * (2 * 6144 * 64 + 64 * 577)
+    = 3.29 MB algorithmic per op (AI 138 FLOP/B: fp32 MFMA bound).  One op = the halo kernel
+    (per-image-range slabs) + its ordered slab sum (in the step the sum is batched at the
+    band's end; here it follows each op).  50 graph-replayed ops timed with HIP events."""
+    from timevqvae.hip._native import call, ptr, stream_ptr, value
+    B, C, H, W, Co = 256, 64, 3, 8, 64
+    x = torch.randn(B, C, H, W, device=device)
+    dy = torch.randn(B, Co, H, W, device=device)
+    dw = torch.zeros(Co, C, 3, 3, device=device)
+    db = torch.zeros(Co, device=device)
+    ws = torch.empty(value("tvq_conv_workspace", 4, B, C, H, W, Co, 3, 3, 1, 0), device=device)
+    fn = (lambda: call("tvq_conv2d_wgrad", ptr(x), B, C, H, W, ptr(dy), Co, W, 3, 3, 1, 0, ptr(dw),
+                       ptr(db), 1, ptr(ws), stream_ptr()))
+    with torch.no_grad():
+        us = _graph_time_us([fn], 50)
+    flops = 2.0 * B * H * W * Co * (C * 9 + 1)
+    byts = 4.0 * (2 * B * H * W * C + Co * (C * 9 + 1))
+    tf = flops / (us * 1e-6) / 1e12
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "r02e_wgrad_traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath))["traffic_bytes"]
+    return {"bound": "mfma", "kernel": "conv_wgrad_halo_kernel<3,3,1> + its ordered slab sum (LF "
+                                       "64->64 3x3 conv weight+bias gradient over 6144 positions, "
+                                       "fp32 MFMA)",
+            "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def roofline_leg(device, ms_per_step):
-    """bench JSON `roofline`: the step's dominant kernel (dominant_leg) at top level, the
-    whole step against the fp32 MFMA peak (`step`), and the largest single conv on MFMA
-    (`conv_t32`, conv_t32_leg)."""
-    out = dominant_leg(device)
+    """bench JSON `roofline`: the step's top kernel by summed time (conv_wgrad_leg) at top
+    level; the largest single launch of the step, the grouped Linear weight gradients of the
+    LF prior (`wgrad_group`, dominant_leg); the whole step against the fp32 MFMA peak
+    (`step`); the largest single conv on MFMA (`conv_t32`, conv_t32_leg)."""
+    out = conv_wgrad_leg(device)
+    out["wgrad_group"] = dominant_leg(device)
     tf = STEP_GFLOP / ms_per_step  # GFLOP / ms = TFLOP/s
     out["step"] = {"bound": "mfma", "gflop": STEP_GFLOP, "achieved": round(tf, 2),
                    "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",

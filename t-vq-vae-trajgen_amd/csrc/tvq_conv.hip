@@ -1393,13 +1393,20 @@ struct WHaloPlan {
   size_t lds;
 };
 
-static constexpr int64_t WHALO_SLAB_MAX = 4 << 20;  // floats
+// slab floats cap of the halo weight gradient (TVQ_WHALO_SLAB_MAX overrides, for A/B)
+static int64_t whalo_slab_max() {
+  static const int64_t v = [] {
+    const char* e = getenv("TVQ_WHALO_SLAB_MAX");
+    return e ? (int64_t)atoll(e) : (int64_t)(8 << 20);  // 8M: LF 64-ch leg 26 vs 30 us at 4M
+  }();
+  return v;
+}
 
 // split count depends only on (N, C, KK, B) so the workspace query can reproduce it
 static int whalo_splits(int64_t N, int64_t C, int KK, int64_t B, int nblk, int cblk) {
   const int64_t kc = C * KK + 1;
   int64_t S = 1024 / (nblk * cblk);
-  const int64_t cap = WHALO_SLAB_MAX / (N * kc);
+  const int64_t cap = whalo_slab_max() / (N * kc);
   if (S > cap) S = cap;
   if (S > B) S = B;
   if (S < 1) S = 1;

@@ -15,4 +15,7 @@ timeout -s KILL 90 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_IN
 if [ "$LEG" = dominant ]; then
   python tools/roof_traffic.py $O $O/traffic.json "grouped weight gradients of the LF prior (16 Linears, 6400 tokens): wgrad_wide_kernel + wgrad_group_reduce_kernel" wgrad_wide_kernel wgrad_group_reduce_kernel
 fi
+if [ "$LEG" = wgrad ]; then
+  python tools/roof_traffic.py $O $O/traffic.json "LF 64->64 3x3 conv weight+bias gradient over 6144 positions: conv_wgrad_halo_kernel + reduce_rows_kernel" conv_wgrad_halo_kernel reduce_rows_kernel
+fi
 echo roofline-done
