@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-end evidence: every -m gpu test, smoke(), the full bench line (all legs), a step-only
-# rocprofv3 kernel table, and the dominant-kernel roofline evidence (PMC traffic).
+# Round-end evidence: every -m gpu test, smoke(), the full bench line (all legs).
+# (profiles: tools/gpu_profiles.sh)
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -10,7 +10,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 grep "smoke ok" gpurun_out/smoke.log
 timeout -k 10 600 python bench.py > gpurun_out/bench_full.log 2>&1 || { tail -20 gpurun_out/bench_full.log; exit 1; }
 tail -1 gpurun_out/bench_full.log > gpurun_out/bench_full.json
-bash tools/gpu_step_prof.sh > gpurun_out/step_prof_out.txt 2>&1 || { tail -20 gpurun_out/step_prof_out.txt; exit 1; }
-grep "launches/step" gpurun_out/step_prof_out.txt
-LEG=dominant bash tools/gpu_roofline.sh > gpurun_out/roof_out.txt 2>&1 || { tail -20 gpurun_out/roof_out.txt; exit 1; }
 echo round-end-done
