@@ -59,6 +59,23 @@ def deferred_codebook_updates():
         _pending = prev
 
 
+_indices_only = [False]
+
+
+@contextlib.contextmanager
+def indices_only():
+    """Eval codebook passes in the body skip the per-code counts and the perplexity (their
+    group-by and reductions): for callers that read only the indices, such as MaskGIT's
+    frozen tokenizer (maskgit.py:117-134 discards the perplexity).  Training passes are
+    unaffected (their EMA needs the statistics)."""
+    prev = _indices_only[0]
+    _indices_only[0] = True
+    try:
+        yield
+    finally:
+        _indices_only[0] = prev
+
+
 def _same_dense_layout(a, b):
     return a.shape == b.shape and a.stride() == b.stride()
 
@@ -120,6 +137,8 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
     # per-code statistics, EMA and perplexity: nothing downstream of the quantised output
     # waits for them (inside streams.concurrent() they run on the aux stream; the region's
     # join completes them before anyone reads the perplexity or the codebook)
+    if _indices_only[0] and not ema:
+        return out, idx, commit, None, None
     src = rows.view(1, M, D) if rows is not None else x
     with streams.offload(src, idx32, kind="vq"):
         counts, perp = _codebook_stats(src, idx32, embed, cluster_size, embed_avg, ema, decay,

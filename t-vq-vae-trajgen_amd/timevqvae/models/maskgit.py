@@ -16,6 +16,7 @@ import torch.nn as nn
 from ..hip import rng, streams, wgrad
 from ..hip.sample import codebook_gather_nchw, mask_len, maskgit_remask, maskgit_sample
 from ..hip.signal import stft_encode
+from ..hip.vq import indices_only
 from ..hip.xf import mask_tokens, masked_cross_entropy
 from ..utils import freeze, quantize, zero_pad_high_freq, zero_pad_low_freq
 from .bidirectional_transformer import BidirectionalTransformer
@@ -103,11 +104,12 @@ class MaskGIT(nn.Module):
     def encode_tokens(self, x):
         """Both branches from one fused STFT pass: (s_l (b n), s_h (b m)) int64."""
         st = stft_encode(x, enc_l=True, enc_h=True)
-        with streams.branch(x.device) as br:  # HF encoder concurrently with LF
-            br.inputs(st)
-            _, s_h, _, _ = quantize(self.encoder_h.encode_timefreq(st["enc_h"]), self.vq_model_h)
-            br.outputs(s_h)
-        _, s_l, _, _ = quantize(self.encoder_l.encode_timefreq(st["enc_l"]), self.vq_model_l)
+        with indices_only():  # the tokens only: no per-code counts / perplexity launches
+            with streams.branch(x.device) as br:  # HF encoder concurrently with LF
+                br.inputs(st)
+                _, s_h, _, _ = quantize(self.encoder_h.encode_timefreq(st["enc_h"]), self.vq_model_h)
+                br.outputs(s_h)
+            _, s_l, _, _ = quantize(self.encoder_l.encode_timefreq(st["enc_l"]), self.vq_model_l)
         br.join()
         return s_l, s_h
 

@@ -173,7 +173,7 @@ class VectorQuantize(nn.Module):
                 vq_loss["loss"] = torch.zeros(1, device=device).requires_grad_(True)
             else:  # eval: a shared constant zero (no fill launch per call; never written)
                 vq_loss["loss"] = _eval_zero(device)
-        cb.perplexity = perp.detach()
+        cb.perplexity = perp.detach() if perp is not None else None
         if not self.channel_last and not self.accept_image_fmap:
             quantize = quantize.transpose(1, 2)
         if self.accept_image_fmap:
