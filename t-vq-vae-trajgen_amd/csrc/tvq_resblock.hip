@@ -29,6 +29,8 @@
 // loads (image, weights, per-channel parameters, epilogue operands) before it waits on
 // any.  Arithmetic is the unfused kernels' (Snake, BN affine / backward formulas, dropout
 // hash) up to the summation order.
+#include <algorithm>
+
 #include "tvq_bn.h"
 #include "tvq_common.h"
 #include "tvq_conv_internal.h"
@@ -325,10 +327,12 @@ __device__ __forceinline__ void rb_channel_partials(double (&s)[NS][3][4], const
 template <class R>
 __global__ __launch_bounds__(RB_T) void rb_fwd1_kernel(RBArgs a) {
   extern __shared__ double rb_smem[];
-  double* red = rb_smem;                                     // [NR][4][64][4][2]
-  float* prm = reinterpret_cast<float*>(red + R::NR * 1024 * 2);  // a1 | b1
+  float* prm = reinterpret_cast<float*>(rb_smem);  // a1 | b1
   float* S = prm + 2 * R::CT;
   float* A = S + R::PLANE;
+  // the channel-partial staging [NR][4][64][4][2] doubles reuses the S / A region once
+  // the conv is done (rb_lds: the max of the two, not their sum -> more blocks per CU)
+  double* red = reinterpret_cast<double*>(S);
   const int b = blockIdx.x, l = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t img0 = (int64_t)b * R::C * R::P;
   RB_MARK(0);
@@ -370,6 +374,7 @@ __global__ __launch_bounds__(RB_T) void rb_fwd1_kernel(RBArgs a) {
     }
   }
   RB_MARK(4);
+  __syncthreads();  // every wave's S / A reads are done before red overwrites them
   rb_channel_partials<R, 2>(s, tl, red, a.B, b, a.part);
   RB_MARK(5);
   if (a.cnt && last_block(a.cnt, a.B))
@@ -515,11 +520,11 @@ __global__ __launch_bounds__(RB_T) void rb_eval_kernel(RBArgs a) {
 template <class R>
 __global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
   extern __shared__ double rb_smem[];
-  double* red = rb_smem;                                     // [NR][4][64][4][3]
-  float* prm = reinterpret_cast<float*>(red + R::NR * 1024 * 3);  // a2|scale|shift|mean|invstd
-  float* G = prm + 5 * R::CT;                                   // g2 planes
-  float* S = G + R::PLANE;                                      // s2 planes
-  float* A = S + R::PLANE;                                      // transposed w2
+  float* prm = reinterpret_cast<float*>(rb_smem);  // a2|scale|shift|mean|invstd
+  float* G = prm + 5 * R::CT;                      // g2 planes
+  float* S = G + R::PLANE;                         // s2 planes
+  float* A = S + R::PLANE;                         // transposed w2
+  double* red = reinterpret_cast<double*>(G);      // [NR][4][64][4][3], after the convs
   const int b = blockIdx.x, l = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t img0 = (int64_t)b * R::C * R::P;
   RB_MARK(0);
@@ -591,6 +596,7 @@ __global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
     }
   }
   RB_MARK(5);
+  __syncthreads();  // G / S / A reads done before red overwrites them
   rb_channel_partials<R, 3>(s, tl, red, a.B, b, a.part);
   RB_MARK(6);
   if (a.cnt && last_block(a.cnt, a.B))
@@ -601,11 +607,11 @@ __global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
 template <class R>
 __global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
   extern __shared__ double rb_smem[];
-  double* red = rb_smem;                                     // [NR][4][64][4][1]
-  float* prm = reinterpret_cast<float*>(red + R::NR * 1024);  // a1|mean|invstd|w|mds|mdsx
-  float* G = prm + 6 * R::CT;                               // dh planes
-  float* S = G + R::PLANE;                                  // s1 planes
-  float* A = S + R::PLANE;                                  // transposed w1
+  float* prm = reinterpret_cast<float*>(rb_smem);  // a1|mean|invstd|w|mds|mdsx
+  float* G = prm + 6 * R::CT;                      // dh planes
+  float* S = G + R::PLANE;                         // s1 planes
+  float* A = S + R::PLANE;                         // transposed w1
+  double* red = reinterpret_cast<double*>(G);      // [NR][4][64][4][1], after the convs
   const int b = blockIdx.x;
   const int64_t img0 = (int64_t)b * R::C * R::P;
   float vd[R::UE], vh[R::UE], vx[R::UE];
@@ -671,6 +677,7 @@ __global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
       s[0][f][r] = (double)(gs * inv_a * t * xv) - (double)(gs * (sn * sn) * inv_a * inv_a);
     }
   }
+  __syncthreads();  // G / S / A reads done before red overwrites them
   rb_channel_partials<R, 1>(s, tl, red, a.B, b, a.part1);
   if (a.cnt && last_block(a.cnt, a.B) && threadIdx.x < 64)
     for (int c = 0; c < R::C; ++c)
@@ -682,11 +689,13 @@ template <class R>
 static size_t rb_lds(int kind) {
   const size_t CT = R::CT, PL = R::PLANE, PA = R::PANEL, RD = (size_t)R::NR * 1024 * 8;
   switch (kind) {
-    case 0: return 2 * RD + 4 * (2 * CT + PL + PA);         // fwd1
-    case 1: return 4 * (4 * CT + PL + PA);                  // fwd2
-    case 2: return 4 * (6 * CT + 2 * PL + 2 * PA);          // eval
-    case 3: return 3 * RD + 4 * (5 * CT + 2 * PL + PA);     // bwd2
-    default: return RD + 4 * (6 * CT + 2 * PL + PA);        // bwd1
+    // fwd1 / bwd2 / bwd1: the double channel-partial staging (n RD) aliases the conv
+    // region that follows the per-channel parameters
+    case 0: return 4 * 2 * CT + std::max(2 * RD, 4 * (PL + PA));       // fwd1
+    case 1: return 4 * (4 * CT + PL + PA);                              // fwd2
+    case 2: return 4 * (6 * CT + 2 * PL + 2 * PA);                      // eval
+    case 3: return 4 * 5 * CT + std::max(3 * RD, 4 * (2 * PL + PA));   // bwd2
+    default: return 4 * 6 * CT + std::max(RD, 4 * (2 * PL + PA));      // bwd1
   }
 }
 
