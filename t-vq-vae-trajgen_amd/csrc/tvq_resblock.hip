@@ -448,8 +448,8 @@ __global__ __launch_bounds__(RB_T) void rb_eval_kernel(RBArgs a) {
   float* prm = reinterpret_cast<float*>(rb_smem);  // a1 | b1 | scale | shift | a2 | b2
   float* S1 = prm + 6 * R::CT;
   float* S2 = S1 + R::PLANE;
-  float* A1 = S2 + R::PLANE;
-  float* A2 = A1 + R::PANEL;
+  float* A1 = S2 + R::PLANE;  // conv1's panel, then conv2's (one panel of LDS: more blocks
+                              // per CU; conv2's weights wait in registers meanwhile)
   const int b = blockIdx.x;
   const int64_t img0 = (int64_t)b * R::C * R::P;
   float v[R::UE];
@@ -481,7 +481,6 @@ __global__ __launch_bounds__(RB_T) void rb_eval_kernel(RBArgs a) {
   rb_border<R>(S1);
   rb_border<R>(S2);
   rb_put_panel<R>(A1, pv1);
-  rb_put_panel<R>(A2, pv2);
   __syncthreads();
   rb_put_img<R>(S1, v, v, [&](int c, int, float x, float) {
     const float al = prm[c];
@@ -503,8 +502,10 @@ __global__ __launch_bounds__(RB_T) void rb_eval_kernel(RBArgs a) {
       }
     }
   }
+  __syncthreads();  // S2 complete; every wave is done reading conv1's panel
+  rb_put_panel<R>(A1, pv2);
   __syncthreads();
-  rb_mma<R, false>(A2, S2, tl, acc);
+  rb_mma<R, false>(A1, S2, tl, acc);
 #pragma unroll
   for (int f = 0; f < 3; ++f) {
     if (f >= tl.nt) continue;
@@ -693,7 +694,7 @@ static size_t rb_lds(int kind) {
     // region that follows the per-channel parameters
     case 0: return 4 * 2 * CT + std::max(2 * RD, 4 * (PL + PA));       // fwd1
     case 1: return 4 * (4 * CT + PL + PA);                              // fwd2
-    case 2: return 4 * (6 * CT + 2 * PL + 2 * PA);                      // eval
+    case 2: return 4 * (6 * CT + 2 * PL + PA);                          // eval
     case 3: return 4 * 5 * CT + std::max(3 * RD, 4 * (2 * PL + PA));   // bwd2
     default: return 4 * 6 * CT + std::max(RD, 4 * (2 * PL + PA));      // bwd1
   }
