@@ -1,9 +1,10 @@
 // VQ codebook kernels (K7/K8/K9 in SURVEY.md §2.2) for gfx950.
 //
-// assign: 32 token rows per 256-thread workgroup.  Each wave keeps its 16 rows'
+// assign: 64 token rows per 512-thread workgroup.  Each wave keeps its 16 rows'
 // x values in registers as fp32 MFMA A-fragments (D/4 VGPRs) for the whole
-// launch and streams the codebook through LDS in 128-code chunks; waves 0/1 own
-// code columns [0,64) of every chunk, waves 2/3 columns [64,128).  x.E^T runs on
+// launch and streams the codebook through LDS in 128-code chunks; waves 0-3 own
+// code columns [0,64) of every chunk, waves 4-7 columns [64,128).  (32-row blocks
+// streamed the whole codebook through LDS twice as often per token row.)  x.E^T runs on
 // v_mfma_f32_16x16x4_f32 (exact fp32 FMA chains); the argmin is a running
 // per-lane (value, index) pair merged across the 16 code lanes by shuffles and
 // across the two code halves through LDS.  The epilogue gathers q = E[idx],
@@ -16,7 +17,8 @@
 
 namespace tvq {
 
-constexpr int VQ_BM = 32;   // token rows per workgroup
+constexpr int VQ_BM = 64;   // token rows per workgroup
+constexpr int VQ_T = 512;   // threads: 4 row groups of 16 x 2 code halves
 constexpr int VQ_CK = 128;  // codes per LDS chunk
 
 // (v, i) "better" for argmin of t with first-index tie break
@@ -69,7 +71,7 @@ __device__ __forceinline__ float gumbel_at(const Svq& sv, uint64_t seed, int64_t
 }
 
 template <int D, bool STOCH>
-__global__ __launch_bounds__(256, 2) void vq_assign_kernel(
+__global__ __launch_bounds__(VQ_T) void vq_assign_kernel(
     const float* __restrict__ x, int64_t M, int64_t N, int64_t sB, int64_t sN, int64_t sD,
     const float* __restrict__ E, const float* __restrict__ ee, int K, int training,
     float* __restrict__ quant, int64_t* __restrict__ idx, int32_t* __restrict__ idx32,
@@ -81,10 +83,10 @@ __global__ __launch_bounds__(256, 2) void vq_assign_kernel(
   float* xx_s = smem + VQ_CK * S;         // [VQ_BM]
   float* bv_s = xx_s + VQ_BM;             // [2][VQ_BM]
   int* bi_s = (int*)(bv_s + 2 * VQ_BM);   // [2][VQ_BM]
-  float* red = (float*)(bi_s + 2 * VQ_BM);  // [4]
+  float* red = (float*)(bi_s + 2 * VQ_BM);  // [8]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int rg = wid & 1, ch = wid >> 1;
+  const int rg = wid & 3, ch = wid >> 2;
   const int r16 = lane & 15, g = lane >> 4;
   const int64_t row0 = (int64_t)blockIdx.x * VQ_BM;
 
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(256, 2) void vq_assign_kernel(
   for (int c0 = 0; c0 < K; c0 += VQ_CK) {
     __syncthreads();  // previous chunk consumed (and xx_s visible on first pass)
     // stage codebook chunk [c0, c0+VQ_CK) into LDS (float4, coalesced along d)
-    for (int e = tid; e < VQ_CK * (D / 4); e += 256) {
+    for (int e = tid; e < VQ_CK * (D / 4); e += VQ_T) {
       const int c = e / (D / 4), d4 = e - c * (D / 4);
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (c0 + c < K) v = *reinterpret_cast<const float4*>(E + (int64_t)(c0 + c) * D + 4 * d4);
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(256, 2) void vq_assign_kernel(
   // epilogue: q = E[idx] (pre-update codebook); straight-through value; commit partial
   float csum = 0.f;
   const bool dfast = (sD == 1);
-  for (int e = tid; e < VQ_BM * D; e += 256) {
+  for (int e = tid; e < VQ_BM * D; e += VQ_T) {
     int r, d;
     if (dfast) { r = e / D; d = e - r * D; } else { d = e / VQ_BM; r = e - d * VQ_BM; }
     const int64_t m = row0 + r;
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(256, 2) void vq_assign_kernel(
     // token-major copy of the block's rows (row m at xt + m * D): the codebook statistics
     // then sum contiguous rows instead of gathering D-strided NCHW elements
     __syncthreads();
-    for (int e = tid; e < VQ_BM * D; e += 256) {
+    for (int e = tid; e < VQ_BM * D; e += VQ_T) {
       const int r = e / D, d = e - r * D;
       if (row0 + r < M) xt[(row0 + r) * D + d] = es[r * (D + 1) + d];
     }
@@ -224,7 +226,9 @@ __global__ __launch_bounds__(256, 2) void vq_assign_kernel(
     csum = wave_sum(csum);
     if (lane == 0) red[wid] = csum;
     __syncthreads();
-    if (tid == 0) commit_partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (tid == 0)
+      commit_partial[blockIdx.x] = ((red[0] + red[1]) + (red[2] + red[3])) +
+                                   ((red[4] + red[5]) + (red[6] + red[7]));
   }
 }
 
@@ -340,18 +344,18 @@ extern "C" int tvq_vq_assign_rows(const float* x, int64_t B, int64_t N, int64_t 
   TVQ_CHECK_ARG(K < INT_MAX, "tvq_vq_assign: K too large");
   const int64_t M = B * N;
   const int64_t nb = tvq_vq_assign_nblocks(M);
-  const size_t lds_tail = (VQ_BM + 4 * VQ_BM) * 4 + 16;
+  const size_t lds_tail = (VQ_BM + 4 * VQ_BM) * 4 + 32;
   hipStream_t st = (hipStream_t)stream;
   const Svq sv = {temp, gumbel, seed_ptr, offset};
 #define TVQ_ASSIGN(DD)                                                                       \
   case DD: {                                                                                 \
     const size_t lds = (size_t)VQ_CK * (DD + 8) * 4 + lds_tail;                              \
     if (sv.temp > 0.f)                                                                       \
-      hipLaunchKernelGGL((vq_assign_kernel<DD, true>), dim3(nb), dim3(256), lds, st, x, M, N,  \
+      hipLaunchKernelGGL((vq_assign_kernel<DD, true>), dim3(nb), dim3(VQ_T), lds, st, x, M, N, \
                          sB, sN, sD, E, ee, (int)K, training, quant, idx, idx32,             \
                          commit_partial, sv, xt);                                            \
     else                                                                                     \
-      hipLaunchKernelGGL((vq_assign_kernel<DD, false>), dim3(nb), dim3(256), lds, st, x, M, N, \
+      hipLaunchKernelGGL((vq_assign_kernel<DD, false>), dim3(nb), dim3(VQ_T), lds, st, x, M, N,\
                          sB, sN, sD, E, ee, (int)K, training, quant, idx, idx32,             \
                          commit_partial, sv, xt);                                            \
     break;                                                                                   \
