@@ -77,6 +77,73 @@ __global__ void rmsnorm_bwd_kernel(const float* __restrict__ dy, const float* __
   }
 }
 
+// The same backward with each row held in registers (D <= 64 ND): a wave loads its next
+// row while it reduces and stores the current one (the loop above pays two dependent
+// load round trips per row).  Every sum has the loop above's order: bitwise equal.
+template <int ND>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_reg_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, int64_t M, int D,
+    const float* __restrict__ g, float scale, const float* __restrict__ inv_norm,
+    const float* __restrict__ dres, float* __restrict__ dx, float* __restrict__ dg_part,
+    int rows_per_block) {
+  extern __shared__ float sh[];  // [waves][D] partial dg
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int d = threadIdx.x; d < nw * D; d += blockDim.x) sh[d] = 0.f;
+  float gv[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) gv[j] = lane + 64 * j < D ? g[lane + 64 * j] : 0.f;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  float cx[ND], cg[ND], cr[ND], nx[ND], ng[ND], nr[ND];
+  float cinv = 0.f, ninv = 0.f;
+  auto load = [&](int64_t row, float(&xv)[ND], float(&gvv)[ND], float(&rv)[ND], float& inv) {
+    const int64_t rr = row < r1 ? row : r0;  // past the block's rows: a valid row, unused
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int d = lane + 64 * j;
+      const int64_t o = rr * D + (d < D ? d : 0);
+      xv[j] = x[o];
+      gvv[j] = dy[o];
+      rv[j] = dres ? dres[o] : 0.f;
+    }
+    inv = inv_norm[rr];
+  };
+  int64_t row = r0 + wid;
+  if (row < r1) load(row, cx, cg, cr, cinv);
+  for (; row < r1; row += nw) {
+    load(row + nw, nx, ng, nr, ninv);
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < ND; ++j)
+      if (lane + 64 * j < D) dot += cg[j] * gv[j] * cx[j];
+    dot = wave_sum(dot);
+    const float c = dot * scale * cinv * cinv * cinv;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int d = lane + 64 * j;
+      if (d < D) {
+        const float v = cg[j] * gv[j] * scale * cinv - cx[j] * c;
+        dx[row * D + d] = dres ? v + cr[j] : v;
+        sh[wid * D + d] += cg[j] * cx[j] * cinv * scale;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      cx[j] = nx[j];
+      cg[j] = ng[j];
+      cr[j] = nr[j];
+    }
+    cinv = ninv;
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int w = 0; w < nw; ++w) s += sh[w * D + d];
+    dg_part[(int64_t)blockIdx.x * D + d] = s;
+  }
+}
+
 // out[d] (+)= sum_p part[p][d]
 __global__ void colsum_kernel(const float* __restrict__ part, int P, int D, float* __restrict__ out,
                               int accumulate) {
@@ -597,8 +664,19 @@ extern "C" int tvq_rmsnorm_bwd(const float* dy, const float* x, int64_t M, int64
   const int rpb = norm_rows_per_block(M);
   const int nb = (int)((M + rpb - 1) / rpb);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(nb), dim3(256), 4 * D * sizeof(float), st, dy, x, M,
-                     (int)D, g, scale, inv_norm, dres, dx, workspace, rpb);
+  const size_t lds = 4 * D * sizeof(float);
+  if (D <= 64)
+    hipLaunchKernelGGL(rmsnorm_bwd_reg_kernel<1>, dim3(nb), dim3(256), lds, st, dy, x, M, (int)D, g,
+                       scale, inv_norm, dres, dx, workspace, rpb);
+  else if (D <= 128)
+    hipLaunchKernelGGL(rmsnorm_bwd_reg_kernel<2>, dim3(nb), dim3(256), lds, st, dy, x, M, (int)D, g,
+                       scale, inv_norm, dres, dx, workspace, rpb);
+  else if (D <= 256)
+    hipLaunchKernelGGL(rmsnorm_bwd_reg_kernel<4>, dim3(nb), dim3(256), lds, st, dy, x, M, (int)D, g,
+                       scale, inv_norm, dres, dx, workspace, rpb);
+  else
+    hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(nb), dim3(256), lds, st, dy, x, M, (int)D, g, scale,
+                       inv_norm, dres, dx, workspace, rpb);
   reduce_rows(workspace, nb, D, D, dg, nullptr, 0, (int)accumulate, workspace + (int64_t)nb * 2 * D,
               st);
   return launch_status("tvq_rmsnorm_bwd");
