@@ -225,6 +225,85 @@ __global__ void layernorm_bwd_kernel(const float* __restrict__ dy, const float* 
   }
 }
 
+// The same backward with each row in registers (D <= 64 ND) and the next row loading
+// while the current one reduces; the sums keep the loop above's order (bitwise equal).
+template <int ND>
+__global__ __launch_bounds__(256) void layernorm_bwd_reg_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, int64_t M, int D,
+    const float* __restrict__ gamma, const float* __restrict__ mean,
+    const float* __restrict__ rstd, float* __restrict__ dx, float* __restrict__ part,
+    int rows_per_block) {
+  extern __shared__ float sh[];  // [waves][2][D]: dgamma, dbeta partials
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int d = threadIdx.x; d < nw * 2 * D; d += blockDim.x) sh[d] = 0.f;
+  float gm[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    const int d = lane + 64 * j;
+    gm[j] = gamma && d < D ? gamma[d] : 1.f;
+  }
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  float cx[ND], cg[ND], nx[ND], ng[ND];
+  float cmu = 0.f, crs = 0.f, nmu = 0.f, nrs = 0.f;
+  auto load = [&](int64_t row, float(&xv)[ND], float(&gv)[ND], float& mu, float& rs) {
+    const int64_t rr = row < r1 ? row : r0;  // past the block's rows: a valid row, unused
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int d = lane + 64 * j;
+      const int64_t o = rr * D + (d < D ? d : 0);
+      xv[j] = x[o];
+      gv[j] = dy[o];
+    }
+    mu = mean[rr];
+    rs = rstd[rr];
+  };
+  int64_t row = r0 + wid;
+  if (row < r1) load(row, cx, cg, cmu, crs);
+  for (; row < r1; row += nw) {
+    load(row + nw, nx, ng, nmu, nrs);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int d = lane + 64 * j;
+      if (d < D) {
+        const float xh = (cx[j] - cmu) * crs;
+        const float gg = cg[j] * gm[j];
+        s1 += gg;
+        s2 += gg * xh;
+        sh[(wid * 2) * D + d] += cg[j] * xh;
+        sh[(wid * 2 + 1) * D + d] += cg[j];
+      }
+    }
+    s1 = wave_sum(s1) / (float)D;
+    s2 = wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int d = lane + 64 * j;
+      if (d < D) {
+        const float xh = (cx[j] - cmu) * crs;
+        const float gg = cg[j] * gm[j];
+        dx[row * D + d] = crs * (gg - s1 - xh * s2);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      cx[j] = nx[j];
+      cg[j] = ng[j];
+    }
+    cmu = nmu;
+    crs = nrs;
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < 2 * D; d += blockDim.x) {
+    const int k = d / D, dd = d - k * D;
+    float s = 0.f;
+    for (int w = 0; w < nw; ++w) s += sh[(w * 2 + k) * D + dd];
+    part[((int64_t)blockIdx.x * 2 + k) * D + dd] = s;
+  }
+}
+
 // dgamma[d] (+)= sum_p ws[p][0][d], dbeta[d] (+)= sum_p ws[p][1][d]
 __global__ void ln_colsum2_kernel(const float* __restrict__ ws, int P, int D,
                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
@@ -699,8 +778,19 @@ extern "C" int tvq_layernorm_bwd(const float* dy, const float* x, int64_t M, int
   const int rpb = norm_rows_per_block(M);
   const int nb = (int)((M + rpb - 1) / rpb);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nb), dim3(256), 8 * D * sizeof(float), st, dy, x, M,
-                     (int)D, gamma, mean, rstd, dx, workspace, rpb);
+  const size_t lds = 8 * D * sizeof(float);
+  if (D <= 64)
+    hipLaunchKernelGGL(layernorm_bwd_reg_kernel<1>, dim3(nb), dim3(256), lds, st, dy, x, M, (int)D,
+                       gamma, mean, rstd, dx, workspace, rpb);
+  else if (D <= 128)
+    hipLaunchKernelGGL(layernorm_bwd_reg_kernel<2>, dim3(nb), dim3(256), lds, st, dy, x, M, (int)D,
+                       gamma, mean, rstd, dx, workspace, rpb);
+  else if (D <= 256)
+    hipLaunchKernelGGL(layernorm_bwd_reg_kernel<4>, dim3(nb), dim3(256), lds, st, dy, x, M, (int)D,
+                       gamma, mean, rstd, dx, workspace, rpb);
+  else
+    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nb), dim3(256), lds, st, dy, x, M, (int)D, gamma,
+                       mean, rstd, dx, workspace, rpb);
   // workspace [nb][2][D]: reduce both halves (rows of length 2D)
   float* rs = workspace + (int64_t)nb * 2 * D;
   if (dgamma) reduce_rows(workspace, nb, D, 2 * D, dgamma, nullptr, 0, (int)accumulate, rs, st);
