@@ -1121,16 +1121,16 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const float* __restrict_
 // through L1/L2; for the T gather (stride-2 transposed) the taps whose source is fractional
 // are skipped per output parity with wave-uniform branches.  Same epilogue as epi_store.
 constexpr int SMALL_NB = 16;
-template <int MODE, int KH, int KW, int SW, bool REPL>
+template <int MODE, int KH, int KW, int SW, bool REPL, int NB>
 __global__ __launch_bounds__(256) void conv_small_kernel(const float* __restrict__ in,
                                                          const float* __restrict__ wt,
                                                          float* __restrict__ out, ConvGeom g,
                                                          Epi e) {
   constexpr int KK = KH * KW;
-  __shared__ floatx4 ws4[SMALL_NB * KK * SMALL_NB / 4];  // [c][t][n]
+  __shared__ floatx4 ws4[SMALL_NB * KK * NB / 4];  // [c][t][n], c < C <= 12 (dispatch)
   float* ws = reinterpret_cast<float*>(ws4);
-  for (int i = threadIdx.x; i < g.C * KK * SMALL_NB; i += 256) {
-    const int n = i % SMALL_NB, ct = i / SMALL_NB;
+  for (int i = threadIdx.x; i < g.C * KK * NB; i += 256) {
+    const int n = i % NB, ct = i / NB;
     const int c = ct / KK, t = ct - c * KK;
     ws[i] = n < g.N ? wt[(int64_t)n * g.wsn + (int64_t)c * g.wsc + t] : 0.f;
   }
@@ -1142,11 +1142,11 @@ __global__ __launch_bounds__(256) void conv_small_kernel(const float* __restrict
   const int64_t bh = tid / wo2;
   const int h = (int)(bh % g.Hout), b = (int)(bh / g.Hout);
   const int wo0 = 2 * j;
-  float acc[2][SMALL_NB];
+  float acc[2][NB];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
-    for (int n = 0; n < SMALL_NB; ++n) acc[p][n] = 0.f;
+    for (int n = 0; n < NB; ++n) acc[p][n] = 0.f;
   const float* inb = in + (int64_t)b * g.C * g.Hin * g.Win;
   for (int c = 0; c < g.C; ++c) {
     const float* inc = inb + (int64_t)c * g.Hin * g.Win;
@@ -1161,7 +1161,7 @@ __global__ __launch_bounds__(256) void conv_small_kernel(const float* __restrict
       const float* row = inc + (int64_t)(hv ? hi : 0) * g.Win;
 #pragma unroll
       for (int kw = 0; kw < KW; ++kw) {
-        const floatx4* w4 = ws4 + ((c * KK + kh * KW + kw) * SMALL_NB) / 4;
+        const floatx4* w4 = ws4 + ((c * KK + kh * KW + kw) * NB) / 4;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
           const int wo = wo0 + p;
@@ -1183,7 +1183,7 @@ __global__ __launch_bounds__(256) void conv_small_kernel(const float* __restrict
           ok = ok && hv && wo < g.Wo;
           const float v = ok ? row[ok ? wi : 0] : 0.f;
 #pragma unroll
-          for (int q = 0; q < SMALL_NB / 4; ++q) {
+          for (int q = 0; q < NB / 4; ++q) {
             const floatx4 w = w4[q];
             acc[p][4 * q + 0] = fmaf(w[0], v, acc[p][4 * q + 0]);
             acc[p][4 * q + 1] = fmaf(w[1], v, acc[p][4 * q + 1]);
@@ -1201,7 +1201,7 @@ __global__ __launch_bounds__(256) void conv_small_kernel(const float* __restrict
     const int wo = wo0 + p;
     if (wo >= g.Wo) continue;
 #pragma unroll
-    for (int n = 0; n < SMALL_NB; ++n) {
+    for (int n = 0; n < NB; ++n) {
       if (n >= g.N) continue;
       const int64_t o = ((int64_t)b * g.N + n) * hw + (int64_t)h * g.Wo + wo;
       float v = acc[p][n] + (e.bias ? e.bias[n] : 0.f);
@@ -2077,8 +2077,16 @@ static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g
   // elsewhere
   if (g_conv_small && MODE == GATHER_T && SW == 2 && g.C <= 12 && g.N <= 12) {
     const int64_t th = (int64_t)g.B * g.Hout * ((g.Wo + 1) / 2);
-    hipLaunchKernelGGL((conv_small_kernel<MODE, KH, KW, SW, REPL>), dim3((unsigned)((th + 255) / 256)),
-                       dim3(256), 0, st, in, wt, out, g, e);
+    // outputs per thread rounded up to 4 (every channel's sum in the same order)
+    const dim3 grid((unsigned)((th + 255) / 256));
+    if (g.N <= 4)
+      hipLaunchKernelGGL((conv_small_kernel<MODE, KH, KW, SW, REPL, 4>), grid, dim3(256), 0, st, in, wt, out, g, e);
+    else if (g.N <= 8)
+      hipLaunchKernelGGL((conv_small_kernel<MODE, KH, KW, SW, REPL, 8>), grid, dim3(256), 0, st, in, wt, out, g, e);
+    else if (g.N <= 12)
+      hipLaunchKernelGGL((conv_small_kernel<MODE, KH, KW, SW, REPL, 12>), grid, dim3(256), 0, st, in, wt, out, g, e);
+    else
+      hipLaunchKernelGGL((conv_small_kernel<MODE, KH, KW, SW, REPL, 16>), grid, dim3(256), 0, st, in, wt, out, g, e);
     return;
   }
   HaloPlan pl;
