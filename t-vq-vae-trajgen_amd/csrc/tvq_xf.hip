@@ -144,6 +144,58 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_reg_kernel(
   }
 }
 
+// D <= 32 (the HF prior): each half-wave takes a row, so a wave runs two rows at a time
+// (the one-row form left half of every wave idle); per-half dg partials in LDS.
+__global__ __launch_bounds__(256) void rmsnorm_bwd_half_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, int64_t M, int D,
+    const float* __restrict__ g, float scale, const float* __restrict__ inv_norm,
+    const float* __restrict__ dres, float* __restrict__ dx, float* __restrict__ dg_part,
+    int rows_per_block) {
+  extern __shared__ float sh[];  // [2 * waves][D] partial dg
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int hl = lane >> 5, d = lane & 31;
+  const int slot = 2 * wid + hl, nslot = 2 * nw;
+  for (int i = threadIdx.x; i < nslot * D; i += blockDim.x) sh[i] = 0.f;
+  const float gv = d < D ? g[d] : 0.f;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  float cx, cg, cr, cinv, nx, ng, nr, ninv;
+  auto load = [&](int64_t row, float& xv, float& gg, float& rv, float& inv) {
+    const int64_t rr = row < r1 ? row : r0;
+    const int64_t o = rr * D + (d < D ? d : 0);
+    xv = x[o];
+    gg = dy[o];
+    rv = dres ? dres[o] : 0.f;
+    inv = inv_norm[rr];
+  };
+  int64_t row = r0 + slot;
+  load(row, cx, cg, cr, cinv);
+  for (; row - hl < r1; row += nslot) {  // both halves iterate together (wave-uniform trip)
+    load(row + nslot, nx, ng, nr, ninv);
+    const bool live = row < r1 && d < D;
+    float dot = live ? cg * gv * cx : 0.f;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);
+    const float c = dot * scale * cinv * cinv * cinv;
+    if (live) {
+      const float v = cg * gv * scale * cinv - cx * c;
+      dx[row * D + d] = dres ? v + cr : v;
+      sh[slot * D + d] += cg * cx * cinv * scale;
+    }
+    cx = nx;
+    cg = ng;
+    cr = nr;
+    cinv = ninv;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += blockDim.x) {
+    float t = 0.f;
+    for (int w = 0; w < nslot; ++w) t += sh[w * D + i];
+    dg_part[(int64_t)blockIdx.x * D + i] = t;
+  }
+}
+
 // out[d] (+)= sum_p part[p][d]
 __global__ void colsum_kernel(const float* __restrict__ part, int P, int D, float* __restrict__ out,
                               int accumulate) {
@@ -744,7 +796,10 @@ extern "C" int tvq_rmsnorm_bwd(const float* dy, const float* x, int64_t M, int64
   const int nb = (int)((M + rpb - 1) / rpb);
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = 4 * D * sizeof(float);
-  if (D <= 64)
+  if (D <= 32)
+    hipLaunchKernelGGL(rmsnorm_bwd_half_kernel, dim3(nb), dim3(256), 2 * lds, st, dy, x, M, (int)D,
+                       g, scale, inv_norm, dres, dx, workspace, rpb);
+  else if (D <= 64)
     hipLaunchKernelGGL(rmsnorm_bwd_reg_kernel<1>, dim3(nb), dim3(256), lds, st, dy, x, M, (int)D, g,
                        scale, inv_norm, dres, dx, workspace, rpb);
   else if (D <= 128)
