@@ -94,6 +94,13 @@ class JointTrainer:
                 for b in m.buffers():
                     if b.is_floating_point():
                         dist.broadcast(b, 0)
+        from timevqvae.hip.dp import ReplicaSync, flatten_bn_buffers
+        self.sync = ReplicaSync(world)
+        # BatchNorm running statistics of the trained modules as one flat buffer (stage1's
+        # encoders / decoders, the HF prior's Upscale): averaged over the replicas every step
+        self.bn_flat = (flatten_bn_buffers([self.s1, self.s2.maskgit.transformer_l,
+                                            self.s2.maskgit.transformer_h])
+                        if world > 1 else None)
         self.device = device
         self._one = torch.ones((), device=device)
         self.graph = None
@@ -102,14 +109,15 @@ class JointTrainer:
         self.packs = PackCache(device) if os.environ.get("TVQ_PACK_CACHE", "1") != "0" else None
 
     def _allreduce(self, opt):
-        """DP exchange: mean of the flat gradients; the layer-dropout gates (which
-        parameter segments some replica's forward used) are OR-ed (MAX), so every replica
-        updates the same segments and the replicas stay identical."""
-        if self.world > 1:
-            dist.all_reduce(opt.flat_grad)
-            opt.flat_grad.mul_(1.0 / self.world)
-            if opt.has_gates:
-                dist.all_reduce(opt.gates, op=dist.ReduceOp.MAX)
+        """DP exchange (timevqvae.hip.dp): mean of the flat gradients; the layer-dropout
+        gates (which parameter segments some replica's forward used) are OR-ed (MAX), so
+        every replica updates the same segments and the replicas stay identical."""
+        self.sync.gradients(opt)
+
+    def _sync_buffers(self):
+        """Mean of the BatchNorm running statistics over the replicas (DDP keeps them
+        equal with broadcast_buffers; here every state_dict tensor stays bitwise equal)."""
+        self.sync.buffers(self.bn_flat)
 
     def _fwd_bwd(self, batch, defer):
         """zero_grad, then stage1's LF and HF bands (forward+backward, one side stream
@@ -144,6 +152,7 @@ class JointTrainer:
             opt.gather_gates()
             self._allreduce(opt)
             opt.step(gates_ready=True)
+        self._sync_buffers()
         return out1, out2
 
     def capture(self, batch):
@@ -170,6 +179,7 @@ class JointTrainer:
         def between1():
             self._allreduce(self.opt1)
             self._allreduce(self.opt2)
+            self._sync_buffers()
             for u in self._pending:
                 u.reduce()
 
@@ -253,7 +263,7 @@ def config0_leg(device, cpu=True):
         from oracle import cpu_baseline
         threads = int(os.environ.get("TVQ_CPU_THREADS", min(16, os.cpu_count() or 1)))
         for b in (32, 256):
-            s = cpu_baseline.measure_stage1(threads, b, 128, 256, steps=2, warmup=1)
+            s = cpu_baseline.measure_stage1(threads, b, 128, 256, steps=5, warmup=2)
             out[f"cpu_B{b}_ms_per_step"] = round(s * 1e3, 1)
         out["cpu_cores"] = threads
     return out
@@ -479,14 +489,21 @@ def sampler_leg(tr, device, num=1024, reps=5):
 
 
 def cpu_baseline_leg():
+    """the CPU port of the joint step (oracle/cpu_baseline.py, every
+    reference dropout on) on the host's cores: 2 untimed warmups, then the median of 5
+    timed steps; the CPU model is recorded.  The port is checked against the reference's
+    own CPU step in the build container (tools/cpu_ref_compare.py ->
+    profiles/r03_cpu_ref_compare.json)."""
     from oracle import cpu_baseline
     threads = int(os.environ.get("TVQ_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    s = cpu_baseline.measure(threads, steps=2, warmup=1)
-    return {"value": round(1.0 / s, 4), "unit": "steps/s", "cores": threads, "kind": "port",
-            "sample": f"2 timed joint steps (after 1 warmup) of oracle/cpu_baseline.py at B=256,C=6,"
-                      f"T=256,K=512 on {threads} torch threads, every reference dropout on: "
-                      f"{s:.3f} s/step (the port runs 0.77x the reference's own stage1 time "
-                      f"and 0.97x its stage2 time at 8 threads, profiles/r02_cpu_ref_compare.json)"}
+    med, ts = cpu_baseline.measure(threads, steps=5, warmup=2, detail=True)
+    return {"value": round(1.0 / med, 4), "unit": "steps/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_baseline.cpu_model(),
+            "step_s": [round(t, 4) for t in ts],
+            "sample": f"median of 5 timed joint steps (after 2 untimed warmups) of "
+                      f"oracle/cpu_baseline.py at B=256,C=6,T=256,K=512 on {threads} torch "
+                      f"threads, every reference dropout on: {med:.3f} s/step "
+                      f"(port vs reference's own CPU step: profiles/r03_cpu_ref_compare.json)"}
 
 
 def main():
@@ -551,6 +568,9 @@ def main():
                                    "(B=256,C=6,T=256), K=512, configs/config.yaml architecture",
                        "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
                        "launch": "eager" if args.eager else "hipgraph",
+                       "value_counts": "per-GPU B=256 joint steps summed over the ranks (one "
+                                       "optimizer step per N of them at N>1)",
+                       "optimizer_steps_per_s": round(args.steps / elapsed, 3),
                        "trajectories_per_s": round(value * B, 1)},
             "losses": {"stage1": round(loss1, 5), "stage2": round(loss2, 5)},
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 3),

@@ -169,29 +169,47 @@ class JointStep:
         return float(loss.detach())
 
 
-def measure(threads, steps=2, warmup=1, B=256):
-    """Seconds per joint step of the CPU restatement (bounded sample)."""
+def cpu_model():
+    """The host CPU's model string (/proc/cpuinfo), for the bench's cpu_baseline record."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
+
+
+def _median_step(fn, steps, warmup):
+    """BASELINE.md §3 protocol: `warmup` untimed steps, then the median of `steps` timed
+    steps (each timed alone).  Returns (median seconds, every step's seconds)."""
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def measure(threads, steps=5, warmup=2, B=256, detail=False):
+    """Seconds per joint step of the CPU restatement: median of `steps` (>= 5) timed steps
+    after `warmup` (2) untimed ones."""
     torch.set_num_threads(threads)
     js = JointStep(B=B)
-    for _ in range(warmup):
-        js.step()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        js.step()
-    return (time.perf_counter() - t0) / steps
+    med, ts = _median_step(js.step, steps, warmup)
+    return (med, ts) if detail else med
 
 
-def measure_stage1(threads, B, T, K, steps=2, warmup=1):
+def measure_stage1(threads, B, T, K, steps=5, warmup=2):
     """Seconds per stage1 train step (BASELINE configs[0]: T=128, K=256, config.yaml
-    widths) of the CPU restatement."""
+    widths) of the CPU restatement: median of `steps` after `warmup`."""
     torch.set_num_threads(threads)
     js = JointStep(B=B, T=T, K=K)
-    for _ in range(warmup):
-        js.step_stage1()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        js.step_stage1()
-    return (time.perf_counter() - t0) / steps
+    return _median_step(js.step_stage1, steps, warmup)[0]
 
 
 def measure_sampler(threads, num=256, reps=1, seed=0, K=512, hid=128, n_classes=5, T=256, C=6):

@@ -158,8 +158,12 @@ def _bn(ctx, sd, p, x):
 
 
 def _dropout(ctx, x, p):
+    """nn.Dropout (vq_vae.py:52): F.dropout (torch's bernoulli_ draw, the reference's own
+    CPU cost); with an explicit generator, the same mask law drawn from it."""
     if not ctx.training or p == 0.0:
         return x
+    if ctx.gen is None:
+        return F.dropout(x, p, training=True)
     keep = (torch.rand(x.shape, generator=ctx.gen) >= p).to(x.dtype)
     return x * keep / (1 - p)
 

@@ -66,11 +66,20 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // Grid-level finish without a second launch: every block of a group publishes its
 // partial results, then takes a ticket; the block that draws the last ticket combines
 // the group's partials in a fixed order, so the result does not depend on arrival
-// order.  The L2s of the 8 XCDs are not coherent, and an agent-scope release fence
-// writes back a whole L2 (measured: 2x slower step), so partials are published with
+// order.  The L2s of the 8 XCDs are not coherent, so the partials are published with
 // write-through stores (st_wt: agent-scope relaxed atomic store, `sc1`), drained with
-// s_waitcnt vmcnt(0) before the ticket, and read back with ld_wt (`sc1` loads that do
-// not hit a stale L2 line).  The last block re-zeroes the counter for the next launch.
+// s_waitcnt vmcnt(0) by every storing wave before the block's barrier, and read back with
+// ld_wt (`sc1` loads that do not hit a stale L1/L2 line).  The ticket itself is an
+// agent-scope acq_rel fetch_add (TVQ_TICKET_ACQ_REL, the default): release orders the
+// block's published partials before its ticket and acquire orders the last block's reads
+// after it, in the HIP memory model's own terms, on top of the write-through hand-off.
+// With TVQ_TICKET_ACQ_REL=0 the ticket is relaxed with wavefront-scope fences around it
+// (the guide's "every payload store and load sc1" form, cdna_hip_programming.md §6
+// Guideline 16: the fences only stop the compiler moving the loads above the ticket).
+// The last block re-zeroes the counter for the next launch.
+#ifndef TVQ_TICKET_ACQ_REL
+#define TVQ_TICKET_ACQ_REL 1
+#endif
 template <typename T>
 __device__ __forceinline__ void st_wt(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -85,9 +94,15 @@ __device__ __forceinline__ bool last_block(int* counter, int total) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's st_wt stores are done
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int t = atomicAdd(counter, 1);
+#if TVQ_TICKET_ACQ_REL
+    const int t = __hip_atomic_fetch_add(counter, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int t = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
     s_last = t == total - 1;
-    if (s_last) atomicExch(counter, 0);
+    if (s_last) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   return s_last != 0;

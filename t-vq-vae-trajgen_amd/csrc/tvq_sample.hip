@@ -66,17 +66,24 @@ __global__ __launch_bounds__(256) void maskgit_sample_kernel(
     const float u = u_cat ? u_cat[t] : uniform01(seed, (uint64_t)t);
     const double v = (double)u * cdf_last;
     const unsigned long long hit = __ballot(incl > v);
-    const int src = hit ? __ffsll(hit) - 1 : 63;
-    int pick = min(K, j0 + per) - 1;  // rounding fallback: the chunk's last code
+    // rounding fallback (no prefix exceeds v, u close to 1): the last chunk holding any
+    // probability, never a trailing chunk of zero-probability codes
+    const unsigned long long pos = __ballot(part > 0.0);
+    const int src = hit ? __ffsll(hit) - 1 : (pos ? 63 - __clzll(pos) : 63);
+    int pick = -1;
     if (lane == src) {
       double acc = incl - part / tot;
+      int last_pos = j0;  // last code of the chunk with positive probability
       for (int j = j0; j < min(K, j0 + per); ++j) {
-        acc += exp((double)l[j] - (double)m) / tot;
+        const double pj = exp((double)l[j] - (double)m) / tot;
+        if (pj > 0.0) last_pos = j;
+        acc += pj;
         if (acc > v) {
           pick = j;
           break;
         }
       }
+      if (pick < 0) pick = last_pos;  // the recomputed sum never passed v (rounding)
     }
     pick = __shfl(pick, src, 64);
     if (lane == 0) {

@@ -21,8 +21,13 @@ constexpr int VQ_BM = 64;   // token rows per workgroup
 constexpr int VQ_T = 512;   // threads: 4 row groups of 16 x 2 code halves
 constexpr int VQ_CK = 128;  // codes per LDS chunk
 
-// (v, i) "better" for argmin of t with first-index tie break
+// (v, i) "better" for argmin of t with first-index tie break.  A NaN distance beats every
+// number (torch.argmax over dist = -t treats NaN as the maximum and returns the first NaN
+// index, vq.py:216-222), and among NaNs the first index wins.
 __device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
+  const bool n = v != v, bn = bv != bv;
+  if (n != bn) return n;
+  if (n) return i < bi;
   return v < bv || (v == bv && i < bi);
 }
 
@@ -156,7 +161,8 @@ __global__ __launch_bounds__(VQ_T) void vq_assign_kernel(
           v = v / sv.temp - gumbel_at(sv, sseed, m < M ? m : 0, K, code);
         }
         if (code >= K) v = INFINITY;
-        if (v < bestv[r]) { bestv[r] = v; besti[r] = code; }  // codes increase: strict < keeps first
+        // codes increase: strict < keeps the first; a NaN beats a number and is never beaten
+        if (v < bestv[r] || (v != v && bestv[r] == bestv[r])) { bestv[r] = v; besti[r] = code; }
       }
     }
   }
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(VQ_T) void vq_assign_kernel(
     float v0 = bv_s[tid], v1 = bv_s[VQ_BM + tid];
     int i0 = bi_s[tid], i1 = bi_s[VQ_BM + tid];
     int bi = better(v1, i1, v0, i0) ? i1 : i0;
-    if (bi < 0 || bi >= K) bi = 0;  // all-NaN row: reference argmax would return a NaN slot
+    if (bi < 0 || bi >= K) bi = 0;  // unreachable for K >= 1 (NaN rows pick their first NaN)
     bi_s[tid] = bi;
     const int64_t m = row0 + tid;
     if (m < M) {

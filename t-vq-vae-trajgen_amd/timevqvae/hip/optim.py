@@ -49,6 +49,11 @@ class FusedAdamW(torch.optim.Optimizer):
         chunk = int(value("tvq_adamw_chunk"))
         chunks, gate_ptrs = [], []
         self._gate_refs = []  # keeps every gate tensor's storage alive
+        # (segment, owner module, index, address at construction): gather_gates checks that
+        # no owner's `_touched` buffer moved (module.to / _apply / buffer replacement) before
+        # the gate kernel dereferences the recorded addresses.  A deepcopy'd parameter loses
+        # its `_tvq_gate` attribute and is updated ungated (plain AdamW).
+        self._gate_owners = []
         off = 0
         with torch.no_grad():
             for s, p in enumerate(ps):
@@ -67,6 +72,7 @@ class FusedAdamW(torch.optim.Optimizer):
                         raise ValueError("FusedAdamW: a gate buffer is not on the parameters' "
                                          "device (build the optimizer after .to(device))")
                     self._gate_refs.append(t)
+                    self._gate_owners.append((s, owner, i, t.data_ptr()))
                     gate_ptrs.append(t.data_ptr() + 4 * i)
                 else:
                     gate_ptrs.append(0)
@@ -93,7 +99,25 @@ class FusedAdamW(torch.optim.Optimizer):
         """gates[s] <- whether segment s's gated branch ran this step (after the forward
         passes; under DP the trainer then all-reduces `gates` with MAX)."""
         if self.has_gates:
+            self._check_gate_buffers()
             call("tvq_adamw_gates", ptr(self.gate_ptrs), self.nseg, ptr(self.gates), stream_ptr())
+
+    def _check_gate_buffers(self):
+        moved = [(seg, o, i) for seg, o, i, a in self._gate_owners if o._touched.data_ptr() != a]
+        if not moved:
+            return
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("FusedAdamW: a layer-dropout gate buffer moved since the optimizer "
+                               "was built; re-run one eager step before capturing")
+        ptrs = self.gate_ptrs.cpu()
+        for seg, o, i in moved:
+            t = o._touched
+            if t.device != self.flat.device:
+                raise ValueError("FusedAdamW: a gate buffer left the parameters' device")
+            ptrs[seg] = t.data_ptr() + 4 * i
+        self.gate_ptrs.copy_(ptrs)
+        self._gate_refs = [o._touched for _, o, _, _ in self._gate_owners]
+        self._gate_owners = [(seg, o, i, o._touched.data_ptr()) for seg, o, i, _ in self._gate_owners]
 
     @torch.no_grad()
     def step(self, closure=None, lr_on_device=False, gates_ready=False):

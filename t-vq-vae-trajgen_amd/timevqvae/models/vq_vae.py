@@ -98,8 +98,12 @@ class ResBlock(nn.Module):
                 p = c[5].p if self.training else 0.0
                 return resblock.resblock_train(x, _a(c[0]), c[1], c[2], _a(c[3]), c[4], p,
                                                self._site)
-            if not (torch.is_grad_enabled() and x.requires_grad) and not (
-                    self.training and c[5].p > 0):
+            # the fused eval launch builds no graph: only when nothing here needs a gradient
+            # (an eval-mode block whose conv / BN / Snake parameters train takes the
+            # autograd path below)
+            needs_grad = torch.is_grad_enabled() and (
+                x.requires_grad or any(p.requires_grad for p in self.parameters()))
+            if not needs_grad and not (self.training and c[5].p > 0):
                 return resblock.resblock_eval(x, _a(c[0]), c[1], c[2], _a(c[3]), c[4])
         s, xs = snake_skip(x, _a(c[0]))  # xs: x, its skip-path gradient summed in Snake bwd
         h = conv2d(s, c[1].weight, c[1].bias)

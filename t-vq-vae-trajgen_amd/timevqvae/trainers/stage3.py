@@ -54,7 +54,14 @@ class Stage3(nn.Module):
         self.decoder_h = self.maskgit.decoder_h
         self.vq_model_h = self.maskgit.vq_model_h
         self.percept_loss_weight = config["fidelity_enhancer"].get("percept_loss_weight", 0.0)
+        if feature_extractor_type not in ("supervised_fcn", "rocket"):
+            raise ValueError(f"unknown feature_extractor_type {feature_extractor_type!r}")
         self.feature_extractor_type = feature_extractor_type
+        # The reference's Metrics draws its ROCKET kernels when the model is built
+        # (evaluation/metrics.py:89-93, from stage3.py:73-83), so the np.random state they
+        # come from is the one at construction, not at the tau search.
+        self._rocket_fn = (_rocket_features(input_length, device or "cuda")
+                           if feature_extractor_type == "rocket" else None)
         self._sched = None
         self._opt = None
 
@@ -62,11 +69,18 @@ class Stage3(nn.Module):
     @torch.no_grad()
     def search_optimal_tau(self, X_train: np.ndarray, device, n_samples: int = 1024,
                            batch_size: int = 32, feature_fn=None):
-        """stage3.py:88-181.  feature_fn(X (n, c, l) float64) -> Z (n, d); the default is the
-        reference's `rocket` extractor (1000 kernels, np.random state as the caller left it)
-        -- the supervised FCN needs its pretrained checkpoint."""
+        """stage3.py:88-181.  feature_fn(X (n, c, l) float64) -> Z (n, d) overrides the
+        extractor.  Without it the extractor follows feature_extractor_type as the reference's
+        Metrics.extract_feature_representations does (metrics.py:107-127): 'rocket' uses the
+        kernels drawn at construction; 'supervised_fcn' needs the pretrained FCN, which is
+        not on this path, so it raises instead of silently using another feature space."""
         if feature_fn is None:
-            feature_fn = _rocket_features(X_train.shape[-1], device)
+            if self.feature_extractor_type != "rocket":
+                raise NotImplementedError(
+                    "search_optimal_tau with feature_extractor_type='supervised_fcn' needs the "
+                    "pretrained FCN extractor (not on the HIP path): pass feature_fn, or build "
+                    "Stage3 with feature_extractor_type='rocket'")
+            feature_fn = self._rocket_fn
         maskgit = self.maskgit.to(device)
         n_iters = -(-n_samples // batch_size)
         xhat = []

@@ -1,44 +1,56 @@
 """Batched sampling helpers -- same API as the reference timevqvae/utils/sample_utils.py
 (unconditional_sample / conditional_sample, sample_utils.py:5-88; the plotting helper is
 not on the path).  MaskGIT.iterative_decoding and decode_token_ind_to_timeseries run on
-the HIP path; results are moved to the host per batch, as in the reference."""
+the HIP path; the batches stay on the device and reach the host in one transfer."""
 import torch
+
+
+def _batch_sizes(n_samples: int, batch_size: int):
+    """Sizes of the sampling batches: full batches, then the remainder (if any)."""
+    full, rest = divmod(int(n_samples), int(batch_size))
+    return [int(batch_size)] * full + ([rest] if rest else [])
 
 
 @torch.no_grad()
 def unconditional_sample(maskgit, n_samples: int, device, class_index=None, batch_size=32,
                          return_representations=False):
-    n_iters = n_samples // batch_size
-    is_residual_batch = False
-    if n_samples % batch_size > 0:
-        n_iters += 1
-        is_residual_batch = True
-    x_new_l, x_new_h, x_new = [], [], []
-    quantize_new_l, quantize_new_h = [], []
-    for i in range(n_iters):
-        b = batch_size
-        if (i + 1 == n_iters) and is_residual_batch:
-            b = n_samples - ((n_iters - 1) * batch_size)
-        embed_ind_l, embed_ind_h = maskgit.iterative_decoding(num=b, device=device,
-                                                              class_index=class_index)
-        if return_representations:
-            x_l, quantize_l = maskgit.decode_token_ind_to_timeseries(embed_ind_l, "lf", True)
-            x_h, quantize_h = maskgit.decode_token_ind_to_timeseries(embed_ind_h, "hf", True)
-            x_l, quantize_l, x_h, quantize_h = x_l.cpu(), quantize_l.cpu(), x_h.cpu(), quantize_h.cpu()
-            quantize_new_l.append(quantize_l)
-            quantize_new_h.append(quantize_h)
-        else:
-            x_l = maskgit.decode_token_ind_to_timeseries(embed_ind_l, "lf").cpu()
-            x_h = maskgit.decode_token_ind_to_timeseries(embed_ind_h, "hf").cpu()
-        x_new_l.append(x_l)
-        x_new_h.append(x_h)
-        x_new.append(x_l + x_h)
-    x_new_l = torch.cat(x_new_l)
-    x_new_h = torch.cat(x_new_h)
-    x_new = torch.cat(x_new)
+    """Same contract as the reference (sample_utils.py:5-64): (x_l, x_h, x) on the host,
+    and with return_representations also the decoder inputs (quantize_l, quantize_h).
+
+    Every batch stays on the device: the sampled token ids, the decoded LF / HF series and
+    the latents are written into preallocated device buffers, and the host receives them in
+    one transfer at the end instead of one `.cpu()` per tensor and batch."""
+    device = torch.device(device)
+    sizes = _batch_sizes(n_samples, batch_size)
+    bufs = None
+    row = 0
+    for b in sizes:
+        s_l, s_h = maskgit.iterative_decoding(num=b, device=device, class_index=class_index)
+        parts = []
+        for s, band in ((s_l, "lf"), (s_h, "hf")):
+            out = maskgit.decode_token_ind_to_timeseries(s, band, return_representations)
+            parts.append(out if return_representations else (out, None))
+        (x_l, q_l), (x_h, q_h) = parts
+        if bufs is None:  # shapes are known after the first batch
+            like = [x_l, x_h] + ([q_l, q_h] if return_representations else [])
+            bufs = [torch.empty((n_samples,) + tuple(t.shape[1:]), device=device, dtype=t.dtype)
+                    for t in like]
+        for buf, t in zip(bufs, (x_l, x_h, q_l, q_h)):
+            buf[row:row + b].copy_(t)
+        row += b
+    if bufs is None:
+        raise ValueError("unconditional_sample: n_samples must be positive")
+    # one device->host copy: the series (and latents) packed into a single flat buffer
+    flat = torch.cat([t.reshape(-1) for t in bufs]).cpu()
+    host, off = [], 0
+    for t in bufs:
+        host.append(flat[off:off + t.numel()].view(t.shape))
+        off += t.numel()
+    x_l, x_h = host[0], host[1]
+    series = (x_l, x_h, x_l + x_h)  # summed on the host, as the reference does
     if return_representations:
-        return (x_new_l, x_new_h, x_new), (torch.cat(quantize_new_l), torch.cat(quantize_new_h))
-    return x_new_l, x_new_h, x_new
+        return series, (host[2], host[3])
+    return series
 
 
 @torch.no_grad()

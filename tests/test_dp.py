@@ -22,19 +22,59 @@ def _worker(rank, world, port, q):
         import bench
         from timevqvae.hip.vq import CodebookUpdate
 
-        # flat gradient average (JointTrainer._allreduce)
-        # + layer-dropout gates OR-ed over ranks (a segment some replica used is updated
-        # on every replica)
+        # flat gradient average (JointTrainer._allreduce -> hip.dp.ReplicaSync) over the
+        # real stage1 / stage2 parameter count, + layer-dropout gates OR-ed over ranks (a
+        # segment some replica used is updated on every replica)
+        import copy
+        from timevqvae.hip.dp import ReplicaSync, batchnorm_modules, flatten_bn_buffers
+        from timevqvae.trainers import Stage1, Stage2
+        from timevqvae.utils import set_seed
+        set_seed(0)  # identical initial replicas (bench.JointTrainer also broadcasts rank 0's)
+        cfg = bench.config(True)
+        s1 = Stage1(64, 3, cfg)
+        s2 = Stage2(None, None, 64, 3, bench.N_CLASSES, config=cfg, stage1=copy.deepcopy(s1))
+        nparam = sum(p.numel() for p in s1.parameters())
+        g = torch.Generator().manual_seed(100 + rank)
+
         class Opt:
-            flat_grad = torch.full((5,), float(rank + 1))
+            flat_grad = torch.randn(nparam, generator=g)
             has_gates = True
             gates = torch.tensor([1.0, 0.0, 0.0]) if rank == 0 else torch.tensor([0.0, 0.0, 1.0])
         tr = bench.JointTrainer.__new__(bench.JointTrainer)
         tr.world = world
+        tr.sync = ReplicaSync(world)
         opt = Opt()
+        mine = opt.flat_grad.clone()
+        both = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(both, mine)
         tr._allreduce(opt)
-        ok_grad = torch.allclose(opt.flat_grad, torch.full((5,), (1 + world) / 2.0))
+        ok_grad = torch.allclose(opt.flat_grad, sum(both) / world, rtol=1e-6, atol=1e-7)
         ok_grad = ok_grad and torch.equal(opt.gates, torch.tensor([1.0, 0.0, 1.0]))
+
+        # BatchNorm running statistics: one flat buffer (every running_mean / running_var
+        # a view of it), averaged over the replicas -> every state_dict tensor bitwise
+        # equal across ranks (DDP broadcast_buffers semantics)
+        mods = [s1, s2.maskgit.transformer_l, s2.maskgit.transformer_h]
+        tr.bn_flat = flatten_bn_buffers(mods)
+        bns = batchnorm_modules(mods)
+        with torch.no_grad():  # per-rank updates, as each replica's forward makes them
+            for b in bns:
+                b.running_mean.add_(torch.randn(b.running_mean.shape, generator=g))
+                b.running_var.mul_(1 + torch.rand(b.running_var.shape, generator=g))
+        views_ok = all(b.running_mean.data_ptr() >= tr.bn_flat.data_ptr() for b in bns)
+        pre = torch.cat([torch.cat([b.running_mean, b.running_var]) for b in bns])
+        tr._sync_buffers()
+        sd = {k: v.clone() for m in (s1, s2) for k, v in m.state_dict().items()}
+        gathered = [None] * world
+        dist.all_gather_object(gathered, sd)
+        ok_sd = all(torch.equal(gathered[0][k], gathered[r][k]) for r in range(world)
+                    for k in sd)
+        pres = [torch.empty_like(pre) for _ in range(world)]
+        dist.all_gather(pres, pre)
+        post = torch.cat([torch.cat([b.running_mean, b.running_var]) for b in bns])
+        ok_bn = views_ok and ok_sd and torch.allclose(post, sum(pres) / world, rtol=1e-6,
+                                                      atol=1e-6)
+        ok_grad = ok_grad and ok_bn
 
         # sync_codebook statistics: summed over ranks before the EMA
         K, D = 4, 3

@@ -5,8 +5,9 @@ average and the sync_codebook all-reduce of the per-code statistics run (referen
 vq.py:155,229,234: every replica's EMA sees the global batch).
 
 Checked after each of 3 replayed steps:
-  * the flat stage1 / stage2 parameters and the stage1 codebook buffers are bitwise equal
-    across the ranks (replicas never drift);
+  * the flat stage1 / stage2 parameters, the stage1 codebook buffers and every other
+    state_dict tensor (BatchNorm running statistics included) are bitwise equal across
+    the ranks (replicas never drift);
   * the stage1 codebook EMA (cluster_size, embed_avg, embed) equals the oracle
     vq_ref.ema over the CONCATENATED shards -- the rank-0 and rank-1 VQ inputs and
     assignments of that step -- from the pre-step buffers."""
@@ -58,7 +59,9 @@ def _worker(rank, world, port, out_dir):
                "idx": {b: seen[b][1].detach().reshape(-1).cpu().clone() for b in vqs},
                "flat1": tr.opt1.flat.detach().cpu().clone(),
                "flat2": tr.opt2.flat.detach().cpu().clone(),
-               "loss1": float(out1["loss"].detach().sum()), "loss2": float(out2["loss"].detach())}
+               "loss1": float(out1["loss"].detach().sum()), "loss2": float(out2["loss"].detach()),
+               "state": {f"s{i}.{k}": v.detach().cpu().clone()
+                         for i, m in ((1, tr.s1), (2, tr.s2)) for k, v in m.state_dict().items()}}
         log.append(rec)
     torch.save(log, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
@@ -85,8 +88,15 @@ def test_joint_trainer_world2_graph_path(tmp_path):
         assert np.isfinite(a["loss1"]) and np.isfinite(a["loss2"])
         assert torch.equal(a["flat1"], b["flat1"]), f"step {s}: stage1 replicas differ"
         assert torch.equal(a["flat2"], b["flat2"]), f"step {s}: stage2 replicas differ"
+        # every state_dict tensor (parameters, BatchNorm running statistics, codebooks,
+        # counters) bitwise equal across the replicas (DDP broadcast_buffers semantics)
+        assert a["state"].keys() == b["state"].keys()
+        diff = [k for k in a["state"] if not torch.equal(a["state"][k], b["state"][k])]
+        assert not diff, f"step {s}: state_dict entries differ across ranks: {diff[:5]}"
         if s == 0:
             assert not torch.equal(a["flat1"], torch.zeros_like(a["flat1"]))
+            rm = [k for k in a["state"] if k.startswith("s1.") and k.endswith("running_mean")]
+            assert rm and any(a["state"][k].abs().sum() > 0 for k in rm)  # BN stats moved
         for band in ("l", "h"):
             for k in ("cluster_size", "embed_avg", "embed"):
                 assert torch.equal(a["post"][band][k], b["post"][band][k]), (s, band, k)

@@ -65,6 +65,22 @@ def test_sample_never_draws_zero_probability_code(cuda):
     assert (selp.cpu() > 0).all()
 
 
+def test_sample_u_near_one_never_draws_trailing_zero_probability_code(cuda):
+    """u just below 1 with trailing codes of probability 0: no prefix may exceed v after
+    rounding, and the fallback must still land on a positive-probability code (the last
+    one), never the zero-probability tail."""
+    from timevqvae.hip.sample import maskgit_sample
+    K = 512
+    logits = torch.zeros(2, 3, K)
+    logits[..., 300:] = -1e4  # p = 0 for codes 300..511 (the last 26 lanes' chunks)
+    s = torch.full((2, 3), K, dtype=torch.int64)
+    for u0 in (1.0 - 2.0 ** -24, 1.0 - 2.0 ** -20, 0.999999):
+        u = torch.full((2, 3), u0)
+        sampled, selp = maskgit_sample(logits.to(cuda), s.to(cuda), K, u_cat=u.to(cuda))
+        assert (sampled.cpu() < 300).all() and (sampled.cpu() >= 290).all(), sampled
+        assert (selp.cpu() > 0).all()
+
+
 def test_mask_by_random_topk_exact_k(cuda):
     """mask_by_random_topk keeps exactly mask_len per row; known tokens (+inf) never mask."""
     from timevqvae.hip.sample import maskgit_remask

@@ -73,7 +73,7 @@ def test_fe_train_step_vs_reference(tag, cuda):
     _grads_close(fe.named_parameters(), g, f"{tag}_")
 
 
-def _stage3(cuda, dropout=0.0):
+def _stage3(cuda, dropout=0.0, feature_extractor_type="supervised_fcn"):
     from test_stage2_golden import _maskgit
     from timevqvae.trainers import Stage3
     mg = _maskgit(cuda)
@@ -85,7 +85,8 @@ def _stage3(cuda, dropout=0.0):
     cfg = {"VQ-VAE": {"n_fft": 4}, "fidelity_enhancer": dict(CFG, dropout=dropout),
            "exp_params": {"lr": 1e-3, "linear_warmup_rate": 0.1},
            "trainer_params": {"max_steps": {"stage3": 100}}}
-    st = Stage3(None, None, None, 128, 6, 5, config=cfg, stage2=_S2(mg))
+    st = Stage3(None, None, None, 128, 6, 5, config=cfg, stage2=_S2(mg), device=cuda,
+                feature_extractor_type=feature_extractor_type)
     vals = fill_state_dict(st.fidelity_enhancer.state_dict(), 23)
     st.fidelity_enhancer.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
     return st.to(cuda)
@@ -161,9 +162,12 @@ def test_gn_snake_dropout_mask_and_gradient(cuda):
 
 @pytest.mark.gpu
 def test_stage3_search_optimal_tau_smoke(cuda):
-    st = _stage3(cuda)
     g = torch.Generator().manual_seed(6)
     X = torch.cumsum(0.1 * torch.randn(48, 6, 128, generator=g), -1).numpy()
+    # the reference's default extractor is the pretrained FCN: no silent ROCKET substitute
+    with pytest.raises(NotImplementedError):
+        _stage3(cuda).search_optimal_tau(X, cuda, n_samples=16, batch_size=16)
+    st = _stage3(cuda, feature_extractor_type="rocket")
     tau = st.search_optimal_tau(X, cuda, n_samples=48, batch_size=16)
     assert tau in CFG["tau_search_rng"]
     assert all(np.isfinite(v) for v in st.tau_fids.values())

@@ -293,3 +293,31 @@ def test_hip_svq_training_ema_uses_sampled_indices(cuda):
     # the straight-through output is the (pre-update) codeword of the sampled index
     np.testing.assert_allclose(q.detach().cpu().numpy()[0], E[ind.reshape(-1).cpu().numpy()],
                                rtol=0, atol=2e-6)
+
+
+@pytest.mark.gpu
+def test_hip_vq_nan_rows_match_torch_argmax(cuda):
+    """NaN distances: torch.argmax (vq.py:216-222) treats NaN as the maximum and returns the
+    first NaN index. A NaN token row therefore maps to code 0, and a NaN codebook row k
+    to code k for every token (the first NaN of each row)."""
+    from timevqvae.models import VectorQuantize
+    torch.manual_seed(3)
+    K, D = 64, 128
+    x = torch.randn(2, 16, D)
+    x[0, 3] = float("nan")
+    x[1, 7, 5] = float("nan")
+    E = torch.randn(K, D)
+    E[9] = float("nan")
+    E[40, 0] = float("nan")
+
+    def ref(xx, EE):
+        flat = xx.reshape(-1, D)
+        dist = -(flat.pow(2).sum(1, keepdim=True) - 2 * flat @ EE.t() + EE.pow(2).sum(1)[None])
+        return dist.argmax(-1).reshape(xx.shape[:-1])
+
+    for EE in (torch.randn(K, D), E):
+        vq = VectorQuantize(D, K).to(cuda).eval()
+        vq._codebook.embed.copy_(EE)
+        _, ind, _, _ = vq(x.to(cuda))
+        want = ref(x, EE)
+        assert (ind.cpu() == want).all(), (ind.cpu()[want != ind.cpu()], want[want != ind.cpu()])

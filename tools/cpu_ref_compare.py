@@ -31,16 +31,24 @@ def batch(B, C, T, seed=1234):
     return x, torch.randint(0, 5, (B, 1), generator=g)
 
 
-def timed(fn, steps, warmup=1):
+def interleaved(fa, fb, steps, warmup=2):
+    """Median seconds per step of fa and of fb, timed alternately step by step (after
+    `warmup` untimed steps of each), so drift of the shared host hits both alike."""
     for _ in range(warmup):
-        fn()
-    t0 = time.perf_counter()
+        fa()
+        fb()
+    ta, tb = [], []
     for _ in range(steps):
-        fn()
-    return (time.perf_counter() - t0) / steps
+        t0 = time.perf_counter()
+        fa()
+        ta.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        fb()
+        tb.append(time.perf_counter() - t0)
+    return float(np.median(ta)), float(np.median(tb))
 
 
-def ref_stage1(ref, B, T, K, steps):
+def ref_stage1(ref, B, T, K):
     torch.manual_seed(0)
     np.random.seed(0)
     cfg = MG._stage1_config(4, 128, K)
@@ -54,10 +62,10 @@ def ref_stage1(ref, B, T, K, steps):
         loss = recons["LF.time"] + recons["HF.time"] + vq["LF"]["loss"] + vq["HF"]["loss"]
         loss.sum().backward()
         opt.step()
-    return timed(step, steps)
+    return step
 
 
-def ref_stage2(ref, bt, maskgit, B, T, K, steps):
+def ref_stage2(ref, bt, maskgit, B, T, K):
     """MaskGIT.forward (reference file) over a frozen reference stage1, AdamW over the
     priors (trainers/stage2.py:49-68,112-119)."""
     torch.manual_seed(0)
@@ -95,7 +103,7 @@ def ref_stage2(ref, bt, maskgit, B, T, K, steps):
         loss, _ = mg(x, y)
         loss.backward()
         opt.step()
-    return timed(step, steps)
+    return step
 
 
 def main():
@@ -103,19 +111,20 @@ def main():
     torch.set_num_threads(threads)
     ref = MG.load_reference()
     bt, maskgit = MG.load_reference_stage2(ref)
-    res = {"threads": threads, "cpu": os.uname().machine, "rows": []}
-    for name, B, T, K, steps in (("stage1 configs[1] (B=256,T=256,K=512)", 256, 256, 512, 3),
-                                 ("stage1 configs[0] (B=32,T=128,K=256)", 32, 128, 256, 5),
-                                 ("stage1 configs[0] (B=256,T=128,K=256)", 256, 128, 256, 3)):
-        r = ref_stage1(ref, B, T, K, steps)
+    from oracle.cpu_baseline import cpu_model
+    res = {"threads": threads, "cpu": cpu_model(),
+           "protocol": "reference and port steps alternated; 2 untimed warmups each, then the "
+                       "median of 7 timed steps each", "rows": []}
+    for name, B, T, K in (("stage1 configs[1] (B=256,T=256,K=512)", 256, 256, 512),
+                          ("stage1 configs[0] (B=32,T=128,K=256)", 32, 128, 256),
+                          ("stage1 configs[0] (B=256,T=128,K=256)", 256, 128, 256)):
         js = cpu_baseline.JointStep(B=B, T=T, K=K)
-        p = timed(js.step_stage1, steps)
+        r, p = interleaved(ref_stage1(ref, B, T, K), js.step_stage1, 7)
         res["rows"].append({"what": name, "reference_s": round(r, 4), "port_s": round(p, 4),
                             "port_over_reference": round(p / r, 3)})
         print(json.dumps(res["rows"][-1]), file=sys.stderr, flush=True)
-    r = ref_stage2(ref, bt, maskgit, 256, 256, 512, 3)
     js = cpu_baseline.JointStep(B=256)
-    p = timed(js.step_stage2, 3)
+    r, p = interleaved(ref_stage2(ref, bt, maskgit, 256, 256, 512), js.step_stage2, 7)
     res["rows"].append({"what": "stage2 configs[2] (B=256,T=256,K=512; T1 restated in both)",
                         "reference_s": round(r, 4), "port_s": round(p, 4),
                         "port_over_reference": round(p / r, 3)})
