@@ -273,6 +273,9 @@ def config0_leg(device, cpu=True):
 # stage2 with every prior branch run): tools/count_step_flops.py over the CPU restatement
 # of the same module tree -> profiles/r02_step_flops.json (169.78 GFLOP).
 STEP_GFLOP = 169.78
+# One sampler batch (BASELINE configs[4]: 1024 trajectories, 10 LF + 1 HF prior forwards and
+# both decoders), counted the same way -> profiles/r03_step_flops.json.
+SAMPLER_GFLOP_1024 = 375.0
 FP32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 
@@ -384,18 +387,81 @@ def conv_wgrad_leg(device):
             "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def resblock_bwd_leg(device, C=16, W=32):
+    """The step's top kernel by summed time (profiles/r03*_step_kernel_stats.csv): the fused
+    ResBlock backward (csrc/tvq_resblock.hip rb_bwd2 + rb_bwd1, reference vq_vae.py:13-62) at
+    its most frequent shape, C = 16 on (256, 16, 3, 32) (8 ops per step).  One op = rb_bwd2
+    (dropout' -> conv2 weight gradient slab row + data gradient -> Snake' -> BN backward
+    partials, BN finish in the last block) + rb_bwd1 (BN' -> conv1 weight gradient + data
+    gradient -> Snake' + identity skip, da1 finish) + the two ordered slab sums (batched at
+    the band's end in the step, here after each op).
+    Algorithmic work per op: two 3x3 data gradients 2 * B*P*C*9C each and two weight+bias
+    gradients 2 * B*P*C*(9C+1) each (P = 3W positions) = 4 * 2 * 256*96*16*144 (+bias) =
+    453.8 MFLOP; bytes: dy, x, h read and dx written (4 * B*C*P*4 B) + both weights read and
+    their gradients written = 6.33 MB (AI 72 FLOP/B: fp32 MFMA bound).  50 graph-replayed ops
+    timed with HIP events on their stream."""
+    from timevqvae.hip import rng
+    from timevqvae.hip._native import call, ptr, stream_ptr, value
+    B, H = 256, 3
+    P = H * W
+    g = torch.Generator(device="cpu").manual_seed(5)
+    rnd = lambda *sh, s=1.0: (torch.randn(*sh, generator=g) * s).to(device)  # noqa: E731
+    x, dy = rnd(B, C, H, W), rnd(B, C, H, W)
+    a1 = (0.2 + 0.3 * torch.rand(C, generator=g)).to(device)
+    a2 = (0.2 + 0.3 * torch.rand(C, generator=g)).to(device)
+    w1, w2 = rnd(C, C, 3, 3, s=0.1), rnd(C, C, 3, 3, s=0.1)
+    b1, b2 = rnd(C, s=0.1), rnd(C, s=0.1)
+    bw, bb = torch.ones(C, device=device), torch.zeros(C, device=device)
+    rm, rv = torch.zeros(C, device=device), torch.ones(C, device=device)
+    nbt = torch.zeros((), dtype=torch.int64, device=device)
+    h, y = torch.empty_like(x), torch.empty_like(x)
+    save = torch.empty(4 * C, device=device)
+    ws = torch.empty(value("tvq_resblock_workspace", B, C, H, W), device=device, dtype=torch.uint8)
+    seed = rng.seed_tensor(device)
+    call("tvq_resblock_train_fwd", ptr(x), B, C, H, W, ptr(a1), ptr(w1), ptr(b1), ptr(bw),
+         ptr(bb), ptr(rm), ptr(rv), ptr(nbt), 0.1, 1e-5, ptr(a2), ptr(w2), ptr(b2), 0.3,
+         ptr(seed), 0, ptr(h), ptr(y), ptr(save), ptr(ws), stream_ptr())
+    dx = torch.empty_like(x)
+    grads = [torch.zeros(t.shape, device=device) for t in (a1, w1, b1, bw, bb, a2, w2, b2)]
+
+    def fn():
+        call("tvq_resblock_bwd", ptr(dy), ptr(x), ptr(h), B, C, H, W, ptr(a1), ptr(w1), ptr(bw),
+             ptr(save), ptr(a2), ptr(w2), 0.3, ptr(seed), 0, ptr(dx), *[ptr(t) for t in grads],
+             1, ptr(ws), stream_ptr())
+    with torch.no_grad():
+        us = _graph_time_us([fn], 50)
+    K = 9 * C
+    flops = 2.0 * (2.0 * B * P * C * K) + 2.0 * (2.0 * B * P * C * (K + 1))
+    byts = 4.0 * (4 * B * C * P + 2 * (C * K + C) + 2 * (C * K + C))
+    tf = flops / (us * 1e-6) / 1e12
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "r03_rbbwd_traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath))["traffic_bytes"]
+    return {"bound": "mfma", "kernel": "fused ResBlock backward, C=16 on (256,16,3,32): "
+                                       "rb_bwd2_kernel + rb_bwd1_kernel<RB<16,32>> + their 2 "
+                                       "ordered slab sums (16x16x4 fp32 MFMA, 8 waves per image)",
+            "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
+            "launches_per_op": 4,
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def roofline_leg(device, ms_per_step):
-    """bench JSON `roofline`: the step's top kernel by summed time (conv_wgrad_leg) at top
-    level; the largest single launch of the step, the grouped Linear weight gradients of the
-    LF prior (`wgrad_group`, dominant_leg); the whole step against the fp32 MFMA peak
-    (`step`); the largest single conv on MFMA (`conv_t32`, conv_t32_leg)."""
-    out = conv_wgrad_leg(device)
+    """bench JSON `roofline`: the step's top kernel by summed time, the fused ResBlock
+    backward (resblock_bwd_leg), at top level; the LF 64-channel conv weight gradient
+    (`conv_wgrad`, conv_wgrad_leg); the largest single launch of the step, the grouped Linear
+    weight gradients of the LF prior (`wgrad_group`, dominant_leg); the whole step against
+    the fp32 MFMA peak (`step`); the largest single conv on MFMA (`conv_t32`)."""
+    out = resblock_bwd_leg(device)
+    out["conv_wgrad"] = conv_wgrad_leg(device)
     out["wgrad_group"] = dominant_leg(device)
     tf = STEP_GFLOP / ms_per_step  # GFLOP / ms = TFLOP/s
     out["step"] = {"bound": "mfma", "gflop": STEP_GFLOP, "achieved": round(tf, 2),
                    "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                    "frac": round(tf / FP32_PEAK_TFLOPS, 4),
-                   "source": "tools/count_step_flops.py -> profiles/r02_step_flops.json"}
+                   "source": "tools/count_step_flops.py -> profiles/r03_step_flops.json"}
     out["step_frac"] = out["step"]["frac"]
     out["conv_t32"] = conv_t32_leg(device)
     return out
@@ -480,7 +546,13 @@ def sampler_leg(tr, device, num=1024, reps=5):
     dt_g_fe, _ = timed(GraphedSampler(mg, num, device, fidelity_enhancer=fe).sample)
     mg.train(was)
     # the reference's TrainedModelSampler.sample = decode + FidelityEnhancer (sampler.py:141-169)
-    return {"num": num, "ms_per_batch": round(dt * 1e3, 3),
+    gflop = SAMPLER_GFLOP_1024 * num / 1024
+    roof = {"bound": "mfma", "gflop": round(gflop, 2), "achieved": round(gflop / (dt * 1e3), 2),
+            "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(gflop / (dt * 1e3) / FP32_PEAK_TFLOPS, 4),
+            "source": "tools/count_step_flops.py -> profiles/r03_step_flops.json "
+                      "(sampler_gflop_per_1024)"}
+    return {"num": num, "ms_per_batch": round(dt * 1e3, 3), "roofline": roof,
             "trajectories_per_s": round(num / dt, 1), "reps": reps, "launch": "hipgraph",
             "eager_ms_per_batch": round(dt_eager * 1e3, 3),
             "fidelity_enhancer_ms": round(dt_fe * 1e3, 3),

@@ -212,11 +212,11 @@ def measure_stage1(threads, B, T, K, steps=5, warmup=2):
     return _median_step(js.step_stage1, steps, warmup)[0]
 
 
-def measure_sampler(threads, num=256, reps=1, seed=0, K=512, hid=128, n_classes=5, T=256, C=6):
-    """Seconds per `num` unconditional samples of the CPU restatement: iterative_decoding
-    (maskgit.py:413-446: 10 LF + 1 HF steps, torch sampling) + decode_token_ind_to_timeseries
-    for LF and HF (maskgit.py:448-477) -- the work of generation/sampler.py per batch."""
-    torch.set_num_threads(threads)
+def sampler_fn(num=256, seed=0, K=512, hid=128, n_classes=5, T=256, C=6):
+    """One batch of `num` unconditional samples of the CPU restatement as a callable:
+    iterative_decoding (maskgit.py:413-446: 10 LF + 1 HF steps, torch sampling) +
+    decode_token_ind_to_timeseries for LF and HF (maskgit.py:448-477) -- the work of
+    generation/sampler.py per batch."""
     spec = O.Stage1Spec(T, C, 4, hid)
     sd = _init_stage1(spec, K, hid, seed)
     xl = _init_xf("lf", K, hid, 128, 4, 2, 24, n_classes, seed + 1)
@@ -237,7 +237,13 @@ def measure_sampler(threads, num=256, reps=1, seed=0, K=512, hid=128, n_classes=
                 z = z.transpose(1, 2).reshape(num, hid, 3, W)
                 out = out + O.decoder_forward(e, sd, f"decoder_{br}.", z, plan, band, C, T)
             return out
+    return run
 
+
+def measure_sampler(threads, num=256, reps=1, seed=0, **kw):
+    """Seconds per `num` unconditional samples of the CPU restatement (sampler_fn)."""
+    torch.set_num_threads(threads)
+    run = sampler_fn(num, seed, **kw)
     run()
     t0 = time.perf_counter()
     for _ in range(reps):

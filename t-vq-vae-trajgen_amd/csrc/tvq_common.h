@@ -69,16 +69,18 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // order.  The L2s of the 8 XCDs are not coherent, so the partials are published with
 // write-through stores (st_wt: agent-scope relaxed atomic store, `sc1`), drained with
 // s_waitcnt vmcnt(0) by every storing wave before the block's barrier, and read back with
-// ld_wt (`sc1` loads that do not hit a stale L1/L2 line).  The ticket itself is an
-// agent-scope acq_rel fetch_add (TVQ_TICKET_ACQ_REL, the default): release orders the
-// block's published partials before its ticket and acquire orders the last block's reads
-// after it, in the HIP memory model's own terms, on top of the write-through hand-off.
-// With TVQ_TICKET_ACQ_REL=0 the ticket is relaxed with wavefront-scope fences around it
-// (the guide's "every payload store and load sc1" form, cdna_hip_programming.md §6
-// Guideline 16: the fences only stop the compiler moving the loads above the ticket).
+// ld_wt (`sc1` loads that do not hit a stale L1/L2 line): the hand-off form of
+// cdna_hip_programming.md §6 Guideline 16 (R1) in which the write-through stores and their
+// drain stand in for the producer's release.  TVQ_TICKET selects the ticket's ordering:
+//   2: agent-scope acq_rel fetch_add -- release / acquire in the HIP memory model's own
+//      terms; the release writes back the XCD's whole L2 in every block (measured: joint
+//      step 6.58 vs 5.75 ms, profiles/r03_ticket_ab.txt);
+//   1 (default): relaxed ticket, and the last block alone takes an agent-scope acquire
+//      fence before it reads the partials;
+//   0: relaxed ticket between wavefront-scope fences (compiler ordering only).
 // The last block re-zeroes the counter for the next launch.
-#ifndef TVQ_TICKET_ACQ_REL
-#define TVQ_TICKET_ACQ_REL 1
+#ifndef TVQ_TICKET
+#define TVQ_TICKET 1
 #endif
 template <typename T>
 __device__ __forceinline__ void st_wt(T* p, T v) {
@@ -94,7 +96,7 @@ __device__ __forceinline__ bool last_block(int* counter, int total) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's st_wt stores are done
   __syncthreads();
   if (threadIdx.x == 0) {
-#if TVQ_TICKET_ACQ_REL
+#if TVQ_TICKET == 2
     const int t = __hip_atomic_fetch_add(counter, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
 #else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -102,7 +104,13 @@ __device__ __forceinline__ bool last_block(int* counter, int total) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #endif
     s_last = t == total - 1;
-    if (s_last) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s_last) {
+#if TVQ_TICKET == 1
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   __syncthreads();
   return s_last != 0;

@@ -20,15 +20,22 @@
 //   rb_bwd1   dh = BN'(du) staged -> dW1 | db1 slab row; ds1 = conv1^T(dh) ->
 //             dx = ds1 * Snake'(x) + dy (identity skip); da1 partials -> last block
 //
-// Convs are v_mfma_f32_16x16x4_f32 tiles, MFMA rows = channels (16-row tiles, zero-padded),
-// columns = 16 positions, both operands from LDS: the forward gathers the halo plane at
-// koff[c*9+t] = c*PS + toff(t); the data gradient is the same gather over the gradient
-// planes with transposed weights and flipped taps; the weight gradient reduces over the
-// image's positions with a ones column for the bias.  Everything is compile-time in (C, W)
-// so the K loops unroll and their LDS reads pipeline; every kernel issues all its global
-// loads (image, weights, per-channel parameters, epilogue operands) before it waits on
-// any.  Arithmetic is the unfused kernels' (Snake, BN affine / backward formulas, dropout
-// hash) up to the summation order.
+// Work split inside a block (RB_NW = 8 waves, one image; 256 images = 256 blocks = 2 waves
+// per SIMD, where 4-wave blocks left each SIMD one wave and nothing to hide latency with):
+//   * elementwise phases (staging the conv inputs, epilogues) run channel-per-wave: wave w
+//     takes channels w, w + 8, ... and its lanes that channel's positions, so global loads
+//     and stores are lane-contiguous and every per-channel sum is one fixed xor tree;
+//   * a conv is NI = (16-position x 16-channel output tiles) x (input-channel chunks of CPC)
+//     items of 9*CPC/4 v_mfma_f32_16x16x4_f32 steps, ~24 items over the 8 waves, 3
+//     interleaved chains per wave; the chunk partials go to LDS and the epilogue sums them
+//     in chunk order;
+//   * a weight gradient is (16 x 16 tiles of the C x (9C+1) slab row) x (position chunks)
+//     items; the chunk partials are summed in order into the image's slab row.
+// Both operands of every MFMA come from LDS: the conv gathers the halo plane at
+// c*PS + toff(t) (the data gradient: transposed weights, flipped taps), the weight gradient
+// reduces over the image's positions with a ones column for the bias.  Arithmetic is the
+// unfused kernels' (Snake, BN affine / backward formulas, dropout hash) up to the
+// summation order, which is fixed.
 #include <algorithm>
 
 #include "tvq_bn.h"
@@ -38,7 +45,10 @@
 
 namespace tvq {
 
-constexpr int RB_T = 256;  // 4 waves per block, one image per block
+#ifndef RB_NW
+#define RB_NW 8
+#endif
+constexpr int RB_T = 64 * RB_NW;  // one image per block
 
 template <int C_, int W_>
 struct RB {
@@ -51,12 +61,26 @@ struct RB {
   static constexpr int KST = K + ((2 - K % 32) + 32) % 32;  // panel row stride == 2 mod 32
   static constexpr int KC = K + 1, KT = (KC + 15) / 16;     // wgrad columns (+bias), tiles
   static constexpr int NT = MT * NR, WT = NR * KT;   // conv / wgrad output tiles
-  static constexpr int TPW = (NT + 3) / 4;           // conv tiles per wave
-  static constexpr int NE = C * P, UE = (NE + RB_T - 1) / RB_T;  // image elements
+  // conv items: NT tiles x NCH chunks of CPC input channels (~24 items)
+  static constexpr int CPC0 = C * NT / 24;
+  static constexpr int CPC = CPC0 <= 4 ? 4 : CPC0 <= 8 ? 8 : CPC0 <= 16 ? 16 : 32;
+  static constexpr int NCH = C / CPC, NI = NT * NCH;
+  static constexpr int PR = P + ((4 - P % 8) + 8) % 8;  // conv partial row stride == 4 mod 8
+  // weight-gradient items: WT tiles x PSPL position chunks
+  static constexpr int PSTEPS = P / 4;
+  static constexpr int PSPL = WT >= 24 ? 1 : (W >= 64 ? 6 : 3);
+  static constexpr int WSTEPS = PSTEPS / PSPL, NIW = WT * PSPL;
+  static constexpr int KCR = KC + ((4 - KC % 8) + 8) % 8;  // wgrad partial row stride
+  // elementwise phases: channels per wave, positions per lane
+  static constexpr int CPW = (C + RB_NW - 1) / RB_NW, PPL = (P + 63) / 64;
   static constexpr int NB = 2 * WP + 6;              // border cells per halo plane
   static constexpr int PLANE = C * PS, PANEL = CT * KST;
   static constexpr int NPAN = CT * K, UP = (NPAN + RB_T - 1) / RB_T;  // panel loads
-  static_assert(P % 16 == 0 && TPW <= 3, "unsupported ResBlock geometry");
+  static constexpr int PARTC = NCH * C * PR;         // conv chunk partials (floats)
+  static constexpr int PARTW = PSPL > 1 ? PSPL * C * KCR : 0;  // wgrad chunk partials
+  static_assert(P % 16 == 0 && C % 4 == 0 && C % CPC == 0 && PSTEPS % PSPL == 0 &&
+                    (PSPL == 1 || W % (4 * WSTEPS) == 0 || 4 * WSTEPS % W == 0),
+                "unsupported ResBlock geometry");
 };
 
 struct RBArgs {  // every pointer / scalar a fused ResBlock kernel reads or writes
@@ -88,11 +112,6 @@ struct RBArgs {  // every pointer / scalar a fused ResBlock kernel reads or writ
   } while (0)
 #endif
 
-__device__ __forceinline__ int rb_toff(int t, int WP) {
-  const int kh = t / 3;
-  return kh * WP + (t - 3 * kh);
-}
-
 // halo offset of position p's top-left window cell
 template <class R>
 __device__ __forceinline__ int rb_pos(int p) {
@@ -100,30 +119,46 @@ __device__ __forceinline__ int rb_pos(int p) {
   return h * R::WP + (p - h * R::W);
 }
 
-// this thread's elements e = tid + u*RB_T of the image (all loads issued, none waited on;
-// consecutive lanes read consecutive addresses and write consecutive LDS cells)
+__device__ __forceinline__ int rb_wid() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// channel-per-wave element layout: element (u, v) of this lane is channel
+// c = wid + RB_NW * u, position p = lane + 64 * v
 template <class R>
-__device__ __forceinline__ void rb_load_img(const float* __restrict__ src, int64_t img0,
-                                            float (&v)[R::UE]) {
+struct RBElems {
+  int c[R::CPW];
+  int p[R::PPL];
+  __device__ __forceinline__ RBElems() {
+    const int wid = rb_wid(), l = threadIdx.x & 63;
 #pragma unroll
-  for (int u = 0; u < R::UE; ++u) {
-    const int e = threadIdx.x + u * RB_T;
-    v[u] = src[img0 + (e < R::NE ? e : 0)];
+    for (int u = 0; u < R::CPW; ++u) c[u] = wid + RB_NW * u;
+#pragma unroll
+    for (int v = 0; v < R::PPL; ++v) p[v] = l + 64 * v;
   }
+  __device__ __forceinline__ bool ok(int u, int v) const { return c[u] < R::C && p[v] < R::P; }
+  __device__ __forceinline__ int64_t gi(int64_t img0, int u, int v) const {
+    return img0 + (int64_t)(c[u] < R::C ? c[u] : 0) * R::P + (p[v] < R::P ? p[v] : 0);
+  }
+  __device__ __forceinline__ int cell(int u, int v) const {  // halo-plane cell
+    return c[u] * R::PS + R::WP + 1 + rb_pos<R>(p[v]);
+  }
+};
+
+// every element of this lane's layout (loads issued, none waited on)
+template <class R>
+__device__ __forceinline__ void rb_load(const float* __restrict__ src, int64_t img0,
+                                        const RBElems<R>& el, float (&v)[R::CPW][R::PPL]) {
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u)
+#pragma unroll
+    for (int q = 0; q < R::PPL; ++q) v[u][q] = src[el.gi(img0, u, q)];
 }
 
-// dst[c*PS + halo(h,w)] = f(c, element e of the image, v[, v2]) for this thread's elements
-template <class R, class F>
-__device__ __forceinline__ void rb_put_img(float* __restrict__ dst, const float (&v)[R::UE],
-                                           const float (&v2)[R::UE], F f) {
+// a per-channel parameter at this lane's channels (0 beyond C)
+template <class R>
+__device__ __forceinline__ void rb_param(const float* __restrict__ src, const RBElems<R>& el,
+                                         float (&v)[R::CPW], float dflt = 0.f) {
 #pragma unroll
-  for (int u = 0; u < R::UE; ++u) {
-    const int e = threadIdx.x + u * RB_T;
-    if (e < R::NE) {
-      const int c = e / R::P, r = e - c * R::P;
-      dst[c * R::PS + R::WP + 1 + rb_pos<R>(r)] = f(c, e, v[u], v2[u]);
-    }
-  }
+  for (int u = 0; u < R::CPW; ++u) v[u] = src ? src[el.c[u] < R::C ? el.c[u] : 0] : dflt;
 }
 
 // zero border of C halo planes (the zero padding of a conv input)
@@ -177,81 +212,101 @@ __device__ __forceinline__ void rb_put_panel(float* __restrict__ A, const float 
   }
 }
 
-// this lane's conv output tiles t = wid + 4f: channel tile nr, position p, halo base
-template <class R>
-struct RBTiles {
-  int nt;  // tiles of this wave
-  int nr[3], p[3], base[3];
-  __device__ __forceinline__ RBTiles() {
-    const int wid = threadIdx.x >> 6, j = threadIdx.x & 15;
-    nt = wid < R::NT ? (R::NT - wid + 3) / 4 : 0;
+// Conv of the staged plane(s) S with the panel A as NI items (tile, chunk); item i's
+// 16 x 16 partial over its CPC input channels goes to Pc[(chunk*C + n)*PR + p].  Each wave
+// runs its items three interleaved chains at a time (a dead chain recomputes a live item
+// on valid addresses and stores nothing: no branch in the loop).  FLIP: data gradient
+// (taps flipped).
+template <class R, bool FLIP>
+__device__ __forceinline__ void rb_conv_items(const float* __restrict__ A,
+                                              const float* __restrict__ S, float* __restrict__ Pc) {
+  const int l = threadIdx.x & 63, j = l & 15, kq = l >> 4, wid = rb_wid();
+  // gather offsets of the 9 MFMA steps of a 4-channel group, relative to its first channel:
+  // step s reads reduction index k = 4s + kq = c*9 + t
+  int roff[9];
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    const int k = 4 * s + kq, c = k / 9, t0 = k - 9 * c, t = FLIP ? 8 - t0 : t0;
+    const int kh = t / 3;
+    roff[s] = c * R::PS + kh * R::WP + (t - 3 * kh);
+  }
+  for (int g0 = wid; g0 < R::NI; g0 += 3 * RB_NW) {
+    int ab[3], sb[3], row0[3], col[3];
+    bool live[3];
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
-      const int t = f < nt ? wid + 4 * f : 0;
-      nr[f] = t / R::MT;
-      p[f] = (t - nr[f] * R::MT) * 16 + j;
-      base[f] = rb_pos<R>(p[f]);
+      const int i = g0 + f * RB_NW;
+      live[f] = i < R::NI;
+      const int ii = live[f] ? i : g0;
+      const int tile = ii % R::NT, ch = ii / R::NT;
+      const int nr = tile / R::MT, mt = tile - nr * R::MT;
+      const int p = mt * 16 + j;
+      ab[f] = (nr * 16 + j) * R::KST + ch * R::CPC * 9 + kq;
+      sb[f] = rb_pos<R>(p) + ch * R::CPC * R::PS;
+      row0[f] = ch * R::C + nr * 16 + 4 * kq;  // partial row of acc register 0
+      col[f] = p;
+    }
+    floatx4 acc[3];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) acc[f] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < R::CPC / 4; ++g)
+#pragma unroll
+      for (int s = 0; s < 9; ++s)
+#pragma unroll
+        for (int f = 0; f < 3; ++f)
+          acc[f] = mfma16x16x4(A[ab[f] + g * 36 + 4 * s], S[sb[f] + g * 4 * R::PS + roff[s]],
+                               acc[f]);
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      if (!live[f]) continue;
+      const int ch = (g0 + f * RB_NW) / R::NT;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = row0[f] - ch * R::C + r;  // channel of this register
+        if (n < R::C) Pc[(row0[f] + r) * R::PR + col[f]] = acc[f][r];
+      }
     }
   }
-  // channel of accumulator register r of tile f
-  __device__ __forceinline__ int chan(int f, int r) const {
-    return nr[f] * 16 + 4 * ((threadIdx.x & 63) >> 4) + r;
-  }
-};
-
-// gather offset of reduction index k = c*9 + t: c*PS + toff(t) (FLIP: toff(8 - t))
-template <class R, bool FLIP>
-__device__ __forceinline__ int rb_koff(int k) {
-  const int c = k / 9, t0 = k - 9 * c;
-  const int t = FLIP ? 8 - t0 : t0;
-  const int kh = t / 3;
-  return c * R::PS + kh * R::WP + (t - 3 * kh);
 }
 
-// acc[f] = A (channel tile nr[f]: 16 x K) x S gathered at base[f] + koff(k), f < 3 (a wave
-// with fewer tiles runs dummies on valid addresses: no branch in the loop)
-template <class R, bool FLIP>
-__device__ __forceinline__ void rb_mma(const float* __restrict__ A, const float* __restrict__ S,
-                                       const RBTiles<R>& tl, floatx4 (&acc)[3]) {
-  const int l = threadIdx.x & 63, j = l & 15, kq = l >> 4;
-  const float* ap[3];
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    ap[f] = A + ((R::NR == 1 ? 0 : tl.nr[f]) * 16 + j) * R::KST + kq;
-    acc[f] = floatx4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll 12
-  for (int q = 0; q < R::K; q += 4) {
-    const int ko = rb_koff<R, FLIP>(q + kq);
-    float av[3];
-    av[0] = ap[0][q];
-#pragma unroll
-    for (int f = 1; f < 3; ++f) av[f] = R::NR == 1 ? av[0] : ap[f][q];
-#pragma unroll
-    for (int f = 0; f < 3; ++f) acc[f] = mfma16x16x4(av[f], S[tl.base[f] + ko], acc[f]);
-  }
-}
-
-// Weight gradient of one image into its slab row: D[n][kc] = sum_p G[n][p] * B[p][kc],
-// B[p][kc] = S[koff(kc) + pos(p)] (kc < K), 1 (kc == K: bias), 0 beyond; rows n >= C are 0.
-// Wave wid takes tiles wid, wid+4, ... in groups of 3 interleaved chains; every load is
-// unconditional (clamped) so the position loop has no branch.
+// conv result at this lane's element (u, v): the chunk partials summed in chunk order
 template <class R>
-__device__ __forceinline__ void rb_wgrad(const float* __restrict__ G, const float* __restrict__ S,
-                                         float* __restrict__ slab_row) {
-  const int l = threadIdx.x & 63, wid = threadIdx.x >> 6, j = l & 15, kq = l >> 4;
-  for (int t0 = wid; t0 < R::WT; t0 += 12) {
-    int gofs[3], ko[3], kc[3], n0[3];
+__device__ __forceinline__ float rb_conv_at(const float* __restrict__ Pc, const RBElems<R>& el,
+                                            int u, int v) {
+  const int c = el.c[u] < R::C ? el.c[u] : 0, p = el.p[v] < R::P ? el.p[v] : 0;
+  float s = Pc[c * R::PR + p];
+#pragma unroll
+  for (int ch = 1; ch < R::NCH; ++ch) s += Pc[(ch * R::C + c) * R::PR + p];
+  return s;
+}
+
+// Weight gradient of one image: D[n][kc] = sum_p G[n][p] * B[p][kc], B[p][kc] =
+// S[koff(kc) + pos(p)] (kc < K), 1 (kc == K: bias), 0 beyond; rows n >= C are 0.  Items
+// (tile, position chunk); PSPL == 1: straight into the slab row, else the chunk partials to
+// Pw[(chunk*C + n)*KCR + kc] (rb_wgrad_sum adds them in chunk order).
+template <class R>
+__device__ __forceinline__ void rb_wgrad_items(const float* __restrict__ G,
+                                               const float* __restrict__ S, float* __restrict__ Pw,
+                                               float* __restrict__ slab_row) {
+  const int l = threadIdx.x & 63, j = l & 15, kq = l >> 4, wid = rb_wid();
+  for (int g0 = wid; g0 < R::NIW; g0 += 3 * RB_NW) {
+    int gofs[3], ko[3], kc[3], n0[3], pc[3];
     float cst[3];
-    bool colv[3], rowv[3];
+    bool colv[3], rowv[3], live[3];
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
-      const int t = t0 + 4 * f < R::WT ? t0 + 4 * f : t0;
-      const int nr = t / R::KT;
-      kc[f] = (t0 + 4 * f < R::WT ? t - nr * R::KT : R::KT) * 16 + j;  // dead tile: kc >= KC
+      const int i = g0 + f * RB_NW;
+      live[f] = i < R::NIW;
+      const int ii = live[f] ? i : g0;
+      const int tile = ii % R::WT;
+      pc[f] = ii / R::WT;
+      const int nr = tile / R::KT;
+      kc[f] = (tile - nr * R::KT) * 16 + j;
       n0[f] = nr * 16;
       colv[f] = kc[f] < R::K;
-      ko[f] = rb_koff<R, false>(colv[f] ? kc[f] : 0);
+      const int k = colv[f] ? kc[f] : 0, c = k / 9, t = k - 9 * c, kh = t / 3;
+      ko[f] = c * R::PS + kh * R::WP + (t - 3 * kh) + pc[f] * 0;
       cst[f] = kc[f] == R::K ? 1.f : 0.f;
       const int n = nr * 16 + j;
       rowv[f] = n < R::C;
@@ -260,11 +315,12 @@ __device__ __forceinline__ void rb_wgrad(const float* __restrict__ G, const floa
     floatx4 acc[3];
 #pragma unroll
     for (int f = 0; f < 3; ++f) acc[f] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-    for (int p0 = 0; p0 < R::P; p0 += 4) {
-      const int po = (p0 / R::W) * R::WP + (p0 % R::W) + kq;  // 4 | W: same row
+#pragma unroll
+    for (int s = 0; s < R::WSTEPS; ++s) {
 #pragma unroll
       for (int f = 0; f < 3; ++f) {
+        const int p0 = (pc[f] * R::WSTEPS + s) * 4;           // 4 | W: one row
+        const int po = (p0 / R::W) * R::WP + (p0 % R::W) + kq;
         const float ga = G[gofs[f] + po];
         const float sb = S[ko[f] + po];
         acc[f] = mfma16x16x4(rowv[f] ? ga : 0.f, colv[f] ? sb : cst[f], acc[f]);
@@ -272,54 +328,50 @@ __device__ __forceinline__ void rb_wgrad(const float* __restrict__ G, const floa
     }
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
-      if (kc[f] >= R::KC) continue;
+      if (!live[f] || kc[f] >= R::KC) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0[f] + 4 * kq + r;
-        if (n < R::C) slab_row[n * R::KC + kc[f]] = acc[f][r];
+        if (n >= R::C) continue;
+        if (R::PSPL == 1)
+          slab_row[n * R::KC + kc[f]] = acc[f][r];
+        else
+          Pw[(pc[f] * R::C + n) * R::KCR + kc[f]] = acc[f][r];
       }
     }
   }
 }
 
-// s[i][f][r]: this lane's partials of channel tl.chan(f, r) (0 for dead tiles / channels)
-// -> summed over the lane's tiles of one channel tile, staged in LDS (red: NR*4*64*4*NS
-// doubles) -> thread (n, i) sums its channel's 64 lane values in a fixed order ->
-// part[(n*B + b)*NS + i] (write-through, for the last block)
-template <class R, int NS>
-__device__ __forceinline__ void rb_channel_partials(double (&s)[NS][3][4], const RBTiles<R>& tl,
-                                                    double* red, int B, int b, double* part) {
-  const int l = threadIdx.x & 63, wid = threadIdx.x >> 6;
+template <class R>
+__device__ __forceinline__ void rb_wgrad_sum(const float* __restrict__ Pw,
+                                             float* __restrict__ slab_row) {
+  if (R::PSPL == 1) return;
+  for (int e = threadIdx.x; e < R::C * R::KC; e += RB_T) {
+    const int n = e / R::KC, kc = e - n * R::KC;
+    float s = Pw[n * R::KCR + kc];
 #pragma unroll
-  for (int nr = 0; nr < R::NR; ++nr) {
-    double v[NS][4];
-#pragma unroll
-    for (int i = 0; i < NS; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double t = 0.0;
-#pragma unroll
-        for (int f = 0; f < 3; ++f)
-          if (f < tl.nt && tl.nr[f] == nr) t += s[i][f][r];
-        v[i][r] = t;
-      }
-    double* dst = red + ((size_t)(nr * 4 + wid) * 64 + l) * 4 * NS;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int i = 0; i < NS; ++i) dst[r * NS + i] = v[i][r];
+    for (int pc = 1; pc < R::PSPL; ++pc) s += Pw[(pc * R::C + n) * R::KCR + kc];
+    slab_row[e] = s;
   }
-  __syncthreads();
-  if (threadIdx.x < R::C * NS) {
-    const int n = threadIdx.x / NS, i = threadIdx.x - n * NS;
-    const int nr = n >> 4, kq = (n & 15) >> 2, r = n & 3;
-    double t = 0.0;
-    for (int wv = 0; wv < 4; ++wv) {
-      const double* src = red + ((size_t)(nr * 4 + wv) * 64 + kq * 16) * 4 * NS + r * NS + i;
+}
+
+// per-channel fp64 sums of this lane's element values (fixed order: over v, then the xor
+// tree) -> lane 0 stores part[(c*B + b)*NS + i] write-through, for the last block
+template <class R, int NS>
+__device__ __forceinline__ void rb_channel_sums(double (&s)[NS][R::CPW][R::PPL],
+                                                const RBElems<R>& el, int B, int b,
+                                                double* part) {
 #pragma unroll
-      for (int jj = 0; jj < 16; ++jj) t += src[jj * 4 * NS];
+  for (int u = 0; u < R::CPW; ++u) {
+    if (el.c[u] >= R::C) continue;  // wave-uniform
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      double t = s[i][u][0];
+#pragma unroll
+      for (int v = 1; v < R::PPL; ++v) t += s[i][u][v];
+      t = wave_sum_d(t);
+      if ((threadIdx.x & 63) == 0) st_wt(part + ((int64_t)el.c[u] * B + b) * NS + i, t);
     }
-    st_wt(part + ((int64_t)n * B + b) * NS + i, t);
   }
 }
 
@@ -327,376 +379,319 @@ __device__ __forceinline__ void rb_channel_partials(double (&s)[NS][3][4], const
 template <class R>
 __global__ __launch_bounds__(RB_T) void rb_fwd1_kernel(RBArgs a) {
   extern __shared__ double rb_smem[];
-  float* prm = reinterpret_cast<float*>(rb_smem);  // a1 | b1
-  float* S = prm + 2 * R::CT;
+  float* S = reinterpret_cast<float*>(rb_smem);
   float* A = S + R::PLANE;
-  // the channel-partial staging [NR][4][64][4][2] doubles reuses the S / A region once
-  // the conv is done (rb_lds: the max of the two, not their sum -> more blocks per CU)
-  double* red = reinterpret_cast<double*>(S);
-  const int b = blockIdx.x, l = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* Pc = A + R::PANEL;
+  const int b = blockIdx.x, l = threadIdx.x & 63, wid = rb_wid();
   const int64_t img0 = (int64_t)b * R::C * R::P;
   RB_MARK(0);
-  float v[R::UE];
-  float pv[R::UP];
-  rb_load_img<R>(a.x, img0, v);
+  const RBElems<R> el;
+  float v[R::CPW][R::PPL], pv[R::UP], a1[R::CPW], b1[R::CPW];
+  rb_load<R>(a.x, img0, el, v);
   rb_load_panel<R, false>(a.w1, pv);
-  if (threadIdx.x < R::C) {
-    prm[threadIdx.x] = a.a1[threadIdx.x];
-    prm[R::CT + threadIdx.x] = a.b1 ? a.b1[threadIdx.x] : 0.f;
-  }
+  rb_param<R>(a.a1, el, a1);
+  rb_param<R>(a.b1, el, b1);
   rb_border<R>(S);
   rb_put_panel<R>(A, pv);
-  __syncthreads();
   RB_MARK(1);
-  rb_put_img<R>(S, v, v, [&](int c, int, float x, float) {
-    const float al = prm[c];
-    return snake_f(x, al, 1.0f / al);
-  });
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u)
+#pragma unroll
+    for (int q = 0; q < R::PPL; ++q)
+      if (el.ok(u, q)) S[el.cell(u, q)] = snake_f(v[u][q], a1[u], 1.0f / a1[u]);
   __syncthreads();
   RB_MARK(2);
-  const RBTiles<R> tl;
-  floatx4 acc[3];
-  rb_mma<R, false>(A, S, tl, acc);
+  rb_conv_items<R, false>(A, S, Pc);
+  __syncthreads();
   RB_MARK(3);
-  double s[2][3][4] = {};
+  double s[2][R::CPW][R::PPL];
 #pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    if (f >= tl.nt) continue;
+  for (int u = 0; u < R::CPW; ++u)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = tl.chan(f, r);
-      if (n < R::C) {
-        const float val = acc[f][r] + prm[R::CT + n];
-        a.h_out[img0 + (int64_t)n * R::P + tl.p[f]] = val;
-        s[0][f][r] = (double)val;
-        s[1][f][r] = (double)val * (double)val;
-      }
+    for (int q = 0; q < R::PPL; ++q) {
+      s[0][u][q] = s[1][u][q] = 0.0;
+      if (!el.ok(u, q)) continue;
+      const float val = rb_conv_at<R>(Pc, el, u, q) + b1[u];
+      a.h_out[el.gi(img0, u, q)] = val;
+      s[0][u][q] = (double)val;
+      s[1][u][q] = (double)val * (double)val;
     }
-  }
   RB_MARK(4);
-  __syncthreads();  // every wave's S / A reads are done before red overwrites them
-  rb_channel_partials<R, 2>(s, tl, red, a.B, b, a.part);
+  rb_channel_sums<R, 2>(s, el, a.B, b, a.part);
   RB_MARK(5);
   if (a.cnt && last_block(a.cnt, a.B))
-    for (int c = wid; c < R::C; c += 4) bn_final_channel(a.part, c, l, a.fin);
+    for (int c = wid; c < R::C; c += RB_NW) bn_final_channel(a.part, c, l, a.fin);
   RB_MARK(6);
 }
 
 template <class R>
 __global__ __launch_bounds__(RB_T) void rb_fwd2_kernel(RBArgs a) {
   extern __shared__ double rb_smem[];
-  float* prm = reinterpret_cast<float*>(rb_smem);  // a2 | scale | shift | b2
-  float* S = prm + 4 * R::CT;
+  float* S = reinterpret_cast<float*>(rb_smem);
   float* A = S + R::PLANE;
+  float* Pc = A + R::PANEL;
   const int b = blockIdx.x;
   const int64_t img0 = (int64_t)b * R::C * R::P;
   RB_MARK(0);
-  float v[R::UE];
-  float pv[R::UP];
-  rb_load_img<R>(a.h, img0, v);
+  const RBElems<R> el;
+  float v[R::CPW][R::PPL], xr[R::CPW][R::PPL], pv[R::UP];
+  float a2[R::CPW], sc[R::CPW], sh[R::CPW], b2[R::CPW];
+  rb_load<R>(a.h, img0, el, v);
   rb_load_panel<R, false>(a.w2, pv);
-  const RBTiles<R> tl;
-  float xr[3][4];  // the residual at this lane's outputs
-#pragma unroll
-  for (int f = 0; f < 3; ++f)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = tl.chan(f, r);
-      xr[f][r] = a.x[img0 + (int64_t)(n < R::C ? n : 0) * R::P + tl.p[f]];
-    }
-  if (threadIdx.x < R::C) {
-    const int c = threadIdx.x;
-    prm[c] = a.a2[c];
-    prm[R::CT + c] = a.save[2 * R::C + c];
-    prm[2 * R::CT + c] = a.save[3 * R::C + c];
-    prm[3 * R::CT + c] = a.b2 ? a.b2[c] : 0.f;
-  }
+  rb_load<R>(a.x, img0, el, xr);
+  rb_param<R>(a.a2, el, a2);
+  rb_param<R>(a.save + 2 * R::C, el, sc);
+  rb_param<R>(a.save + 3 * R::C, el, sh);
+  rb_param<R>(a.b2, el, b2);
   rb_border<R>(S);
   rb_put_panel<R>(A, pv);
-  __syncthreads();
   RB_MARK(1);
-  rb_put_img<R>(S, v, v, [&](int c, int, float hv, float) {
-    const float al = prm[c];
-    return snake_f(fmaf(hv, prm[R::CT + c], prm[2 * R::CT + c]), al, 1.0f / al);
-  });
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u)
+#pragma unroll
+    for (int q = 0; q < R::PPL; ++q)
+      if (el.ok(u, q)) S[el.cell(u, q)] = snake_f(fmaf(v[u][q], sc[u], sh[u]), a2[u], 1.0f / a2[u]);
   __syncthreads();
   RB_MARK(2);
-  floatx4 acc[3];
-  rb_mma<R, false>(A, S, tl, acc);
+  rb_conv_items<R, false>(A, S, Pc);
+  __syncthreads();
   RB_MARK(3);
   const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
 #pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    if (f >= tl.nt) continue;
+  for (int u = 0; u < R::CPW; ++u)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = tl.chan(f, r);
-      if (n < R::C) {
-        const int64_t gi = img0 + (int64_t)n * R::P + tl.p[f];
-        float val = acc[f][r] + prm[3 * R::CT + n];
-        if (a.drop_p > 0.f)
-          val = uniform01(seed, (uint64_t)gi) >= a.drop_p ? val * a.drop_scale : 0.f;
-        a.y[gi] = xr[f][r] + val;
-      }
+    for (int q = 0; q < R::PPL; ++q) {
+      if (!el.ok(u, q)) continue;
+      const int64_t gi = el.gi(img0, u, q);
+      float val = rb_conv_at<R>(Pc, el, u, q) + b2[u];
+      if (a.drop_p > 0.f)
+        val = uniform01(seed, (uint64_t)gi) >= a.drop_p ? val * a.drop_scale : 0.f;
+      a.y[gi] = xr[u][q] + val;
     }
-  }
 }
 
 template <class R>
 __global__ __launch_bounds__(RB_T) void rb_eval_kernel(RBArgs a) {
   extern __shared__ double rb_smem[];
-  float* prm = reinterpret_cast<float*>(rb_smem);  // a1 | b1 | scale | shift | a2 | b2
-  float* S1 = prm + 6 * R::CT;
+  float* S1 = reinterpret_cast<float*>(rb_smem);
   float* S2 = S1 + R::PLANE;
-  float* A1 = S2 + R::PLANE;  // conv1's panel, then conv2's (one panel of LDS: more blocks
-                              // per CU; conv2's weights wait in registers meanwhile)
+  float* A = S2 + R::PLANE;  // conv1's panel, then conv2's (conv2's weights wait in registers)
+  float* Pc = A + R::PANEL;
   const int b = blockIdx.x;
   const int64_t img0 = (int64_t)b * R::C * R::P;
-  float v[R::UE];
-  float pv1[R::UP], pv2[R::UP];
-  rb_load_img<R>(a.x, img0, v);
+  const RBElems<R> el;
+  float v[R::CPW][R::PPL], pv1[R::UP], pv2[R::UP];
+  float a1[R::CPW], b1[R::CPW], a2[R::CPW], b2[R::CPW], sc[R::CPW], sh[R::CPW];
+  rb_load<R>(a.x, img0, el, v);
   rb_load_panel<R, false>(a.w1, pv1);
   rb_load_panel<R, false>(a.w2, pv2);
-  const RBTiles<R> tl;
-  float xr[3][4];
+  rb_param<R>(a.a1, el, a1);
+  rb_param<R>(a.b1, el, b1);
+  rb_param<R>(a.a2, el, a2);
+  rb_param<R>(a.b2, el, b2);
 #pragma unroll
-  for (int f = 0; f < 3; ++f)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = tl.chan(f, r);
-      xr[f][r] = a.x[img0 + (int64_t)(n < R::C ? n : 0) * R::P + tl.p[f]];
-    }
-  if (threadIdx.x < R::C) {
-    const int c = threadIdx.x;
-    // bn_eval_prep_kernel's affine form (then Snake, affine_snake_kernel)
+  for (int u = 0; u < R::CPW; ++u) {  // bn_eval_prep_kernel's affine form
+    const int c = el.c[u] < R::C ? el.c[u] : 0;
     const float inv = 1.0f / sqrtf(a.rvar[c] + a.eps);
-    const float sc = (a.bn_w ? a.bn_w[c] : 1.f) * inv;
-    prm[c] = a.a1[c];
-    prm[R::CT + c] = a.b1 ? a.b1[c] : 0.f;
-    prm[2 * R::CT + c] = sc;
-    prm[3 * R::CT + c] = (a.bn_b ? a.bn_b[c] : 0.f) - a.rmean[c] * sc;
-    prm[4 * R::CT + c] = a.a2[c];
-    prm[5 * R::CT + c] = a.b2 ? a.b2[c] : 0.f;
+    sc[u] = (a.bn_w ? a.bn_w[c] : 1.f) * inv;
+    sh[u] = (a.bn_b ? a.bn_b[c] : 0.f) - a.rmean[c] * sc[u];
   }
   rb_border<R>(S1);
   rb_border<R>(S2);
-  rb_put_panel<R>(A1, pv1);
-  __syncthreads();
-  rb_put_img<R>(S1, v, v, [&](int c, int, float x, float) {
-    const float al = prm[c];
-    return snake_f(x, al, 1.0f / al);
-  });
-  __syncthreads();
-  floatx4 acc[3];
-  rb_mma<R, false>(A1, S1, tl, acc);
+  rb_put_panel<R>(A, pv1);
 #pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    if (f >= tl.nt) continue;
+  for (int u = 0; u < R::CPW; ++u)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = tl.chan(f, r);
-      if (n < R::C) {
-        const float al = prm[4 * R::CT + n];
-        const float u = fmaf(acc[f][r] + prm[R::CT + n], prm[2 * R::CT + n], prm[3 * R::CT + n]);
-        S2[n * R::PS + tl.base[f] + R::WP + 1] = snake_f(u, al, 1.0f / al);
+    for (int q = 0; q < R::PPL; ++q)
+      if (el.ok(u, q)) S1[el.cell(u, q)] = snake_f(v[u][q], a1[u], 1.0f / a1[u]);
+  __syncthreads();
+  rb_conv_items<R, false>(A, S1, Pc);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u)
+#pragma unroll
+    for (int q = 0; q < R::PPL; ++q)
+      if (el.ok(u, q)) {
+        const float hv = fmaf(rb_conv_at<R>(Pc, el, u, q) + b1[u], sc[u], sh[u]);
+        S2[el.cell(u, q)] = snake_f(hv, a2[u], 1.0f / a2[u]);
       }
-    }
-  }
-  __syncthreads();  // S2 complete; every wave is done reading conv1's panel
-  rb_put_panel<R>(A1, pv2);
+  rb_put_panel<R>(A, pv2);  // every wave is past conv1 (the barrier above)
+  __syncthreads();          // S2, conv2's panel complete; conv1's partials consumed
+  rb_conv_items<R, false>(A, S2, Pc);
   __syncthreads();
-  rb_mma<R, false>(A1, S2, tl, acc);
 #pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    if (f >= tl.nt) continue;
+  for (int u = 0; u < R::CPW; ++u)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = tl.chan(f, r);
-      if (n < R::C)
-        a.y[img0 + (int64_t)n * R::P + tl.p[f]] = xr[f][r] + (acc[f][r] + prm[5 * R::CT + n]);
-    }
-  }
+    for (int q = 0; q < R::PPL; ++q)
+      if (el.ok(u, q)) a.y[el.gi(img0, u, q)] = v[u][q] + (rb_conv_at<R>(Pc, el, u, q) + b2[u]);
 }
 
 template <class R>
 __global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
   extern __shared__ double rb_smem[];
-  float* prm = reinterpret_cast<float*>(rb_smem);  // a2|scale|shift|mean|invstd
-  float* G = prm + 5 * R::CT;                      // g2 planes
+  float* G = reinterpret_cast<float*>(rb_smem);  // g2 planes
   float* S = G + R::PLANE;                         // s2 planes
   float* A = S + R::PLANE;                         // transposed w2
-  double* red = reinterpret_cast<double*>(G);      // [NR][4][64][4][3], after the convs
-  const int b = blockIdx.x, l = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* Pc = A + R::PANEL;
+  float* Pw = Pc + R::PARTC;
+  const int b = blockIdx.x, l = threadIdx.x & 63, wid = rb_wid();
   const int64_t img0 = (int64_t)b * R::C * R::P;
   RB_MARK(0);
-  float vg[R::UE], vh[R::UE];
-  float pv[R::UP];
-  rb_load_img<R>(a.dy, img0, vg);
-  rb_load_img<R>(a.h, img0, vh);
+  const RBElems<R> el;
+  float vg[R::CPW][R::PPL], vh[R::CPW][R::PPL], pv[R::UP];
+  float a2[R::CPW], sc[R::CPW], sh[R::CPW], mu[R::CPW], is[R::CPW];
+  rb_load<R>(a.dy, img0, el, vg);
+  rb_load<R>(a.h, img0, el, vh);
   rb_load_panel<R, true>(a.w2, pv);
-  const RBTiles<R> tl;
-  float hr[3][4];
-#pragma unroll
-  for (int f = 0; f < 3; ++f)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = tl.chan(f, r);
-      hr[f][r] = a.h[img0 + (int64_t)(n < R::C ? n : 0) * R::P + tl.p[f]];
-    }
-  if (threadIdx.x < R::C) {
-    const int c = threadIdx.x;
-    prm[c] = a.a2[c];
-    prm[R::CT + c] = a.save[2 * R::C + c];
-    prm[2 * R::CT + c] = a.save[3 * R::C + c];
-    prm[3 * R::CT + c] = a.save[c];
-    prm[4 * R::CT + c] = a.save[R::C + c];
-  }
+  rb_param<R>(a.a2, el, a2);
+  rb_param<R>(a.save + 2 * R::C, el, sc);
+  rb_param<R>(a.save + 3 * R::C, el, sh);
+  rb_param<R>(a.save, el, mu);
+  rb_param<R>(a.save + R::C, el, is);
   rb_border<R>(G);
   rb_border<R>(S);
   rb_put_panel<R>(A, pv);
-  __syncthreads();
   RB_MARK(1);
   const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
-  rb_put_img<R>(G, vg, vg, [&](int, int e, float d, float) {
-    if (a.drop_p > 0.f)
-      return uniform01(seed, (uint64_t)(img0 + e)) >= a.drop_p ? d * a.drop_scale : 0.f;
-    return d;
-  });
-  rb_put_img<R>(S, vh, vh, [&](int c, int, float hv, float) {
-    const float al = prm[c];
-    return snake_f(fmaf(hv, prm[R::CT + c], prm[2 * R::CT + c]), al, 1.0f / al);
-  });
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u)
+#pragma unroll
+    for (int q = 0; q < R::PPL; ++q) {
+      if (!el.ok(u, q)) continue;
+      float d = vg[u][q];
+      if (a.drop_p > 0.f)
+        d = uniform01(seed, (uint64_t)el.gi(img0, u, q)) >= a.drop_p ? d * a.drop_scale : 0.f;
+      G[el.cell(u, q)] = d;
+      S[el.cell(u, q)] = snake_f(fmaf(vh[u][q], sc[u], sh[u]), a2[u], 1.0f / a2[u]);
+    }
   __syncthreads();
   RB_MARK(2);
-  rb_wgrad<R>(G, S, a.slab2 + (int64_t)b * R::C * R::KC);
+  float* slab_row = a.slab2 + (int64_t)b * R::C * R::KC;
+  rb_wgrad_items<R>(G, S, Pw, slab_row);
   RB_MARK(3);
-  floatx4 acc[3];
-  rb_mma<R, true>(A, G, tl, acc);
+  rb_conv_items<R, true>(A, G, Pc);
+  __syncthreads();
   RB_MARK(4);
-  double s[3][3][4] = {};
+  rb_wgrad_sum<R>(Pw, slab_row);
+  double s[3][R::CPW][R::PPL];
 #pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    if (f >= tl.nt) continue;
+  for (int u = 0; u < R::CPW; ++u)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = tl.chan(f, r);
-      if (n >= R::C) continue;
-      const float av = prm[n], inv_a = 1.0f / av;
-      const float hv = hr[f][r];
-      const float gs = acc[f][r];  // d loss / d s2
-      const float u = fmaf(hv, prm[R::CT + n], prm[2 * R::CT + n]);
+    for (int q = 0; q < R::PPL; ++q) {
+      s[0][u][q] = s[1][u][q] = s[2][u][q] = 0.0;
+      if (!el.ok(u, q)) continue;
+      const float av = a2[u], inv_a = 1.0f / av;
+      const float hv = vh[u][q];
+      const float gs = rb_conv_at<R>(Pc, el, u, q);  // d loss / d s2
+      const float uu = fmaf(hv, sc[u], sh[u]);
       float sn, cs;
-      sincosf(av * u, &sn, &cs);
+      sincosf(av * uu, &sn, &cs);
       const float t = 2.0f * sn * cs;
       const float d = gs + gs * inv_a * t * av;  // d loss / d u (bn_bwd_partial_kernel)
-      const float xhat = (hv - prm[3 * R::CT + n]) * prm[4 * R::CT + n];
-      s[0][f][r] = d;
-      s[1][f][r] = (double)d * xhat;
-      s[2][f][r] = (double)(gs * inv_a * t * u) - (double)(gs * (sn * sn) * inv_a * inv_a);
-      a.du[img0 + (int64_t)n * R::P + tl.p[f]] = d;
+      const float xhat = (hv - mu[u]) * is[u];
+      s[0][u][q] = d;
+      s[1][u][q] = (double)d * xhat;
+      s[2][u][q] = (double)(gs * inv_a * t * uu) - (double)(gs * (sn * sn) * inv_a * inv_a);
+      a.du[el.gi(img0, u, q)] = d;
     }
-  }
   RB_MARK(5);
-  __syncthreads();  // G / S / A reads done before red overwrites them
-  rb_channel_partials<R, 3>(s, tl, red, a.B, b, a.part);
+  rb_channel_sums<R, 3>(s, el, a.B, b, a.part);
   RB_MARK(6);
   if (a.cnt && last_block(a.cnt, a.B))
-    for (int c = wid; c < R::C; c += 4) bn_bwd_final_channel(a.part, c, l, a.bfin);
+    for (int c = wid; c < R::C; c += RB_NW) bn_bwd_final_channel(a.part, c, l, a.bfin);
   RB_MARK(7);
 }
 
 template <class R>
 __global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
   extern __shared__ double rb_smem[];
-  float* prm = reinterpret_cast<float*>(rb_smem);  // a1|mean|invstd|w|mds|mdsx
-  float* G = prm + 6 * R::CT;                      // dh planes
+  float* G = reinterpret_cast<float*>(rb_smem);  // dh planes
   float* S = G + R::PLANE;                         // s1 planes
   float* A = S + R::PLANE;                         // transposed w1
-  double* red = reinterpret_cast<double*>(G);      // [NR][4][64][4][1], after the convs
-  const int b = blockIdx.x;
+  float* Pc = A + R::PANEL;
+  float* Pw = Pc + R::PARTC;
+  const int b = blockIdx.x, l = threadIdx.x & 63, wid = rb_wid();
   const int64_t img0 = (int64_t)b * R::C * R::P;
-  float vd[R::UE], vh[R::UE], vx[R::UE];
-  float pv[R::UP];
-  rb_load_img<R>(a.du, img0, vd);
-  rb_load_img<R>(a.h, img0, vh);
-  rb_load_img<R>(a.x, img0, vx);
+  RB_MARK(0);
+  const RBElems<R> el;
+  float vd[R::CPW][R::PPL], vh[R::CPW][R::PPL], vx[R::CPW][R::PPL], vy[R::CPW][R::PPL];
+  float pv[R::UP], a1[R::CPW], mu[R::CPW], is[R::CPW], bw[R::CPW], md[R::CPW], mx[R::CPW];
+  rb_load<R>(a.du, img0, el, vd);
+  rb_load<R>(a.h, img0, el, vh);
+  rb_load<R>(a.x, img0, el, vx);
   rb_load_panel<R, true>(a.w1, pv);
-  const RBTiles<R> tl;
-  float xr[3][4], gr[3][4];
+  rb_load<R>(a.dy, img0, el, vy);
+  rb_param<R>(a.a1, el, a1);
+  rb_param<R>(a.save, el, mu);
+  rb_param<R>(a.save + R::C, el, is);
+  rb_param<R>(a.bn_w, el, bw, 1.f);
 #pragma unroll
-  for (int f = 0; f < 3; ++f)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = tl.chan(f, r);
-      const int64_t gi = img0 + (int64_t)(n < R::C ? n : 0) * R::P + tl.p[f];
-      xr[f][r] = a.x[gi];
-      gr[f][r] = a.dy[gi];
-    }
-  if (threadIdx.x < R::C) {
-    const int c = threadIdx.x;
-    prm[c] = a.a1[c];
-    prm[R::CT + c] = a.save[c];
-    prm[2 * R::CT + c] = a.save[R::C + c];
-    prm[3 * R::CT + c] = a.bn_w ? a.bn_w[c] : 1.f;
-    prm[4 * R::CT + c] = a.coef[2 * c] * a.invN;
-    prm[5 * R::CT + c] = a.coef[2 * c + 1] * a.invN;
+  for (int u = 0; u < R::CPW; ++u) {
+    const int c = el.c[u] < R::C ? el.c[u] : 0;
+    md[u] = a.coef[2 * c] * a.invN;
+    mx[u] = a.coef[2 * c + 1] * a.invN;
   }
   rb_border<R>(G);
   rb_border<R>(S);
   rb_put_panel<R>(A, pv);
-  __syncthreads();
+  RB_MARK(1);
   // dh = w*invstd*(du - mean(du) - xhat*mean(du*xhat))  (bn_bwd_apply_kernel)
-  rb_put_img<R>(G, vd, vh, [&](int c, int, float d, float hv) {
-    const float is = prm[2 * R::CT + c];
-    const float xhat = (hv - prm[R::CT + c]) * is;
-    return prm[3 * R::CT + c] * is * (d - prm[4 * R::CT + c] - xhat * prm[5 * R::CT + c]);
-  });
-  rb_put_img<R>(S, vx, vx, [&](int c, int, float x, float) {
-    const float al = prm[c];
-    return snake_f(x, al, 1.0f / al);
-  });
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u)
+#pragma unroll
+    for (int q = 0; q < R::PPL; ++q) {
+      if (!el.ok(u, q)) continue;
+      const float xhat = (vh[u][q] - mu[u]) * is[u];
+      G[el.cell(u, q)] = bw[u] * is[u] * (vd[u][q] - md[u] - xhat * mx[u]);
+      S[el.cell(u, q)] = snake_f(vx[u][q], a1[u], 1.0f / a1[u]);
+    }
   __syncthreads();
-  rb_wgrad<R>(G, S, a.slab1 + (int64_t)b * R::C * R::KC);
-  floatx4 acc[3];
-  rb_mma<R, true>(A, G, tl, acc);
-  double s[1][3][4] = {};
+  RB_MARK(2);
+  float* slab_row = a.slab1 + (int64_t)b * R::C * R::KC;
+  rb_wgrad_items<R>(G, S, Pw, slab_row);
+  RB_MARK(3);
+  rb_conv_items<R, true>(A, G, Pc);
+  __syncthreads();
+  RB_MARK(4);
+  rb_wgrad_sum<R>(Pw, slab_row);
+  double s[1][R::CPW][R::PPL];
 #pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    if (f >= tl.nt) continue;
+  for (int u = 0; u < R::CPW; ++u)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = tl.chan(f, r);
-      if (n >= R::C) continue;
-      const float av = prm[n], inv_a = 1.0f / av;
-      const float xv = xr[f][r];
-      const float gs = acc[f][r];  // d loss / d s1
+    for (int q = 0; q < R::PPL; ++q) {
+      s[0][u][q] = 0.0;
+      if (!el.ok(u, q)) continue;
+      const float av = a1[u], inv_a = 1.0f / av;
+      const float xv = vx[u][q];
+      const float gs = rb_conv_at<R>(Pc, el, u, q);  // d loss / d s1
       float sn, cs;
       sincosf(av * xv, &sn, &cs);
       const float t = 2.0f * sn * cs;
       // snake_bwd_kernel, plus the identity skip's gradient
-      a.dx[img0 + (int64_t)n * R::P + tl.p[f]] = (gs + gs * inv_a * t * av) + gr[f][r];
-      s[0][f][r] = (double)(gs * inv_a * t * xv) - (double)(gs * (sn * sn) * inv_a * inv_a);
+      a.dx[el.gi(img0, u, q)] = (gs + gs * inv_a * t * av) + vy[u][q];
+      s[0][u][q] = (double)(gs * inv_a * t * xv) - (double)(gs * (sn * sn) * inv_a * inv_a);
     }
-  }
-  __syncthreads();  // G / S / A reads done before red overwrites them
-  rb_channel_partials<R, 1>(s, tl, red, a.B, b, a.part1);
-  if (a.cnt && last_block(a.cnt, a.B) && threadIdx.x < 64)
-    for (int c = 0; c < R::C; ++c)
-      snake_bwd_final_channel(a.part1, R::C, a.B, c, a.da1, a.accumulate);
+  RB_MARK(5);
+  rb_channel_sums<R, 1>(s, el, a.B, b, a.part1);
+  RB_MARK(6);
+  if (a.cnt && last_block(a.cnt, a.B))
+    for (int c = wid; c < R::C; c += RB_NW) {
+      double t[1];
+      wave_chunk_sums<1>(a.part1, c, a.B, l, t);
+      if (l == 0) a.da1[c] = a.accumulate ? a.da1[c] + (float)t[0] : (float)t[0];
+    }
+  RB_MARK(7);
 }
 
 // ---------------------------------------------------------------- host side
 template <class R>
 static size_t rb_lds(int kind) {
-  const size_t CT = R::CT, PL = R::PLANE, PA = R::PANEL, RD = (size_t)R::NR * 1024 * 8;
+  const size_t PL = R::PLANE, PA = R::PANEL, PC = R::PARTC, PW = R::PARTW;
   switch (kind) {
-    // fwd1 / bwd2 / bwd1: the double channel-partial staging (n RD) aliases the conv
-    // region that follows the per-channel parameters
-    case 0: return 4 * 2 * CT + std::max(2 * RD, 4 * (PL + PA));       // fwd1
-    case 1: return 4 * (4 * CT + PL + PA);                              // fwd2
-    case 2: return 4 * (6 * CT + 2 * PL + PA);                          // eval
-    case 3: return 4 * 5 * CT + std::max(3 * RD, 4 * (2 * PL + PA));   // bwd2
-    default: return 4 * 6 * CT + std::max(RD, 4 * (2 * PL + PA));      // bwd1
+    case 0: return 4 * (PL + PA + PC);               // fwd1
+    case 1: return 4 * (PL + PA + PC);               // fwd2
+    case 2: return 4 * (2 * PL + PA + PC);           // eval
+    default: return 4 * (2 * PL + PA + PC + PW);     // bwd2, bwd1
   }
 }
 

@@ -7,6 +7,8 @@ loss_hist with the reference's logged scalar names (stage1.py:183-196).
 One fused STFT kernel produces both encoder inputs and both targets
 (stage1.py:101-113 + vq_vae.py:179-180).
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -19,6 +21,9 @@ from ..hip.signal import stft_encode
 from ..models import VectorQuantize, VQVAEDecoder, VQVAEEncoder
 from ..utils import (compute_downsample_rate, linear_warmup_cosine_annealingLR, quantize,
                      zero_pad_high_freq, zero_pad_low_freq)
+
+# diagnosis only: the stage1 bands a bench run computes (both by default)
+_BANDS = tuple(os.environ.get("TVQ_BENCH_BANDS", "HF,LF").split(","))
 
 
 class Stage1(nn.Module):
@@ -107,6 +112,8 @@ class Stage1(nn.Module):
         s = stft_encode(x, enc_l=True, enc_h=True, tgt_l=True, tgt_h=True)
         parts = {}
         for band in ("HF", "LF"):
+            if band not in _BANDS:  # diagnosis only (TVQ_BENCH_BANDS): time one band alone
+                continue
             with streams.branch(x.device, "s1" + band.lower()) as br:
                 br.inputs(s)
                 part = self._band(band, s)
@@ -121,6 +128,8 @@ class Stage1(nn.Module):
                 br.outputs(part)
         if self._sched is not None:
             self._sched.step()
+        if len(parts) < 2:
+            return lambda: {"loss": torch.zeros((), device=x.device)}
         return lambda: self._loss_hist(*self._assemble(parts))
 
     def training_step(self, batch, batch_idx):

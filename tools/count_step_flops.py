@@ -9,7 +9,10 @@ one-hot EMA matmul (vq.py:229's embed_sum as onehot.T @ x) is subtracted, since 
 segmented sum, not a GEMM.  Stage2 is counted
 with layer dropout off (every branch run: the upper bound of the per-step work).
 
-usage: python tools/count_step_flops.py [B] > profiles/r02_step_flops.json"""
+The sampler batch (BASELINE configs[4]: iterative decoding of 10 LF + 1 HF steps with the
+priors' forwards, then both decoders) is counted the same way, per 1024 trajectories.
+
+usage: python tools/count_step_flops.py [B] > profiles/r03_step_flops.json"""
 import json
 import os
 import sys
@@ -37,7 +40,10 @@ def main():
     K, hid = 512, 128
     tokens = B * (3 * 8 + 3 * 32)  # LF 3x8 and HF 3x32 token grids
     f1 -= 2 * hid * tokens * K  # one-hot EMA matmul of the restatement (stage1 only)
+    # sampler (BASELINE configs[4]): one batch = 10 LF + 1 HF prior forwards + both decoders
+    fs, bys = count(cpu_baseline.sampler_fn(num=B))
     out = {"batch_counted": B,
+           "sampler_gflop_per_1024": fs / B * 1024 / 1e9, "sampler_by_op": bys,
            "stage1_gflop_per_traj": f1 / B / 1e9, "stage2_gflop_per_traj": f2 / B / 1e9,
            "step_gflop_at_B256": (f1 + f2) / B * 256 / 1e9,
            "stage1_by_op": by1, "stage2_by_op": by2}
