@@ -440,6 +440,26 @@ int tvq_upsample_nearest_bwd(const float* dy, int64_t R, int64_t Lin, int64_t Lo
 int tvq_gelu_fwd(const float* x, int64_t n, float* y, tvq_stream_t stream);
 int tvq_gelu_bwd(const float* dy, const float* x, int64_t n, float* dx, tvq_stream_t stream);
 
+/* ---------------------------------------------------------------- fused LF prior (eval)
+ * BidirectionalTransformer.forward_lf (bidirectional_transformer.py:166-192, the
+ * x-transformers encoder of :92-110) in eval mode, as used by MaskGIT.first_pass
+ * (maskgit.py:294-355): embedding (cls row + token + position), project_in, post_emb_norm,
+ * `depth` pre-norm RMSNorm layers (2 heads x 64 attention, ff 128 + GELU), final norm,
+ * project_out, pred_head (Linear + GELU + LayerNorm(eps ln_eps)) and the tied logits
+ * h . tok_emb[:K]^T + bias[:, :K], one wave per sequence.  s: (B, n) tokens (row stride
+ * s_stride), n + 1 <= 32; cls_idx: (B) class indices or NULL (the null class n_classes);
+ * width must be 128.  weights: a HOST array of 5 + 10*depth + 7 device pointers, in order
+ *   tok_emb (K+1, 128), pos_emb (n+1, 128), class_condition_emb (n_classes+1, 128),
+ *   project_in W (128, 128), post_emb_norm gamma (128),
+ *   per layer: attn RMSNorm g, to_q, to_k, to_v (128, 128), to_out (128, 128),
+ *              ff RMSNorm g, ff.0.0 W (128, 128), b (128), ff.2 W (128, 128), b (128),
+ *   final_norm g, project_out W, pred_head.0 W, b, pred_head.2 W, b, bias (n, K+1).
+ * logits: (B, n, K). */
+int tvq_prior_lf_eval(const int64_t* s, int64_t B, int64_t n, int64_t s_stride,
+                      const int64_t* cls_idx, int64_t n_classes, int64_t width,
+                      const float* const* weights, int64_t depth, int64_t K, float ln_eps,
+                      float* logits, tvq_stream_t stream);
+
 /* ---------------------------------------------------------------- MaskGIT sampling
  * One iterative-decoding step of MaskGIT.first_pass / second_pass (maskgit.py:294-411):
  * tvq_maskgit_sample draws, for every token equal to mask_id, a code from

@@ -1,0 +1,353 @@
+// The LF MaskGIT prior's whole forward in eval mode (iterative decoding, maskgit.py:294-355
+// first_pass -> masked_prediction -> BidirectionalTransformer.forward_lf,
+// bidirectional_transformer.py:166-192 with the x-transformers encoder of :92-110) as ONE
+// launch per decoding step: one wave per sequence, every activation in registers.
+//
+//   x = cat(cls_emb[c], tok_emb[s] + pos_emb[:n])              (embed_assemble)
+//   x = LayerNorm_gamma(x W_in^T)                              (project_in, post_emb_norm)
+//   depth x { x += Attn(RMSNorm(x)) W_o^T ; x += W2 GELU(W1 RMSNorm(x) + b1) + b2 }
+//   x = RMSNorm(x) W_out^T                                     (final_norm, project_out)
+//   h = LayerNorm_{w,b,1e-12}(GELU(x W_p^T + b_p))              (pred_head)
+//   logits[:, i-1, k] = h_i . tok_emb[k] + bias[i-1, k],  i = 1..n, k < K   (tied logits)
+//
+// Layout ("token on the lane"): the sequence (n + 1 <= 32 tokens, cls first) sits on the 32
+// columns of v_mfma_f32_32x32x2_f32 tiles, lane l owning token l & 31 and, in its 16
+// accumulator registers per tile, feature rows crow(r, h) (h = l >> 5) of that token.  A
+// Linear y^T = W x^T then takes W as the A operand (lane = output feature, k = the step's
+// feature, straight from L1/L2 with 16-B loads) and x^T as the B operand: the B value of
+// step t is register t of the lane's own token -- the previous layer's output, never moved.
+// The same registers are the A operand of x W^T (token on the lane as the ROW), which is
+// how V comes out feature-on-the-lane for O^T = V^T P^T.  So attention is
+//   S^T = K Q^T (A = K regs, B = Q regs: one query per lane, its keys in registers),
+//   softmax over the registers + one xor-32 shuffle,
+//   O^T = V^T P^T (A = V regs, B = P regs),
+// and the out-projection / FF consume O^T / GELU(u)^T from registers.  Norm statistics
+// are a register sum + one xor-32 shuffle.  Per step and sequence this is 8448 MFMAs
+// (config.yaml LF prior: depth 4, width 128, 2 heads x 64, ff 128, K = 512); the
+// unfused path ran ~30 launches per step, each streaming activations through HBM.
+//
+// Arithmetic follows the unfused kernels' formulas (rmsnorm_fwd, layernorm_fwd, the GEMM
+// epilogue order (acc + bias) + residual, attention_fwd's softmax); sums over features run
+// in a different order (fp32, within the 1e-4 parity bar, tests/test_prior_eval.py).
+#include <math.h>
+
+#include "tvq_common.h"
+#include "tvq_gemm.h"
+
+namespace tvq {
+
+constexpr int PE_D = 128;     // prior width (hidden_dim == embed_dim), heads x 64 == 128
+constexpr int PE_MAXDEPTH = 8;
+constexpr int PE_FIXED = 5, PE_PER_LAYER = 10, PE_TAIL = 7;
+
+struct PriorLayer {
+  const float *g_attn, *wq, *wk, *wv, *wo, *g_ff, *w1, *b1, *w2, *b2;
+};
+struct PriorArgs {
+  const int64_t* s;
+  int64_t ss;  // row stride of s
+  const int64_t* cls;  // (B) class index, nullptr: the null class n_classes
+  int n_classes, B, n, K, depth;
+  const float *tok_emb, *pos_emb, *cls_emb, *w_in, *post_gamma;
+  PriorLayer L[PE_MAXDEPTH];
+  const float *g_final, *w_out, *wp, *bp, *ln_w, *ln_b, *bias;
+  float ln_eps;
+  float* logits;
+};
+
+__device__ __forceinline__ floatx16 pe_mfma(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int pe_crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ void pe_zero(floatx16& a) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a[i] = 0.f;
+}
+
+// a per-feature vector (D floats) in the register layout: v[tile][r] = p[32*tile + crow(r,h)]
+__device__ __forceinline__ void pe_load_vec(const float* __restrict__ p, int h, floatx16 (&v)[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 x = *reinterpret_cast<const float4*>(p + 32 * t + 8 * q + 4 * h);
+      v[t][4 * q] = x.x;
+      v[t][4 * q + 1] = x.y;
+      v[t][4 * q + 2] = x.z;
+      v[t][4 * q + 3] = x.w;
+    }
+}
+
+// acc += over NS MFMA steps t: (WA) A = W[row][kmap(t,h)], B = bv(t);  (!WA) A = bv(t),
+// B = W[row][kmap(t,h)];  kmap(t,h) = 32*(t>>4) + crow(t&15, h).  wr = W + row*ld + k0 + 4h.
+// Every W load of the tile is issued before the first MFMA (they retire in order).
+template <bool WA, int NS, class BV>
+__device__ __forceinline__ floatx16 pe_gemm(const float* __restrict__ wr, BV bv, floatx16 acc) {
+  float4 w[NS / 4];
+#pragma unroll
+  for (int T4 = 0; T4 < NS / 4; ++T4)
+    w[T4] = *reinterpret_cast<const float4*>(wr + 32 * (T4 >> 2) + 8 * (T4 & 3));
+#pragma unroll
+  for (int T4 = 0; T4 < NS / 4; ++T4) {
+    const float wv[4] = {w[T4].x, w[T4].y, w[T4].z, w[T4].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float b = bv(4 * T4 + e);
+      acc = WA ? pe_mfma(wv[e], b, acc) : pe_mfma(b, wv[e], acc);
+    }
+  }
+  return acc;
+}
+
+// y^T = W x^T over the full width (4 output tiles, K = 128): out[t] (no bias)
+__device__ __forceinline__ void pe_linear(const float* __restrict__ W, int r32, int h,
+                                          const floatx16 (&x)[4], floatx16 (&out)[4]) {
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot) {
+    floatx16 acc;
+    pe_zero(acc);
+    out[ot] = pe_gemm<true, 64>(W + (int64_t)(32 * ot + r32) * PE_D + 4 * h,
+                                [&](int t) { return x[t >> 4][t & 15]; }, acc);
+  }
+}
+
+// x-transformers RMSNorm (rmsnorm_fwd_kernel): x * (1 / max(|x|, 1e-12)) * sqrt(D) * g
+__device__ __forceinline__ void pe_rms(const floatx16 (&x)[4], const float* __restrict__ g, int h,
+                                       floatx16 (&y)[4]) {
+  float ss = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ss = fmaf(x[t][r], x[t][r], ss);
+  ss += __shfl_xor(ss, 32, 64);
+  const float inv = 1.0f / fmaxf(sqrtf(ss), 1e-12f);
+  const float scale = sqrtf((float)PE_D);
+  floatx16 gv[4];
+  pe_load_vec(g, h, gv);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) y[t][r] = x[t][r] * inv * scale * gv[t][r];
+}
+
+// LayerNorm over the D features (layernorm_fwd_kernel): (x - mean) * rstd * w (+ b)
+__device__ __forceinline__ void pe_layernorm(floatx16 (&x)[4], const float* __restrict__ w,
+                                             const float* __restrict__ b, float eps, int h) {
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += x[t][r];
+  s += __shfl_xor(s, 32, 64);
+  const float mean = s / (float)PE_D;
+  float v = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float d = x[t][r] - mean;
+      v = fmaf(d, d, v);
+    }
+  v += __shfl_xor(v, 32, 64);
+  const float rstd = 1.0f / sqrtf(v / (float)PE_D + eps);
+  floatx16 wv[4], bv[4];
+  pe_load_vec(w, h, wv);
+  if (b) pe_load_vec(b, h, bv);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float y = (x[t][r] - mean) * rstd * wv[t][r];
+      if (b) y += bv[t][r];
+      x[t][r] = y;
+    }
+}
+
+__global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a) {
+  const int b = blockIdx.x, l = threadIdx.x, r32 = l & 31, h = l >> 5;
+  const int n = a.n, ntok = a.n + 1;  // tokens incl. cls (<= 32)
+  const bool live = r32 < ntok;
+  // ---- embedding: cls row, then token + position rows (zeros on the padding lanes)
+  floatx16 x[4];
+  {
+    const float* src;
+    const float* pos = nullptr;
+    if (r32 == 0) {
+      const int64_t c = a.cls ? a.cls[b] : (int64_t)a.n_classes;
+      src = a.cls_emb + c * PE_D;
+    } else {
+      const int i = live ? r32 - 1 : 0;
+      src = a.tok_emb + a.s[(int64_t)b * a.ss + i] * PE_D;
+      pos = a.pos_emb + (int64_t)i * PE_D;
+    }
+    pe_load_vec(src, h, x);
+    if (pos) {
+      floatx16 p[4];
+      pe_load_vec(pos, h, p);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) x[t][r] += p[t][r];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x[t][r] = live ? x[t][r] : 0.f;
+  }
+  // ---- project_in (no bias) + post_emb_norm (x-transformers LayerNorm: gamma only)
+  {
+    floatx16 y[4];
+    pe_linear(a.w_in, r32, h, x, y);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) x[t] = y[t];
+    pe_layernorm(x, a.post_gamma, nullptr, 1e-5f, h);
+  }
+  // ---- encoder layers (pre-norm, eval: every branch runs)
+  for (int li = 0; li < a.depth; ++li) {
+    const PriorLayer L = a.L[li];
+    floatx16 xn[4], y[4];
+    // attention branch: y = concat_h(softmax(Q_h K_h^T / 8) V_h) W_o^T
+    pe_rms(x, L.g_attn, h, xn);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) pe_zero(y[t]);
+#pragma unroll
+    for (int hd = 0; hd < 2; ++hd) {
+      floatx16 q[2], k[2], v[2], s, o[2];
+      auto bx = [&](int t) { return xn[t >> 4][t & 15]; };
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t row = (int64_t)(64 * hd + 32 * u + r32) * PE_D + 4 * h;
+        pe_zero(q[u]);
+        pe_zero(k[u]);
+        pe_zero(v[u]);
+        q[u] = pe_gemm<true, 64>(L.wq + row, bx, q[u]);   // Q^T: token on the lane
+        k[u] = pe_gemm<true, 64>(L.wk + row, bx, k[u]);   // K^T: token on the lane
+        v[u] = pe_gemm<false, 64>(L.wv + row, bx, v[u]);  // V: feature on the lane
+      }
+      // S^T = K Q^T: lane = query, registers = keys crow(i, h)
+      pe_zero(s);
+#pragma unroll
+      for (int t = 0; t < 32; ++t) s = pe_mfma(k[t >> 4][t & 15], q[t >> 4][t & 15], s);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float sv = pe_crow(i, h) < ntok ? s[i] * 0.125f : -INFINITY;  // 64^-1/2
+        s[i] = sv;
+        mx = fmaxf(mx, sv);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float e = expf(s[i] - mx);
+        s[i] = e;
+        sum += e;
+      }
+      sum += __shfl_xor(sum, 32, 64);
+      const float inv = 1.0f / sum;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] *= inv;
+      // O^T = V^T P^T: lane = query, registers = head features 32u + crow(r, h)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        pe_zero(o[u]);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) o[u] = pe_mfma(v[u][t], s[t], o[u]);
+      }
+      // y += W_o[:, 64hd : 64hd + 64] O_h^T
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot)
+        y[ot] = pe_gemm<true, 32>(L.wo + (int64_t)(32 * ot + r32) * PE_D + 64 * hd + 4 * h,
+                                  [&](int t) { return o[t >> 4][t & 15]; }, y[ot]);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x[t][r] = live ? y[t][r] + x[t][r] : 0.f;
+    // feed-forward branch: y = W2 GELU(W1 xn + b1) + b2
+    pe_rms(x, L.g_ff, h, xn);
+    floatx16 u[4], bv[4];
+    pe_linear(L.w1, r32, h, xn, u);
+    pe_load_vec(L.b1, h, bv);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) u[t][r] = gelu_erf(u[t][r] + bv[t][r]);
+    pe_linear(L.w2, r32, h, u, y);
+    pe_load_vec(L.b2, h, bv);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x[t][r] = live ? (y[t][r] + bv[t][r]) + x[t][r] : 0.f;
+  }
+  // ---- final_norm + project_out (no bias)
+  {
+    floatx16 xn[4];
+    pe_rms(x, a.g_final, h, xn);
+    pe_linear(a.w_out, r32, h, xn, x);
+  }
+  // ---- pred_head: LayerNorm_{w,b}(GELU(x W_p^T + b_p))
+  {
+    floatx16 y[4], bv[4];
+    pe_linear(a.wp, r32, h, x, y);
+    pe_load_vec(a.bp, h, bv);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x[t][r] = gelu_erf(y[t][r] + bv[t][r]);
+    pe_layernorm(x, a.ln_w, a.ln_b, a.ln_eps, h);
+  }
+  // ---- tied logits: lane = code, registers = tokens crow(r, h); the cls row is dropped
+  const int ldb = a.K + 1;
+  float* out = a.logits + (int64_t)b * n * a.K;
+  for (int c0 = 0; c0 < a.K; c0 += 32) {
+    const int code = c0 + r32;
+    const int crow_ = code < a.K ? code : a.K;  // the table has K + 1 rows
+    floatx16 acc;
+    pe_zero(acc);
+    acc = pe_gemm<false, 64>(a.tok_emb + (int64_t)crow_ * PE_D + 4 * h,
+                             [&](int t) { return x[t >> 4][t & 15]; }, acc);
+    if (code < a.K) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int tok = pe_crow(r, h);
+        if (tok >= 1 && tok <= n)
+          out[(int64_t)(tok - 1) * a.K + code] = acc[r] + a.bias[(int64_t)(tok - 1) * ldb + code];
+      }
+    }
+  }
+}
+
+}  // namespace tvq
+
+using namespace tvq;
+
+extern "C" int tvq_prior_lf_eval(const int64_t* s, int64_t B, int64_t n, int64_t s_stride,
+                                 const int64_t* cls_idx, int64_t n_classes, int64_t width,
+                                 const float* const* weights, int64_t depth, int64_t K,
+                                 float ln_eps, float* logits, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(s && weights && logits && B >= 1 && n >= 1 && n + 1 <= 32 && K >= 1 &&
+                    width == PE_D && depth >= 1 && depth <= PE_MAXDEPTH && n_classes >= 0,
+                "tvq_prior_lf_eval: unsupported shape (width 128, n + 1 <= 32, depth <= 8)");
+  PriorArgs a = {};
+  a.s = s; a.ss = s_stride; a.cls = cls_idx; a.n_classes = (int)n_classes;
+  a.B = (int)B; a.n = (int)n; a.K = (int)K; a.depth = (int)depth;
+  const float* const* w = weights;
+  a.tok_emb = w[0]; a.pos_emb = w[1]; a.cls_emb = w[2]; a.w_in = w[3]; a.post_gamma = w[4];
+  for (int i = 0; i < depth; ++i) {
+    const float* const* p = w + PE_FIXED + PE_PER_LAYER * i;
+    a.L[i] = {p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9]};
+  }
+  const float* const* t = w + PE_FIXED + PE_PER_LAYER * depth;
+  a.g_final = t[0]; a.w_out = t[1]; a.wp = t[2]; a.bp = t[3]; a.ln_w = t[4]; a.ln_b = t[5];
+  a.bias = t[6];
+  a.ln_eps = ln_eps;
+  a.logits = logits;
+  for (int i = 0; i < PE_FIXED + PE_PER_LAYER * depth + PE_TAIL; ++i)
+    TVQ_CHECK_ARG(w[i] != nullptr && ((uintptr_t)w[i] & 15) == 0,
+                  "tvq_prior_lf_eval: weight pointers must be non-null and 16-byte aligned");
+  hipLaunchKernelGGL(prior_lf_eval_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream,
+                     a);
+  return launch_status("tvq_prior_lf_eval");
+}

@@ -1,6 +1,7 @@
 """MaskGIT transformer ops on the HIP path (include/tvq.h §MaskGIT transformer)."""
 import contextlib
 import math
+import os
 
 import torch
 
@@ -508,3 +509,60 @@ class _GELU(torch.autograd.Function):
 
 def gelu(x):
     return _GELU.apply(x)
+
+
+# --------------------------------------------------------------------------- fused LF prior
+PRIOR_FUSED = os.environ.get("TVQ_PRIOR_FUSED", "1") != "0"
+
+
+def prior_lf_eval_supported(tf, s):
+    """Whether BidirectionalTransformer `tf` (an LF prior in eval mode, no gradient needed)
+    matches tvq_prior_lf_eval: width 128 everywhere (embed = hidden = heads * 64 = ff inner),
+    RMSNorm layers, depth <= 8, n + 1 <= 32 tokens, fp32 device weights."""
+    if not PRIOR_FUSED or tf.kind != "lf" or tf.training or not s.is_cuda:
+        return False
+    if torch.is_grad_enabled() and any(p.requires_grad for p in tf.parameters()):
+        return False
+    enc = tf.blocks.attn_layers
+    if enc.dim != 128 or tf.tok_emb_l.weight.shape[1] != 128 or len(enc.layers) > 16:
+        return False
+    if s.dim() != 2 or s.shape[1] + 1 > 32 or s.shape[1] != tf.num_tokens:
+        return False
+    for i, (norms, block, _) in enumerate(enc.layers):
+        if not hasattr(norms[0], "scale"):  # RMSNorm
+            return False
+        if i % 2 == 0:  # ("a", "f") * depth
+            if not hasattr(block, "to_q") or block.heads * 64 != 128:
+                return False
+        elif not hasattr(block, "ff") or block.ff[0][0].weight.shape[0] != 128:
+            return False
+    return all(p.dtype == torch.float32 and p.is_cuda and p.is_contiguous()
+               for p in tf.parameters())
+
+
+def prior_lf_eval(tf, s, class_idx=None):
+    """logits (B, n, K) of the LF prior in eval mode as ONE launch (csrc/tvq_prior_eval.hip):
+    the same function as forward_lf's unfused path (embedding, encoder, pred_head, tied
+    logits).  class_idx: (B,) / (B, 1) int64 or None (the null class)."""
+    import ctypes
+    enc = tf.blocks.attn_layers
+    w = [tf.tok_emb_l.weight, tf.pos_emb.weight, tf.class_condition_emb.weight,
+         tf.blocks.project_in.weight, tf.blocks.post_emb_norm.gamma]
+    for i in range(0, len(enc.layers), 2):
+        na, attn, _ = enc.layers[i]
+        nf, ff, _ = enc.layers[i + 1]
+        w += [na[0].g, attn.to_q.weight, attn.to_k.weight, attn.to_v.weight, attn.to_out.weight,
+              nf[0].g, ff.ff[0][0].weight, ff.ff[0][0].bias, ff.ff[2].weight, ff.ff[2].bias]
+    w += [enc.final_norm.g, tf.blocks.project_out.weight, tf.pred_head[0].weight,
+          tf.pred_head[0].bias, tf.pred_head[2].weight, tf.pred_head[2].bias, tf.bias]
+    arr = (ctypes.c_void_p * len(w))(*[ptr(t) for t in w])
+    s = s if s.stride(1) == 1 else s.contiguous()
+    B, n = s.shape
+    K = tf.codebook_size
+    cls = None
+    if class_idx is not None:
+        cls = class_idx.reshape(-1).long().contiguous()
+    logits = torch.empty((B, n, K), device=s.device, dtype=torch.float32)
+    call("tvq_prior_lf_eval", ptr(s), B, n, s.stride(0), ptr(cls), tf.n_classes, 128, arr,
+         len(enc.layers) // 2, K, float(tf.pred_head[2].eps), ptr(logits), stream_ptr())
+    return logits

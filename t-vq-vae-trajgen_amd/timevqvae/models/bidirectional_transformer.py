@@ -28,7 +28,8 @@ from ..hip.conv import conv2d
 from ..hip.linear import gemm, linear
 from ..hip.norm import bn_snake
 from ..hip.xf import (batch_colsum, embed_assemble, embedding, gelu, layer_norm, linear_act,
-                      qkv_attention, rmsnorm, rmsnorm_res, upsample_nearest_t)
+                      prior_lf_eval, prior_lf_eval_supported, qkv_attention, rmsnorm,
+                      rmsnorm_res, upsample_nearest_t)
 from ..hip._native import call, grad_sink, ptr, stream_ptr
 
 
@@ -354,6 +355,9 @@ class BidirectionalTransformer(nn.Module):
 
     def forward_lf(self, s_M_l, class_condition: Union[None, torch.Tensor] = None):
         """bidirectional_transformer.py:166-192."""
+        if prior_lf_eval_supported(self, s_M_l):
+            # eval (sampling): the whole prior as one launch per step (hip.xf.prior_lf_eval)
+            return prior_lf_eval(self, s_M_l, class_condition)
         device = s_M_l.device
         tok = self._tok(s_M_l, self.tok_emb_l.weight, "lf", self._site_l)
         cls_emb = self.class_embedding(class_condition, s_M_l.shape[0], device)

@@ -1,0 +1,73 @@
+"""The fused eval LF prior (csrc/tvq_prior_eval.hip, one launch per decoding step) against
+the unfused HIP path of BidirectionalTransformer.forward_lf and against the oracle
+restatement (oracle/tvq_oracle.transformer_forward; bidirectional_transformer.py:166-192,
+x-transformers restated as T1).  Tolerance: logits within 1e-4 relative (fp32; the fused
+kernel sums features in another order)."""
+import math
+
+import pytest
+import torch
+
+from oracle import tvq_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).norm() / b.norm())
+
+
+def _prior(cuda, depth=4, K=512, n=24, seed=7):
+    from timevqvae.models import BidirectionalTransformer
+    m = BidirectionalTransformer("lf", n, {"lf": K, "hf": K}, 128, hidden_dim=128, n_layers=depth,
+                                 heads=2, ff_mult=1, use_rmsnorm=True, p_unconditional=0.2,
+                                 n_classes=5)
+    gen = torch.Generator().manual_seed(seed)
+    sd = {}
+    for k, v in m.state_dict().items():
+        if not v.is_floating_point():
+            sd[k] = v
+        elif k.endswith((".g", ".gamma")) or (k.startswith("pred_head.2") and k.endswith("weight")):
+            sd[k] = 1.0 + 0.1 * torch.randn(v.shape, generator=gen)
+        else:
+            sd[k] = torch.randn(v.shape, generator=gen) * (
+                0.5 / math.sqrt(max(v.shape[-1], 1)) if v.dim() > 1 else 0.1)
+    m.load_state_dict(sd)
+    return m.to(cuda).eval(), sd
+
+
+@pytest.mark.parametrize("depth,K,n,B,cond", [(4, 512, 24, 64, False), (4, 512, 24, 37, True),
+                                              (2, 64, 24, 16, False), (1, 100, 7, 9, True)])
+def test_fused_prior_matches_unfused_and_oracle(depth, K, n, B, cond, cuda):
+    from timevqvae.hip import xf
+    m, sd = _prior(cuda, depth, K, n)
+    gen = torch.Generator().manual_seed(11)
+    s = torch.randint(0, K + 1, (B, n), generator=gen)  # mask id K included
+    y = torch.randint(0, 5, (B, 1), generator=gen) if cond else None
+    sg, yg = s.to(cuda), (y.to(cuda) if cond else None)
+    with torch.no_grad():
+        assert xf.prior_lf_eval_supported(m, sg)
+        fused = m(sg, class_condition=yg)
+        xf.PRIOR_FUSED = False
+        try:
+            unfused = m(sg, class_condition=yg)
+        finally:
+            xf.PRIOR_FUSED = True
+    cls = y if cond else torch.full((B, 1), 5, dtype=torch.long)
+    ref = O.transformer_forward(O.Ctx(False), sd, "lf", s, None, cls, K, 2, depth)
+    assert fused.shape == unfused.shape == ref.shape == (B, n, K)
+    assert rel(fused, unfused) < 1e-4, rel(fused, unfused)
+    assert rel(fused, ref) < 1e-4, rel(fused, ref)
+    assert float((fused.cpu() - ref).abs().max()) <= 1e-3 * float(ref.abs().max())
+
+
+def test_fused_prior_not_used_when_training_or_grad(cuda):
+    from timevqvae.hip import xf
+    m, _ = _prior(cuda, 1, 64, 24)
+    s = torch.randint(0, 65, (4, 24), device=cuda)
+    assert not xf.prior_lf_eval_supported(m, s)  # parameters require grad, grad enabled
+    with torch.no_grad():
+        assert xf.prior_lf_eval_supported(m, s)
+        m.train()
+        assert not xf.prior_lf_eval_supported(m, s)
