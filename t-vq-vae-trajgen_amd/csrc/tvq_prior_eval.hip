@@ -26,6 +26,16 @@
 // (config.yaml LF prior: depth 4, width 128, 2 heads x 64, ff 128, K = 512); the
 // unfused path ran ~30 launches per step, each streaming activations through HBM.
 //
+// Weights: every Linear's 32-row tiles are consumed in one fixed order (project_in, per
+// layer q/k/v per head and the head's out-projection columns, ff1, ff2, then project_out,
+// pred_head, the tied-logit code tiles).  prior_pack_kernel writes them once per call
+// into a stream in the MFMA operand order (tile -> 16-B group T4 -> lane): every load is one
+// coalesced 1-KB row, and each wave loads the first groups of tile i+1 while it multiplies
+// tile i, so a tile never starts on an L2 round trip.  (A 4-wave block staging the stream
+// through a 2 x 16 KB LDS ring with one barrier per tile measured slower: 591 vs 431 us per
+// launch for the unpipelined direct loads, the barriers and LDS reads exposed at one wave
+// per SIMD.)
+//
 // Arithmetic follows the unfused kernels' formulas (rmsnorm_fwd, layernorm_fwd, the GEMM
 // epilogue order (acc + bias) + residual, attention_fwd's softmax); sums over features run
 // in a different order (fp32, within the 1e-4 parity bar, tests/test_prior_eval.py).
@@ -65,6 +75,69 @@ __device__ __forceinline__ void pe_zero(floatx16& a) {
   for (int i = 0; i < 16; ++i) a[i] = 0.f;
 }
 
+// ---- the weight-tile stream.  Tile idx (order of consumption) -> source rows.
+struct PeTile {
+  const float* w;  // row-major, ld = PE_D
+  int row0, k0, ns, rows;  // first row, first column, MFMA steps (64: K=128, 32: K=64)
+};
+__device__ __forceinline__ int pe_ntiles(int depth, int K) {
+  return 4 + 28 * depth + 8 + (K + 31) / 32;
+}
+__device__ __forceinline__ PeTile pe_tile(const PriorArgs& a, int idx) {
+  if (idx < 4) return {a.w_in, 32 * idx, 0, 64, PE_D};
+  idx -= 4;
+  if (idx < 28 * a.depth) {
+    const PriorLayer& L = a.L[idx / 28];
+    const int j = idx % 28;
+    if (j < 20) {
+      const int hd = j / 10, jj = j % 10;
+      if (jj < 6) {
+        const int u = jj / 3, m = jj % 3;
+        return {m == 0 ? L.wq : (m == 1 ? L.wk : L.wv), 64 * hd + 32 * u, 0, 64, PE_D};
+      }
+      return {L.wo, 32 * (jj - 6), 64 * hd, 32, PE_D};
+    }
+    if (j < 24) return {L.w1, 32 * (j - 20), 0, 64, PE_D};
+    return {L.w2, 32 * (j - 24), 0, 64, PE_D};
+  }
+  idx -= 28 * a.depth;
+  if (idx < 4) return {a.w_out, 32 * idx, 0, 64, PE_D};
+  idx -= 4;
+  if (idx < 4) return {a.wp, 32 * idx, 0, 64, PE_D};
+  idx -= 4;
+  return {a.tok_emb, 32 * idx, 0, 64, a.K};  // code rows >= K are packed as zeros
+}
+// float4 offset of tile idx in the stream: 1024 per 64-step tile, 512 per 32-step tile
+__device__ __forceinline__ int64_t pe_tile_off(int idx, int depth) {
+  int64_t off = 0;
+  if (idx > 4) {
+    const int lt = min(idx - 4, 28 * depth);  // layer tiles before idx
+    const int full = lt / 28, rem = lt % 28;
+    const int outproj = 8 * full + (rem <= 6 ? 0 : min(rem - 6, 4)) + (rem <= 16 ? 0 : min(rem - 16, 4));
+    off = (int64_t)1024 * idx - 512 * outproj;
+  } else {
+    off = (int64_t)1024 * idx;
+  }
+  return off;
+}
+
+// stream element e (float4) of tile t: group T4 = e / 64, lane l = e % 64 ->
+// W[row0 + (l & 31)][k0 + 32*(T4>>2) + 8*(T4&3) + 4*(l>>5) .. +3]
+__global__ __launch_bounds__(256) void prior_pack_kernel(PriorArgs a, float4* __restrict__ out) {
+  const PeTile t = pe_tile(a, blockIdx.x);
+  float4* dst = out + pe_tile_off(blockIdx.x, a.depth);
+  const int n4 = t.ns / 4 * 64;
+  for (int e = threadIdx.x; e < n4; e += 256) {
+    const int T4 = e >> 6, l = e & 63;
+    const int row = t.row0 + (l & 31);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < t.rows)
+      v = *reinterpret_cast<const float4*>(t.w + (int64_t)row * PE_D + t.k0 + 32 * (T4 >> 2) +
+                                           8 * (T4 & 3) + 4 * (l >> 5));
+    dst[e] = v;
+  }
+}
+
 // a per-feature vector (D floats) in the register layout: v[tile][r] = p[32*tile + crow(r,h)]
 __device__ __forceinline__ void pe_load_vec(const float* __restrict__ p, int h, floatx16 (&v)[4]) {
 #pragma unroll
@@ -79,36 +152,68 @@ __device__ __forceinline__ void pe_load_vec(const float* __restrict__ p, int h, 
     }
 }
 
-// acc += over NS MFMA steps t: (WA) A = W[row][kmap(t,h)], B = bv(t);  (!WA) A = bv(t),
-// B = W[row][kmap(t,h)];  kmap(t,h) = 32*(t>>4) + crow(t&15, h).  wr = W + row*ld + k0 + 4h.
-// Every W load of the tile is issued before the first MFMA (they retire in order).
+// Per-wave consumer of the stream (no LDS, no barrier): a tile's 16-B groups are one
+// coalesced 1-KB row each; the first 4 groups of the NEXT tile are loaded while the current
+// tile is multiplied, so each tile starts on operands already in registers and its other
+// groups arrive (in order) behind them.
+struct PeStream {
+  const float4* __restrict__ src;
+  int64_t off;  // float4 offset of the current tile
+  int idx, ntiles, depth, lane;
+  float4 pre[4];  // the current tile's groups 0..3
+};
+
+__device__ __forceinline__ void pe_stream_begin(PeStream& st) {
+  st.idx = 0;
+  st.off = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) st.pre[i] = st.src[i * 64 + st.lane];
+}
+
+// acc += over NS MFMA steps t of the stream's current tile: (WA) A = W[row][kmap(t,h)],
+// B = bv(t);  (!WA) A = bv(t), B = W[row][kmap(t,h)];  kmap(t,h) = 32*(t>>4) + crow(t&15, h).
 template <bool WA, int NS, class BV>
-__device__ __forceinline__ floatx16 pe_gemm(const float* __restrict__ wr, BV bv, floatx16 acc) {
-  float4 w[NS / 4];
+__device__ __forceinline__ floatx16 pe_gemm(PeStream& st, BV bv, floatx16 acc) {
+  constexpr int G = NS / 4;  // 16-B groups of the tile (>= 8)
+  const float4* cur = st.src + st.off;
+  float4 rest[G - 4];
 #pragma unroll
-  for (int T4 = 0; T4 < NS / 4; ++T4)
-    w[T4] = *reinterpret_cast<const float4*>(wr + 32 * (T4 >> 2) + 8 * (T4 & 3));
+  for (int i = 0; i < G - 4; ++i) rest[i] = cur[(4 + i) * 64 + st.lane];
+  const int nidx = st.idx + 1;
+  const int64_t noff = st.off + (int64_t)G * 64;
+  float4 nq[4];
+  if (nidx < st.ntiles) {
 #pragma unroll
-  for (int T4 = 0; T4 < NS / 4; ++T4) {
-    const float wv[4] = {w[T4].x, w[T4].y, w[T4].z, w[T4].w};
+    for (int i = 0; i < 4; ++i) nq[i] = st.src[noff + i * 64 + st.lane];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) nq[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int T4 = 0; T4 < G; ++T4) {
+    const float4 w4 = T4 < 4 ? st.pre[T4] : rest[T4 - 4];
+    const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float b = bv(4 * T4 + e);
       acc = WA ? pe_mfma(wv[e], b, acc) : pe_mfma(b, wv[e], acc);
     }
   }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) st.pre[i] = nq[i];
+  st.off = noff;
+  st.idx = nidx;
   return acc;
 }
 
 // y^T = W x^T over the full width (4 output tiles, K = 128): out[t] (no bias)
-__device__ __forceinline__ void pe_linear(const float* __restrict__ W, int r32, int h,
-                                          const floatx16 (&x)[4], floatx16 (&out)[4]) {
+__device__ __forceinline__ void pe_linear(PeStream& st, const floatx16 (&x)[4],
+                                          floatx16 (&out)[4]) {
 #pragma unroll
   for (int ot = 0; ot < 4; ++ot) {
     floatx16 acc;
     pe_zero(acc);
-    out[ot] = pe_gemm<true, 64>(W + (int64_t)(32 * ot + r32) * PE_D + 4 * h,
-                                [&](int t) { return x[t >> 4][t & 15]; }, acc);
+    out[ot] = pe_gemm<true, 64>(st, [&](int t) { return x[t >> 4][t & 15]; }, acc);
   }
 }
 
@@ -164,10 +269,20 @@ __device__ __forceinline__ void pe_layernorm(floatx16 (&x)[4], const float* __re
     }
 }
 
-__global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a) {
-  const int b = blockIdx.x, l = threadIdx.x, r32 = l & 31, h = l >> 5;
+// one wave (64 threads) per sequence
+__global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
+                                                           const float4* __restrict__ wstream) {
+  const int l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
+  const bool seq_ok = true;
+  const int b = blockIdx.x;
   const int n = a.n, ntok = a.n + 1;  // tokens incl. cls (<= 32)
   const bool live = r32 < ntok;
+  PeStream st;
+  st.src = wstream;
+  st.ntiles = pe_ntiles(a.depth, a.K);
+  st.depth = a.depth;
+  st.lane = l;
+  pe_stream_begin(st);
   // ---- embedding: cls row, then token + position rows (zeros on the padding lanes)
   floatx16 x[4];
   {
@@ -198,7 +313,7 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a) {
   // ---- project_in (no bias) + post_emb_norm (x-transformers LayerNorm: gamma only)
   {
     floatx16 y[4];
-    pe_linear(a.w_in, r32, h, x, y);
+    pe_linear(st, x, y);
 #pragma unroll
     for (int t = 0; t < 4; ++t) x[t] = y[t];
     pe_layernorm(x, a.post_gamma, nullptr, 1e-5f, h);
@@ -217,13 +332,12 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a) {
       auto bx = [&](int t) { return xn[t >> 4][t & 15]; };
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int64_t row = (int64_t)(64 * hd + 32 * u + r32) * PE_D + 4 * h;
         pe_zero(q[u]);
         pe_zero(k[u]);
         pe_zero(v[u]);
-        q[u] = pe_gemm<true, 64>(L.wq + row, bx, q[u]);   // Q^T: token on the lane
-        k[u] = pe_gemm<true, 64>(L.wk + row, bx, k[u]);   // K^T: token on the lane
-        v[u] = pe_gemm<false, 64>(L.wv + row, bx, v[u]);  // V: feature on the lane
+        q[u] = pe_gemm<true, 64>(st, bx, q[u]);   // Q^T: token on the lane
+        k[u] = pe_gemm<true, 64>(st, bx, k[u]);   // K^T: token on the lane
+        v[u] = pe_gemm<false, 64>(st, bx, v[u]);  // V: feature on the lane
       }
       // S^T = K Q^T: lane = query, registers = keys crow(i, h)
       pe_zero(s);
@@ -258,8 +372,7 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a) {
       // y += W_o[:, 64hd : 64hd + 64] O_h^T
 #pragma unroll
       for (int ot = 0; ot < 4; ++ot)
-        y[ot] = pe_gemm<true, 32>(L.wo + (int64_t)(32 * ot + r32) * PE_D + 64 * hd + 4 * h,
-                                  [&](int t) { return o[t >> 4][t & 15]; }, y[ot]);
+        y[ot] = pe_gemm<true, 32>(st, [&](int t) { return o[t >> 4][t & 15]; }, y[ot]);
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -268,13 +381,13 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a) {
     // feed-forward branch: y = W2 GELU(W1 xn + b1) + b2
     pe_rms(x, L.g_ff, h, xn);
     floatx16 u[4], bv[4];
-    pe_linear(L.w1, r32, h, xn, u);
+    pe_linear(st, xn, u);
     pe_load_vec(L.b1, h, bv);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) u[t][r] = gelu_erf(u[t][r] + bv[t][r]);
-    pe_linear(L.w2, r32, h, u, y);
+    pe_linear(st, u, y);
     pe_load_vec(L.b2, h, bv);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -285,12 +398,12 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a) {
   {
     floatx16 xn[4];
     pe_rms(x, a.g_final, h, xn);
-    pe_linear(a.w_out, r32, h, xn, x);
+    pe_linear(st, xn, x);
   }
   // ---- pred_head: LayerNorm_{w,b}(GELU(x W_p^T + b_p))
   {
     floatx16 y[4], bv[4];
-    pe_linear(a.wp, r32, h, x, y);
+    pe_linear(st, x, y);
     pe_load_vec(a.bp, h, bv);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -303,12 +416,10 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a) {
   float* out = a.logits + (int64_t)b * n * a.K;
   for (int c0 = 0; c0 < a.K; c0 += 32) {
     const int code = c0 + r32;
-    const int crow_ = code < a.K ? code : a.K;  // the table has K + 1 rows
     floatx16 acc;
     pe_zero(acc);
-    acc = pe_gemm<false, 64>(a.tok_emb + (int64_t)crow_ * PE_D + 4 * h,
-                             [&](int t) { return x[t >> 4][t & 15]; }, acc);
-    if (code < a.K) {
+    acc = pe_gemm<false, 64>(st, [&](int t) { return x[t >> 4][t & 15]; }, acc);
+    if (seq_ok && code < a.K) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int tok = pe_crow(r, h);
@@ -323,10 +434,18 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a) {
 
 using namespace tvq;
 
+// bytes of the packed weight stream tvq_prior_lf_eval needs as its workspace
+extern "C" int64_t tvq_prior_lf_eval_workspace(int64_t depth, int64_t K) {
+  if (depth < 1 || depth > PE_MAXDEPTH || K < 1) return -1;
+  const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32;  // 64-step tiles
+  return (tiles64 * 1024 + depth * 8 * 512) * 16;
+}
+
 extern "C" int tvq_prior_lf_eval(const int64_t* s, int64_t B, int64_t n, int64_t s_stride,
                                  const int64_t* cls_idx, int64_t n_classes, int64_t width,
                                  const float* const* weights, int64_t depth, int64_t K,
-                                 float ln_eps, float* logits, tvq_stream_t stream) {
+                                 float ln_eps, float* logits, void* workspace,
+                                 tvq_stream_t stream) {
   TVQ_CHECK_ARG(s && weights && logits && B >= 1 && n >= 1 && n + 1 <= 32 && K >= 1 &&
                     width == PE_D && depth >= 1 && depth <= PE_MAXDEPTH && n_classes >= 0,
                 "tvq_prior_lf_eval: unsupported shape (width 128, n + 1 <= 32, depth <= 8)");
@@ -347,7 +466,13 @@ extern "C" int tvq_prior_lf_eval(const int64_t* s, int64_t B, int64_t n, int64_t
   for (int i = 0; i < PE_FIXED + PE_PER_LAYER * depth + PE_TAIL; ++i)
     TVQ_CHECK_ARG(w[i] != nullptr && ((uintptr_t)w[i] & 15) == 0,
                   "tvq_prior_lf_eval: weight pointers must be non-null and 16-byte aligned");
-  hipLaunchKernelGGL(prior_lf_eval_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream,
-                     a);
+  TVQ_CHECK_ARG(workspace && ((uintptr_t)workspace & 15) == 0,
+                "tvq_prior_lf_eval: workspace must be non-null and 16-byte aligned");
+  const int ntiles = 4 + 28 * (int)depth + 8 + (int)((K + 31) / 32);
+  hipStream_t st = (hipStream_t)stream;
+  float4* ws = reinterpret_cast<float4*>(workspace);
+  hipLaunchKernelGGL(prior_pack_kernel, dim3((unsigned)ntiles), dim3(256), 0, st, a, ws);
+  hipLaunchKernelGGL(prior_lf_eval_kernel, dim3((unsigned)B), dim3(64), 0, st, a,
+                     (const float4*)ws);
   return launch_status("tvq_prior_lf_eval");
 }

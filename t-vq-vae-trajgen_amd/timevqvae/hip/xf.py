@@ -562,7 +562,10 @@ def prior_lf_eval(tf, s, class_idx=None):
     cls = None
     if class_idx is not None:
         cls = class_idx.reshape(-1).long().contiguous()
+    depth = len(enc.layers) // 2
     logits = torch.empty((B, n, K), device=s.device, dtype=torch.float32)
+    ws = torch.empty(value("tvq_prior_lf_eval_workspace", depth, K), device=s.device,
+                     dtype=torch.uint8)
     call("tvq_prior_lf_eval", ptr(s), B, n, s.stride(0), ptr(cls), tf.n_classes, 128, arr,
-         len(enc.layers) // 2, K, float(tf.pred_head[2].eps), ptr(logits), stream_ptr())
+         depth, K, float(tf.pred_head[2].eps), ptr(logits), ptr(ws), stream_ptr())
     return logits
