@@ -1387,6 +1387,155 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(const float* __res
   }
 }
 
+// Weight (+ bias) gradient of a 3x3, stride-1, zero-padded conv on narrow (B, C, 3, W)
+// maps (instantiated for W = 8: the LF band's 64 / 128-channel ResBlock convs):
+//   dW[n][c*9 + tap] (+ dB[n]) = sum_{b, p} dY[b, n, p] * X[b, c, window(p, tap)].
+// conv_wgrad_halo_kernel staged one image per step and wrote one 64 x 577 slab per 1-3
+// images (43 MB of HBM traffic per op for 3.3 MB of algorithmic bytes).  Here block
+// (s, nb, cb) owns a 32-row x (CB*9 [+1]) column tile and W8_IMG images: it loads all their
+// dY rows (16-B loads) and input halo planes into LDS at once, the 4 waves each reduce a
+// quarter of the images over all of the tile's columns (5 x 2 independent 16x16x4 MFMA
+// chains), and the 4 partial tiles are summed in wave order through LDS.  One slab row
+// per W8_IMG images: S = B / W8_IMG splits, summed in order by the deferred slab sum.
+constexpr int W8_IMG = 16;
+
+template <int W, int CB>
+__global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restrict__ G,
+                                                           const float* __restrict__ X,
+                                                           float* __restrict__ slab, int B, int C,
+                                                           int N, int kcols, int PS) {
+  constexpr int P = 3 * W, WP = W + 2;
+  constexpr int GST = P + 4;                         // dY row stride in LDS (16-B aligned)
+  constexpr int KB = CB * 9 + 1, KT = (KB + 15) / 16;  // columns (+ bias), 16-col tiles
+  constexpr int TW = KT * 16;                        // combine-buffer row length
+  extern __shared__ float smem[];
+  float* Gs = smem;                                  // [IMG][32][GST]
+  float* Hs = smem + W8_IMG * 32 * GST;              // [IMG][CB + 1][PS] (plane CB: ones)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int j = lane & 15, kq = lane >> 4;
+  const int s = blockIdx.x, n0 = blockIdx.y * 32, c0 = blockIdx.z * CB;
+  const bool bias = c0 + CB >= C && kcols > C * 9;   // this block also owns the bias column
+  const int b0 = s * W8_IMG;
+  const int ni = min(W8_IMG, B - b0);
+  const int hs_img = (CB + 1) * PS;
+  // zero padding and the ones planes
+  for (int e = tid; e < W8_IMG * hs_img; e += 256) Hs[e] = (e % hs_img) >= CB * PS ? 1.f : 0.f;
+  __syncthreads();
+  {  // every load of the group in flight before the first LDS store
+    constexpr int GQ = P / 4, GU = (W8_IMG * 32 * GQ + 255) / 256;
+    float4 gv[GU];
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const int e = tid + u * 256;
+      const int ii = e / (32 * GQ), r = (e / GQ) % 32, q = e % GQ;
+      gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ii < ni && n0 + r < N)
+        gv[u] = *reinterpret_cast<const float4*>(G + ((int64_t)(b0 + ii) * N + n0 + r) * P + 4 * q);
+    }
+    constexpr int XQ = W / 4, XU = (W8_IMG * CB * 3 * XQ + 255) / 256;
+    float4 xv[XU];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const int e = tid + u * 256;
+      const int ii = e / (CB * 3 * XQ), c = (e / (3 * XQ)) % CB, hq = e % (3 * XQ);
+      xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ii < ni && c0 + c < C)
+        xv[u] = *reinterpret_cast<const float4*>(X + ((int64_t)(b0 + ii) * C + c0 + c) * P + 4 * hq);
+    }
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const int e = tid + u * 256;
+      if (e < W8_IMG * 32 * GQ) {
+        const int ii = e / (32 * GQ), r = (e / GQ) % 32, q = e % GQ;
+        *reinterpret_cast<float4*>(Gs + (ii * 32 + r) * GST + 4 * q) = gv[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const int e = tid + u * 256;
+      if (e < W8_IMG * CB * 3 * XQ) {
+        const int ii = e / (CB * 3 * XQ), c = (e / (3 * XQ)) % CB, hq = e % (3 * XQ);
+        const int h = hq / XQ, q = hq % XQ;
+        float* d = Hs + ii * hs_img + c * PS + (h + 1) * WP + 1 + 4 * q;
+        d[0] = xv[u].x; d[1] = xv[u].y; d[2] = xv[u].z; d[3] = xv[u].w;
+      }
+    }
+  }
+  __syncthreads();
+  int koff[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const int kl = t * 16 + j, c = kl / 9, tap = kl - 9 * c;
+    koff[t] = kl < CB * 9 ? c * PS + (tap / 3) * WP + (tap % 3) : CB * PS;
+  }
+  floatx4 acc[2][KT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < KT; ++t) acc[i][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int ii = wid; ii < ni; ii += 4) {
+    const float* gb = Gs + ii * 32 * GST + j * GST + kq;
+    const float* hb = Hs + ii * hs_img + kq;
+#pragma unroll
+    for (int m0 = 0; m0 < P; m0 += 4) {
+      const int base = (m0 / W) * WP + (m0 % W);   // positions m0 .. m0+3: one row
+      const float a0 = gb[m0], a1 = gb[16 * GST + m0];
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const float bv = hb[base + koff[t]];
+        acc[0][t] = mfma16x16x4(a0, bv, acc[0][t]);
+        acc[1][t] = mfma16x16x4(a1, bv, acc[1][t]);
+      }
+    }
+  }
+  __syncthreads();  // Gs / Hs reads done: the combine buffer aliases them
+  float* red = smem;  // [4 waves][32 rows][TW]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(wid * 32 + i * 16 + 4 * kq + r) * TW + t * 16 + j] = acc[i][t][r];
+  __syncthreads();
+  const int kb = CB * 9 + (bias ? 1 : 0);
+  float* out = slab + (int64_t)s * N * kcols;
+  for (int e = tid; e < 32 * kb; e += 256) {
+    const int row = e / kb, col = e - row * kb;
+    const int n = n0 + row;
+    if (n >= N) continue;
+    const float v = ((red[row * TW + col] + red[(32 + row) * TW + col]) +
+                     red[(64 + row) * TW + col]) + red[(96 + row) * TW + col];
+    const int kg = col < CB * 9 ? c0 * 9 + col : C * 9;
+    out[(int64_t)n * kcols + kg] = v;
+  }
+}
+
+template <int W, int CB>
+static size_t w8_lds(int PS) {
+  constexpr int P = 3 * W, GST = P + 4;
+  const size_t a = (size_t)W8_IMG * 32 * GST + (size_t)W8_IMG * (CB + 1) * PS;
+  const size_t red = (size_t)4 * 32 * (((CB * 9 + 1 + 15) / 16) * 16);
+  return 4 * (a > red ? a : red);
+}
+
+// the shapes conv_wgrad_w8_kernel takes (TVQ_CONV_W8=0 turns it off, for A/B)
+static bool w8_on() {
+  static const bool v = [] {
+    const char* e = getenv("TVQ_CONV_W8");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+static bool w8_fits(int64_t B, int64_t C, int64_t H, int64_t Wi, int64_t N, int64_t Wo, int64_t KH,
+                    int64_t KW, int64_t SW, int64_t replicate) {
+  return w8_on() && KH == 3 && KW == 3 && SW == 1 && !replicate && H == 3 && Wi == Wo &&
+         Wi == 8 && N % 32 == 0 && C % 8 == 0 && B % W8_IMG == 0;
+}
+static int64_t w8_ws(int64_t B, int64_t N, int64_t C) {
+  const int64_t S = B / W8_IMG, kc = C * 9 + 1;
+  return S * N * kc + reduce_rows_scratch(S, N * kc);
+}
+
 struct WHaloPlan {
   WHaloGeom g;
   int FN, S, nblk, cblk;
@@ -2411,7 +2560,8 @@ static int64_t conv_wgrad_ws(int64_t N, int64_t C, int64_t KH, int64_t KW, int64
                              int64_t Hout, int64_t Wo) {
   const int64_t a = wgrad_ws(N, C * KH * KW, B * Hout * Wo, nullptr, nullptr);
   const int64_t h = whalo_ws(N, C, KH, KW, B);
-  return a > h ? a : h;
+  const int64_t w = (KH == 3 && KW == 3 && B % W8_IMG == 0) ? w8_ws(B, N, C) : 0;
+  return std::max(a, std::max(h, w));
 }
 
 // op: 0 conv2d fwd, 1 convT2d fwd, 2 conv2d dgrad, 3 convT2d dgrad, 4 conv2d wgrad,
@@ -2475,6 +2625,22 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
                          (int)KW, PH_OF(KH), PW_OF(KW), Ci * KH * KW, KH * KW);
   const int kcols = g.Kred + (db ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
+  if (w8_fits(B, Ci, H, Wi, Co, Wo, KH, KW, SW, replicate)) {
+    const int S = (int)(B / W8_IMG);
+    const int PS = whalo_plane_stride(5 * ((int)Wi + 2), 9, 3, (int)Wi + 2, 1, 8);
+    const dim3 grid((unsigned)S, (unsigned)(Co / 32), (unsigned)(Ci / 8));
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_w8_kernel<8, 8>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+      attr = true;
+    }
+    const size_t lds = w8_lds<8, 8>(PS);
+    hipLaunchKernelGGL((conv_wgrad_w8_kernel<8, 8>), grid, dim3(256), lds, st, dy, x, workspace,
+                       (int)B, (int)Ci, (int)Co, kcols, PS);
+    wgrad_finish(workspace, S, Co, kcols, dw, db, (int)accumulate, st);
+    return launch_status("tvq_conv2d_wgrad(w8)");
+  }
   WHaloPlan pl;
   const bool halo = (g_conv_halo & 2) && whalo_plan((int)B, (int)Ci, (int)H, (int)Wi, (int)Co,
                                                     (int)H, (int)Wo, (int)KH, (int)KW, (int)SW,

@@ -24,21 +24,24 @@ __global__ __launch_bounds__(256) void maskgit_sample_kernel(
     const float* __restrict__ logits, int64_t sb, int64_t sn, int n, int K,
     const int64_t* __restrict__ s_in, int64_t mask_id, const float* __restrict__ u_cat,
     const int64_t* __restrict__ seed_ptr, uint64_t offset, int64_t* __restrict__ sampled,
-    float* __restrict__ selp) {
-  const int b = blockIdx.x;
+    float* __restrict__ selp, int nb) {
+  // one wave per token: token t = blockIdx.x * 4 + wave (all B*n tokens in flight at once;
+  // a block per sequence left each wave a serial loop over n / 4 tokens)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint64_t seed = u_cat ? 0ull : mix_seed(seed_ptr, offset);
   const int per = (K + 63) / 64;  // contiguous logits per lane
   const int j0 = lane * per;
-  for (int i = wid; i < n; i += 4) {
-    const int64_t t = (int64_t)b * n + i;
+  {
+    const int64_t t = (int64_t)blockIdx.x * 4 + wid;
+    if (t >= (int64_t)nb * n) return;
+    const int64_t b = t / n, i = t - b * n;
     const int64_t s0 = s_in[t];
     if (s0 != mask_id) {  // known token: kept, confidence +inf
       if (lane == 0) {
         sampled[t] = s0;
         selp[t] = INFINITY;
       }
-      continue;
+      return;
     }
     const float* l = logits + b * sb + i * sn;
     float m = -INFINITY;
@@ -46,13 +49,8 @@ __global__ __launch_bounds__(256) void maskgit_sample_kernel(
     m = wave_max(m);
     // double softmax numerators over the lane's contiguous chunk
     double part = 0.0;
-    float partf = 0.f;
-    for (int j = j0; j < min(K, j0 + per); ++j) {
-      part += exp((double)l[j] - (double)m);
-      partf += expf(l[j] - m);
-    }
+    for (int j = j0; j < min(K, j0 + per); ++j) part += exp((double)l[j] - (double)m);
     const double tot = wave_sum_dd(part);
-    const float totf = wave_sum(partf);
     // inclusive prefix of the lane chunks (probabilities), then the first chunk whose
     // running sum exceeds v = u * total (strictly: at u = 0 a leading zero-probability
     // code must not be drawn; torch's Categorical never samples one)
@@ -88,7 +86,8 @@ __global__ __launch_bounds__(256) void maskgit_sample_kernel(
     pick = __shfl(pick, src, 64);
     if (lane == 0) {
       sampled[t] = pick;
-      selp[t] = expf(l[pick] - m) / totf;
+      // p(sampled) of the softmax (maskgit.py:320-326), rounded once from the double terms
+      selp[t] = (float)(exp((double)l[pick] - (double)m) / tot);
     }
   }
 }
@@ -150,9 +149,9 @@ extern "C" int tvq_maskgit_sample(const float* logits, int64_t sb, int64_t sn, i
   TVQ_CHECK_ARG(logits && s_in && sampled && selp && B > 0 && n > 0 && K > 0,
                 "tvq_maskgit_sample: bad arguments");
   TVQ_CHECK_ARG(u_cat || seed_ptr, "tvq_maskgit_sample: need u_cat or a seed");
-  hipLaunchKernelGGL(maskgit_sample_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream,
-                     logits, sb, sn, (int)n, (int)K, s_in, mask_id, u_cat, seed_ptr, offset,
-                     sampled, selp);
+  hipLaunchKernelGGL(maskgit_sample_kernel, dim3((unsigned)((B * n + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, logits, sb, sn, (int)n, (int)K, s_in, mask_id, u_cat,
+                     seed_ptr, offset, sampled, selp, (int)B);
   return launch_status("tvq_maskgit_sample");
 }
 

@@ -634,3 +634,23 @@ def test_conv_wide_tile_matches_tap(op, cuda):
     else:
         ref = torch.nn.grad.conv2d_input(x.shape, w, dy, padding=pad)
     close(outs[0].cpu(), ref, what=op)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,Ci,Co", [(256, 64, 64), (256, 128, 64), (48, 64, 128), (40, 64, 64)])
+def test_conv_wgrad_narrow_image_batched(B, Ci, Co, cuda):
+    """conv_wgrad_w8_kernel (3x3 on (B, C, 3, 8) maps, 16 images per block, the 4 waves'
+    partial tiles summed in order) against torch fp32 on the CPU at the step's batch; B = 40
+    (not a multiple of 16) takes the halo kernel instead."""
+    from timevqvae.hip.conv import conv2d
+    gen = torch.Generator().manual_seed(B + Ci + Co)
+    x = torch.randn(B, Ci, 3, 8, generator=gen)
+    w = torch.randn(Co, Ci, 3, 3, generator=gen) * (Ci * 9) ** -0.5
+    b = torch.randn(Co, generator=gen)
+    g = torch.randn(B, Co, 3, 8, generator=gen)
+    wc, bc = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    F.conv2d(x, wc, bc, padding=(1, 1)).backward(g)
+    wd, bd = w.to(cuda).requires_grad_(True), b.to(cuda).requires_grad_(True)
+    conv2d(x.to(cuda), wd, bd).backward(g.to(cuda))
+    close(wd.grad, wc.grad, what="dw")
+    close(bd.grad, bc.grad, what="db")

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Every -m gpu test, smoke(), the full bench line, then a kernel trace of the graphed sampler.
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 180 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+grep "smoke ok" gpurun_out/smoke.log
+timeout -k 10 600 python bench.py > gpurun_out/bench_full.log 2>&1 || { tail -20 gpurun_out/bench_full.log; exit 1; }
+tail -1 gpurun_out/bench_full.log > gpurun_out/bench_full.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sg -o sg -- python tools/sampler_graph_prof.py 3 > gpurun_out/prof_sg.log 2>&1
+echo "rocprof rc=$?"
