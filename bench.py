@@ -353,13 +353,13 @@ def dominant_leg(device):
 
 
 def conv_wgrad_leg(device):
-    """The step's top kernel by summed time (profiles/r02e_step_kernel_stats.csv:
-    conv_wgrad_halo_kernel<3,3,1>, 12 launches per step): the LF band's 64 -> 64 3x3 conv
-    weight (+ bias) gradient on (256, 64, 3, 8), dW[64][577] = sum over 6144 positions of
-    dY x im2col(X) -> 2 * 6144 * 64 * 577 = 453.8 MFLOP and 4 * (2 * 6144 * 64 + 64 * 577)
-    = 3.29 MB algorithmic per op (AI 138 FLOP/B: fp32 MFMA bound).  One op = the halo kernel
-    (per-image-range slabs) + its ordered slab sum (in the step the sum is batched at the
-    band's end; here it follows each op).  50 graph-replayed ops timed with HIP events."""
+    """The LF band's 64 -> 64 3x3 conv weight (+ bias) gradient on (256, 64, 3, 8) (12
+    launches per step): dW[64][577] = sum over 6144 positions of dY x im2col(X) ->
+    2 * 6144 * 64 * 577 = 453.8 MFLOP and 4 * (2 * 6144 * 64 + 64 * 577) = 3.29 MB
+    algorithmic per op (AI 138 FLOP/B: fp32 MFMA bound).  One op = conv_wgrad_w8_kernel
+    (16 images per block, the 4 waves' partial tiles summed in LDS; 16 slab rows) + its
+    ordered slab sum (batched at the band's end in the step; here after each op).  50
+    graph-replayed ops timed with HIP events."""
     from timevqvae.hip._native import call, ptr, stream_ptr, value
     B, C, H, W, Co = 256, 64, 3, 8, 64
     x = torch.randn(B, C, H, W, device=device)
@@ -375,12 +375,12 @@ def conv_wgrad_leg(device):
     byts = 4.0 * (2 * B * H * W * C + Co * (C * 9 + 1))
     tf = flops / (us * 1e-6) / 1e12
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r02e_wgrad_traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "r03_wgrad_traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath))["traffic_bytes"]
-    return {"bound": "mfma", "kernel": "conv_wgrad_halo_kernel<3,3,1> + its ordered slab sum (LF "
+    return {"bound": "mfma", "kernel": "conv_wgrad_w8_kernel<8,8> + its ordered slab sum (LF "
                                        "64->64 3x3 conv weight+bias gradient over 6144 positions, "
-                                       "fp32 MFMA)",
+                                       "16 images per block, fp32 MFMA)",
             "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),

@@ -16,7 +16,7 @@ if [ "$LEG" = dominant ]; then
   python tools/roof_traffic.py $O $O/traffic.json "grouped weight gradients of the LF prior (16 Linears, 6400 tokens): wgrad_wide_kernel + wgrad_group_reduce_kernel" wgrad_wide_kernel wgrad_group_reduce_kernel
 fi
 if [ "$LEG" = wgrad ]; then
-  python tools/roof_traffic.py $O $O/traffic.json "LF 64->64 3x3 conv weight+bias gradient over 6144 positions: conv_wgrad_halo_kernel + reduce_rows_kernel" conv_wgrad_halo_kernel reduce_rows_kernel
+  python tools/roof_traffic.py $O $O/traffic.json "LF 64->64 3x3 conv weight+bias gradient over 6144 positions: conv_wgrad_w8_kernel + reduce_rows_kernel" conv_wgrad_w8_kernel reduce_rows_kernel
 fi
 if [ "$LEG" = rbbwd ]; then
   python tools/roof_traffic.py $O $O/traffic.json "fused ResBlock backward C=16 on (256,16,3,32): rb_bwd2_kernel + rb_bwd1_kernel + 2 ordered slab sums" rb_bwd2_kernel rb_bwd1_kernel reduce_rows

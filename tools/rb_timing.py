@@ -1,12 +1,16 @@
 """Per-block phase timestamps of the fused ResBlock kernels (timing build:
-lib/libtvq_hip_rbtime.so, tvq_resblock.hip compiled with -DRB_TIMING).
+lib_ab/libtvq_hip_rbtime.so, tvq_resblock.hip compiled with -DRB_TIMING).
+Marks (bwd1 / bwd2): m0 start, m1 loads issued + borders + panel stored, m2 inputs staged
+(barrier), m3 weight-gradient items done, m4 conv items done (barrier), m5 epilogue stored,
+m6 channel partials published, m7 last-block finish.  fwd1: m0 start, m1 panel stored,
+m2 staged, m3 conv done, m4 epilogue, m5 partials, m6 finish.
 usage: python tools/rb_timing.py"""
 import ctypes
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["TVQ_HIP_LIB"] = os.path.join(ROOT, "t-vq-vae-trajgen_amd", "lib", "libtvq_hip_rbtime.so")
+os.environ["TVQ_HIP_LIB"] = os.path.join(ROOT, "t-vq-vae-trajgen_amd", "lib_ab", "libtvq_hip_rbtime.so")
 sys.path.insert(0, os.path.join(ROOT, "t-vq-vae-trajgen_amd"))
 import torch  # noqa: E402
 
