@@ -79,33 +79,34 @@ __device__ __forceinline__ void pe_zero(floatx16& a) {
 struct PeTile {
   const float* w;  // row-major, ld = PE_D
   int row0, k0, ns, rows;  // first row, first column, MFMA steps (64: K=128, 32: K=64)
+  const float* gk;  // per-column factor folded into the packed tile (an RMSNorm's g), or null
 };
 __device__ __forceinline__ int pe_ntiles(int depth, int K) {
   return 4 + 28 * depth + 8 + (K + 31) / 32;
 }
 __device__ __forceinline__ PeTile pe_tile(const PriorArgs& a, int idx) {
-  if (idx < 4) return {a.w_in, 32 * idx, 0, 64, PE_D};
+  if (idx < 4) return {a.w_in, 32 * idx, 0, 64, PE_D, nullptr};
   idx -= 4;
   if (idx < 28 * a.depth) {
     const PriorLayer& L = a.L[idx / 28];
     const int j = idx % 28;
     if (j < 20) {
       const int hd = j / 10, jj = j % 10;
-      if (jj < 6) {
+      if (jj < 6) {  // q / k / v read RMSNorm_attn(x): its g is folded in
         const int u = jj / 3, m = jj % 3;
-        return {m == 0 ? L.wq : (m == 1 ? L.wk : L.wv), 64 * hd + 32 * u, 0, 64, PE_D};
+        return {m == 0 ? L.wq : (m == 1 ? L.wk : L.wv), 64 * hd + 32 * u, 0, 64, PE_D, L.g_attn};
       }
-      return {L.wo, 32 * (jj - 6), 64 * hd, 32, PE_D};
+      return {L.wo, 32 * (jj - 6), 64 * hd, 32, PE_D, nullptr};
     }
-    if (j < 24) return {L.w1, 32 * (j - 20), 0, 64, PE_D};
-    return {L.w2, 32 * (j - 24), 0, 64, PE_D};
+    if (j < 24) return {L.w1, 32 * (j - 20), 0, 64, PE_D, L.g_ff};
+    return {L.w2, 32 * (j - 24), 0, 64, PE_D, nullptr};
   }
   idx -= 28 * a.depth;
-  if (idx < 4) return {a.w_out, 32 * idx, 0, 64, PE_D};
+  if (idx < 4) return {a.w_out, 32 * idx, 0, 64, PE_D, a.g_final};
   idx -= 4;
-  if (idx < 4) return {a.wp, 32 * idx, 0, 64, PE_D};
+  if (idx < 4) return {a.wp, 32 * idx, 0, 64, PE_D, nullptr};
   idx -= 4;
-  return {a.tok_emb, 32 * idx, 0, 64, a.K};  // code rows >= K are packed as zeros
+  return {a.tok_emb, 32 * idx, 0, 64, a.K, nullptr};  // code rows >= K are packed as zeros
 }
 // float4 offset of tile idx in the stream: 1024 per 64-step tile, 512 per 32-step tile
 __device__ __forceinline__ int64_t pe_tile_off(int idx, int depth) {
@@ -130,10 +131,13 @@ __global__ __launch_bounds__(256) void prior_pack_kernel(PriorArgs a, float4* __
   for (int e = threadIdx.x; e < n4; e += 256) {
     const int T4 = e >> 6, l = e & 63;
     const int row = t.row0 + (l & 31);
+    const int k = t.k0 + 32 * (T4 >> 2) + 8 * (T4 & 3) + 4 * (l >> 5);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row < t.rows)
-      v = *reinterpret_cast<const float4*>(t.w + (int64_t)row * PE_D + t.k0 + 32 * (T4 >> 2) +
-                                           8 * (T4 & 3) + 4 * (l >> 5));
+    if (row < t.rows) v = *reinterpret_cast<const float4*>(t.w + (int64_t)row * PE_D + k);
+    if (t.gk) {  // W[n][k] * g[k]: RMSNorm's per-feature g moved onto the Linear
+      const float4 g = *reinterpret_cast<const float4*>(t.gk + k);
+      v.x *= g.x; v.y *= g.y; v.z *= g.z; v.w *= g.w;
+    }
     dst[e] = v;
   }
 }
@@ -156,18 +160,21 @@ __device__ __forceinline__ void pe_load_vec(const float* __restrict__ p, int h, 
 // coalesced 1-KB row each; the first 4 groups of the NEXT tile are loaded while the current
 // tile is multiplied, so each tile starts on operands already in registers and its other
 // groups arrive (in order) behind them.
+#ifndef PE_PRE
+#define PE_PRE 4  // 16-B groups of the next tile loaded during the current one
+#endif
 struct PeStream {
   const float4* __restrict__ src;
   int64_t off;  // float4 offset of the current tile
   int idx, ntiles, depth, lane;
-  float4 pre[4];  // the current tile's groups 0..3
+  float4 pre[PE_PRE];  // the current tile's first groups
 };
 
 __device__ __forceinline__ void pe_stream_begin(PeStream& st) {
   st.idx = 0;
   st.off = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) st.pre[i] = st.src[i * 64 + st.lane];
+  for (int i = 0; i < PE_PRE; ++i) st.pre[i] = st.src[i * 64 + st.lane];
 }
 
 // acc += over NS MFMA steps t of the stream's current tile: (WA) A = W[row][kmap(t,h)],
@@ -175,23 +182,24 @@ __device__ __forceinline__ void pe_stream_begin(PeStream& st) {
 template <bool WA, int NS, class BV>
 __device__ __forceinline__ floatx16 pe_gemm(PeStream& st, BV bv, floatx16 acc) {
   constexpr int G = NS / 4;  // 16-B groups of the tile (>= 8)
+  static_assert(G >= PE_PRE, "tile shorter than the prefetch");
   const float4* cur = st.src + st.off;
-  float4 rest[G - 4];
+  float4 rest[G - PE_PRE > 0 ? G - PE_PRE : 1];
 #pragma unroll
-  for (int i = 0; i < G - 4; ++i) rest[i] = cur[(4 + i) * 64 + st.lane];
+  for (int i = 0; i < G - PE_PRE; ++i) rest[i] = cur[(PE_PRE + i) * 64 + st.lane];
   const int nidx = st.idx + 1;
   const int64_t noff = st.off + (int64_t)G * 64;
-  float4 nq[4];
+  float4 nq[PE_PRE];
   if (nidx < st.ntiles) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) nq[i] = st.src[noff + i * 64 + st.lane];
+    for (int i = 0; i < PE_PRE; ++i) nq[i] = st.src[noff + i * 64 + st.lane];
   } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) nq[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < PE_PRE; ++i) nq[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 #pragma unroll
   for (int T4 = 0; T4 < G; ++T4) {
-    const float4 w4 = T4 < 4 ? st.pre[T4] : rest[T4 - 4];
+    const float4 w4 = T4 < PE_PRE ? st.pre[T4] : rest[T4 - PE_PRE];
     const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -200,7 +208,7 @@ __device__ __forceinline__ floatx16 pe_gemm(PeStream& st, BV bv, floatx16 acc) {
     }
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) st.pre[i] = nq[i];
+  for (int i = 0; i < PE_PRE; ++i) st.pre[i] = nq[i];
   st.off = noff;
   st.idx = nidx;
   return acc;
@@ -217,23 +225,50 @@ __device__ __forceinline__ void pe_linear(PeStream& st, const floatx16 (&x)[4],
   }
 }
 
-// x-transformers RMSNorm (rmsnorm_fwd_kernel): x * (1 / max(|x|, 1e-12)) * sqrt(D) * g
-__device__ __forceinline__ void pe_rms(const floatx16 (&x)[4], const float* __restrict__ g, int h,
-                                       floatx16 (&y)[4]) {
+// x-transformers RMSNorm (rmsnorm_fwd_kernel): x * (1 / max(|x|, 1e-12)) * sqrt(D) * g;
+// g is folded into the packed weights of the Linears that read the norm (pe_tile), so only
+// the per-token factor is applied here.
+__device__ __forceinline__ void pe_rms(const floatx16 (&x)[4], floatx16 (&y)[4]) {
   float ss = 0.f;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) ss = fmaf(x[t][r], x[t][r], ss);
   ss += __shfl_xor(ss, 32, 64);
-  const float inv = 1.0f / fmaxf(sqrtf(ss), 1e-12f);
-  const float scale = sqrtf((float)PE_D);
-  floatx16 gv[4];
-  pe_load_vec(g, h, gv);
+  const float f = 1.0f / fmaxf(sqrtf(ss), 1e-12f) * sqrtf((float)PE_D);
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) y[t][r] = x[t][r] * inv * scale * gv[t][r];
+    for (int r = 0; r < 16; ++r) y[t][r] = x[t][r] * f;
+}
+
+// 16 values of a per-feature vector for output tile ot: v[r] = p[32*ot + crow(r,h)]
+__device__ __forceinline__ void pe_load_tile_vec(const float* __restrict__ p, int ot, int h,
+                                                 floatx16& v) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 x = *reinterpret_cast<const float4*>(p + 32 * ot + 8 * q + 4 * h);
+    v[4 * q] = x.x;
+    v[4 * q + 1] = x.y;
+    v[4 * q + 2] = x.z;
+    v[4 * q + 3] = x.w;
+  }
+}
+
+// y^T = W x^T + b (4 output tiles, K = 128); each tile's 16 bias values load while the
+// tile's MFMAs run
+__device__ __forceinline__ void pe_linear_bias(PeStream& st, const floatx16 (&x)[4],
+                                               const float* __restrict__ bias, int h,
+                                               floatx16 (&out)[4]) {
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot) {
+    floatx16 bv, acc;
+    pe_load_tile_vec(bias, ot, h, bv);
+    pe_zero(acc);
+    acc = pe_gemm<true, 64>(st, [&](int t) { return x[t >> 4][t & 15]; }, acc);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[ot][r] = acc[r] + bv[r];
+  }
 }
 
 // LayerNorm over the D features (layernorm_fwd_kernel): (x - mean) * rstd * w (+ b)
@@ -323,7 +358,7 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
     const PriorLayer L = a.L[li];
     floatx16 xn[4], y[4];
     // attention branch: y = concat_h(softmax(Q_h K_h^T / 8) V_h) W_o^T
-    pe_rms(x, L.g_attn, h, xn);
+    pe_rms(x, xn);  // g_attn folded into q / k / v
 #pragma unroll
     for (int t = 0; t < 4; ++t) pe_zero(y[t]);
 #pragma unroll
@@ -379,36 +414,33 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
 #pragma unroll
       for (int r = 0; r < 16; ++r) x[t][r] = live ? y[t][r] + x[t][r] : 0.f;
     // feed-forward branch: y = W2 GELU(W1 xn + b1) + b2
-    pe_rms(x, L.g_ff, h, xn);
-    floatx16 u[4], bv[4];
-    pe_linear(st, xn, u);
-    pe_load_vec(L.b1, h, bv);
+    pe_rms(x, xn);  // g_ff folded into ff1
+    floatx16 u[4];
+    pe_linear_bias(st, xn, L.b1, h, u);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) u[t][r] = gelu_erf(u[t][r] + bv[t][r]);
-    pe_linear(st, u, y);
-    pe_load_vec(L.b2, h, bv);
+      for (int r = 0; r < 16; ++r) u[t][r] = gelu_erf(u[t][r]);
+    pe_linear_bias(st, u, L.b2, h, y);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) x[t][r] = live ? (y[t][r] + bv[t][r]) + x[t][r] : 0.f;
+      for (int r = 0; r < 16; ++r) x[t][r] = live ? y[t][r] + x[t][r] : 0.f;
   }
   // ---- final_norm + project_out (no bias)
   {
     floatx16 xn[4];
-    pe_rms(x, a.g_final, h, xn);
+    pe_rms(x, xn);  // g_final folded into project_out
     pe_linear(st, xn, x);
   }
   // ---- pred_head: LayerNorm_{w,b}(GELU(x W_p^T + b_p))
   {
-    floatx16 y[4], bv[4];
-    pe_linear(st, x, y);
-    pe_load_vec(a.bp, h, bv);
+    floatx16 y[4];
+    pe_linear_bias(st, x, a.bp, h, y);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) x[t][r] = gelu_erf(y[t][r] + bv[t][r]);
+      for (int r = 0; r < 16; ++r) x[t][r] = gelu_erf(y[t][r]);
     pe_layernorm(x, a.ln_w, a.ln_b, a.ln_eps, h);
   }
   // ---- tied logits: lane = code, registers = tokens crow(r, h); the cls row is dropped
