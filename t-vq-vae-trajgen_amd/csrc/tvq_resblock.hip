@@ -18,19 +18,21 @@
 //             -> store du; per-image (sum du, sum du*xhat, da2 term) -> last block: BN
 //             backward coefficients, BN weight / bias grads, da2 (bn_bwd_final_channel)
 //   rb_bwd1   dh = BN'(du) staged -> dW1 | db1 slab row; ds1 = conv1^T(dh) ->
-//             dx = ds1 * Snake'(x) + dy (identity skip); da1 partials -> last block
+//             dx = ds1 * Snake'(x) + dy (identity skip); per-image da1 terms -> a slab
+//             row, summed over the images with the weight-gradient slabs
 //
 // Work split inside a block (RB_NW = 8 waves, one image; 256 images = 256 blocks = 2 waves
 // per SIMD, where 4-wave blocks left each SIMD one wave and nothing to hide latency with):
 //   * elementwise phases (staging the conv inputs, epilogues) run channel-per-wave: wave w
 //     takes channels w, w + 8, ... and its lanes that channel's positions, so global loads
 //     and stores are lane-contiguous and every per-channel sum is one fixed xor tree;
-//   * a conv is NI = (16-position x 16-channel output tiles) x (input-channel chunks of CPC)
-//     items of 9*CPC/4 v_mfma_f32_16x16x4_f32 steps, ~24 items over the 8 waves, 3
-//     interleaved chains per wave; the chunk partials go to LDS and the epilogue sums them
-//     in chunk order;
-//   * a weight gradient is (16 x 16 tiles of the C x (9C+1) slab row) x (position chunks)
-//     items; the chunk partials are summed in order into the image's slab row.
+//   * a conv: each wave owns one (16-channel row tile, input-channel chunk of CPC) pair and
+//     a set of 16-position tiles, run as interleaved v_mfma_f32_16x16x4_f32 chains that
+//     read each weight fragment once; the chunk partials go to LDS and the epilogue sums
+//     them in chunk order;
+//   * a weight gradient: each wave owns a position chunk and a set of 16-column tiles of
+//     the C x (9C+1) slab row, its chains sharing the dY and input-window fragments; the
+//     chunk partials are summed in order into the image's slab row.
 // Both operands of every MFMA come from LDS: the conv gathers the halo plane at
 // c*PS + toff(t) (the data gradient: transposed weights, flipped taps), the weight gradient
 // reduces over the image's positions with a ones column for the bias.  Arithmetic is the
@@ -60,16 +62,21 @@ struct RB {
   static constexpr int K = 9 * C;                    // conv reduction length
   static constexpr int KST = K + ((2 - K % 32) + 32) % 32;  // panel row stride == 2 mod 32
   static constexpr int KC = K + 1, KT = (KC + 15) / 16;     // wgrad columns (+bias), tiles
-  static constexpr int NT = MT * NR, WT = NR * KT;   // conv / wgrad output tiles
-  // conv items: NT tiles x NCH chunks of CPC input channels (~24 items)
-  static constexpr int CPC0 = C * NT / 24;
-  static constexpr int CPC = CPC0 <= 4 ? 4 : CPC0 <= 8 ? 8 : CPC0 <= 16 ? 16 : 32;
-  static constexpr int NCH = C / CPC, NI = NT * NCH;
+  // conv: the waves are NR x NCH (row tile, input-channel chunk of CPC) combos times CMS
+  // position groups; a wave runs CNF 16-position tiles of its combo as interleaved chains
+  // that share the weight operand (1 + CNF LDS reads per CNF MFMAs)
+  static constexpr int NCH = (C / 4) < (RB_NW / NR) ? C / 4 : RB_NW / NR;
+  static constexpr int CPC = C / NCH;
+  static constexpr int CMS = RB_NW / (NR * NCH), CNF = (MT + CMS - 1) / CMS;
   static constexpr int PR = P + ((4 - P % 8) + 8) % 8;  // conv partial row stride == 4 mod 8
-  // weight-gradient items: WT tiles x PSPL position chunks
+  // weight gradient: the KT column tiles dealt over WKG wave groups, the positions split
+  // into WPS chunks (WKG x WPS = RB_NW); a wave runs NR x WNF chains sharing the row (dY)
+  // and column (input window) operands (NR + WNF LDS reads per NR x WNF MFMAs)
   static constexpr int PSTEPS = P / 4;
-  static constexpr int PSPL = WT >= 24 ? 1 : (W >= 64 ? 6 : 3);
-  static constexpr int WSTEPS = PSTEPS / PSPL, NIW = WT * PSPL;
+  static constexpr int WPS0 = C >= 32 ? 1 : (C == 8 && W >= 32) ? 8 : 4;
+  static constexpr int WPS = WPS0 < RB_NW ? WPS0 : RB_NW;
+  static constexpr int WKG = RB_NW / WPS, WNF = (KT + WKG - 1) / WKG;
+  static constexpr int WSTEPS = PSTEPS / WPS;
   static constexpr int KCR = KC + ((4 - KC % 8) + 8) % 8;  // wgrad partial row stride
   // elementwise phases: channels per wave, positions per lane
   static constexpr int CPW = (C + RB_NW - 1) / RB_NW, PPL = (P + 63) / 64;
@@ -77,9 +84,10 @@ struct RB {
   static constexpr int PLANE = C * PS, PANEL = CT * KST;
   static constexpr int NPAN = CT * K, UP = (NPAN + RB_T - 1) / RB_T;  // panel loads
   static constexpr int PARTC = NCH * C * PR;         // conv chunk partials (floats)
-  static constexpr int PARTW = PSPL > 1 ? PSPL * C * KCR : 0;  // wgrad chunk partials
-  static_assert(P % 16 == 0 && C % 4 == 0 && C % CPC == 0 && PSTEPS % PSPL == 0 &&
-                    (PSPL == 1 || W % (4 * WSTEPS) == 0 || 4 * WSTEPS % W == 0),
+  static constexpr int PARTW = WPS > 1 ? WPS * C * KCR : 0;  // wgrad chunk partials
+  static constexpr int CONSTP = 2 * PS;              // a ones plane and a zeros plane
+  static_assert(P % 16 == 0 && W % 4 == 0 && C % NCH == 0 && CPC % 4 == 0 &&
+                    RB_NW % (NR * NCH) == 0 && RB_NW % WPS == 0 && PSTEPS % WPS == 0,
                 "unsupported ResBlock geometry");
 };
 
@@ -89,8 +97,8 @@ struct RBArgs {  // every pointer / scalar a fused ResBlock kernel reads or writ
   const float *bn_w, *bn_b, *rmean, *rvar;  // eval
   const float* save;                         // mean | invstd | scale | shift (C each)
   const float* coef;                         // 2C: (sum du, sum du*xhat) of the backward
-  float *h_out, *y, *du, *dx, *slab1, *slab2, *da1;
-  double *part, *part1;
+  float *h_out, *y, *du, *dx, *slab1, *slab2, *slabda;
+  double* part;
   int* cnt;
   float eps, drop_p, drop_scale, invN;
   const int64_t* seed_ptr;
@@ -212,15 +220,17 @@ __device__ __forceinline__ void rb_put_panel(float* __restrict__ A, const float 
   }
 }
 
-// Conv of the staged plane(s) S with the panel A as NI items (tile, chunk); item i's
-// 16 x 16 partial over its CPC input channels goes to Pc[(chunk*C + n)*PR + p].  Each wave
-// runs its items three interleaved chains at a time (a dead chain recomputes a live item
-// on valid addresses and stores nothing: no branch in the loop).  FLIP: data gradient
+// Conv of the staged plane(s) S with the panel A.  Wave w owns output-row tile nr, input
+// channel chunk ch (CPC channels) and position tiles mt = m, m + CMS, ...: CNF interleaved
+// 16 x 16 chains that read each weight fragment once.  The chunk partial of tile (nr, mt)
+// goes to Pc[(ch*C + n)*PR + p].  A dead chain (mt >= MT, wave-uniform) recomputes tile m
+// on valid addresses and stores nothing, so the loop has no branch.  FLIP: data gradient
 // (taps flipped).
 template <class R, bool FLIP>
 __device__ __forceinline__ void rb_conv_items(const float* __restrict__ A,
                                               const float* __restrict__ S, float* __restrict__ Pc) {
   const int l = threadIdx.x & 63, j = l & 15, kq = l >> 4, wid = rb_wid();
+  const int m = wid % R::CMS, combo = wid / R::CMS, ch = combo % R::NCH, nr = combo / R::NCH;
   // gather offsets of the 9 MFMA steps of a 4-channel group, relative to its first channel:
   // step s reads reduction index k = 4s + kq = c*9 + t
   int roff[9];
@@ -230,42 +240,33 @@ __device__ __forceinline__ void rb_conv_items(const float* __restrict__ A,
     const int kh = t / 3;
     roff[s] = c * R::PS + kh * R::WP + (t - 3 * kh);
   }
-  for (int g0 = wid; g0 < R::NI; g0 += 3 * RB_NW) {
-    int ab[3], sb[3], row0[3], col[3];
-    bool live[3];
+  const float* ap = A + (nr * 16 + j) * R::KST + ch * R::CPC * 9 + kq;
+  const float* sp[R::CNF];
 #pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      const int i = g0 + f * RB_NW;
-      live[f] = i < R::NI;
-      const int ii = live[f] ? i : g0;
-      const int tile = ii % R::NT, ch = ii / R::NT;
-      const int nr = tile / R::MT, mt = tile - nr * R::MT;
-      const int p = mt * 16 + j;
-      ab[f] = (nr * 16 + j) * R::KST + ch * R::CPC * 9 + kq;
-      sb[f] = rb_pos<R>(p) + ch * R::CPC * R::PS;
-      row0[f] = ch * R::C + nr * 16 + 4 * kq;  // partial row of acc register 0
-      col[f] = p;
+  for (int f = 0; f < R::CNF; ++f) {
+    const int mt = m + R::CMS * f;
+    sp[f] = S + rb_pos<R>((mt < R::MT ? mt : m) * 16 + j) + ch * R::CPC * R::PS;
+  }
+  floatx4 acc[R::CNF];
+#pragma unroll
+  for (int f = 0; f < R::CNF; ++f) acc[f] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < R::CPC / 4; ++g)
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const float a = ap[g * 36 + 4 * s];
+#pragma unroll
+      for (int f = 0; f < R::CNF; ++f)
+        acc[f] = mfma16x16x4(a, sp[f][g * 4 * R::PS + roff[s]], acc[f]);
     }
-    floatx4 acc[3];
 #pragma unroll
-    for (int f = 0; f < 3; ++f) acc[f] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int f = 0; f < R::CNF; ++f) {
+    const int mt = m + R::CMS * f;
+    if (mt >= R::MT) continue;  // wave-uniform
 #pragma unroll
-    for (int g = 0; g < R::CPC / 4; ++g)
-#pragma unroll
-      for (int s = 0; s < 9; ++s)
-#pragma unroll
-        for (int f = 0; f < 3; ++f)
-          acc[f] = mfma16x16x4(A[ab[f] + g * 36 + 4 * s], S[sb[f] + g * 4 * R::PS + roff[s]],
-                               acc[f]);
-#pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      if (!live[f]) continue;
-      const int ch = (g0 + f * RB_NW) / R::NT;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = row0[f] - ch * R::C + r;  // channel of this register
-        if (n < R::C) Pc[(row0[f] + r) * R::PR + col[f]] = acc[f][r];
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int n = nr * 16 + 4 * kq + r;  // channel of this register
+      if (n < R::C) Pc[(ch * R::C + n) * R::PR + mt * 16 + j] = acc[f][r];
     }
   }
 }
@@ -282,75 +283,89 @@ __device__ __forceinline__ float rb_conv_at(const float* __restrict__ Pc, const 
 }
 
 // Weight gradient of one image: D[n][kc] = sum_p G[n][p] * B[p][kc], B[p][kc] =
-// S[koff(kc) + pos(p)] (kc < K), 1 (kc == K: bias), 0 beyond; rows n >= C are 0.  Items
-// (tile, position chunk); PSPL == 1: straight into the slab row, else the chunk partials to
-// Pw[(chunk*C + n)*KCR + kc] (rb_wgrad_sum adds them in chunk order).
+// S[koff(kc) + pos(p)] (kc < K), 1 (kc == K: bias), 0 beyond; rows n >= C are 0.  Wave w
+// owns position chunk pc = w / WKG and column tiles kt = w % WKG + WKG*f; each lane's
+// operand pointers are chosen once (the window cell of its column, the ones plane for the
+// bias column, the zeros plane for padding columns and rows), so every MFMA step is two
+// unconditional LDS reads and no branch.  WPS == 1: straight into the slab row, else the
+// chunk partials to Pw[(pc*C + n)*KCR + kc] (rb_wgrad_sum adds them in chunk order).
 template <class R>
 __device__ __forceinline__ void rb_wgrad_items(const float* __restrict__ G,
-                                               const float* __restrict__ S, float* __restrict__ Pw,
+                                               const float* __restrict__ S,
+                                               const float* __restrict__ K1,
+                                               float* __restrict__ Pw,
                                                float* __restrict__ slab_row) {
   const int l = threadIdx.x & 63, j = l & 15, kq = l >> 4, wid = rb_wid();
-  for (int g0 = wid; g0 < R::NIW; g0 += 3 * RB_NW) {
-    int gofs[3], ko[3], kc[3], n0[3], pc[3];
-    float cst[3];
-    bool colv[3], rowv[3], live[3];
+  const int kg = wid % R::WKG, pc = wid / R::WKG;
+  const float* K0 = K1 + R::PS;  // zeros plane
+  const float* gp[R::NR];
 #pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      const int i = g0 + f * RB_NW;
-      live[f] = i < R::NIW;
-      const int ii = live[f] ? i : g0;
-      const int tile = ii % R::WT;
-      pc[f] = ii / R::WT;
-      const int nr = tile / R::KT;
-      kc[f] = (tile - nr * R::KT) * 16 + j;
-      n0[f] = nr * 16;
-      colv[f] = kc[f] < R::K;
-      const int k = colv[f] ? kc[f] : 0, c = k / 9, t = k - 9 * c, kh = t / 3;
-      ko[f] = c * R::PS + kh * R::WP + (t - 3 * kh) + pc[f] * 0;
-      cst[f] = kc[f] == R::K ? 1.f : 0.f;
-      const int n = nr * 16 + j;
-      rowv[f] = n < R::C;
-      gofs[f] = (rowv[f] ? n : 0) * R::PS + R::WP + 1;
-    }
-    floatx4 acc[3];
+  for (int nr = 0; nr < R::NR; ++nr) {
+    const int n = nr * 16 + j;
+    gp[nr] = (n < R::C ? G + n * R::PS : K0) + R::WP + 1;
+  }
+  const float* sp[R::WNF];
 #pragma unroll
-    for (int f = 0; f < 3; ++f) acc[f] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int f = 0; f < R::WNF; ++f) {
+    const int kc = (kg + R::WKG * f) * 16 + j;
+    const int k = kc < R::K ? kc : 0, c = k / 9, t = k - 9 * c, kh = t / 3;
+    sp[f] = kc < R::K ? S + c * R::PS + kh * R::WP + (t - 3 * kh) : kc == R::K ? K1 : K0;
+  }
+  floatx4 acc[R::NR][R::WNF];
 #pragma unroll
-    for (int s = 0; s < R::WSTEPS; ++s) {
+  for (int nr = 0; nr < R::NR; ++nr)
 #pragma unroll
-      for (int f = 0; f < 3; ++f) {
-        const int p0 = (pc[f] * R::WSTEPS + s) * 4;           // 4 | W: one row
-        const int po = (p0 / R::W) * R::WP + (p0 % R::W) + kq;
-        const float ga = G[gofs[f] + po];
-        const float sb = S[ko[f] + po];
-        acc[f] = mfma16x16x4(rowv[f] ? ga : 0.f, colv[f] ? sb : cst[f], acc[f]);
-      }
-    }
+    for (int f = 0; f < R::WNF; ++f) acc[nr][f] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int pbase = pc * R::WSTEPS * 4;
 #pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      if (!live[f] || kc[f] >= R::KC) continue;
+  for (int s = 0; s < R::WSTEPS; ++s) {
+    const int p0 = pbase + 4 * s;                       // 4 | W: one row
+    const int po = p0 + 2 * (p0 / R::W) + kq;          // (p0 / W) * WP + p0 % W + kq
+    float ga[R::NR], sb[R::WNF];
+#pragma unroll
+    for (int nr = 0; nr < R::NR; ++nr) ga[nr] = gp[nr][po];
+#pragma unroll
+    for (int f = 0; f < R::WNF; ++f) sb[f] = sp[f][po];
+#pragma unroll
+    for (int nr = 0; nr < R::NR; ++nr)
+#pragma unroll
+      for (int f = 0; f < R::WNF; ++f) acc[nr][f] = mfma16x16x4(ga[nr], sb[f], acc[nr][f]);
+  }
+#pragma unroll
+  for (int f = 0; f < R::WNF; ++f) {
+    const int kt = kg + R::WKG * f;
+    if (kt >= R::KT) continue;  // wave-uniform
+    const int kc = kt * 16 + j;
+    if (kc >= R::KC) continue;
+#pragma unroll
+    for (int nr = 0; nr < R::NR; ++nr)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = n0[f] + 4 * kq + r;
+        const int n = nr * 16 + 4 * kq + r;
         if (n >= R::C) continue;
-        if (R::PSPL == 1)
-          slab_row[n * R::KC + kc[f]] = acc[f][r];
+        if (R::WPS == 1)
+          slab_row[n * R::KC + kc] = acc[nr][f][r];
         else
-          Pw[(pc[f] * R::C + n) * R::KCR + kc[f]] = acc[f][r];
+          Pw[(pc * R::C + n) * R::KCR + kc] = acc[nr][f][r];
       }
-    }
   }
+}
+
+// the ones plane (bias column) and zeros plane (padding) the weight-gradient items read
+template <class R>
+__device__ __forceinline__ void rb_const_planes(float* __restrict__ K1) {
+  for (int i = threadIdx.x; i < 2 * R::PS; i += RB_T) K1[i] = i < R::PS ? 1.f : 0.f;
 }
 
 template <class R>
 __device__ __forceinline__ void rb_wgrad_sum(const float* __restrict__ Pw,
                                              float* __restrict__ slab_row) {
-  if (R::PSPL == 1) return;
+  if (R::WPS == 1) return;
   for (int e = threadIdx.x; e < R::C * R::KC; e += RB_T) {
     const int n = e / R::KC, kc = e - n * R::KC;
     float s = Pw[n * R::KCR + kc];
 #pragma unroll
-    for (int pc = 1; pc < R::PSPL; ++pc) s += Pw[(pc * R::C + n) * R::KCR + kc];
+    for (int pc = 1; pc < R::WPS; ++pc) s += Pw[(pc * R::C + n) * R::KCR + kc];
     slab_row[e] = s;
   }
 }
@@ -534,6 +549,7 @@ __global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
   float* A = S + R::PLANE;                         // transposed w2
   float* Pc = A + R::PANEL;
   float* Pw = Pc + R::PARTC;
+  float* K1 = Pw + R::PARTW;                       // ones | zeros planes
   const int b = blockIdx.x, l = threadIdx.x & 63, wid = rb_wid();
   const int64_t img0 = (int64_t)b * R::C * R::P;
   RB_MARK(0);
@@ -550,6 +566,7 @@ __global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
   rb_param<R>(a.save + R::C, el, is);
   rb_border<R>(G);
   rb_border<R>(S);
+  rb_const_planes<R>(K1);
   rb_put_panel<R>(A, pv);
   RB_MARK(1);
   const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
@@ -567,7 +584,7 @@ __global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
   __syncthreads();
   RB_MARK(2);
   float* slab_row = a.slab2 + (int64_t)b * R::C * R::KC;
-  rb_wgrad_items<R>(G, S, Pw, slab_row);
+  rb_wgrad_items<R>(G, S, K1, Pw, slab_row);
   RB_MARK(3);
   rb_conv_items<R, true>(A, G, Pc);
   __syncthreads();
@@ -610,7 +627,8 @@ __global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
   float* A = S + R::PLANE;                         // transposed w1
   float* Pc = A + R::PANEL;
   float* Pw = Pc + R::PARTC;
-  const int b = blockIdx.x, l = threadIdx.x & 63, wid = rb_wid();
+  float* K1 = Pw + R::PARTW;                       // ones | zeros planes
+  const int b = blockIdx.x, l = threadIdx.x & 63;
   const int64_t img0 = (int64_t)b * R::C * R::P;
   RB_MARK(0);
   const RBElems<R> el;
@@ -633,6 +651,7 @@ __global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
   }
   rb_border<R>(G);
   rb_border<R>(S);
+  rb_const_planes<R>(K1);
   rb_put_panel<R>(A, pv);
   RB_MARK(1);
   // dh = w*invstd*(du - mean(du) - xhat*mean(du*xhat))  (bn_bwd_apply_kernel)
@@ -648,7 +667,7 @@ __global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
   __syncthreads();
   RB_MARK(2);
   float* slab_row = a.slab1 + (int64_t)b * R::C * R::KC;
-  rb_wgrad_items<R>(G, S, Pw, slab_row);
+  rb_wgrad_items<R>(G, S, K1, Pw, slab_row);
   RB_MARK(3);
   rb_conv_items<R, true>(A, G, Pc);
   __syncthreads();
@@ -672,21 +691,24 @@ __global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
       s[0][u][q] = (double)(gs * inv_a * t * xv) - (double)(gs * (sn * sn) * inv_a * inv_a);
     }
   RB_MARK(5);
-  rb_channel_sums<R, 1>(s, el, a.B, b, a.part1);
+  // this image's da1 term per channel -> its row of the da1 slab (summed over the images
+  // in order by the deferred slab reduction, with the weight-gradient slabs)
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u) {
+    if (el.c[u] >= R::C) continue;  // wave-uniform
+    double t = s[0][u][0];
+#pragma unroll
+    for (int v = 1; v < R::PPL; ++v) t += s[0][u][v];
+    t = wave_sum_d(t);
+    if (l == 0) a.slabda[(int64_t)b * R::C + el.c[u]] = (float)t;
+  }
   RB_MARK(6);
-  if (a.cnt && last_block(a.cnt, a.B))
-    for (int c = wid; c < R::C; c += RB_NW) {
-      double t[1];
-      wave_chunk_sums<1>(a.part1, c, a.B, l, t);
-      if (l == 0) a.da1[c] = a.accumulate ? a.da1[c] + (float)t[0] : (float)t[0];
-    }
-  RB_MARK(7);
 }
 
 // ---------------------------------------------------------------- host side
 template <class R>
 static size_t rb_lds(int kind) {
-  const size_t PL = R::PLANE, PA = R::PANEL, PC = R::PARTC, PW = R::PARTW;
+  const size_t PL = R::PLANE, PA = R::PANEL, PC = R::PARTC, PW = R::PARTW + R::CONSTP;
   switch (kind) {
     case 0: return 4 * (PL + PA + PC);               // fwd1
     case 1: return 4 * (PL + PA + PC);               // fwd2
@@ -766,15 +788,15 @@ static bool rb_supported(int64_t B, int64_t C, int64_t H, int64_t W) {
 static size_t rb_align(size_t n) { return (n + 255) & ~(size_t)255; }
 
 struct RBWs {  // workspace layout (bytes)
-  size_t part, part1, coef, slab2, slab1, du, total;
+  size_t part, slabda, coef, slab2, slab1, du, total;
 };
 static RBWs rb_ws(int64_t B, int64_t C, int64_t W) {
   RBWs w;
   const int64_t kc = 9 * C + 1;
   const size_t slab = (size_t)(B * C * kc + reduce_rows_scratch(B, C * kc));
   w.part = 0;
-  w.part1 = w.part + rb_align((size_t)B * C * 3 * 8);
-  w.coef = w.part1 + rb_align((size_t)B * C * 8);
+  w.slabda = w.part + rb_align((size_t)B * C * 3 * 8);
+  w.coef = w.slabda + rb_align((size_t)(B * C + reduce_rows_scratch(B, C)) * 4);
   w.slab2 = w.coef + rb_align((size_t)2 * C * 4);
   w.slab1 = w.slab2 + rb_align(slab * 4);
   w.du = w.slab1 + rb_align(slab * 4);
@@ -874,8 +896,9 @@ extern "C" int tvq_resblock_bwd(const float* dy, const float* x, const float* h,
   RBArgs a = {};
   a.x = x; a.h = h; a.dy = dy; a.a1 = a1; a.w1 = w1; a.a2 = a2; a.w2 = w2; a.bn_w = bn_w;
   a.save = save; a.coef = coef;
-  a.du = (float*)(ws + w.du); a.dx = dx; a.slab1 = slab1; a.slab2 = slab2; a.da1 = da1;
-  a.part = (double*)(ws + w.part); a.part1 = (double*)(ws + w.part1);
+  float* slabda = (float*)(ws + w.slabda);
+  a.du = (float*)(ws + w.du); a.dx = dx; a.slab1 = slab1; a.slab2 = slab2; a.slabda = slabda;
+  a.part = (double*)(ws + w.part);
   a.B = (int)B; a.accumulate = (int)accumulate;
   a.drop_p = drop_p;
   a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
@@ -885,11 +908,11 @@ extern "C" int tvq_resblock_bwd(const float* dy, const float* x, const float* h,
   a.cnt = counters(1, FIN_NORM);
   rb_dispatch((int)C, (int)W, 3, &a, st, nullptr);
   if (!a.cnt) bn_bwd_final_launch(a.part, a.bfin, st);
-  a.cnt = counters(1, FIN_NORM);
+  a.cnt = nullptr;
   rb_dispatch((int)C, (int)W, 4, &a, st, nullptr);
-  if (!a.cnt) snake_da_final_launch(a.part1, (int)C, (int)B, da1, (int)accumulate, st);
   const int64_t kc = 9 * C + 1;
   conv_wgrad_finish(slab2, (int)B, C, kc, dw2, db2, (int)accumulate, st);
   conv_wgrad_finish(slab1, (int)B, C, kc, dw1, db1, (int)accumulate, st);
+  conv_wgrad_finish(slabda, (int)B, C, 1, da1, nullptr, (int)accumulate, st);
   return launch_status("tvq_resblock_bwd");
 }
