@@ -62,27 +62,36 @@ struct BNFinal {  // per-channel finalize of the training statistics
 
 // one wave (lane 0..63) finalizes channel c: lanes stride the chunk partials, fixed
 // xor-tree combine; running stats with momentum, unbiased running var
+// channel c's affine scale / shift from its sums (s1 = sum x, s2 = sum x^2); `write`: also
+// store save_mean / save_invstd / scale / shift and update the running statistics
+__device__ __forceinline__ void bn_final_from_sums(double s1, double s2, int c, const BNFinal& f,
+                                                   bool write, float& sc, float& sh) {
+  const double mean = s1 / (double)f.N;
+  double var = s2 / (double)f.N - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const double invstd = 1.0 / sqrt(var + (double)f.eps);
+  sc = (float)((double)(f.w ? f.w[c] : 1.f) * invstd);
+  sh = (f.b ? f.b[c] : 0.f) - (float)mean * sc;
+  if (!write) return;
+  if (f.rmean) {
+    const double unb = f.N > 1 ? var * (double)f.N / (double)(f.N - 1) : var;
+    f.rmean[c] = (float)((1.0 - f.momentum) * f.rmean[c] + f.momentum * mean);
+    f.rvar[c] = (float)((1.0 - f.momentum) * f.rvar[c] + f.momentum * unb);
+  }
+  f.save_mean[c] = (float)mean;
+  f.save_invstd[c] = (float)invstd;
+  f.scale[c] = sc;
+  f.shift[c] = sh;
+}
+
 __device__ __forceinline__ void bn_final_channel(const double* part, int c, int lane,
                                                  const BNFinal& f) {
   if (c == 0 && lane == 0 && f.nbt) f.nbt[0] += 1;
   double s[2];
   wave_chunk_sums<2>(part, c, f.chunks, lane, s);
   if (lane != 0) return;
-  const double s1 = s[0], s2 = s[1];
-  const double mean = s1 / (double)f.N;
-  double var = s2 / (double)f.N - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const double invstd = 1.0 / sqrt(var + (double)f.eps);
-  if (f.rmean) {
-    const double unb = f.N > 1 ? var * (double)f.N / (double)(f.N - 1) : var;
-    f.rmean[c] = (float)((1.0 - f.momentum) * f.rmean[c] + f.momentum * mean);
-    f.rvar[c] = (float)((1.0 - f.momentum) * f.rvar[c] + f.momentum * unb);
-  }
-  const float sc = (float)((double)(f.w ? f.w[c] : 1.f) * invstd);
-  f.save_mean[c] = (float)mean;
-  f.save_invstd[c] = (float)invstd;
-  f.scale[c] = sc;
-  f.shift[c] = (f.b ? f.b[c] : 0.f) - (float)mean * sc;
+  float sc, sh;
+  bn_final_from_sums(s[0], s[1], c, f, true, sc, sh);
 }
 
 struct BNBwdFinal {
@@ -92,17 +101,23 @@ struct BNBwdFinal {
 };
 
 // coef[c] = (sum ds, sum ds*xhat) and the parameter grads of channel c (one wave)
+// the parameter gradients of channel c from its sums (s0 = sum ds, s1 = sum ds*xhat,
+// s2 = the Snake a term)
+__device__ __forceinline__ void bn_bwd_params_from_sums(double s0, double s1, double s2, int c,
+                                                        const BNBwdFinal& f) {
+  if (f.dw) f.dw[c] = f.accumulate ? f.dw[c] + (float)s1 : (float)s1;
+  if (f.db) f.db[c] = f.accumulate ? f.db[c] + (float)s0 : (float)s0;
+  if (f.da) f.da[c] = f.accumulate ? f.da[c] + (float)s2 : (float)s2;
+}
+
 __device__ __forceinline__ void bn_bwd_final_channel(const double* part, int c, int lane,
                                                      const BNBwdFinal& f) {
   double s[3];
   wave_chunk_sums<3>(part, c, f.chunks, lane, s);
   if (lane != 0) return;
-  const double s0 = s[0], s1 = s[1], s2 = s[2];
-  f.coef[2 * c] = (float)s0;
-  f.coef[2 * c + 1] = (float)s1;
-  if (f.dw) f.dw[c] = f.accumulate ? f.dw[c] + (float)s1 : (float)s1;
-  if (f.db) f.db[c] = f.accumulate ? f.db[c] + (float)s0 : (float)s0;
-  if (f.da) f.da[c] = f.accumulate ? f.da[c] + (float)s2 : (float)s2;
+  f.coef[2 * c] = (float)s[0];
+  f.coef[2 * c + 1] = (float)s[1];
+  bn_bwd_params_from_sums(s[0], s[1], s[2], c, f);
 }
 
 __device__ __forceinline__ void snake_bwd_final_channel(const double* part, int C, int chunks,

@@ -9,15 +9,18 @@
 //   y = x + Dropout_p(conv2(Snake_a2(BN(conv1(Snake_a1(x)) + b1))) + b2)
 //
 //   rb_fwd1   s1 = Snake_a1(x) staged into LDS -> h = conv1(s1) + b1 -> store h; per-image
-//             BN partial sums (fp64) -> the last block: batch mean / invstd, running stats,
-//             scale / shift (bn_final_channel, as tvq_bn_train_fwd)
-//   rb_fwd2   s2 = Snake_a2(h*scale + shift) staged -> y = x + Dropout(conv2(s2) + b2)
+//             BN partial sums (fp64)
+//   rb_fwd2   every block reduces the partials (same fixed order) to the batch mean /
+//             invstd -> scale / shift (bn_final_channel's arithmetic; block 0 writes them
+//             and the running statistics); s2 = Snake_a2(h*scale + shift) staged ->
+//             y = x + Dropout(conv2(s2) + b2)
 //   rb_eval   both convs in one block with BN from the running statistics (s2 in LDS)
 //   rb_bwd2   g2 = Dropout'(dy) (same counter-hash mask) -> dW2 | db2 per-image slab row;
 //             ds2 = conv2^T(g2) -> du = ds2 * Snake'(u), u = h*scale + shift recomputed
-//             -> store du; per-image (sum du, sum du*xhat, da2 term) -> last block: BN
-//             backward coefficients, BN weight / bias grads, da2 (bn_bwd_final_channel)
-//   rb_bwd1   dh = BN'(du) staged -> dW1 | db1 slab row; ds1 = conv1^T(dh) ->
+//             -> store du; per-image (sum du, sum du*xhat, da2 term)
+//   rb_bwd1   every block reduces those partials to the BN backward coefficients (block 0
+//             writes the BN weight / bias and Snake a2 gradients);
+//             dh = BN'(du) staged -> dW1 | db1 slab row; ds1 = conv1^T(dh) ->
 //             dx = ds1 * Snake'(x) + dy (identity skip); per-image da1 terms -> a slab
 //             row, summed over the images with the weight-gradient slabs
 //
@@ -96,10 +99,8 @@ struct RBArgs {  // every pointer / scalar a fused ResBlock kernel reads or writ
   const float *a1, *w1, *b1, *a2, *w2, *b2;
   const float *bn_w, *bn_b, *rmean, *rvar;  // eval
   const float* save;                         // mean | invstd | scale | shift (C each)
-  const float* coef;                         // 2C: (sum du, sum du*xhat) of the backward
-  float *h_out, *y, *du, *dx, *slab1, *slab2, *slabda;
+  float *h_out, *y, *du, *dx, *slab1, *slab2, *slabda, *slabda2;
   double* part;
-  int* cnt;
   float eps, drop_p, drop_scale, invN;
   const int64_t* seed_ptr;
   uint64_t offset;
@@ -370,10 +371,11 @@ __device__ __forceinline__ void rb_wgrad_sum(const float* __restrict__ Pw,
   }
 }
 
-// per-channel fp64 sums of this lane's element values (fixed order: over v, then the xor
-// tree) -> lane 0 stores part[(c*B + b)*NS + i] write-through, for the last block
-template <class R, int NS>
-__device__ __forceinline__ void rb_channel_sums(double (&s)[NS][R::CPW][R::PPL],
+// per-channel fp64 sums of this lane's element values s[0..NS) (fixed order: over v, then
+// the xor tree) -> lane 0 stores part[(c*NS + i)*B + b] (image-fastest: the consumer's
+// lanes read consecutive images)
+template <class R, int NS, int NT>
+__device__ __forceinline__ void rb_channel_sums(double (&s)[NT][R::CPW][R::PPL],
                                                 const RBElems<R>& el, int B, int b,
                                                 double* part) {
 #pragma unroll
@@ -385,8 +387,71 @@ __device__ __forceinline__ void rb_channel_sums(double (&s)[NS][R::CPW][R::PPL],
 #pragma unroll
       for (int v = 1; v < R::PPL; ++v) t += s[i][u][v];
       t = wave_sum_d(t);
-      if ((threadIdx.x & 63) == 0) st_wt(part + ((int64_t)el.c[u] * B + b) * NS + i, t);
+      if ((threadIdx.x & 63) == 0) part[((int64_t)el.c[u] * NS + i) * B + b] = t;
     }
+  }
+}
+
+// one image's per-channel total of s[i] (same order) -> its row of a float slab, summed
+// over the images in order by the deferred slab reduction (the Snake a gradients)
+template <class R, int NT>
+__device__ __forceinline__ void rb_slab_row_sums(double (&s)[NT][R::CPW][R::PPL], int i,
+                                                 const RBElems<R>& el, int b, float* slab) {
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u) {
+    if (el.c[u] >= R::C) continue;  // wave-uniform
+    double t = s[i][u][0];
+#pragma unroll
+    for (int v = 1; v < R::PPL; ++v) t += s[i][u][v];
+    t = wave_sum_d(t);
+    if ((threadIdx.x & 63) == 0) slab[(int64_t)b * R::C + el.c[u]] = (float)t;
+  }
+}
+
+// Batch totals of NS per-image fp64 partials part[(c*NS + i)*B + b] for this wave's
+// channels.  Every block of the consuming kernel reduces them itself in the same fixed
+// order (each lane its images in increasing b, then the xor tree -- wave_chunk_sums' order),
+// so the blocks agree bit for bit and the producing kernel needs no last block.
+// rb_batch_issue loads the first 64*RB_UB images' values (issued with the block's other
+// prologue loads, so they share one round trip); rb_batch_sums adds them and any further
+// images in order.
+constexpr int RB_UB = 4;
+template <class R, int NS>
+__device__ __forceinline__ void rb_batch_issue(const double* __restrict__ part, int B,
+                                               const RBElems<R>& el,
+                                               double (&v)[R::CPW][RB_UB][NS]) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u) {
+    const int c = el.c[u] < R::C ? el.c[u] : 0;
+#pragma unroll
+    for (int k = 0; k < RB_UB; ++k)
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        v[u][k][i] = l + 64 * k < B ? part[((int64_t)c * NS + i) * B + l + 64 * k] : 0.0;
+  }
+}
+
+template <class R, int NS>
+__device__ __forceinline__ void rb_batch_sums(const double* __restrict__ part, int B,
+                                              const RBElems<R>& el,
+                                              const double (&v)[R::CPW][RB_UB][NS],
+                                              double (&t)[R::CPW][NS]) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u) {
+    const int c = el.c[u] < R::C ? el.c[u] : 0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) t[u][i] = 0.0;
+#pragma unroll
+    for (int k = 0; k < RB_UB; ++k)
+#pragma unroll
+      for (int i = 0; i < NS; ++i) t[u][i] += v[u][k][i];
+    for (int b = l + 64 * RB_UB; b < B; b += 64)  // B > 256 only
+#pragma unroll
+      for (int i = 0; i < NS; ++i) t[u][i] += part[((int64_t)c * NS + i) * B + b];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) t[u][i] = wave_sum_d(t[u][i]);
   }
 }
 
@@ -397,13 +462,13 @@ __global__ __launch_bounds__(RB_T) void rb_fwd1_kernel(RBArgs a) {
   float* S = reinterpret_cast<float*>(rb_smem);
   float* A = S + R::PLANE;
   float* Pc = A + R::PANEL;
-  const int b = blockIdx.x, l = threadIdx.x & 63, wid = rb_wid();
+  const int b = blockIdx.x;
   const int64_t img0 = (int64_t)b * R::C * R::P;
   RB_MARK(0);
   const RBElems<R> el;
   float v[R::CPW][R::PPL], pv[R::UP], a1[R::CPW], b1[R::CPW];
+  rb_load_panel<R, false>(a.w1, pv);  // first: the panel store waits for these alone
   rb_load<R>(a.x, img0, el, v);
-  rb_load_panel<R, false>(a.w1, pv);
   rb_param<R>(a.a1, el, a1);
   rb_param<R>(a.b1, el, b1);
   rb_border<R>(S);
@@ -434,9 +499,6 @@ __global__ __launch_bounds__(RB_T) void rb_fwd1_kernel(RBArgs a) {
   RB_MARK(4);
   rb_channel_sums<R, 2>(s, el, a.B, b, a.part);
   RB_MARK(5);
-  if (a.cnt && last_block(a.cnt, a.B))
-    for (int c = wid; c < R::C; c += RB_NW) bn_final_channel(a.part, c, l, a.fin);
-  RB_MARK(6);
 }
 
 template <class R>
@@ -451,15 +513,25 @@ __global__ __launch_bounds__(RB_T) void rb_fwd2_kernel(RBArgs a) {
   const RBElems<R> el;
   float v[R::CPW][R::PPL], xr[R::CPW][R::PPL], pv[R::UP];
   float a2[R::CPW], sc[R::CPW], sh[R::CPW], b2[R::CPW];
-  rb_load<R>(a.h, img0, el, v);
   rb_load_panel<R, false>(a.w2, pv);
+  rb_load<R>(a.h, img0, el, v);
   rb_load<R>(a.x, img0, el, xr);
   rb_param<R>(a.a2, el, a2);
-  rb_param<R>(a.save + 2 * R::C, el, sc);
-  rb_param<R>(a.save + 3 * R::C, el, sh);
   rb_param<R>(a.b2, el, b2);
+  double bv[R::CPW][RB_UB][2], bs[R::CPW][2];
+  rb_batch_issue<R, 2>(a.part, a.B, el, bv);
   rb_border<R>(S);
   rb_put_panel<R>(A, pv);
+  rb_batch_sums<R, 2>(a.part, a.B, el, bv, bs);
+  // the batch statistics (bn_final_channel's arithmetic); block 0 publishes them (save,
+  // running statistics, num_batches_tracked)
+  const bool pub = b == 0 && (threadIdx.x & 63) == 0;
+  if (pub && threadIdx.x == 0 && a.fin.nbt) a.fin.nbt[0] += 1;
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u) {
+    const int c = el.c[u] < R::C ? el.c[u] : 0;
+    bn_final_from_sums(bs[u][0], bs[u][1], c, a.fin, pub && el.c[u] < R::C, sc[u], sh[u]);
+  }
   RB_MARK(1);
 #pragma unroll
   for (int u = 0; u < R::CPW; ++u)
@@ -550,15 +622,15 @@ __global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
   float* Pc = A + R::PANEL;
   float* Pw = Pc + R::PARTC;
   float* K1 = Pw + R::PARTW;                       // ones | zeros planes
-  const int b = blockIdx.x, l = threadIdx.x & 63, wid = rb_wid();
+  const int b = blockIdx.x;
   const int64_t img0 = (int64_t)b * R::C * R::P;
   RB_MARK(0);
   const RBElems<R> el;
   float vg[R::CPW][R::PPL], vh[R::CPW][R::PPL], pv[R::UP];
   float a2[R::CPW], sc[R::CPW], sh[R::CPW], mu[R::CPW], is[R::CPW];
+  rb_load_panel<R, true>(a.w2, pv);
   rb_load<R>(a.dy, img0, el, vg);
   rb_load<R>(a.h, img0, el, vh);
-  rb_load_panel<R, true>(a.w2, pv);
   rb_param<R>(a.a2, el, a2);
   rb_param<R>(a.save + 2 * R::C, el, sc);
   rb_param<R>(a.save + 3 * R::C, el, sh);
@@ -612,11 +684,9 @@ __global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
       a.du[el.gi(img0, u, q)] = d;
     }
   RB_MARK(5);
-  rb_channel_sums<R, 3>(s, el, a.B, b, a.part);
+  rb_channel_sums<R, 2>(s, el, a.B, b, a.part);
+  rb_slab_row_sums<R>(s, 2, el, b, a.slabda2);
   RB_MARK(6);
-  if (a.cnt && last_block(a.cnt, a.B))
-    for (int c = wid; c < R::C; c += RB_NW) bn_bwd_final_channel(a.part, c, l, a.bfin);
-  RB_MARK(7);
 }
 
 template <class R>
@@ -634,25 +704,32 @@ __global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
   const RBElems<R> el;
   float vd[R::CPW][R::PPL], vh[R::CPW][R::PPL], vx[R::CPW][R::PPL], vy[R::CPW][R::PPL];
   float pv[R::UP], a1[R::CPW], mu[R::CPW], is[R::CPW], bw[R::CPW], md[R::CPW], mx[R::CPW];
+  rb_load_panel<R, true>(a.w1, pv);
   rb_load<R>(a.du, img0, el, vd);
   rb_load<R>(a.h, img0, el, vh);
   rb_load<R>(a.x, img0, el, vx);
-  rb_load_panel<R, true>(a.w1, pv);
   rb_load<R>(a.dy, img0, el, vy);
   rb_param<R>(a.a1, el, a1);
   rb_param<R>(a.save, el, mu);
   rb_param<R>(a.save + R::C, el, is);
   rb_param<R>(a.bn_w, el, bw, 1.f);
-#pragma unroll
-  for (int u = 0; u < R::CPW; ++u) {
-    const int c = el.c[u] < R::C ? el.c[u] : 0;
-    md[u] = a.coef[2 * c] * a.invN;
-    mx[u] = a.coef[2 * c + 1] * a.invN;
-  }
+  // BN backward coefficients (sum du, sum du*xhat) from rb_bwd2's per-image partials;
+  // block 0 writes the BN weight / bias gradients
+  double bv[R::CPW][RB_UB][2], bs[R::CPW][2];
+  rb_batch_issue<R, 2>(a.part, a.B, el, bv);
   rb_border<R>(G);
   rb_border<R>(S);
   rb_const_planes<R>(K1);
   rb_put_panel<R>(A, pv);
+  rb_batch_sums<R, 2>(a.part, a.B, el, bv, bs);
+#pragma unroll
+  for (int u = 0; u < R::CPW; ++u) {
+    const int c = el.c[u] < R::C ? el.c[u] : 0;
+    md[u] = (float)bs[u][0] * a.invN;
+    mx[u] = (float)bs[u][1] * a.invN;
+    if (b == 0 && l == 0 && el.c[u] < R::C)
+      bn_bwd_params_from_sums(bs[u][0], bs[u][1], 0.0, c, a.bfin);
+  }
   RB_MARK(1);
   // dh = w*invstd*(du - mean(du) - xhat*mean(du*xhat))  (bn_bwd_apply_kernel)
 #pragma unroll
@@ -691,17 +768,8 @@ __global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
       s[0][u][q] = (double)(gs * inv_a * t * xv) - (double)(gs * (sn * sn) * inv_a * inv_a);
     }
   RB_MARK(5);
-  // this image's da1 term per channel -> its row of the da1 slab (summed over the images
-  // in order by the deferred slab reduction, with the weight-gradient slabs)
-#pragma unroll
-  for (int u = 0; u < R::CPW; ++u) {
-    if (el.c[u] >= R::C) continue;  // wave-uniform
-    double t = s[0][u][0];
-#pragma unroll
-    for (int v = 1; v < R::PPL; ++v) t += s[0][u][v];
-    t = wave_sum_d(t);
-    if (l == 0) a.slabda[(int64_t)b * R::C + el.c[u]] = (float)t;
-  }
+  // this image's da1 term per channel -> its row of the da1 slab
+  rb_slab_row_sums<R>(s, 0, el, b, a.slabda);
   RB_MARK(6);
 }
 
@@ -788,16 +856,17 @@ static bool rb_supported(int64_t B, int64_t C, int64_t H, int64_t W) {
 static size_t rb_align(size_t n) { return (n + 255) & ~(size_t)255; }
 
 struct RBWs {  // workspace layout (bytes)
-  size_t part, slabda, coef, slab2, slab1, du, total;
+  size_t part, slabda, slabda2, slab2, slab1, du, total;
 };
 static RBWs rb_ws(int64_t B, int64_t C, int64_t W) {
   RBWs w;
   const int64_t kc = 9 * C + 1;
   const size_t slab = (size_t)(B * C * kc + reduce_rows_scratch(B, C * kc));
   w.part = 0;
-  w.slabda = w.part + rb_align((size_t)B * C * 3 * 8);
-  w.coef = w.slabda + rb_align((size_t)(B * C + reduce_rows_scratch(B, C)) * 4);
-  w.slab2 = w.coef + rb_align((size_t)2 * C * 4);
+  const size_t slabd = (size_t)(B * C + reduce_rows_scratch(B, C)) * 4;
+  w.slabda = w.part + rb_align((size_t)B * C * 2 * 8);
+  w.slabda2 = w.slabda + rb_align(slabd);
+  w.slab2 = w.slabda2 + rb_align(slabd);
   w.slab1 = w.slab2 + rb_align(slab * 4);
   w.du = w.slab1 + rb_align(slab * 4);
   w.total = w.du + rb_align((size_t)B * C * 3 * W * 4);
@@ -850,9 +919,7 @@ extern "C" int tvq_resblock_train_fwd(const float* x, int64_t B, int64_t C, int6
   a.offset = offset;
   a.fin = {(int)C, (int)B, B * 3 * W, eps, momentum, bn_w, bn_b, running_mean, running_var,
            num_batches_tracked, save, save + C, save + 2 * C, save + 3 * C};
-  a.cnt = counters(1, FIN_NORM);
   rb_dispatch((int)C, (int)W, 0, &a, st, nullptr);
-  if (!a.cnt) bn_stats_final_launch(a.part, a.fin, st);
   rb_dispatch((int)C, (int)W, 1, &a, st, nullptr);
   return launch_status("tvq_resblock_train_fwd");
 }
@@ -890,13 +957,14 @@ extern "C" int tvq_resblock_bwd(const float* dy, const float* x, const float* h,
   hipStream_t st = (hipStream_t)stream;
   const RBWs w = rb_ws(B, C, W);
   char* ws = (char*)workspace;
-  float* coef = (float*)(ws + w.coef);
   float* slab2 = (float*)(ws + w.slab2);
   float* slab1 = (float*)(ws + w.slab1);
   RBArgs a = {};
   a.x = x; a.h = h; a.dy = dy; a.a1 = a1; a.w1 = w1; a.a2 = a2; a.w2 = w2; a.bn_w = bn_w;
-  a.save = save; a.coef = coef;
+  a.save = save;
   float* slabda = (float*)(ws + w.slabda);
+  float* slabda2 = (float*)(ws + w.slabda2);
+  a.slabda2 = slabda2;
   a.du = (float*)(ws + w.du); a.dx = dx; a.slab1 = slab1; a.slab2 = slab2; a.slabda = slabda;
   a.part = (double*)(ws + w.part);
   a.B = (int)B; a.accumulate = (int)accumulate;
@@ -904,15 +972,13 @@ extern "C" int tvq_resblock_bwd(const float* dy, const float* x, const float* h,
   a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
   a.seed_ptr = seed_ptr; a.offset = offset;
   a.invN = 1.0f / (float)(B * 3 * W);
-  a.bfin = {(int)C, (int)B, coef, dbn_w, dbn_b, da2, (int)accumulate};
-  a.cnt = counters(1, FIN_NORM);
+  a.bfin = {(int)C, (int)B, nullptr, dbn_w, dbn_b, nullptr, (int)accumulate};
   rb_dispatch((int)C, (int)W, 3, &a, st, nullptr);
-  if (!a.cnt) bn_bwd_final_launch(a.part, a.bfin, st);
-  a.cnt = nullptr;
   rb_dispatch((int)C, (int)W, 4, &a, st, nullptr);
   const int64_t kc = 9 * C + 1;
   conv_wgrad_finish(slab2, (int)B, C, kc, dw2, db2, (int)accumulate, st);
   conv_wgrad_finish(slab1, (int)B, C, kc, dw1, db1, (int)accumulate, st);
   conv_wgrad_finish(slabda, (int)B, C, 1, da1, nullptr, (int)accumulate, st);
+  conv_wgrad_finish(slabda2, (int)B, C, 1, da2, nullptr, (int)accumulate, st);
   return launch_status("tvq_resblock_bwd");
 }
