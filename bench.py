@@ -126,6 +126,7 @@ class JointTrainer:
         Returns (out1, out2, deferred codebook updates)."""
         import contextlib
         from timevqvae.hip import streams, wgrad
+        from timevqvae.hip.conv import wgrad_deferred
         from timevqvae.hip.vq import deferred_codebook_updates
         self.opt1.zero_grad()
         self.opt2.zero_grad()
@@ -136,7 +137,9 @@ class JointTrainer:
                 hist1 = self.s1.forward_backward(batch, 0) if only != "stage2" else None
             if only != "stage1":
                 out2 = self.s2.training_step(batch, 0)
-                with wgrad.grouped():  # Linear weight gradients: one grouped launch per stream
+                # Linear weight gradients: one grouped launch per stream; the conv and norm
+                # weight-gradient reductions issued on this stream: one batch at the end
+                with wgrad_deferred(this_stream_only=True), wgrad.grouped():
                     out2["loss"].backward(self._one)  # cached ones: no fill launch per step
             else:
                 out2 = {"loss": torch.zeros(())}
@@ -391,10 +394,11 @@ def resblock_bwd_leg(device, C=16, W=32):
     """The step's top kernel by summed time (profiles/r03*_step_kernel_stats.csv): the fused
     ResBlock backward (csrc/tvq_resblock.hip rb_bwd2 + rb_bwd1, reference vq_vae.py:13-62) at
     its most frequent shape, C = 16 on (256, 16, 3, 32) (8 ops per step).  One op = rb_bwd2
-    (dropout' -> conv2 weight gradient slab row + data gradient -> Snake' -> BN backward
-    partials, BN finish in the last block) + rb_bwd1 (BN' -> conv1 weight gradient + data
-    gradient -> Snake' + identity skip, da1 finish) + the two ordered slab sums (batched at
-    the band's end in the step, here after each op).
+    (dropout' -> conv2 weight gradient slab row + data gradient -> Snake' -> per-image BN
+    backward partials and Snake a2 term) + rb_bwd1 (every block reduces those partials to
+    the BN coefficients -> BN' -> conv1 weight gradient + data gradient -> Snake' + identity
+    skip, per-image Snake a1 term) + one batched launch of the four ordered slab sums
+    (dW2|db2, dW1|db1, da1, da2: as in the step, where they join the band-end batch).
     Algorithmic work per op: two 3x3 data gradients 2 * B*P*C*9C each and two weight+bias
     gradients 2 * B*P*C*(9C+1) each (P = 3W positions) = 4 * 2 * 256*96*16*144 (+bias) =
     453.8 MFLOP; bytes: dy, x, h read and dx written (4 * B*C*P*4 B) + both weights read and
@@ -424,10 +428,12 @@ def resblock_bwd_leg(device, C=16, W=32):
     dx = torch.empty_like(x)
     grads = [torch.zeros(t.shape, device=device) for t in (a1, w1, b1, bw, bb, a2, w2, b2)]
 
-    def fn():
+    def fn():  # as in the step: the slab sums deferred to one batched launch at the end
+        call("tvq_conv_wgrad_defer_begin")
         call("tvq_resblock_bwd", ptr(dy), ptr(x), ptr(h), B, C, H, W, ptr(a1), ptr(w1), ptr(bw),
              ptr(save), ptr(a2), ptr(w2), 0.3, ptr(seed), 0, ptr(dx), *[ptr(t) for t in grads],
              1, ptr(ws), stream_ptr())
+        call("tvq_conv_wgrad_defer_flush", stream_ptr())
     with torch.no_grad():
         us = _graph_time_us([fn], 50)
     K = 9 * C
@@ -439,12 +445,13 @@ def resblock_bwd_leg(device, C=16, W=32):
     if os.path.exists(tpath):
         traffic = json.load(open(tpath))["traffic_bytes"]
     return {"bound": "mfma", "kernel": "fused ResBlock backward, C=16 on (256,16,3,32): "
-                                       "rb_bwd2_kernel + rb_bwd1_kernel<RB<16,32>> + their 2 "
-                                       "ordered slab sums (16x16x4 fp32 MFMA, 8 waves per image)",
+                                       "rb_bwd2_kernel + rb_bwd1_kernel<RB<16,32>> + one "
+                                       "batched ordered slab-sum launch (16x16x4 fp32 MFMA, "
+                                       "8 waves per image)",
             "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
-            "launches_per_op": 4,
+            "launches_per_op": 3,
             "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
 

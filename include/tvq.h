@@ -185,6 +185,11 @@ int64_t tvq_conv_packcache_entries(void);
  * final.  Process-wide host state, one scope at a time. */
 int tvq_conv_wgrad_defer_begin(void);
 int tvq_conv_wgrad_defer_flush(tvq_stream_t stream);
+/* The same scope, recording only the reductions issued on `stream` -- the conv weight
+ * gradients and the RMSNorm / LayerNorm weight gradients accumulated into a flat gradient
+ * (tvq_rmsnorm_bwd / tvq_layernorm_bwd with accumulate = 1); those issued on other streams
+ * run at once.  Flush on the same `stream`. */
+int tvq_wgrad_defer_begin_stream(tvq_stream_t stream);
 /* paused != 0: calls inside the scope reduce immediately (a gradient needed at once) */
 int tvq_conv_wgrad_defer_pause(int64_t paused);
 /* op: 0 conv2d fwd, 1 convT2d fwd, 2 conv2d dgrad, 3 convT2d dgrad, 4 conv2d wgrad,

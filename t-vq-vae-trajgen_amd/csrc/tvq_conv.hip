@@ -1712,6 +1712,12 @@ static bool g_pc_active = false;
 // deferred weight-gradient split sums (see wgrad_finish)
 static std::vector<RrJob> g_rd;
 static bool g_rd_on = false, g_rd_paused = false;
+// the scope's stream (tvq_wgrad_defer_begin_stream): only reductions issued on it are
+// recorded, the others run at once (a flush on one stream orders after that stream's
+// producers only); g_rd_any: the plain begin() records every stream's reductions (the caller
+// flushes on the stream they were all issued on)
+static hipStream_t g_rd_st = nullptr;
+static bool g_rd_any = true;
 
 constexpr int PACK_BATCH = 24;
 struct PackBatch {
@@ -2369,6 +2375,16 @@ extern "C" int tvq_conv_wgrad_defer_begin(void) {
   TVQ_CHECK_ARG(!g_rd_on, "tvq_conv_wgrad_defer_begin: a scope is already open");
   g_rd.clear();
   g_rd_on = true;
+  g_rd_any = true;
+  return TVQ_OK;
+}
+
+extern "C" int tvq_wgrad_defer_begin_stream(tvq_stream_t stream) {
+  TVQ_CHECK_ARG(!g_rd_on, "tvq_wgrad_defer_begin_stream: a scope is already open");
+  g_rd.clear();
+  g_rd_on = true;
+  g_rd_any = false;
+  g_rd_st = (hipStream_t)stream;
   return TVQ_OK;
 }
 
@@ -2594,17 +2610,32 @@ extern "C" int64_t tvq_conv_workspace(int64_t op, int64_t B, int64_t Ci, int64_t
 // slabs' reductions are recorded and run by a few batched launches at the flush instead
 // of one launch per conv (the caller keeps the workspaces alive until then).
 
+static bool rd_records(int64_t rows, hipStream_t st) {
+  return g_rd_on && !g_rd_paused && rows <= RR_ONE_ROWS && (g_rd_any || st == g_rd_st);
+}
+
 static void wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, float* dw,
                          float* db, int accumulate, hipStream_t st) {
   // deterministic split sum; kcols = Kred+1 splits out the bias column.  The level-1
   // scratch follows the slab in the workspace.
   const int64_t L = kcols > 0 && db ? kcols : 0;
-  if (g_rd_on && !g_rd_paused && splits <= RR_ONE_ROWS) {  // the single-level case: batched at the flush
+  if (rd_records(splits, st)) {  // the single-level case: batched at the flush
     g_rd.push_back({slab, dw, db, splits, N * kcols, L, accumulate});
     return;
   }
   reduce_rows(slab, splits, N * kcols, N * kcols, dw, db, L, accumulate,
               slab + (int64_t)splits * N * kcols, st);
+}
+
+// out[0..N) (+)= sum of the P contiguous rows of `in` (a parameter gradient only the
+// optimizer reads): joins the open deferral scope's batch, else reduce_rows now
+void tvq::param_rows_finish(const float* in, int64_t P, int64_t N, float* out, int accumulate,
+                            float* scratch, hipStream_t st) {
+  if (rd_records(P, st)) {
+    g_rd.push_back({in, out, nullptr, P, N, 0, accumulate});
+    return;
+  }
+  reduce_rows(in, P, N, N, out, nullptr, 0, accumulate, scratch, st);
 }
 
 void tvq::conv_wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, float* dw, float* db,

@@ -10,4 +10,9 @@ namespace tvq {
 // floats of scratch must follow the slab.
 void conv_wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, float* dw, float* db,
                        int accumulate, hipStream_t st);
+// out[0..N) (+)= sum of P contiguous rows of `in` -- a parameter gradient the optimizer
+// alone reads (norm weights): batched into the open deferral scope when the scope takes
+// it, else reduce_rows now (scratch: reduce_rows_scratch(P, N) floats)
+void param_rows_finish(const float* in, int64_t P, int64_t N, float* out, int accumulate,
+                       float* scratch, hipStream_t st);
 }  // namespace tvq

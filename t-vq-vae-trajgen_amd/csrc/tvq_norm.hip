@@ -261,6 +261,137 @@ __global__ void dropout_bwd_kernel(const float* __restrict__ dy, int64_t n, floa
     dx[i] = (uniform01(seed, (uint64_t)i) >= p) ? dy[i] * scale : 0.f;
 }
 
+// ---- whole-channel forms: one block owns a channel (B*HW <= BNC_T * PT elements, held
+// in registers), so the statistics and the apply are one launch with no cross-block
+// hand-off.  Per-thread sums in element order, then block_sum_d's fixed tree.
+constexpr int BNC_T = 512;
+
+// training forward: sums -> bn_final_channel's arithmetic (thread 0 publishes save /
+// running statistics / scale / shift) -> y = snake?(x*scale + shift)
+template <int PT>
+__global__ __launch_bounds__(BNC_T) void bn_train_chan_kernel(const float* __restrict__ x, int B,
+                                                             int C, int HW, Div16 dhw,
+                                                             const float* __restrict__ a,
+                                                             float* __restrict__ y, BNFinal f) {
+  __shared__ double red[BNC_T / 64];
+  const int c = blockIdx.x, tid = threadIdx.x, tot = B * HW;
+  float v[PT];
+  int64_t o[PT];
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    const int i = tid + BNC_T * u;
+    o[u] = chan_off(i < tot ? i : 0, C, c, HW, dhw);
+    v[u] = x[o[u]];
+  }
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int u = 0; u < PT; ++u)
+    if (tid + BNC_T * u < tot) {
+      s1 += (double)v[u];
+      s2 += (double)v[u] * (double)v[u];
+    }
+  s1 = block_sum_d(s1, red);
+  s2 = block_sum_d(s2, red);
+  if (c == 0 && tid == 0 && f.nbt) f.nbt[0] += 1;
+  float sc, sh;
+  bn_final_from_sums(s1, s2, c, f, tid == 0, sc, sh);
+  const float av = a ? a[c] : 1.f;
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    if (tid + BNC_T * u >= tot) continue;
+    float t = fmaf(v[u], sc, sh);
+    if (a) t = snake_fwd(t, av);
+    y[o[u]] = t;
+  }
+}
+
+// backward: ds = dy * Snake'(x*scale + shift) (Snake a term), the three channel sums, the
+// parameter gradients (thread 0), then dx = w*invstd*(ds - mean(ds) - xhat*mean(ds*xhat))
+// -- bn_bwd_partial_kernel + bn_bwd_final_channel + bn_bwd_apply_kernel's arithmetic
+template <int PT>
+__global__ __launch_bounds__(BNC_T) void bn_bwd_chan_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, int B, int C, int HW, Div16 dhw,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ w, const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ a, float* __restrict__ dx, BNBwdFinal f) {
+  __shared__ double red[BNC_T / 64];
+  const int c = blockIdx.x, tid = threadIdx.x, tot = B * HW;
+  float xv[PT], g[PT];
+  int64_t o[PT];
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    const int i = tid + BNC_T * u;
+    o[u] = chan_off(i < tot ? i : 0, C, c, HW, dhw);
+    xv[u] = x[o[u]];
+    g[u] = dy[o[u]];
+  }
+  const float mu = mean[c], is = invstd[c], sc = scale[c], sh = shift[c];
+  const float av = a ? a[c] : 1.f, inv_a = 1.0f / av;
+  double s_ds = 0.0, s_dsx = 0.0, s_da = 0.0;
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    if (tid + BNC_T * u >= tot) continue;
+    float ds = g[u];
+    if (a) {
+      const float s = fmaf(xv[u], sc, sh);
+      float sn, cs;
+      sincosf(av * s, &sn, &cs);
+      const float t = 2.0f * sn * cs;
+      ds = g[u] + g[u] * inv_a * t * av;
+      s_da += (double)(g[u] * inv_a * t * s) - (double)(g[u] * (sn * sn) * inv_a * inv_a);
+    }
+    g[u] = ds;
+    const float xhat = (xv[u] - mu) * is;
+    s_ds += ds;
+    s_dsx += (double)ds * xhat;
+  }
+  s_ds = block_sum_d(s_ds, red);
+  s_dsx = block_sum_d(s_dsx, red);
+  s_da = block_sum_d(s_da, red);
+  if (tid == 0) bn_bwd_params_from_sums(s_ds, s_dsx, s_da, c, f);
+  const float invN = 1.0f / (float)tot;
+  const float wc = w ? w[c] : 1.f;
+  const float mds = (float)s_ds * invN, mdsx = (float)s_dsx * invN;
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    if (tid + BNC_T * u >= tot) continue;
+    const float xhat = (xv[u] - mu) * is;
+    dx[o[u]] = wc * is * (g[u] - mds - xhat * mdsx);
+  }
+}
+
+// eval: y = snake?(x*scale + shift) with scale / shift from the running statistics
+// (bn_eval_prep_kernel's arithmetic per element: no separate prep launch)
+__global__ __launch_bounds__(256) void bn_eval_snake_kernel(
+    const float* __restrict__ x, int n, int C, Div16 dhw, const float* __restrict__ w,
+    const float* __restrict__ b, const float* __restrict__ rm, const float* __restrict__ rv,
+    float eps, const float* __restrict__ a, float* __restrict__ y) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int c = div16(i, dhw) % C;
+    const float inv = 1.0f / sqrtf(rv[c] + eps);
+    const float sc = (w ? w[c] : 1.f) * inv;
+    const float sh = (b ? b[c] : 0.f) - rm[c] * sc;
+    float s = fmaf(x[i], sc, sh);
+    if (a) s = snake_fwd(s, a[c]);
+    y[i] = s;
+  }
+}
+
+// whole-channel form: on (TVQ_BN_CHAN, default) for C >= 32 channels of <= BNC_T*48
+// elements; returns the per-thread element count PT (0: the chunked form)
+static int bn_chan_pt(int64_t B, int64_t C, int64_t HW) {
+  static const int on = [] {
+    const char* s = getenv("TVQ_BN_CHAN");
+    return s ? atoi(s) : 1;
+  }();
+  const int64_t n = B * HW;
+  if (!on || C < 32 || n > (int64_t)BNC_T * 48) return 0;
+  const int64_t pt = (n + BNC_T - 1) / BNC_T;
+  return pt <= 8 ? 8 : pt <= 16 ? 16 : pt <= 24 ? 24 : pt <= 32 ? 32 : 48;
+}
+
+#define BNC_CASES(X) X(8) X(16) X(24) X(32) X(48)
+
 void bn_stats_final_launch(const double* part, const BNFinal& f, hipStream_t st) {
   hipLaunchKernelGGL(bn_stats_final_kernel, dim3(f.C), dim3(64), 0, st, part, f);
 }
@@ -311,6 +442,15 @@ extern "C" int tvq_bn_train_fwd(const float* x, int64_t B, int64_t C, int64_t HW
   double* part = (double*)workspace;
   const BNFinal f = {(int)C, chunks, B * HW, eps, momentum, w, b, running_mean, running_var,
                      num_batches_tracked, save_mean, save_invstd, scale_shift, scale_shift + C};
+  if (const int pt = bn_chan_pt(B, C, HW)) {
+#define M_(PT)                                                                                \
+  if (pt == PT)                                                                               \
+    hipLaunchKernelGGL(bn_train_chan_kernel<PT>, dim3((int)C), dim3(BNC_T), 0, st, x, (int)B, \
+                       (int)C, (int)HW, dhw, snake_a, y, f);
+    BNC_CASES(M_)
+#undef M_
+    return launch_status("tvq_bn_train_fwd");
+  }
   int* cnt = counters(C, FIN_NORM);
   hipLaunchKernelGGL(bn_stats_partial_kernel, dim3((int)C, chunks), dim3(256), 0, st, x, (int)B,
                      (int)C, (int)HW, dhw, chunks, part, cnt, f);
@@ -330,11 +470,9 @@ extern "C" int tvq_bn_eval_fwd(const float* x, int64_t B, int64_t C, int64_t HW,
   TVQ_CHECK_ARG(x && y && running_mean && running_var && scale_shift, "tvq_bn_eval_fwd: bad args");
   TVQ_CHECK_ARG(norm_dims_ok(B, C, HW), "tvq_bn_eval_fwd: tensor too large");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_eval_prep_kernel, dim3((int)((C + 63) / 64)), dim3(64), 0, st, w, b,
-                     running_mean, running_var, eps, (int)C, scale_shift, scale_shift + C);
-  hipLaunchKernelGGL(affine_snake_kernel, ew_grid(B * C * HW), dim3(256), 0, st, x,
-                     (int)(B * C * HW), (int)C, (int)HW, make_div16(HW), scale_shift,
-                     scale_shift + C, snake_a, y);
+  hipLaunchKernelGGL(bn_eval_snake_kernel, ew_grid(B * C * HW), dim3(256), 0, st, x,
+                     (int)(B * C * HW), (int)C, make_div16(HW), w, b, running_mean, running_var,
+                     eps, snake_a, y);
   return launch_status("tvq_bn_eval_fwd");
 }
 
@@ -352,6 +490,16 @@ extern "C" int tvq_bn_bwd(const float* dy, const float* x, int64_t B, int64_t C,
   double* part = (double*)workspace;
   float* coef = (float*)(part + (int64_t)C * chunks * 3);
   const BNBwdFinal f = {(int)C, chunks, coef, dw, db, snake_a ? da : nullptr, (int)accumulate};
+  if (const int pt = bn_chan_pt(B, C, HW)) {
+#define M_(PT)                                                                                 \
+  if (pt == PT)                                                                                \
+    hipLaunchKernelGGL(bn_bwd_chan_kernel<PT>, dim3((int)C), dim3(BNC_T), 0, st, dy, x, (int)B,  \
+                       (int)C, (int)HW, dhw, save_mean, save_invstd, w, scale_shift,             \
+                       scale_shift + C, snake_a, dx, f);
+    BNC_CASES(M_)
+#undef M_
+    return launch_status("tvq_bn_bwd");
+  }
   int* cnt = counters(C, FIN_NORM);
   hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3((int)C, chunks), dim3(256), 0, st, dy, x, (int)B,
                      (int)C, (int)HW, dhw, chunks, save_mean, save_invstd, scale_shift,

@@ -13,6 +13,7 @@
 #include <math.h>
 
 #include "tvq_common.h"
+#include "tvq_conv_internal.h"
 #include "tvq_reduce.h"
 
 namespace tvq {
@@ -273,7 +274,7 @@ __global__ void layernorm_bwd_kernel(const float* __restrict__ dy, const float* 
     const int k = d / D, dd = d - k * D;
     float s = 0.f;
     for (int w = 0; w < nw; ++w) s += sh[(w * 2 + k) * D + dd];
-    part[((int64_t)blockIdx.x * 2 + k) * D + dd] = s;
+    part[((int64_t)k * gridDim.x + blockIdx.x) * D + dd] = s;  // [gamma | beta][block][D]
   }
 }
 
@@ -352,7 +353,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_reg_kernel(
     const int k = d / D, dd = d - k * D;
     float s = 0.f;
     for (int w = 0; w < nw; ++w) s += sh[(w * 2 + k) * D + dd];
-    part[((int64_t)blockIdx.x * 2 + k) * D + dd] = s;
+    part[((int64_t)k * gridDim.x + blockIdx.x) * D + dd] = s;  // [gamma | beta][block][D]
   }
 }
 
@@ -811,8 +812,11 @@ extern "C" int tvq_rmsnorm_bwd(const float* dy, const float* x, int64_t M, int64
   else
     hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(nb), dim3(256), lds, st, dy, x, M, (int)D, g, scale,
                        inv_norm, dres, dx, workspace, rpb);
-  reduce_rows(workspace, nb, D, D, dg, nullptr, 0, (int)accumulate, workspace + (int64_t)nb * 2 * D,
-              st);
+  // the gain gradient: into the flat gradient (accumulate) it joins an open deferral scope
+  if (accumulate)
+    param_rows_finish(workspace, nb, D, dg, 1, workspace + (int64_t)nb * 2 * D, st);
+  else
+    reduce_rows(workspace, nb, D, D, dg, nullptr, 0, 0, workspace + (int64_t)nb * 2 * D, st);
   return launch_status("tvq_rmsnorm_bwd");
 }
 
@@ -846,12 +850,17 @@ extern "C" int tvq_layernorm_bwd(const float* dy, const float* x, int64_t M, int
   else
     hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nb), dim3(256), lds, st, dy, x, M, (int)D, gamma,
                        mean, rstd, dx, workspace, rpb);
-  // workspace [nb][2][D]: reduce both halves (rows of length 2D)
+  // workspace [gamma | beta][nb][D]: two slabs of contiguous rows; into the flat gradient
+  // (accumulate) they join an open deferral scope
   float* rs = workspace + (int64_t)nb * 2 * D;
-  if (dgamma) reduce_rows(workspace, nb, D, 2 * D, dgamma, nullptr, 0, (int)accumulate, rs, st);
-  if (dbeta)
-    reduce_rows(workspace + D, nb, D, 2 * D, dbeta, nullptr, 0, (int)accumulate,
-                rs + reduce_rows_scratch(nb, D), st);
+  float* rs2 = rs + reduce_rows_scratch(nb, D);
+  if (accumulate) {
+    if (dgamma) param_rows_finish(workspace, nb, D, dgamma, 1, rs, st);
+    if (dbeta) param_rows_finish(workspace + (int64_t)nb * D, nb, D, dbeta, 1, rs2, st);
+  } else {
+    if (dgamma) reduce_rows(workspace, nb, D, D, dgamma, nullptr, 0, 0, rs, st);
+    if (dbeta) reduce_rows(workspace + (int64_t)nb * D, nb, D, D, dbeta, nullptr, 0, 0, rs2, st);
+  }
   return launch_status("tvq_layernorm_bwd");
 }
 

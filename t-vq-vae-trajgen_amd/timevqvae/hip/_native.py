@@ -133,6 +133,7 @@ sig("tvq_conv_packcache_end")
 sig("tvq_conv_packcache_entries", restype=I64)
 sig("tvq_conv_wgrad_defer_begin")
 sig("tvq_conv_wgrad_defer_flush", P)
+sig("tvq_wgrad_defer_begin_stream", P)
 sig("tvq_conv_wgrad_defer_pause", I64)
 # --- ROCKET features --------------------------------------------------------
 sig("tvq_rocket_apply", P, I64, I64, I64, P, P, P, P, P, P, I64, P, P)

@@ -36,16 +36,22 @@ _defer_keep = None  # workspaces of deferred weight-gradient reductions (wgrad_d
 
 
 @contextlib.contextmanager
-def wgrad_deferred():
+def wgrad_deferred(this_stream_only=False):
     """Inside the scope the conv weight-gradient split sums are recorded and run by a few
     batched launches on the current stream at the exit (tvq_conv_wgrad_defer_*), bit for
     bit the same sums, instead of one reduction launch per conv.  Wrap a backward pass;
-    gradients are final only after the exit."""
+    gradients are final only after the exit.  this_stream_only: record only the reductions
+    issued on the current stream -- conv weight gradients and the norm weight gradients
+    accumulated into a flat gradient (a backward that runs on several streams); the others
+    run at once."""
     global _defer_keep
     if _defer_keep is not None or os.environ.get("TVQ_WGRAD_DEFER", "1") == "0":
         yield  # nested (the outer scope flushes) or switched off
         return
-    call("tvq_conv_wgrad_defer_begin")
+    if this_stream_only:
+        call("tvq_wgrad_defer_begin_stream", stream_ptr())
+    else:
+        call("tvq_conv_wgrad_defer_begin")
     _defer_keep = []
     try:
         yield

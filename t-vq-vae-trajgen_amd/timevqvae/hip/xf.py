@@ -7,6 +7,7 @@ import torch
 
 from . import rng, streams, wgrad
 from ._native import call, grad_sink, ptr, stream_ptr, value
+from .conv import _keep
 from .linear import _bias_grad_rows, gemm, weight_grad
 
 
@@ -40,6 +41,7 @@ class _RMSNorm(torch.autograd.Function):
         ws = torch.empty(value("tvq_norm_bwd_workspace", M, D), device=x2.device)
         call("tvq_rmsnorm_bwd", ptr(dy), ptr(x2), M, D, ptr(g), float(ctx.scale), ptr(inv), None,
              ptr(dx), ptr(dg), int(sink is not None), ptr(ws), stream_ptr())
+        _keep(ws)  # its reduction may be deferred (hip.conv.wgrad_deferred)
         return dx.reshape(ctx.shape), (None if sink is not None else dg), None
 
 
@@ -80,6 +82,7 @@ class _RMSNormRes(torch.autograd.Function):
         ws = torch.empty(value("tvq_norm_bwd_workspace", M, D), device=x2.device)
         call("tvq_rmsnorm_bwd", ptr(dy), ptr(x2), M, D, ptr(g), float(ctx.scale), ptr(inv),
              ptr(dres), ptr(dx), ptr(dg), int(sink is not None), ptr(ws), stream_ptr())
+        _keep(ws)
         return dx.reshape(ctx.shape), (None if sink is not None else dg), None
 
 
@@ -121,6 +124,7 @@ class _LayerNorm(torch.autograd.Function):
         ws = torch.empty(value("tvq_norm_bwd_workspace", M, D), device=x2.device)
         call("tvq_layernorm_bwd", ptr(dy), ptr(x2), M, D, ptr(gamma), ptr(mean), ptr(rstd), ptr(dx),
              ptr(dg), ptr(db), int(direct), ptr(ws), stream_ptr())
+        _keep(ws)
         if direct:
             return dx.reshape(ctx.shape), None, None, None
         return dx.reshape(ctx.shape), dg, db, None

@@ -136,8 +136,11 @@ def test_conv_residual_dropout(cuda):
     torch.testing.assert_close(x.grad, x2.grad, rtol=1e-5, atol=1e-5)
 
 
+# chunked form (C < 32) and the whole-channel form (C >= 32, B*3W <= 24576), including the
+# step's LF (256, 64, 3, 8) and HF (256, 128, 3, 32) shapes
 @pytest.mark.parametrize("B,C,W,snake_on", [(8, 16, 32, True), (4, 4, 128, True), (16, 128, 8, True),
-                                            (8, 256, 96, False)])
+                                            (8, 256, 96, False), (256, 64, 8, True),
+                                            (256, 128, 32, True), (64, 32, 16, False)])
 def test_bn_snake_train(B, C, W, snake_on, cuda):
     from timevqvae.hip.norm import bn_snake
     bn_c = torch.nn.BatchNorm2d(C).train()

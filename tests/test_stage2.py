@@ -248,3 +248,44 @@ def test_bidirectional_transformer_vs_oracle(kind, cuda):
         if e > 1e-4:
             bad.append((k, e))
     assert not bad, bad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["lf", "hf"])
+def test_deferred_norm_and_conv_reductions_bitwise(kind, cuda):
+    """The prior's backward into a flat gradient (FusedAdamW) inside
+    wgrad_deferred(this_stream_only=True) -- the RMSNorm / LayerNorm gain gradients and the
+    Upscale conv weight gradients join one batched reduction at the scope's exit
+    (tvq_wgrad_defer_begin_stream) -- gives bit for bit the gradients of the immediate
+    reductions."""
+    from timevqvae.hip.conv import wgrad_deferred
+    from timevqvae.hip.optim import FusedAdamW
+    from timevqvae.models import BidirectionalTransformer
+    K = 512
+    pm = dict(hidden_dim=128, n_layers=4, heads=2, ff_mult=1) if kind == "lf" else \
+        dict(hidden_dim=32, n_layers=1, heads=1, ff_mult=1)
+    m = BidirectionalTransformer(kind, 24 if kind == "lf" else 96, {"lf": K, "hf": K}, 128,
+                                 use_rmsnorm=True, p_unconditional=0.0, n_classes=5,
+                                 model_dropout=0.0, emb_dropout=0.0, num_tokens_l=24, **pm)
+    _xf_state(m, 11)
+    m = m.to(cuda).train()
+    opt = FusedAdamW(m.parameters())
+    gen = torch.Generator().manual_seed(12)
+    B = 32
+    s_l = torch.randint(0, K + 1, (B, 24), generator=gen).to(cuda)
+    s_h = torch.randint(0, K + 1, (B, 96), generator=gen).to(cuda)
+    y = torch.randint(0, 5, (B, 1), generator=gen).to(cuda)
+    g = torch.randn((B, 24 if kind == "lf" else 96, K), generator=gen).to(cuda)
+    grads = []
+    for deferred in (False, True):
+        opt.zero_grad()
+        out = m(s_l, s_h if kind == "hf" else None, class_condition=y)
+        if deferred:
+            with wgrad_deferred(this_stream_only=True):
+                out.backward(g)
+        else:
+            out.backward(g)
+        torch.cuda.synchronize()
+        grads.append(opt.flat_grad.clone())
+    assert grads[0].abs().sum() > 0
+    assert torch.equal(grads[0], grads[1])

@@ -19,6 +19,6 @@ if [ "$LEG" = wgrad ]; then
   python tools/roof_traffic.py $O $O/traffic.json "LF 64->64 3x3 conv weight+bias gradient over 6144 positions: conv_wgrad_w8_kernel + reduce_rows_kernel" conv_wgrad_w8_kernel reduce_rows_kernel
 fi
 if [ "$LEG" = rbbwd ]; then
-  python tools/roof_traffic.py $O $O/traffic.json "fused ResBlock backward C=16 on (256,16,3,32): rb_bwd2_kernel + rb_bwd1_kernel + 2 ordered slab sums" rb_bwd2_kernel rb_bwd1_kernel reduce_rows
+  python tools/roof_traffic.py $O $O/traffic.json "fused ResBlock backward C=16 on (256,16,3,32): rb_bwd2_kernel + rb_bwd1_kernel + one batched ordered slab-sum launch" rb_bwd2_kernel rb_bwd1_kernel reduce_rows
 fi
 echo roofline-done
