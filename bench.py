@@ -192,7 +192,20 @@ class JointTrainer:
             self.opt1.step(lr_on_device=True, gates_ready=True)
             self.opt2.step(lr_on_device=True, gates_ready=True)
 
-        self.graph = StepGraph([seg1, seg2], [between1, None], warmup=2, before=before).capture()
+        if self.world == 1 and os.environ.get("TVQ_ONE_GRAPH", "1") != "0":
+            # one replica: nothing runs between the segments (no collectives, no deferred
+            # codebook update), so the step is one graph
+            from timevqvae.hip import streams
+
+            def seg12():
+                out = seg1()
+                streams.join(backward_done=True)
+                seg2()
+                return out
+            self.graph = StepGraph([seg12], [None], warmup=2, before=before).capture()
+        else:
+            self.graph = StepGraph([seg1, seg2], [between1, None], warmup=2,
+                                   before=before).capture()
 
 
 class Stage1Trainer:
@@ -452,6 +465,41 @@ def resblock_bwd_leg(device, C=16, W=32):
             "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
             "launches_per_op": 3,
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def linear_fwd_leg(device):
+    """The LF prior's Linear forward at its training shape (gemm_rb2_kernel<64, true>: 14 of
+    its 15 launches per step are this shape): Y = R + X W^T + b over the 6400 token rows of
+    the stage2 batch (B = 256 x 25 tokens), K = N = 128 (hidden 128, ff_mult 1; reference
+    bidirectional_transformer.py / x-transformers Linear).  Algorithmic work per launch:
+    2 M N K = 209.7 MFLOP; bytes X, W, b, R read and Y written = 4 (M K + N K + N + 2 M N) =
+    9.9 MB (AI 21 FLOP/B: at the fp32 MFMA / HBM ridge).  50 graph-replayed launches timed
+    with HIP events on their stream."""
+    from timevqvae.hip.linear import gemm
+    M, N, K = 6400, 128, 128
+    g = torch.Generator(device="cpu").manual_seed(6)
+    x = torch.randn(M, K, generator=g).to(device)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(device)
+    b = (torch.randn(N, generator=g) * 0.1).to(device)
+    r = torch.randn(M, N, generator=g).to(device)
+    y = torch.empty(M, N, device=device)
+    fn = (lambda: gemm(x, K, 1, w, 1, K, M, N, K, out=y, ldc=N, bias=b, R=r, ldr=N))
+    with torch.no_grad():
+        us = _graph_time_us([fn], 50)
+    flops = 2.0 * M * N * K
+    byts = 4.0 * (M * K + N * K + N + 2 * M * N)
+    tf = flops / (us * 1e-6) / 1e12
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "r03_linfwd_traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath))["traffic_bytes"]
+    return {"bound": "mfma", "kernel": "gemm_rb2_kernel<64,true>: LF prior Linear forward "
+                                       "Y = R + X W^T + b, (6400 x 128) x (128 x 128), "
+                                       "32x32x2 fp32 MFMA, one 32x32 tile per wave",
+            "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
             "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
 

@@ -16,3 +16,10 @@ run stage2 TVQ_BENCH_ONLY=stage2
 run stage1_LF TVQ_BENCH_ONLY=stage1 TVQ_BENCH_BANDS=LF
 run stage1_HF TVQ_BENCH_ONLY=stage1 TVQ_BENCH_BANDS=HF
 run joint_LFonly TVQ_BENCH_BANDS=LF
+run joint_HFonly TVQ_BENCH_BANDS=HF
+run bnchan16 TVQ_BN_CHAN=16
+run bnchan8 TVQ_BN_CHAN=8
+run twograph TVQ_ONE_GRAPH=0
+run joint2 TVQ_X=2
+LEG=linfwd bash tools/gpu_roofline.sh > gpurun_out/roof_linfwd.txt 2>&1 || { tail -20 gpurun_out/roof_linfwd.txt; exit 1; }
+tail -2 gpurun_out/roof_linfwd.txt

@@ -21,4 +21,7 @@ fi
 if [ "$LEG" = rbbwd ]; then
   python tools/roof_traffic.py $O $O/traffic.json "fused ResBlock backward C=16 on (256,16,3,32): rb_bwd2_kernel + rb_bwd1_kernel + one batched ordered slab-sum launch" rb_bwd2_kernel rb_bwd1_kernel reduce_rows
 fi
+if [ "$LEG" = linfwd ]; then
+  python tools/roof_traffic.py $O $O/traffic.json "LF prior Linear forward (6400x128)x(128x128) + bias + residual: gemm_rb2_kernel<64,true>" gemm_rb2_kernel
+fi
 echo roofline-done
