@@ -27,7 +27,7 @@ namespace tvq {
 
 __device__ __forceinline__ int crow32(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-template <int KC, int WN, bool B_KCONTIG>
+template <int KC, int WN, bool B_KCONTIG, bool HAS_R, bool HAS_C>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g) {
   constexpr int WM = 4 / WN;
   constexpr int HK = KC / 2;  // contiguous k per lane per chunk
@@ -89,11 +89,23 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g) {
     }
   };
   floatx16 acc;
+  float rv[16], cv[16];  // the tile's residual / accumulated C, requested with its last chunk
+  const int ncl = ncol < g.N ? ncol : g.N - 1;
   auto compute = [&](const float (&a)[HK], int s) {
     const int q = s / nch, c = s - q * nch;
     if (c == 0) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    }
+    if ((HAS_R || HAS_C) && c == nch - 1) {  // loads overlap the chunk's MFMAs
+      const int mb = ((int)blockIdx.x + q * (int)gridDim.x) * TM + wm * 32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int m = mb + crow32(r, h);
+        m = m < g.M ? m : g.M - 1;
+        if (HAS_R) rv[r] = g.R[(int64_t)(g.rmod > 0 ? m % g.rmod : m) * g.ldr + ncl];
+        if (HAS_C) cv[r] = g.C[(int64_t)m * g.ldc + ncl];
+      }
     }
     const float* wf = Ws + ((c * WN + wn) * T4) * 256 + 4 * lane;
 #pragma unroll
@@ -104,21 +116,23 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g) {
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * t4 + 2], b4.z, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * t4 + 3], b4.w, acc, 0, 0, 0);
     }
-    if (c != nch - 1 || ncol >= g.N) return;
-    // epilogue: register r -> row crow32(r, h) of the wave's 32-row tile, column ncol
+    if (c != nch - 1) return;
+    // epilogue: register r -> row crow32(r, h) of the wave's 32-row tile, column ncol;
+    // values combined in every lane, stores predicated (see gemm_rb2_kernel)
     const int mb = ((int)blockIdx.x + q * (int)gridDim.x) * TM + wm * 32;
+    const bool colok = ncol < g.N;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = mb + crow32(r, h);
-      if (m >= g.M) continue;
+      const bool ok = colok && m < g.M;
       float v = acc[r] * g.alpha + bv;
       const int64_t ci = (int64_t)m * g.ldc + ncol;
-      if (g.pre) g.pre[ci] = v;
+      if (g.pre && ok) g.pre[ci] = v;
       if (g.act == 1) v = gelu_erf(v);
       if (g.gate) v *= *g.gate;
-      if (g.R) v += g.R[(int64_t)(g.rmod > 0 ? m % g.rmod : m) * g.ldr + ncol];
-      if (g.accumulate) v += g.C[ci];
-      g.C[ci] = v;
+      if (HAS_R) v += rv[r];
+      if (HAS_C) v += cv[r];
+      if (ok) g.C[ci] = v;
     }
   };
   float a0[HK], a1[HK];
@@ -138,7 +152,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g) {
 // and copied into each wave's registers; each wave then loads its 32 A rows, runs K/2
 // MFMAs and stores (measured the fastest of the forms in this file at the transformer
 // shapes; tools/mfma_probe.hip).
-template <int KH, bool B_KCONTIG>
+template <int KH, bool B_KCONTIG, bool HAS_R, bool HAS_C>
 __global__ __launch_bounds__(256) void gemm_rb2_kernel(GemmArgs g, int nblk, int xcd) {
   constexpr int KP = 2 * KH;
   constexpr int P = KP + 4;
@@ -183,27 +197,51 @@ __global__ __launch_bounds__(256) void gemm_rb2_kernel(GemmArgs g, int nblk, int
     const float4 v = *(const float4*)(src + (k < g.K ? k : 0));
     a[t] = v.x; a[t + 1] = v.y; a[t + 2] = v.z; a[t + 3] = v.w;
   }
+  // the epilogue's operands (bias, gate, residual / accumulated C) requested before the
+  // MFMA chain, so their round trip overlaps it instead of following it: every lane loads
+  // and combines unconditionally (rows / columns clamped), only the stores are predicated
+  // -- a load used under a branch would be sunk past the MFMAs
+  const int ncol = n0 + r32;
+  const int ncl = ncol < g.N ? ncol : g.N - 1;
+  const float bv = g.bias ? g.bias[ncl] : 0.f;
+  const float gv = g.gate ? *g.gate : 1.f;
+  float rv[16], cv[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    int m = mt * 32 + crow32(r, h);
+    m = m < g.M ? m : g.M - 1;
+    if (HAS_R) rv[r] = g.R[(int64_t)(g.rmod > 0 ? m % g.rmod : m) * g.ldr + ncl];
+    if (HAS_C) cv[r] = g.C[(int64_t)m * g.ldc + ncl];
+  }
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
   for (int t = 0; t < KH; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[t], acc, 0, 0, 0);
-  const int ncol = n0 + r32;
-  if (ncol >= g.N) return;
-  const float bv = g.bias ? g.bias[ncol] : 0.f;
+  const bool colok = ncol < g.N;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int m = mt * 32 + crow32(r, h);
-    if (m >= g.M) continue;
+    const bool ok = colok && m < g.M;
     float v = acc[r] * g.alpha + bv;
     const int64_t ci = (int64_t)m * g.ldc + ncol;
-    if (g.pre) g.pre[ci] = v;
+    if (g.pre && ok) g.pre[ci] = v;
     if (g.act == 1) v = gelu_erf(v);
-    if (g.gate) v *= *g.gate;
-    if (g.R) v += g.R[(int64_t)(g.rmod > 0 ? m % g.rmod : m) * g.ldr + ncol];
-    if (g.accumulate) v += g.C[ci];
-    g.C[ci] = v;
+    if (g.gate) v *= gv;
+    if (HAS_R) v += rv[r];
+    if (HAS_C) v += cv[r];
+    if (ok) g.C[ci] = v;
   }
+}
+
+template <int KH, bool BKC, bool HR, bool HC>
+static void launch_rb2_e(const GemmArgs& g, int xcd, hipStream_t st) {
+  const int mb = (g.M + 127) / 128, nb = (g.N + 31) / 32;
+  if (xcd)
+    hipLaunchKernelGGL((gemm_rb2_kernel<KH, BKC, HR, HC>), dim3(xcd_grid(mb, nb)), dim3(256), 0, st,
+                       g, nb, 1);
+  else
+    hipLaunchKernelGGL((gemm_rb2_kernel<KH, BKC, HR, HC>), dim3(mb, nb), dim3(256), 0, st, g, nb, 0);
 }
 
 template <int KH, bool BKC>
@@ -212,21 +250,20 @@ static void launch_rb2(const GemmArgs& g, hipStream_t st) {
     const char* e = getenv("TVQ_GEMM_XCD");
     return e && e[0] == '0' ? 0 : 1;
   }();
-  const int mb = (g.M + 127) / 128, nb = (g.N + 31) / 32;
-  if (xcd)
-    hipLaunchKernelGGL((gemm_rb2_kernel<KH, BKC>), dim3(xcd_grid(mb, nb)), dim3(256), 0, st, g, nb, 1);
-  else
-    hipLaunchKernelGGL((gemm_rb2_kernel<KH, BKC>), dim3(mb, nb), dim3(256), 0, st, g, nb, 0);
+  if (g.R && g.accumulate) launch_rb2_e<KH, BKC, true, true>(g, xcd, st);
+  else if (g.R) launch_rb2_e<KH, BKC, true, false>(g, xcd, st);
+  else if (g.accumulate) launch_rb2_e<KH, BKC, false, true>(g, xcd, st);
+  else launch_rb2_e<KH, BKC, false, false>(g, xcd, st);
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <int KC, int WN, bool BKC>
-static void launch_skinny(const GemmArgs& g, hipStream_t st) {
+template <int KC, int WN, bool BKC, bool HR, bool HC>
+static void launch_skinny_e(const GemmArgs& g, hipStream_t st) {
   const int nch = (g.K + KC - 1) / KC;
   const size_t lds = (size_t)nch * KC * 32 * WN * sizeof(float);
   static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<KC, WN, BKC>,
+    (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<KC, WN, BKC, HR, HC>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
     return true;
   }();
@@ -236,7 +273,15 @@ static void launch_skinny(const GemmArgs& g, hipStream_t st) {
   int gx = 512 / nb;  // two resident blocks per CU, persistent over M
   if (gx < 1) gx = 1;
   if (gx > mtiles) gx = mtiles;
-  hipLaunchKernelGGL((gemm_skinny_kernel<KC, WN, BKC>), dim3(gx, nb), dim3(256), lds, st, g);
+  hipLaunchKernelGGL((gemm_skinny_kernel<KC, WN, BKC, HR, HC>), dim3(gx, nb), dim3(256), lds, st, g);
+}
+
+template <int KC, int WN, bool BKC>
+static void launch_skinny(const GemmArgs& g, hipStream_t st) {
+  if (g.R && g.accumulate) launch_skinny_e<KC, WN, BKC, true, true>(g, st);
+  else if (g.R) launch_skinny_e<KC, WN, BKC, true, false>(g, st);
+  else if (g.accumulate) launch_skinny_e<KC, WN, BKC, false, true>(g, st);
+  else launch_skinny_e<KC, WN, BKC, false, false>(g, st);
 }
 
 template <int KC, bool BKC>
