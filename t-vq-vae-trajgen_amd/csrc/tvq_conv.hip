@@ -21,6 +21,7 @@
 #include "tvq_common.h"
 #include "tvq_reduce.h"
 #include "tvq_conv_internal.h"
+#include "tvq_gemm.h"
 
 #include <stdlib.h>
 
@@ -1536,6 +1537,196 @@ static int64_t w8_ws(int64_t B, int64_t N, int64_t C) {
   return S * N * kc + reduce_rows_scratch(S, N * kc);
 }
 
+// ---------------------------------------------------------------- wide-map weight gradient
+// Weight (+ bias) gradient of stride-1 "same" 3x3 / 1x3 convs on maps whose rows are a
+// multiple of 32 wide, with >= 64 output channels -- the HF band's 128 -> 128 and
+// 16 -> 128 3x3 convs on (256, C, 3, 32) and the HF prior's Upscale Conv1d k3 on
+// (256, C, 1, 96), 7.25 / 4.8 GFLOP each, where the split 16x16x4 kernel with 16-position
+// LDS steps ran at ~0.3 of the fp32 MFMA peak.  A block owns a 128 (n) x 128 (k' = c*KK +
+// tap) tile of one split of the positions; positions go in stages of one 32-wide row
+// segment (b, h, w0 .. w0+31): the stage's dY rows (128 x 32, 16-B loads) and the input rows
+// its k' columns need (channels k0/KK .. (k0+127)/KK, KH rows, 34 floats with the zero
+// halo) are staged in LDS, double-buffered (the next stage's loads are in flight while this
+// one multiplies), and each of the 8 waves runs 2 interleaved v_mfma_f32_32x32x2_f32 chains
+// (32 n rows x 2 x 32 k' columns) over the stage's 16 position pairs.  The bias column
+// (k' = Kred) is summed by the k0 = 0 blocks from the staged dY rows.  Slabs summed in
+// split order (wgrad_finish).
+constexpr int WT_T = 512, WT_AP = 128 + 4;  // threads; staged dY pitch ([p][n], n fastest)
+template <int KH, int KW>
+struct WtCfg {
+  static constexpr int KK = KH * KW, NCH = 128 / KK + 2;  // channels a 128-column tile spans
+  static constexpr int XROW = 34, XCH = KH * XROW;        // staged row, floats per channel
+  static constexpr int AS = 32 * WT_AP, XS = NCH * XCH;   // floats per stage buffer
+  static constexpr int XPER = (XS + WT_T - 1) / WT_T;     // input loads per thread
+  static_assert(XPER <= 32, "staging mask");
+};
+
+struct WtGeom {
+  int B, C, N, H, W, Kred, kcols;
+  int segs;    // 32-wide segments per row (W / 32)
+  int spr;     // stages per split
+  int ntiles;  // 128-row n tiles
+};
+
+__device__ __forceinline__ int wt_crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+template <int KH, int KW>
+struct WtRegs {  // one stage's global loads, in flight until stored to LDS
+  float4 ga[2];
+  float xv[WtCfg<KH, KW>::XPER];
+  uint32_t ok;
+};
+
+template <int KH, int KW>
+__global__ __launch_bounds__(WT_T) void conv_wgrad_t32_kernel(const float* __restrict__ G,
+                                                             const float* __restrict__ X,
+                                                             float* __restrict__ slab, WtGeom g,
+                                                             int ktiles) {
+  using R = WtCfg<KH, KW>;
+  using Regs = WtRegs<KH, KW>;
+  constexpr int PH = KH / 2, PW = (KW - 1) / 2;
+  __shared__ float As[2][R::AS];
+  __shared__ float Xs[2][R::XS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wid & 3, wk = wid >> 2;
+  // XCD-aware map (tvq_gemm.h xcd_tile): the k' / n tiles of one position split share an
+  // XCD, so its dY rows are fetched into one L2 and re-read from there
+  int z, tile;
+  xcd_tile((int)blockIdx.x, ktiles * g.ntiles, &z, &tile);
+  const int nst = g.B * g.H * g.segs;
+  const int s_begin = z * g.spr, s_end = min(nst, s_begin + g.spr);
+  if (s_begin >= nst) return;  // padding block of the XCD map (no split)
+  const int k0 = (tile % ktiles) * 128, n0 = (tile / ktiles) * 128;
+  const int c_lo = k0 / R::KK;
+  // this lane's B-operand offsets into a stage's Xs: columns k' = k0 + 64 wk + 32 j + l % 32
+  // (past Kred: a valid column, never stored)
+  int boff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    int kp = k0 + wk * 64 + j * 32 + (lane & 31);
+    kp = kp < g.Kred ? kp : g.Kred - 1;
+    const int c = kp / R::KK, t = kp - c * R::KK, kh = t / KW, kw = t - kh * KW;
+    boff[j] = (c - c_lo) * R::XCH + kh * R::XROW + kw;
+  }
+  auto load = [&](Regs& q, int s) {
+    if (s >= s_end) return;
+    const int row = s / g.segs, w0 = (s - row * g.segs) * 32;
+    const int b = row / g.H, h = row - b * g.H;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // dY: 128 rows x 32 positions, 8 threads per row
+      const int e = tid + j * WT_T, n = e >> 3, p4 = (e & 7) * 4;
+      const int nn = n0 + n < g.N ? n0 + n : g.N - 1;
+      q.ga[j] = *(const float4*)(G + ((int64_t)(b * g.N + nn) * g.H + h) * g.W + w0 + p4);
+    }
+    q.ok = 0u;
+#pragma unroll
+    for (int u = 0; u < R::XPER; ++u) {  // input rows: (channel, kh, 34 columns)
+      const int e = tid + u * WT_T;
+      const int c = e / R::XCH, r = e - c * R::XCH, kh = r / R::XROW, jj = r - kh * R::XROW;
+      const int cc = c_lo + c, hi = h + kh - PH, wi = w0 - PW + jj;
+      const bool ok = e < R::XS && cc < g.C && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+      q.xv[u] = X[ok ? ((int64_t)(b * g.C + cc) * g.H + hi) * g.W + wi : 0];
+      q.ok |= (ok ? 1u : 0u) << u;
+    }
+  };
+  auto store = [&](const Regs& q, int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int e = tid + j * WT_T, n = e >> 3, p4 = (e & 7) * 4;
+      float* d = As[buf] + p4 * WT_AP + n;
+      d[0] = q.ga[j].x;
+      d[WT_AP] = q.ga[j].y;
+      d[2 * WT_AP] = q.ga[j].z;
+      d[3 * WT_AP] = q.ga[j].w;
+    }
+#pragma unroll
+    for (int u = 0; u < R::XPER; ++u) {
+      const int e = tid + u * WT_T;
+      if (e < R::XS) Xs[buf][e] = (q.ok >> u & 1u) ? q.xv[u] : 0.f;
+    }
+  };
+  floatx16 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  float bsum = 0.f;  // bias partial of row n0 + tid (k0 == 0 blocks, tid < 128)
+  // stage i: LDS buffer i & 1; two stages' loads in flight ahead of the one multiplying
+  auto body = [&](int s, const Regs& next, Regs& free) {
+    const int buf = (s - s_begin) & 1;
+    load(free, s + 2);
+    const float* as = As[buf] + wn * 32 + (lane & 31);
+    const float* xs = Xs[buf];
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int p = 2 * st + (lane >> 5);
+      const float a = as[p * WT_AP];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xs[boff[j] + p], acc[j], 0, 0, 0);
+    }
+    if (k0 == 0 && tid < 128) {
+#pragma unroll 8
+      for (int p = 0; p < 32; ++p) bsum += As[buf][p * WT_AP + tid];
+    }
+    if (s + 1 < s_end) store(next, buf ^ 1);
+    __syncthreads();
+  };
+  Regs r0, r1;
+  load(r0, s_begin);
+  load(r1, s_begin + 1);
+  store(r0, 0);
+  __syncthreads();
+  for (int s = s_begin; s < s_end; s += 2) {
+    body(s, r1, r0);                       // r1: stage s+1; r0 <- stage s+2
+    if (s + 1 < s_end) body(s + 1, r0, r1);  // r0: stage s+2; r1 <- stage s+3
+  }
+  float* sl = slab + (int64_t)z * g.N * g.kcols;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int kp = k0 + wk * 64 + j * 32 + (lane & 31);
+    if (kp >= g.Kred) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = n0 + wn * 32 + wt_crow(r, lane >> 5);
+      if (n < g.N) sl[(int64_t)n * g.kcols + kp] = acc[j][r];
+    }
+  }
+  if (k0 == 0 && tid < 128 && g.kcols > g.Kred && n0 + tid < g.N)
+    sl[(int64_t)(n0 + tid) * g.kcols + g.Kred] = bsum;
+}
+
+// TVQ_CONV_WT32=0 turns the wide-map weight-gradient kernel off (comparisons)
+static bool wt32_fits(int64_t B, int64_t C, int64_t H, int64_t Wi, int64_t N, int64_t Wo,
+                      int64_t KH, int64_t KW, int64_t SW, int64_t replicate) {
+  static const int on = [] {
+    const char* s = getenv("TVQ_CONV_WT32");
+    return s ? atoi(s) : 1;
+  }();
+  return on && SW == 1 && !replicate && KW == 3 && (KH == 1 || KH == 3) && Wi == Wo &&
+         Wi % 32 == 0 && N >= 64 && C >= 64 && B * C * H * Wi < (1ll << 31) &&
+         B * N * H * Wo < (1ll << 31);
+}
+static void wt32_plan(int64_t B, int64_t C, int64_t H, int64_t W, int64_t N, int64_t KK,
+                      int* S, int* spr) {
+  const int64_t kt = (C * KK + 127) / 128, nt = (N + 127) / 128;
+  const int64_t nst = B * H * (W / 32);
+  int64_t s = (512 + kt * nt - 1) / (kt * nt);  // ~2 blocks per CU
+  if (s > 256) s = 256;
+  if (s > nst) s = nst;
+  if (s < 1) s = 1;
+  const int64_t per = (nst + s - 1) / s;
+  *spr = (int)per;
+  *S = (int)((nst + per - 1) / per);
+}
+static int64_t wt32_ws(int64_t B, int64_t C, int64_t H, int64_t W, int64_t N, int64_t KK) {
+  int S, spr;
+  wt32_plan(B, C, H, W, N, KK, &S, &spr);
+  const int64_t kc = C * KK + 1;
+  return (int64_t)S * N * kc + reduce_rows_scratch(S, N * kc);
+}
+
 struct WHaloPlan {
   WHaloGeom g;
   int FN, S, nblk, cblk;
@@ -2577,7 +2768,9 @@ static int64_t conv_wgrad_ws(int64_t N, int64_t C, int64_t KH, int64_t KW, int64
   const int64_t a = wgrad_ws(N, C * KH * KW, B * Hout * Wo, nullptr, nullptr);
   const int64_t h = whalo_ws(N, C, KH, KW, B);
   const int64_t w = (KH == 3 && KW == 3 && B % W8_IMG == 0) ? w8_ws(B, N, C) : 0;
-  return std::max(a, std::max(h, w));
+  const int64_t t = wt32_fits(B, C, Hout, Wo, N, Wo, KH, KW, 1, 0)
+                        ? wt32_ws(B, C, Hout, Wo, N, KH * KW) : 0;
+  return std::max(std::max(a, t), std::max(h, w));
 }
 
 // op: 0 conv2d fwd, 1 convT2d fwd, 2 conv2d dgrad, 3 convT2d dgrad, 4 conv2d wgrad,
@@ -2656,6 +2849,24 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
                          (int)KW, PH_OF(KH), PW_OF(KW), Ci * KH * KW, KH * KW);
   const int kcols = g.Kred + (db ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
+  if (wt32_fits(B, Ci, H, Wi, Co, Wo, KH, KW, SW, replicate)) {
+    WtGeom t;
+    t.B = (int)B; t.C = (int)Ci; t.N = (int)Co; t.H = (int)H; t.W = (int)Wi;
+    t.Kred = g.Kred; t.kcols = kcols; t.segs = (int)(Wi / 32);
+    int S;
+    wt32_plan(B, Ci, H, Wi, Co, KH * KW, &S, &t.spr);
+    const int kt = (g.Kred + 127) / 128;
+    t.ntiles = (int)((Co + 127) / 128);
+    const dim3 grid(xcd_grid(S, kt * t.ntiles));
+    if (KH == 3)
+      hipLaunchKernelGGL((conv_wgrad_t32_kernel<3, 3>), grid, dim3(WT_T), 0, st, dy, x, workspace, t,
+                         kt);
+    else
+      hipLaunchKernelGGL((conv_wgrad_t32_kernel<1, 3>), grid, dim3(WT_T), 0, st, dy, x, workspace, t,
+                         kt);
+    wgrad_finish(workspace, S, Co, kcols, dw, db, (int)accumulate, st);
+    return launch_status("tvq_conv2d_wgrad(t32)");
+  }
   if (w8_fits(B, Ci, H, Wi, Co, Wo, KH, KW, SW, replicate)) {
     const int S = (int)(B / W8_IMG);
     const int PS = whalo_plane_stride(5 * ((int)Wi + 2), 9, 3, (int)Wi + 2, 1, 8);

@@ -61,6 +61,9 @@ def _run_both(fn_hip, fn_ref, shapes, cuda, seed=0):
     (4, 12, 4, 257, "enc"), (3, 8, 16, 64, "enc"), (2, 32, 64, 16, "enc"),
     (4, 8, 8, 64, "res"), (2, 64, 128, 8, "res"), (2, 16, 128, 32, "res"), (3, 128, 16, 32, "res"),
     (2, 64, 128, 8, "proj"), (5, 3, 7, 33, "res"),
+    # the wide-map weight-gradient kernel (conv_wgrad_t32_kernel): the HF 128 -> 128 conv,
+    # an uneven last position split (37 images), a 64-wide map
+    (2, 128, 128, 32, "res"), (37, 128, 128, 32, "res"), (3, 32, 64, 64, "res"),
 ])
 @pytest.mark.parametrize("path", ["default", "halo", "gemm", "tap", "gemm_raw"])
 def test_conv2d(B, Ci, Co, W, kind, path, cuda, conv_path):
@@ -104,10 +107,11 @@ def test_conv_transpose2d(B, Ci, Co, W, path, cuda, conv_path):
         close(d[i].grad, c[i].grad, what=n)
 
 
-def test_conv1d_k3(cuda):
+@pytest.mark.parametrize("B,Ci,Co", [(8, 128, 256), (20, 256, 128)])  # the HF prior's Upscale
+def test_conv1d_k3(B, Ci, Co, cuda):
     from timevqvae.hip.conv import conv2d
     oc, od, c, d = _run_both(lambda x, w, b: conv2d(x, w, b), lambda x, w, b: F.conv1d(x, w, b, padding=1),
-                             [(8, 128, 96), (256, 128, 3), (256,)], cuda)
+                             [(B, Ci, 96), (Co, Ci, 3), (Co,)], cuda)
     close(od, oc, what="fwd")
     for i, n in enumerate(("dx", "dw", "db")):
         close(d[i].grad, c[i].grad, what=n)
