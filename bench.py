@@ -404,7 +404,7 @@ def conv_wgrad_leg(device):
 
 
 def resblock_bwd_leg(device, C=16, W=32):
-    """The step's top kernel by summed time (profiles/r03*_step_kernel_stats.csv): the fused
+    """The round-3a top kernel by summed time (profiles/r03a_step_kernel_stats.csv): the fused
     ResBlock backward (csrc/tvq_resblock.hip rb_bwd2 + rb_bwd1, reference vq_vae.py:13-62) at
     its most frequent shape, C = 16 on (256, 16, 3, 32) (8 ops per step).  One op = rb_bwd2
     (dropout' -> conv2 weight gradient slab row + data gradient -> Snake' -> per-image BN
@@ -468,6 +468,53 @@ def resblock_bwd_leg(device, C=16, W=32):
             "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def vq_assign_leg(device):
+    """The step's top kernel by summed time (profiles/r03b_step_kernel_stats.csv): the VQ
+    codebook assignment vq_assign_kernel (csrc/tvq_vq.hip; reference vq.py:205-222
+    EuclideanCodebook: dist = -(|x|^2 - 2 x E^T + |E|^2), argmax), at the HF band's training
+    shape: the (256, 128, 3, 32) NCHW latent read as (B, 96 tokens, D = 128) through its
+    strides against K = 512 codes, straight-through output, commit partials and the token-
+    major copy for the EMA statistics (tvq_vq_assign_rows, as hip.vq.vq runs it).
+    Algorithmic work per launch: 2 M K D = 2 x 24576 x 512 x 128 = 3.22 GFLOP; bytes: x read,
+    E read, quantised x written, int64 + int32 indices = 4 (2 M D + K D) + 12 M = 25.7 MB
+    (AI 125 FLOP/B: fp32 MFMA bound).  50 graph-replayed launches timed with HIP events."""
+    from timevqvae.hip._native import call, ptr, stream_ptr, value
+    B, D, H, W, K = 256, 128, 3, 32, 512
+    N = H * W
+    M = B * N
+    g = torch.Generator(device="cpu").manual_seed(7)
+    x = torch.randn(B, D, H, W, generator=g).to(device)
+    E = torch.randn(K, D, generator=g).to(device)
+    ee = torch.empty(K, device=device)
+    call("tvq_vq_sqnorm", ptr(E), K, D, ptr(ee), stream_ptr())
+    out = torch.empty_like(x)
+    idx = torch.empty(M, device=device, dtype=torch.long)
+    idx32 = torch.empty(M, device=device, dtype=torch.int32)
+    part = torch.empty(value("tvq_vq_assign_nblocks", M), device=device)
+    rows = torch.empty(M, D, device=device)
+    sB, sN, sD = D * N, 1, N  # the token view (B, N, D) of the NCHW latent
+    fn = (lambda: call("tvq_vq_assign_rows", ptr(x), B, N, D, sB, sN, sD, ptr(E), ptr(ee), K, 1,
+                       0.0, None, None, 0, ptr(out), ptr(idx), ptr(idx32), ptr(part), ptr(rows),
+                       stream_ptr()))
+    with torch.no_grad():
+        us = _graph_time_us([fn], 50)
+    flops = 2.0 * M * K * D
+    byts = 4.0 * (2 * M * D + K * D) + 12.0 * M
+    tf = flops / (us * 1e-6) / 1e12
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "r03_vqassign_traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath))["traffic_bytes"]
+    return {"bound": "mfma", "kernel": "vq_assign_kernel<128,false>: HF codebook assignment, "
+                                       "24576 token rows x 512 codes x D 128, 16x16x4 fp32 "
+                                       "MFMA distances + running argmax, straight-through "
+                                       "output, token-major copy for the EMA statistics",
+            "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def linear_fwd_leg(device):
     """The LF prior's Linear forward at its training shape (gemm_rb2_kernel<64, true>: 14 of
     its 15 launches per step are this shape): Y = R + X W^T + b over the 6400 token rows of
@@ -504,12 +551,16 @@ def linear_fwd_leg(device):
 
 
 def roofline_leg(device, ms_per_step):
-    """bench JSON `roofline`: the step's top kernel by summed time, the fused ResBlock
-    backward (resblock_bwd_leg), at top level; the LF 64-channel conv weight gradient
-    (`conv_wgrad`, conv_wgrad_leg); the largest single launch of the step, the grouped Linear
-    weight gradients of the LF prior (`wgrad_group`, dominant_leg); the whole step against
-    the fp32 MFMA peak (`step`); the largest single conv on MFMA (`conv_t32`)."""
-    out = resblock_bwd_leg(device)
+    """bench JSON `roofline`: the step's top kernel by summed time, the VQ codebook
+    assignment (vq_assign_leg), at top level; the fused ResBlock backward (`resblock_bwd`,
+    resblock_bwd_leg); the LF prior's Linear forward (`linear_fwd`); the LF 64-channel conv
+    weight gradient (`conv_wgrad`, conv_wgrad_leg); the largest single launch of the step,
+    the grouped Linear weight gradients of the LF prior (`wgrad_group`, dominant_leg); the
+    whole step against the fp32 MFMA peak (`step`); the largest single conv on MFMA
+    (`conv_t32`)."""
+    out = vq_assign_leg(device)
+    out["resblock_bwd"] = resblock_bwd_leg(device)
+    out["linear_fwd"] = linear_fwd_leg(device)
     out["conv_wgrad"] = conv_wgrad_leg(device)
     out["wgrad_group"] = dominant_leg(device)
     tf = STEP_GFLOP / ms_per_step  # GFLOP / ms = TFLOP/s

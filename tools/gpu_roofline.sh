@@ -24,4 +24,7 @@ fi
 if [ "$LEG" = linfwd ]; then
   python tools/roof_traffic.py $O $O/traffic.json "LF prior Linear forward (6400x128)x(128x128) + bias + residual: gemm_rb2_kernel<64,true>" gemm_rb2_kernel
 fi
+if [ "$LEG" = vqassign ]; then
+  python tools/roof_traffic.py $O $O/traffic.json "HF VQ codebook assignment, 24576 token rows x 512 codes x D 128 (straight-through, token-major copy): vq_assign_kernel" vq_assign_kernel
+fi
 echo roofline-done
