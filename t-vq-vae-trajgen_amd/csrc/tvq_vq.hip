@@ -1,10 +1,10 @@
 // VQ codebook kernels (K7/K8/K9 in SURVEY.md §2.2) for gfx950.
 //
-// assign: 64 token rows per 512-thread workgroup.  Each wave keeps its 16 rows'
-// x values in registers as fp32 MFMA A-fragments (D/4 VGPRs) for the whole
-// launch and streams the codebook through LDS in 128-code chunks; waves 0-3 own
-// code columns [0,64) of every chunk, waves 4-7 columns [64,128).  (32-row blocks
-// streamed the whole codebook through LDS twice as often per token row.)  x.E^T runs on
+// assign: 16 RG token rows per workgroup of 2 RG waves (RG per launch, vq_rg: 6 for the
+// HF band's 24576 rows -- one workgroup per CU -- and 4 for the LF band's 6144).  Each wave
+// keeps its 16 rows' x values in registers as fp32 MFMA A-fragments (D/4 VGPRs) for the
+// whole launch and streams the codebook through LDS in 128-code chunks; waves 0..RG-1 own
+// code columns [0,64) of every chunk, waves RG..2RG-1 columns [64,128).  x.E^T runs on
 // v_mfma_f32_16x16x4_f32 (exact fp32 FMA chains); the argmin is a running
 // per-lane (value, index) pair merged across the 16 code lanes by shuffles and
 // across the two code halves through LDS.  The epilogue gathers q = E[idx],
@@ -17,8 +17,9 @@
 
 namespace tvq {
 
-constexpr int VQ_BM = 64;   // token rows per workgroup
-constexpr int VQ_T = 512;   // threads: 4 row groups of 16 x 2 code halves
+// a workgroup = RG row groups of 16 token rows x 2 code halves (2 RG waves); RG is chosen
+// per launch (vq_rg) so that the busiest SIMD runs as few waves as possible
+constexpr int VQ_RG_MAX = 6;
 constexpr int VQ_CK = 128;  // codes per LDS chunk
 
 // (v, i) "better" for argmin of t with first-index tie break.  A NaN distance beats every
@@ -75,12 +76,13 @@ __device__ __forceinline__ float gumbel_at(const Svq& sv, uint64_t seed, int64_t
   return -logf(-logf(u));
 }
 
-template <int D, bool STOCH>
-__global__ __launch_bounds__(VQ_T) void vq_assign_kernel(
+template <int D, bool STOCH, int RG>
+__global__ __launch_bounds__(128 * RG) void vq_assign_kernel(
     const float* __restrict__ x, int64_t M, int64_t N, int64_t sB, int64_t sN, int64_t sD,
     const float* __restrict__ E, const float* __restrict__ ee, int K, int training,
     float* __restrict__ quant, int64_t* __restrict__ idx, int32_t* __restrict__ idx32,
     float* __restrict__ commit_partial, Svq sv, float* __restrict__ xt) {
+  constexpr int VQ_BM = 16 * RG, VQ_T = 128 * RG, NW = 2 * RG;
   constexpr int S = D + 8;  // LDS row stride (floats): conflict-free ds_read_b128 B-fragments
   constexpr int NQ = D / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -88,10 +90,10 @@ __global__ __launch_bounds__(VQ_T) void vq_assign_kernel(
   float* xx_s = smem + VQ_CK * S;         // [VQ_BM]
   float* bv_s = xx_s + VQ_BM;             // [2][VQ_BM]
   int* bi_s = (int*)(bv_s + 2 * VQ_BM);   // [2][VQ_BM]
-  float* red = (float*)(bi_s + 2 * VQ_BM);  // [8]
+  float* red = (float*)(bi_s + 2 * VQ_BM);  // [NW]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int rg = wid & 3, ch = wid >> 2;
+  const int rg = wid % RG, ch = wid / RG;
   const int r16 = lane & 15, g = lane >> 4;
   const int64_t row0 = (int64_t)blockIdx.x * VQ_BM;
 
@@ -232,9 +234,12 @@ __global__ __launch_bounds__(VQ_T) void vq_assign_kernel(
     csum = wave_sum(csum);
     if (lane == 0) red[wid] = csum;
     __syncthreads();
-    if (tid == 0)
-      commit_partial[blockIdx.x] = ((red[0] + red[1]) + (red[2] + red[3])) +
-                                   ((red[4] + red[5]) + (red[6] + red[7]));
+    if (tid == 0) {
+      float t = red[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) t += red[w];
+      commit_partial[blockIdx.x] = t;
+    }
   }
 }
 
@@ -315,7 +320,23 @@ extern "C" int tvq_vq_sqnorm(const float* E, int64_t K, int64_t D, float* ee, tv
   return launch_status("tvq_vq_sqnorm");
 }
 
-extern "C" int64_t tvq_vq_assign_nblocks(int64_t M) { return (M + VQ_BM - 1) / VQ_BM; }
+// row groups per workgroup: 6 (96 rows, 12 waves) when that still fills every CU with a
+// workgroup -- the HF band's 24576 rows as 256 workgroups, one per CU: 55 us, where 64-row
+// workgroups (384: two on half the CUs) took 60 us and 48 / 32-row ones 66 / 85 us (each
+// workgroup streams the whole codebook through LDS); else 4 (64 rows)
+static int vq_rg(int64_t M) {
+  static const int forced = [] {
+    const char* e = getenv("TVQ_VQ_RG");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 1 || forced == 2 || forced == 3 || forced == 4 || forced == 6) return forced;
+  return M >= 256 * 96 ? 6 : 4;
+}
+
+extern "C" int64_t tvq_vq_assign_nblocks(int64_t M) {
+  const int rg = vq_rg(M);
+  return (M + 16 * rg - 1) / (16 * rg);
+}
 
 extern "C" int tvq_vq_assign(const float* x, int64_t B, int64_t N, int64_t D, int64_t sB,
                              int64_t sN, int64_t sD, const float* E, const float* ee, int64_t K,
@@ -349,21 +370,27 @@ extern "C" int tvq_vq_assign_rows(const float* x, int64_t B, int64_t N, int64_t 
   TVQ_CHECK_ARG(!training || commit_partial, "tvq_vq_assign: training needs commit_partial");
   TVQ_CHECK_ARG(K < INT_MAX, "tvq_vq_assign: K too large");
   const int64_t M = B * N;
+  const int rg = vq_rg(M);
   const int64_t nb = tvq_vq_assign_nblocks(M);
-  const size_t lds_tail = (VQ_BM + 4 * VQ_BM) * 4 + 32;
+  const size_t lds_tail = (size_t)(16 * rg * 5) * 4 + 4 * 2 * VQ_RG_MAX + 32;
   hipStream_t st = (hipStream_t)stream;
   const Svq sv = {temp, gumbel, seed_ptr, offset};
+#define TVQ_ASSIGN_RG(DD, ST, RGV)                                                           \
+  if (rg == RGV)                                                                             \
+    hipLaunchKernelGGL((vq_assign_kernel<DD, ST, RGV>), dim3(nb), dim3(128 * RGV), lds, st, x,  \
+                       M, N, sB, sN, sD, E, ee, (int)K, training, quant, idx, idx32,         \
+                       commit_partial, sv, xt);
+#define TVQ_ASSIGN_ST(DD, ST) \
+  TVQ_ASSIGN_RG(DD, ST, 1) TVQ_ASSIGN_RG(DD, ST, 2) TVQ_ASSIGN_RG(DD, ST, 3) \
+  TVQ_ASSIGN_RG(DD, ST, 4) TVQ_ASSIGN_RG(DD, ST, 6)
 #define TVQ_ASSIGN(DD)                                                                       \
   case DD: {                                                                                 \
     const size_t lds = (size_t)VQ_CK * (DD + 8) * 4 + lds_tail;                              \
-    if (sv.temp > 0.f)                                                                       \
-      hipLaunchKernelGGL((vq_assign_kernel<DD, true>), dim3(nb), dim3(VQ_T), lds, st, x, M, N, \
-                         sB, sN, sD, E, ee, (int)K, training, quant, idx, idx32,             \
-                         commit_partial, sv, xt);                                            \
-    else                                                                                     \
-      hipLaunchKernelGGL((vq_assign_kernel<DD, false>), dim3(nb), dim3(VQ_T), lds, st, x, M, N,\
-                         sB, sN, sD, E, ee, (int)K, training, quant, idx, idx32,             \
-                         commit_partial, sv, xt);                                            \
+    if (sv.temp > 0.f) {                                                                     \
+      TVQ_ASSIGN_ST(DD, true)                                                                \
+    } else {                                                                                 \
+      TVQ_ASSIGN_ST(DD, false)                                                               \
+    }                                                                                        \
     break;                                                                                   \
   }
   switch (D) {
@@ -375,6 +402,8 @@ extern "C" int tvq_vq_assign_rows(const float* x, int64_t B, int64_t N, int64_t 
       return TVQ_ERR_ARG;
   }
 #undef TVQ_ASSIGN
+#undef TVQ_ASSIGN_ST
+#undef TVQ_ASSIGN_RG
   return launch_status("tvq_vq_assign");
 }
 
