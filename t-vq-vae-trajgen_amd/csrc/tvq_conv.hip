@@ -1213,6 +1213,197 @@ __global__ __launch_bounds__(256) void conv_small_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------- stride-2 small-channel
+// The 3x4 stride-2 convs with <= 16 channels on both sides at the bands' full widths: the
+// EncBlock convs (F, replicate padding), the decoders' ConvTranspose tails (T) and the data
+// gradients of both (T into the replicate canvas / F).  The staged GEMMs above ran them at
+// 0.02-0.1 of peak: 9 K-steps of 16 with a branchy per-element gather and two barriers
+// each.  Here a block owns one image's 64-wide output segment on every output row: the input
+// rows it reads (C x rows x the segment's columns) are staged in LDS once, zero / replicate
+// padding applied while staging, and each wave runs its 16-position tiles as 16x16x4 MFMA
+// chains (rows = output channels, weights held in registers; columns = positions, read from
+// the staged rows).  F: k = (c, kh) x kw on the lane groups, every tap of the window is a
+// term.  T (stride-2 gather): the output parity fixes which two kw have an integer source,
+// so each wave takes one parity and its K is c x kh x {two kw} (half the taps, no zero terms).
+constexpr int S2_SEG = 64;                 // output positions per segment
+constexpr int S2_XRF = 2 * S2_SEG + 2;     // F: staged columns (stride 2, 4 taps)
+constexpr int S2_XRT = S2_SEG / 2 + 4;     // T: staged columns (source offsets -2..2)
+
+// F: out[b,n,h,wo] = sum_{c,kh,kw} w(n,c,kh,kw) in[b,c,h+kh-1,2wo+kw-opw], H = 3
+template <bool REPL, int CS>
+__global__ __launch_bounds__(256) void conv_s2f_kernel(const float* __restrict__ in,
+                                                       const float* __restrict__ wt,
+                                                       float* __restrict__ out, ConvGeom g, Epi e) {
+  constexpr int NS = 3 * CS, RS = 5;  // K-steps (c, kh); staged rows hi = -1..3
+  constexpr int XN = CS * RS * S2_XRF, XPER = (XN + 255) / 256;
+  __shared__ float Xs[XN];
+  const int tid = threadIdx.x, lane = tid & 63, r16 = lane & 15, g4 = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int segs = (g.Wo + S2_SEG - 1) / S2_SEG;
+  const int b = blockIdx.x / segs, w0 = (blockIdx.x - b * segs) * S2_SEG;
+  // weights of row n = r16, tap kw = g4, step s = (c, kh)
+  float af[NS];
+  const int nr = r16 < g.N ? r16 : 0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int c = s / 3, kh = s - 3 * c;
+    const int cc = c < g.C ? c : 0;
+    af[s] = wt[nr * g.wsn + cc * g.wsc + (kh * 4 + g4) * g.wst];
+  }
+  const float* inb = in + (int64_t)b * g.C * g.Hin * g.Win;
+  float xv[XPER];
+  uint64_t okm = 0;
+#pragma unroll
+  for (int u = 0; u < XPER; ++u) {
+    const int i = tid + 256 * u;
+    const int ck = i / S2_XRF, j = i - ck * S2_XRF, c = ck / RS, r = ck - RS * c;
+    int hi = r - 1, wi = 2 * w0 - g.opw + j;
+    bool ok = i < XN && c < g.C;
+    if (REPL) {
+      hi = hi < 0 ? 0 : (hi >= g.Hin ? g.Hin - 1 : hi);
+      wi = wi < 0 ? 0 : (wi >= g.Win ? g.Win - 1 : wi);
+    } else {
+      ok = ok && hi >= 0 && hi < g.Hin && wi >= 0 && wi < g.Win;
+    }
+    xv[u] = inb[ok ? ((int64_t)c * g.Hin + hi) * g.Win + wi : 0];
+    okm |= (uint64_t)(ok ? 1 : 0) << u;
+  }
+#pragma unroll
+  for (int u = 0; u < XPER; ++u) {
+    const int i = tid + 256 * u;
+    if (i < XN) Xs[i] = (okm >> u & 1) ? xv[u] : 0.f;
+  }
+  float bv[1][4];
+  const int nbase = 4 * g4;
+  epi_load_bias<1>(bv, e.bias, nbase, g.N);
+  __syncthreads();
+  // 12 tiles (3 rows x 4 position groups of 16), 3 per wave
+  floatx4 acc[3];
+  const float* xb[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int tile = wid * 3 + t, h = tile >> 2, p0 = (tile & 3) * 16;
+    xb[t] = Xs + h * S2_XRF + 2 * (p0 + r16) + g4;
+    acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int c = s / 3, kh = s - 3 * c, off = (c * RS + kh) * S2_XRF;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) acc[t] = mfma16x16x4(af[s], xb[t][off], acc[t]);
+  }
+  const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
+  const int64_t hw = (int64_t)g.Hout * g.Wo;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int tile = wid * 3 + t, h = tile >> 2;
+    const int wo = w0 + (tile & 3) * 16 + r16;
+    const bool pv = wo < g.Wo;
+    const floatx4 a[1] = {acc[t]};
+    epi_store<1>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + (pv ? wo : 0), hw,
+                 nbase, g.N, pv);
+  }
+}
+
+// T: out[b,n,h,wo] = sum w(n,c,kh,kw) in[b,c,h-kh+oph,(wo-kw+opw)/2] over the integer
+// sources, Hin = 3, HO = Hout (3, or 5 for the replicate canvas)
+template <int CS, int HO>
+__global__ __launch_bounds__(256) void conv_s2t_kernel(const float* __restrict__ in,
+                                                       const float* __restrict__ wt,
+                                                       float* __restrict__ out, ConvGeom g, Epi e) {
+  constexpr int NS = 6 * CS / 4, RS = 7;  // K-steps; staged rows hi = -2..4
+  constexpr int XN = CS * RS * S2_XRT, XPER = (XN + 255) / 256;
+  __shared__ float Xs[XN];
+  const int tid = threadIdx.x, lane = tid & 63, r16 = lane & 15, g4 = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int par = wid & 1, mb = wid >> 1;  // this wave's output parity and 16-column group
+  const int segs = (g.Wo + S2_SEG - 1) / S2_SEG;
+  const int b = blockIdx.x / segs, w0 = (blockIdx.x - b * segs) * S2_SEG;
+  const int m0 = w0 >> 1;  // staged column j <-> source column m0 - 2 + j
+  // step s, lane group g4: k = 4s + g4 = (c, kh, e), kw = q + 2e with q = (par + opw) & 1
+  float af[NS];
+  int soff[NS];
+  const int nr = r16 < g.N ? r16 : 0, q = (par + g.opw) & 1;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int k = 4 * s + g4, c = k / 6, rem = k - 6 * c, kh = rem >> 1, kw = q + 2 * (rem & 1);
+    const int cc = c < g.C ? c : 0;
+    af[s] = wt[nr * g.wsn + cc * g.wsc + (kh * 4 + kw) * g.wst];
+    soff[s] = (c * RS - kh) * S2_XRT + ((par + g.opw - kw) >> 1);
+  }
+  const float* inb = in + (int64_t)b * g.C * g.Hin * g.Win;
+  float xv[XPER];
+  uint32_t okm = 0;
+  static_assert(XPER <= 32, "staging mask");
+#pragma unroll
+  for (int u = 0; u < XPER; ++u) {
+    const int i = tid + 256 * u;
+    const int ck = i / S2_XRT, j = i - ck * S2_XRT, c = ck / RS, r = ck - RS * c;
+    const int hi = r - 2, wi = m0 - 2 + j;
+    const bool ok = i < XN && c < g.C && hi >= 0 && hi < g.Hin && wi >= 0 && wi < g.Win;
+    xv[u] = inb[ok ? ((int64_t)c * g.Hin + hi) * g.Win + wi : 0];
+    okm |= (uint32_t)(ok ? 1 : 0) << u;
+  }
+#pragma unroll
+  for (int u = 0; u < XPER; ++u) {
+    const int i = tid + 256 * u;
+    if (i < XN) Xs[i] = (okm >> u & 1) ? xv[u] : 0.f;
+  }
+  float bv[1][4];
+  const int nbase = 4 * g4;
+  epi_load_bias<1>(bv, e.bias, nbase, g.N);
+  __syncthreads();
+  floatx4 acc[HO];
+  const float* xb = Xs + (g.oph + 2) * S2_XRT + mb * 16 + r16 + 2;
+#pragma unroll
+  for (int h = 0; h < HO; ++h) acc[h] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int h = 0; h < HO; ++h) acc[h] = mfma16x16x4(af[s], xb[h * S2_XRT + soff[s]], acc[h]);
+  const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
+  const int64_t hw = (int64_t)g.Hout * g.Wo;
+  const int wo = w0 + 2 * (mb * 16 + r16) + par;
+  const bool pv = wo < g.Wo;
+#pragma unroll
+  for (int h = 0; h < HO; ++h) {
+    const floatx4 a[1] = {acc[h]};
+    epi_store<1>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + (pv ? wo : 0), hw,
+                 nbase, g.N, pv);
+  }
+}
+
+static int g_conv_s2 = 1;  // conv_s2f / conv_s2t enabled (tvq_conv_config bit 512 turns them off)
+
+// which stride-2 small-channel kernel takes this launch: 0 none, 1 F, 2 T (Hout 3), 3 T (5)
+static int s2_kind(int mode, const ConvGeom& g) {
+  if (!g_conv_s2 || g.C > 16 || g.N > 16 || g.Hin != 3) return 0;
+  if (mode == GATHER_F)
+    return g.Hout == 3 && g.oph == 1 && g.opw >= 0 && g.opw <= 2 ? 1 : 0;
+  if (g.opw < 0 || g.opw > 3) return 0;
+  if (g.Hout == 3 && g.oph == 1) return 2;
+  if (g.Hout == 5 && g.oph == 0) return 3;
+  return 0;
+}
+
+template <bool REPL>
+static void launch_s2(int kind, const float* in, const float* wt, float* out, const ConvGeom& g,
+                      const Epi& e, hipStream_t st) {
+  const dim3 grid((unsigned)(g.B * ((g.Wo + S2_SEG - 1) / S2_SEG)));
+  const int cs = (g.C + 3) / 4;
+#define S2F(CSV) hipLaunchKernelGGL((conv_s2f_kernel<REPL, CSV>), grid, dim3(256), 0, st, in, wt, out, g, e)
+#define S2T(CSV, HOV) hipLaunchKernelGGL((conv_s2t_kernel<CSV, HOV>), grid, dim3(256), 0, st, in, wt, out, g, e)
+  if (kind == 1) {
+    if (cs == 1) S2F(4); else if (cs == 2) S2F(8); else if (cs == 3) S2F(12); else S2F(16);
+  } else if (kind == 2) {
+    if (cs == 1) S2T(4, 3); else if (cs == 2) S2T(8, 3); else if (cs == 3) S2T(12, 3); else S2T(16, 3);
+  } else {
+    if (cs == 1) S2T(4, 5); else if (cs == 2) S2T(8, 5); else if (cs == 3) S2T(12, 5); else S2T(16, 5);
+  }
+#undef S2F
+#undef S2T
+}
+
 static int g_conv_small = 1;  // conv_small_kernel enabled (tvq_conv_config bit 256 turns it off)
 
 static constexpr int HALO_LDS_MAX = 64 * 1024;
@@ -2421,6 +2612,13 @@ static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g
   // stride-2 transposed gathers with <= 12 channels on both sides (the decoders' ConvT tail
   // and DecBlocks 8->4, the EncBlocks' data gradients), loses to the halo / staged paths
   // elsewhere
+  if constexpr (KH == 3 && KW == 4 && SW == 2) {
+    const int k2 = s2_kind(MODE, g);
+    if (k2) {
+      launch_s2<REPL>(k2, in, wt, out, g, e, st);
+      return;
+    }
+  }
   if (g_conv_small && MODE == GATHER_T && SW == 2 && g.C <= 12 && g.N <= 12) {
     const int64_t th = (int64_t)g.B * g.Hout * ((g.Wo + 1) / 2);
     // outputs per thread rounded up to 4 (every channel's sum in the same order)
@@ -2595,7 +2793,7 @@ extern "C" int tvq_conv_wgrad_defer_flush(tvq_stream_t stream) {
 extern "C" int tvq_conv_config(int64_t halo) {
   const int prev = g_conv_halo | (g_conv_t32 ? 0 : 8) | (g_t32_bk == 32 ? 16 : 0) |
                    (g_t32_bk == 16 ? 32 : 0) | (g_t32_nw == 4 ? 64 : 0) |
-                   (g_t32_n64 ? 128 : 0) | (g_conv_small ? 0 : 256);
+                   (g_t32_n64 ? 128 : 0) | (g_conv_small ? 0 : 256) | (g_conv_s2 ? 0 : 512);
   if (halo >= 0) {
     g_conv_halo = (int)(halo & 7);
     g_conv_t32 = (halo & 8) ? 0 : 1;
@@ -2603,6 +2801,7 @@ extern "C" int tvq_conv_config(int64_t halo) {
     g_t32_nw = (halo & 64) ? 4 : 12;
     g_t32_n64 = (halo & 128) ? 1 : 0;
     g_conv_small = (halo & 256) ? 0 : 1;
+    g_conv_s2 = (halo & 512) ? 0 : 1;
   }
   return prev;
 }

@@ -68,7 +68,8 @@ struct RB {
   // conv: the waves are NR x NCH (row tile, input-channel chunk of CPC) combos times CMS
   // position groups; a wave runs CNF 16-position tiles of its combo as interleaved chains
   // that share the weight operand (1 + CNF LDS reads per CNF MFMAs)
-  static constexpr int NCH = (C / 4) < (RB_NW / NR) ? C / 4 : RB_NW / NR;
+  static constexpr int NCH0 = (C / 4) < (RB_NW / NR) ? C / 4 : RB_NW / NR;
+  static constexpr int NCH = NCH0 < 4 ? NCH0 : 4;  // chunk partials stay within the LDS
   static constexpr int CPC = C / NCH;
   static constexpr int CMS = RB_NW / (NR * NCH), CNF = (MT + CMS - 1) / CMS;
   static constexpr int PR = P + ((4 - P % 8) + 8) % 8;  // conv partial row stride == 4 mod 8

@@ -31,14 +31,15 @@ def conv_path(monkeypatch):
     """Select the conv engine: the default per-shape choice, the halo-tile kernel
     wherever it fits, the staged GEMMs with packed weights (32x32-MFMA wide tile where
     eligible; "tap" = the 16x16 tap-major kernel only), or the staged GEMM reading the
-    weights in place."""
+    weights in place; "no_s2" = the default choice without the stride-2 small-channel
+    kernels (conv_s2f / conv_s2t)."""
     from timevqvae.hip import conv as conv_mod
     from timevqvae.hip._native import value
     prev = value("tvq_conv_config", -1)
 
     def select(path):
         monkeypatch.setattr(conv_mod, "USE_WORKSPACE", path != "gemm_raw")
-        value("tvq_conv_config", {"default": 3, "halo": 7, "tap": 8}.get(path, 0))
+        value("tvq_conv_config", {"default": 3, "halo": 7, "tap": 8, "no_s2": 3 | 512}.get(path, 0))
 
     yield select
     value("tvq_conv_config", prev)
@@ -59,13 +60,15 @@ def _run_both(fn_hip, fn_ref, shapes, cuda, seed=0):
 
 @pytest.mark.parametrize("B,Ci,Co,W,kind", [
     (4, 12, 4, 257, "enc"), (3, 8, 16, 64, "enc"), (2, 32, 64, 16, "enc"),
+    # stride-2 small-channel kernels: 16 channels, channels not a multiple of 4, ragged widths
+    (2, 16, 16, 128, "enc"), (2, 6, 5, 70, "enc"), (3, 4, 8, 130, "enc"),
     (4, 8, 8, 64, "res"), (2, 64, 128, 8, "res"), (2, 16, 128, 32, "res"), (3, 128, 16, 32, "res"),
     (2, 64, 128, 8, "proj"), (5, 3, 7, 33, "res"),
     # the wide-map weight-gradient kernel (conv_wgrad_t32_kernel): the HF 128 -> 128 conv,
     # an uneven last position split (37 images), a 64-wide map
     (2, 128, 128, 32, "res"), (37, 128, 128, 32, "res"), (3, 32, 64, 64, "res"),
 ])
-@pytest.mark.parametrize("path", ["default", "halo", "gemm", "tap", "gemm_raw"])
+@pytest.mark.parametrize("path", ["default", "halo", "gemm", "tap", "gemm_raw", "no_s2"])
 def test_conv2d(B, Ci, Co, W, kind, path, cuda, conv_path):
     from timevqvae.hip.conv import conv2d
     conv_path(path)
@@ -91,8 +94,8 @@ def test_conv2d(B, Ci, Co, W, kind, path, cuda, conv_path):
 
 
 @pytest.mark.parametrize("B,Ci,Co,W", [(4, 64, 32, 8), (2, 8, 4, 64), (3, 4, 12, 128), (2, 12, 12, 256),
-                                        (2, 128, 128, 16)])
-@pytest.mark.parametrize("path", ["default", "halo", "gemm", "tap", "gemm_raw"])
+                                        (2, 128, 128, 16), (2, 16, 16, 40), (3, 5, 7, 37)])
+@pytest.mark.parametrize("path", ["default", "halo", "gemm", "tap", "gemm_raw", "no_s2"])
 def test_conv_transpose2d(B, Ci, Co, W, path, cuda, conv_path):
     from timevqvae.hip.conv import conv_transpose2d
     conv_path(path)
