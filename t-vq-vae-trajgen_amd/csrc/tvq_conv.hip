@@ -1404,6 +1404,171 @@ static void launch_s2(int kind, const float* in, const float* wt, float* out, co
 #undef S2T
 }
 
+// Weight (+ bias) gradient of the same stride-2 small-channel convs, in the F-gather form
+// both directions share (conv2d: G = dY, In = x;  ConvTranspose2d: G = x, In = dY):
+//   dW[n][c,kh,kw] = sum_{b,h,w} G[b,n,h,w] In[b,c,h+kh-1,2w+kw-opw],  db[n] = sum G
+// A block (8 waves) walks stages of one image's 64-wide G segment on all 3 rows: the G rows
+// (16 x 192) and the input rows they read (C x 5 x 130, padding applied while staging) go
+// through LDS with the next stage's loads in flight.  Wave w owns k' tiles w%4, w%4+4, ...
+// of the N x (12C+1) slab row for half of the stage's positions (w/4), so a k-step is one
+// G read shared by its tiles; each lane's column pointer is fixed once (window cell, a
+// ones plane for the bias column, a zeros plane past it).  The position halves are summed
+// in order at the end; blocks write slab rows (<= 256, one deferred ordered sum).
+constexpr int W2_T = 512, W2_GS = 3 * S2_SEG + 4, W2_KP = 2 * S2_XRF + 2 * S2_SEG + 8;
+struct W2Geom {
+  int B, C, N, Win, Wo, Kred, kcols, segs, spr, opw;
+};
+
+template <bool REPL, int CS>
+__global__ __launch_bounds__(W2_T) void conv_wgrad_s2_kernel(const float* __restrict__ G,
+                                                            const float* __restrict__ X,
+                                                            float* __restrict__ slab, W2Geom g) {
+  constexpr int RS = 5, XN = CS * RS * S2_XRF, XPER = (XN + W2_T - 1) / W2_T;
+  constexpr int GN = 16 * 3 * S2_SEG, GPER = GN / W2_T;
+  constexpr int KT = (12 * CS + 1 + 15) / 16, TPW = (KT + 3) / 4;
+  constexpr int RED = 4 * TPW * 256;
+  static_assert(XPER <= 32 && GN % W2_T == 0, "staging");
+  __shared__ float Xs[XN > RED ? XN : RED];  // after the stages: the second half's tiles
+  __shared__ float Gs[16 * W2_GS];
+  __shared__ float K1[2 * W2_KP];  // ones | zeros
+  const int tid = threadIdx.x, lane = tid & 63, r16 = lane & 15, g4 = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tg = wid & 3, ph = wid >> 2;  // tile group, position half
+  const int nst = g.B * g.segs, z = blockIdx.x;
+  const int s_begin = z * g.spr, s_end = min(nst, s_begin + g.spr);
+  for (int i = tid; i < 2 * W2_KP; i += W2_T) K1[i] = i < W2_KP ? 1.f : 0.f;
+  // this lane's column pointer per tile (position offsets added per k-step)
+  const float* bp[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int kc = (tg + 4 * t) * 16 + r16;
+    const int k = kc < g.Kred ? kc : 0, c = k / 12, rem = k - 12 * c, kh = rem >> 2;
+    bp[t] = (kc < g.Kred ? Xs + (c * RS + kh) * S2_XRF + (rem & 3)
+                         : (kc == g.Kred && g.kcols > g.Kred ? K1 : K1 + W2_KP)) + 2 * g4;
+  }
+  const float* ap = Gs + r16 * W2_GS + g4;
+  float xv[XPER], gv[GPER];
+  uint32_t okm = 0, gok = 0;
+  auto load = [&](int s) {
+    const int b = s / g.segs, w0 = (s - b * g.segs) * S2_SEG;
+    const float* xb = X + (int64_t)b * g.C * 3 * g.Win;
+#pragma unroll
+    for (int u = 0; u < XPER; ++u) {
+      const int i = tid + W2_T * u;
+      const int ck = i / S2_XRF, j = i - ck * S2_XRF, c = ck / RS, r = ck - RS * c;
+      int hi = r - 1, wi = 2 * w0 - g.opw + j;
+      bool ok = i < XN && c < g.C;
+      if (REPL) {
+        hi = hi < 0 ? 0 : (hi > 2 ? 2 : hi);
+        wi = wi < 0 ? 0 : (wi >= g.Win ? g.Win - 1 : wi);
+      } else {
+        ok = ok && hi >= 0 && hi < 3 && wi >= 0 && wi < g.Win;
+      }
+      xv[u] = xb[ok ? ((int64_t)c * 3 + hi) * g.Win + wi : 0];
+      okm = u == 0 ? (ok ? 1u : 0u) : (okm | (ok ? 1u : 0u) << u);
+    }
+    const float* gb = G + (int64_t)b * g.N * 3 * g.Wo;
+#pragma unroll
+    for (int u = 0; u < GPER; ++u) {
+      const int i = tid + W2_T * u;
+      const int n = i / (3 * S2_SEG), p = i - n * (3 * S2_SEG), h = p / S2_SEG, w = w0 + p - h * S2_SEG;
+      const bool ok = n < g.N && w < g.Wo;
+      gv[u] = gb[ok ? ((int64_t)n * 3 + h) * g.Wo + w : 0];
+      gok = u == 0 ? (ok ? 1u : 0u) : (gok | (ok ? 1u : 0u) << u);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < XPER; ++u) {
+      const int i = tid + W2_T * u;
+      if (i < XN) Xs[i] = (okm >> u & 1u) ? xv[u] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < GPER; ++u) {
+      const int i = tid + W2_T * u;
+      const int n = i / (3 * S2_SEG), p = i - n * (3 * S2_SEG);
+      Gs[n * W2_GS + p] = (gok >> u & 1u) ? gv[u] : 0.f;
+    }
+  };
+  floatx4 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (s_begin < s_end) load(s_begin);
+  for (int s = s_begin; s < s_end; ++s) {
+    __syncthreads();  // the previous stage's reads are done
+    store();
+    __syncthreads();
+    if (s + 1 < s_end) load(s + 1);  // in flight during this stage's chains
+    // this half's 24 k-steps: positions p = 96 ph + 4 i + g4 (row p / 64, column p % 64)
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      const int p0 = 96 * ph + 4 * i, h = p0 / S2_SEG, w = p0 - h * S2_SEG;
+      const float a = ap[p0];
+      const int off = h * S2_XRF + 2 * w;
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) acc[t] = mfma16x16x4(a, bp[t][off], acc[t]);
+    }
+  }
+  __syncthreads();
+  floatx4* red = reinterpret_cast<floatx4*>(Xs);
+  if (ph == 1) {
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) red[(tg * TPW + t) * 64 + lane] = acc[t];
+  }
+  __syncthreads();
+  if (ph == 0) {
+    float* sl = slab + (int64_t)z * g.N * g.kcols;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const floatx4 o = red[(tg * TPW + t) * 64 + lane];
+      const int kc = (tg + 4 * t) * 16 + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 4 * g4 + r;
+        const float v = acc[t][r] + o[r];
+        if (n < g.N && kc < g.kcols) sl[(int64_t)n * g.kcols + kc] = v;
+      }
+    }
+  }
+}
+
+static int g_conv_ws2 = 1;  // conv_wgrad_s2_kernel enabled (tvq_conv_config bit 1024 turns it off)
+
+static bool ws2_fits(int64_t C, int64_t H, int64_t N, int64_t KH, int64_t KW, int64_t SW) {
+  return g_conv_ws2 && KH == 3 && KW == 4 && SW == 2 && H == 3 && C <= 16 && N <= 16;
+}
+static void ws2_plan(int64_t B, int64_t Wo, int* S, int* spr) {
+  const int64_t nst = B * ((Wo + S2_SEG - 1) / S2_SEG);
+  const int64_t s = nst < RR_ONE_ROWS ? nst : RR_ONE_ROWS;
+  const int64_t per = (nst + s - 1) / s;
+  *spr = (int)per;
+  *S = (int)((nst + per - 1) / per);
+}
+static int64_t ws2_ws(int64_t B, int64_t C, int64_t Wo, int64_t N) {
+  int S, spr;
+  ws2_plan(B, Wo, &S, &spr);
+  const int64_t kc = C * 12 + 1;
+  return (int64_t)S * N * kc + reduce_rows_scratch(S, N * kc);
+}
+// G (B, N, 3, Wo) against In (B, C, 3, Win) -> slab rows; returns the row count
+static int ws2_launch(const float* G, const float* X, float* slab, int B, int C, int N, int Win,
+                      int Wo, int kcols, bool repl, hipStream_t st) {
+  W2Geom w;
+  w.B = B; w.C = C; w.N = N; w.Win = Win; w.Wo = Wo; w.Kred = 12 * C; w.kcols = kcols;
+  w.segs = (Wo + S2_SEG - 1) / S2_SEG; w.opw = 1;
+  int S;
+  ws2_plan(B, Wo, &S, &w.spr);
+  const int cs = (C + 3) / 4;
+#define W2L(R, CSV) hipLaunchKernelGGL((conv_wgrad_s2_kernel<R, CSV>), dim3(S), dim3(W2_T), 0, st, G, X, slab, w)
+  if (repl) {
+    if (cs == 1) W2L(true, 4); else if (cs == 2) W2L(true, 8); else if (cs == 3) W2L(true, 12); else W2L(true, 16);
+  } else {
+    if (cs == 1) W2L(false, 4); else if (cs == 2) W2L(false, 8); else if (cs == 3) W2L(false, 12); else W2L(false, 16);
+  }
+#undef W2L
+  return S;
+}
+
 static int g_conv_small = 1;  // conv_small_kernel enabled (tvq_conv_config bit 256 turns it off)
 
 static constexpr int HALO_LDS_MAX = 64 * 1024;
@@ -2793,7 +2958,8 @@ extern "C" int tvq_conv_wgrad_defer_flush(tvq_stream_t stream) {
 extern "C" int tvq_conv_config(int64_t halo) {
   const int prev = g_conv_halo | (g_conv_t32 ? 0 : 8) | (g_t32_bk == 32 ? 16 : 0) |
                    (g_t32_bk == 16 ? 32 : 0) | (g_t32_nw == 4 ? 64 : 0) |
-                   (g_t32_n64 ? 128 : 0) | (g_conv_small ? 0 : 256) | (g_conv_s2 ? 0 : 512);
+                   (g_t32_n64 ? 128 : 0) | (g_conv_small ? 0 : 256) | (g_conv_s2 ? 0 : 512) |
+                   (g_conv_ws2 ? 0 : 1024);
   if (halo >= 0) {
     g_conv_halo = (int)(halo & 7);
     g_conv_t32 = (halo & 8) ? 0 : 1;
@@ -2802,6 +2968,7 @@ extern "C" int tvq_conv_config(int64_t halo) {
     g_t32_n64 = (halo & 128) ? 1 : 0;
     g_conv_small = (halo & 256) ? 0 : 1;
     g_conv_s2 = (halo & 512) ? 0 : 1;
+    g_conv_ws2 = (halo & 1024) ? 0 : 1;
   }
   return prev;
 }
@@ -2969,7 +3136,9 @@ static int64_t conv_wgrad_ws(int64_t N, int64_t C, int64_t KH, int64_t KW, int64
   const int64_t w = (KH == 3 && KW == 3 && B % W8_IMG == 0) ? w8_ws(B, N, C) : 0;
   const int64_t t = wt32_fits(B, C, Hout, Wo, N, Wo, KH, KW, 1, 0)
                         ? wt32_ws(B, C, Hout, Wo, N, KH * KW) : 0;
-  return std::max(std::max(a, t), std::max(h, w));
+  // conv_wgrad_s2 (Wo: the width of G)
+  const int64_t s2 = (KH == 3 && KW == 4 && C <= 16 && N <= 16) ? ws2_ws(B, C, Wo, N) : 0;
+  return std::max(std::max(std::max(a, t), std::max(h, w)), s2);
 }
 
 // op: 0 conv2d fwd, 1 convT2d fwd, 2 conv2d dgrad, 3 convT2d dgrad, 4 conv2d wgrad,
@@ -3048,6 +3217,12 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
                          (int)KW, PH_OF(KH), PW_OF(KW), Ci * KH * KW, KH * KW);
   const int kcols = g.Kred + (db ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
+  if (ws2_fits(Ci, H, Co, KH, KW, SW)) {
+    const int S = ws2_launch(dy, x, workspace, (int)B, (int)Ci, (int)Co, (int)Wi, (int)Wo, kcols,
+                             replicate != 0, st);
+    wgrad_finish(workspace, S, Co, kcols, dw, db, (int)accumulate, st);
+    return launch_status("tvq_conv2d_wgrad(s2)");
+  }
   if (wt32_fits(B, Ci, H, Wi, Co, Wo, KH, KW, SW, replicate)) {
     WtGeom t;
     t.B = (int)B; t.C = (int)Ci; t.N = (int)Co; t.H = (int)H; t.W = (int)Wi;
@@ -3135,6 +3310,12 @@ extern "C" int tvq_convT2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t 
   ConvGeom g = make_geom((int)B, (int)Co, (int)H, (int)Wo, (int)Ci, (int)H, (int)Wi, (int)KH,
                          (int)KW, PH_OF(KH), PW_OF(KW), Co * KH * KW, KH * KW);
   hipStream_t st = (hipStream_t)stream;
+  if (ws2_fits(Co, H, Ci, KH, KW, SW)) {
+    const int S = ws2_launch(x, dy, workspace, (int)B, (int)Co, (int)Ci, (int)Wo, (int)Wi, g.Kred,
+                             false, st);
+    wgrad_finish(workspace, S, Ci, g.Kred, dw, nullptr, (int)accumulate, st);
+    return launch_status("tvq_convT2d_wgrad(s2)");
+  }
   WHaloPlan pl;
   if ((g_conv_halo & 2) && whalo_plan((int)B, (int)Co, (int)H, (int)Wo, (int)Ci, (int)H, (int)Wi,
                                       (int)KH, (int)KW, (int)SW, PH_OF(KH), PW_OF(KW), g.Kred,

@@ -32,14 +32,14 @@ def conv_path(monkeypatch):
     wherever it fits, the staged GEMMs with packed weights (32x32-MFMA wide tile where
     eligible; "tap" = the 16x16 tap-major kernel only), or the staged GEMM reading the
     weights in place; "no_s2" = the default choice without the stride-2 small-channel
-    kernels (conv_s2f / conv_s2t)."""
+    kernels (conv_s2f / conv_s2t / conv_wgrad_s2)."""
     from timevqvae.hip import conv as conv_mod
     from timevqvae.hip._native import value
     prev = value("tvq_conv_config", -1)
 
     def select(path):
         monkeypatch.setattr(conv_mod, "USE_WORKSPACE", path != "gemm_raw")
-        value("tvq_conv_config", {"default": 3, "halo": 7, "tap": 8, "no_s2": 3 | 512}.get(path, 0))
+        value("tvq_conv_config", {"default": 3, "halo": 7, "tap": 8, "no_s2": 3 | 512 | 1024}.get(path, 0))
 
     yield select
     value("tvq_conv_config", prev)
