@@ -1306,8 +1306,11 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(const float* __restrict__
 }
 
 // T: out[b,n,h,wo] = sum w(n,c,kh,kw) in[b,c,h-kh+oph,(wo-kw+opw)/2] over the integer
-// sources, Hin = 3, HO = Hout (3, or 5 for the replicate canvas)
-template <int CS, int HO>
+// sources, Hin = 3, HO = Hout (3, or 5 for the replicate canvas).  FOLD (the data gradient
+// of a replicate-padded conv): the canvas (5 rows, Wo = Wx + 2 columns) is folded onto
+// out = dx (3 rows, Wx columns) in the epilogue -- rows 0+1, 2, 3+4; canvas columns 0 / Wx+1
+// onto dx columns 0 / Wx-1 through LDS -- instead of a canvas store and a fold launch.
+template <int CS, int HO, bool FOLD = false>
 __global__ __launch_bounds__(256) void conv_s2t_kernel(const float* __restrict__ in,
                                                        const float* __restrict__ wt,
                                                        float* __restrict__ out, ConvGeom g, Epi e) {
@@ -1361,9 +1364,36 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(const float* __restrict__
   for (int s = 0; s < NS; ++s)
 #pragma unroll
     for (int h = 0; h < HO; ++h) acc[h] = mfma16x16x4(af[s], xb[h * S2_XRT + soff[s]], acc[h]);
+  const int wo = w0 + 2 * (mb * 16 + r16) + par;
+  if constexpr (FOLD) {
+    static_assert(HO == 5, "fold: replicate canvas");
+    __shared__ floatx4 ex[2][3][4];
+    const int Wx = g.Wo - 2;
+    floatx4 y[3] = {acc[0] + acc[1], acc[2], acc[3] + acc[4]};
+    if (wo == 0 || wo == Wx + 1) {
+#pragma unroll
+      for (int h = 0; h < 3; ++h) ex[wo == 0 ? 0 : 1][h][g4] = y[h];
+    }
+    __syncthreads();
+    if (wo == 1) {
+#pragma unroll
+      for (int h = 0; h < 3; ++h) y[h] = ex[0][h][g4] + y[h];
+    } else if (wo == Wx) {
+#pragma unroll
+      for (int h = 0; h < 3; ++h) y[h] = y[h] + ex[1][h][g4];
+    }
+    const bool pv = wo >= 1 && wo <= Wx;
+#pragma unroll
+    for (int h = 0; h < 3; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = nbase + r;
+        if (pv && n < g.N) out[(((int64_t)b * g.N + n) * 3 + h) * Wx + wo - 1] = y[h][r];
+      }
+    return;
+  }
   const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
   const int64_t hw = (int64_t)g.Hout * g.Wo;
-  const int wo = w0 + 2 * (mb * 16 + r16) + par;
   const bool pv = wo < g.Wo;
 #pragma unroll
   for (int h = 0; h < HO; ++h) {
@@ -1401,6 +1431,21 @@ static void launch_s2(int kind, const float* in, const float* wt, float* out, co
     if (cs == 1) S2T(4, 5); else if (cs == 2) S2T(8, 5); else if (cs == 3) S2T(12, 5); else S2T(16, 5);
   }
 #undef S2F
+#undef S2T
+}
+
+// data gradient of a replicate-padded conv straight into dx (canvas geometry g, Wx = Wo - 2):
+// the canvas columns Wx and Wx + 1 must share a segment
+static bool s2_fold_fits(const ConvGeom& g) {
+  return s2_kind(GATHER_T, g) == 3 && g.Wo >= 4 && (g.Wo - 1) % S2_SEG != 0;
+}
+static void launch_s2_fold(const float* in, const float* wt, float* dx, const ConvGeom& g,
+                           hipStream_t st) {
+  const dim3 grid((unsigned)(g.B * ((g.Wo + S2_SEG - 1) / S2_SEG)));
+  const Epi e = {nullptr, nullptr, 0.f, 1.f, nullptr, 0};
+  const int cs = (g.C + 3) / 4;
+#define S2T(CSV) hipLaunchKernelGGL((conv_s2t_kernel<CSV, 5, true>), grid, dim3(256), 0, st, in, wt, dx, g, e)
+  if (cs == 1) S2T(4); else if (cs == 2) S2T(8); else if (cs == 3) S2T(12); else S2T(16);
 #undef S2T
 }
 
@@ -3075,6 +3120,10 @@ extern "C" int tvq_conv2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t 
     TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
     return launch_status("tvq_conv2d_dgrad");
+  }
+  if (KH == 3 && KW == 4 && SW == 2 && s2_fold_fits(g)) {
+    launch_s2_fold(dy, w, dx, g, st);
+    return launch_status("tvq_conv2d_dgrad(replicate, s2)");
   }
   TVQ_CHECK_ARG(workspace, "tvq_conv2d_dgrad: replicate needs a workspace");
   float* canvas = workspace;

@@ -62,6 +62,7 @@ def _run_both(fn_hip, fn_ref, shapes, cuda, seed=0):
     (4, 12, 4, 257, "enc"), (3, 8, 16, 64, "enc"), (2, 32, 64, 16, "enc"),
     # stride-2 small-channel kernels: 16 channels, channels not a multiple of 4, ragged widths
     (2, 16, 16, 128, "enc"), (2, 6, 5, 70, "enc"), (3, 4, 8, 130, "enc"),
+    (2, 4, 4, 63, "enc"),  # replicate-canvas columns W, W+1 across a segment: canvas + fold
     (4, 8, 8, 64, "res"), (2, 64, 128, 8, "res"), (2, 16, 128, 32, "res"), (3, 128, 16, 32, "res"),
     (2, 64, 128, 8, "proj"), (5, 3, 7, 33, "res"),
     # the wide-map weight-gradient kernel (conv_wgrad_t32_kernel): the HF 128 -> 128 conv,
