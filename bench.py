@@ -330,8 +330,9 @@ def _graph_time_us(fns, reps):
 
 
 def dominant_leg(device):
-    """The step's largest single launch (profiles/r02e_step_kernel_stats.csv): the grouped
-    weight gradient dW_i += dY_i^T X_i of every Linear of a prior, issued once
+    """The step's top kernel by summed time (profiles/r03c_step_kernel_stats.csv:
+    wgrad_wide_kernel, 4 launches and 239 us per step) and its largest single launch: the
+    grouped weight gradient dW_i += dY_i^T X_i of every Linear of a prior, issued once
     at the end of its backward (timevqvae.hip.wgrad; 32x32x2 fp32 MFMA, 64x64 tiles, K =
     tokens split over 4 waves x S blocks) with its ordered slab sum wgrad_group_reduce_kernel
     (one op = these 2 launches).  Timed on the LF prior's set, accumulating into one flat
@@ -356,7 +357,7 @@ def dominant_leg(device):
     byts = sum(4.0 * (K * (M + N) + 2 * M * N) for M, N in shapes)
     tf = flops / (us * 1e-6) / 1e12
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r02e_dominant_traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "r03_dominant_traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath))["traffic_bytes"]
     return {"bound": "mfma", "kernel": "wgrad_wide_kernel + wgrad_group_reduce_kernel (grouped "
@@ -469,8 +470,8 @@ def resblock_bwd_leg(device, C=16, W=32):
 
 
 def vq_assign_leg(device):
-    """The step's top kernel by summed time (profiles/r03b_step_kernel_stats.csv): the VQ
-    codebook assignment vq_assign_kernel (csrc/tvq_vq.hip; reference vq.py:205-222
+    """The VQ codebook assignment vq_assign_kernel (the step's top kernel by summed time in
+    profiles/r03b_step_kernel_stats.csv, second in r03c: 4 launches, 192 us per step) (csrc/tvq_vq.hip; reference vq.py:205-222
     EuclideanCodebook: dist = -(|x|^2 - 2 x E^T + |E|^2), argmax), at the HF band's training
     shape: the (256, 128, 3, 32) NCHW latent read as (B, 96 tokens, D = 128) through its
     strides against K = 512 codes, straight-through output, commit partials and the token-
@@ -551,18 +552,18 @@ def linear_fwd_leg(device):
 
 
 def roofline_leg(device, ms_per_step):
-    """bench JSON `roofline`: the step's top kernel by summed time, the VQ codebook
-    assignment (vq_assign_leg), at top level; the fused ResBlock backward (`resblock_bwd`,
-    resblock_bwd_leg); the LF prior's Linear forward (`linear_fwd`); the LF 64-channel conv
-    weight gradient (`conv_wgrad`, conv_wgrad_leg); the largest single launch of the step,
-    the grouped Linear weight gradients of the LF prior (`wgrad_group`, dominant_leg); the
-    whole step against the fp32 MFMA peak (`step`); the largest single conv on MFMA
-    (`conv_t32`)."""
-    out = vq_assign_leg(device)
+    """bench JSON `roofline`: the step's top kernel by summed time, the grouped Linear
+    weight gradients of the LF prior (dominant_leg), at top level (also under
+    `wgrad_group`); the VQ codebook assignment (`vq_assign`); the fused ResBlock backward
+    (`resblock_bwd`, resblock_bwd_leg); the LF prior's Linear forward (`linear_fwd`); the LF
+    64-channel conv weight gradient (`conv_wgrad`, conv_wgrad_leg); the whole step against
+    the fp32 MFMA peak (`step`); the largest single conv on MFMA (`conv_t32`)."""
+    out = dominant_leg(device)
+    out["wgrad_group"] = dict(out)
+    out["vq_assign"] = vq_assign_leg(device)
     out["resblock_bwd"] = resblock_bwd_leg(device)
     out["linear_fwd"] = linear_fwd_leg(device)
     out["conv_wgrad"] = conv_wgrad_leg(device)
-    out["wgrad_group"] = dominant_leg(device)
     tf = STEP_GFLOP / ms_per_step  # GFLOP / ms = TFLOP/s
     out["step"] = {"bound": "mfma", "gflop": STEP_GFLOP, "achieved": round(tf, 2),
                    "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
