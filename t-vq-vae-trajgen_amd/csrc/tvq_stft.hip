@@ -206,6 +206,51 @@ __global__ void istft_decode_bwd_kernel(const float* __restrict__ dy, int B, int
   }
 }
 
+// Same gradient, one block per (b, c) row: the interpolation's adjoint d(sample)[s] is
+// computed once per sample into LDS (the per-element kernel above recomputes it for each of
+// the up to 3 frames and 6 image planes that read it: ~18x the gather work), then every
+// image element of the row reads its <= 3 samples with the same per-term arithmetic.
+__global__ void istft_decode_bwd_row_kernel(const float* __restrict__ dy, int C, int W, int band,
+                                            Interp ip, int Tout, float* __restrict__ dh) {
+  extern __shared__ float ds[];
+  const int L = W - 1;
+  const int64_t bc = blockIdx.x;
+  const int64_t b = bc / C;
+  const int c = (int)(bc - b * C);
+  const float* dyr = dy + bc * Tout;
+  for (int s = threadIdx.x; s < L; s += blockDim.x) ds[s] = dsample(dyr, ip, Tout, s);
+  __syncthreads();
+  const int n = 2 * 3 * W;
+  float* out = dh + ((b * 2 * C + 2 * c) * 3) * (int64_t)W;  // (b, 2c + z, f, t), z-major
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int z = e / (3 * W), rem = e - z * 3 * W, f = rem / W, t = rem - f * W;
+    float g = 0.f;
+    const bool live = (band == 0)   ? (f == 0 && z == 0)
+                      : (band == 1) ? (f >= 1 && !(f == 2 && z == 1))
+                                    : !(z == 1 && f != 1);
+    if (live) {
+      float k1, k2, k3;
+      if (f == 0) { k1 = 0.5f; k2 = 0.5f; k3 = 0.5f; }
+      else if (f == 2) { k1 = -0.5f; k2 = 0.5f; k3 = -0.5f; }
+      else if (z == 0) { k1 = 0.f; k2 = -1.0f; k3 = 0.f; }
+      else { k1 = -1.0f; k2 = 0.f; k3 = 1.0f; }
+      if (k1 != 0.f && t - 1 >= 0 && t - 1 < L) {
+        const int s = t - 1;
+        g += ds[s] * 0.5f * k1 / (s == 0 ? 1.25f : 1.5f);
+      }
+      if (k2 != 0.f && t < L) {
+        const int s = t;
+        g += ds[s] * 1.0f * k2 / (s == 0 ? 1.25f : 1.5f);
+      }
+      if (k3 != 0.f && t + 1 < L) {
+        const int s = t + 1;
+        g += ds[s] * 0.5f * k3 / 1.5f;
+      }
+    }
+    out[e] = g;
+  }
+}
+
 static int ew_blocks(int64_t n) {
   int64_t b = (n + 255) / 256;
   return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -244,6 +289,12 @@ extern "C" int tvq_istft_decode_bwd(const float* dy, int64_t B, int64_t C, int64
   Interp ip;
   ip.L = (int)W - 1;
   ip.ratio = (float)ip.L / (float)Tout;
+  if (W - 1 <= 16384 && B * C < (1ll << 31)) {  // the row's samples fit the LDS
+    hipLaunchKernelGGL(istft_decode_bwd_row_kernel, dim3((unsigned)(B * C)), dim3(256),
+                       (size_t)(W - 1) * sizeof(float), (hipStream_t)stream, dy, (int)C, (int)W,
+                       (int)band, ip, (int)Tout, dh);
+    return launch_status("tvq_istft_decode_bwd");
+  }
   const int64_t n = B * 2 * C * 3 * W;
   hipLaunchKernelGGL(istft_decode_bwd_kernel, dim3(ew_blocks(n)), dim3(256), 0,
                      (hipStream_t)stream, dy, (int)B, (int)C, (int)W, (int)band, ip, (int)Tout, dh);
