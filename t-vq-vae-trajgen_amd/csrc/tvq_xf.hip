@@ -659,6 +659,38 @@ __global__ void upsample_nearest_t_bwd_kernel(const float* __restrict__ dy, int 
   }
 }
 
+// Same gradient, one block per (b, 64-channel tile): lanes walk consecutive i (so the dY
+// rows are read along j, coalesced) with the per-element loop above, the tile goes through
+// LDS and is written token-major with lanes along d.  Lin <= 128.
+constexpr int UPT_D = 64;
+__global__ __launch_bounds__(256) void upsample_nearest_t_bwd_tile_kernel(
+    const float* __restrict__ dy, int Lin, int D, int Lout, float scale, float* __restrict__ dx) {
+  __shared__ float T[128 * (UPT_D + 1)];
+  const int dtiles = (D + UPT_D - 1) / UPT_D;
+  const int b = blockIdx.x / dtiles, d0 = (blockIdx.x - b * dtiles) * UPT_D;
+  for (int e = threadIdx.x; e < UPT_D * Lin; e += 256) {
+    const int dd = e / Lin, i = e - dd * Lin, d = d0 + dd;
+    float s = 0.f;
+    if (d < D) {
+      const float* row = dy + ((int64_t)b * D + d) * Lout;
+      int j0 = (int)floorf((float)i / scale) - 2;
+      if (j0 < 0) j0 = 0;
+      for (int j = j0; j < Lout; ++j) {
+        int src = (int)floorf((float)j * scale);
+        if (src > Lin - 1) src = Lin - 1;
+        if (src > i) break;
+        if (src == i) s += row[j];
+      }
+    }
+    T[i * (UPT_D + 1) + dd] = s;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < UPT_D * Lin; e += 256) {
+    const int i = e / UPT_D, dd = e - i * UPT_D;
+    if (d0 + dd < D) dx[((int64_t)b * Lin + i) * D + d0 + dd] = T[i * (UPT_D + 1) + dd];
+  }
+}
+
 // out[j*ldo + d] (+)= sum_b in[b*sb + j*sj + d], b in order (one thread per (j, d)): batch
 // sums of position tables (the tied-logits bias (n, K+1), the position embedding)
 __global__ void batch_colsum_kernel(const float* __restrict__ in, int B, int64_t sb, int n,
@@ -746,6 +778,13 @@ extern "C" int tvq_upsample_nearest_t_bwd(const float* dy, int64_t B, int64_t Li
                                           int64_t Lout, float* dx, tvq_stream_t stream) {
   TVQ_CHECK_ARG(dy && dx && B > 0 && Lin > 0 && D > 0 && Lout > 0,
                 "tvq_upsample_nearest_t_bwd: bad args");
+  if (Lin <= 128) {
+    const int64_t blocks = B * ((D + UPT_D - 1) / UPT_D);
+    hipLaunchKernelGGL(upsample_nearest_t_bwd_tile_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, dy, (int)Lin, (int)D, (int)Lout,
+                       (float)Lin / (float)Lout, dx);
+    return launch_status("tvq_upsample_nearest_t_bwd");
+  }
   hipLaunchKernelGGL(upsample_nearest_t_bwd_kernel, dim3(grid_for(B * Lin * D)), dim3(256), 0,
                      (hipStream_t)stream, dy, (int)B, (int)Lin, (int)D, (int)Lout,
                      (float)Lin / (float)Lout, dx);

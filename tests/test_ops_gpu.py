@@ -665,3 +665,22 @@ def test_conv_wgrad_narrow_image_batched(B, Ci, Co, cuda):
     conv2d(x.to(cuda), wd, bd).backward(g.to(cuda))
     close(wd.grad, wc.grad, what="dw")
     close(bd.grad, bc.grad, what="db")
+
+
+@pytest.mark.parametrize("B,Lin,D,Lout", [(4, 32, 128, 96), (3, 25, 70, 97), (2, 130, 16, 300)])
+def test_upsample_nearest_t(B, Lin, D, Lout, cuda):
+    """(b, n, d) -> F.interpolate(x.transpose(1, 2), Lout, 'nearest'): forward and the
+    gradient (tiled kernel for Lin <= 128, the per-element one above) against torch."""
+    from timevqvae.hip.xf import upsample_nearest_t
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(B, Lin, D, generator=gen)
+    gy = torch.randn(B, D, Lout, generator=gen)
+    xc = x.clone().requires_grad_(True)
+    yc = F.interpolate(xc.transpose(1, 2), Lout, mode="nearest")
+    yc.backward(gy)
+    xd = x.to(cuda).requires_grad_(True)
+    yd = upsample_nearest_t(xd, Lout)
+    yd.backward(gy.to(cuda))
+    torch.cuda.synchronize()
+    assert torch.equal(yd.cpu(), yc.detach())
+    close(xd.grad, xc.grad, what="dx")
