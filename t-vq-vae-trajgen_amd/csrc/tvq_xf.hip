@@ -691,21 +691,37 @@ __global__ __launch_bounds__(256) void upsample_nearest_t_bwd_tile_kernel(
   }
 }
 
-// out[j*ldo + d] (+)= sum_b in[b*sb + j*sj + d], b in order (one thread per (j, d)): batch
-// sums of position tables (the tied-logits bias (n, K+1), the position embedding)
-__global__ void batch_colsum_kernel(const float* __restrict__ in, int B, int64_t sb, int n,
-                                    int64_t sj, int D, float* __restrict__ out, int64_t ldo,
-                                    int accumulate) {
-  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (e >= (int64_t)n * D) return;
-  const int j = (int)(e / D), d = (int)(e - (int64_t)j * D);
+// out[j*ldo + d] (+)= sum_b in[b*sb + j*sj + d]: batch sums of position tables (the
+// tied-logits bias (n, K+1), the position embedding).  Block = 32 columns x 8 batch parts:
+// part q sums its images in order, then the 8 partials are added in part order (a fixed
+// order, bitwise reproducible); one thread per column summing all B serially left the
+// launch at 50-200 blocks and 15 us.
+constexpr int BCS_COLS = 32, BCS_PARTS = 8;
+__global__ __launch_bounds__(256) void batch_colsum8_kernel(const float* __restrict__ in, int B,
+                                                            int64_t sb, int n, int64_t sj, int D,
+                                                            float* __restrict__ out, int64_t ldo,
+                                                            int accumulate) {
+  __shared__ float part[BCS_PARTS][BCS_COLS];
+  const int c = threadIdx.x % BCS_COLS, q = threadIdx.x / BCS_COLS;
+  const int64_t e = (int64_t)blockIdx.x * BCS_COLS + c;
+  const bool ok = e < (int64_t)n * D;
+  const int j = ok ? (int)(e / D) : 0, d = ok ? (int)(e - (int64_t)j * D) : 0;
+  const int per = (B + BCS_PARTS - 1) / BCS_PARTS;
+  const int b0 = q * per, b1 = min(B, b0 + per);
   const float* p = in + j * sj + d;
   float s = 0.f;
 #pragma unroll 8
-  for (int b = 0; b < B; ++b) s += p[b * sb];
+  for (int b = b0; b < b1; ++b) s += p[b * sb];
+  part[q][c] = s;
+  __syncthreads();
+  if (q != 0 || !ok) return;
+  float t = part[0][c];
+#pragma unroll
+  for (int k = 1; k < BCS_PARTS; ++k) t += part[k][c];
   float* o = out + j * ldo + d;
-  *o = accumulate ? *o + s : s;
+  *o = accumulate ? *o + t : t;
 }
+
 
 __global__ void scale_by_kernel(const float4* __restrict__ x, int64_t n4, const float* __restrict__ s,
                                 float4* __restrict__ y) {
@@ -749,7 +765,7 @@ extern "C" int tvq_embed_assemble_bwd(const float* dout, int64_t B, int64_t n, i
                        dim3(256), 0, st, dout, (int)B, (int)n, dcls, a1, a2);
   if (dpos) {
     const int64_t Dt = D1 + D2;
-    hipLaunchKernelGGL(batch_colsum_kernel, dim3((unsigned)((n * Dt + 255) / 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(batch_colsum8_kernel, dim3((unsigned)((n * Dt + BCS_COLS - 1) / BCS_COLS)), dim3(256), 0, st,
                        dout + Dt, (int)B, (n + 1) * Dt, (int)n, Dt, (int)Dt, dpos, Dt,
                        (int)accumulate);
   }
@@ -795,8 +811,8 @@ extern "C" int tvq_batch_colsum(const float* in, int64_t B, int64_t sb, int64_t 
                                 int64_t D, float* out, int64_t ldo, int64_t accumulate,
                                 tvq_stream_t stream) {
   TVQ_CHECK_ARG(in && out && B > 0 && n > 0 && D > 0, "tvq_batch_colsum: bad arguments");
-  hipLaunchKernelGGL(batch_colsum_kernel, dim3((unsigned)((n * D + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, in, (int)B, sb, (int)n, sj, (int)D, out, ldo,
+  hipLaunchKernelGGL(batch_colsum8_kernel, dim3((unsigned)((n * D + BCS_COLS - 1) / BCS_COLS)),
+                     dim3(256), 0, (hipStream_t)stream, in, (int)B, sb, (int)n, sj, (int)D, out, ldo,
                      (int)accumulate);
   return launch_status("tvq_batch_colsum");
 }
