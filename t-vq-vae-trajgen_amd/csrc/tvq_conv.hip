@@ -2704,6 +2704,16 @@ static int wd32_splits(const ConvGeom& g, int kcols, int max_s, int* pps) {
   return (g.Mpos + p - 1) / p;
 }
 
+// TVQ_T32_SMALLC=1: the 16 / 48-channel convs into 128 go to the 32x32-MFMA tile with a
+// 16 / 32-wide K stage instead of the halo tile (off by default until measured)
+static bool t32_smallc() {
+  static const int on = [] {
+    const char* v = getenv("TVQ_T32_SMALLC");
+    return v ? atoi(v) : 0;
+  }();
+  return on != 0;
+}
+
 // staged GEMM; `slab` (nullable) enables split-K with splits*N*Mpos floats of partials
 template <int MODE, int KH, int KW, int SW, bool REPL>
 static void launch_gemm(const float* in, const float* wt, float* out, const ConvGeom& g,
@@ -2716,7 +2726,11 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
                         (int64_t)g.B * g.C * g.Hin * g.Win < (1ll << 29) &&
                         (int64_t)KH * KW * g.C * g.N < (1ll << 29);
     const int64_t mt = (g.Mpos + 95) / 96;
-    const bool wide128 = t32_ok && g.C % g_t32_bk == 0 && g.N % 128 == 0 && mt * (g.N / 128) >= 192;
+    // K stage: the configured BK where the channels divide it, else 32 / 16 (C = 16 / 48:
+    // the HF band's 16 -> 128 convs, when t32_smallc() routes them here)
+    const int bk = g.C % g_t32_bk == 0 ? g_t32_bk : (g.C % 32 == 0 ? 32 : 16);
+    const bool wide128 = t32_ok && (g.C % g_t32_bk == 0 || t32_smallc()) && g.N % 128 == 0 &&
+                         mt * (g.N / 128) >= 192;
     const bool wide64 = !wide128 && t32_ok && g_t32_n64 && g.C % 64 == 0 && g.N % 64 == 0 &&
                         mt >= 32;
     if (wide128 || wide64) {
@@ -2740,12 +2754,12 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
       if (wide64) {
         TVQ_T32(64, 6, 64);
       } else if (g_t32_nw == 12) {
-        if (g_t32_bk == 64) TVQ_T32(64, 12, 128);
-        else if (g_t32_bk == 16) TVQ_T32(16, 12, 128);
+        if (bk == 64) TVQ_T32(64, 12, 128);
+        else if (bk == 16) TVQ_T32(16, 12, 128);
         else TVQ_T32(32, 12, 128);
       } else {
-        if (g_t32_bk == 64) TVQ_T32(64, 4, 128);
-        else if (g_t32_bk == 16) TVQ_T32(16, 4, 128);
+        if (bk == 64) TVQ_T32(64, 4, 128);
+        else if (bk == 16) TVQ_T32(16, 4, 128);
         else TVQ_T32(32, 4, 128);
       }
 #undef TVQ_T32
@@ -2806,9 +2820,12 @@ static int g_conv_halo = 3;
 // for 1x1 convs, for C >= 32, and for the stride-2 transposed gathers.  A register-
 // resident-weight variant (whole reduction row per wave in VGPRs) was 1.5-4x slower
 // than both (1 wave/SIMD, uncoalesced weight loads) and was dropped.
-static bool halo_preferred(int mode, int C, int KK, int SW) {
+static bool halo_preferred(int mode, int C, int KK, int SW, int N, int64_t Mpos) {
   if (g_conv_halo & 4) return true;
   if (KK == 1 || C >= 32) return false;
+  // 16 / 48 channels into >= 128 on a full grid: the 32x32-MFMA tile with a 16-wide K stage
+  if (t32_smallc() && g_conv_t32 && C % 16 == 0 && N % 128 == 0 && (Mpos + 95) / 96 * (N / 128) >= 192)
+    return false;
   if (mode == GATHER_T && SW == 2) return false;
   return true;
 }
@@ -2846,7 +2863,7 @@ static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g
   HaloPlan pl;
   const int oh = MODE == GATHER_F ? g.oph : KH - 1 - g.oph;
   const int ow = MODE == GATHER_F ? g.opw : KW - 1 - g.opw;
-  if ((g_conv_halo & 1) && halo_preferred(MODE, g.C, KH * KW, SW) && halo_plan(MODE, g.B, g.C, g.Hin, g.Win, g.N, g.Hout, g.Wo, KH, KW, SW, oh,
+  if ((g_conv_halo & 1) && halo_preferred(MODE, g.C, KH * KW, SW, g.N, g.Mpos) && halo_plan(MODE, g.B, g.C, g.Hin, g.Win, g.N, g.Hout, g.Wo, KH, KW, SW, oh,
                                ow, g.wsn, g.wsc, &pl)) {
     launch_halo<MODE, KH, KW, SW, REPL>(in, wt, out, pl, g.B, e, st);
     return;
