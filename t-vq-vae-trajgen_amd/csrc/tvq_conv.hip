@@ -2704,12 +2704,13 @@ static int wd32_splits(const ConvGeom& g, int kcols, int max_s, int* pps) {
   return (g.Mpos + p - 1) / p;
 }
 
-// TVQ_T32_SMALLC=1: the 16 / 48-channel convs into 128 go to the 32x32-MFMA tile with a
-// 16 / 32-wide K stage instead of the halo tile (off by default until measured)
+// the 16 / 48-channel convs into 128 on the 32x32-MFMA tile with a 16 / 32-wide K stage
+// instead of the halo tile: HF 16 -> 128 3x3 forward and the 128 -> 16 conv's data gradient
+// 32.2 / 30.9 -> 22.1 / 20.3 us, step -30 us (tools/gpu_t32s_ab.sh); TVQ_T32_SMALLC=0 off
 static bool t32_smallc() {
   static const int on = [] {
     const char* v = getenv("TVQ_T32_SMALLC");
-    return v ? atoi(v) : 0;
+    return v ? atoi(v) : 1;
   }();
   return on != 0;
 }

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 500 python -u -m pytest tests/test_ops_gpu.py tests/test_stage1.py -x -q -m gpu -k "conv or stage1" \
+TVQ_T32_SMALLC=1 timeout -k 10 500 python -u -m pytest tests/test_ops_gpu.py tests/test_stage1.py -x -q -m gpu -k "conv or stage1" \
   --timeout 120 --timeout-method thread > gpurun_out/ab_tests.log 2>&1 || { tail -30 gpurun_out/ab_tests.log; exit 1; }
 tail -1 gpurun_out/ab_tests.log
 for v in 1 0; do
