@@ -43,6 +43,13 @@ int tvq_counter_pool(int64_t device, int32_t* zeroed, int64_t n);
  * process lifetime (a graph replays with its capture-time slots), taken from the top
  * half of the pool, which eager launches never use. */
 int tvq_counter_capture(int64_t begin);
+/* Dispatch trace (tests / diagnosis; no reference counterpart).  tvq_plan_trace(1) clears
+ * the log and starts recording one line per launch decision of the host-side plans (conv
+ * kernel variant and its K stage / split plan, fused ResBlock kernels, VQ assignment row
+ * groups); tvq_plan_trace(0) stops.  tvq_plan_read copies the newline-separated log into
+ * buf (NUL-terminated, at most cap-1 bytes) and returns its full length. */
+int tvq_plan_trace(int64_t on);
+int64_t tvq_plan_read(char* buf, int64_t cap);
 
 /* ---------------------------------------------------------------- VQ codebook
  * Replaces EuclideanCodebook.forward (timevqvae/models/vq.py:197-251) and the

@@ -143,6 +143,12 @@ class Ctx:
         self.dropout_p = dropout_p
         self.gen = dropout_gen
         self.updates = {}
+        # tests: code indices to use instead of the argmax (prefix -> (rows,) int64), e.g.
+        # the HIP path's, so an fp32 near-tie that resolved the other way (z differs from
+        # this restatement's by reassociation) does not decouple everything downstream;
+        # vq_forward records each forced row's argmax and fp64 top-2 gap in `ind_check`
+        self.forced_ind = {}
+        self.ind_check = {}
 
 
 def _bn(ctx, sd, p, x):
@@ -265,6 +271,16 @@ def vq_forward(ctx, sd, prefix, x, decay=0.8, eps=1e-5, svq_temp=None):
     flat = x.reshape(-1, x.shape[-1])
     dist = vq_dist(flat, embed)
     ind = vq_sample(dist, svq_temp)
+    forced = ctx.forced_ind.get(prefix)
+    if forced is not None:
+        forced = forced.reshape(-1).to(ind.dtype)
+        with torch.no_grad():
+            d64 = vq_dist(flat.detach().double(), embed.detach().double())
+            top2 = torch.topk(d64, 2, dim=-1).values
+        ctx.ind_check[prefix] = (ind.clone(), forced, (top2[:, 0] - top2[:, 1]),
+                                 flat.detach().double().pow(2).sum(1) +
+                                 embed.detach().double().pow(2).sum(1).max())
+        ind = forced
     onehot = F.one_hot(ind, K).to(x.dtype)
     q = F.embedding(ind, embed).reshape(x.shape)
     ind = ind.reshape(x.shape[:-1])

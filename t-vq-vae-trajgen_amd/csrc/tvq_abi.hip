@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <string>
 
 #include "tvq_common.h"
 
@@ -15,6 +16,22 @@ void set_error(const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
+}
+
+bool g_plan_trace = false;
+static std::mutex g_plan_mu;
+static std::string g_plan_log;
+void plan_note_impl(const char* fmt, ...) {
+  char line[160];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(line, sizeof(line), fmt, ap);
+  va_end(ap);
+  std::lock_guard<std::mutex> lock(g_plan_mu);
+  if (g_plan_log.size() < (1u << 20)) {
+    g_plan_log += line;
+    g_plan_log += '\n';
+  }
 }
 
 namespace {
@@ -85,6 +102,24 @@ extern "C" int tvq_counter_pool(int64_t device, int32_t* zeroed, int64_t n) {
   tvq::g_pools[device].cur = 0;
   tvq::g_pools[device].lo = n;
   return TVQ_OK;
+}
+
+extern "C" int tvq_plan_trace(int64_t on) {
+  std::lock_guard<std::mutex> lock(tvq::g_plan_mu);
+  tvq::g_plan_log.clear();
+  tvq::g_plan_trace = on != 0;
+  return TVQ_OK;
+}
+
+extern "C" int64_t tvq_plan_read(char* buf, int64_t cap) {
+  std::lock_guard<std::mutex> lock(tvq::g_plan_mu);
+  const int64_t n = (int64_t)tvq::g_plan_log.size();
+  if (buf && cap > 0) {
+    const int64_t m = n < cap - 1 ? n : cap - 1;
+    memcpy(buf, tvq::g_plan_log.data(), (size_t)m);
+    buf[m] = 0;
+  }
+  return n;
 }
 
 extern "C" const char* tvq_last_error(void) { return tvq::g_err; }

@@ -29,6 +29,17 @@ inline int launch_status(const char* what) {
   return TVQ_OK;
 }
 
+// Dispatch trace (tvq_plan_trace / tvq_plan_read): while on, every host-side plan records
+// the kernel variant it launched ("conv_t32 bk16 nw12 tn128", "conv_wgrad_s2 S=256
+// spr=2", ...), so a test can confirm which kernel a shape took.  Off by default: one
+// branch per launch.
+extern bool g_plan_trace;
+void plan_note_impl(const char* fmt, ...);
+#define TVQ_PLAN(...)                                   \
+  do {                                                  \
+    if (::tvq::g_plan_trace) ::tvq::plan_note_impl(__VA_ARGS__); \
+  } while (0)
+
 #define TVQ_CHECK_ARG(cond, ...)          \
   do {                                    \
     if (!(cond)) {                        \

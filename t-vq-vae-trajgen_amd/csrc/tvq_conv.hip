@@ -1421,6 +1421,7 @@ static void launch_s2(int kind, const float* in, const float* wt, float* out, co
                       const Epi& e, hipStream_t st) {
   const dim3 grid((unsigned)(g.B * ((g.Wo + S2_SEG - 1) / S2_SEG)));
   const int cs = (g.C + 3) / 4;
+  TVQ_PLAN("conv_s2%s cs%d hout%d", kind == 1 ? "f" : "t", 4 * cs, g.Hout);
 #define S2F(CSV) hipLaunchKernelGGL((conv_s2f_kernel<REPL, CSV>), grid, dim3(256), 0, st, in, wt, out, g, e)
 #define S2T(CSV, HOV) hipLaunchKernelGGL((conv_s2t_kernel<CSV, HOV>), grid, dim3(256), 0, st, in, wt, out, g, e)
   if (kind == 1) {
@@ -1444,6 +1445,7 @@ static void launch_s2_fold(const float* in, const float* wt, float* dx, const Co
   const dim3 grid((unsigned)(g.B * ((g.Wo + S2_SEG - 1) / S2_SEG)));
   const Epi e = {nullptr, nullptr, 0.f, 1.f, nullptr, 0};
   const int cs = (g.C + 3) / 4;
+  TVQ_PLAN("conv_s2t_fold cs%d", 4 * cs);
 #define S2T(CSV) hipLaunchKernelGGL((conv_s2t_kernel<CSV, 5, true>), grid, dim3(256), 0, st, in, wt, dx, g, e)
   if (cs == 1) S2T(4); else if (cs == 2) S2T(8); else if (cs == 3) S2T(12); else S2T(16);
 #undef S2T
@@ -1604,6 +1606,7 @@ static int ws2_launch(const float* G, const float* X, float* slab, int B, int C,
   int S;
   ws2_plan(B, Wo, &S, &w.spr);
   const int cs = (C + 3) / 4;
+  TVQ_PLAN("conv_wgrad_s2 cs%d S=%d spr=%d", 4 * cs, S, w.spr);
 #define W2L(R, CSV) hipLaunchKernelGGL((conv_wgrad_s2_kernel<R, CSV>), dim3(S), dim3(W2_T), 0, st, G, X, slab, w)
   if (repl) {
     if (cs == 1) W2L(true, 4); else if (cs == 2) W2L(true, 8); else if (cs == 3) W2L(true, 12); else W2L(true, 16);
@@ -2752,6 +2755,8 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
   hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, BKV, NWV, TNV>),             \
                      dim3((unsigned)mt, g.N / TNV), dim3(64 * NWV), t32_lds(BKV, TNV), st, in, \
                      wt, out, g, e)
+      TVQ_PLAN("conv_t32 bk%d nw%d tn%d", wide64 ? 64 : bk, wide64 ? 6 : g_t32_nw,
+               wide64 ? 64 : 128);
       if (wide64) {
         TVQ_T32(64, 6, 64);
       } else if (g_t32_nw == 12) {
@@ -2766,10 +2771,14 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
 #undef TVQ_T32
       return;
     }
-    if (launch_d32<MODE, KH, KW, SW, REPL>(in, wt, out, g, e, st)) return;
+    if (launch_d32<MODE, KH, KW, SW, REPL>(in, wt, out, g, e, st)) {
+      TVQ_PLAN("conv_d32");
+      return;
+    }
     int sps;
     const int splits = slab ? tap_splits(g, KH * KW, &sps) : 1;
     if (!slab) sps = KH * KW * ((g.C + 31) / 16);  // >= all K-steps
+    TVQ_PLAN("conv_tap splits%d", splits);
     if (splits > 1) {
       const int64_t n_out = (int64_t)g.Mpos * g.N;
       const Epi raw = {nullptr, nullptr, 0.f, 1.f, nullptr, 0};
@@ -2796,6 +2805,7 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
     return;
   }
   // small channel counts: flat (c, kh, kw) K order keeps the K-steps full
+  TVQ_PLAN("conv_gemm n%d", g.N);
   if (g.N <= 16) {
     dim3 grid((g.Mpos + 255) / 256, (g.N + 15) / 16);
     hipLaunchKernelGGL((conv_gemm_kernel<MODE, KH, KW, SW, REPL, 16, 256, 1, 4>), grid, dim3(256),
@@ -2851,6 +2861,7 @@ static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g
     const int64_t th = (int64_t)g.B * g.Hout * ((g.Wo + 1) / 2);
     // outputs per thread rounded up to 4 (every channel's sum in the same order)
     const dim3 grid((unsigned)((th + 255) / 256));
+    TVQ_PLAN("conv_small n%d", g.N);
     if (g.N <= 4)
       hipLaunchKernelGGL((conv_small_kernel<MODE, KH, KW, SW, REPL, 4>), grid, dim3(256), 0, st, in, wt, out, g, e);
     else if (g.N <= 8)
@@ -2866,6 +2877,7 @@ static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g
   const int ow = MODE == GATHER_F ? g.opw : KW - 1 - g.opw;
   if ((g_conv_halo & 1) && halo_preferred(MODE, g.C, KH * KW, SW, g.N, g.Mpos) && halo_plan(MODE, g.B, g.C, g.Hin, g.Win, g.N, g.Hout, g.Wo, KH, KW, SW, oh,
                                ow, g.wsn, g.wsc, &pl)) {
+    TVQ_PLAN("conv_halo");
     launch_halo<MODE, KH, KW, SW, REPL>(in, wt, out, pl, g.B, e, st);
     return;
   }
@@ -3299,6 +3311,7 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
     const int kt = (g.Kred + 127) / 128;
     t.ntiles = (int)((Co + 127) / 128);
     const dim3 grid(xcd_grid(S, kt * t.ntiles));
+    TVQ_PLAN("conv_wgrad_t32 S=%d", S);
     if (KH == 3)
       hipLaunchKernelGGL((conv_wgrad_t32_kernel<3, 3>), grid, dim3(WT_T), 0, st, dy, x, workspace, t,
                          kt);
@@ -3319,6 +3332,7 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
       attr = true;
     }
     const size_t lds = w8_lds<8, 8>(PS);
+    TVQ_PLAN("conv_wgrad_w8 S=%d", S);
     hipLaunchKernelGGL((conv_wgrad_w8_kernel<8, 8>), grid, dim3(256), lds, st, dy, x, workspace,
                        (int)B, (int)Ci, (int)Co, kcols, PS);
     wgrad_finish(workspace, S, Co, kcols, dw, db, (int)accumulate, st);
@@ -3341,6 +3355,7 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
     const int S = wd32_splits(g, kcols, halo && pl.S > gs ? pl.S : gs, &pps);
     const int ntiles = (int)((Co + 31) / 32), ctiles = (kcols + 31) / 32;
     const unsigned grid = (unsigned)(S * ntiles * ctiles);
+    TVQ_PLAN("conv_wgrad_d32 S=%d", S);
 #define M_(a, b_, c, d)                                                                        \
   hipLaunchKernelGGL((conv_wgrad_d32_kernel<a, b_, c, d>), dim3(grid), dim3(256), 0, st, dy, x, \
                      workspace, g, pps, kcols, ntiles, ctiles);
@@ -3350,6 +3365,7 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
     return launch_status("tvq_conv2d_wgrad(direct)");
   }
   if (halo) {
+    TVQ_PLAN("conv_wgrad_halo S=%d", pl.S);
 #define M_(a, b_, c, d) launch_wgrad_halo<a, b_, c, d>(dy, x, workspace, pl, st);
     TVQ_DISPATCH_KIND(kind, replicate, M_)
 #undef M_
@@ -3358,6 +3374,7 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
   }
   int splits, pps;
   wgrad_ws(Co, g.Kred, g.Mpos, &splits, &pps);
+  TVQ_PLAN("conv_wgrad split=%d", splits);
 #define M_(a, b_, c, d) launch_wgrad<a, b_, c, d>(dy, x, workspace, splits, pps, g, kcols, st);
   TVQ_DISPATCH_KIND(kind, replicate, M_)
 #undef M_
@@ -3387,6 +3404,7 @@ extern "C" int tvq_convT2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t 
   if ((g_conv_halo & 2) && whalo_plan((int)B, (int)Co, (int)H, (int)Wo, (int)Ci, (int)H, (int)Wi,
                                       (int)KH, (int)KW, (int)SW, PH_OF(KH), PW_OF(KW), g.Kred,
                                       &pl)) {
+    TVQ_PLAN("conv_wgrad_halo S=%d", pl.S);
 #define M_(a, b_, c, d) launch_wgrad_halo<a, b_, c, false>(x, dy, workspace, pl, st);
     TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
@@ -3395,6 +3413,7 @@ extern "C" int tvq_convT2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t 
   }
   int splits, pps;
   wgrad_ws(Ci, g.Kred, g.Mpos, &splits, &pps);
+  TVQ_PLAN("conv_wgrad split=%d", splits);
 #define M_(a, b_, c, d) launch_wgrad<a, b_, c, false>(x, dy, workspace, splits, pps, g, g.Kred, st);
   TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_

@@ -806,6 +806,8 @@ static void rb_launch(int kind, const RBArgs& a, hipStream_t st) {
   }
   const dim3 grid(a.B), block(RB_T);
   const size_t lds = rb_lds<R>(kind);
+  static const char* const names[5] = {"rb_fwd1", "rb_fwd2", "rb_eval", "rb_bwd2", "rb_bwd1"};
+  TVQ_PLAN("%s C%d W%d B%d", names[kind < 4 ? kind : 4], R::C, R::W, a.B);
   switch (kind) {
     case 0: hipLaunchKernelGGL(rb_fwd1_kernel<R>, grid, block, lds, st, a); break;
     case 1: hipLaunchKernelGGL(rb_fwd2_kernel<R>, grid, block, lds, st, a); break;

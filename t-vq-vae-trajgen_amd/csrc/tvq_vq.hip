@@ -375,6 +375,7 @@ extern "C" int tvq_vq_assign_rows(const float* x, int64_t B, int64_t N, int64_t 
   const size_t lds_tail = (size_t)(16 * rg * 5) * 4 + 4 * 2 * VQ_RG_MAX + 32;
   hipStream_t st = (hipStream_t)stream;
   const Svq sv = {temp, gumbel, seed_ptr, offset};
+  TVQ_PLAN("vq_assign D%lld rg%d nb%lld%s", (long long)D, rg, (long long)nb, temp > 0.f ? " svq" : "");
 #define TVQ_ASSIGN_RG(DD, ST, RGV)                                                           \
   if (rg == RGV)                                                                             \
     hipLaunchKernelGGL((vq_assign_kernel<DD, ST, RGV>), dim3(nb), dim3(128 * RGV), lds, st, x,  \

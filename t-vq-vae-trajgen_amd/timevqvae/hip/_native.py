@@ -33,6 +33,8 @@ def sig(name, *argtypes, restype=I32):
 
 sig("tvq_counter_pool", I64, P, I64)
 sig("tvq_counter_capture", I64)
+sig("tvq_plan_trace", I64)
+sig("tvq_plan_read", ctypes.c_char_p, I64, restype=I64)
 # --- VQ codebook -----------------------------------------------------------
 sig("tvq_vq_sqnorm", P, I64, I64, P, P)
 sig("tvq_vq_assign_nblocks", I64, restype=I64)
@@ -240,6 +242,28 @@ def call(name, *args):
 
 def value(name, *args):
     return getattr(lib(), name)(*args)
+
+
+class plan_trace:
+    """Record the kernel variants the library's host-side plans launch (tvq_plan_trace);
+    `.lines` holds them after the block (tests confirm which kernel a shape took)."""
+
+    def __enter__(self):
+        lib().tvq_plan_trace(1)
+        self.lines = []
+        return self
+
+    def __exit__(self, *exc):
+        h = lib()
+        n = h.tvq_plan_read(None, 0)
+        buf = ctypes.create_string_buffer(int(n) + 1)
+        h.tvq_plan_read(buf, n + 1)
+        h.tvq_plan_trace(0)
+        self.lines = [s for s in buf.value.decode().split("\n") if s]
+        return False
+
+    def has(self, prefix):
+        return [s for s in self.lines if s.startswith(prefix)]
 
 
 def grad_sink(p):
