@@ -134,7 +134,9 @@ class JointTrainer:
         packs = self.packs.scope() if self.packs is not None else contextlib.nullcontext()
         with packs, streams.concurrent():
             with (deferred_codebook_updates() if defer else contextlib.nullcontext([])) as pend:
-                hist1 = self.s1.forward_backward(batch, 0) if only != "stage2" else None
+                # diagnosis only (TVQ_BENCH_BANDS=LF|HF): one stage1 band alone
+                bands = tuple(os.environ.get("TVQ_BENCH_BANDS", "HF,LF").split(","))
+                hist1 = self.s1.forward_backward(batch, 0, bands) if only != "stage2" else None
             if only != "stage1":
                 out2 = self.s2.training_step(batch, 0)
                 # Linear weight gradients: one grouped launch per stream; the conv and norm

@@ -43,6 +43,15 @@ int tvq_counter_pool(int64_t device, int32_t* zeroed, int64_t n);
  * process lifetime (a graph replays with its capture-time slots), taken from the top
  * half of the pool, which eager launches never use. */
 int tvq_counter_capture(int64_t begin);
+/* Step glue (no reference counterpart; replaces the PyTorch elementwise launches a step
+ * graph held): p[0..n) = value (FusedAdamW.zero_grad of the flat gradient buffer);
+ * p[0] += value (the dropout seed advance of hip/rng.py); out = ((a + b) + c) + d and
+ * out_ab = a + b elementwise over n floats, c / d / out / out_ab nullable (the logged loss
+ * sums of stage1.py:170-198, maskgit.py:155-192). */
+int tvq_fill(float* p, int64_t n, float value, tvq_stream_t stream);
+int tvq_add_i64(int64_t* p, int64_t value, tvq_stream_t stream);
+int tvq_sum4(const float* a, const float* b, const float* c, const float* d, float* out,
+             float* out_ab, int64_t n, tvq_stream_t stream);
 /* Dispatch trace (tests / diagnosis; no reference counterpart).  tvq_plan_trace(1) clears
  * the log and starts recording one line per launch decision of the host-side plans (conv
  * kernel variant and its K stage / split plan, fused ResBlock kernels, VQ assignment row

@@ -102,6 +102,11 @@ __device__ __forceinline__ T ld_wt(const T* p) {
   return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Returns the same value in every thread of the block.
+// REQUIREMENT (TVQ_TICKET 0/1): every partial a last block reads must have been stored with
+// st_wt by its producer (a plain store may sit in the producing XCD's L2, and the reader's
+// ld_wt on another XCD would see stale data with no error); only TVQ_TICKET=2 orders plain
+// stores by itself.  Build with -DTVQ_TICKET=2 (EXTRA=-DTVQ_TICKET=2) to check a suspect
+// producer: the results must be bitwise equal to the default build's.
 __device__ __forceinline__ bool last_block(int* counter, int total) {
   __shared__ int s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's st_wt stores are done

@@ -216,7 +216,11 @@ void reduce_rows_batch(const RrJob* jobs, int n, hipStream_t st) {
 
 // ---------------------------------------------------------------- group-by
 constexpr int GB_CHUNK = 256;
-constexpr int SEG_CH = 32;  // rows per segmented-sum chunk (skewed groups split over waves)
+// rows per segmented-sum chunk: one 4-wave block (32 rows per wave); every value has at least
+// one chunk (an empty value's chunk writes its zero row), skewed values many
+constexpr int SEG_CH = 128;
+__host__ __device__ __forceinline__ int seg_chunks_of(int n) { return n > 0 ? (n + SEG_CH - 1) / SEG_CH : 1; }
+static int64_t seg_max_chunks(int64_t M, int64_t V) { return (M + SEG_CH - 1) / SEG_CH + V; }
 
 template <typename IT>
 __global__ __launch_bounds__(256) void gb_hist_kernel(const IT* __restrict__ idx, int64_t M, int V,
@@ -270,7 +274,8 @@ __device__ __forceinline__ void block_excl_scan2(int& a, int& b, int& tot_a, int
 __global__ __launch_bounds__(1024) void gb_scan_kernel(const int* __restrict__ hist, int chunks,
                                                        int V, int* __restrict__ chunk_off,
                                                        int* __restrict__ offsets,
-                                                       int* __restrict__ seg_start) {
+                                                       int* __restrict__ seg_start,
+                                                       int* __restrict__ chunk_v) {
   extern __shared__ int tot[];  // [V]
   const int per = (V + 1023) / 1024;
   const int v0 = threadIdx.x * per;
@@ -283,7 +288,7 @@ __global__ __launch_bounds__(1024) void gb_scan_kernel(const int* __restrict__ h
     for (int c = 0; c < chunks; ++c) s += hist[(int64_t)c * V + v];
     tot[v] = s;
     t_loc += s;
-    s_loc += (s + SEG_CH - 1) / SEG_CH;
+    s_loc += seg_chunks_of(s);
   }
   int all_t, all_s;
   block_excl_scan2(t_loc, s_loc, all_t, all_s);
@@ -301,11 +306,88 @@ __global__ __launch_bounds__(1024) void gb_scan_kernel(const int* __restrict__ h
       s += h;
     }
     run += tot[v];
-    segs += (tot[v] + SEG_CH - 1) / SEG_CH;
+    const int nc = seg_chunks_of(tot[v]);
+    if (chunk_v)
+      for (int i = 0; i < nc; ++i) chunk_v[segs + i] = v;
+    segs += nc;
   }
   if (threadIdx.x == 0) {
     offsets[V] = all_t;
     if (seg_start) seg_start[V] = all_s;
+  }
+}
+
+// The whole stable counting sort in one 1024-thread block (M <= GB1_MAX_M, V <= 1024: every
+// group-by of the training step).  The indices go to LDS as 16-bit values; wave w owns a
+// contiguous token range and counts it into its own histogram row (integer LDS atomics:
+// exact); thread v then turns the 16 rows of value v into the waves' running offsets
+// (exclusive block scan of the per-value totals and of the chunk counts), and each wave
+// places its tokens in token order: the lanes holding the same value are found by AND-ing
+// the ballots of the value's bits, a lane's rank among them is a popcount, and the highest
+// such lane advances the wave's offset.  Same offsets / perm as the 3-launch path.
+constexpr int GB1_MAX_M = 32768, GB1_MAX_V = 1024, GB1_T = 1024;
+template <typename IT>
+__global__ __launch_bounds__(GB1_T) void gb_sort1_kernel(const IT* __restrict__ idx, int M, int V,
+                                                         int* __restrict__ offsets,
+                                                         int* __restrict__ perm,
+                                                         int* __restrict__ seg_start,
+                                                         int* __restrict__ chunk_v) {
+  extern __shared__ int gb1_smem[];
+  int* hist = gb1_smem;  // [16][V]: counts, then each wave's running offsets
+  unsigned short* vals = reinterpret_cast<unsigned short*>(gb1_smem + 16 * V);  // [M]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int per = ((M + 15) / 16 + 63) / 64 * 64;  // tokens per wave (multiple of 64)
+  for (int i = tid; i < 16 * V; i += GB1_T) hist[i] = 0;
+  for (int m = tid; m < M; m += GB1_T) {
+    const int v = (int)idx[m];
+    vals[m] = (unsigned short)(v >= 0 && v < V ? v : 0xFFFF);
+  }
+  __syncthreads();
+  const int m0 = w * per, m1 = min(M, m0 + per);
+  for (int m = m0 + lane; m < m1; m += 64) {
+    const int v = vals[m];
+    if (v != 0xFFFF) atomicAdd(&hist[w * V + v], 1);
+  }
+  __syncthreads();
+  int tot = 0;
+  if (tid < V)
+    for (int k = 0; k < 16; ++k) tot += hist[k * V + tid];
+  int nc = tid < V ? seg_chunks_of(tot) : 0;
+  int ex_t = tot, ex_c = nc, all_t, all_s;
+  block_excl_scan2(ex_t, ex_c, all_t, all_s);
+  if (tid < V) {
+    offsets[tid] = ex_t;
+    seg_start[tid] = ex_c;
+    for (int i = 0; i < nc; ++i) chunk_v[ex_c + i] = tid;
+    int run = ex_t;
+    for (int k = 0; k < 16; ++k) {
+      const int c = hist[k * V + tid];
+      hist[k * V + tid] = run;
+      run += c;
+    }
+  }
+  if (tid == 0) {
+    offsets[V] = all_t;
+    seg_start[V] = all_s;
+  }
+  __syncthreads();
+  const int nbits = V > 1 ? 32 - __clz(V - 1) : 0;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int g0 = m0; g0 < m1; g0 += 64) {
+    const int m = g0 + lane;
+    const int v = m < m1 ? (int)vals[m] : 0xFFFF;
+    const bool ok = v != 0xFFFF;
+    unsigned long long eq = __ballot(ok);
+    for (int b = 0; b < nbits; ++b) {
+      const bool bit = (v >> b) & 1;
+      const unsigned long long bal = __ballot(bit);
+      eq &= bit ? bal : ~bal;
+    }
+    if (ok) {
+      const int base = hist[w * V + v];
+      perm[base + __popcll(eq & below)] = m;
+      if ((eq >> lane) == 1ull) hist[w * V + v] = base + __popcll(eq);
+    }
   }
 }
 
@@ -330,7 +412,8 @@ __global__ __launch_bounds__(256) void gb_place_kernel(const IT* __restrict__ id
 
 int64_t group_by_scratch_ints(int64_t M, int64_t V) {
   const int64_t chunks = (M + GB_CHUNK - 1) / GB_CHUNK;
-  return 2 * chunks * V + (V + 1);  // hist + chunk_off + seg_start
+  // hist + chunk_off (3-launch path) | seg_start | chunk -> value map
+  return 2 * chunks * V + (V + 1) + seg_max_chunks(M, V);
 }
 
 template <typename IT>
@@ -340,10 +423,26 @@ static void group_by_t(const IT* idx, int64_t M, int64_t V, int* offsets, int* p
   int* hist = scratch;
   int* coff = scratch + (int64_t)chunks * V;
   int* seg_start = coff + (int64_t)chunks * V;
+  int* chunk_v = seg_start + (V + 1);
+  if (M <= GB1_MAX_M && V <= GB1_MAX_V) {
+    const size_t lds = (size_t)16 * V * 4 + (size_t)M * 2;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gb_sort1_kernel<IT>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                16 * GB1_MAX_V * 4 + GB1_MAX_M * 2);
+      attr = true;
+    }
+    TVQ_PLAN("group_by sort1 M%lld V%lld", (long long)M, (long long)V);
+    hipLaunchKernelGGL(gb_sort1_kernel<IT>, dim3(1), dim3(GB1_T), lds, st, idx, (int)M, (int)V,
+                       offsets, perm, seg_start, chunk_v);
+    return;
+  }
+  TVQ_PLAN("group_by 3-launch M%lld V%lld", (long long)M, (long long)V);
   hipLaunchKernelGGL(gb_hist_kernel<IT>, dim3(chunks), dim3(256), V * sizeof(int), st, idx, M,
                      (int)V, hist);
   hipLaunchKernelGGL(gb_scan_kernel, dim3(1), dim3(1024), V * sizeof(int), st, hist, chunks, (int)V,
-                     coff, offsets, seg_start);
+                     coff, offsets, seg_start, chunk_v);
   hipLaunchKernelGGL(gb_place_kernel<IT>, dim3(chunks), dim3(256), 0, st, idx, M, (int)V, coff,
                      perm);
 }
@@ -357,46 +456,30 @@ void group_by_i64(const int64_t* idx, int64_t M, int64_t V, int* offsets, int* p
   group_by_t<int64_t>(idx, M, V, offsets, perm, scratch, st);
 }
 
-// Pass 1: one wave per chunk of <= SEG_CH consecutive sorted rows of ONE value:
-// part[chunk, :] = sum of those rows (fixed order).  Pass 2: one wave per value sums its
-// chunk partials in chunk order.  Skewed groups (the MaskGIT mask token takes most
-// positions) are spread over many waves; results stay bitwise reproducible.
-__device__ __forceinline__ int value_of_chunk(const int* __restrict__ seg_start, int V, int c) {
-  int lo = 0, hi = V - 1;  // largest v with seg_start[v] <= c
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (seg_start[mid] <= c) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
-
-// The chunk's row indices are read once (lane r holds perm[r0 + r]) and broadcast by
-// shuffles, and 8 rows' loads are issued before any is added (in row order), so a chunk
-// costs ~4 memory round trips instead of 2 per row (perm -> row): 40 -> few us per call.
+// Segmented row sums in one launch: block c takes chunk c of the sorted rows (SEG_CH rows of
+// ONE value, chunk_v[c]); its 4 waves sum 32 rows each in order (the wave's row indices read
+// once and broadcast by shuffles, 16 rows' loads in flight before any add), then wave 0 adds
+// the wave partials in wave order.  A value with one chunk (nearly all) is written directly;
+// a skewed value (the MaskGIT mask token, a collapsed code) publishes its chunk partials
+// (write-through) and the block that draws its last ticket sums them in chunk order, so the
+// result never depends on arrival order (bitwise reproducible).  Without a counter pool
+// the partials are summed by seg_combine_kernel instead (same order).
 template <int ND>
-__global__ __launch_bounds__(256) void seg_chunk_kernel(SegRows s, const int* __restrict__ offsets,
-                                                        const int* __restrict__ perm,
-                                                        const int* __restrict__ seg_start, int V,
-                                                        int max_chunks, float* __restrict__ part) {
+__device__ __forceinline__ void seg_rows_wave(const SegRows& s, const int* __restrict__ perm,
+                                              int r0, int n, int v, float (&acc)[ND]) {
   const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (c >= max_chunks || c >= seg_start[V]) return;
-  const int v = value_of_chunk(seg_start, V, c);
-  const int r0 = offsets[v] + (c - seg_start[v]) * SEG_CH;
-  const int r1 = min(offsets[v + 1], r0 + SEG_CH);
-  const int n = r1 - r0;  // <= SEG_CH = 32 rows
   const int pm = lane < n ? perm[r0 + lane] : 0;
-  float acc[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) acc[i] = 0.f;
   const bool drop = s.drop_p > 0.f && (int64_t)v != s.mask_id;
   const uint64_t seed = drop ? mix_seed(s.seed_ptr, s.offset) : 0ull;
   const float sc = drop ? 1.0f / (1.0f - s.drop_p) : 1.0f;
-  for (int rb = 0; rb < n; rb += 8) {
-    float x[8][ND];
-    int64_t mm[8];
+  constexpr int U = ND <= 2 ? 16 : 8;  // rows in flight
+  for (int rb = 0; rb < n; rb += U) {
+    float x[U][ND];
+    int mm[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int m = __shfl(pm, rb + u < n ? rb + u : 0, 64);
       mm[u] = m;
       const int64_t b = m / s.N, nn = m - b * s.N;
@@ -408,76 +491,152 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegRows s, const int* __
       }
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < U; ++u) {
       if (rb + u >= n) break;
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
         const int d = lane + 64 * i;
         float xv = x[u][i];
-        if (drop) xv = uniform01(seed, (uint64_t)(mm[u] * s.D + d)) >= s.drop_p ? xv * sc : 0.f;
+        if (drop) xv = uniform01(seed, (uint64_t)((int64_t)mm[u] * s.D + d)) >= s.drop_p ? xv * sc : 0.f;
         acc[i] += xv;
       }
     }
   }
+}
+
+template <int ND>
+__global__ __launch_bounds__(256) void seg_sum_kernel(SegRows s, const int* __restrict__ offsets,
+                                                      const int* __restrict__ perm,
+                                                      const int* __restrict__ seg_start,
+                                                      const int* __restrict__ chunk_v, int V,
+                                                      float* __restrict__ part,
+                                                      float* __restrict__ out, int accumulate,
+                                                      int* __restrict__ cnt) {
+  __shared__ float red[3][64 * ND];
+  __shared__ float cmb[256];
+  const int c = blockIdx.x;
+  if (c >= seg_start[V]) return;  // block-uniform
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int v = chunk_v[c];
+  const int cs = seg_start[v], ce = seg_start[v + 1];
+  const int r0 = offsets[v] + (c - cs) * SEG_CH, r1 = min(offsets[v + 1], r0 + SEG_CH);
+  const int rw = r0 + 32 * w, n = max(0, min(r1 - rw, 32));
+  float acc[ND];
+  seg_rows_wave<ND>(s, perm, rw, n, v, acc);
+  if (w > 0) {
 #pragma unroll
-  for (int i = 0; i < ND; ++i) {
-    const int d = lane + 64 * i;
-    if (d < s.D) part[(int64_t)c * s.D + d] = acc[i];
+    for (int i = 0; i < ND; ++i) red[w - 1][lane + 64 * i] = acc[i];
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      const int d = lane + 64 * i;
+      const float t = ((acc[i] + red[0][d]) + red[1][d]) + red[2][d];
+      if (d >= s.D) continue;
+      if (ce - cs == 1) {
+        const int64_t e = (int64_t)v * s.D + d;
+        out[e] = accumulate ? out[e] + t : t;
+      } else if (cnt) {
+        st_wt(part + (int64_t)c * s.D + d, t);
+      } else {
+        part[(int64_t)c * s.D + d] = t;
+      }
+    }
+  }
+  if (ce - cs == 1 || !cnt) return;  // block-uniform
+  if (!last_block(cnt + v, ce - cs)) return;
+  // the value's chunk partials in chunk order: thread (j, d) sums chunks cs + j, + J, ...
+  // (16 in flight), then the J partial sums in a fixed pairwise tree
+  int J = 1;
+  while (2 * J * s.D <= 256) J *= 2;
+  for (int d0 = 0; d0 < s.D; d0 += 256 / J) {
+    const int j = threadIdx.x / (256 / J), d = d0 + threadIdx.x % (256 / J);
+    float t = 0.f;
+    if (d < s.D) {
+      int k = cs + j;
+      for (; k + 15 * J < ce; k += 16 * J) {
+        float q[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) q[u] = ld_wt(part + (int64_t)(k + u * J) * s.D + d);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) t += q[u];
+      }
+      for (; k < ce; k += J) t += ld_wt(part + (int64_t)k * s.D + d);
+    }
+    cmb[threadIdx.x] = t;
+    __syncthreads();
+    for (int h = J / 2; h >= 1; h >>= 1) {
+      if (j < h) cmb[threadIdx.x] += cmb[threadIdx.x + h * (256 / J)];
+      __syncthreads();
+    }
+    if (j == 0 && d < s.D) {
+      const int64_t e = (int64_t)v * s.D + d;
+      out[e] = accumulate ? out[e] + cmb[threadIdx.x] : cmb[threadIdx.x];
+    }
+    __syncthreads();
   }
 }
 
-// One block per value: thread (j, d) sums chunks seg_start[v] + j, + J, + 2J, ... of column
-// d in order (J = 256 / D lanes per column), then the J partial sums are added in a fixed
-// pairwise tree through LDS.  A skewed value (the MaskGIT mask token owns most positions:
-// hundreds of chunks) is spread over the block instead of one thread's serial loop (that
-// form took 29 us per call); bitwise reproducible.
+// seg_sum_kernel's combine as a launch (no counter pool): values with > 1 chunk
 __global__ __launch_bounds__(256) void seg_combine_kernel(const float* __restrict__ part,
                                                           const int* __restrict__ seg_start, int V,
                                                           int D, float* __restrict__ out,
                                                           int accumulate) {
-  __shared__ float red[256];
+  __shared__ float cmb[256];
   const int v = blockIdx.x;
-  const int c0 = seg_start[v], c1 = seg_start[v + 1];
-  int J = 1;  // the largest power of two with J * D <= 256
+  const int cs = seg_start[v], ce = seg_start[v + 1];
+  if (ce - cs <= 1) return;
+  int J = 1;
   while (2 * J * D <= 256) J *= 2;
   for (int d0 = 0; d0 < D; d0 += 256 / J) {
     const int j = threadIdx.x / (256 / J), d = d0 + threadIdx.x % (256 / J);
     float t = 0.f;
-    if (d < D)
-      for (int c = c0 + j; c < c1; c += J) t += part[(int64_t)c * D + d];
-    red[threadIdx.x] = t;
+    if (d < D) {
+      int k = cs + j;
+      for (; k + 15 * J < ce; k += 16 * J) {
+        float q[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) q[u] = part[(int64_t)(k + u * J) * D + d];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) t += q[u];
+      }
+      for (; k < ce; k += J) t += part[(int64_t)k * D + d];
+    }
+    cmb[threadIdx.x] = t;
     __syncthreads();
-    for (int w = J / 2; w >= 1; w >>= 1) {  // red[j] += red[j + w] over column slots
-      if (j < w) red[threadIdx.x] += red[threadIdx.x + w * (256 / J)];
+    for (int h = J / 2; h >= 1; h >>= 1) {
+      if (j < h) cmb[threadIdx.x] += cmb[threadIdx.x + h * (256 / J)];
       __syncthreads();
     }
     if (j == 0 && d < D) {
       const int64_t e = (int64_t)v * D + d;
-      out[e] = accumulate ? out[e] + red[threadIdx.x] : red[threadIdx.x];
+      out[e] = accumulate ? out[e] + cmb[threadIdx.x] : cmb[threadIdx.x];
     }
     __syncthreads();
   }
 }
 
 int64_t seg_rowsum_scratch_floats(int64_t M, int64_t V, int64_t D) {
-  return ((M + SEG_CH - 1) / SEG_CH + V) * D;
+  return seg_max_chunks(M, V) * D;
 }
 
 void seg_rowsum(const SegRows& s, const int* offsets, const int* perm, const int* seg_start,
                 int64_t M, int64_t V, float* out, int accumulate, float* part, hipStream_t st) {
-  const int max_chunks = (int)((M + SEG_CH - 1) / SEG_CH + V);
-  const dim3 grid((unsigned)((max_chunks + 3) / 4));
-  if (s.D <= 64)
-    hipLaunchKernelGGL(seg_chunk_kernel<1>, grid, dim3(256), 0, st, s, offsets, perm, seg_start,
-                       (int)V, max_chunks, part);
-  else if (s.D <= 128)
-    hipLaunchKernelGGL(seg_chunk_kernel<2>, grid, dim3(256), 0, st, s, offsets, perm, seg_start,
-                       (int)V, max_chunks, part);
-  else
-    hipLaunchKernelGGL(seg_chunk_kernel<8>, grid, dim3(256), 0, st, s, offsets, perm, seg_start,
-                       (int)V, max_chunks, part);
-  hipLaunchKernelGGL(seg_combine_kernel, dim3((unsigned)V), dim3(256), 0, st, part, seg_start, (int)V,
-                     s.D, out, accumulate);
+  const int max_chunks = (int)seg_max_chunks(M, V);
+  const int* chunk_v = seg_start + (V + 1);
+  int* cnt = counters(V, FIN_REDUCE);
+  const dim3 grid((unsigned)max_chunks);
+#define SEG_L(NDV) hipLaunchKernelGGL(seg_sum_kernel<NDV>, grid, dim3(256), 0, st, s, offsets, perm, \
+                                      seg_start, chunk_v, (int)V, part, out, accumulate, cnt)
+  if (s.D <= 64) SEG_L(1);
+  else if (s.D <= 128) SEG_L(2);
+  else if (s.D <= 256) SEG_L(4);
+  else SEG_L(8);
+#undef SEG_L
+  if (!cnt)
+    hipLaunchKernelGGL(seg_combine_kernel, dim3((unsigned)V), dim3(256), 0, st, part, seg_start,
+                       (int)V, s.D, out, accumulate);
 }
 
 int* group_by_seg_start(int* scratch, int64_t M, int64_t V) {

@@ -199,3 +199,70 @@ extern "C" int tvq_layer_drop(const int64_t* seed_ptr, uint64_t offset, float p,
                      offset, p, (int)n, keep, touched, (int)accumulate);
   return launch_status("tvq_layer_drop");
 }
+
+// ---------------------------------------------------------------- step glue
+// The few elementwise ops a training step still needed from PyTorch (zero the flat
+// gradients, advance the dropout seed, add up the logged losses) as HIP launches, so a
+// replayed step graph holds no at::native kernel.
+namespace tvq {
+__global__ __launch_bounds__(256) void fill_f32_kernel(float* __restrict__ p, int64_t n, float v,
+                                                       int vec) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  if (vec) {
+    float4* q = reinterpret_cast<float4*>(p);
+    const float4 f = make_float4(v, v, v, v);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n / 4; i += stride) q[i] = f;
+    for (int64_t i = n / 4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) p[i] = v;
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) p[i] = v;
+  }
+}
+
+__global__ void add_i64_kernel(int64_t* __restrict__ p, int64_t v) {
+  if (threadIdx.x == 0) p[0] += v;
+}
+
+// out = ((a + b) + c) + d elementwise (c, d nullable), out_ab = a + b (nullable): the
+// evaluation order of Python's `a + b + c + d`
+__global__ __launch_bounds__(256) void sum4_kernel(const float* __restrict__ a,
+                                                   const float* __restrict__ b,
+                                                   const float* __restrict__ c,
+                                                   const float* __restrict__ d,
+                                                   float* __restrict__ out,
+                                                   float* __restrict__ out_ab, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float ab = a[i] + b[i];
+    float t = ab;
+    if (c) t = t + c[i];
+    if (d) t = t + d[i];
+    if (out) out[i] = t;
+    if (out_ab) out_ab[i] = ab;
+  }
+}
+}  // namespace tvq
+
+extern "C" int tvq_fill(float* p, int64_t n, float value, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(p && n >= 0, "tvq_fill: bad arguments");
+  if (n == 0) return TVQ_OK;
+  const int vec = ((uintptr_t)p & 15) == 0;
+  int64_t blocks = ((vec ? n / 4 : n) + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+  hipLaunchKernelGGL(fill_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p,
+                     n, value, vec);
+  return launch_status("tvq_fill");
+}
+
+extern "C" int tvq_add_i64(int64_t* p, int64_t value, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(p, "tvq_add_i64: bad arguments");
+  hipLaunchKernelGGL(add_i64_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, p, value);
+  return launch_status("tvq_add_i64");
+}
+
+extern "C" int tvq_sum4(const float* a, const float* b, const float* c, const float* d, float* out,
+                        float* out_ab, int64_t n, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(a && b && (out || out_ab) && n > 0 && (c || !d), "tvq_sum4: bad arguments");
+  const int64_t blocks = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  hipLaunchKernelGGL(sum4_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, b, c,
+                     d, out, out_ab, n);
+  return launch_status("tvq_sum4");
+}

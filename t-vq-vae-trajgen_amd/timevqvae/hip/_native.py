@@ -35,6 +35,9 @@ sig("tvq_counter_pool", I64, P, I64)
 sig("tvq_counter_capture", I64)
 sig("tvq_plan_trace", I64)
 sig("tvq_plan_read", ctypes.c_char_p, I64, restype=I64)
+sig("tvq_fill", P, I64, ctypes.c_float, P)
+sig("tvq_add_i64", P, I64, P)
+sig("tvq_sum4", P, P, P, P, P, P, I64, P)
 # --- VQ codebook -----------------------------------------------------------
 sig("tvq_vq_sqnorm", P, I64, I64, P, P)
 sig("tvq_vq_assign_nblocks", I64, restype=I64)

@@ -35,3 +35,43 @@ def mse_loss(inp, target):
 
 def l1_loss(inp, target):
     return _Loss.apply(inp, target, 1)
+
+
+def _flat_same(ts):
+    n = ts[0].numel()
+    return all(t.is_cuda and t.dtype == torch.float32 and t.numel() == n and t.is_contiguous()
+               for t in ts)
+
+
+class _Add2(torch.autograd.Function):
+    """a + b (same shape) as one tvq_sum4 launch; the backward passes the gradient to both
+    without a kernel (MaskGIT's mask_pred_loss_l + mask_pred_loss_h, maskgit.py:192)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        out = torch.empty_like(a)
+        call("tvq_sum4", ptr(a), ptr(b), None, None, ptr(out), None, a.numel(), stream_ptr())
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+def add_losses(a, b):
+    if not _flat_same((a, b)) or a.shape != b.shape:
+        return a + b
+    return _Add2.apply(a, b)
+
+
+@torch.no_grad()
+def loss_sums(rl, rh, vl, vh):
+    """((rl + rh) + vl) + vh and rl + rh -- the logged totals of stage1.py:170-198 -- in one
+    tvq_sum4 launch (no autograd: the bands were backpropagated from their own roots)."""
+    ts = (rl, rh, vl, vh)
+    if not _flat_same(ts):
+        return ((rl + rh) + vl) + vh, rl + rh
+    out, ab = torch.empty_like(vl), torch.empty_like(rl)  # shapes of the broadcast sums
+    call("tvq_sum4", ptr(rl), ptr(rh), ptr(vl.reshape(rl.shape)), ptr(vh.reshape(rl.shape)),
+         ptr(out), ptr(ab), rl.numel(), stream_ptr())
+    return out, ab

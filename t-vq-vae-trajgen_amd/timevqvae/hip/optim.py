@@ -93,7 +93,7 @@ class FusedAdamW(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = False):
         # gradients accumulate in place into the flat buffer views
         _grad_epoch[0] += 1
-        self.flat_grad.zero_()
+        call("tvq_fill", ptr(self.flat_grad), self.flat_grad.numel(), 0.0, stream_ptr())
 
     def gather_gates(self):
         """gates[s] <- whether segment s's gated branch ran this step (after the forward

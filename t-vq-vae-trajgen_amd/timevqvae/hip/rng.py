@@ -56,7 +56,8 @@ def advance(device):
     """Advance the device seed (call once per training step; capturable) and restart the
     per-step call index."""
     _calls[0] = 0
-    seed_tensor(device).add_(1)
+    from ._native import call, ptr, stream_ptr
+    call("tvq_add_i64", ptr(seed_tensor(device)), 1, stream_ptr())
 
 
 _device_decisions = [False]

@@ -540,8 +540,10 @@ def prior_lf_eval_supported(tf, s):
                 return False
         elif not hasattr(block, "ff") or block.ff[0][0].weight.shape[0] != 128:
             return False
-    return all(p.dtype == torch.float32 and p.is_cuda and p.is_contiguous()
-               for p in tf.parameters())
+    # tvq_prior_lf_eval reads every weight with 16-byte loads (TVQ_CHECK_ARG there): a
+    # FusedAdamW flat buffer packs parameters without padding, so check, don't assume
+    return all(p.dtype == torch.float32 and p.is_cuda and p.is_contiguous() and
+               p.data_ptr() % 16 == 0 for p in tf.parameters())
 
 
 def prior_lf_eval(tf, s, class_idx=None):

@@ -16,6 +16,7 @@ import torch.nn as nn
 from ..hip import rng, streams, wgrad
 from ..hip.sample import codebook_gather_nchw, mask_len, maskgit_remask, maskgit_sample
 from ..hip.signal import stft_encode
+from ..hip.loss import add_losses
 from ..hip.vq import indices_only
 from ..hip.xf import mask_tokens, masked_cross_entropy
 from ..utils import freeze, quantize, zero_pad_high_freq, zero_pad_low_freq
@@ -155,7 +156,7 @@ class MaskGIT(nn.Module):
             br.join()
         finally:
             self.transformer_l._class_rand = self.transformer_h._class_rand = None
-        return mask_pred_loss_l + mask_pred_loss_h, (mask_pred_loss_l, mask_pred_loss_h)
+        return add_losses(mask_pred_loss_l, mask_pred_loss_h), (mask_pred_loss_l, mask_pred_loss_h)
 
     def _randomly_mask_tokens(self, s, mask_token_id, device, ratio=None, rand=None):
         """maskgit.py:194-216 on device; returns (s_M, mask) with mask=True for kept tokens.

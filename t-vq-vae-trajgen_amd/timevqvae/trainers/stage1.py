@@ -7,23 +7,18 @@ loss_hist with the reference's logged scalar names (stage1.py:183-196).
 One fused STFT kernel produces both encoder inputs and both targets
 (stage1.py:101-113 + vq_vae.py:179-180).
 """
-import os
-
 import torch
 import torch.nn as nn
 
 from ..hip import streams, wgrad
 from ..hip.conv import wgrad_deferred
-from ..hip.loss import l1_loss, mse_loss
+from ..hip.loss import l1_loss, loss_sums, mse_loss
 from ..hip.optim import FusedAdamW
 from ..utils.checkpoint import adapt_state_dict, read_state_dict, save_checkpoint
 from ..hip.signal import stft_encode
 from ..models import VectorQuantize, VQVAEDecoder, VQVAEEncoder
 from ..utils import (compute_downsample_rate, linear_warmup_cosine_annealingLR, quantize,
                      zero_pad_high_freq, zero_pad_low_freq)
-
-# diagnosis only: the stage1 bands a bench run computes (both by default)
-_BANDS = tuple(os.environ.get("TVQ_BENCH_BANDS", "HF,LF").split(","))
 
 
 class Stage1(nn.Module):
@@ -102,17 +97,19 @@ class Stage1(nn.Module):
         perplexities = {"LF": parts["LF"][3], "HF": parts["HF"][3]}
         return recons_loss, vq_losses, perplexities
 
-    def forward_backward(self, batch, batch_idx=0):
+    def forward_backward(self, batch, batch_idx=0, bands=("HF", "LF")):
         """training_step + backward of its loss, with each band's forward AND backward on
         its own stream inside streams.concurrent() (both fork off the current stream).
         The two bands are disjoint subgraphs of the loss sum, so backpropagating
         (recons + vq loss) per band gives exactly the gradients of loss.sum().  Returns a
-        callable that builds training_step's dict; call it after the region's join."""
+        callable that builds training_step's dict; call it after the region's join.
+        `bands` (diagnosis: bench.py's TVQ_BENCH_BANDS times one band alone) must name both
+        bands for a training step; a single band returns a zero loss."""
         x, y = batch
         s = stft_encode(x, enc_l=True, enc_h=True, tgt_l=True, tgt_h=True)
         parts = {}
         for band in ("HF", "LF"):
-            if band not in _BANDS:  # diagnosis only (TVQ_BENCH_BANDS): time one band alone
+            if band not in bands:
                 continue
             with streams.branch(x.device, "s1" + band.lower()) as br:
                 br.inputs(s)
@@ -130,7 +127,7 @@ class Stage1(nn.Module):
             self._sched.step()
         if len(parts) < 2:
             return lambda: {"loss": torch.zeros((), device=x.device)}
-        return lambda: self._loss_hist(*self._assemble(parts))
+        return lambda: self._loss_hist(*self._assemble(parts), fused=True)
 
     def training_step(self, batch, batch_idx):
         """stage1.py:170-198: loss and the logged scalars; steps the LR scheduler."""
@@ -140,12 +137,17 @@ class Stage1(nn.Module):
         return self._loss_hist(recons_loss, vq_losses, perplexities)
 
     @staticmethod
-    def _loss_hist(recons_loss, vq_losses, perplexities):
-        loss = ((recons_loss["LF.time"] + recons_loss["HF.time"]) + vq_losses["LF"]["loss"]
-                + vq_losses["HF"]["loss"])
+    def _loss_hist(recons_loss, vq_losses, perplexities, fused=False):
+        """fused: the sums for logging only (after forward_backward), one launch"""
+        rl, rh = recons_loss["LF.time"], recons_loss["HF.time"]
+        if fused:
+            loss, rsum = loss_sums(rl, rh, vq_losses["LF"]["loss"], vq_losses["HF"]["loss"])
+        else:
+            loss = (rl + rh) + vq_losses["LF"]["loss"] + vq_losses["HF"]["loss"]
+            rsum = rl + rh
         return {
             "loss": loss,
-            "recons_loss.time": recons_loss["LF.time"] + recons_loss["HF.time"],
+            "recons_loss.time": rsum,
             "recons_loss.LF.time": recons_loss["LF.time"],
             "recons_loss.HF.time": recons_loss["HF.time"],
             "commit_loss.LF": vq_losses["LF"]["commit_loss"],

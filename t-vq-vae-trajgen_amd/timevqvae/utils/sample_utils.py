@@ -1,7 +1,7 @@
 """Batched sampling helpers -- same API as the reference timevqvae/utils/sample_utils.py
 (unconditional_sample / conditional_sample, sample_utils.py:5-88; the plotting helper is
 not on the path).  MaskGIT.iterative_decoding and decode_token_ind_to_timeseries run on
-the HIP path; the batches stay on the device and reach the host in one transfer."""
+the HIP path; each batch reaches the host by an asynchronous copy into pinned memory."""
 import torch
 
 
@@ -17,13 +17,17 @@ def unconditional_sample(maskgit, n_samples: int, device, class_index=None, batc
     """Same contract as the reference (sample_utils.py:5-64): (x_l, x_h, x) on the host,
     and with return_representations also the decoder inputs (quantize_l, quantize_h).
 
-    Every batch stays on the device: the sampled token ids, the decoded LF / HF series and
-    the latents are written into preallocated device buffers, and the host receives them in
-    one transfer at the end instead of one `.cpu()` per tensor and batch."""
+    Each batch's decoded LF / HF series (and latents) are copied asynchronously into
+    preallocated pinned host buffers (non_blocking device->host copies on the stream; one
+    synchronisation at the end), so device memory stays bounded by one batch, as the
+    reference's per-batch `.cpu()` keeps it, without a host round trip per batch."""
     device = torch.device(device)
     sizes = _batch_sizes(n_samples, batch_size)
-    bufs = None
+    if not sizes:
+        raise ValueError("unconditional_sample: n_samples must be positive")
+    host = None
     row = 0
+    pin = device.type == "cuda"
     for b in sizes:
         s_l, s_h = maskgit.iterative_decoding(num=b, device=device, class_index=class_index)
         parts = []
@@ -31,21 +35,15 @@ def unconditional_sample(maskgit, n_samples: int, device, class_index=None, batc
             out = maskgit.decode_token_ind_to_timeseries(s, band, return_representations)
             parts.append(out if return_representations else (out, None))
         (x_l, q_l), (x_h, q_h) = parts
-        if bufs is None:  # shapes are known after the first batch
-            like = [x_l, x_h] + ([q_l, q_h] if return_representations else [])
-            bufs = [torch.empty((n_samples,) + tuple(t.shape[1:]), device=device, dtype=t.dtype)
-                    for t in like]
-        for buf, t in zip(bufs, (x_l, x_h, q_l, q_h)):
-            buf[row:row + b].copy_(t)
+        outs = [x_l, x_h] + ([q_l, q_h] if return_representations else [])
+        if host is None:  # shapes are known after the first batch
+            host = [torch.empty((n_samples,) + tuple(t.shape[1:]), dtype=t.dtype, pin_memory=pin)
+                    for t in outs]
+        for h, t in zip(host, outs):
+            h[row:row + b].copy_(t, non_blocking=pin)
         row += b
-    if bufs is None:
-        raise ValueError("unconditional_sample: n_samples must be positive")
-    # one device->host copy: the series (and latents) packed into a single flat buffer
-    flat = torch.cat([t.reshape(-1) for t in bufs]).cpu()
-    host, off = [], 0
-    for t in bufs:
-        host.append(flat[off:off + t.numel()].view(t.shape))
-        off += t.numel()
+    if pin:
+        torch.cuda.current_stream(device).synchronize()
     x_l, x_h = host[0], host[1]
     series = (x_l, x_h, x_l + x_h)  # summed on the host, as the reference does
     if return_representations:

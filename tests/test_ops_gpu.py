@@ -684,3 +684,4 @@ def test_upsample_nearest_t(B, Lin, D, Lout, cuda):
     torch.cuda.synchronize()
     assert torch.equal(yd.cpu(), yc.detach())
     close(xd.grad, xc.grad, what="dx")
+

@@ -60,6 +60,33 @@ def test_fused_prior_matches_unfused_and_oracle(depth, K, n, B, cond, cuda):
     assert rel(fused, unfused) < 1e-4, rel(fused, unfused)
     assert rel(fused, ref) < 1e-4, rel(fused, ref)
     assert float((fused.cpu() - ref).abs().max()) <= 1e-3 * float(ref.abs().max())
+    # what MaskGIT's decoding consumes: the per-token argmax (greedy choice / confidence
+    # ranking) agrees with the oracle's wherever the oracle's top-2 logit gap exceeds the
+    # fp32 reassociation noise (1e-4 of the row's logit scale)
+    top2 = torch.topk(ref.double(), 2, dim=-1).values
+    gap = top2[..., 0] - top2[..., 1]
+    scale = ref.double().abs().amax(-1)
+    clear = gap > 1e-4 * scale
+    agree = fused.cpu().argmax(-1) == ref.argmax(-1)
+    assert bool(agree[clear].all()), int((~agree & clear).sum())
+    assert float(clear.float().mean()) > 0.99
+
+
+def test_fused_prior_declines_unaligned_weights(cuda):
+    """tvq_prior_lf_eval reads weights with 16-byte loads: a parameter whose storage is not
+    16-byte aligned (e.g. packed after an odd-sized one in a flat buffer) must send the
+    prior down the unfused path, not raise (prior_lf_eval_supported)."""
+    from timevqvae.hip import xf
+    m, _ = _prior(cuda, 1, 64, 24)
+    s = torch.randint(0, 65, (4, 24), device=cuda)
+    w = m.blocks.project_in.weight
+    buf = torch.empty(w.numel() + 1, device=cuda)
+    buf[1:].copy_(w.detach().reshape(-1))
+    with torch.no_grad():
+        assert xf.prior_lf_eval_supported(m, s)
+        w.data = buf[1:].view_as(w)  # 4 bytes past a 256-byte-aligned allocation
+        assert not xf.prior_lf_eval_supported(m, s)
+        m(s)  # the unfused path still runs
 
 
 def test_fused_prior_not_used_when_training_or_grad(cuda):
