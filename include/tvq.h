@@ -440,6 +440,32 @@ int tvq_embedding_bwd(const int64_t* idx, int64_t M, int64_t D, const float* g, 
                       int64_t V, float* tgrad, int64_t accumulate, int64_t mask_id, float drop_p,
                       const int64_t* seed_ptr, uint64_t offset, int32_t* workspace,
                       tvq_stream_t stream);
+/* Tied logits + masked cross-entropy in training, the logits never written
+ * (bidirectional_transformer.py:186-191 + maskgit.py:183-191):
+ *   logits[m, k] = h[m, :] . W[k, :] + bias[m % n, k]   (k < K; h (M, D) row-major, D in
+ *                  {32, 64, 128}; W (>= K, D) the tied token table; bias row stride ldb)
+ *   out = {mean over rows with keep[m] == false of (lse[m] - logits[m, target[m]]), count}
+ * lse (M floats) is kept for the backward.  K % 32 == 0; h, W 16-byte aligned.
+ * Backward (gout: d loss, stats: fwd `out`): dh (M, D) written (NULL: skipped); dW (K, D)
+ * and dbias (n, ldb; columns >= K get 0) summed over rows in a fixed split order and added
+ * when accumulate (NULL: skipped).  workspace: tvq_tied_ce_workspace floats, the same
+ * buffer for fwd and bwd. */
+int64_t tvq_tied_ce_workspace(int64_t M, int64_t D, int64_t K, int64_t n, int64_t ldb);
+int tvq_tied_ce_fwd(const float* h, int64_t M, int64_t D, const float* W, int64_t K,
+                    const float* bias, int64_t n, int64_t ldb, const int64_t* target,
+                    const bool* keep, float* lse, float* out, float* workspace,
+                    tvq_stream_t stream);
+int tvq_tied_ce_bwd(const float* h, int64_t M, int64_t D, const float* W, int64_t K,
+                    const float* bias, int64_t n, int64_t ldb, const int64_t* target,
+                    const bool* keep, const float* lse, const float* stats, const float* gout,
+                    float* dh, float* dW, float* dbias, int64_t accumulate, float* workspace,
+                    tvq_stream_t stream);
+/* embed[:, 1:, :] of the priors (the class token dropped before the head,
+ * bidirectional_transformer.py:188,233): backward == 0: y (B, n, D) from x (B, n+1, D);
+ * backward != 0: its adjoint, y (B, n+1, D) from x (B, n, D) with zero class rows.  D % 4 == 0,
+ * 16-byte aligned. */
+int tvq_drop_first_token(const float* x, int64_t B, int64_t n, int64_t D, float* y,
+                         int64_t backward, tvq_stream_t stream);
 /* F.cross_entropy(logits[~keep], s[~keep]) (maskgit.py:183-191); out = {loss, count}. */
 int64_t tvq_masked_ce_workspace(int64_t M);
 int tvq_masked_ce_fwd(const float* logits, int64_t ldl, int64_t M, int64_t K,

@@ -45,4 +45,7 @@ int64_t seg_rowsum_scratch_floats(int64_t M, int64_t V, int64_t D);
 int* group_by_seg_start(int* scratch, int64_t M, int64_t V);
 void seg_rowsum(const SegRows& s, const int* offsets, const int* perm, const int* seg_start,
                 int64_t M, int64_t V, float* out, int accumulate, float* part, hipStream_t st);
+// the mean of a masked cross-entropy from per-block (loss sum, count) pairs part[2 P]:
+// out = {sum / count, count} (tvq_xf.hip masked_ce_final_kernel), one block
+void masked_ce_final(const float* part, int P, float* out, hipStream_t st);
 }  // namespace tvq

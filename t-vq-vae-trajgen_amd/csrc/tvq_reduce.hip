@@ -221,6 +221,19 @@ constexpr int GB_CHUNK = 256;
 constexpr int SEG_CH = 128;
 __host__ __device__ __forceinline__ int seg_chunks_of(int n) { return n > 0 ? (n + SEG_CH - 1) / SEG_CH : 1; }
 static int64_t seg_max_chunks(int64_t M, int64_t V) { return (M + SEG_CH - 1) / SEG_CH + V; }
+__host__ __device__ __forceinline__ int* seg_chunk_infos(int* seg_start, int64_t V) {
+  const uintptr_t p = reinterpret_cast<uintptr_t>(seg_start + V + 1);
+  return reinterpret_cast<int*>((p + 15) & ~(uintptr_t)15);
+}
+// chunk descriptors (int4 per chunk: value, first sorted row, rows, first chunk | count << 16)
+// for the nc chunks of value v whose rows start at sorted position r0: one load per block
+__device__ __forceinline__ void seg_chunk_info(int* info, int v, int r0, int n, int cs, int nc) {
+  for (int i = 0; i < nc; ++i) {
+    const int a = r0 + i * SEG_CH;
+    const int4 d = make_int4(v, a, min(n - i * SEG_CH, SEG_CH), cs | (nc << 16));
+    reinterpret_cast<int4*>(info)[cs + i] = d;
+  }
+}
 
 template <typename IT>
 __global__ __launch_bounds__(256) void gb_hist_kernel(const IT* __restrict__ idx, int64_t M, int V,
@@ -305,10 +318,9 @@ __global__ __launch_bounds__(1024) void gb_scan_kernel(const int* __restrict__ h
       chunk_off[(int64_t)c * V + v] = s;
       s += h;
     }
-    run += tot[v];
     const int nc = seg_chunks_of(tot[v]);
-    if (chunk_v)
-      for (int i = 0; i < nc; ++i) chunk_v[segs + i] = v;
+    if (chunk_v) seg_chunk_info(chunk_v, v, run, tot[v], segs, nc);
+    run += tot[v];
     segs += nc;
   }
   if (threadIdx.x == 0) {
@@ -325,7 +337,12 @@ __global__ __launch_bounds__(1024) void gb_scan_kernel(const int* __restrict__ h
 // places its tokens in token order: the lanes holding the same value are found by AND-ing
 // the ballots of the value's bits, a lane's rank among them is a popcount, and the highest
 // such lane advances the wave's offset.  Same offsets / perm as the 3-launch path.
-constexpr int GB1_MAX_M = 32768, GB1_MAX_V = 1024, GB1_T = 1024;
+// Measured in the joint step (round 4, profiles/r04e_step_kernels.csv): one block is the
+// fastest form for the class-embedding group-bys (M = 256: 4.5 us against ~15 for the three
+// launches) but loses on the token group-bys (M = 6144 / 24576: 16-47 / 88-115 us), a long
+// serial chain on one CU that shares it with the step's other three streams.  Above
+// GB1_MAX_M the three-launch sort runs instead.
+constexpr int GB1_MAX_M = 2048, GB1_MAX_V = 1024, GB1_T = 1024;
 template <typename IT>
 __global__ __launch_bounds__(GB1_T) void gb_sort1_kernel(const IT* __restrict__ idx, int M, int V,
                                                          int* __restrict__ offsets,
@@ -338,9 +355,20 @@ __global__ __launch_bounds__(GB1_T) void gb_sort1_kernel(const IT* __restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int per = ((M + 15) / 16 + 63) / 64 * 64;  // tokens per wave (multiple of 64)
   for (int i = tid; i < 16 * V; i += GB1_T) hist[i] = 0;
-  for (int m = tid; m < M; m += GB1_T) {
-    const int v = (int)idx[m];
-    vals[m] = (unsigned short)(v >= 0 && v < V ? v : 0xFFFF);
+  // 8 loads in flight per thread (a load -> LDS store per iteration waits a full memory
+  // round trip each time: 24 of them for M = 24576)
+  for (int m0i = 0; m0i < M; m0i += 8 * GB1_T) {
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int m = m0i + u * GB1_T + tid;
+      v[u] = m < M ? (int)idx[m] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int m = m0i + u * GB1_T + tid;
+      if (m < M) vals[m] = (unsigned short)(v[u] >= 0 && v[u] < V ? v[u] : 0xFFFF);
+    }
   }
   __syncthreads();
   const int m0 = w * per, m1 = min(M, m0 + per);
@@ -358,7 +386,7 @@ __global__ __launch_bounds__(GB1_T) void gb_sort1_kernel(const IT* __restrict__ 
   if (tid < V) {
     offsets[tid] = ex_t;
     seg_start[tid] = ex_c;
-    for (int i = 0; i < nc; ++i) chunk_v[ex_c + i] = tid;
+    seg_chunk_info(chunk_v, tid, ex_t, tot, ex_c, nc);
     int run = ex_t;
     for (int k = 0; k < 16; ++k) {
       const int c = hist[k * V + tid];
@@ -412,8 +440,8 @@ __global__ __launch_bounds__(256) void gb_place_kernel(const IT* __restrict__ id
 
 int64_t group_by_scratch_ints(int64_t M, int64_t V) {
   const int64_t chunks = (M + GB_CHUNK - 1) / GB_CHUNK;
-  // hist + chunk_off (3-launch path) | seg_start | chunk -> value map
-  return 2 * chunks * V + (V + 1) + seg_max_chunks(M, V);
+  // hist + chunk_off (3-launch path) | seg_start | (16-B aligned) chunk descriptors
+  return 2 * chunks * V + (V + 1) + 4 + 4 * seg_max_chunks(M, V);
 }
 
 template <typename IT>
@@ -423,16 +451,9 @@ static void group_by_t(const IT* idx, int64_t M, int64_t V, int* offsets, int* p
   int* hist = scratch;
   int* coff = scratch + (int64_t)chunks * V;
   int* seg_start = coff + (int64_t)chunks * V;
-  int* chunk_v = seg_start + (V + 1);
+  int* chunk_v = seg_chunk_infos(seg_start, V);
   if (M <= GB1_MAX_M && V <= GB1_MAX_V) {
-    const size_t lds = (size_t)16 * V * 4 + (size_t)M * 2;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gb_sort1_kernel<IT>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                16 * GB1_MAX_V * 4 + GB1_MAX_M * 2);
-      attr = true;
-    }
+    const size_t lds = (size_t)16 * V * 4 + (size_t)M * 2;  // <= 68 KB
     TVQ_PLAN("group_by sort1 M%lld V%lld", (long long)M, (long long)V);
     hipLaunchKernelGGL(gb_sort1_kernel<IT>, dim3(1), dim3(GB1_T), lds, st, idx, (int)M, (int)V,
                        offsets, perm, seg_start, chunk_v);
@@ -515,11 +536,12 @@ __global__ __launch_bounds__(256) void seg_sum_kernel(SegRows s, const int* __re
   __shared__ float red[3][64 * ND];
   __shared__ float cmb[256];
   const int c = blockIdx.x;
-  if (c >= seg_start[V]) return;  // block-uniform
+  const int total = seg_start[V];
+  const int4 d4 = reinterpret_cast<const int4*>(chunk_v)[c < total ? c : 0];
+  if (c >= total) return;  // block-uniform
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int v = chunk_v[c];
-  const int cs = seg_start[v], ce = seg_start[v + 1];
-  const int r0 = offsets[v] + (c - cs) * SEG_CH, r1 = min(offsets[v + 1], r0 + SEG_CH);
+  const int v = d4.x, r0 = d4.y, r1 = d4.y + d4.z;
+  const int cs = d4.w & 0xFFFF, ce = cs + (d4.w >> 16);
   const int rw = r0 + 32 * w, n = max(0, min(r1 - rw, 32));
   float acc[ND];
   seg_rows_wave<ND>(s, perm, rw, n, v, acc);
@@ -618,13 +640,14 @@ __global__ __launch_bounds__(256) void seg_combine_kernel(const float* __restric
 }
 
 int64_t seg_rowsum_scratch_floats(int64_t M, int64_t V, int64_t D) {
+  // (the chunk descriptors live in the group-by scratch, seg_chunk_infos)
   return seg_max_chunks(M, V) * D;
 }
 
 void seg_rowsum(const SegRows& s, const int* offsets, const int* perm, const int* seg_start,
                 int64_t M, int64_t V, float* out, int accumulate, float* part, hipStream_t st) {
   const int max_chunks = (int)seg_max_chunks(M, V);
-  const int* chunk_v = seg_start + (V + 1);
+  const int* chunk_v = seg_chunk_infos(const_cast<int*>(seg_start), V);
   int* cnt = counters(V, FIN_REDUCE);
   const dim3 grid((unsigned)max_chunks);
 #define SEG_L(NDV) hipLaunchKernelGGL(seg_sum_kernel<NDV>, grid, dim3(256), 0, st, s, offsets, perm, \

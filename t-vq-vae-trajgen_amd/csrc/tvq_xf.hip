@@ -436,6 +436,10 @@ __global__ __launch_bounds__(256) void masked_ce_final_kernel(const float* __res
   if (threadIdx.x == 0) { out[0] = s / c; out[1] = c; }
 }
 
+void masked_ce_final(const float* part, int P, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(masked_ce_final_kernel, dim3(1), dim3(256), 0, st, part, P, out);
+}
+
 // dlogits[m,k] = keep[m] ? 0 : g/cnt * (softmax - onehot)
 __global__ void masked_ce_bwd_kernel(const float* __restrict__ logits, int64_t ldl, int64_t M, int K,
                                      const int64_t* __restrict__ target,
@@ -1030,4 +1034,39 @@ extern "C" int tvq_gelu_bwd(const float* dy, const float* x, int64_t n, float* d
   hipLaunchKernelGGL(gelu_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dy, x, n,
                      dx);
   return launch_status("tvq_gelu_bwd");
+}
+
+// ---------------------------------------------------------------- drop the class token
+// y[b, i, :] = x[b, i + 1, :] (embed[:, 1:, :].contiguous(), bidirectional_transformer.py:
+// 188, 233) and its adjoint dx[b, 0, :] = 0, dx[b, i + 1, :] = dy[b, i, :]: float4 lanes
+namespace tvq {
+__global__ __launch_bounds__(256) void drop_first_kernel(const float4* __restrict__ src,
+                                                         float4* __restrict__ dst, int64_t B,
+                                                         int n, int D4, int backward) {
+  const int64_t tot = backward ? B * (n + 1) * D4 : B * n * D4;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < tot; e += (int64_t)gridDim.x * 256) {
+    const int d = (int)(e % D4);
+    const int64_t r = e / D4;
+    if (backward) {  // dst row r = (b, j) of (B, n + 1)
+      const int64_t b = r / (n + 1);
+      const int j = (int)(r - b * (n + 1));
+      dst[e] = j == 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : src[(b * n + j - 1) * D4 + d];
+    } else {  // dst row r = (b, i) of (B, n)
+      const int64_t b = r / n;
+      const int i = (int)(r - b * n);
+      dst[e] = src[(b * (n + 1) + i + 1) * D4 + d];
+    }
+  }
+}
+}  // namespace tvq
+
+extern "C" int tvq_drop_first_token(const float* x, int64_t B, int64_t n, int64_t D, float* y,
+                                    int64_t backward, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && y && B > 0 && n > 0 && D > 0 && D % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
+                    ((uintptr_t)y & 15) == 0, "tvq_drop_first_token: bad arguments");
+  const int64_t tot = (backward ? B * (n + 1) : B * n) * (D / 4);
+  hipLaunchKernelGGL(drop_first_kernel, dim3(grid_for(tot)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), B, (int)n,
+                     (int)(D / 4), (int)backward);
+  return launch_status("tvq_drop_first_token");
 }

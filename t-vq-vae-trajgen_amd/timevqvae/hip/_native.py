@@ -121,6 +121,10 @@ sig("tvq_embedding_fwd", P, I64, I64, P, P, I64, I64, F32, P, U64, P)
 sig("tvq_embedding_bwd_workspace", I64, I64, restype=I64)
 sig("tvq_embedding_bwd", P, I64, I64, P, I64, I64, P, I64, I64, F32, P, U64, P, P)
 sig("tvq_masked_ce_workspace", I64, restype=I64)
+sig("tvq_drop_first_token", P, I64, I64, I64, P, I64, P)
+sig("tvq_tied_ce_workspace", I64, I64, I64, I64, I64, restype=I64)
+sig("tvq_tied_ce_fwd", P, I64, I64, P, I64, P, I64, I64, P, P, P, P, P, P)
+sig("tvq_tied_ce_bwd", P, I64, I64, P, I64, P, I64, I64, P, P, P, P, P, P, P, P, I64, P, P)
 sig("tvq_masked_ce_fwd", P, I64, I64, I64, P, P, P, P, P, P)
 sig("tvq_masked_ce_bwd", P, I64, I64, I64, P, P, P, P, P, P, I64, P)
 sig("tvq_mask_tokens", P, I64, I64, I64, P, U64, P, P, P, P, P)

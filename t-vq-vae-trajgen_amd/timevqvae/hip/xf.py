@@ -575,3 +575,31 @@ def prior_lf_eval(tf, s, class_idx=None):
     call("tvq_prior_lf_eval", ptr(s), B, n, s.stride(0), ptr(cls), tf.n_classes, 128, arr,
          depth, K, float(tf.pred_head[2].eps), ptr(logits), ptr(ws), stream_ptr())
     return logits
+
+
+class _DropFirst(torch.autograd.Function):
+    """x[:, 1:, :] as a contiguous tensor (tvq_drop_first_token), its backward one kernel
+    writing the zero class rows (instead of a PyTorch copy, fill and copy)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        B, n1, D = x.shape
+        x = x.contiguous()
+        y = torch.empty((B, n1 - 1, D), device=x.device, dtype=x.dtype)
+        call("tvq_drop_first_token", ptr(x), B, n1 - 1, D, ptr(y), 0, stream_ptr())
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        B, n, D = g.shape
+        g = g.contiguous()
+        dx = torch.empty((B, n + 1, D), device=g.device, dtype=g.dtype)
+        call("tvq_drop_first_token", ptr(g), B, n, D, ptr(dx), 1, stream_ptr())
+        return dx
+
+
+def drop_first_token(x):
+    """embed[:, 1:, :] (B, n+1, D) -> (B, n, D) contiguous on the HIP path."""
+    if x.shape[-1] % 4 or not x.is_cuda:
+        return x[:, 1:, :].contiguous()
+    return _DropFirst.apply(x)
