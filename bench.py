@@ -298,6 +298,48 @@ FP32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 
 
+# PMC evidence of the roofline legs: profiles/<PROFILE_TAG>_<leg>_traffic.json, written by
+# tools/gpu_roofline.sh + tools/roof_traffic.py on the tree named in its "tree" field
+PROFILE_TAG = "r04"
+
+
+def _traffic(leg):
+    """(traffic bytes per op, evidence file, profiled tree) or (None, None, None)."""
+    path = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_{leg}_traffic.json")
+    if not os.path.exists(path):
+        return None, None, None
+    d = json.load(open(path))
+    return d["traffic_bytes"], os.path.relpath(path, ROOT), d.get("tree")
+
+
+def _with_traffic(res, leg):
+    t, src, tree = _traffic(leg)
+    res["traffic"] = t
+    res["traffic_source"] = src
+    res["traffic_tree"] = tree
+    if t:
+        res["traffic_over_algorithmic"] = round(t / res["algorithmic_bytes"], 3)
+    return res
+
+
+def cu_weighted_leg():
+    """Sum of the step's algorithmic FLOPs over the summed device time of all its kernels
+    (profiles/<PROFILE_TAG>_step_kernel_stats.csv, rocprofv3 over graph-replayed steps): the
+    fraction of the fp32 peak the CUs deliver while busy, across all four streams."""
+    path = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_step_kernel_stats.csv")
+    if not os.path.exists(path):
+        return None
+    import csv
+    rows = list(csv.DictReader(open(path)))
+    us = sum(float(r["us_per_step"]) for r in rows)
+    launches = sum(float(r["calls_per_step"]) for r in rows)
+    tf = STEP_GFLOP / (us * 1e-3)  # GFLOP / ms = TFLOP/s
+    return {"bound": "mfma", "gflop": STEP_GFLOP, "kernel_us_per_step": round(us, 1),
+            "launches_per_step": launches, "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(tf / FP32_PEAK_TFLOPS, 4),
+            "source": os.path.relpath(path, ROOT)}
+
+
 def _graph_time_us(fns, reps):
     """Average device time per launch of `fns` (each called `reps` times, interleaved),
     captured in one hipGraph on a side stream and timed with HIP events recorded on that
@@ -358,17 +400,13 @@ def dominant_leg(device):
     flops = sum(2.0 * K * M * N for M, N in shapes)
     byts = sum(4.0 * (K * (M + N) + 2 * M * N) for M, N in shapes)
     tf = flops / (us * 1e-6) / 1e12
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r03_dominant_traffic.json")
-    if os.path.exists(tpath):
-        traffic = json.load(open(tpath))["traffic_bytes"]
-    return {"bound": "mfma", "kernel": "wgrad_wide_kernel + wgrad_group_reduce_kernel (grouped "
+    return _with_traffic({"bound": "mfma", "kernel": "wgrad_wide_kernel + wgrad_group_reduce_kernel (grouped "
                                        "weight gradients of the LF prior's 16 Linears, "
                                        "dW_i += dY_i^T X_i over 6400 tokens, fp32 MFMA)",
             "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4),
             "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
-            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, "dominant")
 
 
 def conv_wgrad_leg(device):
@@ -393,17 +431,13 @@ def conv_wgrad_leg(device):
     flops = 2.0 * B * H * W * Co * (C * 9 + 1)
     byts = 4.0 * (2 * B * H * W * C + Co * (C * 9 + 1))
     tf = flops / (us * 1e-6) / 1e12
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r03_wgrad_traffic.json")
-    if os.path.exists(tpath):
-        traffic = json.load(open(tpath))["traffic_bytes"]
-    return {"bound": "mfma", "kernel": "conv_wgrad_w8_kernel<8,8> + its ordered slab sum (LF "
+    return _with_traffic({"bound": "mfma", "kernel": "conv_wgrad_w8_kernel<8,8> + its ordered slab sum (LF "
                                        "64->64 3x3 conv weight+bias gradient over 6144 positions, "
                                        "16 images per block, fp32 MFMA)",
             "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4),
             "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
-            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, "wgrad")
 
 
 def resblock_bwd_leg(device, C=16, W=32):
@@ -456,19 +490,15 @@ def resblock_bwd_leg(device, C=16, W=32):
     flops = 2.0 * (2.0 * B * P * C * K) + 2.0 * (2.0 * B * P * C * (K + 1))
     byts = 4.0 * (4 * B * C * P + 2 * (C * K + C) + 2 * (C * K + C))
     tf = flops / (us * 1e-6) / 1e12
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r03_rbbwd_traffic.json")
-    if os.path.exists(tpath):
-        traffic = json.load(open(tpath))["traffic_bytes"]
-    return {"bound": "mfma", "kernel": "fused ResBlock backward, C=16 on (256,16,3,32): "
+    return _with_traffic({"bound": "mfma", "kernel": "fused ResBlock backward, C=16 on (256,16,3,32): "
                                        "rb_bwd2_kernel + rb_bwd1_kernel<RB<16,32>> + one "
                                        "batched ordered slab-sum launch (16x16x4 fp32 MFMA, "
                                        "8 waves per image)",
             "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4),
             "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
             "launches_per_op": 3,
-            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, "rbbwd")
 
 
 def vq_assign_leg(device):
@@ -504,18 +534,14 @@ def vq_assign_leg(device):
     flops = 2.0 * M * K * D
     byts = 4.0 * (2 * M * D + K * D) + 12.0 * M
     tf = flops / (us * 1e-6) / 1e12
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r03_vqassign_traffic.json")
-    if os.path.exists(tpath):
-        traffic = json.load(open(tpath))["traffic_bytes"]
-    return {"bound": "mfma", "kernel": "vq_assign_kernel<128,false>: HF codebook assignment, "
+    return _with_traffic({"bound": "mfma", "kernel": "vq_assign_kernel<128,false>: HF codebook assignment, "
                                        "24576 token rows x 512 codes x D 128, 16x16x4 fp32 "
                                        "MFMA distances + running argmax, straight-through "
                                        "output, token-major copy for the EMA statistics",
             "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4),
             "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
-            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, "vqassign")
 
 
 def linear_fwd_leg(device):
@@ -540,17 +566,13 @@ def linear_fwd_leg(device):
     flops = 2.0 * M * N * K
     byts = 4.0 * (M * K + N * K + N + 2 * M * N)
     tf = flops / (us * 1e-6) / 1e12
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r03_linfwd_traffic.json")
-    if os.path.exists(tpath):
-        traffic = json.load(open(tpath))["traffic_bytes"]
-    return {"bound": "mfma", "kernel": "gemm_rb2_kernel<64,true>: LF prior Linear forward "
+    return _with_traffic({"bound": "mfma", "kernel": "gemm_rb2_kernel<64,true>: LF prior Linear forward "
                                        "Y = R + X W^T + b, (6400 x 128) x (128 x 128), "
                                        "32x32x2 fp32 MFMA, one 32x32 tile per wave",
             "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4),
             "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
-            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, "linfwd")
 
 
 def roofline_leg(device, ms_per_step):
@@ -572,6 +594,7 @@ def roofline_leg(device, ms_per_step):
                    "frac": round(tf / FP32_PEAK_TFLOPS, 4),
                    "source": "tools/count_step_flops.py -> profiles/r03_step_flops.json"}
     out["step_frac"] = out["step"]["frac"]
+    out["cu_weighted"] = cu_weighted_leg()
     out["conv_t32"] = conv_t32_leg(device)
     return out
 
@@ -585,9 +608,9 @@ def conv_t32_leg(device):
     runs as one conv_t32_kernel launch (128-channel x 96-position tile on the 32x32x2 fp32
     MFMA, no split-K) reading the weight the step's pack cache packed once at the scope's
     begin (hip.conv.PackCache).  The committed rocprofv3 summary
-    (profiles/r01f_roofline_kernel_stats.csv) lists the launches; `traffic` is the
-    PMC-measured HBM bytes per op from profiles/r01f_roofline_traffic.json (FETCH_SIZE x2 +
-    WRITE_SIZE passes)."""
+    (profiles/<PROFILE_TAG>_t32_kernel_stats.csv) lists the launches; `traffic` is the
+    PMC-measured HBM bytes per op from profiles/<PROFILE_TAG>_t32_traffic.json (FETCH_SIZE x2 +
+    WRITE_SIZE passes on the tree its "tree" field names)."""
     from timevqvae.hip.conv import PackCache, conv2d
     x = torch.randn(256, 128, 3, 32, device=device)
     w = torch.randn(128, 128, 3, 3, device=device) * 0.03
@@ -608,17 +631,13 @@ def conv_t32_leg(device):
     ms = e0.elapsed_time(e1) / n
     flops = 2.0 * (256 * 3 * 32) * 128 * (128 * 9)
     achieved = flops / (ms * 1e-3) / 1e12
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r01f_roofline_traffic.json")
-    if os.path.exists(tpath):
-        traffic = json.load(open(tpath))["traffic_bytes"]
-    return {"bound": "mfma", "kernel": "conv2d 128->128 3x3 @ (256,128,3,32): "
+    return _with_traffic({"bound": "mfma", "kernel": "conv2d 128->128 3x3 @ (256,128,3,32): "
                                        "conv_t32_kernel<F,3,3,1,BK64,NW12> (32x32x2 fp32 MFMA; "
                                        "weight packed once per step by the pack cache)",
             "achieved": round(achieved, 2), "peak": 157.3, "unit": "TFLOP/s",
-            "frac": round(achieved / 157.3, 4), "traffic": traffic,
+            "frac": round(achieved / 157.3, 4),
             "algorithmic_bytes": 4 * (256 * 128 * 3 * 32 * 2 + 128 * 128 * 9),
-            "avg_launch_ms": round(ms, 4), "flops_per_launch": flops}
+            "avg_launch_ms": round(ms, 4), "flops_per_launch": flops}, "t32")
 
 
 def sampler_leg(tr, device, num=1024, reps=5):

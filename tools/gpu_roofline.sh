@@ -27,4 +27,7 @@ fi
 if [ "$LEG" = vqassign ]; then
   python tools/roof_traffic.py $O $O/traffic.json "HF VQ codebook assignment, 24576 token rows x 512 codes x D 128 (straight-through, token-major copy): vq_assign_kernel" vq_assign_kernel
 fi
+if [ "$LEG" = t32 ]; then
+  python tools/roof_traffic.py $O $O/traffic.json "HF ResBlock 128->128 3x3 conv on (256,128,3,32): conv_t32_kernel (pack-cached weights)" conv_t32_kernel
+fi
 echo roofline-done

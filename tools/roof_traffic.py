@@ -59,6 +59,9 @@ def main():
     res["write_MB"] = round(wmb, 3)
     res["traffic_bytes"] = int((fmb + wmb) * 1024 * 1024)
     res["op_avg_us_rocprof"] = round(us, 2)
+    import os
+    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), ".tree")
+    res["tree"] = open(tf).read().strip() if os.path.exists(tf) else None  # git HEAD profiled
     res["source"] = ("tools/gpu_roofline.sh: rocprofv3 --kernel-trace --stats, then --pmc FETCH_SIZE / "
                      "WRITE_SIZE / SQ_* passes of tools/roofline_only.py; FETCH_SIZE doubled per "
                      "MI355X_MICROARCH.md HBM section; tools/roof_traffic.py")
