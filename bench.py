@@ -66,11 +66,15 @@ class JointTrainer:
     one being trained), so they run concurrently: stage1's LF and HF bands each do
     forward+backward on a side stream while stage2 runs on the current stream with its
     HF encoder / HF transformer on side streams (timevqvae.hip.streams).
-    Graph mode (default): the step is captured as two hipGraph segments
-      [advance seed, zero_grad x2, stage1 LF | stage1 HF | stage2 fwd+bwd]
-        -> [codebook EMA (if deferred), AdamW1, AdamW2]
-    with the DP all-reduces (flat gradients, sync_codebook statistics) and the LR
-    schedulers run eagerly between / before the segments.
+    Graph mode (default), one replica: the step is one hipGraph
+      [advance seed, zero_grad x2, stage1 LF | stage1 HF | stage2 fwd+bwd, AdamW1, AdamW2].
+    Replicas (world > 1): stage1 and stage2 are captured as two graphs replayed on two
+    streams (hip.graph.BranchStepGraph); each is followed on its stream by its own DP
+    exchange (flat gradients + gates, BatchNorm statistics, stage1's sync_codebook
+    statistics), so one stage's all-reduces run while the other's backward still computes;
+    a final graph applies the codebook EMAs and both AdamW steps.  TVQ_DP_OVERLAP=0 keeps
+    the previous form (one fwd+bwd graph, every exchange after it).  The LR schedulers run
+    on the host before each replay.
     """
 
     def __init__(self, device, world, cfg=None, length=T, channels=C):
@@ -96,17 +100,22 @@ class JointTrainer:
                         dist.broadcast(b, 0)
         from timevqvae.hip.dp import ReplicaSync, flatten_bn_buffers
         self.sync = ReplicaSync(world)
-        # BatchNorm running statistics of the trained modules as one flat buffer (stage1's
-        # encoders / decoders, the HF prior's Upscale): averaged over the replicas every step
-        self.bn_flat = (flatten_bn_buffers([self.s1, self.s2.maskgit.transformer_l,
-                                            self.s2.maskgit.transformer_h])
-                        if world > 1 else None)
+        # BatchNorm running statistics of the trained modules, one flat buffer per stage
+        # (stage1's encoders / decoders; the HF prior's Upscale): averaged over the replicas
+        # every step, each right after its stage's backward
+        self.bn_flat = ([flatten_bn_buffers([self.s1]),
+                         flatten_bn_buffers([self.s2.maskgit.transformer_l,
+                                             self.s2.maskgit.transformer_h])]
+                        if world > 1 else [])
         self.device = device
         self._one = torch.ones((), device=device)
         self.graph = None
         self._pending = []
         from timevqvae.hip.conv import PackCache
-        self.packs = PackCache(device) if os.environ.get("TVQ_PACK_CACHE", "1") != "0" else None
+        on = os.environ.get("TVQ_PACK_CACHE", "1") != "0"
+        self.packs = PackCache(device) if on else None
+        # the DP form captures each stage as its own graph, each with its own cache
+        self.packs12 = (PackCache(device), PackCache(device)) if on and world > 1 else (None, None)
 
     def _allreduce(self, opt):
         """DP exchange (timevqvae.hip.dp): mean of the flat gradients; the layer-dropout
@@ -114,10 +123,38 @@ class JointTrainer:
         every replica updates the same segments and the replicas stay identical."""
         self.sync.gradients(opt)
 
-    def _sync_buffers(self):
+    def _sync_buffers(self, which=(0, 1)):
         """Mean of the BatchNorm running statistics over the replicas (DDP keeps them
-        equal with broadcast_buffers; here every state_dict tensor stays bitwise equal)."""
-        self.sync.buffers(self.bn_flat)
+        equal with broadcast_buffers; here every state_dict tensor stays bitwise equal).
+        `which`: the stages whose buffers to average (the mean is elementwise, so averaging
+        the stages separately gives the same bits as one buffer)."""
+        for i in which:
+            if i < len(self.bn_flat):
+                self.sync.buffers(self.bn_flat[i])
+
+    def _stage1_fwd_bwd(self, batch, packs):
+        """Stage1 alone (the DP form's first branch): LF and HF bands forward+backward on
+        their side streams, the codebook updates deferred.  Returns (out1, updates)."""
+        import contextlib
+        from timevqvae.hip import streams
+        from timevqvae.hip.vq import deferred_codebook_updates
+        with (packs.scope() if packs is not None else contextlib.nullcontext()), \
+                streams.concurrent(), deferred_codebook_updates() as pend:
+            hist1 = self.s1.forward_backward(batch, 0)
+        return hist1(), pend
+
+    def _stage2_fwd_bwd(self, batch, packs):
+        """Stage2 alone (the DP form's second branch): forward+backward on the current
+        stream with its HF chains on side streams."""
+        import contextlib
+        from timevqvae.hip import streams, wgrad
+        from timevqvae.hip.conv import wgrad_deferred
+        with (packs.scope() if packs is not None else contextlib.nullcontext()), \
+                streams.concurrent():
+            out2 = self.s2.training_step(batch, 0)
+            with wgrad_deferred(this_stream_only=True), wgrad.grouped():
+                out2["loss"].backward(self._one)
+        return out2
 
     def _fwd_bwd(self, batch, defer):
         """zero_grad, then stage1's LF and HF bands (forward+backward, one side stream
@@ -149,7 +186,9 @@ class JointTrainer:
 
     def step(self, batch):
         if self.graph is not None:
-            return self.graph.replay()[0]
+            outs = self.graph.replay()
+            # StepGraph: the first segment returns (out1, out2); BranchStepGraph: one per stage
+            return outs[0] if type(self.graph).__name__ == "StepGraph" else tuple(outs)
         from timevqvae.hip import rng
         rng.advance(self.device)
         out1, out2, _ = self._fwd_bwd(batch, defer=False)
@@ -205,7 +244,40 @@ class JointTrainer:
                 seg2()
                 return out
             self.graph = StepGraph([seg12], [None], warmup=2, before=before).capture()
-        else:
+        elif os.environ.get("TVQ_DP_OVERLAP", "1") != "0":
+            # replicas: stage1 and stage2 forward+backward as two graphs on two streams, each
+            # followed at once by its own exchange (its stage's flat gradients + gates, its
+            # BatchNorm statistics, for stage1 the sync_codebook statistics), so one stage's
+            # all-reduces overlap the other stage's backward; then [codebook EMA, AdamW x2]
+            from timevqvae.hip.graph import BranchStepGraph
+
+            def branch1():
+                rng.restart_calls()  # the seed advance itself runs eagerly before replay
+                self.opt1.zero_grad()
+                out1, self._pending = self._stage1_fwd_bwd(batch, self.packs12[0])
+                self.opt1.gather_gates()
+                return out1
+
+            def after1():
+                self._allreduce(self.opt1)
+                self._sync_buffers((0,))
+                for u in self._pending:
+                    u.reduce()
+
+            def branch2():
+                self.opt2.zero_grad()
+                out2 = self._stage2_fwd_bwd(batch, self.packs12[1])
+                self.opt2.gather_gates()
+                return out2
+
+            def after2():
+                self._allreduce(self.opt2)
+                self._sync_buffers((1,))
+
+            self.graph = BranchStepGraph(lambda: rng.advance(self.device), [branch1, branch2],
+                                         [after1, after2], seg2, warmup=2,
+                                         before=before).capture()
+        else:  # TVQ_DP_OVERLAP=0: one fwd+bwd graph, every exchange after it
             self.graph = StepGraph([seg1, seg2], [between1, None], warmup=2,
                                    before=before).capture()
 

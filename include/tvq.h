@@ -189,11 +189,14 @@ int tvq_conv_config(int64_t halo);
  * repacks every (weight, view) recorded under `id` into `arena` with a few batched
  * launches on `stream`; inside the scope a recorded weight is read from its arena slot and
  * a new one is packed into a fresh slot and recorded (arena full -> the per-call path).
- * A different id (or arena) drops the recorded entries.  The weights must not change
- * between begin and end (open it around forward+backward, not the optimizer step); the
- * scope is process-wide host state, one at a time.  entries() = recorded count. */
+ * Each id keeps its own entries (two graph segments with their own caches each repack only
+ * their weights); beginning an id with another arena drops its entries, release(id) frees
+ * them.  The weights must not change between begin and end (open it around
+ * forward+backward, not the optimizer step); one scope is open at a time (process-wide
+ * host state).  entries() = the last scope's recorded count. */
 int tvq_conv_packcache_begin(int64_t id, float* arena, int64_t cap_floats, tvq_stream_t stream);
 int tvq_conv_packcache_end(void);
+int tvq_conv_packcache_release(int64_t id);
 int64_t tvq_conv_packcache_entries(void);
 
 /* Deferred weight-gradient reductions: between begin() and flush(stream), the split sums
@@ -510,22 +513,44 @@ int tvq_prior_lf_eval(const int64_t* s, int64_t B, int64_t n, int64_t s_stride,
                       const int64_t* cls_idx, int64_t n_classes, int64_t width,
                       const float* const* weights, int64_t depth, int64_t K, float ln_eps,
                       float* logits, void* workspace, tvq_stream_t stream);
+/* tvq_prior_lf_eval followed by the categorical draw of tvq_maskgit_sample (same race, same
+ * noise counters) in the same launch: the tied logits are drawn from in registers and never
+ * written (logits, nullable, receives them for checking).  s doubles as the tokens whose
+ * mask_id entries are drawn (the others are kept, p = +inf). */
+int tvq_prior_lf_eval_sample(const int64_t* s, int64_t B, int64_t n, int64_t s_stride,
+                             const int64_t* cls_idx, int64_t n_classes, int64_t width,
+                             const float* const* weights, int64_t depth, int64_t K, float ln_eps,
+                             int64_t mask_id, const float* gumbel, const int64_t* seed_ptr,
+                             uint64_t offset, int64_t* sampled, float* selp, float* logits,
+                             void* workspace, tvq_stream_t stream);
 
 /* ---------------------------------------------------------------- MaskGIT sampling
  * One iterative-decoding step of MaskGIT.first_pass / second_pass (maskgit.py:294-411):
  * tvq_maskgit_sample draws, for every token equal to mask_id, a code from
- * Categorical(softmax(logits)) (maskgit.py:302-310) by inverse CDF at u (double softmax and
- * prefix), keeps the other tokens, and writes p(sampled) (fp32 softmax; +inf for kept
- * tokens, maskgit.py:320-326).  logits (B, n, K) with batch/token strides (sb, sn).
+ * Categorical(logits) as Categorical.sample runs it (maskgit.py:307-315 ->
+ * torch.multinomial's n_sample = 1 exponential race: argmax_k l_k + Gumbel_k, ties to the
+ * lowest k), keeps the other tokens, and writes p(sampled) (fp32 softmax, double sum; +inf
+ * for kept tokens, maskgit.py:320-326).  logits (B, n, K) with batch/token strides (sb, sn).
  * tvq_maskgit_remask: confidence = log(p + 1e-5) + temperature * Gumbel, re-mask exactly
  * the k lowest-confidence tokens of each row (mask_by_random_topk, maskgit.py:238-267,
  * ties by index) -> s_out (nullable) and/or masking (uint8, nullable).
- * Noise: u_cat / u_gumbel (B*n uniforms) when given, else the counter hash of
- * (*seed_ptr, offset, element). */
+ * Noise: gumbel (B*n*K Gumbel values, row-major) / u_gumbel (B*n uniforms) when given,
+ * else the counter hash of (*seed_ptr, offset, element).
+ * tvq_tied_logits_sample: tvq_maskgit_sample of logits = h W[:K]^T + bias[i, :K] (the
+ * priors' tied output head, bidirectional_transformer.py:186-191; row m = b n + i) without
+ * writing the logits: h (M, D), D 64 or 128; W (>= K, D); bias (n, ldb); h, W and the
+ * workspace (tvq_tied_logits_sample_workspace(K, D, n) bytes) 16-byte aligned.
+ * logits_out (M, K, nullable) receives the logits the draw used. */
 int tvq_maskgit_sample(const float* logits, int64_t sb, int64_t sn, int64_t B, int64_t n,
-                       int64_t K, const int64_t* s_in, int64_t mask_id, const float* u_cat,
+                       int64_t K, const int64_t* s_in, int64_t mask_id, const float* gumbel,
                        const int64_t* seed_ptr, uint64_t offset, int64_t* sampled, float* selp,
                        tvq_stream_t stream);
+int64_t tvq_tied_logits_sample_workspace(int64_t K, int64_t D, int64_t n);
+int tvq_tied_logits_sample(const float* h, int64_t M, int64_t D, const float* W, int64_t K,
+                           const float* bias, int64_t n, int64_t ldb, const int64_t* s_in,
+                           int64_t mask_id, const float* gumbel, const int64_t* seed_ptr,
+                           uint64_t offset, int64_t* sampled, float* selp, float* logits_out,
+                           void* workspace, tvq_stream_t stream);
 int tvq_maskgit_remask(const float* selp, int64_t B, int64_t n, int64_t k, float temperature,
                        const float* u_gumbel, const int64_t* seed_ptr, uint64_t offset,
                        const int64_t* sampled, int64_t mask_id, int64_t* s_out, uint8_t* masking,

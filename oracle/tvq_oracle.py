@@ -390,34 +390,49 @@ def random_mask_tokens(s, mask_token_id, ratio, rand):
     return s_M, mask
 
 
-def sample_step(logits, s, mask_token_id, t, T, unknown0, temperature, u_cat, u_gumbel):
-    """One iteration of first_pass/second_pass (maskgit.py:302-346) with injected noise.
+def race_sample(logits, s, mask_token_id, gumbel):
+    """The categorical draw of first_pass/second_pass (maskgit.py:307-315) with injected noise.
 
-    Categorical sampling by inverse CDF of softmax(logits) at u_cat (b,n) (double softmax and
-    prefix: the first code whose CDF exceeds u, so a zero-probability code is never
-    drawn, as torch's Categorical); Gumbel noise -log(-log(u_gumbel)).  The mask length is
-    floor(unknown0 * gamma(ratio)) in float32 as in the reference.  Returns the re-masked
-    token set.
-    """
-    probs = F.softmax(logits.double(), dim=-1)
-    cdf = torch.cumsum(probs, dim=-1)
-    sampled = torch.searchsorted(cdf, u_cat.double().unsqueeze(-1) * cdf[..., -1:],
-                                 right=True).squeeze(-1)
-    sampled = sampled.clamp(max=logits.shape[-1] - 1)
+    Categorical(logits).sample() runs torch.multinomial(probs, 1), whose n_sample = 1 path is
+    the exponential race argmax_k p_k / q_k, q_k ~ Exp(1) (ATen Distributions.cpp,
+    multinomial) -- in log form argmax_k l_k + g_k with Gumbel g_k = -log q_k.  The kernels
+    add the injected fp32 g to the fp32 logits, so the keys here are the same fp32 sums and
+    the argmax (first index of the maximum, as torch.argmax) is exact.  Known tokens are
+    kept.  Also returns p(sampled) of the softmax in double (maskgit.py:320-326), +inf for
+    known tokens."""
+    keys = logits.float() + gumbel.float()
+    sampled = keys.argmax(-1)
     unknown = s == mask_token_id
     sampled = torch.where(unknown, sampled, s)
+    sel = torch.gather(F.softmax(logits.double(), dim=-1), -1, sampled.unsqueeze(-1)).squeeze(-1)
+    sel = torch.where(unknown, sel, torch.full_like(sel, float("inf")))
+    return sampled, sel
+
+
+def remask_step(sel, sampled, mask_token_id, t, T, unknown0, temperature, u_gumbel):
+    """mask_by_random_topk (maskgit.py:238-267, 317-346) on given p(sampled): confidence
+    log(p + 1e-5) + temperature (1 - ratio) Gumbel(u_gumbel), the k = floor(unknown0 *
+    gamma(ratio)) (float32, as the reference) lowest re-masked per row."""
     ratio = (t + 1) / T
     mask_ratio = gamma_cosine(ratio)
-    sel = torch.gather(F.softmax(logits, dim=-1), -1, sampled.unsqueeze(-1)).squeeze(-1)
-    sel = torch.where(unknown, sel, torch.full_like(sel, float("inf")))
     mask_len = torch.clip(torch.floor(unknown0.float() * mask_ratio), min=0.0)
     g = -torch.log((-torch.log(u_gumbel.clamp(min=1e-20))).clamp(min=1e-20))
-    conf = torch.log(sel + 1e-5) + temperature * (1.0 - ratio) * g
+    conf = torch.log(sel.float() + 1e-5) + temperature * (1.0 - ratio) * g
     k = int(mask_len.unique().item())
     idx = torch.topk(conf, k=k, dim=-1, largest=False).indices
     masking = torch.zeros_like(conf, dtype=torch.bool)
     masking.scatter_(1, idx, True)
     return torch.where(masking, torch.full_like(sampled, mask_token_id), sampled)
+
+
+def sample_step(logits, s, mask_token_id, t, T, unknown0, temperature, gumbel, u_gumbel):
+    """One iteration of first_pass/second_pass (maskgit.py:302-346) with injected noise:
+    race_sample, then remask_step on the fp32 softmax p(sampled) the reference gathers."""
+    sampled, _ = race_sample(logits, s, mask_token_id, gumbel)
+    unknown = s == mask_token_id
+    sel = torch.gather(F.softmax(logits.float(), dim=-1), -1, sampled.unsqueeze(-1)).squeeze(-1)
+    sel = torch.where(unknown, sel, torch.full_like(sel, float("inf")))
+    return remask_step(sel, sampled, mask_token_id, t, T, unknown0, temperature, u_gumbel)
 
 
 # ----------------------------------------------------------------------------

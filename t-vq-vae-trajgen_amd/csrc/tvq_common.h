@@ -174,4 +174,25 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t ctr) {
   return (hash_u32(seed * 0xD1B54A32D192ED03ull + ctr) >> 8) * (1.0f / 16777216.0f);
 }
 
+// Categorical draws by exponential race -- torch.multinomial's own n_sample = 1 algorithm
+// (argmax_k p_k / q_k, q_k ~ Exp(1)), which Categorical.sample calls -- in log form:
+// argmax_k l_k + g_k with g_k = -log q_k (Gumbel), ties to the lowest k.  One draw per
+// (token, code), so the noise is a cheap 32-bit counter hash keyed by the call's stream
+// key; u = (2j + 1) 2^-24 is exact in fp32 and strictly inside (0, 1), and q is clamped
+// away from 0, so g is finite: a code whose fp32 softmax probability is 0 (l_k < max - 103)
+// can never win, g being within [-2.9, 17.4].
+__device__ __forceinline__ uint32_t race_key(uint64_t seed) {
+  return (uint32_t)(seed ^ (seed >> 32));
+}
+__device__ __forceinline__ float race_gumbel(uint32_t key, uint32_t ctr) {
+  uint32_t x = ctr * 0x9E3779B9u + key;
+  x ^= x >> 16;
+  x *= 0x21F0AAADu;
+  x ^= x >> 15;
+  x *= 0x735A2D97u;
+  x ^= x >> 15;
+  const float u = (float)((x >> 9) * 2u + 1u) * (1.0f / 16777216.0f);
+  return -__logf(fmaxf(-__logf(u), 2.9802322e-08f));
+}
+
 }  // namespace tvq

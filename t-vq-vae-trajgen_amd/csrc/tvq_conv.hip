@@ -25,6 +25,7 @@
 
 #include <stdlib.h>
 
+#include <map>
 #include <vector>
 
 namespace tvq {
@@ -2293,17 +2294,24 @@ __global__ void conv_pack_weight_kernel(const float* __restrict__ w, int N, int 
 // next scope's begin every recorded entry is repacked from the current weights by a few
 // batched launches, and the convs of the scope read their slot without packing again.
 // The scope must not contain weight updates (a trainer opens it around forward+backward,
-// the optimizer step is outside).  Entries belong to one cache id and are dropped when
-// another id begins, so a freed model's weights are never read.
+// the optimizer step is outside).  Entries belong to one cache id (one arena); several ids
+// keep their entries side by side, so two step segments captured as separate graphs (the
+// DP trainer's stage1 and stage2) each repack only their own weights.  An id's entries are
+// dropped by tvq_conv_packcache_release (its owner is freed) or when the id begins with
+// another arena.
 struct PackEntry {
   const float* src;
   int N, C, KK;
   int64_t wsn, wsc, off;
 };
-static std::vector<PackEntry> g_pc;
-static int64_t g_pc_id = -1, g_pc_cap = 0, g_pc_used = 0;
-static float* g_pc_arena = nullptr;
-static bool g_pc_active = false;
+struct PackCacheState {
+  std::vector<PackEntry> entries;
+  float* arena = nullptr;
+  int64_t cap = 0, used = 0;
+};
+static std::map<int64_t, PackCacheState> g_pcs;
+static PackCacheState* g_pc_cur = nullptr;  // the open scope's cache (null: no scope)
+static int64_t g_pc_last = -1;              // id of the last scope (entries query)
 // deferred weight-gradient split sums (see wgrad_finish)
 static std::vector<RrJob> g_rd;
 static bool g_rd_on = false, g_rd_paused = false;
@@ -2353,19 +2361,19 @@ static const float* pack_weight(const float* wt, ConvGeom& g, int KK, float* ws,
   const int64_t total = (int64_t)g.N * g.C * KK;
   float* dst = ws;
   bool need = true;
-  if (g_pc_active) {
-    for (const PackEntry& p : g_pc)
+  if (PackCacheState* pc = g_pc_cur) {
+    for (const PackEntry& p : pc->entries)
       if (p.src == wt && p.N == g.N && p.C == g.C && p.KK == KK && p.wsn == g.wsn &&
           p.wsc == g.wsc) {
-        dst = g_pc_arena + p.off;
+        dst = pc->arena + p.off;
         need = false;  // repacked at this scope's begin
         break;
       }
     const int64_t slot = (total + 63) / 64 * 64;
-    if (need && g_pc_used + slot <= g_pc_cap) {
-      g_pc.push_back({wt, g.N, g.C, KK, g.wsn, g.wsc, g_pc_used});
-      dst = g_pc_arena + g_pc_used;
-      g_pc_used += slot;
+    if (need && pc->used + slot <= pc->cap) {
+      pc->entries.push_back({wt, g.N, g.C, KK, g.wsn, g.wsc, pc->used});
+      dst = pc->arena + pc->used;
+      pc->used += slot;
     }
   }
   if (need) pack_launch(wt, g.N, g.C, KK, g.wsn, g.wsc, dst, st);
@@ -2966,39 +2974,51 @@ static Epi make_epi(const float* bias, const float* residual, float drop_p,
 extern "C" int tvq_conv_packcache_begin(int64_t id, float* arena, int64_t cap_floats,
                                         tvq_stream_t stream) {
   TVQ_CHECK_ARG(id >= 0 && arena && cap_floats > 0, "tvq_conv_packcache_begin: bad arguments");
-  TVQ_CHECK_ARG(!g_pc_active, "tvq_conv_packcache_begin: a scope is already open");
-  if (id != g_pc_id || arena != g_pc_arena || cap_floats != g_pc_cap) {
-    g_pc.clear();
-    g_pc_id = id;
-    g_pc_arena = arena;
-    g_pc_cap = cap_floats;
-    g_pc_used = 0;
+  TVQ_CHECK_ARG(!g_pc_cur, "tvq_conv_packcache_begin: a scope is already open");
+  PackCacheState& pc = g_pcs[id];
+  if (arena != pc.arena || cap_floats != pc.cap) {
+    pc.entries.clear();
+    pc.arena = arena;
+    pc.cap = cap_floats;
+    pc.used = 0;
   }
   hipStream_t st = (hipStream_t)stream;
-  for (size_t i0 = 0; i0 < g_pc.size(); i0 += PACK_BATCH) {
+  for (size_t i0 = 0; i0 < pc.entries.size(); i0 += PACK_BATCH) {
     PackBatch b;
     int n = 0;
     int64_t most = 0;
-    for (size_t i = i0; i < g_pc.size() && n < PACK_BATCH; ++i, ++n) {
-      const PackEntry& p = g_pc[i];
+    for (size_t i = i0; i < pc.entries.size() && n < PACK_BATCH; ++i, ++n) {
+      const PackEntry& p = pc.entries[i];
       b.src[n] = p.src; b.wsn[n] = p.wsn; b.wsc[n] = p.wsc; b.off[n] = p.off;
       b.N[n] = p.N; b.C[n] = p.C; b.KK[n] = p.KK;
       const int64_t t = (int64_t)p.N * p.C * p.KK;
       most = t > most ? t : most;
     }
     const int bx = (int)((most + 255) / 256 < 512 ? (most + 255) / 256 : 512);
-    hipLaunchKernelGGL(conv_pack_multi_kernel, dim3(bx, n), dim3(256), 0, st, b, g_pc_arena);
+    hipLaunchKernelGGL(conv_pack_multi_kernel, dim3(bx, n), dim3(256), 0, st, b, pc.arena);
   }
-  g_pc_active = true;
+  g_pc_cur = &pc;
+  g_pc_last = id;
   return launch_status("tvq_conv_packcache_begin");
 }
 
 extern "C" int tvq_conv_packcache_end(void) {
-  g_pc_active = false;
+  g_pc_cur = nullptr;
   return TVQ_OK;
 }
 
-extern "C" int64_t tvq_conv_packcache_entries(void) { return (int64_t)g_pc.size(); }
+extern "C" int tvq_conv_packcache_release(int64_t id) {
+  auto it = g_pcs.find(id);
+  if (it == g_pcs.end()) return TVQ_OK;
+  TVQ_CHECK_ARG(g_pc_cur != &it->second, "tvq_conv_packcache_release: the cache's scope is open");
+  g_pcs.erase(it);
+  return TVQ_OK;
+}
+
+extern "C" int64_t tvq_conv_packcache_entries(void) {
+  auto it = g_pcs.find(g_pc_last);
+  return it == g_pcs.end() ? 0 : (int64_t)it->second.entries.size();
+}
 
 extern "C" int tvq_conv_wgrad_defer_begin(void) {
   TVQ_CHECK_ARG(!g_rd_on, "tvq_conv_wgrad_defer_begin: a scope is already open");

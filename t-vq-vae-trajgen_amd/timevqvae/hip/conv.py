@@ -101,6 +101,12 @@ class PackCache:
         finally:
             call("tvq_conv_packcache_end")
 
+    def __del__(self):
+        try:
+            call("tvq_conv_packcache_release", self.id)
+        except Exception:  # interpreter shutdown: the library may be gone
+            pass
+
     @staticmethod
     def entries():
         return value("tvq_conv_packcache_entries")

@@ -83,3 +83,93 @@ class StepGraph:
             if btw is not None:
                 btw()
         return self.outputs
+
+
+class BranchStepGraph:
+    """A step whose independent parts run as separate graphs on their own streams, each
+    followed by its own eager exchange, then a final graph:
+
+        before(); pre()                                  eager, current stream
+        branch i: graph_i ; after_i()                    stream S_i (waits for pre)
+        final graph                                      current stream (waits for every S_i)
+
+    The DP trainer's form (bench.JointTrainer at world > 1): stage1's and stage2's
+    forward+backward are the branches, each branch's all-reduces start as soon as its own
+    backward ends -- while the other branch still computes -- and the optimizers are the
+    final graph.  Each graph has its own memory pool: branch graphs replay concurrently, so
+    their allocations must not alias (graphs sharing a pool must replay in capture order).
+    """
+
+    def __init__(self, pre, branches, afters, final, warmup=2, before=None):
+        self.pre, self.branches, self.afters = pre, list(branches), list(afters)
+        self.final, self.before, self.warmup = final, before, warmup
+        self.graphs = self.final_graph = None
+        self.outputs = None
+        self._streams = None
+
+    def _eager(self):
+        if self.before is not None:
+            self.before()
+        self.pre()
+        outs = []
+        for br, aft in zip(self.branches, self.afters):
+            outs.append(br())
+            streams.join(backward_done=True)
+            if aft is not None:
+                aft()
+        self.final()
+        streams.join(backward_done=True)
+        return outs
+
+    def capture(self):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side), rng.device_decisions():
+            for _ in range(self.warmup):
+                self._eager()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graphs, self.outputs = [], []
+        call("tvq_counter_capture", 1)
+        gc_on = gc.isenabled()
+        gc.collect()
+        gc.disable()
+        try:
+            with rng.device_decisions():
+                # pre() is not captured (it runs eagerly before every replay); the branches
+                # restore any host state it sets (bench: rng.restart_calls())
+                for br in self.branches:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle()):
+                        out = br()
+                        streams.join(backward_done=True)
+                    self.graphs.append(g)
+                    self.outputs.append(out)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle()):
+                    self.final()
+                    streams.join(backward_done=True)
+                self.final_graph = g
+        finally:
+            call("tvq_counter_capture", 0)
+            if gc_on:
+                gc.enable()
+        torch.cuda.synchronize()
+        self._streams = [torch.cuda.Stream() for _ in self.branches]
+        return self
+
+    def replay(self):
+        if self.before is not None:
+            self.before()
+        cur = torch.cuda.current_stream()
+        self.pre()
+        for g, aft, st in zip(self.graphs, self.afters, self._streams):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                g.replay()
+                if aft is not None:
+                    aft()
+        for st in self._streams:
+            cur.wait_stream(st)
+        self.final_graph.replay()
+        return self.outputs

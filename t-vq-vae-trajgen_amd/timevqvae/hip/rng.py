@@ -52,6 +52,12 @@ def manual_seed(seed: int):
         t.fill_(int(seed))
 
 
+def restart_calls():
+    """Restart the per-step call index only (host state; advance() does it too): for a step
+    captured in several graphs whose seed advance runs outside them."""
+    _calls[0] = 0
+
+
 def advance(device):
     """Advance the device seed (call once per training step; capturable) and restart the
     per-step call index."""

@@ -7,7 +7,7 @@ import numpy as np
 import torch
 
 from . import rng
-from ._native import call, ptr, stream_ptr
+from ._native import call, ptr, stream_ptr, value
 
 
 def mask_len(unknown0: int, mask_ratio: float) -> int:
@@ -15,8 +15,12 @@ def mask_len(unknown0: int, mask_ratio: float) -> int:
     return max(0, int(np.floor(np.float32(unknown0) * np.float32(mask_ratio))))
 
 
-def maskgit_sample(logits, s, mask_id, u_cat=None, site=0):
-    """(sampled ids with known tokens kept, p(sampled) with +inf for known tokens)."""
+def maskgit_sample(logits, s, mask_id, gumbel=None, site=0):
+    """(sampled ids with known tokens kept, p(sampled) with +inf for known tokens).
+
+    The draw is Categorical(logits).sample() as torch runs it -- torch.multinomial's
+    n_sample = 1 exponential race, argmax_k l_k + Gumbel_k (maskgit.py:307-315) -- with the
+    Gumbel noise from the device seed's counter hash, or `gumbel` (B, n, K) when given."""
     B, n, K = logits.shape
     sb, sn, sk = logits.stride()
     if sk != 1:
@@ -24,12 +28,47 @@ def maskgit_sample(logits, s, mask_id, u_cat=None, site=0):
     s = s.contiguous()
     sampled = torch.empty_like(s)
     selp = torch.empty((B, n), device=logits.device, dtype=torch.float32)
-    seed = rng.seed_tensor(logits.device) if u_cat is None else None
-    off = rng.call_offset(site) if u_cat is None else 0
+    seed = rng.seed_tensor(logits.device) if gumbel is None else None
+    off = rng.call_offset(site) if gumbel is None else 0
     call("tvq_maskgit_sample", ptr(logits), sb, sn, B, n, K, ptr(s), int(mask_id),
-         ptr(u_cat.contiguous() if u_cat is not None else None), ptr(seed), off, ptr(sampled),
+         ptr(gumbel.contiguous() if gumbel is not None else None), ptr(seed), off, ptr(sampled),
          ptr(selp), stream_ptr())
     return sampled, selp
+
+
+_tls_ws = {}
+
+
+def tied_logits_sample(h, W, bias, K, s, mask_id, gumbel=None, site=0, want_logits=False):
+    """maskgit_sample(h @ W[:K]^T + bias[:, :K], s, mask_id) in one pass: the tied logits of
+    the prior's head (bidirectional_transformer.py:186-191) computed on MFMA and consumed by
+    the race in registers, never written to memory (include/tvq.h tvq_tied_logits_sample).
+    h (B, n, D) with D 64 or 128; bias (n, ldb >= K).  want_logits: also return the logits
+    the draw used (tests)."""
+    B, n, D = h.shape
+    M = B * n
+    h2 = h.reshape(M, D).contiguous()
+    s = s.contiguous()
+    dev = h.device
+    nb = bias.shape[0]
+    key = (dev, K, D, nb)
+    ws = _tls_ws.get(key)
+    if ws is None:
+        nbytes = value("tvq_tied_logits_sample_workspace", K, D, nb)
+        if nbytes < 0:
+            raise ValueError("tied_logits_sample: unsupported shape")
+        ws = torch.empty((nbytes + 15) // 16 * 4, device=dev, dtype=torch.float32)
+        _tls_ws[key] = ws
+    sampled = torch.empty_like(s)
+    selp = torch.empty((B, n), device=dev, dtype=torch.float32)
+    logits = torch.empty((B, n, K), device=dev, dtype=torch.float32) if want_logits else None
+    seed = rng.seed_tensor(dev) if gumbel is None else None
+    off = rng.call_offset(site) if gumbel is None else 0
+    call("tvq_tied_logits_sample", ptr(h2), M, D, ptr(W.contiguous()), K, ptr(bias), nb,
+         bias.stride(0), ptr(s), int(mask_id),
+         ptr(gumbel.contiguous() if gumbel is not None else None), ptr(seed), off,
+         ptr(sampled), ptr(selp), ptr(logits), ptr(ws), stream_ptr())
+    return (sampled, selp, logits) if want_logits else (sampled, selp)
 
 
 def maskgit_remask(selp, k, temperature, sampled=None, mask_id=0, u_gumbel=None, site=0,

@@ -546,10 +546,7 @@ def prior_lf_eval_supported(tf, s):
                p.data_ptr() % 16 == 0 for p in tf.parameters())
 
 
-def prior_lf_eval(tf, s, class_idx=None):
-    """logits (B, n, K) of the LF prior in eval mode as ONE launch (csrc/tvq_prior_eval.hip):
-    the same function as forward_lf's unfused path (embedding, encoder, pred_head, tied
-    logits).  class_idx: (B,) / (B, 1) int64 or None (the null class)."""
+def _prior_lf_args(tf, s, class_idx):
     import ctypes
     enc = tf.blocks.attn_layers
     w = [tf.tok_emb_l.weight, tf.pos_emb.weight, tf.class_condition_emb.weight,
@@ -563,18 +560,44 @@ def prior_lf_eval(tf, s, class_idx=None):
           tf.pred_head[0].bias, tf.pred_head[2].weight, tf.pred_head[2].bias, tf.bias]
     arr = (ctypes.c_void_p * len(w))(*[ptr(t) for t in w])
     s = s if s.stride(1) == 1 else s.contiguous()
-    B, n = s.shape
-    K = tf.codebook_size
-    cls = None
-    if class_idx is not None:
-        cls = class_idx.reshape(-1).long().contiguous()
+    cls = class_idx.reshape(-1).long().contiguous() if class_idx is not None else None
     depth = len(enc.layers) // 2
-    logits = torch.empty((B, n, K), device=s.device, dtype=torch.float32)
+    K = tf.codebook_size
     ws = torch.empty(value("tvq_prior_lf_eval_workspace", depth, K), device=s.device,
                      dtype=torch.uint8)
+    return s, cls, arr, depth, K, ws
+
+
+def prior_lf_eval(tf, s, class_idx=None):
+    """logits (B, n, K) of the LF prior in eval mode as ONE launch (csrc/tvq_prior_eval.hip):
+    the same function as forward_lf's unfused path (embedding, encoder, pred_head, tied
+    logits).  class_idx: (B,) / (B, 1) int64 or None (the null class)."""
+    s, cls, arr, depth, K, ws = _prior_lf_args(tf, s, class_idx)
+    B, n = s.shape
+    logits = torch.empty((B, n, K), device=s.device, dtype=torch.float32)
     call("tvq_prior_lf_eval", ptr(s), B, n, s.stride(0), ptr(cls), tf.n_classes, 128, arr,
          depth, K, float(tf.pred_head[2].eps), ptr(logits), ptr(ws), stream_ptr())
     return logits
+
+
+def prior_lf_eval_sample(tf, s, class_idx, mask_id, gumbel=None, site=0, want_logits=False):
+    """prior_lf_eval + hip.sample.maskgit_sample in ONE launch: the tied logits are drawn
+    from by the race in registers and never written (tvq_prior_lf_eval_sample).  Returns
+    (sampled, p(sampled)[, logits])."""
+    from . import rng
+    s, cls, arr, depth, K, ws = _prior_lf_args(tf, s, class_idx)
+    B, n = s.shape
+    dev = s.device
+    sampled = torch.empty((B, n), device=dev, dtype=torch.int64)
+    selp = torch.empty((B, n), device=dev, dtype=torch.float32)
+    logits = torch.empty((B, n, K), device=dev, dtype=torch.float32) if want_logits else None
+    seed = rng.seed_tensor(dev) if gumbel is None else None
+    off = rng.call_offset(site) if gumbel is None else 0
+    call("tvq_prior_lf_eval_sample", ptr(s), B, n, s.stride(0), ptr(cls), tf.n_classes, 128, arr,
+         depth, K, float(tf.pred_head[2].eps), int(mask_id),
+         ptr(gumbel.contiguous() if gumbel is not None else None), ptr(seed), off,
+         ptr(sampled), ptr(selp), ptr(logits), ptr(ws), stream_ptr())
+    return (sampled, selp, logits) if want_logits else (sampled, selp)
 
 
 class _DropFirst(torch.autograd.Function):

@@ -17,6 +17,7 @@ FF: Linear(+b) -> GELU -> Dropout -> Linear(+b).  PARITY UNPINNED: no reference
 output exists for this part; project_in/out are bias-free
 as in x-transformers >= 1.2x.
 """
+import os
 import random
 from typing import Union
 
@@ -28,9 +29,15 @@ from ..hip.conv import _immediate, _keep, conv2d
 from ..hip.linear import gemm, linear
 from ..hip.norm import bn_snake
 from ..hip.xf import (batch_colsum, drop_first_token, embed_assemble, embedding, gelu,
-                      layer_norm, linear_act, prior_lf_eval, prior_lf_eval_supported,
-                      qkv_attention, rmsnorm, rmsnorm_res, upsample_nearest_t)
+                      layer_norm, linear_act, prior_lf_eval, prior_lf_eval_sample,
+                      prior_lf_eval_supported, qkv_attention, rmsnorm, rmsnorm_res,
+                      upsample_nearest_t)
 from ..hip._native import call, grad_sink, ptr, stream_ptr, value
+from ..hip.sample import maskgit_sample, tied_logits_sample
+
+# the HF prior's sampling step straight from its head (no logits in memory); 0: form the
+# logits and sample them (A/B and diagnosis)
+FUSED_SAMPLE = os.environ.get("TVQ_FUSED_SAMPLE", "1") != "0"
 
 
 # ------------------------------------------------------------------ x-transformers tree
@@ -432,6 +439,28 @@ class BidirectionalTransformer(nn.Module):
         embed = embed_assemble(cls_emb, tl, th, self.pos_emb.weight, n)
         embed = self.blocks(embed)
         return self._head(drop_first_token(embed))
+
+    def sample(self, s_M_l, s_M_h=None, class_condition=None, mask_id=None, gumbel=None,
+               site=0, want_logits=False):
+        """One categorical draw per token of this prior's logits (maskgit.py:302-326): the
+        sampled codes (known tokens -- the ones != mask_id of the band being decoded -- kept)
+        and p(sampled) (+inf for known tokens).  The HF prior in eval mode draws straight
+        from its head (hip.sample.tied_logits_sample: the logits never reach memory);
+        otherwise the logits are formed and hip.sample.maskgit_sample draws from them.
+        want_logits: also return the logits (tests)."""
+        s = s_M_l if self.kind == "lf" else s_M_h
+        if self.kind == "lf" and FUSED_SAMPLE and prior_lf_eval_supported(self, s_M_l):
+            return prior_lf_eval_sample(self, s_M_l, class_condition, mask_id, gumbel=gumbel,
+                                        site=site, want_logits=want_logits)
+        if (self.kind == "hf" and not self.training and FUSED_SAMPLE
+                and self.tok_emb_h.weight.shape[1] in (64, 128)):
+            return tied_logits_sample(self._embed_hf(s_M_l, s_M_h, class_condition),
+                                      self.tok_emb_h.weight, self.bias, self.codebook_size, s,
+                                      mask_id, gumbel=gumbel, site=site, want_logits=want_logits)
+        logits = self(s_M_l, s_M_h, class_condition) if self.kind == "hf" else \
+            self(s_M_l, class_condition=class_condition)
+        out = maskgit_sample(logits, s, mask_id, gumbel=gumbel, site=site)
+        return out + (logits,) if want_logits else out
 
     def masked_ce(self, target, keep, s_M_l, s_M_h=None, class_condition=None):
         """F.cross_entropy(self(...)[~keep], target[~keep]) (maskgit.py:183-191) with the tied

@@ -208,14 +208,28 @@ class MaskGIT(nn.Module):
         return maskgit_remask(probs.float(), k, temperature, site=self._site_sample,
                               want_masking=True)
 
-    def _decode_pass(self, transformer_call, s, mask_id, T, temperature, unknown0, gamma):
-        """One of first_pass / second_pass: T steps of (logits -> sample -> re-mask)."""
+    def sample_tokens(self, transformer, class_condition, mask_id, *s_in, gumbel=None,
+                      want_logits=False):
+        """The categorical draw of one decoding step (maskgit.py:302-326): masked_prediction's
+        logits -> Categorical(logits).sample() -> (sampled with known tokens kept,
+        p(sampled)).  Without guidance (cfg 1 or no class) the prior draws straight from its
+        head (BidirectionalTransformer.sample); with guidance the two forwards' logits are
+        mixed first."""
+        if class_condition is None or self.cfg_scale == 1.0:
+            return transformer.sample(*s_in, class_condition=class_condition, mask_id=mask_id,
+                                      gumbel=gumbel, site=self._site_sample,
+                                      want_logits=want_logits)
+        logits = self.masked_prediction(transformer, class_condition, *s_in)
+        out = maskgit_sample(logits, s_in[-1], mask_id, gumbel=gumbel, site=self._site_sample)
+        return out + (logits,) if want_logits else out
+
+    def _decode_pass(self, sample_call, s, mask_id, T, temperature, unknown0, gamma):
+        """One of first_pass / second_pass: T steps of (draw -> re-mask)."""
         n0 = int(unknown0.max().item()) if torch.is_tensor(unknown0) else int(unknown0)
         for t in range(T):
-            logits = transformer_call(s)
             ratio = 1.0 * (t + 1) / T
             k = mask_len(n0, gamma(ratio))
-            sampled, selp = maskgit_sample(logits, s, mask_id, site=self._site_sample)
+            sampled, selp = sample_call(s)
             s = maskgit_remask(selp, k, temperature * (1.0 - ratio), sampled, mask_id,
                                site=self._site_sample)
         return s
@@ -223,17 +237,19 @@ class MaskGIT(nn.Module):
     def first_pass(self, s_l: torch.Tensor, unknown_number_in_the_beginning_l,
                    class_condition: Union[torch.Tensor, None], gamma: Callable, device):
         """maskgit.py:294-355."""
+        mask_id = self.mask_token_ids["lf"]
         return self._decode_pass(
-            lambda s: self.masked_prediction(self.transformer_l, class_condition, s), s_l,
-            self.mask_token_ids["lf"], self.T["lf"], self.choice_temperature_l,
+            lambda s: self.sample_tokens(self.transformer_l, class_condition, mask_id, s), s_l,
+            mask_id, self.T["lf"], self.choice_temperature_l,
             unknown_number_in_the_beginning_l, gamma)
 
     def second_pass(self, s_l: torch.Tensor, s_h: torch.Tensor, unknown_number_in_the_beginning_h,
                     class_condition: Union[torch.Tensor, None], gamma: Callable, device):
         """maskgit.py:357-411."""
+        mask_id = self.mask_token_ids["hf"]
         return self._decode_pass(
-            lambda s: self.masked_prediction(self.transformer_h, class_condition, s_l, s), s_h,
-            self.mask_token_ids["hf"], self.T["hf"], self.choice_temperature_h,
+            lambda s: self.sample_tokens(self.transformer_h, class_condition, mask_id, s_l, s),
+            s_h, mask_id, self.T["hf"], self.choice_temperature_h,
             unknown_number_in_the_beginning_h, gamma)
 
     @torch.no_grad()

@@ -81,8 +81,13 @@ class GraphedSampler:
         if fidelity_enhancer is not None:
             fidelity_enhancer.eval()
 
+        from ..hip.conv import PackCache
+        # the convs' packed weights: repacked by a few batched launches at the start of each
+        # replay instead of one pack launch per conv (the weights are fixed within a batch)
+        self.packs = PackCache(self.device)
+
         def batch():
-            with torch.no_grad():
+            with torch.no_grad(), self.packs.scope():
                 rng.advance(self.device)
                 s_l, s_h = maskgit.iterative_decoding(num=num, device=self.device,
                                                       class_index=class_index)

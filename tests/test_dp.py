@@ -1,7 +1,10 @@
 """Data-parallel logic on CPU (gloo, world_size 2): the pieces of the multi-GPU step that
 are not kernels -- the flat-gradient all-reduce/average of bench.JointTrainer and the
 deferred sync_codebook reduction of hip.vq.CodebookUpdate (the reference's
-sync_codebook all-reduce of cluster sizes and embedding sums, vq.py:229,234)."""
+sync_codebook all-reduce of cluster sizes and embedding sums, vq.py:229,234).  The DP
+step exchanges each stage's gradients and BatchNorm statistics separately (right after
+that stage's backward); that split exchange is checked bitwise equal to one flat
+exchange of everything."""
 import os
 import sys
 
@@ -55,15 +58,23 @@ def _worker(rank, world, port, q):
         # a view of it), averaged over the replicas -> every state_dict tensor bitwise
         # equal across ranks (DDP broadcast_buffers semantics)
         mods = [s1, s2.maskgit.transformer_l, s2.maskgit.transformer_h]
-        tr.bn_flat = flatten_bn_buffers(mods)
+        # one flat buffer per stage, as JointTrainer holds them
+        tr.bn_flat = [flatten_bn_buffers([s1]), flatten_bn_buffers(mods[1:])]
         bns = batchnorm_modules(mods)
         with torch.no_grad():  # per-rank updates, as each replica's forward makes them
             for b in bns:
                 b.running_mean.add_(torch.randn(b.running_mean.shape, generator=g))
                 b.running_var.mul_(1 + torch.rand(b.running_var.shape, generator=g))
-        views_ok = all(b.running_mean.data_ptr() >= tr.bn_flat.data_ptr() for b in bns)
+        views_ok = all(any(f.data_ptr() <= b.running_mean.data_ptr() < f.data_ptr() +
+                           4 * f.numel() for f in tr.bn_flat) for b in bns)
         pre = torch.cat([torch.cat([b.running_mean, b.running_var]) for b in bns])
-        tr._sync_buffers()
+        # the DP form's split exchange (each stage's buffer right after its backward) is
+        # bitwise equal to one flat exchange of everything
+        flat_once = torch.cat([f.clone() for f in tr.bn_flat])
+        ReplicaSync(world).buffers(flat_once)
+        tr._sync_buffers((0,))
+        tr._sync_buffers((1,))
+        ok_split = torch.equal(torch.cat(tr.bn_flat), flat_once)
         sd = {k: v.clone() for m in (s1, s2) for k, v in m.state_dict().items()}
         gathered = [None] * world
         dist.all_gather_object(gathered, sd)
@@ -72,8 +83,23 @@ def _worker(rank, world, port, q):
         pres = [torch.empty_like(pre) for _ in range(world)]
         dist.all_gather(pres, pre)
         post = torch.cat([torch.cat([b.running_mean, b.running_var]) for b in bns])
-        ok_bn = views_ok and ok_sd and torch.allclose(post, sum(pres) / world, rtol=1e-6,
-                                                      atol=1e-6)
+        ok_bn = views_ok and ok_sd and ok_split and torch.allclose(post, sum(pres) / world,
+                                                                   rtol=1e-6, atol=1e-6)
+        # the same for the flat gradients: stage1's and stage2's buffers exchanged
+        # separately == one exchange of their concatenation, bitwise
+        g1 = torch.randn(nparam, generator=g)
+        g2 = torch.randn(sum(p.numel() for p in s2.parameters() if p.requires_grad),
+                         generator=g)
+
+        class O:
+            def __init__(self, t):
+                self.flat_grad, self.has_gates = t, False
+        both_once = O(torch.cat([g1, g2]))
+        o1, o2 = O(g1.clone()), O(g2.clone())
+        tr._allreduce(both_once)
+        tr._allreduce(o1)
+        tr._allreduce(o2)
+        ok_bn = ok_bn and torch.equal(torch.cat([o1.flat_grad, o2.flat_grad]), both_once.flat_grad)
         ok_grad = ok_grad and ok_bn
 
         # sync_codebook statistics: summed over ranks before the EMA

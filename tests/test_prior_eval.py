@@ -72,6 +72,47 @@ def test_fused_prior_matches_unfused_and_oracle(depth, K, n, B, cond, cuda):
     assert float(clear.float().mean()) > 0.99
 
 
+@pytest.mark.parametrize("depth,K,n,B,cond", [(4, 512, 24, 64, False), (2, 100, 7, 9, True)])
+def test_fused_prior_draw(depth, K, n, B, cond, cuda):
+    """tvq_prior_lf_eval_sample (the decoding step's draw in the prior's launch): its logits
+    equal the logits-only launch's within 1e-6, its draw is exactly the oracle race on those
+    logits with the injected Gumbel noise, p(sampled) within 2e-6 of the double softmax,
+    known tokens kept; with the device noise it draws what maskgit_sample draws from the
+    same logits at the same stream offset."""
+    from timevqvae.hip import rng, xf
+    from timevqvae.hip._native import plan_trace
+    from timevqvae.hip.sample import maskgit_sample
+    m, sd = _prior(cuda, depth, K, n)
+    gen = torch.Generator().manual_seed(5)
+    s = torch.randint(0, K, (B, n), generator=gen)
+    s[torch.rand(B, n, generator=gen) < 0.6] = K  # mask id K: drawn; the rest kept
+    y = torch.randint(0, 5, (B, 1), generator=gen) if cond else None
+    sg, yg = s.to(cuda), (y.to(cuda) if cond else None)
+    u = torch.rand(B, n, K, generator=gen).clamp(1e-7, 1 - 1e-7)
+    gum = -torch.log(-torch.log(u))
+    with torch.no_grad(), plan_trace() as tr:
+        sampled, selp, lg = xf.prior_lf_eval_sample(m, sg, yg, K, gumbel=gum.to(cuda),
+                                                    want_logits=True)
+        plain = xf.prior_lf_eval(m, sg, yg)
+        torch.cuda.synchronize()
+    assert tr.has("prior_lf_eval_sample")
+    assert float((lg - plain).abs().max()) <= 1e-6 * float(plain.abs().max())
+    want, sel = O.race_sample(lg.cpu(), s, K, gum)
+    assert torch.equal(sampled.cpu(), want)
+    unk = s == K
+    assert torch.isinf(selp.cpu()[~unk]).all()
+    assert float(((selp.cpu()[unk].double() - sel[unk]).abs() / sel[unk]).max()) < 2e-6
+    with torch.no_grad():
+        rng.manual_seed(8)
+        a, pa, lg2 = xf.prior_lf_eval_sample(m, sg, yg, K, site=3, want_logits=True)
+        rng.manual_seed(8)
+        b, pb = maskgit_sample(lg2, sg, K, site=3)
+        torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    fin = torch.isfinite(pb)
+    assert float(((pa[fin] - pb[fin]).abs() / pb[fin]).max()) < 2e-6
+
+
 def test_fused_prior_declines_unaligned_weights(cuda):
     """tvq_prior_lf_eval reads weights with 16-byte loads: a parameter whose storage is not
     16-byte aligned (e.g. packed after an odd-sized one in a flat buffer) must send the

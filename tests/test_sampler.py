@@ -1,9 +1,12 @@
 """MaskGIT sampling on the HIP path vs the oracle.
 
-The reference draws with torch's RNG (Categorical.sample, uniform_ Gumbel noise), which a
-GPU kernel cannot reproduce; the oracle's `sample_step` restates one decoding step of
-first_pass / second_pass (maskgit.py:294-411) with the noise injected, and the kernels are
-run on the same injected noise.  Parity: sampled codes and re-masked token sets exact.
+The reference draws with torch's RNG (Categorical.sample -> multinomial's exponential race,
+uniform_ Gumbel noise), which a GPU kernel cannot reproduce; the oracle restates one decoding
+step of first_pass / second_pass (maskgit.py:294-411) with the noise injected
+(race_sample: argmax of logits + Gumbel; remask_step), and the kernels are run on the same
+injected noise.  Parity: sampled codes and re-masked token sets exact; p(sampled) within
+2e-6 relative of the double softmax.  The device noise itself is checked for the
+distribution it draws (frequencies) and for never drawing a 0-probability code.
 """
 import os
 import sys
@@ -16,6 +19,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 pytestmark = pytest.mark.gpu
+
+
+def _gumbel(shape, g):
+    u = torch.rand(shape, generator=g).clamp(1e-7, 1 - 1e-7)
+    return -torch.log(-torch.log(u))
 
 
 @pytest.mark.parametrize("B,n,K,t,T,temp", [(16, 96, 512, 0, 1, 4.0), (32, 24, 512, 3, 10, 10.0),
@@ -31,54 +39,121 @@ def test_sample_step_vs_oracle(B, n, K, t, T, temp, cuda):
     for i in range(B):  # the first n_known positions of a random order are already decoded
         perm = torch.randperm(n, generator=g)
         s[i, perm[n_known:]] = mask_id
-    u_cat = torch.rand(B, n, generator=g)
+    gum = _gumbel((B, n, K), g)
     u_g = torch.rand(B, n, generator=g)
-    ref = O.sample_step(logits, s, mask_id, t, T, torch.full((B,), n), temp, u_cat, u_g)
 
     ratio = (t + 1) / T
-    sampled, selp = maskgit_sample(logits.to(cuda), s.to(cuda), mask_id, u_cat=u_cat.to(cuda))
+    sampled, selp = maskgit_sample(logits.to(cuda), s.to(cuda), mask_id, gumbel=gum.to(cuda))
     k = mask_len(n, O.gamma_cosine(ratio))
     out = maskgit_remask(selp, k, temp * (1.0 - ratio), sampled, mask_id, u_gumbel=u_g.to(cuda))
     torch.cuda.synchronize()
-    # categorical draw: exact vs the double-precision inverse CDF
-    probs = torch.softmax(logits.double(), -1)
-    cdf = torch.cumsum(probs, -1)
-    want = torch.searchsorted(cdf, u_cat.double().unsqueeze(-1) * cdf[..., -1:],
-                              right=True).squeeze(-1)
-    want = torch.where(s == mask_id, want.clamp(max=K - 1), s)
+    # the race draw: exact (same fp32 keys, first index of the maximum)
+    want, sel = O.race_sample(logits, s, mask_id, gum)
     assert torch.equal(sampled.cpu(), want)
+    # p(sampled): the fp32 softmax within 2e-6 relative of the double one
+    known = s != mask_id
+    assert torch.isinf(selp.cpu()[known]).all()
+    got = selp.cpu()[~known].double()
+    assert float(((got - sel[~known]).abs() / sel[~known]).max()) < 2e-6
+    # the re-mask on the kernel's p(sampled): exact
+    ref = O.remask_step(selp.cpu(), sampled.cpu(), mask_id, t, T, torch.full((B,), n), temp, u_g)
     assert torch.equal(out.cpu(), ref)
     assert int((out == mask_id).sum(1).max()) == k == int((out == mask_id).sum(1).min())
 
 
 def test_sample_never_draws_zero_probability_code(cuda):
-    """u = 0 with leading codes whose probability underflows to 0: the draw is the first
-    code of positive probability (torch's Categorical never samples a 0-probability code)."""
+    """Codes whose fp32 softmax probability is 0 (logit 1e4 below the max) are never drawn
+    by the device noise (Gumbel within [-2.9, 17.4]), wherever they sit in the row -- torch's
+    multinomial never samples a 0-probability code -- and the draws spread over the rest."""
+    from timevqvae.hip import rng
     from timevqvae.hip.sample import maskgit_sample
     K = 512
-    logits = torch.zeros(2, 3, K)
-    logits[..., :70] = -1e4  # exp underflows: p = 0 for codes 0..69 (two lanes' chunks)
-    s = torch.full((2, 3), K, dtype=torch.int64)
-    u = torch.zeros(2, 3)
-    sampled, selp = maskgit_sample(logits.to(cuda), s.to(cuda), K, u_cat=u.to(cuda))
-    assert (sampled.cpu() == 70).all()
+    logits = torch.zeros(64, 96, K)
+    logits[..., :70] = -1e4
+    logits[..., 300:] = -1e4
+    s = torch.full((64, 96), K, dtype=torch.int64)
+    rng.manual_seed(3)
+    sampled, selp = maskgit_sample(logits.to(cuda), s.to(cuda), K)
+    sc = sampled.cpu()
+    assert ((sc >= 70) & (sc < 300)).all()
     assert (selp.cpu() > 0).all()
+    # uniform over the 230 live codes: every one drawn among 6144 draws, none > 3x its share
+    counts = torch.bincount(sc.reshape(-1), minlength=K)[70:300]
+    assert (counts > 0).all() and int(counts.max()) < 3 * 6144 / 230
 
 
-def test_sample_u_near_one_never_draws_trailing_zero_probability_code(cuda):
-    """u just below 1 with trailing codes of probability 0: no prefix may exceed v after
-    rounding, and the fallback must still land on a positive-probability code (the last
-    one), never the zero-probability tail."""
+def test_sample_race_frequencies(cuda):
+    """The device-noise race draws Categorical(softmax(logits)): empirical frequencies over
+    65536 draws of one 8-code distribution within 5 sigma of p."""
+    from timevqvae.hip import rng
     from timevqvae.hip.sample import maskgit_sample
-    K = 512
-    logits = torch.zeros(2, 3, K)
-    logits[..., 300:] = -1e4  # p = 0 for codes 300..511 (the last 26 lanes' chunks)
-    s = torch.full((2, 3), K, dtype=torch.int64)
-    for u0 in (1.0 - 2.0 ** -24, 1.0 - 2.0 ** -20, 0.999999):
-        u = torch.full((2, 3), u0)
-        sampled, selp = maskgit_sample(logits.to(cuda), s.to(cuda), K, u_cat=u.to(cuda))
-        assert (sampled.cpu() < 300).all() and (sampled.cpu() >= 290).all(), sampled
-        assert (selp.cpu() > 0).all()
+    K = 8
+    lg = torch.tensor([0.0, 1.0, -1.0, 2.0, 0.5, -3.0, 1.5, 0.2])
+    p = torch.softmax(lg.double(), 0)
+    logits = lg.expand(256, 256, K).contiguous()
+    s = torch.full((256, 256), K, dtype=torch.int64)
+    rng.manual_seed(9)
+    sampled, _ = maskgit_sample(logits.to(cuda), s.to(cuda), K)
+    f = torch.bincount(sampled.cpu().reshape(-1), minlength=K).double() / 65536
+    sig = (p * (1 - p) / 65536).sqrt()
+    assert float(((f - p).abs() / sig).max()) < 5.0, (f, p)
+
+
+@pytest.mark.parametrize("B,n,D,K", [(1024, 96, 128, 512), (5, 13, 128, 100), (3, 7, 64, 33)])
+def test_tied_logits_sample_vs_oracle(B, n, D, K, cuda):
+    """The fused head + draw (tvq_tied_logits_sample): its logits within 1e-5 of torch's
+    h W[:K]^T + bias, its draw exactly the race on those logits, p(sampled) within 2e-6,
+    known tokens kept; and the same draw as maskgit_sample on its logits."""
+    from oracle import tvq_oracle as O
+    from timevqvae.hip._native import plan_trace
+    from timevqvae.hip.sample import maskgit_sample, tied_logits_sample
+    g = torch.Generator().manual_seed(B + n + D + K)
+    h = torch.randn(B, n, D, generator=g)
+    W = torch.randn(K + 1, D, generator=g) * D ** -0.5
+    bias = torch.randn(n, K + 1, generator=g) * 0.3
+    mask_id = K
+    s = torch.randint(0, K, (B, n), generator=g)
+    s[torch.rand(B, n, generator=g) < 0.7] = mask_id
+    gum = _gumbel((B, n, K), g)
+    with plan_trace() as tr:
+        sampled, selp, lg = tied_logits_sample(h.to(cuda), W.to(cuda), bias.to(cuda), K,
+                                               s.to(cuda), mask_id, gumbel=gum.to(cuda),
+                                               want_logits=True)
+        torch.cuda.synchronize()
+    assert tr.has("tied_logits_sample")
+    want_l = (h.double() @ W[:K].double().t() + bias[:, :K].double()).float()
+    lc = lg.cpu()
+    assert float((lc - want_l).abs().max()) < 1e-5 * float(want_l.abs().max())
+    want, sel = O.race_sample(lc, s, mask_id, gum)
+    assert torch.equal(sampled.cpu(), want)
+    known = s != mask_id
+    assert torch.isinf(selp.cpu()[known]).all()
+    got = selp.cpu()[~known].double()
+    assert float(((got - sel[~known]).abs() / sel[~known]).max()) < 2e-6
+    s2, p2 = maskgit_sample(lg, s.to(cuda), mask_id, gumbel=gum.to(cuda))
+    assert torch.equal(s2.cpu(), sampled.cpu())
+    assert float(((p2.cpu()[~known] - selp.cpu()[~known]).abs() / p2.cpu()[~known]).max()) < 2e-6
+
+
+def test_tied_logits_sample_device_noise_matches_unfused(cuda):
+    """With the device noise (no injection) the fused head draws exactly what maskgit_sample
+    draws from the fused head's own logits at the same stream offset: both hash the same
+    (stream key, token * K + code) counter."""
+    from timevqvae.hip import rng
+    from timevqvae.hip.sample import maskgit_sample, tied_logits_sample
+    g = torch.Generator().manual_seed(77)
+    B, n, D, K = 64, 96, 128, 512
+    h = torch.randn(B, n, D, generator=g).to(cuda)
+    W = (torch.randn(K + 1, D, generator=g) * D ** -0.5).to(cuda)
+    bias = (torch.randn(n, K + 1, generator=g) * 0.3).to(cuda)
+    s = torch.full((B, n), K, dtype=torch.int64, device=cuda)
+    rng.manual_seed(4)
+    a, pa, lg = tied_logits_sample(h, W, bias, K, s, K, site=7, want_logits=True)
+    rng.manual_seed(4)
+    b, pb = maskgit_sample(lg, s, K, site=7)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert float(((pa - pb).abs() / pb).max()) < 2e-6
 
 
 def test_mask_by_random_topk_exact_k(cuda):

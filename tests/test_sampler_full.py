@@ -6,11 +6,14 @@ Reference: maskgit.py:294-477 (first_pass / second_pass / iterative_decoding /
 decode_token_ind_to_timeseries), utils/sample_utils.py:5-64, generation/sampler.py:141-169.
 
 Parity at full size:
-  - every decoding step is driven with injected noise (u_cat for the Categorical draw,
-    u_gumbel for the confidence noise); each step's logits equal the oracle transformer
-    (oracle/tvq_oracle.transformer_forward) on the same tokens within 1e-4 relative, and
-    the oracle's sample step (tvq_oracle.sample_step) fed the HIP logits gives exactly the
-    HIP step's re-masked token set;
+  - every decoding step runs the product's draw (MaskGIT.sample_tokens: the LF prior's
+    fused eval kernel + the race kernel; the HF prior's fused head + race, whose logits
+    never reach memory, exported here for the check) with injected noise (Gumbel noise for
+    the Categorical race, u_gumbel for the confidence noise); each step's logits equal the
+    oracle transformer (oracle/tvq_oracle.transformer_forward) on the same tokens within
+    1e-4 relative, the draws equal the oracle race (tvq_oracle.race_sample) on those
+    logits exactly, p(sampled) is within 2e-6 of the double softmax, and the re-mask
+    equals tvq_oracle.remask_step exactly;
   - the decoded series of a 64-row subset equal the oracle decoder within 1e-4 relative;
   - the graphed batch (GraphedSampler) equals the eager batch bit for bit, every token is
     decoded, codes are in range, and x == x_l + x_h.
@@ -45,7 +48,8 @@ def _state(mod):
 
 def test_decode_1024_stepwise_vs_oracle(mg, cuda):
     from oracle import tvq_oracle as O
-    from timevqvae.hip.sample import mask_len, maskgit_remask, maskgit_sample
+    from timevqvae.hip._native import plan_trace
+    from timevqvae.hip.sample import mask_len, maskgit_remask
     g = torch.Generator().manual_seed(2024)
     pl = mg.config["MaskGIT"]["prior_model_l"]
     ph = mg.config["MaskGIT"]["prior_model_h"]
@@ -53,21 +57,35 @@ def test_decode_1024_stepwise_vs_oracle(mg, cuda):
     null = torch.full((NUM, 1), mg.transformer_l.n_classes, dtype=torch.long)
     ctx = O.Ctx(False)
 
-    def drive(kind, s, T, temp, n0, logit_fn, ref_fn):
+    def drive(kind, s, T, temp, n0, draw_fn, ref_fn):
         K = mg.mask_token_ids[kind]
         for t in range(T):
-            logits = logit_fn(s)
+            u = torch.rand(NUM, n0, K, generator=g).clamp(1e-7, 1 - 1e-7)
+            gum = -torch.log(-torch.log(u))
+            del u
+            # the product's draw (MaskGIT.sample_tokens; HF: the fused head), with the
+            # logits it drew from
+            with plan_trace() as tr:
+                sampled, selp, logits = draw_fn(s, gum.to(cuda))
+                torch.cuda.synchronize()
+            if kind == "hf":
+                assert tr.has("tied_logits_sample"), tr.lines
             ref = ref_fn(s.cpu())
             assert logits.shape == ref.shape == (NUM, n0, K)
             e = rel(logits, ref)
             assert e < 1e-4, f"{kind} step {t}: logits rel err {e}"
-            u_cat = torch.rand(NUM, n0, generator=g)
+            sc = s.cpu()
+            want, sel = O.race_sample(logits.cpu(), sc, K, gum)
+            assert torch.equal(sampled.cpu(), want), f"{kind} step {t}: draws differ"
+            unk = sc == K
+            ps = selp.cpu()
+            assert torch.isinf(ps[~unk]).all()
+            pe = float(((ps[unk].double() - sel[unk]).abs() / sel[unk]).max())
+            assert pe < 2e-6, f"{kind} step {t}: p(sampled) rel err {pe}"
             u_g = torch.rand(NUM, n0, generator=g)
-            want = O.sample_step(logits.cpu(), s.cpu(), K, t, T, torch.full((NUM,), n0), temp,
-                                 u_cat, u_g)
             ratio = (t + 1) / T
-            sampled, selp = maskgit_sample(logits, s, K, u_cat=u_cat.to(cuda))
             k = mask_len(n0, O.gamma_cosine(ratio))
+            want = O.remask_step(ps, want, K, t, T, torch.full((NUM,), n0), temp, u_g)
             s = maskgit_remask(selp, k, temp * (1.0 - ratio), sampled, K, u_gumbel=u_g.to(cuda))
             got = s.cpu()
             assert torch.equal(got, want), (
@@ -79,7 +97,8 @@ def test_decode_1024_stepwise_vs_oracle(mg, cuda):
         K = mg.mask_token_ids["lf"]
         s_l = torch.full((NUM, 24), K, dtype=torch.int64, device=cuda)
         s_l = drive("lf", s_l, mg.T["lf"], mg.choice_temperature_l, 24,
-                    lambda s: mg.masked_prediction(mg.transformer_l, None, s),
+                    lambda s, gum: mg.sample_tokens(mg.transformer_l, None, K, s, gumbel=gum,
+                                                    want_logits=True),
                     lambda s: O.transformer_forward(ctx, sd_l, "lf", s, None, null, K,
                                                     pl["heads"], pl["n_layers"]))
         s_lc = s_l.cpu()
@@ -87,7 +106,8 @@ def test_decode_1024_stepwise_vs_oracle(mg, cuda):
         Kh = mg.mask_token_ids["hf"]
         s_h = torch.full((NUM, 96), Kh, dtype=torch.int64, device=cuda)
         s_h = drive("hf", s_h, mg.T["hf"], mg.choice_temperature_h, 96,
-                    lambda s: mg.masked_prediction(mg.transformer_h, None, s_l, s),
+                    lambda s, gum: mg.sample_tokens(mg.transformer_h, None, Kh, s_l, s,
+                                                    gumbel=gum, want_logits=True),
                     lambda s: O.transformer_forward(ctx, sd_h, "hf", s_lc, s, null, Kh,
                                                     ph["heads"], ph["n_layers"]))
         s_hc = s_h.cpu()
