@@ -49,6 +49,7 @@ int tvq_counter_capture(int64_t begin);
  * out_ab = a + b elementwise over n floats, c / d / out / out_ab nullable (the logged loss
  * sums of stage1.py:170-198, maskgit.py:155-192). */
 int tvq_fill(float* p, int64_t n, float value, tvq_stream_t stream);
+int tvq_fill_i64(int64_t* p, int64_t n, int64_t value, tvq_stream_t stream);
 int tvq_add_i64(int64_t* p, int64_t value, tvq_stream_t stream);
 int tvq_sum4(const float* a, const float* b, const float* c, const float* d, float* out,
              float* out_ab, int64_t n, tvq_stream_t stream);
@@ -197,6 +198,8 @@ int tvq_conv_config(int64_t halo);
 int tvq_conv_packcache_begin(int64_t id, float* arena, int64_t cap_floats, tvq_stream_t stream);
 int tvq_conv_packcache_end(void);
 int tvq_conv_packcache_release(int64_t id);
+/* pause(1) / pause(0): convs between them bypass the open scope (weights computed inside it). */
+int tvq_conv_packcache_pause(int64_t on);
 int64_t tvq_conv_packcache_entries(void);
 
 /* Deferred weight-gradient reductions: between begin() and flush(stream), the split sums

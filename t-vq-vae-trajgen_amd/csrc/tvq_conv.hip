@@ -3007,6 +3007,22 @@ extern "C" int tvq_conv_packcache_end(void) {
   return TVQ_OK;
 }
 
+// pause(1): convs run without the open scope's cache (weights computed inside the scope,
+// e.g. folded per call, must not be recorded: the cache repacks at the NEXT scope's begin,
+// before such a weight is recomputed); pause(0) resumes it
+static PackCacheState* g_pc_paused = nullptr;
+extern "C" int tvq_conv_packcache_pause(int64_t on) {
+  if (on) {
+    TVQ_CHECK_ARG(!g_pc_paused, "tvq_conv_packcache_pause: already paused");
+    g_pc_paused = g_pc_cur;
+    g_pc_cur = nullptr;
+  } else {
+    g_pc_cur = g_pc_paused;
+    g_pc_paused = nullptr;
+  }
+  return TVQ_OK;
+}
+
 extern "C" int tvq_conv_packcache_release(int64_t id) {
   auto it = g_pcs.find(id);
   if (it == g_pcs.end()) return TVQ_OK;

@@ -218,6 +218,12 @@ __global__ __launch_bounds__(256) void fill_f32_kernel(float* __restrict__ p, in
   }
 }
 
+__global__ __launch_bounds__(256) void fill_i64_kernel(int64_t* __restrict__ p, int64_t n,
+                                                       int64_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    p[i] = v;
+}
+
 __global__ void add_i64_kernel(int64_t* __restrict__ p, int64_t v) {
   if (threadIdx.x == 0) p[0] += v;
 }
@@ -250,6 +256,16 @@ extern "C" int tvq_fill(float* p, int64_t n, float value, tvq_stream_t stream) {
   hipLaunchKernelGGL(fill_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p,
                      n, value, vec);
   return launch_status("tvq_fill");
+}
+
+extern "C" int tvq_fill_i64(int64_t* p, int64_t n, int64_t value, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(p && n >= 0, "tvq_fill_i64: bad arguments");
+  if (n == 0) return TVQ_OK;
+  int64_t blocks = (n + 255) / 256;
+  blocks = blocks > 2048 ? 2048 : blocks;
+  hipLaunchKernelGGL(fill_i64_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p,
+                     n, value);
+  return launch_status("tvq_fill_i64");
 }
 
 extern "C" int tvq_add_i64(int64_t* p, int64_t value, tvq_stream_t stream) {

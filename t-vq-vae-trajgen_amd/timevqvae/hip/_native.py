@@ -36,6 +36,7 @@ sig("tvq_counter_capture", I64)
 sig("tvq_plan_trace", I64)
 sig("tvq_plan_read", ctypes.c_char_p, I64, restype=I64)
 sig("tvq_fill", P, I64, ctypes.c_float, P)
+sig("tvq_fill_i64", P, I64, I64, P)
 sig("tvq_add_i64", P, I64, P)
 sig("tvq_sum4", P, P, P, P, P, P, I64, P)
 # --- VQ codebook -----------------------------------------------------------
@@ -144,6 +145,7 @@ sig("tvq_maskgit_remask", P, I64, I64, I64, F32, P, P, U64, P, I64, P, P, P)
 sig("tvq_conv_packcache_begin", I64, P, I64, P)
 sig("tvq_conv_packcache_end")
 sig("tvq_conv_packcache_release", I64)
+sig("tvq_conv_packcache_pause", I64)
 sig("tvq_conv_packcache_entries", restype=I64)
 sig("tvq_conv_wgrad_defer_begin")
 sig("tvq_conv_wgrad_defer_flush", P)

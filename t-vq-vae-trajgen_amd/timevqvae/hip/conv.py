@@ -108,6 +108,18 @@ class PackCache:
             pass
 
     @staticmethod
+    @contextlib.contextmanager
+    def paused():
+        """Convs inside bypass any open scope (for weights computed inside the scope: the
+        cache repacks recorded weights at the next scope's begin, before such a weight is
+        recomputed)."""
+        call("tvq_conv_packcache_pause", 1)
+        try:
+            yield
+        finally:
+            call("tvq_conv_packcache_pause", 0)
+
+    @staticmethod
     def entries():
         return value("tvq_conv_packcache_entries")
 

@@ -15,6 +15,17 @@ def mask_len(unknown0: int, mask_ratio: float) -> int:
     return max(0, int(np.floor(np.float32(unknown0) * np.float32(mask_ratio))))
 
 
+def full_tokens(shape, value, device):
+    """torch.full(shape, value, int64) on the HIP path (tvq_fill_i64): the all-masked token
+    rows of MaskGIT.create_input_tokens_normal (maskgit.py:230-236)."""
+    t = torch.empty(shape, dtype=torch.int64, device=device)
+    if t.is_cuda:
+        call("tvq_fill_i64", ptr(t), t.numel(), int(value), stream_ptr())
+    else:
+        t.fill_(int(value))
+    return t
+
+
 def maskgit_sample(logits, s, mask_id, gumbel=None, site=0):
     """(sampled ids with known tokens kept, p(sampled) with +inf for known tokens).
 

@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from ..hip import rng, streams
-from ..hip.conv import _immediate, _keep, conv2d
+from ..hip.conv import PackCache, _immediate, _keep, conv2d
 from ..hip.linear import gemm, linear
 from ..hip.norm import bn_snake
 from ..hip.xf import (batch_colsum, drop_first_token, embed_assemble, embedding, gelu,
@@ -33,7 +33,7 @@ from ..hip.xf import (batch_colsum, drop_first_token, embed_assemble, embedding,
                       prior_lf_eval_supported, qkv_attention, rmsnorm, rmsnorm_res,
                       upsample_nearest_t)
 from ..hip._native import call, grad_sink, ptr, stream_ptr, value
-from ..hip.sample import maskgit_sample, tied_logits_sample
+from ..hip.sample import codebook_gather_nchw, full_tokens, maskgit_sample, tied_logits_sample
 
 # the HF prior's sampling step straight from its head (no logits in memory); 0: form the
 # logits and sample them (A/B and diagnosis)
@@ -379,7 +379,7 @@ class BidirectionalTransformer(nn.Module):
         """bidirectional_transformer.py:124-150.  `_class_rand` (tests only): the uniform
         draws of the classifier-free-guidance drop, injected instead of torch.rand."""
         if class_condition is None:
-            idx = torch.full((batch_size, 1), self.n_classes, dtype=torch.long, device=device)
+            idx = full_tokens((batch_size, 1), self.n_classes, device)
         elif self.training:
             # drop to the null class where u > p fails, u ~ U[0,1) per sample: one kernel
             # (the device counter RNG; the reference's torch.rand draws can be injected)
@@ -454,13 +454,64 @@ class BidirectionalTransformer(nn.Module):
                                         site=site, want_logits=want_logits)
         if (self.kind == "hf" and not self.training and FUSED_SAMPLE
                 and self.tok_emb_h.weight.shape[1] in (64, 128)):
-            return tied_logits_sample(self._embed_hf(s_M_l, s_M_h, class_condition),
+            return tied_logits_sample(self._head_hf_eval(s_M_l, s_M_h, class_condition),
                                       self.tok_emb_h.weight, self.bias, self.codebook_size, s,
                                       mask_id, gumbel=gumbel, site=site, want_logits=want_logits)
         logits = self(s_M_l, s_M_h, class_condition) if self.kind == "hf" else \
             self(s_M_l, class_condition=class_condition)
         out = maskgit_sample(logits, s, mask_id, gumbel=gumbel, site=site)
         return out + (logits,) if want_logits else out
+
+    @torch.no_grad()
+    def _head_hf_eval(self, s_M_l, s_M_h, class_condition):
+        """The HF prior's head output in eval mode (the input of the tied logits), with the
+        Linears that meet without a nonlinearity between them composed (weights fixed while
+        sampling; the same function up to fp32 reassociation):
+          * project_in after cat(Upscale(tl), th) + pos: its tl half folds into Upscale's
+            last conv (256 -> 32 output channels instead of 256 -> 128 then 128 -> 32), its
+            th half into the token table (tok_emb_h W_in[:, D:]^T, gathered per token), and
+            the position / class tables are projected once;
+          * project_out then pred_head's Linear: one 32 -> 128 Linear (W_p W_out).
+        The (B, n + 1, 2 D) embedding and the (B, n, 2 D) project_out output are never
+        formed.  bidirectional_transformer.py:12-30, 194-236."""
+        from ..hip.linear import gemm
+        dev = s_M_l.device
+        B, n = s_M_h.shape
+        D = self.tok_emb_h.weight.shape[1]
+        W_in = self.blocks.project_in.weight  # (d, 2 D)
+        d = W_in.shape[0]
+        up = self.projector.conv
+        W2, b2 = up[3].weight, up[3].bias  # (D, H, 3), (D)
+        H = W2.shape[1]
+        # folded tables / weights (tiny GEMMs)
+        W2c = gemm(W_in, 2 * D, 1, W2, H * 3, 1, d, H * 3, D).view(d, H, 3)
+        b2c = gemm(W_in, 2 * D, 1, b2, 1, 1, d, 1, D).view(d)
+        Th = gemm(self.tok_emb_h.weight, D, 1, W_in[:, D:], 1, 2 * D,
+                  self.tok_emb_h.weight.shape[0], d, D)
+        P = gemm(self.pos_emb.weight, 2 * D, 1, W_in, 1, 2 * D, self.pos_emb.weight.shape[0], d,
+                 2 * D)
+        C = gemm(self.class_condition_emb.weight, 2 * D, 1, W_in, 1, 2 * D,
+                 self.class_condition_emb.weight.shape[0], d, 2 * D)
+        lin, ln = self.pred_head[0], self.pred_head[2]
+        W_out = self.blocks.project_out.weight  # (2 D, d)
+        Wc = gemm(lin.weight, 2 * D, 1, W_out, d, 1, lin.weight.shape[0], d, 2 * D)
+        # x1 = cat(C[cls], Upscale'(tl) + Th[s_h] + P[:n]) = project_in(embed)
+        tl = self._tok(s_M_l, self.tok_emb_l.weight, "lf", self._site_l)
+        x = upsample_nearest_t(tl, n)
+        x = gelu(conv2d(x, up[0].weight, up[0].bias))
+        x = bn_snake(x, up[2], None)
+        r = codebook_gather_nchw(s_M_h, Th, 1, n).view(B, d, n)  # Th[s_h] channels-first
+        with PackCache.paused():  # W2c is computed per call: never cached
+            u = conv2d(x, W2c, b2c, residual=r)  # (B, d, n)
+        if class_condition is None:
+            idx = full_tokens((B, 1), self.n_classes, dev)
+        else:
+            idx = class_condition.long()
+        x = embed_assemble(embedding(idx, C), u.transpose(1, 2), None, P, n)
+        x = self.blocks.post_emb_norm(x)
+        x = self.blocks.attn_layers(x)
+        h = linear_act(drop_first_token(x), Wc, lin.bias, gelu=True)
+        return layer_norm(h, ln.weight, ln.bias, ln.eps)
 
     def masked_ce(self, target, keep, s_M_l, s_M_h=None, class_condition=None):
         """F.cross_entropy(self(...)[~keep], target[~keep]) (maskgit.py:183-191) with the tied

@@ -15,7 +15,8 @@ import torch
 import torch.nn as nn
 
 from ..hip import rng, streams, wgrad
-from ..hip.sample import codebook_gather_nchw, mask_len, maskgit_remask, maskgit_sample
+from ..hip.sample import (codebook_gather_nchw, full_tokens, mask_len, maskgit_remask,
+                          maskgit_sample)
 from ..hip.signal import stft_encode
 from ..hip.loss import add_losses
 from ..hip.vq import indices_only
@@ -199,7 +200,7 @@ class MaskGIT(nn.Module):
 
     def create_input_tokens_normal(self, num, num_tokens, mask_token_ids, device):
         """maskgit.py:230-236."""
-        return torch.full((num, num_tokens), mask_token_ids, dtype=torch.int64, device=device)
+        return full_tokens((num, num_tokens), mask_token_ids, device)
 
     def mask_by_random_topk(self, mask_len, probs, temperature=1.0, device="cpu"):
         """maskgit.py:238-267: bool masking of exactly mask_len lowest-confidence tokens

@@ -4,6 +4,8 @@ not on the path).  MaskGIT.iterative_decoding and decode_token_ind_to_timeseries
 the HIP path; each batch reaches the host by an asynchronous copy into pinned memory."""
 import torch
 
+from ..hip.loss import add_losses
+
 
 def _batch_sizes(n_samples: int, batch_size: int):
     """Sizes of the sampling batches: full batches, then the remainder (if any)."""
@@ -93,7 +95,7 @@ class GraphedSampler:
                                                       class_index=class_index)
                 x_l = maskgit.decode_token_ind_to_timeseries(s_l, "lf")
                 x_h = maskgit.decode_token_ind_to_timeseries(s_h, "hf")
-                out = (x_l, x_h, x_l + x_h)
+                out = (x_l, x_h, add_losses(x_l, x_h))  # one HIP add (tvq_sum4)
                 if fidelity_enhancer is not None:
                     out = out + (fidelity_enhancer(out[2]),)
                 return out

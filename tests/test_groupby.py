@@ -1,6 +1,6 @@
 """The deterministic group-by sums behind nn.Embedding's backward and the VQ embed_sum
 (csrc/tvq_reduce.hip: gb_sort1_kernel -- the single-block stable counting sort -- or the
-3-launch sort above 32768 rows, then seg_sum_kernel with its in-launch combine of skewed
+3-launch sort above 2048 rows, then seg_sum_kernel with its in-launch combine of skewed
 values) against torch fp64 index_add, on uniform, skewed (one value owning 60 % of the rows,
 as the MaskGIT mask token does), sparse (most values empty) and tiny (the class embedding)
 index sets; every call is run twice and must be bitwise equal.  Tolerance: rel-L2 1e-6
@@ -47,7 +47,7 @@ def test_embedding_bwd_groupby(kind, M, V, D, accumulate, cuda):
             torch.cuda.synchronize()
         outs.append(tg.cpu())
     assert torch.equal(outs[0], outs[1])
-    want = "group_by sort1" if M <= 32768 else "group_by 3-launch"
+    want = "group_by sort1" if M <= 2048 and V <= 1024 else "group_by 3-launch"
     assert tr.has(want), tr.lines
     err = float((outs[0].double() - ref).norm() / ref.norm())
     assert err < 1e-6, err

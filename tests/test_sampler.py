@@ -156,6 +156,36 @@ def test_tied_logits_sample_device_noise_matches_unfused(cuda):
     assert float(((pa - pb).abs() / pb).max()) < 2e-6
 
 
+def test_hf_eval_head_folded_matches_forward_hf(cuda):
+    """The HF prior's eval draw path (BidirectionalTransformer._head_hf_eval: project_in folded
+    into Upscale's last conv and the token / position / class tables, project_out composed
+    with pred_head's Linear) gives forward_hf's logits within 1e-5 relative (fp32
+    reassociation), null and real class; and the draw equals the race on those logits."""
+    from oracle import tvq_oracle as O
+    from timevqvae.hip._native import plan_trace
+    mg = _maskgit(cuda)
+    tf = mg.transformer_h
+    K = mg.mask_token_ids["hf"]
+    g = torch.Generator().manual_seed(21)
+    B = 6
+    s_l = torch.randint(0, mg.mask_token_ids["lf"], (B, mg.num_tokens_l), generator=g).to(cuda)
+    s_h = torch.randint(0, K + 1, (B, mg.num_tokens_h), generator=g).to(cuda)
+    for cls in (None, torch.randint(0, 5, (B, 1), generator=g).to(cuda)):
+        with torch.no_grad():
+            want = tf(s_l, s_h, class_condition=cls)
+            u = torch.rand(want.shape, generator=g).clamp(1e-7, 1 - 1e-7)
+            gum = -torch.log(-torch.log(u))
+            with plan_trace() as tr:
+                sampled, selp, got = tf.sample(s_l, s_h, class_condition=cls, mask_id=K,
+                                               gumbel=gum.to(cuda), want_logits=True)
+                torch.cuda.synchronize()
+        assert tr.has("tied_logits_sample")
+        err = float((got - want).norm() / want.norm())
+        assert err < 1e-5, err
+        race, _ = O.race_sample(got.cpu(), s_h.cpu(), K, gum)
+        assert torch.equal(sampled.cpu(), race)
+
+
 def test_mask_by_random_topk_exact_k(cuda):
     """mask_by_random_topk keeps exactly mask_len per row; known tokens (+inf) never mask."""
     from timevqvae.hip.sample import maskgit_remask

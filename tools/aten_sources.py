@@ -52,11 +52,16 @@ def main():
     if sys.argv[1:] == ["sampler"]:
         mg = tr.s2.maskgit.eval()
 
-        def work():
+        from timevqvae.hip import rng
+        from timevqvae.hip.loss import add_losses
+
+        def work():  # GraphedSampler's batch, eager
             with torch.no_grad():
+                rng.advance(dev)
                 s_l, s_h = mg.iterative_decoding(num=1024, device=dev)
-                mg.decode_token_ind_to_timeseries(s_l, "lf")
-                mg.decode_token_ind_to_timeseries(s_h, "hf")
+                x_l = mg.decode_token_ind_to_timeseries(s_l, "lf")
+                x_h = mg.decode_token_ind_to_timeseries(s_h, "hf")
+                add_losses(x_l, x_h)
     else:
         def work():
             tr.step(batch)
