@@ -185,14 +185,17 @@ __device__ __forceinline__ uint32_t race_key(uint64_t seed) {
   return (uint32_t)(seed ^ (seed >> 32));
 }
 __device__ __forceinline__ float race_gumbel(uint32_t key, uint32_t ctr) {
-  uint32_t x = ctr * 0x9E3779B9u + key;
+  uint32_t x = ctr + key;  // lowbias32 (2 multiplies: per (token, code) this is hot)
   x ^= x >> 16;
-  x *= 0x21F0AAADu;
+  x *= 0x7FEB352Du;
   x ^= x >> 15;
-  x *= 0x735A2D97u;
-  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
   const float u = (float)((x >> 9) * 2u + 1u) * (1.0f / 16777216.0f);
-  return -__logf(fmaxf(-__logf(u), 2.9802322e-08f));
+  // raw v_log_f32 (log2; u >= 2^-24 and q >= 2^-25 are normal): -ln(-ln u) without the
+  // library log's denormal scaling
+  const float q = fmaxf(-0.69314718f * __builtin_amdgcn_logf(u), 2.9802322e-08f);
+  return -0.69314718f * __builtin_amdgcn_logf(q);
 }
 
 }  // namespace tvq

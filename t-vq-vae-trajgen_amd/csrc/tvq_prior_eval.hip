@@ -84,6 +84,22 @@ __device__ __forceinline__ void pe_zero(floatx16& a) {
   for (int i = 0; i < 16; ++i) a[i] = 0.f;
 }
 
+// GELU(x) = x/2 (1 + erf(x / sqrt 2)) with erf by Abramowitz-Stegun 7.1.26 (|error| <=
+// 1.5e-7, branch-free: one reciprocal, one exp, a degree-5 polynomial) instead of the
+// library erff's range branches, which diverge across a wave's 64 values: the GELUs were a
+// quarter of this kernel's VALU instructions.  Within fp32 noise of the exact form at the
+// 1e-4 bar of tests/test_prior_eval.py; the training path keeps the library erff.
+__device__ __forceinline__ float pe_gelu(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = 1.0f - p * t * __expf(-z * z);  // erf(|x| / sqrt 2)
+  return 0.5f * x * (1.0f + copysignf(e, x));
+}
+
 // ---- the weight-tile stream.  Tile idx (order of consumption) -> source rows.
 struct PeTile {
   const float* w;  // row-major, ld = PE_D
@@ -192,12 +208,15 @@ template <bool WA, int NS, class BV>
 __device__ __forceinline__ floatx16 pe_gemm(PeStream& st, BV bv, floatx16 acc) {
   constexpr int G = NS / 4;  // 16-B groups of the tile (>= 8)
   static_assert(G >= PE_PRE, "tile shorter than the prefetch");
-  const float4* cur = st.src + st.off;
+  // wave-uniform tile offset in an SGPR: every load below is scalar base + the lane's
+  // 16-byte slot + an immediate (no per-load address arithmetic on the VALU)
+  const int off = __builtin_amdgcn_readfirstlane((int)st.off);
+  const float4* cur = st.src + off;
   float4 rest[G - PE_PRE > 0 ? G - PE_PRE : 1];
 #pragma unroll
   for (int i = 0; i < G - PE_PRE; ++i) rest[i] = cur[(PE_PRE + i) * 64 + st.lane];
   const int nidx = st.idx + 1;
-  const int64_t noff = st.off + (int64_t)G * 64;
+  const int noff = off + G * 64;
   float4 nq[PE_PRE];
   if (nidx < st.ntiles) {
 #pragma unroll
@@ -429,7 +448,7 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) u[t][r] = gelu_erf(u[t][r]);
+      for (int r = 0; r < 16; ++r) u[t][r] = pe_gelu(u[t][r]);
     pe_linear_bias(st, u, L.b2, h, y);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -449,7 +468,7 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) x[t][r] = gelu_erf(y[t][r]);
+      for (int r = 0; r < 16; ++r) x[t][r] = pe_gelu(y[t][r]);
     pe_layernorm(x, a.ln_w, a.ln_b, a.ln_eps, h);
   }
   const int ldb = a.K + 1;
@@ -461,7 +480,9 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
     const bool tok_ok = tok >= 1 && tok <= n;
     const int64_t t = (int64_t)b * n + (tok_ok ? tok - 1 : 0);
     const float* brow = a.bias + (int64_t)(tok_ok ? tok - 1 : 0) * ldb;
-    const float* grow = (a.gumbel && tok_ok) ? a.gumbel + t * a.K : nullptr;
+    // every lane reads a valid row (t is clamped for the cls / padding lanes, which store
+    // nothing): race_tile<true> dereferences it unconditionally
+    const float* grow = a.gumbel ? a.gumbel + t * a.K : nullptr;
     const uint32_t key = a.gumbel ? 0u : race_key(mix_seed(a.seed_ptr, a.offset));
     float* lout = (a.logits && tok_ok) ? a.logits + t * a.K : nullptr;
     RaceState rs;
@@ -485,7 +506,8 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
           if (code < a.K) lout[code] = v[r];
         }
       }
-      race_tile(rs, v, c0, h, a.K, grow, key, (uint32_t)t * (uint32_t)a.K);
+      if (a.gumbel) race_tile<true>(rs, v, c0, h, a.K, grow, key, (uint32_t)t * (uint32_t)a.K);
+      else race_tile<false>(rs, v, c0, h, a.K, grow, key, (uint32_t)t * (uint32_t)a.K);
     }
     int pick;
     float p;
@@ -634,7 +656,7 @@ __device__ __forceinline__ floatx16 pe2_gemm(PeStream2& st, BV bv, floatx16 acc)
     }
     // branch-free: past the stream's end the last group is re-read (never consumed)
     const int nxt = min(st.pos + T4 + PE2_D, st.total - 1);
-    st.q[T4 % PE2_D] = st.src[(int64_t)nxt * 64 + st.lane];
+    st.q[T4 % PE2_D] = (st.src + __builtin_amdgcn_readfirstlane(nxt) * 64)[st.lane];
   }
   st.pos += G;
   return acc;
@@ -884,7 +906,7 @@ __device__ __forceinline__ void prior_lf_eval2_body(const PriorArgs& a,
           pe_zero(acc);
           acc = pe2_gemm<true, 64>(st, [&](int t) { return xn[t >> 4][t & 15]; }, acc);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) u[j][r] = gelu_erf(acc[r] + bv[r]);
+          for (int r = 0; r < 16; ++r) u[j][r] = pe_gelu(acc[r] + bv[r]);
         }
       }
 #pragma unroll
@@ -926,7 +948,7 @@ __device__ __forceinline__ void prior_lf_eval2_body(const PriorArgs& a,
       pe_zero(acc);
       acc = pe2_gemm<true, 64>(st, [&](int t) { return x[t >> 4][t & 15]; }, acc);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) y2[j][r] = gelu_erf(acc[r] + bv[r]);
+      for (int r = 0; r < 16; ++r) y2[j][r] = pe_gelu(acc[r] + bv[r]);
     }
     pe2_gather<W>(buf, y2, x, l);
     pe2_layernorm(x, a.ln_w, a.ln_b, a.ln_eps, h);
@@ -941,7 +963,9 @@ __device__ __forceinline__ void prior_lf_eval2_body(const PriorArgs& a,
     const bool tok_ok = tok >= 1 && tok <= n;
     const int64_t t = (int64_t)b * n + (tok_ok ? tok - 1 : 0);
     const float* brow = a.bias + (int64_t)(tok_ok ? tok - 1 : 0) * ldb;
-    const float* grow = (a.gumbel && tok_ok) ? a.gumbel + t * a.K : nullptr;
+    // every lane reads a valid row (t is clamped for the cls / padding lanes, which store
+    // nothing): race_tile<true> dereferences it unconditionally
+    const float* grow = a.gumbel ? a.gumbel + t * a.K : nullptr;
     const uint32_t key = a.gumbel ? 0u : race_key(mix_seed(a.seed_ptr, a.offset));
     float* lout = (a.logits && tok_ok) ? a.logits + t * a.K : nullptr;
     RaceState rs;
@@ -966,7 +990,8 @@ __device__ __forceinline__ void prior_lf_eval2_body(const PriorArgs& a,
           if (code < a.K) lout[code] = v[r];
         }
       }
-      race_tile(rs, v, c0, h, a.K, grow, key, (uint32_t)t * (uint32_t)a.K);
+      if (a.gumbel) race_tile<true>(rs, v, c0, h, a.K, grow, key, (uint32_t)t * (uint32_t)a.K);
+      else race_tile<false>(rs, v, c0, h, a.K, grow, key, (uint32_t)t * (uint32_t)a.K);
     }
     race_halves(rs);
     // the two waves' code halves meet in LDS (wave 1 publishes, wave 0 finishes)
@@ -1058,9 +1083,14 @@ static int prior_lf_eval_launch(PriorArgs& a, const int64_t* s, int64_t B, int64
   const int ntiles = 4 + 28 * (int)depth + 8 + (int)((K + 31) / 32);
   hipStream_t st = (hipStream_t)stream;
   float4* ws = reinterpret_cast<float4*>(workspace);
-  static const bool two = [] {  // TVQ_PRIOR_WAVES=1: the one-wave kernel (A/B)
+  // TVQ_PRIOR_WAVES=2: the two-wave kernel.  Measured slower (sampler batch 5.86 vs 5.57 ms,
+  // 356 vs 327 us per launch, tools/gpu_r4j.sh): the LDS exchanges, barriers and the work
+  // both waves repeat (norm statistics, LayerNorms) cost more than the second wave hides --
+  // the one-wave kernel's MFMA pipe was already ~64 % busy with its VALU phases mostly
+  // short (profiles/r04_prior_pmc.txt)
+  static const bool two = [] {
     const char* e = getenv("TVQ_PRIOR_WAVES");
-    return !(e && e[0] == '1');
+    return e && e[0] == '2';
   }();
   if (two) {
     // both waves' streams: 6 + 16 * depth tiles each, plus the code tiles

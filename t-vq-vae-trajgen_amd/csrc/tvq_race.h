@@ -32,32 +32,36 @@ __device__ __forceinline__ void race_init(RaceState& st) {
 __device__ __forceinline__ int race_crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // one tile's 16 logits v[r] = l(code0 + crow(r, h)), codes >= K masked out; noise from the
-// injected row g (g[code]) or the hash at counter ctr0 + code
+// injected row g (g[code], INJ) or the hash at counter ctr0 + code
+template <bool INJ>
 __device__ __forceinline__ void race_tile(RaceState& st, const float (&v)[16], int code0, int h,
                                           int K, const float* __restrict__ g, uint32_t key,
                                           uint32_t ctr0) {
+  const bool full = code0 + 32 <= K;  // wave-uniform: no per-code guard on full tiles
   float tmax = -INFINITY;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int code = code0 + race_crow(r, h);
-    if (code < K) {
-      tmax = fmaxf(tmax, v[r]);
-      const float rk = v[r] + (g ? g[code] : race_gumbel(key, ctr0 + (uint32_t)code));
-      if (rk > st.best) {  // codes increase along r and the tiles: the first of ties stays
-        st.best = rk;
-        st.bl = v[r];
-        st.bk = code;
-      }
+    const bool ok = full || code < K;
+    // INJ: g must be a valid row for every lane; the index is clamped so no load (even a
+    // speculated one) leaves the row
+    const float noise = INJ ? g[ok ? code : 0] : race_gumbel(key, ctr0 + (uint32_t)code);
+    const float rk = ok ? v[r] + noise : -INFINITY;
+    tmax = fmaxf(tmax, ok ? v[r] : -INFINITY);
+    if (rk > st.best) {  // codes increase along r and the tiles: the first of ties stays
+      st.best = rk;
+      st.bl = v[r];
+      st.bk = code;
     }
   }
-  if (tmax > st.m) {
-    if (st.m > -INFINITY) st.s *= exp((double)st.m - (double)tmax);
-    st.m = tmax;
-  }
+  // rescale to a new running max (an fp32 factor, like the terms)
+  const float mn = fmaxf(st.m, tmax);
+  st.s *= (double)(st.m > -INFINITY ? __expf(st.m - mn) : 1.0f);
+  st.m = mn;
   float ts = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r)
-    if (code0 + race_crow(r, h) < K) ts += __expf(v[r] - st.m);
+    ts += (full || code0 + race_crow(r, h) < K) ? __expf(v[r] - st.m) : 0.f;
   st.s += (double)ts;
 }
 

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void tls_pack_kernel(const float* __restrict__
 
 // one wave per 32 rows (token on the lane), the code tiles streamed through registers with
 // the next tile's operand groups loading while the current one multiplies
-template <int D>
+template <int D, bool INJ>
 __global__ __launch_bounds__(256) void tied_logits_sample_kernel(TlsArgs a) {
   constexpr int G = D / 8;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, r32 = lane & 31, h = lane >> 5;
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) void tied_logits_sample_kernel(TlsArgs a) {
         if (code < a.K) a.logits_out[m * a.K + code] = v[r];
       }
     }
-    race_tile(st, v, 32 * c, h, a.K, grow, key, ctr0);
+    race_tile<INJ>(st, v, 32 * c, h, a.K, grow, key, ctr0);
   }
   int pick;
   float p;
@@ -341,11 +341,13 @@ extern "C" int tvq_tied_logits_sample(const float* h, int64_t M, int64_t D, cons
   if (D == 128) {
     hipLaunchKernelGGL(tls_pack_kernel<128>, dim3((unsigned)(Kt + n)), dim3(256), 0, st, W, (int)K,
                        bias, ldb, wpk, bpk, Kt);
-    hipLaunchKernelGGL(tied_logits_sample_kernel<128>, dim3(blocks), dim3(256), 0, st, a);
+    if (gumbel) hipLaunchKernelGGL((tied_logits_sample_kernel<128, true>), dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tied_logits_sample_kernel<128, false>), dim3(blocks), dim3(256), 0, st, a);
   } else {
     hipLaunchKernelGGL(tls_pack_kernel<64>, dim3((unsigned)(Kt + n)), dim3(256), 0, st, W, (int)K,
                        bias, ldb, wpk, bpk, Kt);
-    hipLaunchKernelGGL(tied_logits_sample_kernel<64>, dim3(blocks), dim3(256), 0, st, a);
+    if (gumbel) hipLaunchKernelGGL((tied_logits_sample_kernel<64, true>), dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tied_logits_sample_kernel<64, false>), dim3(blocks), dim3(256), 0, st, a);
   }
   TVQ_PLAN("tied_logits_sample D=%d K=%d M=%lld", (int)D, (int)K, (long long)M);
   return launch_status("tvq_tied_logits_sample");

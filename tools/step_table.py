@@ -5,7 +5,7 @@ The last `steps` steps are cut at the AdamW launches (2 per step: stage1, stage2
 every kernel in them is tabulated: calls per step, average duration, time per step and
 share of the summed kernel time.  Also reports the wall span per step (the critical path
 of the concurrent streams) and launches per step.
-usage: python tools/step_table.py trace.csv [steps] [out.csv]"""
+usage: python tools/step_table.py trace.csv [steps] [out.csv] [start-marker kernel]"""
 import collections
 import csv
 import re
@@ -21,9 +21,16 @@ def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     out = sys.argv[3] if len(sys.argv) > 3 else None
-    ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
-    first = ends[-1 - 2 * steps] + 1
-    sel = rows[first:ends[-1] + 1]
+    marker = sys.argv[4] if len(sys.argv) > 4 else None
+    if marker:  # the last `steps` units each START at a `marker` launch (one per unit) and
+        # run to the end of the trace (tools/sampler_graph_prof.py: add_i64_kernel, the
+        # seed advance that opens every replayed sampling batch)
+        starts = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+        sel = rows[starts[-steps]:]
+    else:
+        ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
+        first = ends[-1 - 2 * steps] + 1
+        sel = rows[first:ends[-1] + 1]
     t0 = int(sel[0]["Start_Timestamp"])
     t1 = max(int(r["End_Timestamp"]) for r in sel)
     agg = collections.defaultdict(lambda: [0, 0])
