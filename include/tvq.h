@@ -509,9 +509,10 @@ int tvq_gelu_bwd(const float* dy, const float* x, int64_t n, float* dx, tvq_stre
  *   per layer: attn RMSNorm g, to_q, to_k, to_v (128, 128), to_out (128, 128),
  *              ff RMSNorm g, ff.0.0 W (128, 128), b (128), ff.2 W (128, 128), b (128),
  *   final_norm g, project_out W, pred_head.0 W, b, pred_head.2 W, b, bias (n, K+1).
- * logits: (B, n, K).  workspace: tvq_prior_lf_eval_workspace(depth, K) bytes (16-B aligned)
+ * logits: (B, n, K).  workspace: tvq_prior_lf_eval_workspace(depth, K, n, n_classes) bytes
+ * (16-B aligned)
  * receive the weights repacked once per call into the kernel's operand order. */
-int64_t tvq_prior_lf_eval_workspace(int64_t depth, int64_t K);
+int64_t tvq_prior_lf_eval_workspace(int64_t depth, int64_t K, int64_t n, int64_t n_classes);
 int tvq_prior_lf_eval(const int64_t* s, int64_t B, int64_t n, int64_t s_stride,
                       const int64_t* cls_idx, int64_t n_classes, int64_t width,
                       const float* const* weights, int64_t depth, int64_t K, float ln_eps,

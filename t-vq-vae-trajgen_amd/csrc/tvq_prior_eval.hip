@@ -72,6 +72,9 @@ struct PriorArgs {
   uint64_t offset;
   int64_t* sampled;
   float* selp;
+  // project_in folded into the embedding tables (one-wave kernel): rows tok [0, K+1),
+  // pos [K+1, K+1+n), cls [K+1+n, ...) of (table row) W_in^T, written by prior_fold_kernel
+  float* ftab;
 };
 
 __device__ __forceinline__ floatx16 pe_mfma(float a, float b, floatx16 c) {
@@ -149,9 +152,12 @@ __device__ __forceinline__ int64_t pe_tile_off(int idx, int depth) {
 
 // stream element e (float4) of tile t: group T4 = e / 64, lane l = e % 64 ->
 // W[row0 + (l & 31)][k0 + 32*(T4>>2) + 8*(T4&3) + 4*(l>>5) .. +3]
-__global__ __launch_bounds__(256) void prior_pack_kernel(PriorArgs a, float4* __restrict__ out) {
-  const PeTile t = pe_tile(a, blockIdx.x);
-  float4* dst = out + pe_tile_off(blockIdx.x, a.depth);
+// first: the stream's first tile (4 when project_in is folded into the tables)
+__global__ __launch_bounds__(256) void prior_pack_kernel(PriorArgs a, float4* __restrict__ out,
+                                                         int first) {
+  const int idx = (int)blockIdx.x + first;
+  const PeTile t = pe_tile(a, idx);
+  float4* dst = out + pe_tile_off(idx, a.depth) - pe_tile_off(first, a.depth);
   const int n4 = t.ns / 4 * 64;
   for (int e = threadIdx.x; e < n4; e += 256) {
     const int T4 = e >> 6, l = e & 63;
@@ -165,6 +171,30 @@ __global__ __launch_bounds__(256) void prior_pack_kernel(PriorArgs a, float4* __
     }
     dst[e] = v;
   }
+}
+
+// project_in folded into the tables the embedding reads: row r of tok_emb (r < K+1), pos_emb
+// (the next n) or cls_emb (the rest) times W_in^T -- cat(cls, tok + pos) W_in^T is then a
+// gather and an add of projected rows (the same function up to fp32 reassociation), and the
+// 256 project_in MFMAs per sequence and their 4 weight tiles leave the launch
+__global__ __launch_bounds__(128) void prior_fold_kernel(PriorArgs a) {
+  const int r = blockIdx.x, j = threadIdx.x;
+  const int V = a.K + 1;
+  const float* src = r < V ? a.tok_emb + (int64_t)r * PE_D
+                   : (r < V + a.n ? a.pos_emb + (int64_t)(r - V) * PE_D
+                                  : a.cls_emb + (int64_t)(r - V - a.n) * PE_D);
+  const float* w = a.w_in + (int64_t)j * PE_D;
+  float acc = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < PE_D; k += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(src + k);
+    const float4 y = *reinterpret_cast<const float4*>(w + k);
+    acc = fmaf(x.x, y.x, acc);
+    acc = fmaf(x.y, y.y, acc);
+    acc = fmaf(x.z, y.z, acc);
+    acc = fmaf(x.w, y.w, acc);
+  }
+  a.ftab[(int64_t)r * PE_D + j] = acc;
 }
 
 // a per-feature vector (D floats) in the register layout: v[tile][r] = p[32*tile + crow(r,h)]
@@ -342,22 +372,24 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
   const bool live = r32 < ntok;
   PeStream st;
   st.src = wstream;
-  st.ntiles = pe_ntiles(a.depth, a.K);
+  st.ntiles = pe_ntiles(a.depth, a.K) - 4;  // project_in's tiles are folded into ftab
   st.depth = a.depth;
   st.lane = l;
   pe_stream_begin(st);
-  // ---- embedding: cls row, then token + position rows (zeros on the padding lanes)
+  // ---- project_in(embedding) from the folded tables: the cls row, then token + position
+  // rows (zeros on the padding lanes)
   floatx16 x[4];
   {
+    const int V = a.K + 1;
     const float* src;
     const float* pos = nullptr;
     if (r32 == 0) {
       const int64_t c = a.cls ? a.cls[b] : (int64_t)a.n_classes;
-      src = a.cls_emb + c * PE_D;
+      src = a.ftab + (V + n + c) * PE_D;
     } else {
       const int i = live ? r32 - 1 : 0;
-      src = a.tok_emb + a.s[(int64_t)b * a.ss + i] * PE_D;
-      pos = a.pos_emb + (int64_t)i * PE_D;
+      src = a.ftab + a.s[(int64_t)b * a.ss + i] * PE_D;
+      pos = a.ftab + (int64_t)(V + i) * PE_D;
     }
     pe_load_vec(src, h, x);
     if (pos) {
@@ -373,14 +405,8 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
 #pragma unroll
       for (int r = 0; r < 16; ++r) x[t][r] = live ? x[t][r] : 0.f;
   }
-  // ---- project_in (no bias) + post_emb_norm (x-transformers LayerNorm: gamma only)
-  {
-    floatx16 y[4];
-    pe_linear(st, x, y);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) x[t] = y[t];
-    pe_layernorm(x, a.post_gamma, nullptr, 1e-5f, h);
-  }
+  // ---- post_emb_norm (x-transformers LayerNorm: gamma only)
+  pe_layernorm(x, a.post_gamma, nullptr, 1e-5f, h);
   // ---- encoder layers (pre-norm, eval: every branch runs)
   for (int li = 0; li < a.depth; ++li) {
     const PriorLayer L = a.L[li];
@@ -1049,10 +1075,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 using namespace tvq;
 
 // bytes of the packed weight stream tvq_prior_lf_eval needs as its workspace
-extern "C" int64_t tvq_prior_lf_eval_workspace(int64_t depth, int64_t K) {
-  if (depth < 1 || depth > PE_MAXDEPTH || K < 1) return -1;
+extern "C" int64_t tvq_prior_lf_eval_workspace(int64_t depth, int64_t K, int64_t n,
+                                               int64_t n_classes) {
+  if (depth < 1 || depth > PE_MAXDEPTH || K < 1 || n < 1 || n_classes < 0) return -1;
   const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32;  // 64-step tiles
-  return (tiles64 * 1024 + depth * 8 * 512) * 16;
+  const int64_t stream = (tiles64 * 1024 + depth * 8 * 512) * 16;
+  return stream + (K + 1 + n + n_classes + 1) * PE_D * 4;  // + the folded tables
 }
 
 static int prior_lf_eval_launch(PriorArgs& a, const int64_t* s, int64_t B, int64_t n,
@@ -1099,7 +1127,11 @@ static int prior_lf_eval_launch(PriorArgs& a, const int64_t* s, int64_t B, int64
     hipLaunchKernelGGL(prior_lf_eval2_kernel, dim3((unsigned)B), dim3(128), 0, st, a,
                        (const float4*)ws);
   } else {
-    hipLaunchKernelGGL(prior_pack_kernel, dim3((unsigned)ntiles), dim3(256), 0, st, a, ws);
+    const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32;
+    a.ftab = reinterpret_cast<float*>(ws + tiles64 * 1024 + depth * 8 * 512);
+    hipLaunchKernelGGL(prior_fold_kernel, dim3((unsigned)(K + 1 + n + n_classes + 1)), dim3(128), 0,
+                       st, a);
+    hipLaunchKernelGGL(prior_pack_kernel, dim3((unsigned)(ntiles - 4)), dim3(256), 0, st, a, ws, 4);
     hipLaunchKernelGGL(prior_lf_eval_kernel, dim3((unsigned)B), dim3(64), 0, st, a,
                        (const float4*)ws);
   }

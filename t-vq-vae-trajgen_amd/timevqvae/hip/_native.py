@@ -134,7 +134,7 @@ sig("tvq_upsample_nearest_bwd", P, I64, I64, I64, P, P)
 sig("tvq_gelu_fwd", P, I64, P, P)
 sig("tvq_gelu_bwd", P, P, I64, P, P)
 # --- MaskGIT sampling ------------------------------------------------------------
-sig("tvq_prior_lf_eval_workspace", I64, I64, restype=I64)
+sig("tvq_prior_lf_eval_workspace", I64, I64, I64, I64, restype=I64)
 sig("tvq_prior_lf_eval", P, I64, I64, I64, P, I64, I64, P, I64, I64, F32, P, P, P)
 sig("tvq_prior_lf_eval_sample", P, I64, I64, I64, P, I64, I64, P, I64, I64, F32, I64, P, P, U64,
     P, P, P, P, P)

@@ -563,8 +563,8 @@ def _prior_lf_args(tf, s, class_idx):
     cls = class_idx.reshape(-1).long().contiguous() if class_idx is not None else None
     depth = len(enc.layers) // 2
     K = tf.codebook_size
-    ws = torch.empty(value("tvq_prior_lf_eval_workspace", depth, K), device=s.device,
-                     dtype=torch.uint8)
+    ws = torch.empty(value("tvq_prior_lf_eval_workspace", depth, K, s.shape[1], tf.n_classes),
+                     device=s.device, dtype=torch.uint8)
     return s, cls, arr, depth, K, ws
 
 
