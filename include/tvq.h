@@ -520,13 +520,15 @@ int tvq_prior_lf_eval(const int64_t* s, int64_t B, int64_t n, int64_t s_stride,
 /* tvq_prior_lf_eval followed by the categorical draw of tvq_maskgit_sample (same race, same
  * noise counters) in the same launch: the tied logits are drawn from in registers and never
  * written (logits, nullable, receives them for checking).  s doubles as the tokens whose
- * mask_id entries are drawn (the others are kept, p = +inf). */
+ * mask_id entries are drawn (the others are kept, p = +inf).  workspace_ready != 0: the
+ * workspace already holds this call's weights packed (an earlier call with the same weights,
+ * e.g. the previous decoding step): the packing launches are skipped. */
 int tvq_prior_lf_eval_sample(const int64_t* s, int64_t B, int64_t n, int64_t s_stride,
                              const int64_t* cls_idx, int64_t n_classes, int64_t width,
                              const float* const* weights, int64_t depth, int64_t K, float ln_eps,
                              int64_t mask_id, const float* gumbel, const int64_t* seed_ptr,
                              uint64_t offset, int64_t* sampled, float* selp, float* logits,
-                             void* workspace, tvq_stream_t stream);
+                             void* workspace, int64_t workspace_ready, tvq_stream_t stream);
 
 /* ---------------------------------------------------------------- MaskGIT sampling
  * One iterative-decoding step of MaskGIT.first_pass / second_pass (maskgit.py:294-411):

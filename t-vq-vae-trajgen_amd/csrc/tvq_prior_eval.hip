@@ -362,6 +362,49 @@ __device__ __forceinline__ void pe_layernorm(floatx16 (&x)[4], const float* __re
     }
 }
 
+// The tied logits + race of the one-wave kernel, software-pipelined: tile c + 1's MFMA chain
+// and tile c's race (VALU only, independent of it) sit in one basic block, so the scheduler
+// can issue the race into the MFMA chain's gaps instead of after it.  The stream ends with a
+// zero tile, consumed by the last iteration's (discarded) chain.  lout (tests): the logits.
+template <bool INJ, bool LOUT>
+__device__ __forceinline__ void pe_draw(PeStream& st, const floatx16 (&x)[4], RaceState& rs,
+                                        const float* __restrict__ brow,
+                                        const float* __restrict__ grow, uint32_t key,
+                                        uint32_t ctr0, float* __restrict__ lout, bool store_ok,
+                                        int K, int h) {
+  auto bx = [&](int tt) { return x[tt >> 4][tt & 15]; };
+  auto bias = [&](int c0, float (&v)[16]) {  // clamped: the past-the-end tile reads row K - 1
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = brow[min(c0 + race_crow(r, h), K - 1)];
+  };
+  float vb[16];
+  bias(0, vb);
+  floatx16 acc;
+  pe_zero(acc);
+  acc = pe_gemm<true, 64>(st, bx, acc);
+  for (int c0 = 0; c0 < K; c0 += 32) {
+    float vn[16];
+    bias(c0 + 32, vn);  // before the next chain's stream loads (loads return in order)
+    floatx16 accn;
+    pe_zero(accn);
+    accn = pe_gemm<true, 64>(st, bx, accn);
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = acc[r] + vb[r];
+    if (LOUT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int code = c0 + race_crow(r, h);
+        if (store_ok && code < K) lout[code] = v[r];
+      }
+    }
+    race_tile<INJ>(rs, v, c0, h, K, grow, key, ctr0);
+    acc = accn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) vb[r] = vn[r];
+  }
+}
+
 // one wave (64 threads) per sequence
 __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
                                                            const float4* __restrict__ wstream) {
@@ -372,7 +415,8 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
   const bool live = r32 < ntok;
   PeStream st;
   st.src = wstream;
-  st.ntiles = pe_ntiles(a.depth, a.K) - 4;  // project_in's tiles are folded into ftab
+  // project_in's tiles are folded into ftab; draw mode ends with one zero code tile
+  st.ntiles = pe_ntiles(a.depth, a.K) - 4 + (a.sampled ? 1 : 0);
   st.depth = a.depth;
   st.lane = l;
   pe_stream_begin(st);
@@ -510,31 +554,20 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
     // nothing): race_tile<true> dereferences it unconditionally
     const float* grow = a.gumbel ? a.gumbel + t * a.K : nullptr;
     const uint32_t key = a.gumbel ? 0u : race_key(mix_seed(a.seed_ptr, a.offset));
-    float* lout = (a.logits && tok_ok) ? a.logits + t * a.K : nullptr;
+    // the variant is chosen on wave-uniform arguments only (the MFMA chains inside need every
+    // lane); the cls / padding lanes' logits stores are predicated off inside
+    float* lout = a.logits ? a.logits + t * a.K : nullptr;
     RaceState rs;
     race_init(rs);
-    for (int c0 = 0; c0 < a.K; c0 += 32) {
-      float v[16];  // the bias first: loads return in order, the stream prefetch comes next
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int code = c0 + race_crow(r, h);
-        v[r] = code < a.K ? brow[code] : 0.f;
-      }
-      floatx16 acc;
-      pe_zero(acc);
-      acc = pe_gemm<true, 64>(st, [&](int tt) { return x[tt >> 4][tt & 15]; }, acc);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] += acc[r];
-      if (lout) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int code = c0 + race_crow(r, h);
-          if (code < a.K) lout[code] = v[r];
-        }
-      }
-      if (a.gumbel) race_tile<true>(rs, v, c0, h, a.K, grow, key, (uint32_t)t * (uint32_t)a.K);
-      else race_tile<false>(rs, v, c0, h, a.K, grow, key, (uint32_t)t * (uint32_t)a.K);
-    }
+    const uint32_t ctr0 = (uint32_t)t * (uint32_t)a.K;
+    if (!a.gumbel && !a.logits)
+      pe_draw<false, false>(st, x, rs, brow, nullptr, key, ctr0, nullptr, tok_ok, a.K, h);
+    else if (!a.gumbel)
+      pe_draw<false, true>(st, x, rs, brow, nullptr, key, ctr0, lout, tok_ok, a.K, h);
+    else if (!a.logits)
+      pe_draw<true, false>(st, x, rs, brow, grow, key, ctr0, nullptr, tok_ok, a.K, h);
+    else
+      pe_draw<true, true>(st, x, rs, brow, grow, key, ctr0, lout, tok_ok, a.K, h);
     int pick;
     float p;
     race_finish(rs, pick, p);
@@ -1078,7 +1111,8 @@ using namespace tvq;
 extern "C" int64_t tvq_prior_lf_eval_workspace(int64_t depth, int64_t K, int64_t n,
                                                int64_t n_classes) {
   if (depth < 1 || depth > PE_MAXDEPTH || K < 1 || n < 1 || n_classes < 0) return -1;
-  const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32;  // 64-step tiles
+  // 64-step tiles (+1: the draw's zero tile)
+  const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32 + 1;
   const int64_t stream = (tiles64 * 1024 + depth * 8 * 512) * 16;
   return stream + (K + 1 + n + n_classes + 1) * PE_D * 4;  // + the folded tables
 }
@@ -1086,8 +1120,8 @@ extern "C" int64_t tvq_prior_lf_eval_workspace(int64_t depth, int64_t K, int64_t
 static int prior_lf_eval_launch(PriorArgs& a, const int64_t* s, int64_t B, int64_t n,
                                 int64_t s_stride, const int64_t* cls_idx, int64_t n_classes,
                                 int64_t width, const float* const* weights, int64_t depth,
-                                int64_t K, float ln_eps, void* workspace, tvq_stream_t stream,
-                                const char* name) {
+                                int64_t K, float ln_eps, void* workspace, bool ready,
+                                tvq_stream_t stream, const char* name) {
   TVQ_CHECK_ARG(s && weights && B >= 1 && n >= 1 && n + 1 <= 32 && K >= 1 &&
                     width == PE_D && depth >= 1 && depth <= PE_MAXDEPTH && n_classes >= 0,
                 "tvq_prior_lf_eval: unsupported shape (width 128, n + 1 <= 32, depth <= 8)");
@@ -1123,15 +1157,19 @@ static int prior_lf_eval_launch(PriorArgs& a, const int64_t* s, int64_t B, int64
   if (two) {
     // both waves' streams: 6 + 16 * depth tiles each, plus the code tiles
     const int ntiles2 = 12 + 2 * PE2_PER_LAYER * (int)depth + (int)((K + 31) / 32);
-    hipLaunchKernelGGL(prior_pack2_kernel, dim3((unsigned)ntiles2), dim3(256), 0, st, a, ws);
+    if (!ready)
+      hipLaunchKernelGGL(prior_pack2_kernel, dim3((unsigned)ntiles2), dim3(256), 0, st, a, ws);
     hipLaunchKernelGGL(prior_lf_eval2_kernel, dim3((unsigned)B), dim3(128), 0, st, a,
                        (const float4*)ws);
   } else {
-    const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32;
+    const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32 + 1;  // as the workspace
     a.ftab = reinterpret_cast<float*>(ws + tiles64 * 1024 + depth * 8 * 512);
-    hipLaunchKernelGGL(prior_fold_kernel, dim3((unsigned)(K + 1 + n + n_classes + 1)), dim3(128), 0,
-                       st, a);
-    hipLaunchKernelGGL(prior_pack_kernel, dim3((unsigned)(ntiles - 4)), dim3(256), 0, st, a, ws, 4);
+    if (!ready) {  // weights -> folded tables + packed stream (+ the zero tile the draw's
+                   // pipelined loop reads past the last code tile)
+      hipLaunchKernelGGL(prior_fold_kernel, dim3((unsigned)(K + 1 + n + n_classes + 1)), dim3(128),
+                         0, st, a);
+      hipLaunchKernelGGL(prior_pack_kernel, dim3((unsigned)(ntiles - 3)), dim3(256), 0, st, a, ws, 4);
+    }
     hipLaunchKernelGGL(prior_lf_eval_kernel, dim3((unsigned)B), dim3(64), 0, st, a,
                        (const float4*)ws);
   }
@@ -1148,7 +1186,7 @@ extern "C" int tvq_prior_lf_eval(const int64_t* s, int64_t B, int64_t n, int64_t
   PriorArgs a = {};
   a.logits = logits;
   return prior_lf_eval_launch(a, s, B, n, s_stride, cls_idx, n_classes, width, weights, depth, K,
-                              ln_eps, workspace, stream, "tvq_prior_lf_eval");
+                              ln_eps, workspace, false, stream, "tvq_prior_lf_eval");
 }
 
 extern "C" int tvq_prior_lf_eval_sample(const int64_t* s, int64_t B, int64_t n, int64_t s_stride,
@@ -1157,7 +1195,8 @@ extern "C" int tvq_prior_lf_eval_sample(const int64_t* s, int64_t B, int64_t n, 
                                         float ln_eps, int64_t mask_id, const float* gumbel,
                                         const int64_t* seed_ptr, uint64_t offset,
                                         int64_t* sampled, float* selp, float* logits,
-                                        void* workspace, tvq_stream_t stream) {
+                                        void* workspace, int64_t workspace_ready,
+                                        tvq_stream_t stream) {
   TVQ_CHECK_ARG(sampled && selp, "tvq_prior_lf_eval_sample: null outputs");
   TVQ_CHECK_ARG(gumbel || seed_ptr, "tvq_prior_lf_eval_sample: need gumbel noise or a seed");
   TVQ_CHECK_ARG(gumbel || B * n * K < (int64_t)1 << 32, "tvq_prior_lf_eval_sample: B n K >= 2^32");
@@ -1167,5 +1206,6 @@ extern "C" int tvq_prior_lf_eval_sample(const int64_t* s, int64_t B, int64_t n, 
   a.sampled = sampled; a.selp = selp;
   TVQ_PLAN("prior_lf_eval_sample B=%lld n=%lld K=%lld", (long long)B, (long long)n, (long long)K);
   return prior_lf_eval_launch(a, s, B, n, s_stride, cls_idx, n_classes, width, weights, depth, K,
-                              ln_eps, workspace, stream, "tvq_prior_lf_eval_sample");
+                              ln_eps, workspace, workspace_ready != 0, stream,
+                              "tvq_prior_lf_eval_sample");
 }

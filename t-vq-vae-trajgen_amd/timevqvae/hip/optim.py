@@ -88,7 +88,7 @@ class FusedAdamW(torch.optim.Optimizer):
     def push_lr(self):
         """Write param_groups[0]['lr'] into the device {lr, step} pair (for graph replays,
         whose captured update reads the lr from the device: step(lr_on_device=True))."""
-        self.lr_step[0:1].fill_(float(self.param_groups[0]["lr"]))
+        call("tvq_fill", ptr(self.lr_step), 1, float(self.param_groups[0]["lr"]), stream_ptr())
 
     def zero_grad(self, set_to_none: bool = False):
         # gradients accumulate in place into the flat buffer views

@@ -179,6 +179,64 @@ def linear_act(x, weight, bias=None, gelu=False):
     return _LinearAct.apply(x, weight, bias, 1 if gelu else 0)
 
 
+# ---------------------------------------------------------------- fused feed-forward
+FUSED_FF = os.environ.get("TVQ_FUSED_FF", "1") != "0"
+
+
+class _FusedFF(torch.autograd.Function):
+    """r + gate * (dropout(GELU(xn W1^T + b1)) W2^T + b2) with D = inner = 128 in one launch
+    forward and one backward (csrc/tvq_ffn.hip; x-transformers FeedForward in the pre-norm
+    residual, bidirectional_transformer.py:92-110).  Weight / bias gradients go through the
+    grouped weight-gradient path like every Linear's; dW2 / db2 are taken from the ungated
+    output gradient: when the layer-dropout gate is 0 the branch's segment is skipped by
+    FusedAdamW (its gradient is never read), and when it is 1 the two are the same."""
+
+    @staticmethod
+    def forward(ctx, xn, r, w1, b1, w2, b2, gate, p, site):
+        shp = xn.shape
+        x2 = xn.reshape(-1, 128).contiguous()
+        r2 = r.reshape(-1, 128).contiguous()
+        M = x2.shape[0]
+        y, pre, hd = (torch.empty_like(x2) for _ in range(3))
+        seed = rng.seed_tensor(xn.device) if p > 0 else None
+        off = rng.call_offset(site) if p > 0 else 0
+        call("tvq_ffn_fwd", ptr(x2), ptr(r2), M, 128, ptr(w1), ptr(b1), ptr(w2), ptr(b2),
+             ptr(gate), float(p), ptr(seed), off, ptr(y), ptr(pre), ptr(hd), stream_ptr())
+        ctx.save_for_backward(x2, pre, hd, w1, w2)
+        ctx.cfg = (float(p), off, shp)
+        ctx.seed, ctx.gate = seed, gate
+        ctx.params = (w1, b1, w2, b2)
+        ctx.wg_tag = wgrad.current_tag()
+        return y.reshape(shp)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, pre, hd, w1, w2 = ctx.saved_tensors
+        p, off, shp = ctx.cfg
+        g2 = gy.reshape(-1, 128).contiguous()
+        M = g2.shape[0]
+        d_pre, dxn = torch.empty_like(g2), torch.empty_like(g2)
+        call("tvq_ffn_bwd", ptr(g2), ptr(pre), M, 128, ptr(w1), ptr(w2), ptr(ctx.gate), p,
+             ptr(ctx.seed), off, ptr(d_pre), ptr(dxn), stream_ptr())
+        need = ctx.needs_input_grad
+        W1p, b1p, W2p, b2p = ctx.params
+        dw2 = weight_grad(g2, hd, W2p, M, 128, 128, ctx.wg_tag) if need[4] else None
+        db2 = _bias_grad_rows(g2, grad_sink(b2p)) if need[5] else None
+        dw1 = weight_grad(d_pre, x2, W1p, M, 128, 128, ctx.wg_tag) if need[2] else None
+        db1 = _bias_grad_rows(d_pre, grad_sink(b1p)) if need[3] else None
+        return (dxn.reshape(shp) if need[0] else None, gy if need[1] else None, dw1, db1, dw2,
+                db2, None, None, None)
+
+
+def fused_ff_supported(x, w1, w2):
+    return (FUSED_FF and x.is_cuda and x.shape[-1] == 128 and tuple(w1.shape) == (128, 128)
+            and tuple(w2.shape) == (128, 128))
+
+
+def fused_ff(xn, r, w1, b1, w2, b2, gate, p, site):
+    return _FusedFF.apply(xn, r, w1, b1, w2, b2, gate, float(p), int(site))
+
+
 # ---------------------------------------------------------------- attention
 class _Attention(torch.autograd.Function):
     @staticmethod
@@ -546,7 +604,7 @@ def prior_lf_eval_supported(tf, s):
                p.data_ptr() % 16 == 0 for p in tf.parameters())
 
 
-def _prior_lf_args(tf, s, class_idx):
+def _prior_lf_args(tf, s, class_idx, ws=None):
     import ctypes
     enc = tf.blocks.attn_layers
     w = [tf.tok_emb_l.weight, tf.pos_emb.weight, tf.class_condition_emb.weight,
@@ -563,9 +621,17 @@ def _prior_lf_args(tf, s, class_idx):
     cls = class_idx.reshape(-1).long().contiguous() if class_idx is not None else None
     depth = len(enc.layers) // 2
     K = tf.codebook_size
-    ws = torch.empty(value("tvq_prior_lf_eval_workspace", depth, K, s.shape[1], tf.n_classes),
-                     device=s.device, dtype=torch.uint8)
+    if ws is None:
+        ws = prior_lf_eval_workspace(tf, s)
     return s, cls, arr, depth, K, ws
+
+
+def prior_lf_eval_workspace(tf, s):
+    """The packed-weight workspace of tvq_prior_lf_eval(_sample) for prior `tf` and tokens
+    like `s` (reusable across calls with the same weights: see prior_lf_eval_sample)."""
+    depth = len(tf.blocks.attn_layers.layers) // 2
+    return torch.empty(value("tvq_prior_lf_eval_workspace", depth, tf.codebook_size, s.shape[1],
+                             tf.n_classes), device=s.device, dtype=torch.uint8)
 
 
 def prior_lf_eval(tf, s, class_idx=None):
@@ -580,12 +646,14 @@ def prior_lf_eval(tf, s, class_idx=None):
     return logits
 
 
-def prior_lf_eval_sample(tf, s, class_idx, mask_id, gumbel=None, site=0, want_logits=False):
+def prior_lf_eval_sample(tf, s, class_idx, mask_id, gumbel=None, site=0, want_logits=False,
+                         ws=None, ready=False):
     """prior_lf_eval + hip.sample.maskgit_sample in ONE launch: the tied logits are drawn
     from by the race in registers and never written (tvq_prior_lf_eval_sample).  Returns
-    (sampled, p(sampled)[, logits])."""
+    (sampled, p(sampled)[, logits]).  ws / ready: a workspace from an earlier call with the
+    same weights (ready=True skips packing them again: the decoding steps after the first)."""
     from . import rng
-    s, cls, arr, depth, K, ws = _prior_lf_args(tf, s, class_idx)
+    s, cls, arr, depth, K, ws = _prior_lf_args(tf, s, class_idx, ws)
     B, n = s.shape
     dev = s.device
     sampled = torch.empty((B, n), device=dev, dtype=torch.int64)
@@ -596,7 +664,7 @@ def prior_lf_eval_sample(tf, s, class_idx, mask_id, gumbel=None, site=0, want_lo
     call("tvq_prior_lf_eval_sample", ptr(s), B, n, s.stride(0), ptr(cls), tf.n_classes, 128, arr,
          depth, K, float(tf.pred_head[2].eps), int(mask_id),
          ptr(gumbel.contiguous() if gumbel is not None else None), ptr(seed), off,
-         ptr(sampled), ptr(selp), ptr(logits), ptr(ws), stream_ptr())
+         ptr(sampled), ptr(selp), ptr(logits), ptr(ws), int(bool(ready)), stream_ptr())
     return (sampled, selp, logits) if want_logits else (sampled, selp)
 
 

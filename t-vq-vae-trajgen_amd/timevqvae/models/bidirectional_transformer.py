@@ -28,9 +28,10 @@ from ..hip import rng, streams
 from ..hip.conv import PackCache, _immediate, _keep, conv2d
 from ..hip.linear import gemm, linear
 from ..hip.norm import bn_snake
-from ..hip.xf import (batch_colsum, drop_first_token, embed_assemble, embedding, gelu,
+from ..hip.xf import (batch_colsum, drop_first_token, embed_assemble, embedding, fused_ff,
+                      fused_ff_supported, gelu,
                       layer_norm, linear_act, prior_lf_eval, prior_lf_eval_sample,
-                      prior_lf_eval_supported, qkv_attention, rmsnorm, rmsnorm_res,
+                      prior_lf_eval_supported, prior_lf_eval_workspace, qkv_attention, rmsnorm, rmsnorm_res,
                       upsample_nearest_t)
 from ..hip._native import call, grad_sink, ptr, stream_ptr, value
 from ..hip.sample import codebook_gather_nchw, full_tokens, maskgit_sample, tied_logits_sample
@@ -90,8 +91,13 @@ class FeedForward(nn.Module):
 
     def forward(self, x, residual, gate=None):
         lin1 = self.ff[0][0]
-        h = linear_act(x, lin1.weight, lin1.bias, gelu=True)
         p = self.ff[1].p if self.training else 0.0
+        lin2 = self.ff[2]
+        if fused_ff_supported(x, lin1.weight, lin2.weight):
+            # the whole branch + residual in one launch each way (hip.xf.fused_ff)
+            return fused_ff(x, residual, lin1.weight, lin1.bias, lin2.weight, lin2.bias, gate, p,
+                            self._site)
+        h = linear_act(x, lin1.weight, lin1.bias, gelu=True)
         if p > 0:
             h = dropout(h, p, self._site)
         lin2 = self.ff[2]
@@ -345,6 +351,7 @@ class BidirectionalTransformer(nn.Module):
         kind = kind.lower()
         assert kind in ["lf", "hf"], "invalid `kind`."
         self.kind = kind
+        self._eval_ws = {}  # (device, n) -> packed-weight workspace of the LF eval launch
         self.num_tokens = num_tokens
         self.n_classes = n_classes
         self.p_unconditional = p_unconditional
@@ -441,17 +448,26 @@ class BidirectionalTransformer(nn.Module):
         return self._head(drop_first_token(embed))
 
     def sample(self, s_M_l, s_M_h=None, class_condition=None, mask_id=None, gumbel=None,
-               site=0, want_logits=False):
+               site=0, want_logits=False, first=True):
         """One categorical draw per token of this prior's logits (maskgit.py:302-326): the
         sampled codes (known tokens -- the ones != mask_id of the band being decoded -- kept)
         and p(sampled) (+inf for known tokens).  The HF prior in eval mode draws straight
         from its head (hip.sample.tied_logits_sample: the logits never reach memory);
         otherwise the logits are formed and hip.sample.maskgit_sample draws from them.
-        want_logits: also return the logits (tests)."""
+        want_logits: also return the logits (tests).  first=False: the weights are those of
+        the previous call (the decoding steps after a pass's first), so the LF launch reuses
+        their packed copy."""
         s = s_M_l if self.kind == "lf" else s_M_h
         if self.kind == "lf" and FUSED_SAMPLE and prior_lf_eval_supported(self, s_M_l):
+            key = (s_M_l.device, s_M_l.shape[1])
+            ws = self._eval_ws.get(key)
+            fresh = ws is None
+            if fresh:
+                ws = prior_lf_eval_workspace(self, s_M_l)
+                self._eval_ws[key] = ws
             return prior_lf_eval_sample(self, s_M_l, class_condition, mask_id, gumbel=gumbel,
-                                        site=site, want_logits=want_logits)
+                                        site=site, want_logits=want_logits, ws=ws,
+                                        ready=not (first or fresh))
         if (self.kind == "hf" and not self.training and FUSED_SAMPLE
                 and self.tok_emb_h.weight.shape[1] in (64, 128)):
             return tied_logits_sample(self._head_hf_eval(s_M_l, s_M_h, class_condition),

@@ -210,7 +210,7 @@ class MaskGIT(nn.Module):
                               want_masking=True)
 
     def sample_tokens(self, transformer, class_condition, mask_id, *s_in, gumbel=None,
-                      want_logits=False):
+                      want_logits=False, first=True):
         """The categorical draw of one decoding step (maskgit.py:302-326): masked_prediction's
         logits -> Categorical(logits).sample() -> (sampled with known tokens kept,
         p(sampled)).  Without guidance (cfg 1 or no class) the prior draws straight from its
@@ -219,7 +219,7 @@ class MaskGIT(nn.Module):
         if class_condition is None or self.cfg_scale == 1.0:
             return transformer.sample(*s_in, class_condition=class_condition, mask_id=mask_id,
                                       gumbel=gumbel, site=self._site_sample,
-                                      want_logits=want_logits)
+                                      want_logits=want_logits, first=first)
         logits = self.masked_prediction(transformer, class_condition, *s_in)
         out = maskgit_sample(logits, s_in[-1], mask_id, gumbel=gumbel, site=self._site_sample)
         return out + (logits,) if want_logits else out
@@ -230,7 +230,7 @@ class MaskGIT(nn.Module):
         for t in range(T):
             ratio = 1.0 * (t + 1) / T
             k = mask_len(n0, gamma(ratio))
-            sampled, selp = sample_call(s)
+            sampled, selp = sample_call(s, t == 0)  # later steps reuse the packed weights
             s = maskgit_remask(selp, k, temperature * (1.0 - ratio), sampled, mask_id,
                                site=self._site_sample)
         return s
@@ -240,7 +240,8 @@ class MaskGIT(nn.Module):
         """maskgit.py:294-355."""
         mask_id = self.mask_token_ids["lf"]
         return self._decode_pass(
-            lambda s: self.sample_tokens(self.transformer_l, class_condition, mask_id, s), s_l,
+            lambda s, first: self.sample_tokens(self.transformer_l, class_condition, mask_id, s,
+                                                first=first), s_l,
             mask_id, self.T["lf"], self.choice_temperature_l,
             unknown_number_in_the_beginning_l, gamma)
 
@@ -249,7 +250,8 @@ class MaskGIT(nn.Module):
         """maskgit.py:357-411."""
         mask_id = self.mask_token_ids["hf"]
         return self._decode_pass(
-            lambda s: self.sample_tokens(self.transformer_h, class_condition, mask_id, s_l, s),
+            lambda s, first: self.sample_tokens(self.transformer_h, class_condition, mask_id, s_l,
+                                                s, first=first),
             s_h, mask_id, self.T["hf"], self.choice_temperature_h,
             unknown_number_in_the_beginning_h, gamma)
 

@@ -1,7 +1,7 @@
 """List every PyTorch-native device op of one eager joint step (or sampler batch) with where it
 comes from: the autograd node running it (backward) or the Python call site (forward).
 Views, allocations and metadata ops launch no kernel and are skipped.
-usage: python tools/aten_sources.py [sampler]"""
+usage: python tools/aten_sources.py [sampler|capture]"""
 import collections
 import os
 import sys
@@ -62,6 +62,14 @@ def main():
                 x_l = mg.decode_token_ind_to_timeseries(s_l, "lf")
                 x_h = mg.decode_token_ind_to_timeseries(s_h, "hf")
                 add_losses(x_l, x_h)
+    elif sys.argv[1:] == ["capture"]:  # the ops recorded into the step graph (and warmup)
+        log = Log()
+        with log:
+            tr.capture(batch)
+        torch.cuda.synchronize()
+        for (name, site), n in sorted(log.sites.items(), key=lambda x: -x[1]):
+            print(f"{n:4d} {name:40s} {site}")
+        return
     else:
         def work():
             tr.step(batch)
