@@ -362,10 +362,11 @@ __device__ __forceinline__ void pe_layernorm(floatx16 (&x)[4], const float* __re
     }
 }
 
-// The tied logits + race of the one-wave kernel, software-pipelined: tile c + 1's MFMA chain
-// and tile c's race (VALU only, independent of it) sit in one basic block, so the scheduler
-// can issue the race into the MFMA chain's gaps instead of after it.  The stream ends with a
-// zero tile, consumed by the last iteration's (discarded) chain.  lout (tests): the logits.
+// The tied logits + race of the one-wave kernel; the variants are compile-time so the
+// product path (device noise, no logits copy) has no branch in its loop.  (Software-
+// pipelining tile c + 1's MFMA chain against tile c's race in one basic block measured
+// slower: 328 vs 317 us per launch, the extra live accumulator pushing values into AGPR
+// moves.)  lout (tests): the logits.
 template <bool INJ, bool LOUT>
 __device__ __forceinline__ void pe_draw(PeStream& st, const floatx16 (&x)[4], RaceState& rs,
                                         const float* __restrict__ brow,
@@ -373,24 +374,15 @@ __device__ __forceinline__ void pe_draw(PeStream& st, const floatx16 (&x)[4], Ra
                                         uint32_t ctr0, float* __restrict__ lout, bool store_ok,
                                         int K, int h) {
   auto bx = [&](int tt) { return x[tt >> 4][tt & 15]; };
-  auto bias = [&](int c0, float (&v)[16]) {  // clamped: the past-the-end tile reads row K - 1
+  for (int c0 = 0; c0 < K; c0 += 32) {
+    float v[16];  // the bias first: loads return in order, the stream prefetch comes next
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = brow[min(c0 + race_crow(r, h), K - 1)];
-  };
-  float vb[16];
-  bias(0, vb);
-  floatx16 acc;
-  pe_zero(acc);
-  acc = pe_gemm<true, 64>(st, bx, acc);
-  for (int c0 = 0; c0 < K; c0 += 32) {
-    float vn[16];
-    bias(c0 + 32, vn);  // before the next chain's stream loads (loads return in order)
-    floatx16 accn;
-    pe_zero(accn);
-    accn = pe_gemm<true, 64>(st, bx, accn);
-    float v[16];
+    floatx16 acc;
+    pe_zero(acc);
+    acc = pe_gemm<true, 64>(st, bx, acc);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = acc[r] + vb[r];
+    for (int r = 0; r < 16; ++r) v[r] += acc[r];
     if (LOUT) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -399,9 +391,6 @@ __device__ __forceinline__ void pe_draw(PeStream& st, const floatx16 (&x)[4], Ra
       }
     }
     race_tile<INJ>(rs, v, c0, h, K, grow, key, ctr0);
-    acc = accn;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) vb[r] = vn[r];
   }
 }
 
@@ -415,8 +404,7 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
   const bool live = r32 < ntok;
   PeStream st;
   st.src = wstream;
-  // project_in's tiles are folded into ftab; draw mode ends with one zero code tile
-  st.ntiles = pe_ntiles(a.depth, a.K) - 4 + (a.sampled ? 1 : 0);
+  st.ntiles = pe_ntiles(a.depth, a.K) - 4;  // project_in's tiles are folded into ftab
   st.depth = a.depth;
   st.lane = l;
   pe_stream_begin(st);
@@ -1111,8 +1099,7 @@ using namespace tvq;
 extern "C" int64_t tvq_prior_lf_eval_workspace(int64_t depth, int64_t K, int64_t n,
                                                int64_t n_classes) {
   if (depth < 1 || depth > PE_MAXDEPTH || K < 1 || n < 1 || n_classes < 0) return -1;
-  // 64-step tiles (+1: the draw's zero tile)
-  const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32 + 1;
+  const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32;  // 64-step tiles
   const int64_t stream = (tiles64 * 1024 + depth * 8 * 512) * 16;
   return stream + (K + 1 + n + n_classes + 1) * PE_D * 4;  // + the folded tables
 }
@@ -1162,13 +1149,12 @@ static int prior_lf_eval_launch(PriorArgs& a, const int64_t* s, int64_t B, int64
     hipLaunchKernelGGL(prior_lf_eval2_kernel, dim3((unsigned)B), dim3(128), 0, st, a,
                        (const float4*)ws);
   } else {
-    const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32 + 1;  // as the workspace
+    const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32;  // as the workspace
     a.ftab = reinterpret_cast<float*>(ws + tiles64 * 1024 + depth * 8 * 512);
-    if (!ready) {  // weights -> folded tables + packed stream (+ the zero tile the draw's
-                   // pipelined loop reads past the last code tile)
+    if (!ready) {  // weights -> folded tables + packed stream
       hipLaunchKernelGGL(prior_fold_kernel, dim3((unsigned)(K + 1 + n + n_classes + 1)), dim3(128),
                          0, st, a);
-      hipLaunchKernelGGL(prior_pack_kernel, dim3((unsigned)(ntiles - 3)), dim3(256), 0, st, a, ws, 4);
+      hipLaunchKernelGGL(prior_pack_kernel, dim3((unsigned)(ntiles - 4)), dim3(256), 0, st, a, ws, 4);
     }
     hipLaunchKernelGGL(prior_lf_eval_kernel, dim3((unsigned)B), dim3(64), 0, st, a,
                        (const float4*)ws);
