@@ -229,6 +229,25 @@ int tvq_conv2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
 int tvq_convT2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi, const float* w,
                     const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t SW, float* y,
                     const float* residual, float* workspace, tvq_stream_t stream);
+/* Eval-mode conv (/ transposed conv) [-> GELU] -> BatchNorm2d from its running statistics
+ * -> Snake (snake_a nullable) in one launch: VQVAEDecBlock.block / ResBlock.convs[1:4] /
+ * Upscale's Conv1d -> GELU -> BN (pre_gelu = 1) while sampling (vq_vae.py:31-48,98-118,
+ * bidirectional_transformer.py:37-52); tvq_conv2d_fwd / tvq_convT2d_fwd followed by
+ * tvq_gelu_fwd and tvq_bn_eval_fwd up to the Snake's sin^2 evaluation (~1e-7 relative).
+ * Shapes whose conv path has no fused epilogue run the eval BN as a second launch.
+ * Workspace as the plain forward's. */
+int tvq_conv2d_fwd_bn_eval(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
+                           const float* w, const float* bias, int64_t Co, int64_t KH, int64_t KW,
+                           int64_t SW, int64_t replicate, int64_t pre_gelu, const float* bn_w,
+                           const float* bn_b,
+                           const float* running_mean, const float* running_var, float eps,
+                           const float* snake_a, float* y, float* workspace, tvq_stream_t stream);
+int tvq_convT2d_fwd_bn_eval(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
+                            const float* w, const float* bias, int64_t Co, int64_t KH, int64_t KW,
+                            int64_t SW, const float* bn_w, const float* bn_b,
+                            const float* running_mean, const float* running_var, float eps,
+                            const float* snake_a, float* y, float* workspace,
+                            tvq_stream_t stream);
 int tvq_conv2d_dgrad(const float* dy, int64_t B, int64_t Co, int64_t H, int64_t Wo,
                      const float* w, int64_t Ci, int64_t KH, int64_t KW, int64_t SW,
                      int64_t replicate, float* dx, int64_t Wi, float* workspace,

@@ -156,6 +156,38 @@ __device__ __forceinline__ float snake_f(float x, float a, float inv_a) {
   return x + inv_a * (s * s);
 }
 
+// sin(y)^2 for Snake epilogues fused into other kernels: Cody-Waite reduction by pi/2 in
+// three fp32 parts (exact enough for |y| < 2^17; Snake arguments are a * BatchNorm output)
+// and the Cephes single-precision sin / cos polynomials on [-pi/4, pi/4] (relative error
+// ~1e-7); the quadrant's sign drops out of the square.  Unlike sinf it has no Payne-Hanek
+// path, whose registers would otherwise be reserved in every kernel that inlines it.
+__device__ __forceinline__ float sin2_cw(float y) {
+  const float k = rintf(y * 0.636619772f);
+  float r = fmaf(-k, 1.57079637e+00f, y);
+  r = fmaf(-k, -4.37113883e-08f, r);
+  r = fmaf(-k, -1.71512451e-15f, r);
+  const float z = r * r;
+  const float sn = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f) * z, r, r);
+  const float cs = fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                             4.166664568298827e-2f) * z, z, fmaf(-0.5f, z, 1.0f));
+  return ((int)k & 1) ? cs * cs : sn * sn;
+}
+
+// GELU(x) = x/2 (1 + erf(x / sqrt 2)) with erf by Abramowitz-Stegun 7.1.26 (|error| <=
+// 1.5e-7, branch-free: one reciprocal, one exp, a degree-5 polynomial) for eval-path
+// epilogues; within fp32 noise of the exact form at the tests' 1e-4 / 1e-6 bars.  The
+// training path keeps the library erff.
+__device__ __forceinline__ float gelu_as(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = 1.0f - p * t * __expf(-z * z);  // erf(|x| / sqrt 2)
+  return 0.5f * x * (1.0f + copysignf(e, x));
+}
+
 // counter-based RNG (Philox-lite / splitmix hash) for dropout masks: uniform in [0,1)
 __device__ __forceinline__ uint32_t hash_u32(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;

@@ -100,7 +100,43 @@ struct Epi {
   float drop_scale;
   const int64_t* seed_ptr;
   uint64_t offset;
+  // eval-mode BatchNorm (+ Snake) applied to conv + bias before the dropout / residual
+  // (VQVAEDecBlock / ResBlock's conv -> BN -> Snake while sampling; null: off)
+  const float* bn_w;
+  const float* bn_b;
+  const float* bn_rm;
+  const float* bn_rv;
+  const float* snake_a;
+  float bn_eps;
+  int gelu;  // GELU (erf form) on conv + bias before the BN (Upscale: Conv1d -> GELU -> BN)
 };
+
+// bn_eval_snake_kernel's BN arithmetic (tvq_norm.hip) for channel n: v -> v sc + sh, then
+// Snake (a = 0: none) with its sin^2 from sin2_cw (within ~1e-7 relative of sinf's)
+struct PostCh {
+  float sc, sh, a;
+};
+__device__ __forceinline__ PostCh epi_post_ch(const Epi& e, int n) {
+  PostCh p;
+  const float inv = 1.0f / sqrtf(e.bn_rv[n] + e.bn_eps);
+  p.sc = (e.bn_w ? e.bn_w[n] : 1.f) * inv;
+  p.sh = (e.bn_b ? e.bn_b[n] : 0.f) - e.bn_rm[n] * p.sc;
+  p.a = e.snake_a ? e.snake_a[n] : 0.f;
+  return p;
+}
+__device__ __forceinline__ float epi_post_apply(const PostCh& p, float v, bool gelu) {
+  if (gelu) v = gelu_as(v);  // branch-free erf (tvq_common.h), ~1e-7 of tvq_gelu_fwd's
+  float s = fmaf(v, p.sc, p.sh);
+  if (p.a != 0.f) s = s + (1.0f / p.a) * sin2_cw(p.a * s);
+  return s;
+}
+__device__ __forceinline__ float epi_post(const Epi& e, float v, int n) {
+  return e.bn_rv ? epi_post_apply(epi_post_ch(e, n), v, e.gelu != 0) : v;
+}
+
+// Set by the launch paths whose epilogue applied Epi's BN / Snake (tvq_conv2d_fwd_bn_eval
+// launches the standalone eval BN after any other path)
+static thread_local bool t_post_done = false;
 
 // Epilogue helpers.  Every global load here is unconditional (clamped index) so the
 // compiler issues them together instead of one load + wait per element.
@@ -118,16 +154,36 @@ __device__ __forceinline__ void epi_load_bias(float (&bv)[FN][4], const float* _
 
 // a[i][r]: channel nbase + i*16 + r at flat offset ob + n*hw (ob for a clamped position
 // when !pv, so every address is in bounds)
+// POST kernels: the per-channel BN / Snake terms of a lane's FN x 4 channels, loaded once
+// before the epilogue's position loop (as epi_load_bias does for the bias)
 template <int FN>
+struct PostTile {
+  PostCh c[FN][4];
+};
+template <int FN>
+__device__ __forceinline__ void epi_load_post(PostTile<FN>& pt, const Epi& e, int nbase, int N) {
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pt.c[i][r] = epi_post_ch(e, min(nbase + i * 16 + r, N - 1));
+}
+
+template <int FN, bool POST = false>
 __device__ __forceinline__ void epi_store(float* __restrict__ out, const Epi& e, uint64_t seed,
                                           const float (&bv)[FN][4], const floatx4 (&a)[FN],
                                           int64_t ob, int64_t hw, int nbase, int N, bool pv,
-                                          bool wt = false) {
+                                          bool wt = false, const PostTile<FN>* pt = nullptr) {
   float v[FN][4];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[i][r] = a[i][r] + bv[i][r];
+  if constexpr (POST) {  // a separate instantiation: its terms would crowd every conv's epilogue
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[i][r] = epi_post_apply(pt->c[i][r], v[i][r], e.gelu != 0);
+  }
   if (e.drop_p > 0.f) {
 #pragma unroll
     for (int i = 0; i < FN; ++i)
@@ -281,7 +337,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const float* __restrict_
 // Tap-major variant for C % 16 == 0: the K loop runs over (tap, channel block), so a
 // thread's spatial source (and its validity) is computed once per tap and every
 // gathered element costs one multiply-add and one predicated load.
-template <int MODE, int KH, int KW, int SW, bool REPL, int TN, int TM, int WN, int WM, int BK>
+template <int MODE, int KH, int KW, int SW, bool REPL, int TN, int TM, int WN, int WM, int BK,
+          bool POST = false>
 __global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__ in,
                                                       const float* __restrict__ wt,
                                                       float* __restrict__ out, ConvGeom g, Epi e,
@@ -402,6 +459,8 @@ __global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__
   const int nbase = n0 + wn * FN * 16 + 4 * g4;
   float bv[FN][4];
   epi_load_bias<FN>(bv, e.bias, nbase, g.N);
+  PostTile<FN> pt;
+  if constexpr (POST) epi_load_post<FN>(pt, e, nbase, g.N);
   const int64_t hw = (int64_t)g.Hout * g.Wo;
 #pragma unroll
   for (int j = 0; j < FM; ++j) {
@@ -415,8 +474,8 @@ __global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__
     floatx4 a[FN];
 #pragma unroll
     for (int i = 0; i < FN; ++i) a[i] = acc[i][j];
-    epi_store<FN>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + w, hw, nbase, g.N,
-                  pv, cnt != nullptr);
+    epi_store<FN, POST>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + w, hw, nbase,
+                        g.N, pv, cnt != nullptr, &pt);
   }
   if (cnt && last_block(cnt + blockIdx.y * gridDim.x + blockIdx.x, (int)gridDim.z)) {
     const uint64_t fseed = fe.drop_p > 0.f ? mix_seed(fe.seed_ptr, fe.offset) : 0ull;
@@ -432,6 +491,7 @@ __global__ __launch_bounds__(256) void conv_tap_kernel(const float* __restrict__
 #pragma unroll 4
       for (int z = 0; z < (int)gridDim.z; ++z) v += ld_wt(slab + (int64_t)z * zstride + o);
       if (fe.bias) v += fe.bias[n];
+      v = epi_post(fe, v, n);
       if (fe.drop_p > 0.f) v = uniform01(fseed, (uint64_t)o) >= fe.drop_p ? v * fe.drop_scale : 0.f;
       if (fe.residual) v += fe.residual[o];
       fout[o] = v;
@@ -463,7 +523,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_
 // accumulators) or 3 NWN (each wave one 32x32 tile, up to 3 waves per SIMD so one wave's
 // barrier / address work hides behind the others' MFMAs; the first NWN waves stage the
 // weights, the other 2 NWN the input).  Same k order in every variant.
-template <int MODE, int KH, int KW, int SW, bool REPL, int BK, int NW, int TN>
+template <int MODE, int KH, int KW, int SW, bool REPL, int BK, int NW, int TN, bool POST = false>
 __global__ __launch_bounds__(NW * 64) void conv_t32_kernel(const float* __restrict__ in,
                                                       const float* __restrict__ wt,
                                                       float* __restrict__ out, ConvGeom g,
@@ -621,6 +681,12 @@ __global__ __launch_bounds__(NW * 64) void conv_t32_kernel(const float* __restri
   // position m0 + 32 (wpos + jb) + lane % 32); bias, dropout, residual as epi_store
   const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
   const int64_t hw = (int64_t)g.Hout * g.Wo;
+  PostCh pc[POST ? 16 : 1];  // POST: this lane's 16 channels' BN / Snake terms
+  if constexpr (POST) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      pc[r] = epi_post_ch(e, min(n0 + wch * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl, g.N - 1));
+  }
 #pragma unroll
   for (int jb = 0; jb < NJ; ++jb) {
     const int m = m0 + (wpos + jb) * 32 + r32;
@@ -637,6 +703,7 @@ __global__ __launch_bounds__(NW * 64) void conv_t32_kernel(const float* __restri
       if (!pv || n >= g.N) continue;
       const int64_t o = ob + (int64_t)n * hw;
       float v = acc[jb][r] + (e.bias ? e.bias[n] : 0.f);
+      if constexpr (POST) v = epi_post_apply(pc[r], v, e.gelu != 0);
       if (e.drop_p > 0.f) v = uniform01(seed, (uint64_t)o) >= e.drop_p ? v * e.drop_scale : 0.f;
       if (e.residual) v += e.residual[o];
       out[o] = v;
@@ -1311,7 +1378,7 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(const float* __restrict__
 // of a replicate-padded conv): the canvas (5 rows, Wo = Wx + 2 columns) is folded onto
 // out = dx (3 rows, Wx columns) in the epilogue -- rows 0+1, 2, 3+4; canvas columns 0 / Wx+1
 // onto dx columns 0 / Wx-1 through LDS -- instead of a canvas store and a fold launch.
-template <int CS, int HO, bool FOLD = false>
+template <int CS, int HO, bool FOLD = false, bool POST = false>
 __global__ __launch_bounds__(256) void conv_s2t_kernel(const float* __restrict__ in,
                                                        const float* __restrict__ wt,
                                                        float* __restrict__ out, ConvGeom g, Epi e) {
@@ -1396,11 +1463,13 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(const float* __restrict__
   const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
   const int64_t hw = (int64_t)g.Hout * g.Wo;
   const bool pv = wo < g.Wo;
+  PostTile<1> pt;
+  if constexpr (POST) epi_load_post<1>(pt, e, nbase, g.N);
 #pragma unroll
   for (int h = 0; h < HO; ++h) {
     const floatx4 a[1] = {acc[h]};
-    epi_store<1>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + (pv ? wo : 0), hw,
-                 nbase, g.N, pv);
+    epi_store<1, POST>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + (pv ? wo : 0),
+                       hw, nbase, g.N, pv, false, &pt);
   }
 }
 
@@ -1424,10 +1493,20 @@ static void launch_s2(int kind, const float* in, const float* wt, float* out, co
   const int cs = (g.C + 3) / 4;
   TVQ_PLAN("conv_s2%s cs%d hout%d", kind == 1 ? "f" : "t", 4 * cs, g.Hout);
 #define S2F(CSV) hipLaunchKernelGGL((conv_s2f_kernel<REPL, CSV>), grid, dim3(256), 0, st, in, wt, out, g, e)
-#define S2T(CSV, HOV) hipLaunchKernelGGL((conv_s2t_kernel<CSV, HOV>), grid, dim3(256), 0, st, in, wt, out, g, e)
+#define S2T(CSV, HOV)                                                                            \
+  do {                                                                                           \
+    if (e.bn_rv)                                                                                 \
+      hipLaunchKernelGGL((conv_s2t_kernel<CSV, HOV, false, true>), grid, dim3(256), 0, st, in, wt, \
+                         out, g, e);                                                             \
+    else                                                                                         \
+      hipLaunchKernelGGL((conv_s2t_kernel<CSV, HOV>), grid, dim3(256), 0, st, in, wt, out, g, e); \
+  } while (0)
   if (kind == 1) {
     if (cs == 1) S2F(4); else if (cs == 2) S2F(8); else if (cs == 3) S2F(12); else S2F(16);
-  } else if (kind == 2) {
+    return;
+  }
+  t_post_done = e.bn_rv != nullptr;
+  if (kind == 2) {
     if (cs == 1) S2T(4, 3); else if (cs == 2) S2T(8, 3); else if (cs == 3) S2T(12, 3); else S2T(16, 3);
   } else {
     if (cs == 1) S2T(4, 5); else if (cs == 2) S2T(8, 5); else if (cs == 3) S2T(12, 5); else S2T(16, 5);
@@ -2262,11 +2341,21 @@ __global__ __launch_bounds__(256) void conv_splitk_epi_kernel(const float* __res
                                                              Div16 dhw, Epi e,
                                                              float* __restrict__ out) {
   const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
+  // eval BN / Snake terms once per channel (N <= 256 here: tvq_conv2d_fwd_bn_eval's shapes)
+  __shared__ PostCh pcs[256];
+  const bool post = e.bn_rv != nullptr && N <= 256;
+  if (post) {
+    for (int n = threadIdx.x; n < N; n += 256) pcs[n] = epi_post_ch(e, n);
+    __syncthreads();
+  }
   for (int o = blockIdx.x * 256 + threadIdx.x; o < n_out; o += gridDim.x * 256) {
     float v = 0.f;
 #pragma unroll 4
     for (int z = 0; z < splits; ++z) v += slab[(int64_t)z * n_out + o];
-    if (e.bias) v += e.bias[div16(o, dhw) % N];
+    const int n = div16(o, dhw) % N;
+    if (e.bias) v += e.bias[n];
+    if (post) v = epi_post_apply(pcs[n], v, e.gelu != 0);
+    else v = epi_post(e, v, n);
     if (e.drop_p > 0.f) v = uniform01(seed, (uint64_t)o) >= e.drop_p ? v * e.drop_scale : 0.f;
     if (e.residual) v += e.residual[o];
     out[o] = v;
@@ -2416,6 +2505,27 @@ static void launch_tap(const float* in, const float* wt, float* out, const ConvG
   tap_tile(g.N, &TN, &TM);
   dim3 grid((g.Mpos + TM - 1) / TM, (g.N + TN - 1) / TN, splits);
   const Epi fin = fe ? *fe : e;
+  // the eval conv -> BN -> Snake shapes (ResBlock 3x3 / 1x1, DecBlock ConvT, Upscale Conv1d)
+  // have epilogue-fused variants; the split-K finish applies `fin`'s BN itself
+  constexpr bool post_kind = (MODE == GATHER_F && ((KH == 3 && KW == 3) || (KH == 1 && KW == 3 && !REPL) ||
+                                                   (KH == 1 && KW == 1))) ||
+                             (MODE == GATHER_T && KH == 3 && KW == 4 && SW == 2);
+  if constexpr (post_kind) {
+    if (splits == 1 && e.bn_rv) {
+      t_post_done = true;
+      if (TN == 16)
+        hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 16, 256, 1, 4, BK, true>), grid,
+                           dim3(256), 0, st, in, wt, out, g, e, sps, zstride, cnt, fout, fin);
+      else if (TN == 32)
+        hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 32, 128, 2, 2, BK, true>), grid,
+                           dim3(256), 0, st, in, wt, out, g, e, sps, zstride, cnt, fout, fin);
+      else
+        hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 64, 128, 2, 2, BK, true>), grid,
+                           dim3(256), 0, st, in, wt, out, g, e, sps, zstride, cnt, fout, fin);
+      return;
+    }
+  }
+  if (cnt && fin.bn_rv) t_post_done = true;
   if (TN == 16)
     hipLaunchKernelGGL((conv_tap_kernel<MODE, KH, KW, SW, REPL, 16, 256, 1, 4, BK>), grid,
                        dim3(256), 0, st, in, wt, out, g, e, sps, zstride, cnt, fout, fin);
@@ -2543,7 +2653,7 @@ __global__ __launch_bounds__(64 * NW) void conv_d32_kernel(const float* __restri
     const int b2 = (int)fdiv((uint32_t)mm, g.fd_hwo);
     const int h2 = (int)bh2 - b2 * g.Hout;
     const int64_t o = (((int64_t)b2 * g.N + n) * g.Hout + h2) * g.Wo + w2;
-    float v = part[0] + (e.bias ? e.bias[n] : 0.f);
+    float v = epi_post(e, part[0] + (e.bias ? e.bias[n] : 0.f), n);
     if (e.drop_p > 0.f) v = uniform01(seed, (uint64_t)o) >= e.drop_p ? v * e.drop_scale : 0.f;
     if (e.residual) v += e.residual[o];
     out[o] = v;
@@ -2763,6 +2873,33 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
   hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, BKV, NWV, TNV>),             \
                      dim3((unsigned)mt, g.N / TNV), dim3(64 * NWV), t32_lds(BKV, TNV), st, in, \
                      wt, out, g, e)
+      // eval conv -> BN (-> Snake / after GELU): the epilogue-fused instance (12 waves, 128
+      // channels; Upscale's Conv1d, the 128-channel ResBlock convs)
+      constexpr bool t32_post = MODE == GATHER_F && !REPL &&
+                                ((KH == 1 && KW == 3) || (KH == 3 && KW == 3));
+      if constexpr (t32_post) {
+        if (e.bn_rv && !wide64 && g_t32_nw == 12 && (bk == 64 || bk == 32)) {
+          static bool lds_post = false;
+          if (!lds_post) {
+            (void)hipFuncSetAttribute(
+                reinterpret_cast<const void*>(
+                    &conv_t32_kernel<MODE, KH, KW, SW, REPL, 64, 12, 128, true>),
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)t32_lds(64, 128));
+            lds_post = true;
+          }
+          TVQ_PLAN("conv_t32 bk%d nw12 tn128 post", bk);
+          if (bk == 64)
+            hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, 64, 12, 128, true>),
+                               dim3((unsigned)mt, g.N / 128), dim3(64 * 12), t32_lds(64, 128), st,
+                               in, wt, out, g, e);
+          else
+            hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, 32, 12, 128, true>),
+                               dim3((unsigned)mt, g.N / 128), dim3(64 * 12), t32_lds(32, 128), st,
+                               in, wt, out, g, e);
+          t_post_done = true;
+          return;
+        }
+      }
       TVQ_PLAN("conv_t32 bk%d nw%d tn%d", wide64 ? 64 : bk, wide64 ? 6 : g_t32_nw,
                wide64 ? 64 : 128);
       if (wide64) {
@@ -2780,6 +2917,7 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
       return;
     }
     if (launch_d32<MODE, KH, KW, SW, REPL>(in, wt, out, g, e, st)) {
+      t_post_done = e.bn_rv != nullptr;
       TVQ_PLAN("conv_d32");
       return;
     }
@@ -2804,6 +2942,7 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
       if (blocks > 8192) blocks = 8192;
       hipLaunchKernelGGL(conv_splitk_epi_kernel, dim3(blocks), dim3(256), 0, st, slab, splits,
                          (int)n_out, g.N, make_div16((int64_t)g.Hout * g.Wo), e, out);
+      t_post_done = e.bn_rv != nullptr;
       return;
     }
     if (g.C % 32 == 0)
@@ -2961,7 +3100,7 @@ using namespace tvq;
 
 static Epi make_epi(const float* bias, const float* residual, float drop_p,
                     const int64_t* seed_ptr, uint64_t offset) {
-  Epi e;
+  Epi e = {};
   e.bias = bias;
   e.residual = residual;
   e.drop_p = drop_p;
@@ -3166,6 +3305,84 @@ extern "C" int tvq_convT2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H,
   TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
   return launch_status("tvq_convT2d_fwd");
+}
+
+// Eval-mode conv -> BatchNorm(running statistics) -> Snake in one launch: the BN affine
+// and the Snake are the conv epilogue's (epi_post), no (B, Co, H, W) round trip through
+// HBM between them.  Same results, bit for bit, as tvq_conv2d_fwd + tvq_bn_eval_fwd.
+extern "C" int tvq_conv2d_fwd_bn_eval(const float* x, int64_t B, int64_t Ci, int64_t H,
+                                      int64_t Wi, const float* w, const float* bias, int64_t Co,
+                                      int64_t KH, int64_t KW, int64_t SW, int64_t replicate,
+                                      int64_t pre_gelu, const float* bn_w, const float* bn_b,
+                                      const float* running_mean, const float* running_var,
+                                      float eps, const float* snake_a, float* y,
+                                      float* workspace, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && w && y && running_mean && running_var && B > 0 && Ci > 0 && Co > 0,
+                "tvq_conv2d_fwd_bn_eval: bad arguments");
+  const int kind = kind_of((int)KH, (int)KW, (int)SW);
+  TVQ_CHECK_ARG(kind >= 0, "tvq_conv2d_fwd_bn_eval: unsupported kernel");
+  ConvGeom g = geom_conv_fwd(B, Ci, H, Wi, Co, KH, KW, SW);
+  TVQ_CHECK_ARG(geom_ok(g), "tvq_conv2d_fwd_bn_eval: bad geometry");
+  Epi e = make_epi(bias, nullptr, 0.f, nullptr, 0);
+  e.bn_w = bn_w;
+  e.bn_b = bn_b;
+  e.bn_rm = running_mean;
+  e.bn_rv = running_var;
+  e.bn_eps = eps;
+  e.snake_a = snake_a;
+  e.gelu = pre_gelu != 0;
+  hipStream_t st = (hipStream_t)stream;
+  TVQ_PLAN("conv_bn_eval");
+  t_post_done = false;
+#define M_(a, b_, c, d) launch_conv<GATHER_F, a, b_, c, d>(x, w, y, g, workspace, e, st);
+  TVQ_DISPATCH_KIND(kind, replicate, M_)
+#undef M_
+  if (!t_post_done) {  // this shape's conv path has no fused epilogue: the eval BN after it
+    TVQ_PLAN("bn_eval separate");
+    if (pre_gelu) {
+      const int rg = tvq_gelu_fwd(y, B * Co * g.Hout * g.Wo, y, stream);
+      if (rg != TVQ_OK) return rg;
+    }
+    const int rc = tvq_bn_eval_fwd(y, B, Co, (int64_t)g.Hout * g.Wo, bn_w, bn_b, running_mean,
+                                   running_var, eps, snake_a, y, y, stream);
+    if (rc != TVQ_OK) return rc;
+  }
+  return launch_status("tvq_conv2d_fwd_bn_eval");
+}
+
+extern "C" int tvq_convT2d_fwd_bn_eval(const float* x, int64_t B, int64_t Ci, int64_t H,
+                                       int64_t Wi, const float* w, const float* bias, int64_t Co,
+                                       int64_t KH, int64_t KW, int64_t SW, const float* bn_w,
+                                       const float* bn_b, const float* running_mean,
+                                       const float* running_var, float eps,
+                                       const float* snake_a, float* y, float* workspace,
+                                       tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && w && y && running_mean && running_var && B > 0 && Ci > 0 && Co > 0,
+                "tvq_convT2d_fwd_bn_eval: bad arguments");
+  const int kind = kind_of((int)KH, (int)KW, (int)SW);
+  TVQ_CHECK_ARG(kind >= 0, "tvq_convT2d_fwd_bn_eval: unsupported kernel");
+  ConvGeom g = geom_convT_fwd(B, Ci, H, Wi, Co, KH, KW, SW);
+  TVQ_CHECK_ARG(geom_ok(g), "tvq_convT2d_fwd_bn_eval: bad geometry");
+  Epi e = make_epi(bias, nullptr, 0.f, nullptr, 0);
+  e.bn_w = bn_w;
+  e.bn_b = bn_b;
+  e.bn_rm = running_mean;
+  e.bn_rv = running_var;
+  e.bn_eps = eps;
+  e.snake_a = snake_a;
+  hipStream_t st = (hipStream_t)stream;
+  TVQ_PLAN("convT_bn_eval");
+  t_post_done = false;
+#define M_(a, b_, c, d) launch_conv<GATHER_T, a, b_, c, false>(x, w, y, g, workspace, e, st);
+  TVQ_DISPATCH_KIND(kind, 0, M_)
+#undef M_
+  if (!t_post_done) {  // this shape's conv path has no fused epilogue: the eval BN after it
+    TVQ_PLAN("bn_eval separate");
+    const int rc = tvq_bn_eval_fwd(y, B, Co, (int64_t)g.Hout * g.Wo, bn_w, bn_b, running_mean,
+                                   running_var, eps, snake_a, y, y, stream);
+    if (rc != TVQ_OK) return rc;
+  }
+  return launch_status("tvq_convT2d_fwd_bn_eval");
 }
 
 // workspace: [replicate canvas][pack + split-K slab]; required when replicate

@@ -87,21 +87,9 @@ __device__ __forceinline__ void pe_zero(floatx16& a) {
   for (int i = 0; i < 16; ++i) a[i] = 0.f;
 }
 
-// GELU(x) = x/2 (1 + erf(x / sqrt 2)) with erf by Abramowitz-Stegun 7.1.26 (|error| <=
-// 1.5e-7, branch-free: one reciprocal, one exp, a degree-5 polynomial) instead of the
-// library erff's range branches, which diverge across a wave's 64 values: the GELUs were a
-// quarter of this kernel's VALU instructions.  Within fp32 noise of the exact form at the
-// 1e-4 bar of tests/test_prior_eval.py; the training path keeps the library erff.
-__device__ __forceinline__ float pe_gelu(float x) {
-  const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  const float e = 1.0f - p * t * __expf(-z * z);  // erf(|x| / sqrt 2)
-  return 0.5f * x * (1.0f + copysignf(e, x));
-}
+// GELU by gelu_as (tvq_common.h): branch-free, the library erff's range branches diverged
+// across a wave's 64 values and the GELUs were a quarter of this kernel's VALU instructions
+__device__ __forceinline__ float pe_gelu(float x) { return gelu_as(x); }
 
 // ---- the weight-tile stream.  Tile idx (order of consumption) -> source rows.
 struct PeTile {

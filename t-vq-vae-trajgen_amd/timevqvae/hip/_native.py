@@ -64,6 +64,10 @@ sig("tvq_conv_config", I64)
 sig("tvq_conv_workspace", I64, I64, I64, I64, I64, I64, I64, I64, I64, I64, restype=I64)
 sig("tvq_conv2d_fwd", P, I64, I64, I64, I64, P, P, I64, I64, I64, I64, I64, P, P, F32, P, U64, P, P)
 sig("tvq_convT2d_fwd", P, I64, I64, I64, I64, P, P, I64, I64, I64, I64, P, P, P, P)
+sig("tvq_conv2d_fwd_bn_eval", P, I64, I64, I64, I64, P, P, I64, I64, I64, I64, I64, I64, P, P, P, P,
+    F32, P, P, P, P)
+sig("tvq_convT2d_fwd_bn_eval", P, I64, I64, I64, I64, P, P, I64, I64, I64, I64, P, P, P, P, F32, P,
+    P, P, P)
 sig("tvq_conv2d_dgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, P, I64, P, P)
 sig("tvq_convT2d_dgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, P, I64, P, P)
 sig("tvq_conv2d_wgrad", P, I64, I64, I64, I64, P, I64, I64, I64, I64, I64, I64, P, P, I64, P, P)

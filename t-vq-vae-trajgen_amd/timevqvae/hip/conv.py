@@ -272,3 +272,53 @@ class _ConvT2d(torch.autograd.Function):
 
 def conv_transpose2d(x, weight, bias=None, stride_w=2):
     return _ConvT2d.apply(x, weight, bias, int(stride_w))
+
+
+FUSED_BN_EVAL = os.environ.get("TVQ_FUSED_BN_EVAL", "1") != "0"
+
+
+def bn_eval_fusable(x, bn, *params):
+    """An eval-mode conv -> BN (-> Snake) pair can run as one launch when nothing needs a
+    gradient (the sampler's decoders, vq_vae.py:31-48,98-118)."""
+    if not FUSED_BN_EVAL or bn.training:
+        return False
+    if torch.is_grad_enabled() and (x.requires_grad or any(
+            p is not None and p.requires_grad for p in params + (bn.weight, bn.bias))):
+        return False
+    return True
+
+
+def conv2d_bn_eval(x, weight, bias, bn, a=None, stride_w=1, replicate=False, pre_gelu=False):
+    """snake_a(BatchNorm_eval([GELU](conv(x) + bias))) in one launch (tvq_conv2d_fwd_bn_eval);
+    no autograd.  a: the Snake parameter or None."""
+    squeeze = x.dim() == 3
+    x4 = _as4d(x).contiguous()
+    w4 = _as4d(weight).contiguous() if weight.dim() == 3 else weight.contiguous()
+    B, Ci, H, Wi = x4.shape
+    Co, _, KH, KW = w4.shape
+    SW = int(stride_w)
+    Wo = value("tvq_conv_out_width", Wi, KW, SW, 0)
+    y = torch.empty((B, Co, H, Wo), device=x.device, dtype=torch.float32)
+    ws = _conv_ws(OP_FWD, x.device, B, Ci, H, Wi, Co, KH, KW, SW)
+    call("tvq_conv2d_fwd_bn_eval", ptr(x4), B, Ci, H, Wi, ptr(w4), ptr(bias), Co, KH, KW, SW,
+         int(replicate), int(pre_gelu), ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
+         ptr(bn.running_var),
+         float(bn.eps), ptr(a.reshape(-1) if a is not None else None), ptr(y), ptr(ws),
+         stream_ptr())
+    return y.squeeze(2) if squeeze else y
+
+
+def conv_transpose2d_bn_eval(x, weight, bias, bn, a=None, stride_w=2):
+    """snake_a(BatchNorm_eval(conv_transpose(x) + bias)) in one launch; no autograd."""
+    x = x.contiguous()
+    w = weight.contiguous()
+    B, Ci, H, Wi = x.shape
+    _, Co, KH, KW = w.shape
+    SW = int(stride_w)
+    Wo = value("tvq_conv_out_width", Wi, KW, SW, 1)
+    y = torch.empty((B, Co, H, Wo), device=x.device, dtype=torch.float32)
+    ws = _conv_ws(OP_T_FWD, x.device, B, Ci, H, Wi, Co, KH, KW, SW)
+    call("tvq_convT2d_fwd_bn_eval", ptr(x), B, Ci, H, Wi, ptr(w), ptr(bias), Co, KH, KW, SW,
+         ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var), float(bn.eps),
+         ptr(a.reshape(-1) if a is not None else None), ptr(y), ptr(ws), stream_ptr())
+    return y

@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from ..hip import rng, streams
-from ..hip.conv import PackCache, _immediate, _keep, conv2d
+from ..hip.conv import PackCache, _immediate, _keep, bn_eval_fusable, conv2d, conv2d_bn_eval
 from ..hip.linear import gemm, linear
 from ..hip.norm import bn_snake
 from ..hip.xf import (batch_colsum, drop_first_token, embed_assemble, embedding, fused_ff,
@@ -335,8 +335,11 @@ class Upscale(nn.Module):
         """x: (b n d) -> (b m d)."""
         x = upsample_nearest_t(x, upscale_size)          # b n d -> b d m, one kernel
         c = self.conv
-        x = gelu(conv2d(x, c[0].weight, c[0].bias))
-        x = bn_snake(x, c[2], None)
+        if bn_eval_fusable(x, c[2], c[0].weight, c[0].bias):  # eval: one launch
+            x = conv2d_bn_eval(x, c[0].weight, c[0].bias, c[2], None, pre_gelu=True)
+        else:
+            x = gelu(conv2d(x, c[0].weight, c[0].bias))
+            x = bn_snake(x, c[2], None)
         x = conv2d(x, c[3].weight, c[3].bias)
         return x.transpose(1, 2)                         # b m d
 
@@ -514,8 +517,11 @@ class BidirectionalTransformer(nn.Module):
         # x1 = cat(C[cls], Upscale'(tl) + Th[s_h] + P[:n]) = project_in(embed)
         tl = self._tok(s_M_l, self.tok_emb_l.weight, "lf", self._site_l)
         x = upsample_nearest_t(tl, n)
-        x = gelu(conv2d(x, up[0].weight, up[0].bias))
-        x = bn_snake(x, up[2], None)
+        if bn_eval_fusable(x, up[2], up[0].weight, up[0].bias):
+            x = conv2d_bn_eval(x, up[0].weight, up[0].bias, up[2], None, pre_gelu=True)
+        else:
+            x = gelu(conv2d(x, up[0].weight, up[0].bias))
+            x = bn_snake(x, up[2], None)
         r = codebook_gather_nchw(s_M_h, Th, 1, n).view(B, d, n)  # Th[s_h] channels-first
         with PackCache.paused():  # W2c is computed per call: never cached
             u = conv2d(x, W2c, b2c, residual=r)  # (B, d, n)

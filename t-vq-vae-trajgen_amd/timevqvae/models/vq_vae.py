@@ -17,7 +17,8 @@ import torch
 import torch.nn as nn
 
 from ..hip import resblock, rng
-from ..hip.conv import conv2d, conv_transpose2d
+from ..hip.conv import (bn_eval_fusable, conv2d, conv2d_bn_eval, conv_transpose2d,
+                        conv_transpose2d_bn_eval)
 from ..hip.linear import linear
 from ..hip.norm import bn_snake, snake, snake_skip
 from ..hip.signal import istft_decode, stft_encode
@@ -106,8 +107,11 @@ class ResBlock(nn.Module):
             if not needs_grad and not (self.training and c[5].p > 0):
                 return resblock.resblock_eval(x, _a(c[0]), c[1], c[2], _a(c[3]), c[4])
         s, xs = snake_skip(x, _a(c[0]))  # xs: x, its skip-path gradient summed in Snake bwd
-        h = conv2d(s, c[1].weight, c[1].bias)
-        h = bn_snake(h, c[2], _a(c[3]))
+        if bn_eval_fusable(s, c[2], c[1].weight, c[1].bias, c[3].a):
+            h = conv2d_bn_eval(s, c[1].weight, c[1].bias, c[2], _a(c[3]))  # one launch
+        else:
+            h = conv2d(s, c[1].weight, c[1].bias)
+            h = bn_snake(h, c[2], _a(c[3]))
         r = xs if isinstance(self.proj, nn.Identity) else conv2d(xs, self.proj.weight, self.proj.bias)
         p = c[5].p if self.training else 0.0
         return conv2d(h, c[4].weight, c[4].bias, residual=r, drop_p=p, site=self._site)
@@ -127,6 +131,9 @@ class VQVAEEncBlock(nn.Module):
         b = self.block
         if self.training and b[3].p > 0:
             raise NotImplementedError("EncBlock dropout>0 is not on the path (vq_vae.py:156)")
+        if bn_eval_fusable(x, b[1], b[0].weight, b[0].bias, b[2].a):
+            return conv2d_bn_eval(x, b[0].weight, b[0].bias, b[1], _a(b[2]), stride_w=2,
+                                  replicate=True)
         h = conv2d(x, b[0].weight, b[0].bias, stride_w=2, replicate=True)
         return bn_snake(h, b[1], _a(b[2]))
 
@@ -144,6 +151,8 @@ class VQVAEDecBlock(nn.Module):
         b = self.block
         if self.training and b[3].p > 0:
             raise NotImplementedError("DecBlock dropout>0 is not on the path")
+        if bn_eval_fusable(x, b[1], b[0].weight, b[0].bias, b[2].a):
+            return conv_transpose2d_bn_eval(x, b[0].weight, b[0].bias, b[1], _a(b[2]))
         h = conv_transpose2d(x, b[0].weight, b[0].bias, stride_w=2)
         return bn_snake(h, b[1], _a(b[2]))
 
