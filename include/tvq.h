@@ -512,6 +512,20 @@ int tvq_upsample_nearest(const float* x, int64_t R, int64_t Lin, int64_t Lout, f
 int tvq_upsample_nearest_bwd(const float* dy, int64_t R, int64_t Lin, int64_t Lout, float* dx,
                              tvq_stream_t stream);
 int tvq_gelu_fwd(const float* x, int64_t n, float* y, tvq_stream_t stream);
+/* The priors' FeedForward branch in training (x-transformers FeedForward in the pre-norm
+ * residual, bidirectional_transformer.py:92-110, ff_mult 1), D = 128, M token rows:
+ *   pre = xn W1^T + b1 (M x 128), hd = Dropout_p(GELU(pre)) (the mask: uniform01 of
+ *   (seed, offset) at m * 128 + j >= p), y = r + gate * (hd W2^T + b2)   (gate nullable: 1)
+ * one launch; 16-byte aligned pointers.  tvq_ffn_bwd: from gy = dL/dy the pre-activation
+ * gradient d_pre (M x 128, for the W1 / b1 gradients) and d(xn); the W2 / b2 gradients are
+ * the caller's (hd^T (gate gy)).  p in [0, 1). */
+int tvq_ffn_fwd(const float* xn, const float* r, int64_t M, int64_t D, const float* W1,
+                const float* b1, const float* W2, const float* b2, const float* gate, float p,
+                const int64_t* seed_ptr, uint64_t offset, float* y, float* pre, float* hd,
+                tvq_stream_t stream);
+int tvq_ffn_bwd(const float* gy, const float* pre, int64_t M, int64_t D, const float* W1,
+                const float* W2, const float* gate, float p, const int64_t* seed_ptr,
+                uint64_t offset, float* d_pre, float* dxn, tvq_stream_t stream);
 int tvq_gelu_bwd(const float* dy, const float* x, int64_t n, float* dx, tvq_stream_t stream);
 
 /* ---------------------------------------------------------------- fused LF prior (eval)
