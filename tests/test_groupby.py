@@ -3,7 +3,8 @@
 3-launch sort above 2048 rows, then seg_sum_kernel with its in-launch combine of skewed
 values) against torch fp64 index_add, on uniform, skewed (one value owning 60 % of the rows,
 as the MaskGIT mask token does), sparse (most values empty) and tiny (the class embedding)
-index sets; every call is run twice and must be bitwise equal.  Tolerance: rel-L2 1e-6
+index sets, and a 5000-value vocabulary (the wide placement kernel); every call is run
+twice and must be bitwise equal.  Tolerance: rel-L2 1e-6
 against fp64 (fp32 sums of <= 32768 rows in a fixed order)."""
 import pytest
 import torch
@@ -26,7 +27,7 @@ def _case(kind, M, V, gen):
 @pytest.mark.parametrize("kind,M,V,D", [
     ("uniform", 24576, 513, 128), ("skewed", 24576, 513, 128), ("sparse", 6144, 513, 128),
     ("uniform", 256, 6, 256), ("skewed", 6144, 513, 64), ("uniform", 32768, 1024, 32),
-    ("skewed", 40000, 300, 128), ("uniform", 3, 1, 128)])
+    ("skewed", 40000, 300, 128), ("uniform", 3, 1, 128), ("skewed", 8192, 5000, 32)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_embedding_bwd_groupby(kind, M, V, D, accumulate, cuda):
     from timevqvae.hip._native import call, plan_trace, ptr, stream_ptr, value
