@@ -37,7 +37,7 @@ def _latent_width(T: int, n_enc_blocks: int) -> int:
 # TVQ_FUSED_CE=1: the priors' training loss through the fused tied-logits CE (csrc/tvq_ce.hip,
 # no logits in HBM).  Off by default: it recomputes the logits in both backward kernels (5
 # logits-sized GEMMs instead of 3, 16 vs 9.6 GFLOP at B=256), and measured 4.79 vs 4.72 ms
-# per joint step (tools/gpu_r4e.sh): the logits GEMMs were MFMA-bound, not memory-bound.
+# per joint step (tools/ab/r04/gpu_r4e.sh): the logits GEMMs were MFMA-bound, not memory-bound.
 FUSED_CE = os.environ.get("TVQ_FUSED_CE", "0") == "1"
 
 
