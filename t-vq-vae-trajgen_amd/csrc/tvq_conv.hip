@@ -1021,7 +1021,7 @@ __device__ __forceinline__ void halo_fill(float* __restrict__ Hs, const float* _
   }
 }
 
-template <int MODE, int KH, int KW, int SW, bool REPL, int FN, int KS>
+template <int MODE, int KH, int KW, int SW, bool REPL, int FN, int KS, bool POST = false>
 __global__ __launch_bounds__(256) void conv_halo_kernel(const float* __restrict__ in,
                                                        const float* __restrict__ wt,
                                                        float* __restrict__ out, HaloGeom g,
@@ -1120,6 +1120,8 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const float* __restrict_
   const int nbase = n0 + kq * 4;
   float bv[FN][4];
   epi_load_bias<FN>(bv, e.bias, nbase, g.N);
+  PostTile<FN> pt;
+  if constexpr (POST) epi_load_post<FN>(pt, e, nbase, g.N);
   const int64_t hwo = (int64_t)g.Hout * g.Wo;
   auto store = [&](int mt, const floatx4 (&a)[FN]) {
     const int p = mt * 16 + j;
@@ -1127,8 +1129,8 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const float* __restrict_
     const int pp = pv ? p : 0;
     const int h = div16(pp, g.dv_wo);
     const int w = pp - h * g.Wo;
-    epi_store<FN>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + w, hwo, nbase,
-                  g.N, pv);
+    epi_store<FN, POST>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + w, hwo,
+                        nbase, g.N, pv, false, &pt);
   };
 
   floatx4 acc[FN][4];
@@ -1298,7 +1300,7 @@ constexpr int S2_XRF = 2 * S2_SEG + 2;     // F: staged columns (stride 2, 4 tap
 constexpr int S2_XRT = S2_SEG / 2 + 4;     // T: staged columns (source offsets -2..2)
 
 // F: out[b,n,h,wo] = sum_{c,kh,kw} w(n,c,kh,kw) in[b,c,h+kh-1,2wo+kw-opw], H = 3
-template <bool REPL, int CS>
+template <bool REPL, int CS, bool POST = false>
 __global__ __launch_bounds__(256) void conv_s2f_kernel(const float* __restrict__ in,
                                                        const float* __restrict__ wt,
                                                        float* __restrict__ out, ConvGeom g, Epi e) {
@@ -1362,14 +1364,16 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(const float* __restrict__
   }
   const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
   const int64_t hw = (int64_t)g.Hout * g.Wo;
+  PostTile<1> pt;
+  if constexpr (POST) epi_load_post<1>(pt, e, nbase, g.N);
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
     const int tile = wid * 3 + t, h = tile >> 2;
     const int wo = w0 + (tile & 3) * 16 + r16;
     const bool pv = wo < g.Wo;
     const floatx4 a[1] = {acc[t]};
-    epi_store<1>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + (pv ? wo : 0), hw,
-                 nbase, g.N, pv);
+    epi_store<1, POST>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + (pv ? wo : 0),
+                       hw, nbase, g.N, pv, false, &pt);
   }
 }
 
@@ -1492,7 +1496,14 @@ static void launch_s2(int kind, const float* in, const float* wt, float* out, co
   const dim3 grid((unsigned)(g.B * ((g.Wo + S2_SEG - 1) / S2_SEG)));
   const int cs = (g.C + 3) / 4;
   TVQ_PLAN("conv_s2%s cs%d hout%d", kind == 1 ? "f" : "t", 4 * cs, g.Hout);
-#define S2F(CSV) hipLaunchKernelGGL((conv_s2f_kernel<REPL, CSV>), grid, dim3(256), 0, st, in, wt, out, g, e)
+#define S2F(CSV)                                                                                \
+  do {                                                                                          \
+    if (e.bn_rv)                                                                                \
+      hipLaunchKernelGGL((conv_s2f_kernel<REPL, CSV, true>), grid, dim3(256), 0, st, in, wt, out, \
+                         g, e);                                                                 \
+    else                                                                                        \
+      hipLaunchKernelGGL((conv_s2f_kernel<REPL, CSV>), grid, dim3(256), 0, st, in, wt, out, g, e); \
+  } while (0)
 #define S2T(CSV, HOV)                                                                            \
   do {                                                                                           \
     if (e.bn_rv)                                                                                 \
@@ -1501,11 +1512,11 @@ static void launch_s2(int kind, const float* in, const float* wt, float* out, co
     else                                                                                         \
       hipLaunchKernelGGL((conv_s2t_kernel<CSV, HOV>), grid, dim3(256), 0, st, in, wt, out, g, e); \
   } while (0)
+  t_post_done = e.bn_rv != nullptr;
   if (kind == 1) {
     if (cs == 1) S2F(4); else if (cs == 2) S2F(8); else if (cs == 3) S2F(12); else S2F(16);
     return;
   }
-  t_post_done = e.bn_rv != nullptr;
   if (kind == 2) {
     if (cs == 1) S2T(4, 3); else if (cs == 2) S2T(8, 3); else if (cs == 3) S2T(12, 3); else S2T(16, 3);
   } else {
@@ -1752,6 +1763,22 @@ template <int MODE, int KH, int KW, int SW, bool REPL>
 static void launch_halo(const float* in, const float* wt, float* out, const HaloPlan& pl, int B,
                         const Epi& e, hipStream_t st) {
   const dim3 grid(B, (pl.g.N + pl.FN * 16 - 1) / (pl.FN * 16));
+  // the eval EncBlock (replicate 3x4 stride-2 conv -> BN -> Snake): an epilogue-fused instance
+  if constexpr (MODE == GATHER_F && KH == 3 && KW == 4 && SW == 2 && REPL) {
+    if (e.bn_rv) {
+      t_post_done = true;
+#define HP_(FN_, KS_)                                                                             \
+  hipLaunchKernelGGL((conv_halo_kernel<MODE, KH, KW, SW, REPL, FN_, KS_, true>), grid, dim3(256), \
+                     pl.lds, st, in, wt, out, pl.g, e)
+      if (pl.KS == 4) {
+        if (pl.FN == 1) HP_(1, 4); else if (pl.FN == 2) HP_(2, 4); else HP_(4, 4);
+      } else {
+        if (pl.FN == 1) HP_(1, 1); else if (pl.FN == 2) HP_(2, 1); else HP_(4, 1);
+      }
+#undef HP_
+      return;
+    }
+  }
 #define H_(FN_, KS_)                                                                          \
   hipLaunchKernelGGL((conv_halo_kernel<MODE, KH, KW, SW, REPL, FN_, KS_>), grid, dim3(256), \
                      pl.lds, st, in, wt, out, pl.g, e)
@@ -2508,7 +2535,8 @@ static void launch_tap(const float* in, const float* wt, float* out, const ConvG
   // the eval conv -> BN -> Snake shapes (ResBlock 3x3 / 1x1, DecBlock ConvT, Upscale Conv1d)
   // have epilogue-fused variants; the split-K finish applies `fin`'s BN itself
   constexpr bool post_kind = (MODE == GATHER_F && ((KH == 3 && KW == 3) || (KH == 1 && KW == 3 && !REPL) ||
-                                                   (KH == 1 && KW == 1))) ||
+                                                   (KH == 1 && KW == 1) ||
+                                                   (KH == 3 && KW == 4 && SW == 2 && REPL))) ||
                              (MODE == GATHER_T && KH == 3 && KW == 4 && SW == 2);
   if constexpr (post_kind) {
     if (splits == 1 && e.bn_rv) {
@@ -2878,7 +2906,7 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
       constexpr bool t32_post = MODE == GATHER_F && !REPL &&
                                 ((KH == 1 && KW == 3) || (KH == 3 && KW == 3));
       if constexpr (t32_post) {
-        if (e.bn_rv && !wide64 && g_t32_nw == 12 && (bk == 64 || bk == 32)) {
+        if (e.bn_rv && !wide64 && g_t32_nw == 12) {
           static bool lds_post = false;
           if (!lds_post) {
             (void)hipFuncSetAttribute(
@@ -2892,9 +2920,13 @@ static void launch_gemm(const float* in, const float* wt, float* out, const Conv
             hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, 64, 12, 128, true>),
                                dim3((unsigned)mt, g.N / 128), dim3(64 * 12), t32_lds(64, 128), st,
                                in, wt, out, g, e);
-          else
+          else if (bk == 32)
             hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, 32, 12, 128, true>),
                                dim3((unsigned)mt, g.N / 128), dim3(64 * 12), t32_lds(32, 128), st,
+                               in, wt, out, g, e);
+          else  // the 16-channel -> 128 convs (HF encoder's last ResBlock)
+            hipLaunchKernelGGL((conv_t32_kernel<MODE, KH, KW, SW, REPL, 16, 12, 128, true>),
+                               dim3((unsigned)mt, g.N / 128), dim3(64 * 12), t32_lds(16, 128), st,
                                in, wt, out, g, e);
           t_post_done = true;
           return;

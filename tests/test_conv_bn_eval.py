@@ -44,10 +44,14 @@ SHAPES = [
     (1024, 128, 3, 8, 64, False, True),
     (1024, 64, 3, 8, 64, False, True),
     (1024, 128, 3, 32, 16, False, True),
+    (256, 16, 3, 32, 128, False, True),
     (1024, 64, 3, 8, 32, True, True),
     (1024, 32, 3, 16, 16, True, True),
     (1024, 16, 3, 32, 8, True, True),
     (1024, 8, 3, 64, 4, True, True),
+    (256, 12, 3, 257, 4, "enc", True),
+    (256, 4, 3, 129, 8, "enc", True),
+    (256, 16, 3, 33, 32, "enc", True),
     (3, 8, 3, 17, 8, False, False),
     (5, 12, 3, 33, 12, True, False),
     (2, 64, 3, 8, 64, False, False),
@@ -63,18 +67,28 @@ def test_conv_bn_eval_matches_two_launches(B, Ci, H, Wi, Co, tr, must_fuse, with
     from timevqvae.hip.norm import bn_snake
     torch.manual_seed(B + Ci + Co)
     x = torch.randn(B, Ci, H, Wi, device=cuda)
-    w = (torch.randn(Ci, Co, 3, 4) if tr else torch.randn(Co, Ci, 3, 3)).to(cuda) * (Ci * 9) ** -0.5
+    enc = tr == "enc"  # EncBlock: replicate-padded 3x4 stride-2 conv
+    tr = tr is True
+    w = (torch.randn(Ci, Co, 3, 4) if tr else torch.randn(Co, Ci, 3, 4 if enc else 3)).to(cuda) * (Ci * 9) ** -0.5
     b = torch.randn(Co, device=cuda) * 0.1
     bn, a = _bn(Co, cuda, B + Co)
     a = a if with_snake else None
     with torch.no_grad():
         with plan_trace() as tr_:
-            y = conv_transpose2d_bn_eval(x, w, b, bn, a) if tr else conv2d_bn_eval(x, w, b, bn, a)
+            if enc:
+                y = conv2d_bn_eval(x, w, b, bn, a, stride_w=2, replicate=True)
+            else:
+                y = conv_transpose2d_bn_eval(x, w, b, bn, a) if tr else conv2d_bn_eval(x, w, b, bn, a)
             torch.cuda.synchronize()
-        h = conv_transpose2d(x, w, b) if tr else conv2d(x, w, b)
+        if enc:
+            h = conv2d(x, w, b, stride_w=2, replicate=True)
+            hr = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="replicate"), w, b, stride=(1, 2))
+        else:
+            h = conv_transpose2d(x, w, b) if tr else conv2d(x, w, b)
+            hr = (F.conv_transpose2d(x, w, b, stride=(1, 2), padding=(1, 1)) if tr
+                  else F.conv2d(x, w, b, padding=1))
         want = bn_snake(h, bn, a)
-        ref = _torch_ref((F.conv_transpose2d(x, w, b, stride=(1, 2), padding=(1, 1)) if tr
-                          else F.conv2d(x, w, b, padding=1)), bn, a)
+        ref = _torch_ref(hr, bn, a)
     sep = tr_.has("bn_eval separate")
     if must_fuse:
         assert not sep, tr_.lines

@@ -1,0 +1,20 @@
+#!/bin/bash
+# EncBlock eval conv + BN (conv_s2f POST): tests, joint step, step kernel table
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_conv_bn_eval.py tests/test_stage2_golden.py tests/test_stage2.py tests/test_graph.py tests/test_sampler_full.py > gpurun_out/r4r_tests.log 2>&1 || { tail -40 gpurun_out/r4r_tests.log; exit 1; }
+tail -1 gpurun_out/r4r_tests.log
+STEPARGS="--no-sampler --no-roofline --no-config0 --no-cpu-baseline"
+for i in 1 2; do
+for F in 1 0; do
+TVQ_FUSED_BN_EVAL=$F timeout -k 10 300 python bench.py --steps 30 --warmup 5 $STEPARGS > gpurun_out/r4r_bench.log 2>&1 || { tail -20 gpurun_out/r4r_bench.log; exit 1; }
+echo "fused=$F $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r4r_bench.log)"
+done
+done
+rm -rf gpurun_out/r4r_step
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4r_step -o step -- python bench.py --steps 5 --warmup 2 $STEPARGS > gpurun_out/r4r_step.log 2>&1 || { tail -20 gpurun_out/r4r_step.log; exit 1; }
+T=$(find gpurun_out/r4r_step -name "*kernel_trace.csv" | head -1)
+python tools/step_table.py "$T" 5 gpurun_out/r4r_step_table.csv > gpurun_out/r4r_table.txt
+head -1 gpurun_out/r4r_table.txt
+grep -E "bn_eval|s2f|snake_fwd" gpurun_out/r4r_step_table.csv
