@@ -712,7 +712,7 @@ def conv_t32_leg(device):
             "avg_launch_ms": round(ms, 4), "flops_per_launch": flops}, "t32")
 
 
-def sampler_leg(tr, device, num=1024, reps=5):
+def sampler_leg(tr, device, num=1024, reps=5, graph_reps=20):
     """BASELINE configs[4]: MaskGIT iterative decoding (LF 10 steps + HF 1 step) of `num`
     trajectories + LF/HF decoding to (num, 6, 256), with the bench's stage2 weights
     (tools/sampler_bench.py is the standalone version with a CPU baseline)."""
@@ -729,21 +729,22 @@ def sampler_leg(tr, device, num=1024, reps=5):
     from timevqvae.utils.sample_utils import GraphedSampler
     fe = FidelityEnhancer(T, C, config(False)).to(device).eval()
 
-    def timed(fn):
+    def timed(fn, n=reps):
+        fn()  # (a GraphedSampler captures here)
         fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(reps):
+        for _ in range(n):
             out = fn()
         torch.cuda.synchronize()
-        return (time.perf_counter() - t0) / reps, out
+        return (time.perf_counter() - t0) / n, out
 
     with torch.no_grad():
         dt_eager, x_new = timed(run)
         dt_fe, _ = timed(lambda: fe(x_new))
     # the whole batch as one hipGraph (GraphedSampler), without and with the FE
-    dt, _ = timed(GraphedSampler(mg, num, device).sample)
-    dt_g_fe, _ = timed(GraphedSampler(mg, num, device, fidelity_enhancer=fe).sample)
+    dt, _ = timed(GraphedSampler(mg, num, device).sample, graph_reps)
+    dt_g_fe, _ = timed(GraphedSampler(mg, num, device, fidelity_enhancer=fe).sample, graph_reps)
     mg.train(was)
     # the reference's TrainedModelSampler.sample = decode + FidelityEnhancer (sampler.py:141-169)
     gflop = SAMPLER_GFLOP_1024 * num / 1024
@@ -753,7 +754,8 @@ def sampler_leg(tr, device, num=1024, reps=5):
             "source": "tools/count_step_flops.py -> profiles/r03_step_flops.json "
                       "(sampler_gflop_per_1024)"}
     return {"num": num, "ms_per_batch": round(dt * 1e3, 3), "roofline": roof,
-            "trajectories_per_s": round(num / dt, 1), "reps": reps, "launch": "hipgraph",
+            "trajectories_per_s": round(num / dt, 1), "reps": graph_reps, "eager_reps": reps,
+            "launch": "hipgraph",
             "eager_ms_per_batch": round(dt_eager * 1e3, 3),
             "fidelity_enhancer_ms": round(dt_fe * 1e3, 3),
             "with_fe_ms_per_batch": round(dt_g_fe * 1e3, 3),
