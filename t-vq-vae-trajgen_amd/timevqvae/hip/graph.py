@@ -98,11 +98,19 @@ class BranchStepGraph:
     backward ends -- while the other branch still computes -- and the optimizers are the
     final graph.  Each graph has its own memory pool: branch graphs replay concurrently, so
     their allocations must not alias (graphs sharing a pool must replay in capture order).
+
+    replay_order: the order the branches (and their exchanges) are enqueued at replay.  The
+    collectives of one process group run in host-issue order on its communication stream
+    (torch's ProcessGroupNCCL stream; the same order on every rank, so RCCL cannot
+    deadlock), so the branch that finishes first must be issued first for its exchange to
+    overlap the other branch's compute.  Capture always runs in list order.
     """
 
-    def __init__(self, pre, branches, afters, final, warmup=2, before=None):
+    def __init__(self, pre, branches, afters, final, warmup=2, before=None, replay_order=None):
         self.pre, self.branches, self.afters = pre, list(branches), list(afters)
         self.final, self.before, self.warmup = final, before, warmup
+        self.order = list(replay_order) if replay_order is not None else list(range(len(self.branches)))
+        assert sorted(self.order) == list(range(len(self.branches))), "replay_order: a permutation"
         self.graphs = self.final_graph = None
         self.outputs = None
         self._streams = None
@@ -163,7 +171,8 @@ class BranchStepGraph:
             self.before()
         cur = torch.cuda.current_stream()
         self.pre()
-        for g, aft, st in zip(self.graphs, self.afters, self._streams):
+        for i in self.order:
+            g, aft, st = self.graphs[i], self.afters[i], self._streams[i]
             st.wait_stream(cur)
             with torch.cuda.stream(st):
                 g.replay()
