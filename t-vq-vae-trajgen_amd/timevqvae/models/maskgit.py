@@ -256,10 +256,13 @@ class MaskGIT(nn.Module):
             unknown_number_in_the_beginning_h, gamma)
 
     @torch.no_grad()
-    def iterative_decoding(self, num=1, mode="cosine", class_index=None, device="cpu"):
+    def iterative_decoding(self, num=1, mode="cosine", class_index=None, device="cpu",
+                           after_lf=None):
         """maskgit.py:413-446 -> (s_l (num, n), s_h (num, m)) int64, on `device`.  Every
         step stays on the device; the only host values are the per-step mask lengths,
-        known in advance (all tokens start masked)."""
+        known in advance (all tokens start masked).  after_lf(s_l), if given, is called once
+        the LF tokens are final, before the HF pass (GraphedSampler forks the LF decoder
+        onto a side stream there); the HF pass only reads s_l."""
         s_l = self.create_input_tokens_normal(num, self.num_tokens_l, self.mask_token_ids["lf"],
                                               device)
         s_h = self.create_input_tokens_normal(num, self.num_tokens_h, self.mask_token_ids["hf"],
@@ -268,6 +271,8 @@ class MaskGIT(nn.Module):
         class_condition = (torch.full((num, 1), int(class_index), dtype=torch.int32, device=device)
                            if class_index is not None else None)
         s_l = self.first_pass(s_l, self.num_tokens_l, class_condition, gamma, device)
+        if after_lf is not None:
+            after_lf(s_l)
         s_h = self.second_pass(s_l, s_h, self.num_tokens_h, class_condition, gamma, device)
         return s_l, s_h
 

@@ -2,6 +2,8 @@
 (unconditional_sample / conditional_sample, sample_utils.py:5-88; the plotting helper is
 not on the path).  MaskGIT.iterative_decoding and decode_token_ind_to_timeseries run on
 the HIP path; each batch reaches the host by an asynchronous copy into pinned memory."""
+import os
+
 import torch
 
 from ..hip.loss import add_losses
@@ -87,14 +89,32 @@ class GraphedSampler:
         # the convs' packed weights: repacked by a few batched launches at the start of each
         # replay instead of one pack launch per conv (the weights are fixed within a batch)
         self.packs = PackCache(self.device)
+        # the LF decoder needs only the final LF tokens: it runs on a side stream while the
+        # HF prior's pass and the HF decoder run (TVQ_SAMPLER_OVERLAP=0: one stream)
+        overlap = os.environ.get("TVQ_SAMPLER_OVERLAP", "1") != "0" and self.device.type == "cuda"
+        self._side = torch.cuda.Stream(self.device) if overlap else None
 
         def batch():
             with torch.no_grad(), self.packs.scope():
                 rng.advance(self.device)
+                held = {}
+
+                def after_lf(s_l):
+                    if self._side is None:
+                        return
+                    self._side.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(self._side):
+                        held["x_l"] = maskgit.decode_token_ind_to_timeseries(s_l, "lf")
+
                 s_l, s_h = maskgit.iterative_decoding(num=num, device=self.device,
-                                                      class_index=class_index)
-                x_l = maskgit.decode_token_ind_to_timeseries(s_l, "lf")
+                                                      class_index=class_index,
+                                                      after_lf=after_lf)
                 x_h = maskgit.decode_token_ind_to_timeseries(s_h, "hf")
+                if self._side is not None:
+                    torch.cuda.current_stream(self.device).wait_stream(self._side)
+                    x_l = held["x_l"]
+                else:
+                    x_l = maskgit.decode_token_ind_to_timeseries(s_l, "lf")
                 out = (x_l, x_h, add_losses(x_l, x_h))  # one HIP add (tvq_sum4)
                 if fidelity_enhancer is not None:
                     out = out + (fidelity_enhancer(out[2]),)
