@@ -797,9 +797,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 path on a one-GPU box (all ranks on cuda:0 over gloo; RCCL
+    # refuses two ranks on one device): TVQ_BENCH_REHEARSAL=1.  Timings so obtained are not
+    # scaling numbers.
+    rehearsal = os.environ.get("TVQ_BENCH_REHEARSAL", "0") == "1"
+    if rehearsal:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if rehearsal else "nccl")
     device = torch.device("cuda", local)
     tr = JointTrainer(device, world)
     batch = synthetic_batch(1234 + rank, device)
