@@ -111,6 +111,7 @@ class JointTrainer:
         self._one = torch.ones((), device=device)
         self.graph = None
         self._pending = []
+        self._scheds = (None, None)
         from timevqvae.hip.conv import PackCache
         on = os.environ.get("TVQ_PACK_CACHE", "1") != "0"
         self.packs = PackCache(device) if on else None
@@ -156,19 +157,23 @@ class JointTrainer:
                 out2["loss"].backward(self._one)
         return out2
 
-    def _fwd_bwd(self, batch, defer):
+    def _fwd_bwd(self, batch, defer, only=None, packs=None):
         """zero_grad, then stage1's LF and HF bands (forward+backward, one side stream
         each) || stage2 forward+backward on the current stream (with its own HF side
-        streams); every stream is joined when the region ends.
+        streams); every stream is joined when the region ends.  only: "stage1" / "stage2"
+        runs that stage alone (the bench's per-stage legs).
         Returns (out1, out2, deferred codebook updates)."""
         import contextlib
         from timevqvae.hip import streams, wgrad
         from timevqvae.hip.conv import wgrad_deferred
         from timevqvae.hip.vq import deferred_codebook_updates
-        self.opt1.zero_grad()
-        self.opt2.zero_grad()
-        only = os.environ.get("TVQ_BENCH_ONLY")  # diagnosis: time one stage alone
-        packs = self.packs.scope() if self.packs is not None else contextlib.nullcontext()
+        only = only or os.environ.get("TVQ_BENCH_ONLY")  # diagnosis: time one stage alone
+        if only != "stage2":
+            self.opt1.zero_grad()
+        if only != "stage1":
+            self.opt2.zero_grad()
+        packs = packs if packs is not None else self.packs
+        packs = packs.scope() if packs is not None else contextlib.nullcontext()
         with packs, streams.concurrent():
             with (deferred_codebook_updates() if defer else contextlib.nullcontext([])) as pend:
                 # diagnosis only (TVQ_BENCH_BANDS=LF|HF): one stage1 band alone
@@ -199,11 +204,51 @@ class JointTrainer:
         self._sync_buffers()
         return out1, out2
 
+    def stage_alone_ms(self, batch, which, steps=20, warmup=3):
+        """One stage's optimizer step alone (the reference trains the stages one after the
+        other), as its own hipGraph [advance seed, zero_grad, fwd+bwd (+ codebook EMA),
+        AdamW] with its own weight-pack cache, replayed `steps` times after `warmup`: the
+        per-stage reading beside the concurrent joint step.  World 1 only."""
+        from timevqvae.hip import rng
+        from timevqvae.hip.conv import PackCache
+        from timevqvae.hip.graph import StepGraph
+        opt = self.opt1 if which == "stage1" else self.opt2
+        sch = self._scheds[0 if which == "stage1" else 1]
+        packs = PackCache(self.device) if self.packs is not None else None
+
+        def before():
+            if sch is not None:
+                sch.step()
+            opt.push_lr()
+
+        def seg():
+            from timevqvae.hip import streams
+            rng.advance(self.device)
+            out = self._fwd_bwd(batch, False, only=which, packs=packs)
+            opt.gather_gates()
+            streams.join(backward_done=True)
+            opt.step(lr_on_device=True, gates_ready=True)
+            return out
+
+        g = StepGraph([seg], [None], warmup=2, before=before).capture()
+        for _ in range(warmup):
+            g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        del g
+        torch.cuda.synchronize()
+        return dt * 1e3
+
     def capture(self, batch):
         """Capture the step (runs 2 eager warmup steps first)."""
         from timevqvae.hip import rng
         from timevqvae.hip.graph import StepGraph
         scheds = (self.s1._sched, self.s2._sched)
+        self._scheds = scheds
         self.s1._sched = self.s2._sched = None  # stepped on the host before each replay
         defer = self.world > 1  # sync_codebook all-reduce must sit between segments
 
@@ -368,6 +413,11 @@ STEP_GFLOP = 169.78
 # One sampler batch (BASELINE configs[4]: 1024 trajectories, 10 LF + 1 HF prior forwards and
 # both decoders), counted the same way -> profiles/r03_step_flops.json.
 SAMPLER_GFLOP_1024 = 375.0
+# What the sampler batch executes (tools/count_step_flops.py `sampler_executed_gflop_per_1024`):
+# the reference algorithm's count less the Linears the eval heads compose away while sampling
+# (LF project_in folded into the embedding tables; the HF project_in folded into Upscale's last
+# conv and the token table, project_out composed with pred_head's Linear).
+SAMPLER_EXEC_GFLOP_1024 = 343.2
 FP32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 
@@ -714,10 +764,13 @@ def conv_t32_leg(device):
             "avg_launch_ms": round(ms, 4), "flops_per_launch": flops}, "t32")
 
 
-def sampler_leg(tr, device, num=1024, reps=5, graph_reps=20):
+def sampler_leg(tr, device, num=1024, reps=5, graph_reps=20, world=1):
     """BASELINE configs[4]: MaskGIT iterative decoding (LF 10 steps + HF 1 step) of `num`
     trajectories + LF/HF decoding to (num, 6, 256), with the bench's stage2 weights
-    (tools/sampler_bench.py is the standalone version with a CPU baseline)."""
+    (tools/sampler_bench.py is the standalone version with a CPU baseline).  At world > 1
+    every rank runs its own replica of the graphed batch at the same time (sampling does not
+    shard: N GPUs are N replicas, configs[4]'s "8 GPU throughput"): barrier, `graph_reps`
+    replays, barrier, the max elapsed over the ranks -> aggregate trajectories/s."""
     mg = tr.s2.maskgit
     was = mg.training
     mg.eval()
@@ -731,37 +784,59 @@ def sampler_leg(tr, device, num=1024, reps=5, graph_reps=20):
     from timevqvae.utils.sample_utils import GraphedSampler
     fe = FidelityEnhancer(T, C, config(False)).to(device).eval()
 
-    def timed(fn, n=reps):
+    def timed(fn, n=reps, sync_ranks=False):
         fn()  # (a GraphedSampler captures here)
         fn()
         torch.cuda.synchronize()
+        if sync_ranks:
+            dist.barrier()
         t0 = time.perf_counter()
         for _ in range(n):
             out = fn()
         torch.cuda.synchronize()
-        return (time.perf_counter() - t0) / n, out
+        if sync_ranks:
+            dist.barrier()
+        dt = (time.perf_counter() - t0) / n
+        if sync_ranks:
+            t = torch.tensor([dt], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t)
+        return dt, out
 
     with torch.no_grad():
         dt_eager, x_new = timed(run)
         dt_fe, _ = timed(lambda: fe(x_new))
     # the whole batch as one hipGraph (GraphedSampler), without and with the FE
-    dt, _ = timed(GraphedSampler(mg, num, device).sample, graph_reps)
-    dt_g_fe, _ = timed(GraphedSampler(mg, num, device, fidelity_enhancer=fe).sample, graph_reps)
+    dt, _ = timed(GraphedSampler(mg, num, device).sample, graph_reps, sync_ranks=world > 1)
+    dt_g_fe, _ = timed(GraphedSampler(mg, num, device, fidelity_enhancer=fe).sample, graph_reps,
+                       sync_ranks=world > 1)
     mg.train(was)
     # the reference's TrainedModelSampler.sample = decode + FidelityEnhancer (sampler.py:141-169)
     gflop = SAMPLER_GFLOP_1024 * num / 1024
+    gexec = SAMPLER_EXEC_GFLOP_1024 * num / 1024
     roof = {"bound": "mfma", "gflop": round(gflop, 2), "achieved": round(gflop / (dt * 1e3), 2),
             "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(gflop / (dt * 1e3) / FP32_PEAK_TFLOPS, 4),
-            "source": "tools/count_step_flops.py -> profiles/r03_step_flops.json "
-                      "(sampler_gflop_per_1024)"}
-    return {"num": num, "ms_per_batch": round(dt * 1e3, 3), "roofline": roof,
-            "trajectories_per_s": round(num / dt, 1), "reps": graph_reps, "eager_reps": reps,
-            "launch": "hipgraph",
-            "eager_ms_per_batch": round(dt_eager * 1e3, 3),
-            "fidelity_enhancer_ms": round(dt_fe * 1e3, 3),
-            "with_fe_ms_per_batch": round(dt_g_fe * 1e3, 3),
-            "with_fe_trajectories_per_s": round(num / dt_g_fe, 1)}
+            "frac_counts": "the reference algorithm's FLOPs (what the batch computes, as the "
+                           "reference would)",
+            "executed_gflop": round(gexec, 2),
+            "executed_frac": round(gexec / (dt * 1e3) / FP32_PEAK_TFLOPS, 4),
+            "executed_counts": "the FLOPs the folded eval heads actually execute",
+            "source": "tools/count_step_flops.py -> profiles/r05_step_flops.json "
+                      "(sampler_gflop_per_1024, sampler_executed_gflop_per_1024)"}
+    out = {"num": num, "ms_per_batch": round(dt * 1e3, 3), "roofline": roof,
+           "trajectories_per_s": round(num / dt, 1), "reps": graph_reps, "eager_reps": reps,
+           "launch": "hipgraph",
+           "eager_ms_per_batch": round(dt_eager * 1e3, 3),
+           "fidelity_enhancer_ms": round(dt_fe * 1e3, 3),
+           "with_fe_ms_per_batch": round(dt_g_fe * 1e3, 3),
+           "with_fe_trajectories_per_s": round(num / dt_g_fe, 1)}
+    if world > 1:
+        out.update({"replicas": world, "ms_per_batch_is": "max over the ranks, all replicas "
+                                                           "sampling at once",
+                    "aggregate_trajectories_per_s": round(world * num / dt, 1),
+                    "aggregate_with_fe_trajectories_per_s": round(world * num / dt_g_fe, 1)})
+    return out
 
 
 def cpu_baseline_leg():
@@ -791,6 +866,7 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-sampler", action="store_true")
     ap.add_argument("--no-config0", action="store_true")
+    ap.add_argument("--no-stage-legs", action="store_true", help="skip the per-stage legs")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     args = ap.parse_args()
 
@@ -824,12 +900,20 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    rank_elapsed = [elapsed]
     if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+        t = torch.zeros(world, device=device, dtype=torch.float64)
+        t[rank] = elapsed
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)  # every rank's own elapsed time
+        rank_elapsed = [float(v) for v in t.cpu()]
+        elapsed = max(rank_elapsed)
     loss1 = float(out1["loss"].detach().sum())
     loss2 = float(out2["loss"].detach())
+    # each stage's optimizer step alone (graph-replayed; the reference trains them one after
+    # the other), beside the concurrent joint step
+    alone = None
+    if world == 1 and not args.eager and not args.no_stage_legs:
+        alone = {w: round(tr.stage_alone_ms(batch, w), 3) for w in ("stage1", "stage2")}
 
     if rank == 0:
         value = world * args.steps / elapsed
@@ -857,14 +941,33 @@ def main():
             "losses": {"stage1": round(loss1, 5), "stage2": round(loss2, 5)},
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 3),
         }
+        if alone is not None:
+            res["stage1_ms_per_step"] = alone["stage1"]
+            res["stage2_ms_per_step"] = alone["stage2"]
+            res["sequential_ms_per_step"] = round(alone["stage1"] + alone["stage2"], 3)
+            res["ms_per_step_is"] = ("stage1 and stage2 steps run concurrently on one GPU "
+                                     "(independent: stage2 trains on a frozen stage1 snapshot); "
+                                     "sequential_ms_per_step = the two stages alone, one after "
+                                     "the other, as the reference trains them")
+        if world > 1:
+            res["dist"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                           "rank_elapsed_s": [round(v, 6) for v in rank_elapsed],
+                           "physical_gpus": 1 if rehearsal else world}
+            if rehearsal:
+                res["rehearsal"] = True
+                res["parallelism_note"] = ("REHEARSAL: every rank on cuda:0 over gloo; not a "
+                                           "multi-GPU measurement")
         if not args.no_roofline:
             res["roofline"] = roofline_leg(device, res["ms_per_step"])
-        if not args.no_sampler:
-            res["sampler"] = sampler_leg(tr, device)
-        if not args.no_config0 and world == 1:
+        if not args.no_config0 and world == 1:  # (before the sampler: rank 0 only)
             res["config0"] = config0_leg(device, cpu=not args.no_cpu_baseline)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline_leg()
+    if not args.no_sampler:  # every rank: replicas sample concurrently at world > 1
+        samp = sampler_leg(tr, device, world=world)
+    if rank == 0:
+        if not args.no_sampler:
+            res["sampler"] = samp
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -33,6 +33,9 @@ typedef void* tvq_stream_t; /* hipStream_t */
 
 const char* tvq_last_error(void);
 int tvq_abi_version(void);
+/* Source stamp compiled in by csrc/Makefile: the first 16 hex digits of the sha1 of every
+ * csrc *.hip / *.h (sorted by name) followed by include/tvq.h. */
+const char* tvq_source_hash(void);
 /* Register a zeroed pool of n int32 counters on `device` (a HIP device index).  The
  * kernels that finish a grid-level reduction in their last-arriving block (BatchNorm /
  * Snake statistics, column sums, split-K slabs) take slots from it and leave them
@@ -180,8 +183,7 @@ int tvq_conv_out_width(int64_t Win, int64_t KW, int64_t SW, int64_t transposed);
  * wide-channel tile, 16 / 32 = its K stage BK = 32 / 16 (default 64), 64 = its 4-wave
  * block (default 12 waves), 128 = its 64-channel variant for narrow maps (default off),
  * 256 = no direct small transposed-gather kernel, 512 = no stride-2 small-channel conv
- * kernels (conv_s2f / conv_s2t), 1024 = no stride-2 small-channel weight-gradient kernel,
- * 2048 = the channel-chunked halo kernel for wide-input -> <= 16-output convs (default off);
+ * kernels (conv_s2f / conv_s2t), 1024 = no stride-2 small-channel weight-gradient kernel;
  * 0 forces the staged GEMMs (with the stride-2 kernels); < 0 only queries.  Default 3.
  * Returns the previous setting. */
 int tvq_conv_config(int64_t halo);
@@ -466,26 +468,6 @@ int tvq_embedding_bwd(const int64_t* idx, int64_t M, int64_t D, const float* g, 
                       int64_t V, float* tgrad, int64_t accumulate, int64_t mask_id, float drop_p,
                       const int64_t* seed_ptr, uint64_t offset, int32_t* workspace,
                       tvq_stream_t stream);
-/* Tied logits + masked cross-entropy in training, the logits never written
- * (bidirectional_transformer.py:186-191 + maskgit.py:183-191):
- *   logits[m, k] = h[m, :] . W[k, :] + bias[m % n, k]   (k < K; h (M, D) row-major, D in
- *                  {32, 64, 128}; W (>= K, D) the tied token table; bias row stride ldb)
- *   out = {mean over rows with keep[m] == false of (lse[m] - logits[m, target[m]]), count}
- * lse (M floats) is kept for the backward.  K % 32 == 0; h, W 16-byte aligned.
- * Backward (gout: d loss, stats: fwd `out`): dh (M, D) written (NULL: skipped); dW (K, D)
- * and dbias (n, ldb; columns >= K get 0) summed over rows in a fixed split order and added
- * when accumulate (NULL: skipped).  workspace: tvq_tied_ce_workspace floats, the same
- * buffer for fwd and bwd. */
-int64_t tvq_tied_ce_workspace(int64_t M, int64_t D, int64_t K, int64_t n, int64_t ldb);
-int tvq_tied_ce_fwd(const float* h, int64_t M, int64_t D, const float* W, int64_t K,
-                    const float* bias, int64_t n, int64_t ldb, const int64_t* target,
-                    const bool* keep, float* lse, float* out, float* workspace,
-                    tvq_stream_t stream);
-int tvq_tied_ce_bwd(const float* h, int64_t M, int64_t D, const float* W, int64_t K,
-                    const float* bias, int64_t n, int64_t ldb, const int64_t* target,
-                    const bool* keep, const float* lse, const float* stats, const float* gout,
-                    float* dh, float* dW, float* dbias, int64_t accumulate, float* workspace,
-                    tvq_stream_t stream);
 /* embed[:, 1:, :] of the priors (the class token dropped before the head,
  * bidirectional_transformer.py:188,233): backward == 0: y (B, n, D) from x (B, n+1, D);
  * backward != 0: its adjoint, y (B, n+1, D) from x (B, n, D) with zero class rows.  D % 4 == 0,
@@ -518,15 +500,17 @@ int tvq_gelu_fwd(const float* x, int64_t n, float* y, tvq_stream_t stream);
  *   pre = xn W1^T + b1 (M x 128), hd = Dropout_p(GELU(pre)) (the mask: uniform01 of
  *   (seed, offset) at m * 128 + j >= p), y = r + gate * (hd W2^T + b2)   (gate nullable: 1)
  * one launch; 16-byte aligned pointers.  tvq_ffn_bwd: from gy = dL/dy the pre-activation
- * gradient d_pre (M x 128, for the W1 / b1 gradients) and d(xn); the W2 / b2 gradients are
- * the caller's (hd^T (gate gy)).  p in [0, 1). */
+ * gradient d_pre (M x 128, for the W1 / b1 gradients), d(xn) and, when gate and gy_gated are
+ * both non-null, gy_gated = gate * gy (M x 128): the W2 / b2 gradients are the caller's,
+ * hd^T (gate gy) and colsum(gate gy), so a dropped branch (gate 0) gets zero there.
+ * p in [0, 1). */
 int tvq_ffn_fwd(const float* xn, const float* r, int64_t M, int64_t D, const float* W1,
                 const float* b1, const float* W2, const float* b2, const float* gate, float p,
                 const int64_t* seed_ptr, uint64_t offset, float* y, float* pre, float* hd,
                 tvq_stream_t stream);
 int tvq_ffn_bwd(const float* gy, const float* pre, int64_t M, int64_t D, const float* W1,
                 const float* W2, const float* gate, float p, const int64_t* seed_ptr,
-                uint64_t offset, float* d_pre, float* dxn, tvq_stream_t stream);
+                uint64_t offset, float* d_pre, float* dxn, float* gy_gated, tvq_stream_t stream);
 int tvq_gelu_bwd(const float* dy, const float* x, int64_t n, float* dx, tvq_stream_t stream);
 
 /* ---------------------------------------------------------------- fused LF prior (eval)

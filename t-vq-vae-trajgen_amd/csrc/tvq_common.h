@@ -214,10 +214,13 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t ctr) {
 // away from 0, so g is finite: a code whose fp32 softmax probability is 0 (l_k < max - 103)
 // can never win, g being within [-2.9, 17.4].
 __device__ __forceinline__ uint32_t race_key(uint64_t seed) {
-  return (uint32_t)(seed ^ (seed >> 32));
+  return hash_u32(seed);
 }
 __device__ __forceinline__ float race_gumbel(uint32_t key, uint32_t ctr) {
-  uint32_t x = ctr + key;  // lowbias32 (2 multiplies: per (token, code) this is hot)
+  // the key enters as an affine map ctr * (key | 1) + key before lowbias32 (2 multiplies:
+  // per (token, code) this is hot): two calls' counter ranges meet only at scattered
+  // points, never as a shifted copy of one stream (which ctr + key alone would give)
+  uint32_t x = ctr * (key | 1u) + key;
   x ^= x >> 16;
   x *= 0x7FEB352Du;
   x ^= x >> 15;

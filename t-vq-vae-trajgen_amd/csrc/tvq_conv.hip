@@ -1184,113 +1184,6 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const float* __restrict_
   }
 }
 
-// Wide input, 16 outputs (the HF ResBlock's 128 -> 16 conv and 1x1 projection, the data
-// gradient of the 16 -> 128 conv; 0.11 of peak on the 16-row tap GEMM, which re-gathers every
-// input element once per tap from L2): one image per 4-wave block as in conv_halo_kernel, but
-// its channels staged in chunks of CC through LDS (halo planes + the 16 x CC*KK weight panel
-// of the chunk), the accumulators kept across chunks, so the input is read from HBM once and
-// a 128-channel image needs 42 KB of LDS instead of 169 KB.  Wave w owns the 16-position tiles
-// w, w + 4, ... (<= 4 each, P <= 256); reduction order: chunks in order, k in order inside.
-template <int MODE, int KH, int KW, int SW, bool REPL, int CC, bool POST = false>
-__global__ __launch_bounds__(256) void conv_halo_cc_kernel(const float* __restrict__ in,
-                                                          const float* __restrict__ wt,
-                                                          float* __restrict__ out, HaloGeom g,
-                                                          Epi e) {
-  constexpr int KK = KH * KW, KC = CC * KK;
-  constexpr int CSW = MODE == GATHER_F ? SW : 1;
-  extern __shared__ float smem[];
-  float* Hs = smem;                                     // [CC][PS]
-  float* As = Hs + CC * g.PS;                           // [16][KST]
-  int* koff = reinterpret_cast<int*>(As + 16 * g.KST);  // [KC]
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int b = blockIdx.x;
-  const int j = lane & 15, kq = lane >> 4;
-  const int HWin = g.Hin * g.Win;
-  for (int k = tid; k < KC; k += 256) {
-    const int c = k / KK, t = k - c * KK;
-    const int tl = MODE == GATHER_F ? t : KK - 1 - t;
-    koff[k] = c * g.PS + (tl / KW) * g.WP + (tl % KW);
-  }
-  const int fa = min(4, (g.MT - wid + 3) / 4);  // this wave's tiles: wid + 4 f, f < fa
-  int base[4];
-#pragma unroll
-  for (int f = 0; f < 4; ++f) {
-    const int p = (wid + 4 * f) * 16 + j;
-    const int pp = p < g.P ? p : 0;
-    const int h = div16(pp, g.dv_wo);
-    const int w = pp - h * g.Wo;
-    base[f] = h * g.WP + w * CSW;
-  }
-  floatx4 acc[4];
-#pragma unroll
-  for (int f = 0; f < 4; ++f) acc[f] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const bool n_inner = g.wsn < g.wsc;  // dgrad layout (c, n, t)
-  for (int c0 = 0; c0 < g.C; c0 += CC) {
-    if (c0 > 0) __syncthreads();  // every wave done with the previous chunk
-    halo_fill<MODE, KH, KW, SW, REPL>(Hs, in + ((int64_t)b * g.C + c0) * HWin, CC, CC, g.Hin,
-                                      g.Win, g.HP, g.WP, g.PS, g.oh, g.ow, g.dv_hw, g.dv_wp, tid);
-    for (int base0 = tid; base0 < 16 * KC; base0 += 256 * HALO_U) {
-      float v[HALO_U];
-      int dst[HALO_U];
-#pragma unroll
-      for (int u = 0; u < HALO_U; ++u) {
-        const int idx = base0 + u * 256;
-        v[u] = 0.f;
-        dst[u] = -1;
-        if (idx < 16 * KC) {
-          int nn, c, t;
-          if (n_inner) {
-            t = idx % KK;
-            const int r = idx / KK;
-            c = r / 16;
-            nn = r - c * 16;
-          } else {
-            nn = idx / KC;
-            const int k = idx - nn * KC;
-            c = k / KK;
-            t = k - c * KK;
-          }
-          dst[u] = nn * g.KST + c * KK + t;
-          if (nn < g.N) v[u] = wt[(int64_t)nn * g.wsn + (int64_t)(c0 + c) * g.wsc + t];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < HALO_U; ++u)
-        if (dst[u] >= 0) As[dst[u]] = v[u];
-    }
-    __syncthreads();
-    const float* ap = As + j * g.KST + kq;
-#pragma unroll 4
-    for (int q = 0; q < KC / 4; ++q) {
-      const int ko = koff[q * 4 + kq];
-      const float af = ap[q * 4];
-#pragma unroll
-      for (int f = 0; f < 4; ++f)
-        if (f < fa) acc[f] = mfma16x16x4(af, Hs[base[f] + ko], acc[f]);
-    }
-  }
-  const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
-  const int nbase = kq * 4;
-  float bv[1][4];
-  epi_load_bias<1>(bv, e.bias, nbase, g.N);
-  PostTile<1> pt;
-  if constexpr (POST) epi_load_post<1>(pt, e, nbase, g.N);
-  const int64_t hwo = (int64_t)g.Hout * g.Wo;
-#pragma unroll
-  for (int f = 0; f < 4; ++f) {
-    if (f < fa) {
-      const int p = (wid + 4 * f) * 16 + j;
-      const bool pv = p < g.P;
-      const int pp = pv ? p : 0;
-      const int h = div16(pp, g.dv_wo);
-      const int w = pp - h * g.Wo;
-      const floatx4 a[1] = {acc[f]};
-      epi_store<1, POST>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + w, hwo,
-                         nbase, g.N, pv, false, &pt);
-    }
-  }
-}
-
 // Direct convolution for few channels on both sides (C, N <= 16): the stride-2 encoder /
 // decoder convs and the decoders' ConvTranspose tail (12 <-> 4 / 12 channels at W up to
 // 512), where an MFMA tile would be mostly padding and the staged GEMMs are latency-bound.
@@ -3127,43 +3020,6 @@ static bool halo_preferred(int mode, int C, int KK, int SW, int N, int64_t Mpos)
   return true;
 }
 
-// conv_halo_cc_kernel: wide input (C % 32 == 0, C >= 64) into <= 16 outputs, stride 1, one
-// image of <= 256 positions per block.  Off by default (tvq_conv_config bit 2048 turns it on):
-// measured (tools/ab/r04/gpu_r4t.sh) 121 us for the HF 128 -> 16 3x3 conv at B = 256 against
-// 51 us on the 16-row tap GEMM -- one 4-wave block per image leaves one wave per SIMD, and
-// every MFMA step waits on two dependent LDS reads (the tap offset, then the window value);
-// sampler batch 5.62-5.64 vs 5.50-5.53 ms.
-constexpr int HCC_CC = 32;
-static int g_conv_hcc = 0;
-static bool hcc_on() { return g_conv_hcc != 0; }
-static bool halo_cc_plan(int mode, const ConvGeom& cg, int KH, int KW, int oh, int ow, HaloGeom* out,
-                         size_t* lds) {
-  if (!hcc_on() || cg.N > 16 || cg.C < 64 || cg.C % HCC_CC != 0 || cg.Hout * cg.Wo > 256 ||
-      cg.Wo < 2)
-    return false;
-  HaloGeom g;
-  g.C = cg.C; g.Cp = cg.C; g.Hin = cg.Hin; g.Win = cg.Win; g.N = cg.N; g.Hout = cg.Hout;
-  g.Wo = cg.Wo; g.oh = oh; g.ow = ow;
-  g.HP = cg.Hout + KH - 1;
-  g.WP = mode == GATHER_F ? (cg.Wo - 1) + KW : cg.Wo + KW - 1;
-  const int hw = g.HP * g.WP;
-  g.PS = hw + ((16 - hw % 32) + 32) % 32;
-  g.P = cg.Hout * cg.Wo;
-  g.MT = (g.P + 15) / 16;
-  g.wsn = cg.wsn; g.wsc = cg.wsc;
-  const int KC = HCC_CC * KH * KW;
-  g.KST = KC + ((2 - KC % 32) + 32) % 32;
-  g.dv_hw = make_div16(hw);
-  g.dv_wp = make_div16(g.WP);
-  g.dv_wo = make_div16(cg.Wo);
-  g.dv_k = make_div16(KC);
-  const size_t fl = (size_t)HCC_CC * g.PS + (size_t)16 * g.KST + KC;
-  if (fl * 4 > (size_t)HALO_LDS_MAX) return false;
-  *out = g;
-  *lds = fl * 4;
-  return true;
-}
-
 // halo path when the image + weight panel fit in LDS, else the staged GEMM
 // workspace (nullable) = [packed weight N*C*KK][split-K slab]; see conv_gemm_ws
 template <int MODE, int KH, int KW, int SW, bool REPL>
@@ -3198,22 +3054,6 @@ static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g
   HaloPlan pl;
   const int oh = MODE == GATHER_F ? g.oph : KH - 1 - g.oph;
   const int ow = MODE == GATHER_F ? g.opw : KW - 1 - g.opw;
-  if constexpr (SW == 1 && !REPL) {
-    HaloGeom hg;
-    size_t lds;
-    if (halo_cc_plan(MODE, g, KH, KW, oh, ow, &hg, &lds)) {
-      TVQ_PLAN("conv_halo_cc c%d n%d", g.C, g.N);
-      if (e.bn_rv) {
-        t_post_done = true;
-        hipLaunchKernelGGL((conv_halo_cc_kernel<MODE, KH, KW, SW, REPL, HCC_CC, true>), dim3(g.B),
-                           dim3(256), lds, st, in, wt, out, hg, e);
-      } else {
-        hipLaunchKernelGGL((conv_halo_cc_kernel<MODE, KH, KW, SW, REPL, HCC_CC>), dim3(g.B),
-                           dim3(256), lds, st, in, wt, out, hg, e);
-      }
-      return;
-    }
-  }
   if ((g_conv_halo & 1) && halo_preferred(MODE, g.C, KH * KW, SW, g.N, g.Mpos) && halo_plan(MODE, g.B, g.C, g.Hin, g.Win, g.N, g.Hout, g.Wo, KH, KW, SW, oh,
                                ow, g.wsn, g.wsc, &pl)) {
     TVQ_PLAN("conv_halo");
@@ -3401,7 +3241,7 @@ extern "C" int tvq_conv_config(int64_t halo) {
   const int prev = g_conv_halo | (g_conv_t32 ? 0 : 8) | (g_t32_bk == 32 ? 16 : 0) |
                    (g_t32_bk == 16 ? 32 : 0) | (g_t32_nw == 4 ? 64 : 0) |
                    (g_t32_n64 ? 128 : 0) | (g_conv_small ? 0 : 256) | (g_conv_s2 ? 0 : 512) |
-                   (g_conv_ws2 ? 0 : 1024) | (g_conv_hcc ? 2048 : 0);
+                   (g_conv_ws2 ? 0 : 1024);
   if (halo >= 0) {
     g_conv_halo = (int)(halo & 7);
     g_conv_t32 = (halo & 8) ? 0 : 1;
@@ -3411,7 +3251,6 @@ extern "C" int tvq_conv_config(int64_t halo) {
     g_conv_small = (halo & 256) ? 0 : 1;
     g_conv_s2 = (halo & 512) ? 0 : 1;
     g_conv_ws2 = (halo & 1024) ? 0 : 1;
-    g_conv_hcc = (halo & 2048) ? 1 : 0;
   }
   return prev;
 }
@@ -3502,7 +3341,10 @@ extern "C" int tvq_convT2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H,
 
 // Eval-mode conv -> BatchNorm(running statistics) -> Snake in one launch: the BN affine
 // and the Snake are the conv epilogue's (epi_post), no (B, Co, H, W) round trip through
-// HBM between them.  Same results, bit for bit, as tvq_conv2d_fwd + tvq_bn_eval_fwd.
+// HBM between them.  The same function as tvq_conv2d_fwd + tvq_bn_eval_fwd within ~1e-7
+// relative, not bit for bit: the epilogue's GELU is the branch-free A&S erf (gelu_as) and its
+// Snake sin^2 a Cody-Waite / polynomial form, where the separate launches call erff / sinf
+// (tests/test_conv_bn_eval.py: 1e-6 of the two-launch path).
 extern "C" int tvq_conv2d_fwd_bn_eval(const float* x, int64_t B, int64_t Ci, int64_t H,
                                       int64_t Wi, const float* w, const float* bias, int64_t Co,
                                       int64_t KH, int64_t KW, int64_t SW, int64_t replicate,

@@ -117,7 +117,7 @@ __device__ __forceinline__ void ff_exchange(float4 (*buf)[4][64], int w, const f
 
 struct FfArgs {
   const float *xn, *r, *W1, *b1, *W2, *b2, *gate, *gy, *pre_in;
-  float *y, *pre, *hd, *d_pre, *dxn;
+  float *y, *pre, *hd, *d_pre, *dxn, *gy_gated;
   const int64_t* seed_ptr;
   uint64_t offset;
   float p, scale;
@@ -191,6 +191,18 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfArgs a) {
   {
     float gb[64];
     ff_load_row(a.gy + m * FF_D, h, gb);
+    // gate * gy for the W2 / b2 gradients (a dropped branch's weights get a zero gradient):
+    // wave w stores the row's 32-feature slice w, already in registers
+    if (a.gy_gated && ok) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q == w)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(a.gy_gated + m * FF_D + 32 * q + 8 * g + 4 * h) =
+                make_float4(gt * gb[16 * q + 4 * g], gt * gb[16 * q + 4 * g + 1],
+                            gt * gb[16 * q + 4 * g + 2], gt * gb[16 * q + 4 * g + 3]);
+    }
     // d_hd (inner features 32 w ..) = gy W2: A(i, k) = W2[k][32 w + i]
     const floatx16 acc = ff_tile<true>(a.W2, 32 * w, gb, lane);
 #pragma unroll
@@ -250,15 +262,16 @@ extern "C" int tvq_ffn_fwd(const float* xn, const float* r, int64_t M, int64_t D
 extern "C" int tvq_ffn_bwd(const float* gy, const float* pre, int64_t M, int64_t D,
                            const float* W1, const float* W2, const float* gate, float p,
                            const int64_t* seed_ptr, uint64_t offset, float* d_pre, float* dxn,
-                           tvq_stream_t stream) {
+                           float* gy_gated, tvq_stream_t stream) {
   TVQ_CHECK_ARG(gy && pre && W1 && W2 && d_pre && dxn && M > 0 && D == FF_D && p >= 0.f &&
                     p < 1.f && (p == 0.f || seed_ptr),
                 "tvq_ffn_bwd: bad arguments (D must be 128)");
-  TVQ_CHECK_ARG(ff_aligned(gy) && ff_aligned(pre) && ff_aligned(d_pre) && ff_aligned(dxn),
+  TVQ_CHECK_ARG(ff_aligned(gy) && ff_aligned(pre) && ff_aligned(d_pre) && ff_aligned(dxn) &&
+                    ff_aligned(gy_gated),
                 "tvq_ffn_bwd: pointers must be 16-byte aligned");
   FfArgs a = {};
   a.gy = gy; a.pre_in = pre; a.W1 = W1; a.W2 = W2; a.gate = gate;
-  a.d_pre = d_pre; a.dxn = dxn; a.seed_ptr = seed_ptr; a.offset = offset;
+  a.d_pre = d_pre; a.dxn = dxn; a.gy_gated = gate ? gy_gated : nullptr; a.seed_ptr = seed_ptr; a.offset = offset;
   a.p = p; a.scale = p > 0.f ? 1.0f / (1.0f - p) : 1.0f; a.M = (int)M;
   hipLaunchKernelGGL(ffn_bwd_kernel, dim3((unsigned)((M + 31) / 32)), dim3(256), 0,
                      (hipStream_t)stream, a);

@@ -31,6 +31,36 @@ def sig(name, *argtypes, restype=I32):
     SIGNATURES[name] = (list(argtypes), restype)
 
 
+CSRC = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "csrc")
+
+
+def source_hash():
+    """The stamp csrc/Makefile compiles into the library (tvq_source_hash): sha1 of every
+    csrc *.hip / *.h sorted by name, then include/tvq.h, first 16 hex digits."""
+    import hashlib
+    h = hashlib.sha1()
+    names = sorted(n for n in os.listdir(CSRC) if n.endswith((".hip", ".h")))
+    for n in names + [os.path.join("..", "..", "include", "tvq.h")]:
+        with open(os.path.join(CSRC, n), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def built_hash(path=None):
+    """tvq_source_hash() of the built library at `path` (None if missing or unstamped),
+    read without initialising the GPU."""
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        return None
+    try:
+        f = ctypes.CDLL(path).tvq_source_hash
+    except (OSError, AttributeError):
+        return None
+    f.restype = ctypes.c_char_p
+    return f().decode()
+
+
+sig("tvq_source_hash", restype=ctypes.c_char_p)
 sig("tvq_counter_pool", I64, P, I64)
 sig("tvq_counter_capture", I64)
 sig("tvq_plan_trace", I64)
@@ -127,9 +157,6 @@ sig("tvq_embedding_bwd_workspace", I64, I64, restype=I64)
 sig("tvq_embedding_bwd", P, I64, I64, P, I64, I64, P, I64, I64, F32, P, U64, P, P)
 sig("tvq_masked_ce_workspace", I64, restype=I64)
 sig("tvq_drop_first_token", P, I64, I64, I64, P, I64, P)
-sig("tvq_tied_ce_workspace", I64, I64, I64, I64, I64, restype=I64)
-sig("tvq_tied_ce_fwd", P, I64, I64, P, I64, P, I64, I64, P, P, P, P, P, P)
-sig("tvq_tied_ce_bwd", P, I64, I64, P, I64, P, I64, I64, P, P, P, P, P, P, P, P, I64, P, P)
 sig("tvq_masked_ce_fwd", P, I64, I64, I64, P, P, P, P, P, P)
 sig("tvq_masked_ce_bwd", P, I64, I64, I64, P, P, P, P, P, P, I64, P)
 sig("tvq_mask_tokens", P, I64, I64, I64, P, U64, P, P, P, P, P)
@@ -141,7 +168,7 @@ sig("tvq_gelu_bwd", P, P, I64, P, P)
 sig("tvq_prior_lf_eval_workspace", I64, I64, I64, I64, restype=I64)
 sig("tvq_prior_lf_eval", P, I64, I64, I64, P, I64, I64, P, I64, I64, F32, P, P, P)
 sig("tvq_ffn_fwd", P, P, I64, I64, P, P, P, P, P, F32, P, U64, P, P, P, P)
-sig("tvq_ffn_bwd", P, P, I64, I64, P, P, P, F32, P, U64, P, P, P)
+sig("tvq_ffn_bwd", P, P, I64, I64, P, P, P, F32, P, U64, P, P, P, P)
 sig("tvq_prior_lf_eval_sample", P, I64, I64, I64, P, I64, I64, P, I64, I64, F32, I64, P, P, U64,
     P, P, P, P, I64, P)
 sig("tvq_maskgit_sample", P, I64, I64, I64, I64, I64, P, I64, P, P, U64, P, P, P)

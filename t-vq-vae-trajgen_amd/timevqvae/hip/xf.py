@@ -187,9 +187,10 @@ class _FusedFF(torch.autograd.Function):
     """r + gate * (dropout(GELU(xn W1^T + b1)) W2^T + b2) with D = inner = 128 in one launch
     forward and one backward (csrc/tvq_ffn.hip; x-transformers FeedForward in the pre-norm
     residual, bidirectional_transformer.py:92-110).  Weight / bias gradients go through the
-    grouped weight-gradient path like every Linear's; dW2 / db2 are taken from the ungated
-    output gradient: when the layer-dropout gate is 0 the branch's segment is skipped by
-    FusedAdamW (its gradient is never read), and when it is 1 the two are the same."""
+    grouped weight-gradient path like every Linear's; dW2 / db2 are taken from gate * gy,
+    which the backward kernel writes when a gate is given (as the per-op path's scale_by):
+    a forward whose branch was dropped adds exactly zero to them, whatever other forwards
+    (gradient accumulation) or replicas did with the same segment."""
 
     @staticmethod
     def forward(ctx, xn, r, w1, b1, w2, b2, gate, p, site):
@@ -216,12 +217,14 @@ class _FusedFF(torch.autograd.Function):
         g2 = gy.reshape(-1, 128).contiguous()
         M = g2.shape[0]
         d_pre, dxn = torch.empty_like(g2), torch.empty_like(g2)
-        call("tvq_ffn_bwd", ptr(g2), ptr(pre), M, 128, ptr(w1), ptr(w2), ptr(ctx.gate), p,
-             ptr(ctx.seed), off, ptr(d_pre), ptr(dxn), stream_ptr())
         need = ctx.needs_input_grad
+        gg = torch.empty_like(g2) if ctx.gate is not None and (need[4] or need[5]) else None
+        call("tvq_ffn_bwd", ptr(g2), ptr(pre), M, 128, ptr(w1), ptr(w2), ptr(ctx.gate), p,
+             ptr(ctx.seed), off, ptr(d_pre), ptr(dxn), ptr(gg), stream_ptr())
         W1p, b1p, W2p, b2p = ctx.params
-        dw2 = weight_grad(g2, hd, W2p, M, 128, 128, ctx.wg_tag) if need[4] else None
-        db2 = _bias_grad_rows(g2, grad_sink(b2p)) if need[5] else None
+        g2w = gg if gg is not None else g2
+        dw2 = weight_grad(g2w, hd, W2p, M, 128, 128, ctx.wg_tag) if need[4] else None
+        db2 = _bias_grad_rows(g2w, grad_sink(b2p)) if need[5] else None
         dw1 = weight_grad(d_pre, x2, W1p, M, 128, 128, ctx.wg_tag) if need[2] else None
         db1 = _bias_grad_rows(d_pre, grad_sink(b1p)) if need[3] else None
         return (dxn.reshape(shp) if need[0] else None, gy if need[1] else None, dw1, db1, dw2,

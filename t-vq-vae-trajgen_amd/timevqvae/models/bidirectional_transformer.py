@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from ..hip import rng, streams
-from ..hip.conv import PackCache, _immediate, _keep, bn_eval_fusable, conv2d, conv2d_bn_eval
+from ..hip.conv import PackCache, bn_eval_fusable, conv2d, conv2d_bn_eval
 from ..hip.linear import gemm, linear
 from ..hip.norm import bn_snake
 from ..hip.xf import (batch_colsum, drop_first_token, embed_assemble, embedding, fused_ff,
@@ -273,52 +273,6 @@ class _TiedLogits(torch.autograd.Function):
         return dh, dW, dbias, None
 
 
-class _TiedCE(torch.autograd.Function):
-    """F.cross_entropy((embed @ W[:K]^T + bias[:, :K])[~keep], target[~keep]) without the
-    logits in memory (csrc/tvq_ce.hip; bidirectional_transformer.py:186-191 +
-    maskgit.py:183-191): the training loss of a prior when nothing else reads its logits."""
-
-    @staticmethod
-    def forward(ctx, h, W, bias, K, target, keep):
-        B, n, D = h.shape
-        h2 = h.reshape(B * n, D).contiguous()
-        M = B * n
-        t = target.reshape(-1).contiguous()
-        kp = keep.reshape(-1).contiguous()
-        dev = h.device
-        ws = torch.empty(value("tvq_tied_ce_workspace", M, D, K, bias.shape[0], bias.shape[1]),
-                         device=dev)
-        lse = torch.empty(M, device=dev)
-        out = torch.empty(2, device=dev)
-        call("tvq_tied_ce_fwd", ptr(h2), M, D, ptr(W), K, ptr(bias), bias.shape[0], bias.shape[1],
-             ptr(t), ptr(kp), ptr(lse), ptr(out), ptr(ws), stream_ptr())
-        ctx.save_for_backward(h2, W, bias, t, kp, lse, out, ws)
-        ctx.params = (W, bias)
-        ctx.cfg = (B, n, D, K)
-        return out[0]
-
-    @staticmethod
-    def backward(ctx, g):
-        h2, W, bias, t, kp, lse, stats, ws = ctx.saved_tensors
-        B, n, D, K = ctx.cfg
-        M = B * n
-        W_p, b_p = ctx.params
-        need_h, need_w, need_b = ctx.needs_input_grad[:3]
-        dh = torch.empty_like(h2) if need_h else None
-        sw = grad_sink(W_p) if need_w else None
-        sb = grad_sink(b_p) if need_b else None
-        dW = sw if sw is not None else (torch.zeros_like(W) if need_w else None)
-        db = sb if sb is not None else (torch.zeros_like(bias) if need_b else None)
-        gg = g.reshape(1).contiguous()
-        with _immediate(sw is None or sb is None):
-            call("tvq_tied_ce_bwd", ptr(h2), M, D, ptr(W), K, ptr(bias), bias.shape[0],
-                 bias.shape[1], ptr(t), ptr(kp), ptr(lse), ptr(stats), ptr(gg), ptr(dh), ptr(dW),
-                 ptr(db), 1, ptr(ws), stream_ptr())
-        _keep(ws)
-        return (dh.reshape(B, n, D) if dh is not None else None,
-                None if sw is not None else dW, None if sb is not None else db, None, None, None)
-
-
 class Upscale(nn.Module):
     """bidirectional_transformer.py:12-30: nearest x(m/n) -> Conv1d(k3) -> GELU -> BN1d -> Conv1d(k3)."""
 
@@ -534,15 +488,6 @@ class BidirectionalTransformer(nn.Module):
         x = self.blocks.attn_layers(x)
         h = linear_act(drop_first_token(x), Wc, lin.bias, gelu=True)
         return layer_norm(h, ln.weight, ln.bias, ln.eps)
-
-    def masked_ce(self, target, keep, s_M_l, s_M_h=None, class_condition=None):
-        """F.cross_entropy(self(...)[~keep], target[~keep]) (maskgit.py:183-191) with the tied
-        logits and the CE fused (_TiedCE): MaskGIT's training loss of this prior."""
-        if self.kind == "lf":
-            embed, table = self._embed_lf(s_M_l, class_condition), self.tok_emb_l.weight
-        else:
-            embed, table = self._embed_hf(s_M_l, s_M_h, class_condition), self.tok_emb_h.weight
-        return _TiedCE.apply(embed, table, self.bias, self.codebook_size, target, keep)
 
     def forward(self, s_M_l, s_M_h=None, class_condition: Union[None, torch.Tensor] = None):
         if self.kind == "lf":

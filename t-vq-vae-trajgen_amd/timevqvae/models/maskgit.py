@@ -34,11 +34,6 @@ def _latent_width(T: int, n_enc_blocks: int) -> int:
     return W
 
 
-# TVQ_FUSED_CE=1: the priors' training loss through the fused tied-logits CE (csrc/tvq_ce.hip,
-# no logits in HBM).  Off by default: it recomputes the logits in both backward kernels (5
-# logits-sized GEMMs instead of 3, 16 vs 9.6 GFLOP at B=256), and measured 4.79 vs 4.72 ms
-# per joint step (tools/ab/r04/gpu_r4e.sh): the logits GEMMs were MFMA-bound, not memory-bound.
-FUSED_CE = os.environ.get("TVQ_FUSED_CE", "0") == "1"
 
 
 class MaskGIT(nn.Module):
@@ -153,24 +148,15 @@ class MaskGIT(nn.Module):
         self.transformer_l._class_rand = dr.get("cls_l")
         self.transformer_h._class_rand = dr.get("cls_h")
         try:
-            # cfg_scale 1 (or no class): masked_prediction is one plain forward, and nothing
-            # but the masked CE reads its logits -> the fused tied-logits CE (no logits in HBM)
-            fused = self.cfg_scale == 1.0 and FUSED_CE
             with streams.branch(x.device) as br:  # HF transformer concurrently with LF
                 br.inputs(y, s_l_M, s_h_M, s_h, keep_h)
                 with wgrad.tag("prior_h"):  # its weight gradients: one grouped launch
-                    if fused:
-                        mask_pred_loss_h = self.transformer_h.masked_ce(s_h, keep_h, s_l_M, s_h_M, y)
-                    else:
-                        logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
-                        mask_pred_loss_h = masked_cross_entropy(logits_h, s_h, keep_h)
+                    logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
+                    mask_pred_loss_h = masked_cross_entropy(logits_h, s_h, keep_h)
                 br.outputs(mask_pred_loss_h)
             with wgrad.tag("prior_l"):
-                if fused:
-                    mask_pred_loss_l = self.transformer_l.masked_ce(s_l, keep_l, s_l_M, None, y)
-                else:
-                    logits_l = self.masked_prediction(self.transformer_l, y, s_l_M)
-                    mask_pred_loss_l = masked_cross_entropy(logits_l, s_l, keep_l)
+                logits_l = self.masked_prediction(self.transformer_l, y, s_l_M)
+                mask_pred_loss_l = masked_cross_entropy(logits_l, s_l, keep_l)
             br.join()
         finally:
             self.transformer_l._class_rand = self.transformer_h._class_rand = None

@@ -44,3 +44,13 @@ def test_product_refuses_cpu_tensors():
     from timevqvae.hip._native import NativeError, ptr
     with pytest.raises(NativeError):
         ptr(torch.zeros(3))
+
+
+def test_library_stamp_matches_sources():
+    """The library carries the hash of the sources it was built from (csrc/Makefile
+    tvq_source_hash); __graft_entry__.build() rebuilds when it differs, so the library the
+    GPU tests load is the tree's."""
+    from timevqvae.hip import _native
+    assert _native.built_hash() == _native.source_hash(), (
+        f"libtvq_hip.so was built from other sources ({_native.built_hash()} vs "
+        f"{_native.source_hash()}): run __graft_entry__.build()")

@@ -206,6 +206,26 @@ def _batch():
     return synthetic_batch(1234, "cpu")
 
 
+def ref_expr_flips(z, embed, got, what):
+    """Code indices against the reference's own expression on the SAME z (vq.py:210-222,
+    EuclideanCodebook.forward: dist = -(|x|^2 - 2 x E^T + |E|^2), argmax; fp32 torch on the
+    CPU, as the reference runs it) and against its fp64 argmax: the number of rows whose HIP
+    index differs, printed (the GPU test log's `flips=` lines) and returned.  A flip could
+    only come from a near-tie inside fp32 rounding; the assertion is that none occurs."""
+    D = embed.shape[-1]
+    x = z.detach().reshape(-1, D).float().cpu()
+    e = embed.detach().float().cpu().t()
+    dist = -(x.pow(2).sum(1, keepdim=True) - 2 * x @ e + e.pow(2).sum(0, keepdim=True))
+    ref32 = dist.argmax(-1)
+    xd, ed = x.double(), e.double()
+    ref64 = (-(xd.pow(2).sum(1, keepdim=True) - 2 * xd @ ed + ed.pow(2).sum(0, keepdim=True))).argmax(-1)
+    g = got.detach().reshape(-1).cpu().long()
+    f32, f64 = int((g != ref32).sum()), int((g != ref64).sum())
+    print(f"{what}: rows={g.numel()} flips={f32} (vs the reference's fp32 torch.argmax) "
+          f"flips64={f64} (vs fp64)", flush=True)
+    return f32
+
+
 def _check_indices(ctx, prefix):
     argmax, forced, gap, scale = ctx.ind_check[prefix]
     bad = torch.nonzero(argmax != forced).flatten()
@@ -232,10 +252,14 @@ def test_stage1_step_full_size_vs_oracle(cuda):
     s1 = s1.to(cuda).train()
     opt = s1.configure_optimizers()["optimizer"]
     s1._sched = None
-    cap = {}
+    cap, zin = {}, {}
+    emb0 = {n: sd[f"{n}._codebook.embed"].clone() for n in ("vq_model_l", "vq_model_h")}
+
+    def _hook(mod, inp, o, n):
+        cap[n] = o[1].detach().clone()
+        zin[n] = inp[0].detach().clone()
     hooks = [getattr(s1, n).register_forward_hook(
-        lambda mod, inp, o, n=n: cap.__setitem__(n, o[1].detach().clone()))
-        for n in ("vq_model_l", "vq_model_h")]
+        lambda mod, inp, o, n=n: _hook(mod, inp, o, n)) for n in ("vq_model_l", "vq_model_h")]
     opt.zero_grad()
     packs = PackCache(cuda)
     with _trace() as tr:
@@ -259,8 +283,12 @@ def test_stage1_step_full_size_vs_oracle(cuda):
     spec = O.Stage1Spec(T, C)
     ref = O.stage1_forward(ctx, sdo, spec, x)
     ref["loss"].backward()
-    flips = sum(_check_indices(ctx, p) for p in ("vq_model_l.", "vq_model_h."))
-    assert flips <= 8, flips
+    # index exactness: the HIP codes against the reference's own fp32 expression on the same z
+    flips = {n: ref_expr_flips(zin[n], emb0[n], cap[n], f"stage1 B=256 {n}")
+             for n in ("vq_model_l", "vq_model_h")}
+    assert all(v == 0 for v in flips.values()), flips
+    flips_oracle = sum(_check_indices(ctx, p) for p in ("vq_model_l.", "vq_model_h."))
+    assert flips_oracle <= 8, flips_oracle
     for k, rk in (("loss", "loss"), ("recons_loss.LF.time", "recons_lf"),
                   ("recons_loss.HF.time", "recons_hf"), ("commit_loss.LF", "commit_lf"),
                   ("commit_loss.HF", "commit_hf"), ("perplexity.LF", "perp_lf"),
@@ -326,8 +354,19 @@ def test_stage2_step_full_size_vs_oracle(cuda):
              "ratio_h": npr.uniform(0, 1, B), "rand_h": torch.rand(B, nh, generator=g),
              "cls_l": torch.rand(B, 1, generator=g), "cls_h": torch.rand(B, 1, generator=g)}
     xd, yd = x.to(cuda), y.to(cuda)
+    from timevqvae.models import VectorQuantize
+    zin = {}
+    vqs = [(n, m) for n, m in mg.named_modules() if isinstance(m, VectorQuantize)]
+    hooks = [m.register_forward_hook(lambda mod, inp, o, n=n: zin.__setitem__(n, (inp[0].detach().clone(), o[1].detach().clone())))
+             for n, m in vqs]
     with torch.no_grad():
         s_l, s_h = mg.encode_tokens(xd)
+    for h in hooks:
+        h.remove()
+    # index exactness of the frozen stage1's codes (encode_to_z_q, maskgit.py:94-110)
+    flips = {n: ref_expr_flips(z, m._codebook.embed, ind, f"stage2 encode B=256 {n}")
+             for n, m in vqs for z, ind in [zin[n]]}
+    assert len(flips) == 2 and all(v == 0 for v in flips.values()), flips
     opt.zero_grad()
     packs = PackCache(cuda)
     one = torch.ones((), device=cuda)

@@ -59,13 +59,21 @@ def test_fused_ff_matches_per_op_path(B, n, p, gated, cuda):
 
 
 def test_fused_ff_gate_zero_drops_the_branch(cuda):
-    """gate 0 (a dropped branch under graph capture): y == r and no gradient reaches x."""
+    """gate 0 (a dropped branch under graph capture): y == r, no gradient reaches x, and
+    every weight / bias gradient of the branch is exactly zero (dW2 / db2 come from
+    gate * gy, so a dropped forward adds nothing under gradient accumulation either)."""
     from timevqvae.models.bidirectional_transformer import FeedForward
     torch.manual_seed(1)
     ff = FeedForward(128, 1, 0.3).to(cuda).train()
     x = torch.randn(64, 25, 128, device=cuda)
     r = torch.randn(64, 25, 128, device=cuda)
     gy = torch.randn(64, 25, 128, device=cuda)
-    y, dx, dr, _ = _run(ff, x, r, torch.zeros(1, device=cuda), True, gy)
+    y, dx, dr, grads = _run(ff, x, r, torch.zeros(1, device=cuda), True, gy)
     assert torch.equal(y, r)
     assert float(dx.abs().max()) == 0.0 and torch.equal(dr, gy)
+    for k, g in grads.items():
+        assert float(g.abs().max()) == 0.0, k
+    # and the per-op path agrees
+    _, _, _, ref = _run(ff, x, r, torch.zeros(1, device=cuda), False, gy)
+    for k, g in ref.items():
+        assert float(g.abs().max()) == 0.0, k

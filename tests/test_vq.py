@@ -145,6 +145,9 @@ def test_hip_vq_vs_c_oracle_full_size(M, K, D, layout, cuda):
     torch.cuda.synchronize()
     got = ind.cpu().numpy().reshape(-1)
     assert_index_parity(got, want, gap, gap_tol(xh, E), f"M={M} K={K} D={D}")
+    # and against the reference's own fp32 expression (vq.py:210-222) on the same x
+    from test_fullsize_parity import ref_expr_flips
+    assert ref_expr_flips(x, torch.from_numpy(E), ind, f"vq M={M} K={K} D={D}") == 0
     cs2, ea2, E2, counts, p = vq_ref.ema(xh, got, cs, ea)
     np.testing.assert_allclose(vq._codebook.cluster_size.cpu().numpy(), cs2, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(vq._codebook.embed_avg.cpu().numpy(), ea2, rtol=1e-4, atol=1e-4)

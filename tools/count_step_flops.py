@@ -12,7 +12,16 @@ with layer dropout off (every branch run: the upper bound of the per-step work).
 The sampler batch (BASELINE configs[4]: iterative decoding of 10 LF + 1 HF steps with the
 priors' forwards, then both decoders) is counted the same way, per 1024 trajectories.
 
-usage: python tools/count_step_flops.py [B] > profiles/r03_step_flops.json"""
+`sampler_executed_gflop_per_1024` is what the HIP sampler executes: the same count less the
+Linears its eval heads compose away (hip path, models/bidirectional_transformer.py
+_head_hf_eval and the LF prior's folded tables), from the config.yaml shapes:
+  LF project_in (128 -> 128) on 25 tokens x 10 decoding steps, folded into the tables;
+  HF Upscale's last conv 256 -> 128 (k 3) becomes 256 -> 32 (project_in's tl half folded in);
+  HF project_in (256 -> 32) on 97 tokens: its th half gathered from a projected table;
+  HF project_out (32 -> 256) then pred_head's Linear (256 -> 128): one 32 -> 128 Linear.
+(the folded tables themselves, once per batch, are < 0.05 GFLOP and not subtracted)
+
+usage: python tools/count_step_flops.py [B] > profiles/r05_step_flops.json"""
 import json
 import os
 import sys
@@ -42,8 +51,14 @@ def main():
     f1 -= 2 * hid * tokens * K  # one-hot EMA matmul of the restatement (stage1 only)
     # sampler (BASELINE configs[4]): one batch = 10 LF + 1 HF prior forwards + both decoders
     fs, bys = count(cpu_baseline.sampler_fn(num=B))
+    n_l, n_h, d_l, D_h, d_h, H_up, steps_l = 24, 96, 128, 128, 32, 256, 10
+    saved = (2 * d_l * d_l * (n_l + 1) * steps_l  # LF project_in
+             + 2 * n_h * H_up * 3 * (D_h - d_h)  # Upscale last conv 256 -> 128 vs -> 32
+             + 2 * (n_h + 1) * 2 * D_h * d_h  # HF project_in
+             + 2 * n_h * (d_h * 2 * D_h + 2 * D_h * D_h - d_h * D_h))  # project_out + pred_head
     out = {"batch_counted": B,
            "sampler_gflop_per_1024": fs / B * 1024 / 1e9, "sampler_by_op": bys,
+           "sampler_executed_gflop_per_1024": fs / B * 1024 / 1e9 - saved * 1024 / 1e9,
            "stage1_gflop_per_traj": f1 / B / 1e9, "stage2_gflop_per_traj": f2 / B / 1e9,
            "step_gflop_at_B256": (f1 + f2) / B * 256 / 1e9,
            "stage1_by_op": by1, "stage2_by_op": by2}
