@@ -304,13 +304,19 @@ int tvq_snake_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t
 int tvq_dropout_bwd(const float* dy, int64_t n, float p, const int64_t* seed_ptr,
                     uint64_t offset, float* dx, tvq_stream_t stream);
 
-/* ---- fused small-channel ResBlock (vq_vae.py:13-62), C_in == C_out = C in {8,16,32}, H = 3,
- * W in {16,32,64}, C*W <= 1024 (csrc/tvq_resblock.hip):
+/* ---- fused ResBlock (vq_vae.py:13-62), C_in == C_out = C in {8,16,32}, H = 3,
+ * W in {16,32,64}, C*W <= 1024 (csrc/tvq_resblock.hip), and C = 64, W = 8 (the LF band's
+ * 64-channel maps, csrc/tvq_resblock_w8.hip: weights from L2, the weight gradients by the
+ * image-batched tvq_conv2d_wgrad inside tvq_resblock_bwd):
  *   y = x + Dropout_p(conv2(Snake_a2(BN(conv1(Snake_a1(x)) + b1))) + b2)
  * replaces tvq_snake_fwd + tvq_conv2d_fwd + tvq_bn_train_fwd + tvq_conv2d_fwd(residual,
  * dropout) and their backward.  Weights (C,C,3,3), a1/a2/biases/BN params (C,). */
 /* bytes of workspace for B images, or -1 when the shape is not supported */
 int64_t tvq_resblock_workspace(int64_t B, int64_t C, int64_t H, int64_t W);
+/* floats of the `h` buffer the training forward fills and the backward reads: B*C*3*W (the
+ * conv1 output) for C in {8,16,32}; 3*B*C*3*W for C = 64, W = 8 (conv1 output | Snake_a1(x) |
+ * Snake_a2(BN(h)), the weight gradients' inputs); -1 when the shape is not supported */
+int64_t tvq_resblock_saved_floats(int64_t B, int64_t C, int64_t H, int64_t W);
 /* training forward: h (B,C,3,W) = conv1 output (kept for backward), y (B,C,3,W), save
  * (4C floats) = batch mean | invstd | BN scale | BN shift; running stats updated in place
  * (momentum, unbiased var, num_batches_tracked += 1) */

@@ -2499,6 +2499,41 @@ static const float* pack_weight(const float* wt, ConvGeom& g, int KK, float* ws,
   return dst;
 }
 
+// A (weight, view) packed [tap][c][n] for a kernel outside the conv engine (the fused LF
+// ResBlock): from the open pack-cache scope (recorded and repacked at each scope's begin like
+// the engine's own), else packed into `ws`, else (no scope, no ws) the unpacked weight.
+// Returns the pointer and the view's strides (n, c, tap) in *sn / *sc / *st.
+const float* conv_pack_view(const float* w, int N, int C, int KK, int64_t wsn, int64_t wsc,
+                            float* ws, hipStream_t st, int64_t* sn, int64_t* sc, int64_t* stp) {
+  ConvGeom g = {};
+  g.N = N;
+  g.C = C;
+  g.wsn = wsn;
+  g.wsc = wsc;
+  g.wst = 1;
+  float* dst = ws;
+  if (PackCacheState* pc = g_pc_cur) {
+    for (const PackEntry& p : pc->entries)
+      if (p.src == w && p.N == N && p.C == C && p.KK == KK && p.wsn == wsn && p.wsc == wsc) {
+        *sn = 1; *sc = N; *stp = (int64_t)N * C;
+        return pc->arena + p.off;
+      }
+    const int64_t slot = ((int64_t)N * C * KK + 63) / 64 * 64;
+    if (pc->used + slot <= pc->cap) {
+      pc->entries.push_back({w, N, C, KK, wsn, wsc, pc->used});
+      dst = pc->arena + pc->used;
+      pc->used += slot;
+    }
+  }
+  if (!dst) {
+    *sn = wsn; *sc = wsc; *stp = 1;
+    return w;
+  }
+  pack_launch(w, N, C, KK, wsn, wsc, dst, st);
+  *sn = 1; *sc = N; *stp = (int64_t)N * C;
+  return dst;
+}
+
 static void tap_tile(int N, int* TN, int* TM) {
   if (N <= 16) { *TN = 16; *TM = 256; }
   else if (N <= 32) { *TN = 32; *TM = 128; }

@@ -15,4 +15,9 @@ void conv_wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, float*
 // it, else reduce_rows now (scratch: reduce_rows_scratch(P, N) floats)
 void param_rows_finish(const float* in, int64_t P, int64_t N, float* out, int accumulate,
                        float* scratch, hipStream_t st);
+// A weight's (n, c, tap) view (element w[n*wsn + c*wsc + tap]) packed [tap][c][n] from the
+// open pack-cache scope, else into ws (N*C*KK floats), else unpacked when ws is null; the
+// returned pointer's strides (n, c, tap) go to *sn, *sc, *st.
+const float* conv_pack_view(const float* w, int N, int C, int KK, int64_t wsn, int64_t wsc,
+                            float* ws, hipStream_t st, int64_t* sn, int64_t* sc, int64_t* stp);
 }  // namespace tvq

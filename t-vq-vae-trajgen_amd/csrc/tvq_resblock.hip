@@ -961,6 +961,25 @@ static RBWs rb_ws(int64_t B, int64_t C, int64_t W) {
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// the LF band's 64-channel ResBlock on (B, 64, 3, 8) (tvq_resblock_w8.hip)
+bool w8_supported(int64_t B, int64_t C, int64_t H, int64_t W);
+int64_t w8_workspace(int64_t B);
+int64_t w8_saved_floats(int64_t B);
+int w8_train_fwd(const float* x, int64_t B, const float* a1, const float* w1, const float* b1,
+                 const float* bn_w, const float* bn_b, float* running_mean, float* running_var,
+                 int64_t* nbt, float momentum, float eps, const float* a2, const float* w2,
+                 const float* b2, float drop_p, const int64_t* seed_ptr, uint64_t offset,
+                 float* saved, float* y, float* save, void* workspace, hipStream_t st);
+int w8_eval_fwd(const float* x, int64_t B, const float* a1, const float* w1, const float* b1,
+                const float* bn_w, const float* bn_b, const float* running_mean,
+                const float* running_var, float eps, const float* a2, const float* w2,
+                const float* b2, float* y, hipStream_t st);
+int w8_bwd(const float* dy, const float* x, const float* saved, int64_t B, const float* a1,
+           const float* w1, const float* bn_w, const float* save, const float* a2,
+           const float* w2, float drop_p, const int64_t* seed_ptr, uint64_t offset, float* dx,
+           float* da1, float* dw1, float* db1, float* dbn_w, float* dbn_b, float* da2, float* dw2,
+           float* db2, int64_t accumulate, void* workspace, hipStream_t st);
+
 }  // namespace tvq
 
 using namespace tvq;
@@ -975,8 +994,15 @@ extern "C" int tvq_rb_timing(unsigned long long* buf) {
 #endif
 
 extern "C" int64_t tvq_resblock_workspace(int64_t B, int64_t C, int64_t H, int64_t W) {
+  if (w8_supported(B, C, H, W)) return w8_workspace(B);
   if (!rb_supported(B, C, H, W)) return -1;
   return (int64_t)rb_ws(B, C, W).total;
+}
+
+extern "C" int64_t tvq_resblock_saved_floats(int64_t B, int64_t C, int64_t H, int64_t W) {
+  if (w8_supported(B, C, H, W)) return w8_saved_floats(B);
+  if (!rb_supported(B, C, H, W)) return -1;
+  return B * C * H * W;
 }
 
 extern "C" int tvq_resblock_train_fwd(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
@@ -987,13 +1013,18 @@ extern "C" int tvq_resblock_train_fwd(const float* x, int64_t B, int64_t C, int6
                                       const float* b2, float drop_p, const int64_t* seed_ptr,
                                       uint64_t offset, float* h, float* y, float* save,
                                       void* workspace, tvq_stream_t stream) {
-  TVQ_CHECK_ARG(rb_supported(B, C, H, W), "tvq_resblock_train_fwd: unsupported shape");
+  const bool w8 = w8_supported(B, C, H, W);
+  TVQ_CHECK_ARG(w8 || rb_supported(B, C, H, W), "tvq_resblock_train_fwd: unsupported shape");
   TVQ_CHECK_ARG(x && a1 && w1 && a2 && w2 && h && y && save && workspace && running_mean &&
                     running_var && aligned16(x) && aligned16(h),
                 "tvq_resblock_train_fwd: bad arguments");
   TVQ_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || seed_ptr),
                 "tvq_resblock_train_fwd: bad dropout");
   hipStream_t st = (hipStream_t)stream;
+  if (w8)
+    return w8_train_fwd(x, B, a1, w1, b1, bn_w, bn_b, running_mean, running_var,
+                        num_batches_tracked, momentum, eps, a2, w2, b2, drop_p, seed_ptr, offset, h,
+                        y, save, workspace, st);
   RBArgs a = {};
   a.x = x; a.h = h; a.a1 = a1; a.w1 = w1; a.b1 = b1; a.a2 = a2; a.w2 = w2; a.b2 = b2;
   a.save = save; a.h_out = h; a.y = y;
@@ -1016,9 +1047,13 @@ extern "C" int tvq_resblock_eval_fwd(const float* x, int64_t B, int64_t C, int64
                                      const float* running_mean, const float* running_var,
                                      float eps, const float* a2, const float* w2, const float* b2,
                                      float* y, tvq_stream_t stream) {
-  TVQ_CHECK_ARG(rb_supported(B, C, H, W), "tvq_resblock_eval_fwd: unsupported shape");
+  const bool w8 = w8_supported(B, C, H, W);
+  TVQ_CHECK_ARG(w8 || rb_supported(B, C, H, W), "tvq_resblock_eval_fwd: unsupported shape");
   TVQ_CHECK_ARG(x && a1 && w1 && a2 && w2 && y && running_mean && running_var && aligned16(x),
                 "tvq_resblock_eval_fwd: bad arguments");
+  if (w8)
+    return w8_eval_fwd(x, B, a1, w1, b1, bn_w, bn_b, running_mean, running_var, eps, a2, w2, b2,
+                       y, (hipStream_t)stream);
   RBArgs a = {};
   a.x = x; a.a1 = a1; a.w1 = w1; a.b1 = b1; a.bn_w = bn_w; a.bn_b = bn_b;
   a.rmean = running_mean; a.rvar = running_var; a.eps = eps;
@@ -1034,13 +1069,17 @@ extern "C" int tvq_resblock_bwd(const float* dy, const float* x, const float* h,
                                 uint64_t offset, float* dx, float* da1, float* dw1, float* db1,
                                 float* dbn_w, float* dbn_b, float* da2, float* dw2, float* db2,
                                 int64_t accumulate, void* workspace, tvq_stream_t stream) {
-  TVQ_CHECK_ARG(rb_supported(B, C, H, W), "tvq_resblock_bwd: unsupported shape");
+  const bool w8 = w8_supported(B, C, H, W);
+  TVQ_CHECK_ARG(w8 || rb_supported(B, C, H, W), "tvq_resblock_bwd: unsupported shape");
   TVQ_CHECK_ARG(dy && x && h && a1 && w1 && save && a2 && w2 && dx && da1 && dw1 && db1 && da2 &&
                     dw2 && db2 && workspace && aligned16(dy) && aligned16(x) && aligned16(h),
                 "tvq_resblock_bwd: bad arguments");
   TVQ_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || seed_ptr),
                 "tvq_resblock_bwd: bad dropout");
   hipStream_t st = (hipStream_t)stream;
+  if (w8)
+    return w8_bwd(dy, x, h, B, a1, w1, bn_w, save, a2, w2, drop_p, seed_ptr, offset, dx, da1, dw1,
+                  db1, dbn_w, dbn_b, da2, dw2, db2, accumulate, workspace, st);
   const RBWs w = rb_ws(B, C, W);
   char* ws = (char*)workspace;
   float* slab2 = (float*)(ws + w.slab2);

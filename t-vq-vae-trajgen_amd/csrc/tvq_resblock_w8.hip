@@ -1,0 +1,582 @@
+// Fused ResBlock(64, 64) of the LF band on its (B, 64, 3, 8) maps (reference
+// vq_vae.py:13-62; the last two encoder and first two decoder ResBlocks of the LF VQ-VAE):
+//
+//   y = x + Dropout_p(conv2(Snake_a2(BN(conv1(Snake_a1(x)) + b1))) + b2)
+//
+// The small-channel fused ResBlocks (tvq_resblock.hip) keep the whole 3x3 weight panel in
+// LDS; a 64-channel panel is 147 KB, so here the weights stream from L2 as the MFMA A
+// operand (packed [tap][c][n] by the step's pack cache: one coalesced 128-B row per half-wave
+// and step) while the image -- 64 channels x 3 x 8, a 20 KB halo-plane stack -- is staged in
+// LDS once per conv.  One 8-wave block per image (256 images = one block per CU); wave w
+// owns output tile w & 1 (32 channels) and input-channel chunk w >> 1 (16 channels): 9 taps
+// x 8 v_mfma_f32_32x32x2_f32 steps, its 72 weight values loaded before the first MFMA; the
+// 4 chunk partials of a tile are summed in LDS in chunk order.  The 24 positions of an image
+// fill 24 of the tile's 32 columns.
+//
+//   w8_fwd1  s1 = Snake_a1(x) staged (and stored: the conv1 weight gradient's input) ->
+//            h = conv1(s1) + b1 -> store h; per-image fp64 BN partial sums
+//   w8_fwd2  every block reduces the 256 images' partials in one fixed order to the batch
+//            mean / invstd (block 0 publishes them and the running statistics);
+//            s2 = Snake_a2(BN(h)) staged (and stored) -> y = x + Dropout(conv2(s2) + b2)
+//   w8_bwd2  g2 = Dropout'(dy) staged (and stored) -> ds2 = conv2^T(g2) -> du = ds2 *
+//            Snake'(u) (u = BN(h) recomputed) -> store du; per-image (sum du, sum du xhat)
+//            and the Snake a2 term (a slab row)
+//   w8_bwd1  every block reduces those partials to the BN backward coefficients (block 0
+//            writes the BN weight / bias gradients); dh = BN'(du) staged (and stored) ->
+//            ds1 = conv1^T(dh) -> dx = ds1 * Snake'(x) + dy; the Snake a1 term (a slab row)
+//   weight gradients: tvq_conv2d_wgrad on (s2, g2) and (s1, dh) -- the image-batched
+//            conv_wgrad_w8 kernel (a 64 x 577 slab row per image would be 148 KB)
+//   w8_eval  both convs in one launch with BN from the running statistics (the frozen
+//            encoder of stage2, the LF decoder while sampling)
+//
+// Replaces, per ResBlock: tvq_snake_fwd, two conv launches, the whole-channel BN kernel, and
+// in the backward the dropout, snake and BN kernels and two data-gradient convs.  Arithmetic
+// is the per-op kernels' (Snake, BN affine / backward formulas, the dropout hash at the flat
+// NCHW index) up to the summation order, which is fixed.
+#include "tvq_bn.h"
+#include "tvq_common.h"
+#include "tvq_conv_internal.h"
+#include "tvq_reduce.h"
+
+namespace tvq {
+namespace w8 {
+
+constexpr int C = 64, W = 8, P = 3 * W, NW = 8, T = 64 * NW;
+constexpr int WP = W + 2;      // halo row stride
+constexpr int PS = 80;         // halo plane stride (5 x 10 cells, padded; == 16 mod 32)
+constexpr int PLANE = C * PS;  // floats
+constexpr int CPC = 16;        // input channels per wave chunk
+constexpr int RED = NW * 16 * 64;
+constexpr int K = 9 * C;
+
+struct WView {  // element (row n, reduction channel c, tap t) at w[n*sn + c*sc + t*st]
+  const float* w;
+  int64_t sn, sc, st;
+};
+
+struct Args {
+  const float *x, *h, *dy, *du_in;
+  const float *a1, *b1, *a2, *b2;
+  const float *bn_w, *bn_b, *rmean, *rvar;  // eval / BN backward
+  const float* save;                         // mean | invstd | scale | shift
+  WView w1, w2;                              // forward views (eval / fwd) or data-gradient views
+  float *h_out, *s_out, *y, *du, *dx, *g_out, *slabda;
+  double* part;
+  float eps, drop_p, drop_scale, invN;
+  const int64_t* seed_ptr;
+  uint64_t offset;
+  int B, accumulate;
+  BNFinal fin;
+  BNBwdFinal bfin;
+};
+
+__device__ __forceinline__ int wid_() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// halo cell of position p (the 3x3 window's centre)
+__device__ __forceinline__ int cell(int c, int p) { return c * PS + WP + 1 + (p / W) * WP + p % W; }
+
+// zero the border cells of the 64 halo planes
+__device__ __forceinline__ void border(float* __restrict__ S) {
+  for (int i = threadIdx.x; i < C * 26; i += T) {
+    const int c = i / 26, r = i - 26 * c;
+    int o;
+    if (r < WP) o = r;
+    else if (r < 2 * WP) o = 4 * WP + (r - WP);
+    else {
+      const int k = r - 2 * WP;
+      o = (1 + (k >> 1)) * WP + ((k & 1) ? W + 1 : 0);
+    }
+    S[c * PS + o] = 0.f;
+  }
+}
+
+// Elementwise layout: wave w, iteration j -> channel 8w + 2j + (lane >> 5), position lane & 31
+// (valid below 24); a channel's 24 positions sit in one 32-lane half.
+__device__ __forceinline__ int el_c(int j) { return 8 * wid_() + 2 * j + ((threadIdx.x & 63) >> 5); }
+__device__ __forceinline__ int el_p() { return threadIdx.x & 31; }
+
+// sum over the lane's 32-lane half (fixed xor tree)
+__device__ __forceinline__ double half_sum_d(double v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// The block's conv of the staged planes S: D[row][pos] for rows 32 (w & 1) .. and input
+// chunk w >> 1, partial tile to red[w][16][64].  FLIP: the data gradient (taps mirrored).
+template <bool FLIP>
+__device__ __forceinline__ void conv(const WView wv, const float* __restrict__ S,
+                                     float* __restrict__ red) {
+  const int lane = threadIdx.x & 63, wid = wid_();
+  const int r32 = lane & 31, hl = lane >> 5;
+  const int nt = wid & 1, c0 = (wid >> 1) * CPC;
+  const float* wp = wv.w + (int64_t)(32 * nt + r32) * wv.sn + (int64_t)(c0 + hl) * wv.sc;
+  float a[9][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[t][u] = wp[(int64_t)(2 * u) * wv.sc + (int64_t)t * wv.st];
+  const int m = r32 < P ? r32 : 0;
+  const float* sp = S + (c0 + hl) * PS + (m / W) * WP + (m % W);
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int tt = FLIP ? 8 - t : t, off = (tt / 3) * WP + tt % 3;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t][u], sp[2 * u * PS + off], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[(wid * 16 + r) * 64 + lane] = acc[r];
+}
+
+// conv result (row n, position p): the 4 chunk partials of tile n / 32 summed in order
+__device__ __forceinline__ float conv_at(const float* __restrict__ red, int n, int p) {
+  const int nt = n >> 5, i = n & 31, h = (i >> 2) & 1, r = (i & 3) + 4 * (i >> 3);
+  const int l = p + 32 * h;
+  float s = red[(nt * 16 + r) * 64 + l];
+#pragma unroll
+  for (int ch = 1; ch < 4; ++ch) s += red[((nt + 2 * ch) * 16 + r) * 64 + l];
+  return s;
+}
+
+// Batch totals of the NS per-image fp64 partials part[(c*NS + i)*B + b] of this wave's 8
+// channels 8w + q (q < 8), in every block in one fixed order (lane l: images l, l + 64, ..,
+// then the xor tree): t[q][i] in every lane.
+template <int NS>
+__device__ __forceinline__ void batch_sums(const double* __restrict__ part, int B,
+                                           double (&t)[8][NS]) {
+  const int l = threadIdx.x & 63, w = wid_();
+  double v[8][NS][4];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int b = l + 64 * k;
+        v[q][i][k] = b < B ? part[((int64_t)(8 * w + q) * NS + i) * B + b] : 0.0;
+      }
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      double s = v[q][i][0] + v[q][i][1] + v[q][i][2] + v[q][i][3];
+      for (int b = l + 256; b < B; b += 64) s += part[((int64_t)(8 * w + q) * NS + i) * B + b];
+      t[q][i] = wave_sum_d(s);
+    }
+}
+
+// ---------------------------------------------------------------- kernels
+__global__ __launch_bounds__(T) void w8_fwd1_kernel(Args a) {
+  extern __shared__ float sm[];
+  float* S = sm;
+  float* red = sm + PLANE;
+  const int b = blockIdx.x, p = el_p(), hl = (threadIdx.x & 63) >> 5;
+  const int64_t img0 = (int64_t)b * C * P;
+  float xv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) xv[j] = p < P ? a.x[img0 + el_c(j) * P + p] : 0.f;
+  border(S);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = el_c(j);
+    if (p >= P) continue;
+    const float av = a.a1[c];
+    const float s = snake_f(xv[j], av, 1.0f / av);
+    S[cell(c, p)] = s;
+    a.s_out[img0 + c * P + p] = s;
+  }
+  __syncthreads();
+  conv<false>(a.w1, S, red);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = el_c(j);
+    double s0 = 0.0, s1 = 0.0;
+    if (p < P) {
+      const float v = conv_at(red, c, p) + a.b1[c];
+      a.h_out[img0 + c * P + p] = v;
+      s0 = (double)v;
+      s1 = (double)v * (double)v;
+    }
+    s0 = half_sum_d(s0);
+    s1 = half_sum_d(s1);
+    if ((threadIdx.x & 31) == 0) {
+      a.part[((int64_t)c * 2 + 0) * a.B + b] = s0;
+      a.part[((int64_t)c * 2 + 1) * a.B + b] = s1;
+    }
+  }
+  (void)hl;
+}
+
+__global__ __launch_bounds__(T) void w8_fwd2_kernel(Args a) {
+  extern __shared__ float sm[];
+  float* S = sm;
+  float* red = sm + PLANE;
+  const int b = blockIdx.x, p = el_p(), l = threadIdx.x & 63, hl = l >> 5, w = wid_();
+  const int64_t img0 = (int64_t)b * C * P;
+  float hv[4], xv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t gi = img0 + el_c(j) * P + (p < P ? p : 0);
+    hv[j] = a.h[gi];
+    xv[j] = a.x[gi];
+  }
+  double t[8][2];
+  batch_sums<2>(a.part, a.B, t);
+  border(S);
+  // the batch statistics (bn_final_from_sums); block 0 publishes them
+  const bool pub = b == 0 && l == 0;
+  if (pub && w == 0 && a.fin.nbt) a.fin.nbt[0] += 1;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bn_final_from_sums(t[q][0], t[q][1], 8 * w + q, a.fin, pub, sc[q], sh[q]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = el_c(j);
+    if (p >= P) continue;
+    const float scv = hl ? sc[2 * j + 1] : sc[2 * j], shv = hl ? sh[2 * j + 1] : sh[2 * j];
+    const float av = a.a2[c];
+    const float s = snake_f(fmaf(hv[j], scv, shv), av, 1.0f / av);
+    S[cell(c, p)] = s;
+    a.s_out[img0 + c * P + p] = s;
+  }
+  __syncthreads();
+  conv<false>(a.w2, S, red);
+  __syncthreads();
+  const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = el_c(j);
+    if (p >= P) continue;
+    const int64_t gi = img0 + c * P + p;
+    float v = conv_at(red, c, p) + a.b2[c];
+    if (a.drop_p > 0.f) v = uniform01(seed, (uint64_t)gi) >= a.drop_p ? v * a.drop_scale : 0.f;
+    a.y[gi] = xv[j] + v;
+  }
+}
+
+__global__ __launch_bounds__(T) void w8_eval_kernel(Args a) {
+  extern __shared__ float sm[];
+  float* S = sm;
+  float* red = sm + PLANE;
+  const int b = blockIdx.x, p = el_p();
+  const int64_t img0 = (int64_t)b * C * P;
+  float xv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) xv[j] = a.x[img0 + el_c(j) * P + (p < P ? p : 0)];
+  border(S);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = el_c(j);
+    if (p >= P) continue;
+    const float av = a.a1[c];
+    S[cell(c, p)] = snake_f(xv[j], av, 1.0f / av);
+  }
+  __syncthreads();
+  conv<false>(a.w1, S, red);
+  __syncthreads();
+  float s2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // BN from the running statistics (bn_eval's affine form)
+    const int c = el_c(j);
+    const float inv = 1.0f / sqrtf(a.rvar[c] + a.eps);
+    const float scv = (a.bn_w ? a.bn_w[c] : 1.f) * inv;
+    const float shv = (a.bn_b ? a.bn_b[c] : 0.f) - a.rmean[c] * scv;
+    const float av = a.a2[c];
+    s2[j] = snake_f(fmaf(conv_at(red, c, p < P ? p : 0) + a.b1[c], scv, shv), av, 1.0f / av);
+  }
+  __syncthreads();  // conv1's partials read; S free
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (p < P) S[cell(el_c(j), p)] = s2[j];
+  __syncthreads();
+  conv<false>(a.w2, S, red);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = el_c(j);
+    if (p < P) a.y[img0 + c * P + p] = xv[j] + (conv_at(red, c, p) + a.b2[c]);
+  }
+}
+
+__global__ __launch_bounds__(T) void w8_bwd2_kernel(Args a) {
+  extern __shared__ float sm[];
+  float* G = sm;
+  float* red = sm + PLANE;
+  const int b = blockIdx.x, p = el_p();
+  const int64_t img0 = (int64_t)b * C * P;
+  float gv[4], hv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t gi = img0 + el_c(j) * P + (p < P ? p : 0);
+    gv[j] = a.dy[gi];
+    hv[j] = a.h[gi];
+  }
+  border(G);
+  const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = el_c(j);
+    if (p >= P) continue;
+    const int64_t gi = img0 + c * P + p;
+    float d = gv[j];
+    if (a.drop_p > 0.f) d = uniform01(seed, (uint64_t)gi) >= a.drop_p ? d * a.drop_scale : 0.f;
+    G[cell(c, p)] = d;
+    a.g_out[gi] = d;
+  }
+  __syncthreads();
+  conv<true>(a.w2, G, red);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = el_c(j);
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    if (p < P) {
+      const float av = a.a2[c], inv_a = 1.0f / av;
+      const float sc = a.save[2 * C + c], sh = a.save[3 * C + c];
+      const float mu = a.save[c], is = a.save[C + c];
+      const float gs = conv_at(red, c, p);  // d loss / d s2
+      const float uu = fmaf(hv[j], sc, sh);
+      float sn, cs;
+      sincosf(av * uu, &sn, &cs);
+      const float tt = 2.0f * sn * cs;
+      const float d = gs + gs * inv_a * tt * av;  // d loss / d u (bn_bwd_partial_kernel)
+      const float xhat = (hv[j] - mu) * is;
+      a.du[img0 + c * P + p] = d;
+      s0 = d;
+      s1 = (double)d * xhat;
+      s2 = (double)(gs * inv_a * tt * uu) - (double)(gs * (sn * sn) * inv_a * inv_a);
+    }
+    s0 = half_sum_d(s0);
+    s1 = half_sum_d(s1);
+    s2 = half_sum_d(s2);
+    if ((threadIdx.x & 31) == 0) {
+      a.part[((int64_t)c * 2 + 0) * a.B + b] = s0;
+      a.part[((int64_t)c * 2 + 1) * a.B + b] = s1;
+      a.slabda[(int64_t)b * C + c] = (float)s2;
+    }
+  }
+}
+
+__global__ __launch_bounds__(T) void w8_bwd1_kernel(Args a) {
+  extern __shared__ float sm[];
+  float* G = sm;
+  float* red = sm + PLANE;
+  const int b = blockIdx.x, p = el_p(), l = threadIdx.x & 63, hl = l >> 5, w = wid_();
+  const int64_t img0 = (int64_t)b * C * P;
+  float dv[4], hv[4], xv[4], yv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t gi = img0 + el_c(j) * P + (p < P ? p : 0);
+    dv[j] = a.du_in[gi];
+    hv[j] = a.h[gi];
+    xv[j] = a.x[gi];  // the epilogue's operands, requested with the prologue's
+    yv[j] = a.dy[gi];
+  }
+  double t[8][2];
+  batch_sums<2>(a.part, a.B, t);
+  border(G);
+  float md[8], mx[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    md[q] = (float)t[q][0] * a.invN;
+    mx[q] = (float)t[q][1] * a.invN;
+    if (b == 0 && l == 0) bn_bwd_params_from_sums(t[q][0], t[q][1], 0.0, 8 * w + q, a.bfin);
+  }
+  // dh = w * invstd * (du - mean(du) - xhat * mean(du * xhat))  (bn_bwd_apply_kernel)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = el_c(j);
+    if (p >= P) continue;
+    const float mdv = hl ? md[2 * j + 1] : md[2 * j], mxv = hl ? mx[2 * j + 1] : mx[2 * j];
+    const float mu = a.save[c], is = a.save[C + c], bw = a.bn_w ? a.bn_w[c] : 1.f;
+    const float xhat = (hv[j] - mu) * is;
+    const float g = bw * is * (dv[j] - mdv - xhat * mxv);
+    G[cell(c, p)] = g;
+    a.g_out[img0 + c * P + p] = g;
+  }
+  __syncthreads();
+  conv<true>(a.w1, G, red);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = el_c(j);
+    double s0 = 0.0;
+    if (p < P) {
+      const int64_t gi = img0 + c * P + p;
+      const float av = a.a1[c], inv_a = 1.0f / av;
+      const float gs = conv_at(red, c, p);  // d loss / d s1
+      float sn, cs;
+      sincosf(av * xv[j], &sn, &cs);
+      const float tt = 2.0f * sn * cs;
+      // snake_bwd_kernel, plus the identity skip's gradient
+      a.dx[gi] = (gs + gs * inv_a * tt * av) + yv[j];
+      s0 = (double)(gs * inv_a * tt * xv[j]) - (double)(gs * (sn * sn) * inv_a * inv_a);
+    }
+    s0 = half_sum_d(s0);
+    if ((threadIdx.x & 31) == 0) a.slabda[(int64_t)b * C + c] = (float)s0;
+  }
+}
+
+constexpr size_t LDS = 4 * (size_t)(PLANE + RED);
+
+static void set_lds() {
+  static bool done = false;
+  if (done) return;
+  const void* ks[] = {(const void*)&w8_fwd1_kernel, (const void*)&w8_fwd2_kernel,
+                      (const void*)&w8_eval_kernel, (const void*)&w8_bwd2_kernel,
+                      (const void*)&w8_bwd1_kernel};
+  for (const void* k : ks)
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
+  done = true;
+}
+
+static size_t al(size_t n) { return (n + 255) & ~(size_t)255; }
+
+struct Ws {  // workspace layout (bytes)
+  size_t part, slabda1, slabda2, g2, dh, du, wg1, wg2, pk, total;
+};
+static Ws ws_layout(int64_t B) {
+  Ws w;
+  const size_t img = (size_t)B * C * P * 4;
+  const size_t slabd = (size_t)(B * C + reduce_rows_scratch(B, C)) * 4;
+  const size_t wg = (size_t)tvq_conv_workspace(4, B, C, 3, W, C, 3, 3, 1, 0) * 4;
+  w.part = 0;
+  w.slabda1 = w.part + al((size_t)B * C * 2 * 8);
+  w.slabda2 = w.slabda1 + al(slabd);
+  w.g2 = w.slabda2 + al(slabd);
+  w.dh = w.g2 + al(img);
+  w.du = w.dh + al(img);
+  w.wg1 = w.du + al(img);
+  w.wg2 = w.wg1 + al(wg);
+  w.pk = w.wg2 + al(wg);
+  w.total = w.pk + al((size_t)4 * K * C * 4);  // w1, w2 forward and data-gradient packs
+  return w;
+}
+
+static WView view(const float* w, bool transposed, float* ws, hipStream_t st) {
+  WView v;
+  // forward: rows = output channels n (stride K), reduction = input channels c (stride 9);
+  // data gradient: rows = input channels, reduction = output channels
+  v.w = conv_pack_view(w, C, C, 9, transposed ? 9 : K, transposed ? K : 9, ws, st, &v.sn,
+                       &v.sc, &v.st);
+  return v;
+}
+
+}  // namespace w8
+
+bool w8_supported(int64_t B, int64_t C, int64_t H, int64_t W) {
+  return C == w8::C && H == 3 && W == w8::W && B >= 1 && B * C * 3 * W < (1ll << 31);
+}
+int64_t w8_workspace(int64_t B) { return (int64_t)w8::ws_layout(B).total; }
+int64_t w8_saved_floats(int64_t B) { return 3 * B * w8::C * w8::P; }  // h | s1 | s2
+
+int w8_train_fwd(const float* x, int64_t B, const float* a1, const float* w1, const float* b1,
+                 const float* bn_w, const float* bn_b, float* running_mean, float* running_var,
+                 int64_t* nbt, float momentum, float eps, const float* a2, const float* w2,
+                 const float* b2, float drop_p, const int64_t* seed_ptr, uint64_t offset,
+                 float* saved, float* y, float* save, void* workspace, hipStream_t st) {
+  using namespace w8;
+  set_lds();
+  const Ws L = ws_layout(B);
+  char* ws = (char*)workspace;
+  float* pk = (float*)(ws + L.pk);
+  const int64_t img = B * C * P;
+  Args a = {};
+  a.x = x; a.a1 = a1; a.b1 = b1; a.a2 = a2; a.b2 = b2;
+  a.w1 = view(w1, false, pk, st);
+  a.w2 = view(w2, false, pk + K * C, st);
+  a.h_out = saved; a.h = saved; a.y = y;
+  a.part = (double*)(ws + L.part);
+  a.B = (int)B;
+  a.drop_p = drop_p;
+  a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  a.seed_ptr = seed_ptr; a.offset = offset;
+  a.fin = {C, (int)B, B * P, eps, momentum, bn_w, bn_b, running_mean, running_var, nbt,
+           save, save + C, save + 2 * C, save + 3 * C};
+  TVQ_PLAN("w8_fwd1 C%d W%d B%lld", C, W, (long long)B);
+  a.s_out = saved + img;  // s1
+  hipLaunchKernelGGL(w8_fwd1_kernel, dim3((unsigned)B), dim3(T), LDS, st, a);
+  TVQ_PLAN("w8_fwd2 C%d W%d B%lld", C, W, (long long)B);
+  a.s_out = saved + 2 * img;  // s2
+  hipLaunchKernelGGL(w8_fwd2_kernel, dim3((unsigned)B), dim3(T), LDS, st, a);
+  return launch_status("tvq_resblock_train_fwd");
+}
+
+int w8_eval_fwd(const float* x, int64_t B, const float* a1, const float* w1, const float* b1,
+                const float* bn_w, const float* bn_b, const float* running_mean,
+                const float* running_var, float eps, const float* a2, const float* w2,
+                const float* b2, float* y, hipStream_t st) {
+  using namespace w8;
+  set_lds();
+  Args a = {};
+  a.x = x; a.a1 = a1; a.b1 = b1; a.a2 = a2; a.b2 = b2;
+  a.bn_w = bn_w; a.bn_b = bn_b; a.rmean = running_mean; a.rvar = running_var; a.eps = eps;
+  // no workspace: the open pack-cache scope's packs, else the weights as they are
+  a.w1 = view(w1, false, nullptr, st);
+  a.w2 = view(w2, false, nullptr, st);
+  a.y = y; a.B = (int)B;
+  TVQ_PLAN("w8_eval C%d W%d B%lld packed=%d", C, W, (long long)B, (int)(a.w1.sn == 1));
+  hipLaunchKernelGGL(w8_eval_kernel, dim3((unsigned)B), dim3(T), LDS, st, a);
+  return launch_status("tvq_resblock_eval_fwd");
+}
+
+int w8_bwd(const float* dy, const float* x, const float* saved, int64_t B, const float* a1,
+           const float* w1, const float* bn_w, const float* save, const float* a2,
+           const float* w2, float drop_p, const int64_t* seed_ptr, uint64_t offset, float* dx,
+           float* da1, float* dw1, float* db1, float* dbn_w, float* dbn_b, float* da2, float* dw2,
+           float* db2, int64_t accumulate, void* workspace, hipStream_t st) {
+  using namespace w8;
+  set_lds();
+  const Ws L = ws_layout(B);
+  char* ws = (char*)workspace;
+  float* pk = (float*)(ws + L.pk);
+  const int64_t img = B * C * P;
+  const float* h = saved;
+  const float* s1 = saved + img;
+  const float* s2 = saved + 2 * img;
+  float* g2 = (float*)(ws + L.g2);
+  float* dh = (float*)(ws + L.dh);
+  float* du = (float*)(ws + L.du);
+  float* slabda1 = (float*)(ws + L.slabda1);
+  float* slabda2 = (float*)(ws + L.slabda2);
+  Args a = {};
+  a.x = x; a.h = h; a.dy = dy; a.du_in = du;
+  a.a1 = a1; a.a2 = a2; a.bn_w = bn_w; a.save = save;
+  a.w1 = view(w1, true, pk + 2 * K * C, st);
+  a.w2 = view(w2, true, pk + 3 * K * C, st);
+  a.du = du; a.dx = dx;
+  a.part = (double*)(ws + L.part);
+  a.B = (int)B; a.accumulate = (int)accumulate;
+  a.drop_p = drop_p;
+  a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  a.seed_ptr = seed_ptr; a.offset = offset;
+  a.invN = 1.0f / (float)(B * P);
+  a.bfin = {C, (int)B, nullptr, dbn_w, dbn_b, nullptr, (int)accumulate};
+  TVQ_PLAN("w8_bwd2 C%d W%d B%lld", C, W, (long long)B);
+  a.g_out = g2; a.slabda = slabda2;
+  hipLaunchKernelGGL(w8_bwd2_kernel, dim3((unsigned)B), dim3(T), LDS, st, a);
+  int rc = launch_status("tvq_resblock_bwd");
+  if (rc) return rc;
+  // conv2's weight gradient from (s2, g2) while the next kernel waits on nothing of it
+  rc = tvq_conv2d_wgrad(s2, B, C, 3, W, g2, C, W, 3, 3, 1, 0, dw2, db2, accumulate,
+                        (float*)(ws + L.wg2), st);
+  if (rc) return rc;
+  TVQ_PLAN("w8_bwd1 C%d W%d B%lld", C, W, (long long)B);
+  a.g_out = dh; a.slabda = slabda1;
+  hipLaunchKernelGGL(w8_bwd1_kernel, dim3((unsigned)B), dim3(T), LDS, st, a);
+  rc = launch_status("tvq_resblock_bwd");
+  if (rc) return rc;
+  rc = tvq_conv2d_wgrad(s1, B, C, 3, W, dh, C, W, 3, 3, 1, 0, dw1, db1, accumulate,
+                        (float*)(ws + L.wg1), st);
+  if (rc) return rc;
+  conv_wgrad_finish(slabda1, (int)B, C, 1, da1, nullptr, (int)accumulate, st);
+  conv_wgrad_finish(slabda2, (int)B, C, 1, da2, nullptr, (int)accumulate, st);
+  return launch_status("tvq_resblock_bwd");
+}
+
+}  // namespace tvq

@@ -114,6 +114,7 @@ sig("tvq_snake_workspace", I64, I64, I64, restype=I64)
 sig("tvq_snake_bwd", P, P, I64, I64, I64, P, P, P, P, I64, P, P)
 sig("tvq_dropout_bwd", P, I64, F32, P, U64, P, P)
 sig("tvq_resblock_workspace", I64, I64, I64, I64, restype=I64)
+sig("tvq_resblock_saved_floats", I64, I64, I64, I64, restype=I64)
 sig("tvq_resblock_train_fwd", P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, F32, F32, P, P, P,
     F32, P, U64, P, P, P, P, P)
 sig("tvq_resblock_eval_fwd", P, I64, I64, I64, I64, P, P, P, P, P, P, P, F32, P, P, P, P, P)

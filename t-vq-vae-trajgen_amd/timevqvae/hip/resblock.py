@@ -1,6 +1,7 @@
-"""Fused small-channel ResBlock (include/tvq.h §fused ResBlock, csrc/tvq_resblock.hip).
+"""Fused ResBlock (include/tvq.h §fused ResBlock, csrc/tvq_resblock.hip, tvq_resblock_w8.hip).
 
-ResBlock(C, C) of vq_vae.py:13-62 with C in {8, 16, 32} on the (B, C, 3, W) STFT image:
+ResBlock(C, C) of vq_vae.py:13-62 with C in {8, 16, 32} on the (B, C, 3, W) STFT image, and
+C = 64 on the LF band's (B, 64, 3, 8) maps:
   y = x + Dropout_p(conv2(Snake_a2(BN(conv1(Snake_a1(x)) + b1))) + b2)
 as 2 launches forward (training), 1 (eval), 2 backward, instead of one kernel per op.
 `supported()` says when it applies; models/vq_vae.ResBlock falls back to the per-op path
@@ -36,7 +37,9 @@ class _ResBlockTrain(torch.autograd.Function):
                 drop_p, site):
         x = x.contiguous()
         B, C, H, W = x.shape
-        h = torch.empty_like(x)
+        # the backward's saved activations: conv1's output (and, C = 64, the two Snake
+        # outputs the weight gradients read)
+        h = torch.empty(value("tvq_resblock_saved_floats", B, C, H, W), device=x.device)
         y = torch.empty_like(x)
         save = torch.empty(4 * C, device=x.device, dtype=torch.float32)
         seed = rng.seed_tensor(x.device) if drop_p > 0 else None

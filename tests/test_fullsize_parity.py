@@ -137,11 +137,12 @@ def _resblock(Cc, seed):
     return m
 
 
-@pytest.mark.parametrize("Cc,W", [(8, 64), (16, 32), (32, 16)])
+@pytest.mark.parametrize("Cc,W", [(8, 64), (16, 32), (32, 16), (64, 8)])
 def test_fused_resblock_full_batch_vs_oracle(Cc, W, cuda):
     """ResBlock(C, C) (vq_vae.py:13-62) at the step's (256, C, 3, W) maps: the fused kernels
-    (rb_fwd1/2, rb_bwd2/1) against tvq_oracle.res_block with CPU autograd: output, every
-    parameter gradient, dx, BN running statistics."""
+    (rb_fwd1/2, rb_bwd2/1; C = 64: w8_fwd1/2, w8_bwd2/1 with the image-batched weight
+    gradients) against tvq_oracle.res_block with CPU autograd: output, every parameter
+    gradient, dx, BN running statistics."""
     m = _resblock(Cc, 10 + Cc)
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     gen = torch.Generator().manual_seed(Cc)
@@ -163,8 +164,11 @@ def test_fused_resblock_full_batch_vs_oracle(Cc, W, cuda):
         yd = md(xd)
         yd.backward(gy.to(cuda))
         torch.cuda.synchronize()
-    for kern in ("rb_fwd1", "rb_fwd2", "rb_bwd2", "rb_bwd1"):
-        assert tr.has(f"{kern} C{Cc} W{W} B{B}"), (kern, tr.lines)
+    pre = "w8" if Cc == 64 else "rb"
+    for kern in ("fwd1", "fwd2", "bwd2", "bwd1"):
+        assert tr.has(f"{pre}_{kern} C{Cc} W{W} B{B}"), (kern, tr.lines)
+    if Cc == 64:
+        assert tr.has("conv_wgrad_w8"), tr.lines
     ok, err, s = max_ok(yd, yc)
     assert ok, ("y", err, s)
     ok, err, s = max_ok(xd.grad, xc.grad)
@@ -271,7 +275,8 @@ def test_stage1_step_full_size_vs_oracle(cuda):
         h.remove()
     # the benched variants ran
     for want in ("conv_t32 bk16", "conv_wgrad_s2", "rb_bwd1 C16 W32 B256", "rb_bwd1 C8 W64 B256",
-                 "rb_bwd1 C32 W16 B256", "vq_assign D128 rg6", "conv_wgrad_t32", "conv_wgrad_w8"):
+                 "rb_bwd1 C32 W16 B256", "w8_bwd1 C64 W8 B256", "w8_fwd2 C64 W8 B256",
+                 "vq_assign D128 rg6", "conv_wgrad_t32", "conv_wgrad_w8"):
         assert tr.has(want), (want, sorted(set(tr.lines)))
     assert any(int(s.split("spr=")[1]) > 1 for s in tr.has("conv_wgrad_s2")), tr.has("conv_wgrad_s2")
     # oracle on the same weights, batch and (near-tie-checked) indices
@@ -377,6 +382,7 @@ def test_stage2_step_full_size_vs_oracle(cuda):
                 loss.backward(one)
         torch.cuda.synchronize()
     assert tr.has("vq_assign D128"), tr.lines
+    assert tr.has("w8_eval C64 W8 B256 packed=1"), tr.lines  # the frozen LF encoder
     # tokens: the frozen stage1 (eval) through the oracle, near-ties checked
     e = O.Ctx(False)
     spec = O.Stage1Spec(T, C)

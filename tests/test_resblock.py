@@ -1,4 +1,5 @@
-"""Fused small-channel ResBlock (csrc/tvq_resblock.hip) against the per-op HIP path it
+"""Fused ResBlock (csrc/tvq_resblock.hip, C in {8, 16, 32}; tvq_resblock_w8.hip, C = 64 on
+the LF band's W = 8 maps) against the per-op HIP path it
 replaces (Snake -> conv -> BN+Snake -> conv+dropout+residual kernels, which the G3 goldens
 pin to the reference): training forward (y, BN running stats), every gradient, the same
 dropout mask, and the eval forward.  Tolerance: rel 2e-5 of each tensor's max (different
@@ -9,7 +10,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 SHAPES = [(8, 8, 64), (8, 16, 32), (4, 16, 16), (16, 8, 32), (3, 32, 16), (2, 32, 32),
-          (2, 16, 64), (5, 8, 16)]
+          (2, 16, 64), (5, 8, 16), (8, 64, 8), (3, 64, 8), (300, 64, 8)]
 
 
 def _block(C, drop, seed=0):
@@ -87,6 +88,24 @@ def test_fused_resblock_train_matches_per_op(B, C, W, drop):
         assert ((y2 - x) == 0).float().mean().item() > 0.2
 
 
+def test_fused_resblock_w8_eval_packed_and_unpacked():
+    """The C = 64 eval kernel reads packed weights inside a pack-cache scope and the raw
+    (n, c, tap) weights outside one: the same results either way."""
+    from timevqvae.hip.conv import PackCache
+    from timevqvae.hip._native import plan_trace
+    x = torch.randn(6, 64, 3, 8, device="cuda")
+    m = _block(64, 0.3).eval()
+    with torch.no_grad(), plan_trace() as tr:
+        y1 = m(x)
+        with PackCache(x.device).scope():
+            y2 = m(x)
+            y3 = m(x)
+        torch.cuda.synchronize()
+    assert tr.has("w8_eval C64 W8 B6 packed=0") and tr.has("w8_eval C64 W8 B6 packed=1"), tr.lines
+    _close(y2, y1, "packed vs raw")
+    assert torch.equal(y2, y3)
+
+
 @pytest.mark.parametrize("B,C,W", SHAPES)
 def test_fused_resblock_eval_matches_per_op(B, C, W):
     x = torch.randn(B, C, 3, W, device="cuda")
@@ -98,7 +117,9 @@ def test_fused_resblock_eval_matches_per_op(B, C, W):
 
 def test_fused_resblock_declines_unsupported_shapes():
     from timevqvae.hip import resblock
-    assert not resblock.supported(torch.empty(2, 64, 3, 8, device="cuda"), 64, 64)
+    assert resblock.supported(torch.empty(2, 64, 3, 8, device="cuda"), 64, 64)
+    assert not resblock.supported(torch.empty(2, 64, 3, 16, device="cuda"), 64, 64)
+    assert not resblock.supported(torch.empty(2, 128, 3, 8, device="cuda"), 128, 128)
     assert not resblock.supported(torch.empty(2, 32, 3, 64, device="cuda"), 32, 32)
     assert not resblock.supported(torch.empty(2, 4, 3, 32, device="cuda"), 4, 4)
     assert not resblock.supported(torch.empty(2, 8, 3, 20, device="cuda"), 8, 8)
