@@ -15,15 +15,19 @@
 //
 //   w8_fwd1  s1 = Snake_a1(x) staged (and stored: the conv1 weight gradient's input) ->
 //            h = conv1(s1) + b1 -> store h; per-image fp64 BN partial sums
-//   w8_fwd2  every block reduces the 256 images' partials in one fixed order to the batch
-//            mean / invstd (block 0 publishes them and the running statistics);
-//            s2 = Snake_a2(BN(h)) staged (and stored) -> y = x + Dropout(conv2(s2) + b2)
+//   (bn_stats_final_kernel: 64 one-wave blocks reduce the partials in a fixed order to the
+//            batch mean / invstd / affine form and the running statistics)
+//   w8_fwd2  s2 = Snake_a2(BN(h)) staged (and stored) -> y = x + Dropout(conv2(s2) + b2)
 //   w8_bwd2  g2 = Dropout'(dy) staged (and stored) -> ds2 = conv2^T(g2) -> du = ds2 *
-//            Snake'(u) (u = BN(h) recomputed) -> store du; per-image (sum du, sum du xhat)
-//            and the Snake a2 term (a slab row)
-//   w8_bwd1  every block reduces those partials to the BN backward coefficients (block 0
-//            writes the BN weight / bias gradients); dh = BN'(du) staged (and stored) ->
-//            ds1 = conv1^T(dh) -> dx = ds1 * Snake'(x) + dy; the Snake a1 term (a slab row)
+//            Snake'(u) (u = BN(h) recomputed) -> store du; per-image (sum du, sum du xhat,
+//            Snake a2 term)
+//   (bn_bwd_final_kernel: those partials -> the BN backward coefficients, the BN weight /
+//            bias and Snake a2 gradients)
+//   w8_bwd1  dh = BN'(du) staged (and stored) -> ds1 = conv1^T(dh) -> dx = ds1 * Snake'(x)
+//            + dy; the Snake a1 term (a slab row)
+// Reducing the 256 images' partials in every consumer block (as the small-channel kernels
+// do) read 256 KB of partials per block and held them in 128 VGPRs: 24 us per fwd2 / bwd1
+// launch (round 5); the one-wave-per-channel finish launch is ~3 us.
 //   weight gradients: tvq_conv2d_wgrad on (s2, g2) and (s1, dh) -- the image-batched
 //            conv_wgrad_w8 kernel (a 64 x 577 slab row per image would be 148 KB)
 //   w8_eval  both convs in one launch with BN from the running statistics (the frozen
@@ -59,6 +63,7 @@ struct Args {
   const float *a1, *b1, *a2, *b2;
   const float *bn_w, *bn_b, *rmean, *rvar;  // eval / BN backward
   const float* save;                         // mean | invstd | scale | shift
+  const float* coef;                         // BN backward (sum du, sum du xhat) per channel
   WView w1, w2;                              // forward views (eval / fwd) or data-gradient views
   float *h_out, *s_out, *y, *du, *dx, *g_out, *slabda;
   double* part;
@@ -102,20 +107,31 @@ __device__ __forceinline__ double half_sum_d(double v) {
   return v;
 }
 
-// The block's conv of the staged planes S: D[row][pos] for rows 32 (w & 1) .. and input
-// chunk w >> 1, partial tile to red[w][16][64].  FLIP: the data gradient (taps mirrored).
-template <bool FLIP>
-__device__ __forceinline__ void conv(const WView wv, const float* __restrict__ S,
-                                     float* __restrict__ red) {
+// This lane's 72 weight values of the block's conv: a[t][u] = W(row 32 (w & 1) + (l & 31),
+// reduction channel 16 (w >> 1) + (l >> 5) + 2u, tap t).  Issued at the kernel's start (the
+// weights do not depend on the staged image), so their L2 round trip overlaps the prologue;
+// the scheduling barrier keeps the compiler from sinking them next to their MFMAs.
+__device__ __forceinline__ void load_w(const WView wv, float (&a)[9][8]) {
   const int lane = threadIdx.x & 63, wid = wid_();
   const int r32 = lane & 31, hl = lane >> 5;
   const int nt = wid & 1, c0 = (wid >> 1) * CPC;
   const float* wp = wv.w + (int64_t)(32 * nt + r32) * wv.sn + (int64_t)(c0 + hl) * wv.sc;
-  float a[9][8];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int u = 0; u < 8; ++u) a[t][u] = wp[(int64_t)(2 * u) * wv.sc + (int64_t)t * wv.st];
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// The block's conv of the staged planes S: D[row][pos] for rows 32 (w & 1) .. and input
+// chunk w >> 1 (weights `a` from load_w), partial tile to red[w][16][64].  FLIP: the data
+// gradient (taps mirrored).
+template <bool FLIP>
+__device__ __forceinline__ void conv(const float (&a)[9][8], const float* __restrict__ S,
+                                     float* __restrict__ red) {
+  const int lane = threadIdx.x & 63, wid = wid_();
+  const int r32 = lane & 31, hl = lane >> 5;
+  const int c0 = (wid >> 1) * CPC;
   const int m = r32 < P ? r32 : 0;
   const float* sp = S + (c0 + hl) * PS + (m / W) * WP + (m % W);
   floatx16 acc;
@@ -142,110 +158,85 @@ __device__ __forceinline__ float conv_at(const float* __restrict__ red, int n, i
   return s;
 }
 
-// Batch totals of the NS per-image fp64 partials part[(c*NS + i)*B + b] of this wave's 8
-// channels 8w + q (q < 8), in every block in one fixed order (lane l: images l, l + 64, ..,
-// then the xor tree): t[q][i] in every lane.
-template <int NS>
-__device__ __forceinline__ void batch_sums(const double* __restrict__ part, int B,
-                                           double (&t)[8][NS]) {
-  const int l = threadIdx.x & 63, w = wid_();
-  double v[8][NS][4];
-#pragma unroll
-  for (int q = 0; q < 8; ++q)
-#pragma unroll
-    for (int i = 0; i < NS; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int b = l + 64 * k;
-        v[q][i][k] = b < B ? part[((int64_t)(8 * w + q) * NS + i) * B + b] : 0.0;
-      }
-#pragma unroll
-  for (int q = 0; q < 8; ++q)
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      double s = v[q][i][0] + v[q][i][1] + v[q][i][2] + v[q][i][3];
-      for (int b = l + 256; b < B; b += 64) s += part[((int64_t)(8 * w + q) * NS + i) * B + b];
-      t[q][i] = wave_sum_d(s);
-    }
-}
-
 // ---------------------------------------------------------------- kernels
 __global__ __launch_bounds__(T) void w8_fwd1_kernel(Args a) {
   extern __shared__ float sm[];
   float* S = sm;
   float* red = sm + PLANE;
-  const int b = blockIdx.x, p = el_p(), hl = (threadIdx.x & 63) >> 5;
+  const int b = blockIdx.x, p = el_p();
   const int64_t img0 = (int64_t)b * C * P;
-  float xv[4];
+  float wa[9][8], xv[4], av[4], bv[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) xv[j] = p < P ? a.x[img0 + el_c(j) * P + p] : 0.f;
+  for (int j = 0; j < 4; ++j) {
+    xv[j] = a.x[img0 + el_c(j) * P + (p < P ? p : 0)];
+    av[j] = a.a1[el_c(j)];
+    bv[j] = a.b1[el_c(j)];
+  }
+  load_w(a.w1, wa);  // after the staging operands: their wait leaves the weights in flight
   border(S);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = el_c(j);
     if (p >= P) continue;
-    const float av = a.a1[c];
-    const float s = snake_f(xv[j], av, 1.0f / av);
+    const float s = snake_f(xv[j], av[j], 1.0f / av[j]);
     S[cell(c, p)] = s;
     a.s_out[img0 + c * P + p] = s;
   }
   __syncthreads();
-  conv<false>(a.w1, S, red);
+  conv<false>(wa, S, red);
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = el_c(j);
     double s0 = 0.0, s1 = 0.0;
     if (p < P) {
-      const float v = conv_at(red, c, p) + a.b1[c];
+      const float v = conv_at(red, c, p) + bv[j];
       a.h_out[img0 + c * P + p] = v;
       s0 = (double)v;
       s1 = (double)v * (double)v;
     }
     s0 = half_sum_d(s0);
     s1 = half_sum_d(s1);
-    if ((threadIdx.x & 31) == 0) {
-      a.part[((int64_t)c * 2 + 0) * a.B + b] = s0;
-      a.part[((int64_t)c * 2 + 1) * a.B + b] = s1;
+    if ((threadIdx.x & 31) == 0) {  // [c][image][2]: bn_stats_final_kernel's chunk layout
+      a.part[((int64_t)c * a.B + b) * 2 + 0] = s0;
+      a.part[((int64_t)c * a.B + b) * 2 + 1] = s1;
     }
   }
-  (void)hl;
 }
 
 __global__ __launch_bounds__(T) void w8_fwd2_kernel(Args a) {
   extern __shared__ float sm[];
   float* S = sm;
   float* red = sm + PLANE;
-  const int b = blockIdx.x, p = el_p(), l = threadIdx.x & 63, hl = l >> 5, w = wid_();
+  const int b = blockIdx.x, p = el_p();
   const int64_t img0 = (int64_t)b * C * P;
-  float hv[4], xv[4];
+  float wa[9][8], hv[4], xv[4], av[4], bv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t gi = img0 + el_c(j) * P + (p < P ? p : 0);
     hv[j] = a.h[gi];
     xv[j] = a.x[gi];
+    av[j] = a.a2[el_c(j)];
+    bv[j] = a.b2[el_c(j)];
   }
-  double t[8][2];
-  batch_sums<2>(a.part, a.B, t);
-  border(S);
-  // the batch statistics (bn_final_from_sums); block 0 publishes them
-  const bool pub = b == 0 && l == 0;
-  if (pub && w == 0 && a.fin.nbt) a.fin.nbt[0] += 1;
-  float sc[8], sh[8];
+  float sc[4], sh[4];  // the batch statistics' affine form (bn_stats_final_kernel's)
 #pragma unroll
-  for (int q = 0; q < 8; ++q) bn_final_from_sums(t[q][0], t[q][1], 8 * w + q, a.fin, pub, sc[q], sh[q]);
+  for (int j = 0; j < 4; ++j) {
+    sc[j] = a.save[2 * C + el_c(j)];
+    sh[j] = a.save[3 * C + el_c(j)];
+  }
+  load_w(a.w2, wa);
+  border(S);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = el_c(j);
     if (p >= P) continue;
-    const float scv = hl ? sc[2 * j + 1] : sc[2 * j], shv = hl ? sh[2 * j + 1] : sh[2 * j];
-    const float av = a.a2[c];
-    const float s = snake_f(fmaf(hv[j], scv, shv), av, 1.0f / av);
+    const float s = snake_f(fmaf(hv[j], sc[j], sh[j]), av[j], 1.0f / av[j]);
     S[cell(c, p)] = s;
     a.s_out[img0 + c * P + p] = s;
   }
   __syncthreads();
-  conv<false>(a.w2, S, red);
+  conv<false>(wa, S, red);
   __syncthreads();
   const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
 #pragma unroll
@@ -253,7 +244,7 @@ __global__ __launch_bounds__(T) void w8_fwd2_kernel(Args a) {
     const int c = el_c(j);
     if (p >= P) continue;
     const int64_t gi = img0 + c * P + p;
-    float v = conv_at(red, c, p) + a.b2[c];
+    float v = conv_at(red, c, p) + bv[j];
     if (a.drop_p > 0.f) v = uniform01(seed, (uint64_t)gi) >= a.drop_p ? v * a.drop_scale : 0.f;
     a.y[gi] = xv[j] + v;
   }
@@ -265,9 +256,10 @@ __global__ __launch_bounds__(T) void w8_eval_kernel(Args a) {
   float* red = sm + PLANE;
   const int b = blockIdx.x, p = el_p();
   const int64_t img0 = (int64_t)b * C * P;
-  float xv[4];
+  float wa[9][8], xv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) xv[j] = a.x[img0 + el_c(j) * P + (p < P ? p : 0)];
+  load_w(a.w1, wa);
   border(S);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -277,7 +269,8 @@ __global__ __launch_bounds__(T) void w8_eval_kernel(Args a) {
     S[cell(c, p)] = snake_f(xv[j], av, 1.0f / av);
   }
   __syncthreads();
-  conv<false>(a.w1, S, red);
+  conv<false>(wa, S, red);
+  load_w(a.w2, wa);  // conv2's weights in flight during conv1's epilogue
   __syncthreads();
   float s2[4];
 #pragma unroll
@@ -294,7 +287,7 @@ __global__ __launch_bounds__(T) void w8_eval_kernel(Args a) {
   for (int j = 0; j < 4; ++j)
     if (p < P) S[cell(el_c(j), p)] = s2[j];
   __syncthreads();
-  conv<false>(a.w2, S, red);
+  conv<false>(wa, S, red);
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -309,13 +302,14 @@ __global__ __launch_bounds__(T) void w8_bwd2_kernel(Args a) {
   float* red = sm + PLANE;
   const int b = blockIdx.x, p = el_p();
   const int64_t img0 = (int64_t)b * C * P;
-  float gv[4], hv[4];
+  float wa[9][8], gv[4], hv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t gi = img0 + el_c(j) * P + (p < P ? p : 0);
     gv[j] = a.dy[gi];
     hv[j] = a.h[gi];
   }
+  load_w(a.w2, wa);
   border(G);
   const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
 #pragma unroll
@@ -329,7 +323,7 @@ __global__ __launch_bounds__(T) void w8_bwd2_kernel(Args a) {
     a.g_out[gi] = d;
   }
   __syncthreads();
-  conv<true>(a.w2, G, red);
+  conv<true>(wa, G, red);
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -354,10 +348,11 @@ __global__ __launch_bounds__(T) void w8_bwd2_kernel(Args a) {
     s0 = half_sum_d(s0);
     s1 = half_sum_d(s1);
     s2 = half_sum_d(s2);
-    if ((threadIdx.x & 31) == 0) {
-      a.part[((int64_t)c * 2 + 0) * a.B + b] = s0;
-      a.part[((int64_t)c * 2 + 1) * a.B + b] = s1;
-      a.slabda[(int64_t)b * C + c] = (float)s2;
+    if ((threadIdx.x & 31) == 0) {  // [c][image][3]: bn_bwd_final_kernel's chunk layout
+      double* pp = a.part + ((int64_t)c * a.B + b) * 3;
+      pp[0] = s0;
+      pp[1] = s1;
+      pp[2] = s2;
     }
   }
 }
@@ -366,9 +361,9 @@ __global__ __launch_bounds__(T) void w8_bwd1_kernel(Args a) {
   extern __shared__ float sm[];
   float* G = sm;
   float* red = sm + PLANE;
-  const int b = blockIdx.x, p = el_p(), l = threadIdx.x & 63, hl = l >> 5, w = wid_();
+  const int b = blockIdx.x, p = el_p();
   const int64_t img0 = (int64_t)b * C * P;
-  float dv[4], hv[4], xv[4], yv[4];
+  float wa[9][8], dv[4], hv[4], xv[4], yv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t gi = img0 + el_c(j) * P + (p < P ? p : 0);
@@ -377,30 +372,27 @@ __global__ __launch_bounds__(T) void w8_bwd1_kernel(Args a) {
     xv[j] = a.x[gi];  // the epilogue's operands, requested with the prologue's
     yv[j] = a.dy[gi];
   }
-  double t[8][2];
-  batch_sums<2>(a.part, a.B, t);
-  border(G);
-  float md[8], mx[8];
+  float md[4], mx[4];  // the BN backward coefficients (bn_bwd_final_kernel's sums)
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    md[q] = (float)t[q][0] * a.invN;
-    mx[q] = (float)t[q][1] * a.invN;
-    if (b == 0 && l == 0) bn_bwd_params_from_sums(t[q][0], t[q][1], 0.0, 8 * w + q, a.bfin);
+  for (int j = 0; j < 4; ++j) {
+    md[j] = a.coef[2 * el_c(j)] * a.invN;
+    mx[j] = a.coef[2 * el_c(j) + 1] * a.invN;
   }
+  load_w(a.w1, wa);
+  border(G);
   // dh = w * invstd * (du - mean(du) - xhat * mean(du * xhat))  (bn_bwd_apply_kernel)
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = el_c(j);
     if (p >= P) continue;
-    const float mdv = hl ? md[2 * j + 1] : md[2 * j], mxv = hl ? mx[2 * j + 1] : mx[2 * j];
     const float mu = a.save[c], is = a.save[C + c], bw = a.bn_w ? a.bn_w[c] : 1.f;
     const float xhat = (hv[j] - mu) * is;
-    const float g = bw * is * (dv[j] - mdv - xhat * mxv);
+    const float g = bw * is * (dv[j] - md[j] - xhat * mx[j]);
     G[cell(c, p)] = g;
     a.g_out[img0 + c * P + p] = g;
   }
   __syncthreads();
-  conv<true>(a.w1, G, red);
+  conv<true>(wa, G, red);
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -446,7 +438,7 @@ static Ws ws_layout(int64_t B) {
   const size_t slabd = (size_t)(B * C + reduce_rows_scratch(B, C)) * 4;
   const size_t wg = (size_t)tvq_conv_workspace(4, B, C, 3, W, C, 3, 3, 1, 0) * 4;
   w.part = 0;
-  w.slabda1 = w.part + al((size_t)B * C * 2 * 8);
+  w.slabda1 = w.part + al((size_t)B * C * 3 * 8);
   w.slabda2 = w.slabda1 + al(slabd);
   w.g2 = w.slabda2 + al(slabd);
   w.dh = w.g2 + al(img);
@@ -501,6 +493,9 @@ int w8_train_fwd(const float* x, int64_t B, const float* a1, const float* w1, co
   TVQ_PLAN("w8_fwd1 C%d W%d B%lld", C, W, (long long)B);
   a.s_out = saved + img;  // s1
   hipLaunchKernelGGL(w8_fwd1_kernel, dim3((unsigned)B), dim3(T), LDS, st, a);
+  a.fin.chunks = (int)B;  // the per-image partials -> save, running statistics
+  bn_stats_final_launch(a.part, a.fin, st);
+  a.save = save;
   TVQ_PLAN("w8_fwd2 C%d W%d B%lld", C, W, (long long)B);
   a.s_out = saved + 2 * img;  // s2
   hipLaunchKernelGGL(w8_fwd2_kernel, dim3((unsigned)B), dim3(T), LDS, st, a);
@@ -543,7 +538,6 @@ int w8_bwd(const float* dy, const float* x, const float* saved, int64_t B, const
   float* dh = (float*)(ws + L.dh);
   float* du = (float*)(ws + L.du);
   float* slabda1 = (float*)(ws + L.slabda1);
-  float* slabda2 = (float*)(ws + L.slabda2);
   Args a = {};
   a.x = x; a.h = h; a.dy = dy; a.du_in = du;
   a.a1 = a1; a.a2 = a2; a.bn_w = bn_w; a.save = save;
@@ -556,13 +550,17 @@ int w8_bwd(const float* dy, const float* x, const float* saved, int64_t B, const
   a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
   a.seed_ptr = seed_ptr; a.offset = offset;
   a.invN = 1.0f / (float)(B * P);
-  a.bfin = {C, (int)B, nullptr, dbn_w, dbn_b, nullptr, (int)accumulate};
+  float* coef = (float*)(ws + L.slabda2);  // 2C floats
+  a.bfin = {C, (int)B, coef, dbn_w, dbn_b, da2, (int)accumulate};
+  a.coef = coef;
   TVQ_PLAN("w8_bwd2 C%d W%d B%lld", C, W, (long long)B);
-  a.g_out = g2; a.slabda = slabda2;
+  a.g_out = g2;
   hipLaunchKernelGGL(w8_bwd2_kernel, dim3((unsigned)B), dim3(T), LDS, st, a);
   int rc = launch_status("tvq_resblock_bwd");
   if (rc) return rc;
   // conv2's weight gradient from (s2, g2) while the next kernel waits on nothing of it
+  // per-image partials -> the BN backward coefficients, BN weight / bias and Snake a2 gradients
+  bn_bwd_final_launch(a.part, a.bfin, st);
   rc = tvq_conv2d_wgrad(s2, B, C, 3, W, g2, C, W, 3, 3, 1, 0, dw2, db2, accumulate,
                         (float*)(ws + L.wg2), st);
   if (rc) return rc;
@@ -575,7 +573,6 @@ int w8_bwd(const float* dy, const float* x, const float* saved, int64_t B, const
                         (float*)(ws + L.wg1), st);
   if (rc) return rc;
   conv_wgrad_finish(slabda1, (int)B, C, 1, da1, nullptr, (int)accumulate, st);
-  conv_wgrad_finish(slabda2, (int)B, C, 1, da2, nullptr, (int)accumulate, st);
   return launch_status("tvq_resblock_bwd");
 }
 
