@@ -518,6 +518,32 @@ int tvq_ffn_bwd(const float* gy, const float* pre, int64_t M, int64_t D, const f
                 const float* W2, const float* gate, float p, const int64_t* seed_ptr,
                 uint64_t offset, float* d_pre, float* dxn, float* gy_gated, tvq_stream_t stream);
 int tvq_gelu_bwd(const float* dy, const float* x, int64_t n, float* dx, tvq_stream_t stream);
+/* The priors' attention branch in training (x-transformers pre-norm layer with RMSNorm,
+ * bidirectional_transformer.py:92-110), D = 128, 2 heads of 64, S <= 32 tokens per sequence,
+ * B sequences of row-major (B*S, 128) token rows (csrc/tvq_xattn.hip):
+ *   xn = RMSNorm_g(x) (x / max(|x|, 1e-12) * nscale * g), [q|k|v] = xn [Wq;Wk;Wv]^T (Wqkv:
+ *   384 x 128 row-major), per head P = Dropout_p(softmax(q k^T / 8)) (the mask of
+ *   tvq_attention_fwd), o = P v, y = x + gate * (o Wo^T)   (gate nullable: 1)
+ * one launch; it also writes xn (B*S x 128), inv (B*S: 1 / max(|x|, 1e-12)), qkv (B*S x 384),
+ * o (B*S x 128) and lse (B*2*S) for the backward and the weight gradients.
+ * tvq_attn_branch_bwd: from gy = dL/dy: dx (the residual and RMSNorm paths), dqkv (B*S x 384;
+ * the caller's dWqkv = dqkv^T xn), gy_gated = gate * gy (when gate and gy_gated are both
+ * non-null; the caller's dWo = gy_gated^T o, else gy^T o), dg (written, or added when
+ * accumulate: then batched into an open tvq_wgrad_defer scope).  workspace:
+ * tvq_attn_branch_workspace(B, 128) floats.  16-byte aligned rows; p in [0, 1). */
+int64_t tvq_attn_branch_workspace(int64_t B, int64_t D);
+int tvq_attn_branch_fwd(const float* x, int64_t B, int64_t S, int64_t D, int64_t heads,
+                        const float* g, float nscale, const float* Wqkv, const float* Wo,
+                        const float* gate, float drop_p, const int64_t* seed_ptr, uint64_t offset,
+                        float* y, float* xn, float* inv, float* qkv, float* o, float* lse,
+                        tvq_stream_t stream);
+int tvq_attn_branch_bwd(const float* gy, const float* x, int64_t B, int64_t S, int64_t D,
+                        int64_t heads, const float* g, float nscale, const float* inv,
+                        const float* Wqkv, const float* Wo, const float* gate, float drop_p,
+                        const int64_t* seed_ptr, uint64_t offset, const float* qkv, const float* o,
+                        const float* lse, float* dx, float* dqkv, float* gy_gated, float* dg,
+                        int64_t accumulate, float* workspace, tvq_stream_t stream);
+
 
 /* ---------------------------------------------------------------- fused LF prior (eval)
  * BidirectionalTransformer.forward_lf (bidirectional_transformer.py:166-192, the

@@ -170,6 +170,10 @@ sig("tvq_prior_lf_eval_workspace", I64, I64, I64, I64, restype=I64)
 sig("tvq_prior_lf_eval", P, I64, I64, I64, P, I64, I64, P, I64, I64, F32, P, P, P)
 sig("tvq_ffn_fwd", P, P, I64, I64, P, P, P, P, P, F32, P, U64, P, P, P, P)
 sig("tvq_ffn_bwd", P, P, I64, I64, P, P, P, F32, P, U64, P, P, P, P)
+sig("tvq_attn_branch_workspace", I64, I64, restype=I64)
+sig("tvq_attn_branch_fwd", P, I64, I64, I64, I64, P, F32, P, P, P, F32, P, U64, P, P, P, P, P, P, P)
+sig("tvq_attn_branch_bwd", P, P, I64, I64, I64, I64, P, F32, P, P, P, P, F32, P, U64, P, P, P, P, P,
+    P, P, I64, P, P)
 sig("tvq_prior_lf_eval_sample", P, I64, I64, I64, P, I64, I64, P, I64, I64, F32, I64, P, P, U64,
     P, P, P, P, I64, P)
 sig("tvq_maskgit_sample", P, I64, I64, I64, I64, I64, P, I64, P, P, U64, P, P, P)

@@ -240,6 +240,95 @@ def fused_ff(xn, r, w1, b1, w2, b2, gate, p, site):
     return _FusedFF.apply(xn, r, w1, b1, w2, b2, gate, float(p), int(site))
 
 
+# ---------------------------------------------------------------- fused attention branch
+FUSED_ATTN = os.environ.get("TVQ_FUSED_ATTN", "1") != "0"
+
+
+class _AttnBranch(torch.autograd.Function):
+    """x + gate * Attention(RMSNorm(x)) for the LF prior's width (128, 2 heads of 64, S <= 32)
+    in one launch forward and one backward (csrc/tvq_xattn.hip; x-transformers pre-norm
+    attention layer, bidirectional_transformer.py:92-110).  The weight gradients go through
+    the grouped weight-gradient path like every Linear's: dWqkv = dqkv^T xn into the stacked
+    flat-gradient view (as _QKVAttention), dWo = (gate gy)^T o; the RMSNorm gain gradient is a
+    deferred slab sum."""
+
+    @staticmethod
+    def forward(ctx, x, g, wq, wk, wv, wo, gate, heads, p, site):
+        B, S, D = x.shape
+        M = B * S
+        x2 = x.reshape(M, D).contiguous()
+        W = _stacked([wq, wk, wv], (3 * D, D))
+        if W is None:
+            W = torch.cat([wq, wk, wv], 0).contiguous()
+        dev = x.device
+        y, xn, o = (torch.empty_like(x2) for _ in range(3))
+        inv = torch.empty(M, device=dev)
+        qkv = torch.empty((M, 3 * D), device=dev)
+        lse = torch.empty(B * heads * S, device=dev)
+        seed = rng.seed_tensor(dev) if p > 0 else None
+        off = rng.call_offset(site) if p > 0 else 0
+        call("tvq_attn_branch_fwd", ptr(x2), B, S, D, heads, ptr(g), math.sqrt(D), ptr(W), ptr(wo),
+             ptr(gate), float(p), ptr(seed), off, ptr(y), ptr(xn), ptr(inv), ptr(qkv), ptr(o),
+             ptr(lse), stream_ptr())
+        ctx.save_for_backward(x2, xn, inv, qkv, o, lse, W)
+        ctx.params = (wq, wk, wv, wo, g)
+        ctx.gate, ctx.seed = gate, seed
+        ctx.cfg = (B, S, D, heads, float(p), off)
+        ctx.wg_tag = wgrad.current_tag()
+        return y.reshape(B, S, D)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, xn, inv, qkv, o, lse, W = ctx.saved_tensors
+        B, S, D, heads, p, off = ctx.cfg
+        wq, wk, wv, wo, g = ctx.params
+        M, L = B * S, 3 * D
+        dev = x2.device
+        g2 = gy.reshape(M, D).contiguous()
+        need = ctx.needs_input_grad
+        dx = torch.empty_like(x2)
+        dqkv = torch.empty((M, L), device=dev)
+        gg = torch.empty_like(g2) if ctx.gate is not None else None
+        sink_g = grad_sink(g)
+        dg = sink_g if sink_g is not None else torch.empty(D, device=dev)
+        ws = torch.empty(value("tvq_attn_branch_workspace", B, D), device=dev)
+        call("tvq_attn_branch_bwd", ptr(g2), ptr(x2), B, S, D, heads, ptr(g), math.sqrt(D), ptr(inv),
+             ptr(W), ptr(wo), ptr(ctx.gate), p, ptr(ctx.seed), off, ptr(qkv), ptr(o), ptr(lse),
+             ptr(dx), ptr(dqkv), ptr(gg), ptr(dg), int(sink_g is not None), ptr(ws), stream_ptr())
+        _keep(ws)  # its gain-gradient reduction may be deferred
+        dws = [None, None, None]
+        if any(need[2:5]):
+            sinks = [grad_sink(w) for w in (wq, wk, wv)]
+            sink = _stacked(sinks, (L, D)) if all(s_ is not None for s_ in sinks) else None
+            if sink is not None:  # into the flat gradient (stacked view)
+                if not wgrad.defer(dqkv, L, xn, D, sink, D, L, D, M, ctx.wg_tag):
+                    with streams.offload(dqkv, xn):
+                        gemm(dqkv, 1, L, xn, D, 1, L, D, M, out=sink, ldc=D, accumulate=True)
+            else:
+                dW = gemm(dqkv, 1, L, xn, D, 1, L, D, M)
+                dws = [dW[i * D:(i + 1) * D] for i in range(3)]
+        dwo = weight_grad(gg if gg is not None else g2, o, wo, M, D, D, ctx.wg_tag) if need[5] else None
+        return (dx.reshape(B, S, D), None if sink_g is not None else dg, *dws, dwo, None, None, None,
+                None)
+
+
+def attn_branch_supported(x, g, attn):
+    """Whether the fused attention branch (tvq_attn_branch_*) takes this layer: width 128,
+    2 heads of 64, <= 32 tokens, fp32 device weights on 16-byte boundaries."""
+    if not (FUSED_ATTN and x.is_cuda and x.dim() == 3 and x.shape[-1] == 128 and x.shape[1] <= 32
+            and attn.heads == 2):
+        return False
+    ws = (g, attn.to_q.weight, attn.to_k.weight, attn.to_v.weight, attn.to_out.weight)
+    return all(w.dtype == torch.float32 and w.is_cuda and w.is_contiguous() and
+               w.data_ptr() % 16 == 0 for w in ws) and tuple(attn.to_q.weight.shape) == (128, 128)
+
+
+def attn_branch(x, g, attn, gate, p):
+    """x + gate * attn(RMSNorm_g(x)) (pre-norm residual attention layer) on the fused path."""
+    return _AttnBranch.apply(x, g, attn.to_q.weight, attn.to_k.weight, attn.to_v.weight,
+                             attn.to_out.weight, gate, int(attn.heads), float(p), int(attn._site))
+
+
 # ---------------------------------------------------------------- attention
 class _Attention(torch.autograd.Function):
     @staticmethod

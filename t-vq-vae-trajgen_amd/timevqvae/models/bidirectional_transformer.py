@@ -28,8 +28,8 @@ from ..hip import rng, streams
 from ..hip.conv import PackCache, bn_eval_fusable, conv2d, conv2d_bn_eval
 from ..hip.linear import gemm, linear
 from ..hip.norm import bn_snake
-from ..hip.xf import (batch_colsum, drop_first_token, embed_assemble, embedding, fused_ff,
-                      fused_ff_supported, gelu,
+from ..hip.xf import (attn_branch, attn_branch_supported, batch_colsum, drop_first_token,
+                      embed_assemble, embedding, fused_ff, fused_ff_supported, gelu,
                       layer_norm, linear_act, prior_lf_eval, prior_lf_eval_sample,
                       prior_lf_eval_supported, prior_lf_eval_workspace, qkv_attention, rmsnorm, rmsnorm_res,
                       upsample_nearest_t)
@@ -175,6 +175,11 @@ class Encoder(nn.Module):
             # branch's output-Linear epilogue (its backward scales the branch gradient)
             gate = self._keep[i:i + 1] if device_gates else None
             if isinstance(norms[0], RMSNorm):
+                if isinstance(block, Attention) and attn_branch_supported(x, norms[0].g, block):
+                    # RMSNorm + attention + out-projection + gated residual: one launch each way
+                    x = attn_branch(x, norms[0].g, block, gate,
+                                    block.dropout if self.training else 0.0)
+                    continue
                 n, r = rmsnorm_res(x, norms[0].g)  # residual gradient summed in the norm bwd
                 x = block(n, residual=r, gate=gate)
             else:
