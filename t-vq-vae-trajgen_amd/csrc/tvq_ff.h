@@ -31,47 +31,55 @@ __device__ __forceinline__ void ff_load_row(const float* __restrict__ row, int h
 // acc[r] (row i = crow(r, h) of the wave's 32-row tile, column = the lane's token) +=
 // sum_t A(i, k_t) B(k_t, token), k_t = 32 (t >> 4) + crow(t & 15, h): A from the weight row
 // W[row0 + (l & 31)][k] (row-major, ld 128: 16-B loads) or, TRANS, W[k][col0 + (l & 31)]
-// (the transposed access of a data gradient: one 4-B load per step, 128 B per half-wave)
+// (the transposed access of a data gradient: one 4-B load per step, 128 B per half-wave).
+// ff_wload issues all 64 A values of a tile at once (one L2 round trip per tile; a kernel can
+// request the next tile's while it multiplies this one), ff_mma runs the 64 MFMA steps.
 template <bool TRANS>
-__device__ __forceinline__ floatx16 ff_tile_acc(const float* __restrict__ W, int rc0,
-                                                const float (&b)[64], int lane, floatx16 acc) {
+__device__ __forceinline__ void ff_wload(const float* __restrict__ W, int rc0, int lane,
+                                         float (&wa)[64]) {
   const int i = lane & 31, h = lane >> 5;
   if (!TRANS) {
     const float* wr = W + (int64_t)(rc0 + i) * FF_D;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float4 a[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) a[g] = *reinterpret_cast<const float4*>(wr + 32 * q + 8 * g + 4 * h);
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g].x, b[16 * q + 4 * g], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g].y, b[16 * q + 4 * g + 1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g].z, b[16 * q + 4 * g + 2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g].w, b[16 * q + 4 * g + 3], acc, 0, 0, 0);
+        const float4 v = *reinterpret_cast<const float4*>(wr + 32 * q + 8 * g + 4 * h);
+        wa[16 * q + 4 * g] = v.x;
+        wa[16 * q + 4 * g + 1] = v.y;
+        wa[16 * q + 4 * g + 2] = v.z;
+        wa[16 * q + 4 * g + 3] = v.w;
       }
-    }
   } else {
     const float* wc = W + rc0 + i;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float a[16];
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) a[r] = wc[(int64_t)(32 * q + ff_crow(r, h)) * FF_D];
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[r], b[16 * q + r], acc, 0, 0, 0);
-    }
+      for (int r = 0; r < 16; ++r) wa[16 * q + r] = wc[(int64_t)(32 * q + ff_crow(r, h)) * FF_D];
   }
+}
+__device__ __forceinline__ floatx16 ff_mma(const float (&wa)[64], const float (&b)[64], floatx16 acc) {
+#pragma unroll
+  for (int t = 0; t < 64; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[t], b[t], acc, 0, 0, 0);
   return acc;
+}
+__device__ __forceinline__ floatx16 ff_zero() {
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  return acc;
+}
+template <bool TRANS>
+__device__ __forceinline__ floatx16 ff_tile_acc(const float* __restrict__ W, int rc0,
+                                                const float (&b)[64], int lane, floatx16 acc) {
+  float wa[64];
+  ff_wload<TRANS>(W, rc0, lane, wa);
+  return ff_mma(wa, b, acc);
 }
 template <bool TRANS>
 __device__ __forceinline__ floatx16 ff_tile(const float* __restrict__ W, int rc0, const float (&b)[64],
                                             int lane) {
-  floatx16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  return ff_tile_acc<TRANS>(W, rc0, b, lane, acc);
+  return ff_tile_acc<TRANS>(W, rc0, b, lane, ff_zero());
 }
 
 // 4 values of a per-feature vector for register group g of tile w: p[32 w + 8 g + 4 h ..]

@@ -49,11 +49,14 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfArgs a) {
   const bool ok = m0 + j < a.M;
   const int64_t m = ok ? m0 + j : a.M - 1;
   const uint64_t seed = a.p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
-  float hd[16];
+  float hd[16], wa[64], wb[64];
   {
     float xb[64];
     ff_load_row(a.xn + m * FF_D, h, xb);
-    const floatx16 acc = ff_tile<false>(a.W1, 32 * w, xb, lane);
+    ff_wload<false>(a.W1, 32 * w, lane, wa);
+    ff_wload<false>(a.W2, 32 * w, lane, wb);  // the second Linear's, in flight meanwhile
+    __builtin_amdgcn_sched_barrier(0);
+    const floatx16 acc = ff_mma(wa, xb, ff_zero());
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const float4 bb = ff_vec4(a.b1, w, g, h);
@@ -77,7 +80,7 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfArgs a) {
   }
   float hb[64];
   ff_exchange(buf, w, hd, hb, lane);
-  const floatx16 acc = ff_tile<false>(a.W2, 32 * w, hb, lane);
+  const floatx16 acc = ff_mma(wb, hb, ff_zero());
   const float gt = a.gate ? *a.gate : 1.0f;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -105,10 +108,12 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfArgs a) {
   const int64_t m = ok ? m0 + j : a.M - 1;
   const uint64_t seed = a.p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
   const float gt = a.gate ? *a.gate : 1.0f;
-  float dp[16];
+  float dp[16], wa[64], wb[64];
   {
     float gb[64];
     ff_load_row(a.gy + m * FF_D, h, gb);
+    ff_wload<true>(a.W2, 32 * w, lane, wa);
+    __builtin_amdgcn_sched_barrier(0);
     // gate * gy for the W2 / b2 gradients (a dropped branch's weights get a zero gradient):
     // wave w stores the row's 32-feature slice w, already in registers
     if (a.gy_gated && ok) {
@@ -122,7 +127,9 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfArgs a) {
                             gt * gb[16 * q + 4 * g + 2], gt * gb[16 * q + 4 * g + 3]);
     }
     // d_hd (inner features 32 w ..) = gy W2: A(i, k) = W2[k][32 w + i]
-    const floatx16 acc = ff_tile<true>(a.W2, 32 * w, gb, lane);
+    ff_wload<true>(a.W1, 32 * w, lane, wb);  // the second product's, in flight meanwhile
+    __builtin_amdgcn_sched_barrier(0);
+    const floatx16 acc = ff_mma(wa, gb, ff_zero());
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int64_t o = m * FF_D + 32 * w + 8 * g + 4 * h;
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfArgs a) {
   float db[64];
   ff_exchange(buf, w, dp, db, lane);
   // dxn (features 32 w ..) = d_pre W1: A(i, k) = W1[k][32 w + i]
-  const floatx16 acc = ff_tile<true>(a.W1, 32 * w, db, lane);
+  const floatx16 acc = ff_mma(wb, db, ff_zero());
 #pragma unroll
   for (int g = 0; g < 4; ++g)
     if (ok)

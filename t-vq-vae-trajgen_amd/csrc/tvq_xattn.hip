@@ -109,8 +109,10 @@ __global__ __launch_bounds__(T) void xattn_fwd_kernel(Args a) {
   const int b = blockIdx.x, S = a.S;
   const bool valid = j < S;
   const int64_t row = (int64_t)b * S + (valid ? j : S - 1);
-  float xb[64];
+  float xb[64], wa[64], wb[64];
   ff_load_row(a.x + row * D, h, xb);
+  ff_wload<false>(a.Wqkv, 32 * w, lane, wa);  // Wq's rows: in flight during the RMSNorm
+  __builtin_amdgcn_sched_barrier(0);
   // RMSNorm (tvq_rmsnorm_fwd's arithmetic)
   float ss = 0.f;
 #pragma unroll
@@ -131,10 +133,17 @@ __global__ __launch_bounds__(T) void xattn_fwd_kernel(Args a) {
     store_fm(a.xn + row * D, 32 * w, h, slice(xn, w));
     if (w == 0 && h == 0) a.inv[row] = inv;
   }
-  // Q / K / V tiles w (token on the lane)
-  const floatx16 qt = ff_tile<false>(a.Wqkv, 32 * w, xn, lane);
-  const floatx16 kt = ff_tile<false>(a.Wqkv + D * D, 32 * w, xn, lane);
-  const floatx16 vt = ff_tile<false>(a.Wqkv + 2 * D * D, 32 * w, xn, lane);
+  // Q / K / V tiles w (token on the lane); each tile's weights requested before the previous
+  // tile's MFMAs
+  ff_wload<false>(a.Wqkv + D * D, 32 * w, lane, wb);
+  __builtin_amdgcn_sched_barrier(0);
+  const floatx16 qt = ff_mma(wa, xn, ff_zero());
+  ff_wload<false>(a.Wqkv + 2 * D * D, 32 * w, lane, wa);
+  __builtin_amdgcn_sched_barrier(0);
+  const floatx16 kt = ff_mma(wb, xn, ff_zero());
+  ff_wload<false>(a.Wo, 32 * w, lane, wb);  // the out-projection's, kept for the end
+  __builtin_amdgcn_sched_barrier(0);
+  const floatx16 vt = ff_mma(wa, xn, ff_zero());
   if (valid) {
     float* qr = a.qkv + row * 3 * D;
     store_fm(qr, 32 * w, h, qt);
@@ -196,7 +205,7 @@ __global__ __launch_bounds__(T) void xattn_fwd_kernel(Args a) {
   float oa[16], ob[64];
   to_arr(ot, oa);
   ff_exchange(reinterpret_cast<float4(*)[4][64]>(&ex[0][0][0]), w, oa, ob, lane);
-  const floatx16 yt = ff_tile<false>(a.Wo, 32 * w, ob, lane);
+  const floatx16 yt = ff_mma(wb, ob, ff_zero());
   const float gt = a.gate ? *a.gate : 1.0f;
   const floatx16 xr = slice(xb, w);
   floatx16 yv;
@@ -223,14 +232,19 @@ __global__ __launch_bounds__(T) void xattn_bwd_kernel(Args a) {
   const int64_t row = (int64_t)b * S + (valid ? j : S - 1);
   const float gt = a.gate ? *a.gate : 1.0f;
   floatx16 dot;  // dO tile w: (gate gy) Wo
+  float wa[64];
   {
     float gb[64];
     ff_load_row(a.gy + row * D, h, gb);
+    ff_wload<true>(a.Wo, 32 * w, lane, wa);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 64; ++i) gb[i] *= gt;
     if (a.gyg && valid) store_fm(a.gyg + row * D, 32 * w, h, slice(gb, w));
-    dot = ff_tile<true>(a.Wo, 32 * w, gb, lane);
+    dot = ff_mma(wa, gb, ff_zero());
   }
+  ff_wload<true>(a.Wqkv, 32 * w, lane, wa);  // the dxn product's first weights, early
+  __builtin_amdgcn_sched_barrier(0);
   const float* qr = a.qkv_in + row * 3 * D;
   const floatx16 qt = load_fm(qr, 32 * w, h);
   const floatx16 kt = load_fm(qr + D, 32 * w, h);
@@ -323,18 +337,22 @@ __global__ __launch_bounds__(T) void xattn_bwd_kernel(Args a) {
   // dxn tile w = dQ Wq + dK Wk + dV Wv (whole rows through the exchange buffer)
   __syncthreads();  // the dS transposes are read
   auto* buf = reinterpret_cast<float4(*)[4][64]>(sm + B_EX);
-  float ta[16], bx[64];
+  float ta[16], bx[64], wb[64];
   to_arr(dqt, ta);
   ff_exchange(buf, w, ta, bx, lane);
-  floatx16 dn = ff_tile<true>(a.Wqkv, 32 * w, bx, lane);
+  ff_wload<true>(a.Wqkv + D * D, 32 * w, lane, wb);
+  __builtin_amdgcn_sched_barrier(0);
+  floatx16 dn = ff_mma(wa, bx, ff_zero());
   __syncthreads();
   to_arr(dkt, ta);
   ff_exchange(buf, w, ta, bx, lane);
-  dn = ff_tile_acc<true>(a.Wqkv + D * D, 32 * w, bx, lane, dn);
+  ff_wload<true>(a.Wqkv + 2 * D * D, 32 * w, lane, wa);
+  __builtin_amdgcn_sched_barrier(0);
+  dn = ff_mma(wb, bx, dn);
   __syncthreads();
   to_arr(dvt, ta);
   ff_exchange(buf, w, ta, bx, lane);
-  dn = ff_tile_acc<true>(a.Wqkv + 2 * D * D, 32 * w, bx, lane, dn);
+  dn = ff_mma(wa, bx, dn);
   // RMSNorm backward (tvq_rmsnorm_bwd's arithmetic) + the residual path's gradient
   const floatx16 xt = load_fm(a.x + row * D, 32 * w, h);
   const floatx16 gyt = load_fm(a.gy + row * D, 32 * w, h);

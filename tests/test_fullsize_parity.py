@@ -383,6 +383,7 @@ def test_stage2_step_full_size_vs_oracle(cuda):
         torch.cuda.synchronize()
     assert tr.has("vq_assign D128"), tr.lines
     assert tr.has("w8_eval C64 W8 B256 packed=1"), tr.lines  # the frozen LF encoder
+    assert tr.has("attn_branch_fwd B256 S25") and tr.has("attn_branch_bwd B256 S25"), tr.lines
     # tokens: the frozen stage1 (eval) through the oracle, near-ties checked
     e = O.Ctx(False)
     spec = O.Stage1Spec(T, C)

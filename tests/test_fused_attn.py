@@ -63,6 +63,12 @@ def test_fused_attn_matches_per_op_path(B, n, p, gated, cuda):
     yb, gb = _run(norm, attn, x, gate, False, gy, p)
     assert rel(ya, yb) < 1e-5, rel(ya, yb)
     for k in gb:
+        if n == 1 and k in ("to_q.weight", "to_k.weight"):
+            # one token: softmax over one key is exactly 1, the true dQ / dK are 0 and both
+            # paths hold rounding noise only
+            scale = float(gb["to_v.weight"].abs().max())
+            assert float((ga[k] - gb[k]).abs().max()) <= 1e-5 * scale, k
+            continue
         assert rel(ga[k], gb[k]) < 1e-5, (k, rel(ga[k], gb[k]))
     if p == 0.0:  # and against torch's own arithmetic of the layer
         xx = x.clone()
