@@ -183,7 +183,8 @@ int tvq_conv_out_width(int64_t Win, int64_t KW, int64_t SW, int64_t transposed);
  * wide-channel tile, 16 / 32 = its K stage BK = 32 / 16 (default 64), 64 = its 4-wave
  * block (default 12 waves), 128 = its 64-channel variant for narrow maps (default off),
  * 256 = no direct small transposed-gather kernel, 512 = no stride-2 small-channel conv
- * kernels (conv_s2f / conv_s2t), 1024 = no stride-2 small-channel weight-gradient kernel;
+ * kernels (conv_s2f / conv_s2t), 1024 = no stride-2 small-channel weight-gradient kernel,
+ * 2048 = no few-output wide-input kernel (conv_n16: 128 -> <= 16 channels on (B, 128, 3, 32));
  * 0 forces the staged GEMMs (with the stride-2 kernels); < 0 only queries.  Default 3.
  * Returns the previous setting. */
 int tvq_conv_config(int64_t halo);

@@ -2601,6 +2601,7 @@ static void launch_tap(const float* in, const float* wt, float* out, const ConvG
 }
 
 static int g_conv_t32 = 1;  // conv_t32_kernel enabled (tvq_conv_config bit 8 turns it off)
+static int g_conv_n16 = 1;  // conv_n16_kernel enabled (tvq_conv_config bit 2048 turns it off)
 
 // ---------------------------------------------------------------- direct path
 // Convolutions of narrow maps with >= 32 channels on both sides -- the LF band's 64 /
@@ -3055,6 +3056,123 @@ static bool halo_preferred(int mode, int C, int KK, int SW, int N, int64_t Mpos)
   return true;
 }
 
+// ---------------------------------------------------------------- few outputs, wide input
+// The HF band's 128 -> <= 16 channel convs on (B, 128, 3, 32): ResBlock(128, 16)'s 3x3 conv1
+// and 1x1 projection forward (the decoder's first block), ResBlock(16, 128)'s data gradients
+// (the encoder's last block) -- a 24,576 x 16 output with a 1,152- (or 128-) deep reduction.
+// The tap-major GEMM gave them 96 blocks of a 16-row tile (0.11 of the fp32 peak, 51 us for
+// the 3x3 at B = 256).  Here one 8-wave block owns one image: its C x 3 x 32 input is staged
+// once into zero-padded LDS halo planes (C x 5 x 34), every B operand of the
+// v_mfma_f32_16x16x4_f32 chains is an LDS read at an immediate offset from the lane's base
+// (the reduction is tap-major, k = tap * C + c, so a step never crosses a tap), and the A
+// operand comes straight from the [tap][c][n]-packed weight (a wave's 64 lanes read 256
+// contiguous bytes per step).  Wave w takes input channels 32 (w & 3) .. for every tap (72
+// steps for 3x3) and position tiles 3 (w >> 2) .. + 2 (3 chains sharing each weight value);
+// the 4 channel splits are summed in LDS in split order.
+constexpr int N16_H = 3, N16_W = 32, N16_P = 96, N16_WPD = 34, N16_PS = 176, N16_T = 512;
+static bool n16_geom_ok(int mode, const ConvGeom& g, int KH, int KW, int SW, bool repl) {
+  return SW == 1 && !repl && g.N <= 16 && g.C == 128 && g.Hin == N16_H && g.Hout == N16_H &&
+         g.Win == N16_W && g.Wo == N16_W && g.oph == KH / 2 && g.opw == (KW - 1) / 2 &&
+         ((KH == 3 && KW == 3) || (KH == 1 && KW == 1)) && (mode == GATHER_F || mode == GATHER_T);
+}
+constexpr size_t N16_LDS = 4 * ((size_t)128 * N16_PS + 4 * 16 * N16_P);
+
+template <int MODE, int KH, int KW, bool POST>
+__global__ __launch_bounds__(N16_T) void conv_n16_kernel(const float* __restrict__ in,
+                                                         const float* __restrict__ wp,
+                                                         float* __restrict__ out, ConvGeom g,
+                                                         Epi e) {
+  constexpr int C = 128, KK = KH * KW, SPT = 8;  // 8 steps of 4 channels per tap and split
+  extern __shared__ float n16_smem[];
+  float* Pl = n16_smem;               // [C][PS] halo planes
+  float* red = n16_smem + C * N16_PS;  // [4 splits][16 rows][96 positions]
+  const int tid = threadIdx.x, lane = tid & 63, j = lane & 15, kq = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ks = w & 3, pg = w >> 2, b = blockIdx.x, N = g.N;
+  // the image's values (24 per thread in flight) and this wave's weights
+  const float* inb = in + (int64_t)b * C * N16_P;
+  float xv[C * N16_P / N16_T];
+#pragma unroll
+  for (int i = 0; i < C * N16_P / N16_T; ++i) xv[i] = inb[tid + N16_T * i];
+  const int nn = j < N ? j : N - 1;
+  float a[KK][SPT];
+#pragma unroll
+  for (int t = 0; t < KK; ++t)
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) a[t][s] = wp[((int64_t)t * C + 32 * ks + 4 * s + kq) * N + nn];
+  for (int i = tid; i < C * N16_PS; i += N16_T) Pl[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < C * N16_P / N16_T; ++i) {
+    const int el = tid + N16_T * i, c = el / N16_P, p = el - c * N16_P;
+    Pl[c * N16_PS + (p / N16_W + 1) * N16_WPD + p % N16_W + 1] = xv[i];
+  }
+  __syncthreads();
+  // lane base: channel 32 ks + kq, the window centre of position 16 tile + j of row tile / 2
+  const float* sp = Pl + (32 * ks + kq) * N16_PS + N16_WPD + 1 + j;
+  floatx4 acc[3];
+#pragma unroll
+  for (int f = 0; f < 3; ++f) acc[f] = floatx4{0.f, 0.f, 0.f, 0.f};
+  int pb[3];
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    const int tile = 3 * pg + f;  // 16 positions of row tile / 2
+    pb[f] = (tile >> 1) * N16_WPD + 16 * (tile & 1);
+  }
+#pragma unroll
+  for (int t = 0; t < KK; ++t) {
+    const int kh = t / KW, kw = t % KW;
+    const int dr = MODE == GATHER_F ? kh - KH / 2 : KH / 2 - kh;
+    const int dc = MODE == GATHER_F ? kw - (KW - 1) / 2 : (KW - 1) / 2 - kw;
+    const int off = dr * N16_WPD + dc;
+#pragma unroll
+    for (int s = 0; s < SPT; ++s)
+#pragma unroll
+      for (int f = 0; f < 3; ++f)
+        acc[f] = mfma16x16x4(a[t][s], sp[pb[f] + 4 * s * N16_PS + off], acc[f]);
+  }
+#pragma unroll
+  for (int f = 0; f < 3; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(ks * 16 + 4 * kq + r) * N16_P + 16 * (3 * pg + f) + j] = acc[f][r];
+  __syncthreads();
+  const uint64_t seed = e.drop_p > 0.f ? mix_seed(e.seed_ptr, e.offset) : 0ull;
+  for (int el = tid; el < N * N16_P; el += N16_T) {
+    const int n = el / N16_P, p = el - n * N16_P;
+    float v = red[n * N16_P + p];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) v += red[(k * 16 + n) * N16_P + p];
+    v += e.bias ? e.bias[n] : 0.f;
+    if (POST) v = epi_post(e, v, n);
+    const int64_t o = ((int64_t)b * N + n) * N16_P + p;
+    if (e.drop_p > 0.f) v = uniform01(seed, (uint64_t)o) >= e.drop_p ? v * e.drop_scale : 0.f;
+    if (e.residual) v += e.residual[o];
+    out[o] = v;
+  }
+}
+
+template <int MODE, int KH, int KW>
+static void launch_n16(const float* in, const float* wt, float* out, const ConvGeom& g,
+                       const Epi& e, hipStream_t st) {
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)conv_n16_kernel<MODE, KH, KW, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)N16_LDS);
+    (void)hipFuncSetAttribute((const void*)conv_n16_kernel<MODE, KH, KW, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)N16_LDS);
+    return true;
+  }();
+  (void)attr;
+  TVQ_PLAN("conv_n16 k%dx%d mode%d n%d", KH, KW, MODE, g.N);
+  if (e.bn_rv) {
+    t_post_done = true;
+    hipLaunchKernelGGL((conv_n16_kernel<MODE, KH, KW, true>), dim3(g.B), dim3(N16_T), N16_LDS, st,
+                       in, wt, out, g, e);
+  } else {
+    hipLaunchKernelGGL((conv_n16_kernel<MODE, KH, KW, false>), dim3(g.B), dim3(N16_T), N16_LDS,
+                       st, in, wt, out, g, e);
+  }
+}
+
 // halo path when the image + weight panel fit in LDS, else the staged GEMM
 // workspace (nullable) = [packed weight N*C*KK][split-K slab]; see conv_gemm_ws
 template <int MODE, int KH, int KW, int SW, bool REPL>
@@ -3085,6 +3203,13 @@ static void launch_conv(const float* in, const float* wt, float* out, ConvGeom g
     else
       hipLaunchKernelGGL((conv_small_kernel<MODE, KH, KW, SW, REPL, 16>), grid, dim3(256), 0, st, in, wt, out, g, e);
     return;
+  }
+  if constexpr (SW == 1 && !REPL && ((KH == 3 && KW == 3) || (KH == 1 && KW == 1))) {
+    if (ws && g_conv_n16 && n16_geom_ok(MODE, g, KH, KW, SW, REPL)) {
+      wt = pack_weight(wt, g, KH * KW, ws, st);  // [tap][c][n]
+      launch_n16<MODE, KH, KW>(in, wt, out, g, e, st);
+      return;
+    }
   }
   HaloPlan pl;
   const int oh = MODE == GATHER_F ? g.oph : KH - 1 - g.oph;
@@ -3276,7 +3401,7 @@ extern "C" int tvq_conv_config(int64_t halo) {
   const int prev = g_conv_halo | (g_conv_t32 ? 0 : 8) | (g_t32_bk == 32 ? 16 : 0) |
                    (g_t32_bk == 16 ? 32 : 0) | (g_t32_nw == 4 ? 64 : 0) |
                    (g_t32_n64 ? 128 : 0) | (g_conv_small ? 0 : 256) | (g_conv_s2 ? 0 : 512) |
-                   (g_conv_ws2 ? 0 : 1024);
+                   (g_conv_ws2 ? 0 : 1024) | (g_conv_n16 ? 0 : 2048);
   if (halo >= 0) {
     g_conv_halo = (int)(halo & 7);
     g_conv_t32 = (halo & 8) ? 0 : 1;
@@ -3286,6 +3411,7 @@ extern "C" int tvq_conv_config(int64_t halo) {
     g_conv_small = (halo & 256) ? 0 : 1;
     g_conv_s2 = (halo & 512) ? 0 : 1;
     g_conv_ws2 = (halo & 1024) ? 0 : 1;
+    g_conv_n16 = (halo & 2048) ? 0 : 1;
   }
   return prev;
 }

@@ -58,7 +58,7 @@ def _conv_case(kind, Ci, Co, W, cuda, want_fwd=None, want_dgrad=None, want_wgrad
     the dispatch trace of each direction must contain the expected kernel."""
     from timevqvae.hip.conv import conv2d, conv_transpose2d
     gen = torch.Generator().manual_seed(Ci * 131 + Co * 7 + W)
-    KH, KW = 3, (3 if kind == "res" else 4)
+    KH, KW = (1, 1) if kind == "proj" else (3, (3 if kind == "res" else 4))
     x = torch.randn(B, Ci, 3, W, generator=gen)
     wshape = (Ci, Co, KH, KW) if kind == "convt" else (Co, Ci, KH, KW)
     w = torch.randn(*wshape, generator=gen) * (Ci * KH * KW) ** -0.5
@@ -66,6 +66,8 @@ def _conv_case(kind, Ci, Co, W, cuda, want_fwd=None, want_dgrad=None, want_wgrad
     xc, wc, bc = (t.clone().requires_grad_(True) for t in (x, w, b))
     if kind == "res":
         yc = F.conv2d(xc, wc, bc, padding=(1, 1))
+    elif kind == "proj":
+        yc = F.conv2d(xc, wc, bc)
     elif kind == "enc":
         yc = F.conv2d(F.pad(xc, (1, 1, 1, 1), mode="replicate"), wc, bc, stride=(1, 2))
     else:
@@ -77,7 +79,7 @@ def _conv_case(kind, Ci, Co, W, cuda, want_fwd=None, want_dgrad=None, want_wgrad
         if kind == "convt":
             yd = conv_transpose2d(xd, wd, bd)
         else:
-            yd = conv2d(xd, wd, bd, stride_w=1 if kind == "res" else 2, replicate=kind == "enc")
+            yd = conv2d(xd, wd, bd, stride_w=2 if kind == "enc" else 1, replicate=kind == "enc")
         torch.cuda.synchronize()
     with _trace() as tb:
         yd.backward(g.to(cuda))
@@ -103,6 +105,21 @@ def test_conv_128_to_16_dgrad_on_t32_bk16(cuda):
     """HF decoder ResBlock(128 -> 16) conv on (256, 128, 3, 32): its data gradient gathers
     16 channels into 128 on the same tile."""
     _conv_case("res", 128, 16, 32, cuda, want_dgrad="conv_t32 bk16")
+
+
+@pytest.mark.parametrize("kind", ["res", "proj"])
+def test_conv_128_to_16_on_n16(kind, cuda):
+    """HF decoder ResBlock(128 -> 16): its 3x3 conv1 and 1x1 projection forward on
+    (256, 128, 3, 32) take the few-output wide-input kernel (conv_n16_kernel, one image per
+    block, tap-major reduction from LDS halo planes)."""
+    _conv_case(kind, 128, 16, 32, cuda, want_fwd="conv_n16 k%s mode0" % ("3x3" if kind == "res" else "1x1"))
+
+
+@pytest.mark.parametrize("kind", ["res", "proj"])
+def test_conv_16_to_128_dgrad_on_n16(kind, cuda):
+    """HF encoder ResBlock(16 -> 128): the data gradients of its 3x3 conv1 and 1x1 projection
+    (128 -> 16 gathers, flipped taps) on conv_n16_kernel."""
+    _conv_case(kind, 16, 128, 32, cuda, want_dgrad="conv_n16 k%s mode1" % ("3x3" if kind == "res" else "1x1"))
 
 
 # the band-end stride-2 small-channel convs at B=256 (EncBlocks: input width; ConvT: input
