@@ -1912,10 +1912,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(const float* __res
 constexpr int W8_IMG = 16;
 
 template <int W, int CB>
-__global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restrict__ G,
-                                                           const float* __restrict__ X,
-                                                           float* __restrict__ slab, int B, int C,
-                                                           int N, int kcols, int PS) {
+__global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restrict__ G0,
+                                                           const float* __restrict__ X0,
+                                                           float* __restrict__ slab0, int B, int C,
+                                                           int N, int kcols, int PS,
+                                                           const float* __restrict__ G1 = nullptr,
+                                                           const float* __restrict__ X1 = nullptr,
+                                                           float* __restrict__ slab1 = nullptr) {
   constexpr int P = 3 * W, WP = W + 2;
   constexpr int GST = P + 4;                         // dY row stride in LDS (16-B aligned)
   constexpr int KB = CB * 9 + 1, KT = (KB + 15) / 16;  // columns (+ bias), 16-col tiles
@@ -1925,7 +1928,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restr
   float* Hs = smem + W8_IMG * 32 * GST;              // [IMG][CB + 1][PS] (plane CB: ones)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 15, kq = lane >> 4;
-  const int s = blockIdx.x, n0 = blockIdx.y * 32, c0 = blockIdx.z * CB;
+  // a pair launch (conv_wgrad_w8_pair) stacks a second problem of the same shape on the
+  // upper half of blockIdx.y
+  const int nty = (N + 31) / 32, pb = (int)blockIdx.y >= nty;
+  const float* __restrict__ G = pb ? G1 : G0;
+  const float* __restrict__ X = pb ? X1 : X0;
+  float* __restrict__ slab = pb ? slab1 : slab0;
+  const int s = blockIdx.x, n0 = ((int)blockIdx.y - pb * nty) * 32, c0 = blockIdx.z * CB;
   const bool bias = c0 + CB >= C && kcols > C * 9;   // this block also owns the bias column
   const int b0 = s * W8_IMG;
   const int ni = min(W8_IMG, B - b0);
@@ -2047,6 +2056,13 @@ static int64_t w8_ws(int64_t B, int64_t N, int64_t C) {
   const int64_t S = B / W8_IMG, kc = C * 9 + 1;
   return S * N * kc + reduce_rows_scratch(S, N * kc);
 }
+
+// Two weight (+ bias) gradients of the same 3x3 shape on (B, C, 3, 8) maps in one launch:
+// the fused LF ResBlock's conv1 and conv2 (tvq_resblock_w8.hip).  Each problem's slab goes
+// to its own workspace (w8_ws floats) and its own ordered sum.
+static void w8_pair_launch(const float* x0, const float* dy0, float* ws0, float* dw0, float* db0,
+                           const float* x1, const float* dy1, float* ws1, float* dw1, float* db1,
+                           int64_t B, int64_t C, int64_t N, int accumulate, hipStream_t st);
 
 // ---------------------------------------------------------------- wide-map weight gradient
 // Weight (+ bias) gradient of stride-1 "same" 3x3 / 1x3 convs on maps whose rows are a
@@ -3734,6 +3750,35 @@ void tvq::conv_wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, f
 
 // Conv2d weight (+bias) gradient: dW[co,ci,kh,kw] (+)= sum dY[b,co,h,wo] X[b,ci,h+kh-PH, wo*SW+kw-PW],
 // db[co] (+)= sum dY[b,co,h,wo] (db may be NULL)
+namespace tvq {
+static void w8_pair_launch(const float* x0, const float* dy0, float* ws0, float* dw0, float* db0,
+                           const float* x1, const float* dy1, float* ws1, float* dw1, float* db1,
+                           int64_t B, int64_t C, int64_t N, int accumulate, hipStream_t st) {
+  const int S = (int)(B / W8_IMG);
+  const int PS = whalo_plane_stride(5 * (8 + 2), 9, 3, 8 + 2, 1, 8);
+  const dim3 grid((unsigned)S, (unsigned)(2 * (N / 32)), (unsigned)(C / 8));
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_w8_kernel<8, 8>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    attr = true;
+  }
+  const int kcols = (int)(C * 9 + 1);
+  TVQ_PLAN("conv_wgrad_w8 pair S=%d", S);
+  hipLaunchKernelGGL((conv_wgrad_w8_kernel<8, 8>), grid, dim3(256), (w8_lds<8, 8>(PS)), st, dy0, x0,
+                     ws0, (int)B, (int)C, (int)N, kcols, PS, dy1, x1, ws1);
+  wgrad_finish(ws0, S, N, kcols, dw0, db0, accumulate, st);
+  wgrad_finish(ws1, S, N, kcols, dw1, db1, accumulate, st);
+}
+bool conv_wgrad_w8_pair(const float* x0, const float* dy0, float* ws0, float* dw0, float* db0,
+                        const float* x1, const float* dy1, float* ws1, float* dw1, float* db1,
+                        int64_t B, int64_t C, int64_t N, int accumulate, hipStream_t st) {
+  if (!w8_fits(B, C, 3, 8, N, 8, 3, 3, 1, 0)) return false;
+  w8_pair_launch(x0, dy0, ws0, dw0, db0, x1, dy1, ws1, dw1, db1, B, C, N, accumulate, st);
+  return true;
+}
+}  // namespace tvq
+
 extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
                                 const float* dy, int64_t Co, int64_t Wo, int64_t KH, int64_t KW,
                                 int64_t SW, int64_t replicate, float* dw, float* db,

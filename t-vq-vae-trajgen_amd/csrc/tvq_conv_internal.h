@@ -20,4 +20,10 @@ void param_rows_finish(const float* in, int64_t P, int64_t N, float* out, int ac
 // returned pointer's strides (n, c, tap) go to *sn, *sc, *st.
 const float* conv_pack_view(const float* w, int N, int C, int KK, int64_t wsn, int64_t wsc,
                             float* ws, hipStream_t st, int64_t* sn, int64_t* sc, int64_t* stp);
+// Two 3x3 weight (+ bias) gradients of one (B, C, 3, 8) -> N shape in one launch (the fused LF
+// ResBlock's pair); false (nothing launched) when the shape is not conv_wgrad_w8's.
+// ws0 / ws1: tvq_conv_workspace(4, ...) floats each, alive until the deferral scope's flush.
+bool conv_wgrad_w8_pair(const float* x0, const float* dy0, float* ws0, float* dw0, float* db0,
+                        const float* x1, const float* dy1, float* ws1, float* dw1, float* db1,
+                        int64_t B, int64_t C, int64_t N, int accumulate, hipStream_t st);
 }  // namespace tvq

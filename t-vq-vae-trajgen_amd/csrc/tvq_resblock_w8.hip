@@ -28,7 +28,7 @@
 // Reducing the 256 images' partials in every consumer block (as the small-channel kernels
 // do) read 256 KB of partials per block and held them in 128 VGPRs: 24 us per fwd2 / bwd1
 // launch (round 5); the one-wave-per-channel finish launch is ~3 us.
-//   weight gradients: tvq_conv2d_wgrad on (s2, g2) and (s1, dh) -- the image-batched
+//   weight gradients: (s2, g2) and (s1, dh) in one launch of the image-batched
 //            conv_wgrad_w8 kernel (a 64 x 577 slab row per image would be 148 KB)
 //   w8_eval  both convs in one launch with BN from the running statistics (the frozen
 //            encoder of stage2, the LF decoder while sampling)
@@ -558,20 +558,23 @@ int w8_bwd(const float* dy, const float* x, const float* saved, int64_t B, const
   hipLaunchKernelGGL(w8_bwd2_kernel, dim3((unsigned)B), dim3(T), LDS, st, a);
   int rc = launch_status("tvq_resblock_bwd");
   if (rc) return rc;
-  // conv2's weight gradient from (s2, g2) while the next kernel waits on nothing of it
   // per-image partials -> the BN backward coefficients, BN weight / bias and Snake a2 gradients
   bn_bwd_final_launch(a.part, a.bfin, st);
-  rc = tvq_conv2d_wgrad(s2, B, C, 3, W, g2, C, W, 3, 3, 1, 0, dw2, db2, accumulate,
-                        (float*)(ws + L.wg2), st);
-  if (rc) return rc;
   TVQ_PLAN("w8_bwd1 C%d W%d B%lld", C, W, (long long)B);
   a.g_out = dh; a.slabda = slabda1;
   hipLaunchKernelGGL(w8_bwd1_kernel, dim3((unsigned)B), dim3(T), LDS, st, a);
   rc = launch_status("tvq_resblock_bwd");
   if (rc) return rc;
-  rc = tvq_conv2d_wgrad(s1, B, C, 3, W, dh, C, W, 3, 3, 1, 0, dw1, db1, accumulate,
-                        (float*)(ws + L.wg1), st);
-  if (rc) return rc;
+  // both convs' weight gradients, (s2, g2) and (s1, dh), in one launch
+  if (!conv_wgrad_w8_pair(s2, g2, (float*)(ws + L.wg2), dw2, db2, s1, dh, (float*)(ws + L.wg1),
+                          dw1, db1, B, C, C, (int)accumulate, st)) {
+    rc = tvq_conv2d_wgrad(s2, B, C, 3, W, g2, C, W, 3, 3, 1, 0, dw2, db2, accumulate,
+                          (float*)(ws + L.wg2), st);
+    if (rc) return rc;
+    rc = tvq_conv2d_wgrad(s1, B, C, 3, W, dh, C, W, 3, 3, 1, 0, dw1, db1, accumulate,
+                          (float*)(ws + L.wg1), st);
+    if (rc) return rc;
+  }
   conv_wgrad_finish(slabda1, (int)B, C, 1, da1, nullptr, (int)accumulate, st);
   return launch_status("tvq_resblock_bwd");
 }
