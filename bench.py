@@ -424,7 +424,7 @@ HBM_PEAK_GBS = 8000.0
 
 # PMC evidence of the roofline legs: profiles/<PROFILE_TAG>_<leg>_traffic.json, written by
 # tools/gpu_roofline.sh + tools/roof_traffic.py on the tree named in its "tree" field
-PROFILE_TAG = "r04"
+PROFILE_TAG = "r05"
 
 
 def _traffic(leg):
@@ -699,6 +699,121 @@ def linear_fwd_leg(device):
             "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, "linfwd")
 
 
+def attn_branch_leg(device):
+    """The LF prior's fused attention branch forward (csrc/tvq_xattn.hip, round 5; reference
+    bidirectional_transformer.py:92-110): RMSNorm + QKV + 2-head softmax attention (dropout
+    0.3) + gated out-projection + residual for 256 sequences of 25 tokens, one launch.
+    Algorithmic work: QKV 2*6400*128*384 + scores and P V 2 heads * 256 * 2 * (2*25*25*64) +
+    out-projection 2*6400*128*128 = 920.6 MFLOP; bytes: x read, the 4 weights read, y, xn,
+    qkv, o written (+ inv, lse) = 23.4 MB (AI 39 FLOP/B: fp32 MFMA bound).  50 graph-replayed
+    launches timed with HIP events on their stream."""
+    import math
+    from timevqvae.hip import rng
+    from timevqvae.hip._native import call, ptr, stream_ptr
+    B, S, D = 256, 25, 128
+    M = B * S
+    g = torch.Generator(device="cpu").manual_seed(11)
+    rnd = lambda *sh, s=1.0: (torch.randn(*sh, generator=g) * s).to(device)  # noqa: E731
+    x, W, Wo, gn = rnd(M, D), rnd(3 * D, D, s=0.08), rnd(D, D, s=0.08), 1 + rnd(D, s=0.1)
+    gate = torch.ones(1, device=device)
+    seed = rng.seed_tensor(device)
+    y, xn, o = (torch.empty(M, D, device=device) for _ in range(3))
+    inv = torch.empty(M, device=device)
+    qkv = torch.empty(M, 3 * D, device=device)
+    lse = torch.empty(B * 2 * S, device=device)
+    fn = (lambda: call("tvq_attn_branch_fwd", ptr(x), B, S, D, 2, ptr(gn), math.sqrt(D), ptr(W),
+                       ptr(Wo), ptr(gate), 0.3, ptr(seed), 0, ptr(y), ptr(xn), ptr(inv), ptr(qkv),
+                       ptr(o), ptr(lse), stream_ptr()))
+    with torch.no_grad():
+        us = _graph_time_us([fn], 50)
+    flops = 2.0 * M * D * 3 * D + 2 * B * 2 * (2 * S * S * 64) + 2.0 * M * D * D
+    byts = 4.0 * (M * D + 4 * D * D + D + 3 * M * D + 3 * M * D + M + B * 2 * S)
+    tf = flops / (us * 1e-6) / 1e12
+    return _with_traffic({"bound": "mfma", "kernel": "xattn_fwd_kernel: fused LF prior attention "
+                                       "branch (RMSNorm + QKV + attention + gated out-projection"
+                                       " + residual), 256 x 25 tokens, 32x32x2 fp32 MFMA",
+            "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4),
+            "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, "attn")
+
+
+def conv_n16_leg(device):
+    """The HF decoder ResBlock(128 -> 16)'s 3x3 conv on (256, 128, 3, 32) on the few-output
+    wide-input kernel (conv_n16_kernel, round 5): 2 * 24576 * 16 * 1152 = 906.0 MFLOP;
+    bytes: input 12.58 MB read + output 1.57 MB written + weight = 14.2 MB (AI 64 FLOP/B).
+    50 graph-replayed launches inside a pack-cache scope (the weight packed once, as in the
+    step) timed with HIP events."""
+    from timevqvae.hip._native import call, ptr, stream_ptr, value
+    B, C, H, W, N = 256, 128, 3, 32, 16
+    g = torch.Generator(device="cpu").manual_seed(12)
+    x = torch.randn(B, C, H, W, generator=g).to(device)
+    w = (torch.randn(N, C, 3, 3, generator=g) * 0.03).to(device)
+    b = torch.zeros(N, device=device)
+    y = torch.empty(B, N, H, W, device=device)
+    ws = torch.empty(value("tvq_conv_workspace", 0, B, C, H, W, N, 3, 3, 1, 0), device=device)
+    fn = (lambda: call("tvq_conv2d_fwd", ptr(x), B, C, H, W, ptr(w), ptr(b), N, 3, 3, 1, 0, ptr(y),
+                       None, 0.0, None, 0, ptr(ws), stream_ptr()))
+    from timevqvae.hip.conv import PackCache
+    cache = PackCache(device, floats=1 << 20)
+    with torch.no_grad(), cache.scope():
+        us = _graph_time_us([fn], 50)
+    flops = 2.0 * B * H * W * N * C * 9
+    byts = 4.0 * (B * C * H * W + B * N * H * W + N * C * 9)
+    tf = flops / (us * 1e-6) / 1e12
+    return _with_traffic({"bound": "mfma", "kernel": "conv_n16_kernel<F,3,3>: HF 128->16 3x3 conv "
+                                       "on (256,128,3,32), one image per 8-wave block, 16x16x4 "
+                                       "fp32 MFMA (weight packed once by the pack cache)",
+            "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4),
+            "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, "n16")
+
+
+def rb64_fwd_leg(device):
+    """The LF band's fused ResBlock(64, 64) training forward on (256, 64, 3, 8)
+    (csrc/tvq_resblock_w8.hip, round 5; vq_vae.py:13-62): w8_fwd1 + the BN finish +
+    w8_fwd2 (3 launches; the weights packed once by a pack-cache scope).  Algorithmic work: two 3x3 convs 2 * 2*6144*64*576 = 906.0 MFLOP;
+    bytes: x read, y written, h / Snake_a1(x) / Snake_a2(BN(h)) written for the backward and
+    both weights read = 4 * (5 * 393216 + 2 * 36928) = 8.16 MB.  50 graph-replayed ops."""
+    from timevqvae.hip import rng
+    from timevqvae.hip._native import call, ptr, stream_ptr, value
+    B, C, H, W = 256, 64, 3, 8
+    g = torch.Generator(device="cpu").manual_seed(13)
+    x = torch.randn(B, C, H, W, generator=g).to(device)
+    a1 = (0.2 + 0.3 * torch.rand(C, generator=g)).to(device)
+    a2 = (0.2 + 0.3 * torch.rand(C, generator=g)).to(device)
+    w1 = (torch.randn(C, C, 3, 3, generator=g) * 0.04).to(device)
+    w2 = (torch.randn(C, C, 3, 3, generator=g) * 0.04).to(device)
+    b1, b2 = torch.zeros(C, device=device), torch.zeros(C, device=device)
+    bw, bb = torch.ones(C, device=device), torch.zeros(C, device=device)
+    rm, rv = torch.zeros(C, device=device), torch.ones(C, device=device)
+    nbt = torch.zeros((), dtype=torch.int64, device=device)
+    h = torch.empty(value("tvq_resblock_saved_floats", B, C, H, W), device=device)
+    y = torch.empty_like(x)
+    save = torch.empty(4 * C, device=device)
+    ws = torch.empty(value("tvq_resblock_workspace", B, C, H, W), device=device, dtype=torch.uint8)
+    seed = rng.seed_tensor(device)
+    fn = (lambda: call("tvq_resblock_train_fwd", ptr(x), B, C, H, W, ptr(a1), ptr(w1), ptr(b1),
+                       ptr(bw), ptr(bb), ptr(rm), ptr(rv), ptr(nbt), 0.1, 1e-5, ptr(a2), ptr(w2),
+                       ptr(b2), 0.3, ptr(seed), 0, ptr(h), ptr(y), ptr(save), ptr(ws), stream_ptr()))
+    from timevqvae.hip.conv import PackCache
+    cache = PackCache(device, floats=1 << 20)
+    with torch.no_grad(), cache.scope():  # the weights packed once, as in the step
+        us = _graph_time_us([fn], 50)
+    flops = 2.0 * (2.0 * B * H * W * C * 9 * C)
+    byts = 4.0 * (5 * B * C * H * W + 2 * (C * C * 9 + C))
+    tf = flops / (us * 1e-6) / 1e12
+    return _with_traffic({"bound": "mfma", "kernel": "w8_fwd1_kernel + bn_stats_final_kernel + "
+                                       "w8_fwd2_kernel: fused LF ResBlock(64,64) training forward "
+                                       "on (256,64,3,8), one image per 8-wave block, weights from "
+                                       "L2, 32x32x2 fp32 MFMA",
+            "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "launches_per_op": 3,
+            "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, "rb64")
+
+
 def roofline_leg(device, ms_per_step):
     """bench JSON `roofline`: the step's top kernel by summed time, the grouped Linear
     weight gradients of the LF prior (dominant_leg), at top level (also under
@@ -720,6 +835,9 @@ def roofline_leg(device, ms_per_step):
     out["step_frac"] = out["step"]["frac"]
     out["cu_weighted"] = cu_weighted_leg()
     out["conv_t32"] = conv_t32_leg(device)
+    out["attn_branch"] = attn_branch_leg(device)
+    out["conv_n16"] = conv_n16_leg(device)
+    out["rb64_fwd"] = rb64_fwd_leg(device)
     return out
 
 

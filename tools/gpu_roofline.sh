@@ -30,4 +30,13 @@ fi
 if [ "$LEG" = t32 ]; then
   python tools/roof_traffic.py $O $O/traffic.json "HF ResBlock 128->128 3x3 conv on (256,128,3,32): conv_t32_kernel (pack-cached weights)" conv_t32_kernel
 fi
+if [ "$LEG" = attn ]; then
+  python tools/roof_traffic.py $O $O/traffic.json "fused LF prior attention branch forward, 256 x 25 tokens: xattn_fwd_kernel" xattn_fwd_kernel
+fi
+if [ "$LEG" = n16 ]; then
+  python tools/roof_traffic.py $O $O/traffic.json "HF 128->16 3x3 conv on (256,128,3,32): conv_n16_kernel" conv_n16_kernel
+fi
+if [ "$LEG" = rb64 ]; then
+  python tools/roof_traffic.py $O $O/traffic.json "fused LF ResBlock(64,64) training forward on (256,64,3,8): w8_fwd1 + bn_stats_final + w8_fwd2" w8_fwd1_kernel bn_stats_final_kernel w8_fwd2_kernel
+fi
 echo roofline-done
