@@ -374,6 +374,15 @@ int tvq_wgrad_group(int64_t n, const float* const* dY, const int64_t* ldy, const
                     const int64_t* ldx, float* const* dW, const int64_t* ldw, const int64_t* M,
                     const int64_t* N, const int64_t* K, int64_t accumulate, float* workspace,
                     tvq_stream_t stream);
+/* The same with each layer's bias gradient in the same launch pair (replaces one column-sum
+ * launch per Linear, bias_grad_rows / tvq_channel_sum): dB_i[m] (+)= sum_k dY_i[k*ldy_i + m]
+ * for the i with dB_i != NULL (dB: host array of n device pointers, entries may be NULL;
+ * dB itself may be NULL).  Fixed order: run-to-run bitwise identical. */
+int tvq_wgrad_group_bias(int64_t n, const float* const* dY, const int64_t* ldy,
+                         const float* const* X, const int64_t* ldx, float* const* dW,
+                         const int64_t* ldw, float* const* dB, const int64_t* M, const int64_t* N,
+                         const int64_t* K, int64_t accumulate, float* workspace,
+                         tvq_stream_t stream);
 
 /* ------------------------------------------------------ losses, optimizer
  * F.mse_loss (kind 0) / F.l1_loss (kind 1) means (stage1.py:129,133); backward

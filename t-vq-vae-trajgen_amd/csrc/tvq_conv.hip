@@ -2444,15 +2444,16 @@ struct PackCacheState {
 static std::map<int64_t, PackCacheState> g_pcs;
 static PackCacheState* g_pc_cur = nullptr;  // the open scope's cache (null: no scope)
 static int64_t g_pc_last = -1;              // id of the last scope (entries query)
-// deferred weight-gradient split sums (see wgrad_finish)
-static std::vector<RrJob> g_rd;
+// deferred weight-gradient split sums (see wgrad_finish), each with the stream its producer
+// ran on: the flush issues each stream's records as one batch on that stream (ordered after
+// that stream's producers), so a backward spread over several streams (a branch's side
+// stream) defers its reductions too
+struct RdRec {
+  RrJob job;
+  hipStream_t st;
+};
+static std::vector<RdRec> g_rd;
 static bool g_rd_on = false, g_rd_paused = false;
-// the scope's stream (tvq_wgrad_defer_begin_stream): only reductions issued on it are
-// recorded, the others run at once (a flush on one stream orders after that stream's
-// producers only); g_rd_any: the plain begin() records every stream's reductions (the caller
-// flushes on the stream they were all issued on)
-static hipStream_t g_rd_st = nullptr;
-static bool g_rd_any = true;
 
 constexpr int PACK_BATCH = 24;
 struct PackBatch {
@@ -3387,17 +3388,13 @@ extern "C" int tvq_conv_wgrad_defer_begin(void) {
   TVQ_CHECK_ARG(!g_rd_on, "tvq_conv_wgrad_defer_begin: a scope is already open");
   g_rd.clear();
   g_rd_on = true;
-  g_rd_any = true;
   return TVQ_OK;
 }
 
+// kept for the ABI: every record now carries its own stream, so this is begin()
 extern "C" int tvq_wgrad_defer_begin_stream(tvq_stream_t stream) {
-  TVQ_CHECK_ARG(!g_rd_on, "tvq_wgrad_defer_begin_stream: a scope is already open");
-  g_rd.clear();
-  g_rd_on = true;
-  g_rd_any = false;
-  g_rd_st = (hipStream_t)stream;
-  return TVQ_OK;
+  (void)stream;
+  return tvq_conv_wgrad_defer_begin();
 }
 
 extern "C" int tvq_conv_wgrad_defer_pause(int64_t paused) {
@@ -3408,8 +3405,20 @@ extern "C" int tvq_conv_wgrad_defer_pause(int64_t paused) {
 extern "C" int tvq_conv_wgrad_defer_flush(tvq_stream_t stream) {
   g_rd_on = false;
   g_rd_paused = false;
-  if (!g_rd.empty()) reduce_rows_batch(g_rd.data(), (int)g_rd.size(), (hipStream_t)stream);
-  g_rd.clear();
+  // one batch per producing stream, in first-record order ((void)stream: kept for the ABI)
+  (void)stream;
+  std::vector<RrJob> jobs;
+  while (!g_rd.empty()) {
+    const hipStream_t st = g_rd.front().st;
+    jobs.clear();
+    std::vector<RdRec> rest;
+    for (const RdRec& r : g_rd) {
+      if (r.st == st) jobs.push_back(r.job);
+      else rest.push_back(r);
+    }
+    reduce_rows_batch(jobs.data(), (int)jobs.size(), st);
+    g_rd.swap(rest);
+  }
   return launch_status("tvq_conv_wgrad_defer_flush");
 }
 
@@ -3715,8 +3724,8 @@ extern "C" int64_t tvq_conv_workspace(int64_t op, int64_t B, int64_t Ci, int64_t
 // slabs' reductions are recorded and run by a few batched launches at the flush instead
 // of one launch per conv (the caller keeps the workspaces alive until then).
 
-static bool rd_records(int64_t rows, hipStream_t st) {
-  return g_rd_on && !g_rd_paused && rows <= RR_ONE_ROWS && (g_rd_any || st == g_rd_st);
+static bool rd_records(int64_t rows) {
+  return g_rd_on && !g_rd_paused && rows <= RR_ONE_ROWS;
 }
 
 static void wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, float* dw,
@@ -3724,8 +3733,8 @@ static void wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, floa
   // deterministic split sum; kcols = Kred+1 splits out the bias column.  The level-1
   // scratch follows the slab in the workspace.
   const int64_t L = kcols > 0 && db ? kcols : 0;
-  if (rd_records(splits, st)) {  // the single-level case: batched at the flush
-    g_rd.push_back({slab, dw, db, splits, N * kcols, L, accumulate});
+  if (rd_records(splits)) {  // the single-level case: batched at the flush
+    g_rd.push_back({{slab, dw, db, splits, N * kcols, L, accumulate}, st});
     return;
   }
   reduce_rows(slab, splits, N * kcols, N * kcols, dw, db, L, accumulate,
@@ -3736,8 +3745,8 @@ static void wgrad_finish(float* slab, int splits, int64_t N, int64_t kcols, floa
 // optimizer reads): joins the open deferral scope's batch, else reduce_rows now
 void tvq::param_rows_finish(const float* in, int64_t P, int64_t N, float* out, int accumulate,
                             float* scratch, hipStream_t st) {
-  if (rd_records(P, st)) {
-    g_rd.push_back({in, out, nullptr, P, N, 0, accumulate});
+  if (rd_records(P)) {
+    g_rd.push_back({{in, out, nullptr, P, N, 0, accumulate}, st});
     return;
   }
   reduce_rows(in, P, N, N, out, nullptr, 0, accumulate, scratch, st);

@@ -117,22 +117,42 @@ void reduce_rows(const float* in, int64_t P, int64_t N, int64_t ld, float* out, 
                        out, out2, L, accumulate, 1, nullptr, nullptr);
 }
 
-// Batched single-level column sums: blockIdx.x runs over the jobs' column blocks (cb0 =
-// prefix of column-block counts); each block is exactly reduce_rows_kernel's direct path.
-constexpr int RR_BATCH = 24;
+// Batched single-level column sums: blockIdx.x runs over the jobs' column blocks (each job
+// takes ceil(N / cols) consecutive blocks, found by a scalar scan of the job list); each
+// block is exactly reduce_rows_kernel's direct path.  Up to RR_BATCH jobs per launch (the
+// band-end batch of a stage1 band is ~80 slabs: one launch, was four of 24).
+constexpr int RR_BATCH = 96;
+struct RrJobK {  // 40 bytes: RR_BATCH of them stay inside a 4 KB kernel-argument block
+  const float* in;
+  float* out;
+  float* out2;
+  int P, N, L, accumulate;
+};
 struct RrBatch {
-  RrJob job[RR_BATCH];
-  int cb0[RR_BATCH + 1];
+  RrJobK job[RR_BATCH];
   int n;
 };
+static_assert(sizeof(RrBatch) <= 3900, "reduce_rows batch kernel arguments");
+
+// the job of block `blk` and its first block (wave-uniform scan)
+__device__ __forceinline__ int rr_job_of(const RrBatch& b, int blk, int cols, int& first) {
+  int j = 0, b0 = 0;
+  for (; j + 1 < b.n; ++j) {
+    const int nb = (b.job[j].N + cols - 1) / cols;
+    if (blk < b0 + nb) break;
+    b0 += nb;
+  }
+  first = b0;
+  return j;
+}
 
 __global__ __launch_bounds__(256) void reduce_rows_batch_kernel(RrBatch b) {
   __shared__ float sh[RR_GROUPS][RR_COLS];
-  int j = 0;
-  while (j + 1 < b.n && (int)blockIdx.x >= b.cb0[j + 1]) ++j;
-  const RrJob& jb = b.job[j];
+  int first;
+  const int j = rr_job_of(b, (int)blockIdx.x, RR_COLS, first);
+  const RrJobK& jb = b.job[j];
   const int c = threadIdx.x % RR_COLS, g = threadIdx.x / RR_COLS;
-  const int64_t col = (int64_t)(blockIdx.x - b.cb0[j]) * RR_COLS + c;
+  const int64_t col = (int64_t)(blockIdx.x - first) * RR_COLS + c;
   const float t = rr_colsum<false>(jb.in, 0, jb.P, jb.N, col, jb.N, sh, c, g);
   if (g == 0 && col < jb.N) rr_store(t, col, jb.out, jb.out2, jb.L, jb.accumulate);
 }
@@ -144,11 +164,11 @@ __global__ __launch_bounds__(256) void reduce_rows_batch_kernel(RrBatch b) {
 // instructions (the band-end batch of the conv weight-gradient slabs reads 140-200 MB).
 __global__ __launch_bounds__(256) void reduce_rows_batch4_kernel(RrBatch b) {
   __shared__ float4 sh[RR_GROUPS][RR_COLS];
-  int j = 0;
-  while (j + 1 < b.n && (int)blockIdx.x >= b.cb0[j + 1]) ++j;
-  const RrJob& jb = b.job[j];
+  int first;
+  const int j = rr_job_of(b, (int)blockIdx.x, 4 * RR_COLS, first);
+  const RrJobK& jb = b.job[j];
   const int c = threadIdx.x % RR_COLS, g = threadIdx.x / RR_COLS;
-  const int64_t col = ((int64_t)(blockIdx.x - b.cb0[j]) * RR_COLS + c) * 4;
+  const int64_t col = ((int64_t)(blockIdx.x - first) * RR_COLS + c) * 4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (col < jb.N) {
     const float* in = jb.in + col;
@@ -192,16 +212,17 @@ void reduce_rows_batch(const RrJob* jobs, int n, hipStream_t st) {
       if (k == 0) return;
       RrBatch b;
       b.n = k;
-      b.cb0[0] = 0;
       const int cols = wide ? 4 * RR_COLS : RR_COLS;
+      int blocks = 0;
       for (int i = 0; i < k; ++i) {
-        b.job[i] = sel[i];
-        b.cb0[i + 1] = b.cb0[i] + (int)((sel[i].N + cols - 1) / cols);
+        b.job[i] = {sel[i].in, sel[i].out, sel[i].out2, (int)sel[i].P, (int)sel[i].N,
+                    (int)sel[i].L, sel[i].accumulate};
+        blocks += (int)((sel[i].N + cols - 1) / cols);
       }
       if (wide)
-        hipLaunchKernelGGL(reduce_rows_batch4_kernel, dim3((unsigned)b.cb0[k]), dim3(256), 0, st, b);
+        hipLaunchKernelGGL(reduce_rows_batch4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b);
       else
-        hipLaunchKernelGGL(reduce_rows_batch_kernel, dim3((unsigned)b.cb0[k]), dim3(256), 0, st, b);
+        hipLaunchKernelGGL(reduce_rows_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b);
       k = 0;
     };
     for (int i = 0; i < n; ++i) {

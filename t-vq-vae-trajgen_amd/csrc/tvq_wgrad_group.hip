@@ -23,6 +23,12 @@
 // records the same way whatever the streams (timevqvae.hip.wgrad tags).  Every sum has a
 // fixed order independent of scheduling: results are run-to-run identical.
 //
+// Bias gradients ride along: a descriptor with a bias output (db_m = sum_k dY(m, k), the
+// Linear's bias gradient) has its n-tile-0 blocks also sum the dY values they already load,
+// in the same fixed order as the tile (steps in order, then the two lane halves, then the
+// waves (w0 + w2) + (w1 + w3)), into a per-split bias slab that the reduce launch sums;
+// no separate column-sum launch per Linear.
+//
 // XCD map: block b runs on XCD b % 8; logical index L = (b % 8) * per + b / 8 walks
 // (descriptor, split, tile), so one XCD holds whole splits: a split's dY / X token rows
 // are fetched into one L2 and re-read from it by every tile of that split.
@@ -40,6 +46,7 @@ struct WgDesc {
   const float* A;  // dY: A(m, k) = A[k * lda + m]   (m = output feature, k = token)
   const float* B;  // X:  B(k, n) = B[k * ldb + n]   (n = input feature)
   float* C;        // dW: C[m * ldc + n]
+  float* Cb;       // optional db: Cb[m] (+)= sum_k A(m, k)
   int lda, ldb, ldc;
   int M, N, K;
   int kper;        // k span of one split (multiple of 8 KC)
@@ -47,15 +54,44 @@ struct WgDesc {
   int tiles, tiles_n;
   int blk0;        // first logical block of this descriptor (tiles * S of them)
   int rb0;         // first block of this descriptor in the reduce launch
+  int rbb0;        // first block of its bias sum in the reduce launch
   int accumulate;  // C += result
   int64_t slab;    // its S slabs of M x N partials in the workspace
+  int64_t bslab;   // its S bias slabs of M partials (Cb, S > 1)
 };
 
 struct WgGroup {
   WgDesc d[WG_MAXD];
   float* ws;
   int n, per, blocks;
+  int rbias;  // first bias block of the reduce launch
 };
+
+// the bias partial of a block: per-lane sums v[i] of rows m0 + row(i, lane) over this
+// wave's steps -> the two lane halves (h = 0, 1) -> the waves (w0 + w2) + (w1 + w3) -> the
+// split's slab row (S > 1) or Cb (+)=.  ROWS: rows per tile; row(i, lane) as the caller's.
+template <int NV, int ROWS, typename RowOf>
+__device__ __forceinline__ void wg_bias_store(const WgGroup& G, const WgDesc& d, int z, int m0,
+                                             const float (&v)[NV], RowOf row_of, float* bred) {
+  const int tid = (int)threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float t = v[i] + __shfl_xor(v[i], 32);  // h0 + h1 (commutative: same in both)
+    if (lane < 32) bred[wid * ROWS + row_of(i, lane)] = t;
+  }
+  __syncthreads();
+  for (int r = tid; r < ROWS; r += 256) {
+    const int m = m0 + r;
+    if (m >= d.M) continue;
+    const float s = (bred[r] + bred[2 * ROWS + r]) + (bred[ROWS + r] + bred[3 * ROWS + r]);
+    if (d.S > 1) {
+      G.ws[d.bslab + (int64_t)z * d.M + m] = s;
+    } else {
+      float* c = d.Cb + m;
+      *c = d.accumulate ? s + *c : s;
+    }
+  }
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wg_rsrc(const float* p, int64_t floats) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)(floats * 4), 0x00020000);
@@ -70,6 +106,7 @@ template <int TW, int KC>
 __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(WgGroup G) {
   constexpr int WSZ = TW * TW * 16 * 64;  // one wave's partial tile in LDS
   __shared__ float red[4 * WSZ];
+  __shared__ float bred[4 * 32 * TW];
   const int b = (int)blockIdx.x;
   const int L = (b & 7) * G.per + (b >> 3);
   if (L >= G.blocks) return;  // padding block of the XCD map (whole block)
@@ -99,12 +136,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(WgGroup G) {
     vb[i] = (h * ldb + min(n0 + 32 * i + r32, d.N - 1)) * 4;
   }
   floatx16 acc[TW][TW];
+  float bs[TW];  // bias partials (used by n-tile-0 blocks of a descriptor with Cb)
 #pragma unroll
-  for (int i = 0; i < TW; ++i)
+  for (int i = 0; i < TW; ++i) {
+    bs[i] = 0.f;
 #pragma unroll
     for (int j = 0; j < TW; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  }
 
   // step s: this lane's k = kb + 2 s + h; past ke: A zeroed by a select.  The chunk loop
   // has no data-dependent branch: the next chunk's loads are always in flight while this
@@ -129,6 +169,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(WgGroup G) {
 #pragma unroll
       for (int i = 0; i < TW; ++i) {
         const float av = ok ? ad[u][i] : 0.f;
+        bs[i] += av;
 #pragma unroll
         for (int j = 0; j < TW; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bd[u][j], acc[i][j], 0, 0, 0);
@@ -151,6 +192,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(WgGroup G) {
     __builtin_amdgcn_sched_barrier(0);
   }
 
+  if (d.Cb && tn == 0)  // block-uniform
+    wg_bias_store<TW, 32 * TW>(G, d, z, m0, bs, [](int i, int ln) { return 32 * i + ln; }, bred);
   // the 4 waves' partial tiles -> LDS; thread e then owns tile elements e, e + 256, ...
   // (row-major, so the global stores coalesce): (w0 + w2) + (w1 + w3), the wide form's order
 #pragma unroll
@@ -191,6 +234,7 @@ template <int KC>
 __global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WgGroup G) {
   constexpr int WSZ = 8 * 16 * 64;  // one wave's partial tile in LDS
   __shared__ float red[2 * WSZ];
+  __shared__ float bred[4 * 128];
   const int b = (int)blockIdx.x;
   const int L = (b & 7) * G.per + (b >> 3);
   if (L >= G.blocks) return;  // padding block of the XCD map (whole block)
@@ -215,6 +259,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WgGroup G) {
   const int va = (h * lda + min(m0 + 4 * r32, d.M - 4)) * 4;
   const int vb = (h * ldb + min(n0 + 2 * r32, d.N - 2)) * 4;
   floatx16 acc[4][2];
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};  // bias partials of rows m0 + 4 r + j
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -239,6 +284,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WgGroup G) {
                            ok ? ad[u].w : 0.f};
       const float bv[2] = {bd[u].x, bd[u].y};
 #pragma unroll
+      for (int j = 0; j < 4; ++j) bs[j] += av[j];
+#pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
@@ -260,6 +307,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WgGroup G) {
     mul(a1, b1, (c + 1) * KC);
     __builtin_amdgcn_sched_barrier(0);
   }
+  if (d.Cb && tn == 0)  // block-uniform
+    wg_bias_store<4, 128>(G, d, z, m0, bs, [](int j, int ln) { return 4 * ln + j; }, bred);
   // (w0 + w2) + (w1 + w3): waves 2, 3 -> LDS, waves 0, 1 add; wave 1 -> LDS, wave 0 adds
   float* slot = red + (wid & 1) * WSZ + lane;
   if (wid >= 2) {
@@ -312,6 +361,20 @@ __global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WgGroup G) {
 // descriptor per block
 __global__ __launch_bounds__(256) void wgrad_group_reduce_kernel(WgGroup G) {
   const int b = (int)blockIdx.x;
+  if (b >= G.rbias) {  // bias slabs: 256 rows of one descriptor's bias per block
+    int di = -1;
+    for (int i = 0; i < G.n; ++i) di = (G.d[i].Cb && G.d[i].S > 1 && G.d[i].rbb0 <= b) ? i : di;
+    if (di < 0) return;
+    const WgDesc& d = G.d[di];
+    const int m = (b - d.rbb0) * 256 + (int)threadIdx.x;
+    if (m >= d.M) return;
+    const float* p = G.ws + d.bslab + m;
+    float s = 0.f;
+    for (int z = 0; z < d.S; ++z) s += p[(int64_t)z * d.M];
+    float* c = d.Cb + m;
+    *c = d.accumulate ? s + *c : s;
+    return;
+  }
   int di = 0;
   for (int i = 1; i < G.n; ++i) di = G.d[i].rb0 <= b ? i : di;
   const WgDesc& d = G.d[di];
@@ -377,13 +440,15 @@ static bool wide_aligned(const float* A, int64_t lda, const float* B, int64_t ld
 }
 
 // an upper bound (the alignment that picks a class is not known here): S <= 64 and
-// S <= ceil(K / 64) for every descriptor
+// S <= ceil(K / 64) for every descriptor; room for a bias slab per descriptor
+static int64_t wg_smax(int64_t K) { return (K + 63) / 64 < 64 ? (K + 63) / 64 : 64; }
+
 extern "C" int64_t tvq_wgrad_group_workspace(int64_t n, const int64_t* M, const int64_t* N,
                                              const int64_t* K) {
   int64_t need = 0;
   for (int64_t i = 0; i < n; ++i) {
-    const int64_t s = (K[i] + 63) / 64 < 64 ? (K[i] + 63) / 64 : 64;
-    if (s > 1) need += s * M[i] * N[i];
+    const int64_t s = wg_smax(K[i]);
+    if (s > 1) need += s * M[i] * (N[i] + 1);
   }
   return need;
 }
@@ -393,6 +458,15 @@ extern "C" int tvq_wgrad_group(int64_t n, const float* const* dY, const int64_t*
                                const int64_t* ldw, const int64_t* M, const int64_t* N,
                                const int64_t* K, int64_t accumulate, float* workspace,
                                tvq_stream_t stream) {
+  return tvq_wgrad_group_bias(n, dY, ldy, X, ldx, dW, ldw, nullptr, M, N, K, accumulate,
+                              workspace, stream);
+}
+
+extern "C" int tvq_wgrad_group_bias(int64_t n, const float* const* dY, const int64_t* ldy,
+                                    const float* const* X, const int64_t* ldx, float* const* dW,
+                                    const int64_t* ldw, float* const* dB, const int64_t* M,
+                                    const int64_t* N, const int64_t* K, int64_t accumulate,
+                                    float* workspace, tvq_stream_t stream) {
   TVQ_CHECK_ARG(n >= 0 && dY && ldy && X && ldx && dW && ldw && M && N && K,
                 "tvq_wgrad_group: bad arguments");
   hipStream_t st = (hipStream_t)stream;
@@ -403,13 +477,19 @@ extern "C" int tvq_wgrad_group(int64_t n, const float* const* dY, const int64_t*
                       M[j] * ldw[j] < ((int64_t)1 << 31),
                   "tvq_wgrad_group: bad descriptor %lld", (long long)j);
   int64_t* slab_of = (int64_t*)alloca(sizeof(int64_t) * (n > 0 ? n : 1));
+  int64_t* bslab_of = (int64_t*)alloca(sizeof(int64_t) * (n > 0 ? n : 1));
   int* cls = (int*)alloca(sizeof(int) * (n > 0 ? n : 1));
   int64_t slab0 = 0;
   for (int64_t j = 0; j < n; ++j) {  // each descriptor's slabs at its workspace-bound offset
     slab_of[j] = slab0;
-    const int64_t s = (K[j] + 63) / 64 < 64 ? (K[j] + 63) / 64 : 64;
+    const int64_t s = wg_smax(K[j]);
     if (s > 1) slab0 += s * M[j] * N[j];
     cls[j] = wg_class(M[j], N[j], wide_aligned(dY[j], ldy[j], X[j], ldx[j]));
+  }
+  for (int64_t j = 0; j < n; ++j) {  // then the bias slabs
+    bslab_of[j] = slab0;
+    const int64_t s = wg_smax(K[j]);
+    if (s > 1) slab0 += s * M[j];
   }
   TVQ_CHECK_ARG(slab0 == 0 || workspace, "tvq_wgrad_group: workspace required");
   // one launch pair per chunk of <= WG_MAXD descriptors of one class, in order on `stream`
@@ -437,6 +517,7 @@ extern "C" int tvq_wgrad_group(int64_t n, const float* const* dY, const int64_t*
         d.A = dY[q];
         d.B = X[q];
         d.C = dW[q];
+        d.Cb = dB ? dB[q] : nullptr;
         d.lda = (int)ldy[q];
         d.ldb = (int)ldx[q];
         d.ldc = (int)ldw[q];
@@ -450,8 +531,15 @@ extern "C" int tvq_wgrad_group(int64_t n, const float* const* dY, const int64_t*
         d.rb0 = rb;
         d.accumulate = (int)accumulate;
         d.slab = slab_of[q];
+        d.bslab = bslab_of[q];
         blk += d.tiles * d.S;
         if (d.S > 1) rb += (int)((M[q] * N[q] + 255) / 256);
+      }
+      G.rbias = rb;
+      for (int i = 0; i < cnt; ++i) {
+        WgDesc& d = G.d[i];
+        d.rbb0 = rb;
+        if (d.Cb && d.S > 1) rb += (d.M + 255) / 256;
       }
       G.blocks = blk;
       G.per = (blk + 7) / 8;

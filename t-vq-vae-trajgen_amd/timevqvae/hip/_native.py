@@ -127,6 +127,7 @@ sig("tvq_gemm_workspace", I64, I64, I64, restype=I64)
 sig("tvq_gemm", P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, F32, P, P, I64, I64, I64, P, I64, P, P, P)
 sig("tvq_wgrad_group_workspace", I64, P, P, P, restype=I64)
 sig("tvq_wgrad_group", I64, P, P, P, P, P, P, P, P, P, I64, P, P)
+sig("tvq_wgrad_group_bias", I64, P, P, P, P, P, P, P, P, P, P, I64, P, P)
 # --- losses / optimizer --------------------------------------------------------
 sig("tvq_loss_workspace", I64, restype=I64)
 sig("tvq_loss_fwd", P, P, I64, I64, P, P, P)

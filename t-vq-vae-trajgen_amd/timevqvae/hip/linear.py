@@ -33,10 +33,18 @@ def _bias_grad_rows(g2, sink=None):
     return out
 
 
-def weight_grad(g, x2, w_param, M, N, K, tag=None):
+def weight_grad(g, x2, w_param, M, N, K, tag=None, b_param=None):
     """dW = g^T x (N x K): accumulated into the flat grad view when available (deferred to
-    the grouped launch inside a wgrad.grouped() scope; `tag`: the forward's wgrad tag)."""
+    the grouped launch inside a wgrad.grouped() scope; `tag`: the forward's wgrad tag).
+    With `b_param`: returns (dW, db), db = the column sums of g; inside a grouped() scope,
+    with both flat-gradient views available, db rides in the same grouped launch."""
     sink = grad_sink(w_param)
+    if b_param is not None:
+        bsink = grad_sink(b_param)
+        if sink is not None and bsink is not None and wgrad.defer(
+                g, N, x2, K, sink, K, N, K, M, tag, db=bsink):
+            return None, None
+        return weight_grad(g, x2, w_param, M, N, K, tag), _bias_grad_rows(g, bsink)
     if sink is not None:  # into the flat gradient: off the critical path
         if wgrad.defer(g, N, x2, K, sink, K, N, K, M, tag):  # grouped at the backward's end
             return None
@@ -85,10 +93,13 @@ class _Linear(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = gemm(g, N, 1, w, K, 1, M, K, N).reshape(ctx.shp)
-        if ctx.needs_input_grad[1]:
-            dw = weight_grad(g, x2, ctx.params[0], M, N, K, ctx.wg_tag)
-        if ctx.has[0] and ctx.needs_input_grad[2]:
-            db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
+        if ctx.needs_input_grad[1] and ctx.has[0] and ctx.needs_input_grad[2]:
+            dw, db = weight_grad(g, x2, ctx.params[0], M, N, K, ctx.wg_tag, ctx.params[1])
+        else:
+            if ctx.needs_input_grad[1]:
+                dw = weight_grad(g, x2, ctx.params[0], M, N, K, ctx.wg_tag)
+            if ctx.has[0] and ctx.needs_input_grad[2]:
+                db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
         return dx, dw, db, dres, None
 
 
@@ -117,10 +128,13 @@ class _LinearSelfRes(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = gemm(g, K, 1, w.contiguous(), K, 1, M, K, K, R=g, ldr=K).reshape(ctx.shp)
-        if ctx.needs_input_grad[1]:
-            dw = weight_grad(g, x2, ctx.params[0], M, K, K, ctx.wg_tag)
-        if ctx.params[1] is not None and ctx.needs_input_grad[2]:
-            db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
+        if ctx.needs_input_grad[1] and ctx.params[1] is not None and ctx.needs_input_grad[2]:
+            dw, db = weight_grad(g, x2, ctx.params[0], M, K, K, ctx.wg_tag, ctx.params[1])
+        else:
+            if ctx.needs_input_grad[1]:
+                dw = weight_grad(g, x2, ctx.params[0], M, K, K, ctx.wg_tag)
+            if ctx.params[1] is not None and ctx.needs_input_grad[2]:
+                db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
         return dx, dw, db
 
 

@@ -65,8 +65,9 @@ def grouped():
 
 
 def launch(recs):
-    """dW (+)= dY^T X for each record (dy, ldy, x, ldx, dw, ldw, M, N, K, keep) in one
-    tvq_wgrad_group call on the current stream."""
+    """dW (+)= dY^T X for each record (dy, ldy, x, ldx, dw, ldw, M, N, K[, db]) in one
+    tvq_wgrad_group_bias call on the current stream; a record's optional 10th entry is its
+    bias gradient db (+)= the column sums of dY, taken in the same launch pair."""
     n = len(recs)
     dev = recs[0][0].device
     if _DEBUG:
@@ -80,8 +81,11 @@ def launch(recs):
     ws = torch.empty(wsz, device=dev, dtype=torch.float32) if wsz > 0 else None
     dy, x, dw = Ps(*[ptr(r[0]) for r in recs]), Ps(*[ptr(r[2]) for r in recs]), Ps(*[ptr(r[4]) for r in recs])
     ldy, ldx, ldw = I64s(*[r[1] for r in recs]), I64s(*[r[3] for r in recs]), I64s(*[r[5] for r in recs])
-    call("tvq_wgrad_group", n, ctypes.addressof(dy), ctypes.addressof(ldy), ctypes.addressof(x),
-         ctypes.addressof(ldx), ctypes.addressof(dw), ctypes.addressof(ldw), ctypes.addressof(M),
+    dbs = [r[9] if len(r) > 9 else None for r in recs]
+    db = Ps(*[ptr(t) if t is not None else None for t in dbs])
+    call("tvq_wgrad_group_bias", n, ctypes.addressof(dy), ctypes.addressof(ldy), ctypes.addressof(x),
+         ctypes.addressof(ldx), ctypes.addressof(dw), ctypes.addressof(ldw),
+         ctypes.addressof(db) if any(t is not None for t in dbs) else None, ctypes.addressof(M),
          ctypes.addressof(N), ctypes.addressof(K), 1, ptr(ws),
          torch.cuda.current_stream().cuda_stream)
 
@@ -91,20 +95,29 @@ def _span(t, rows, ld, cols):
     return a, a + 4 * ((rows - 1) * ld + cols)
 
 
-def defer(dy, ldy, x, ldx, dw, ldw, M, N, K, tag=None):
+def _spans(r):
+    out = [_span(r[4], r[6], r[5], r[7])]
+    if len(r) > 9 and r[9] is not None:
+        out.append(_span(r[9], 1, r[6], r[6]))
+    return out
+
+
+def defer(dy, ldy, x, ldx, dw, ldw, M, N, K, tag=None, db=None):
     """Record dW[m*ldw + n] += sum_k dY[k*ldy + m] X[k*ldx + n] (m < M, n < N, k < K)
-    when a grouped() scope is active (returns True); else returns False and the caller
-    launches it.  The flat-gradient view `dw` must not be read or written by anything
-    else before the scope's exit (Linear weight gradients: read by the optimizer only).
-    `tag`: the current_tag() of the layer's forward (records group per stream and tag)."""
+    -- and, with `db` (a contiguous flat-gradient view of M floats), db[m] += sum_k
+    dY[k*ldy + m] -- when a grouped() scope is active (returns True); else returns False
+    and the caller launches it.  The flat-gradient views must not be read or written by
+    anything else before the scope's exit (Linear weight / bias gradients: read by the
+    optimizer only).  `tag`: the current_tag() of the layer's forward (records group per
+    stream and tag)."""
     if _pending is None:
         return False
-    rec = (dy, ldy, x, ldx, dw, ldw, M, N, K)
+    rec = (dy, ldy, x, ldx, dw, ldw, M, N, K, db)
     st = torch.cuda.current_stream()
     recs = _pending.setdefault((st, tag), [])
-    lo, hi = _span(dw, M, ldw, N)
+    mine = _spans(rec)
     for other in [v for (s_, _), v in _pending.items() if s_ == st]:
-        if any(lo < h and l < hi for l, h in (_span(r[4], r[6], r[5], r[7]) for r in other)):
+        if any(lo < h and l < hi for r in other for l, h in _spans(r) for lo, hi in mine):
             launch(other)  # same output: keep the accumulation order
             other.clear()
     recs.append(rec)

@@ -168,10 +168,13 @@ class _LinearAct(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = gemm(g, N, 1, w, K, 1, M, K, N).reshape(ctx.shape)
-        if ctx.needs_input_grad[1]:
-            dw = weight_grad(g, x2, ctx.params[0], M, N, K, ctx.wg_tag)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
+        if ctx.needs_input_grad[1] and ctx.has_b and ctx.needs_input_grad[2]:
+            dw, db = weight_grad(g, x2, ctx.params[0], M, N, K, ctx.wg_tag, ctx.params[1])
+        else:
+            if ctx.needs_input_grad[1]:
+                dw = weight_grad(g, x2, ctx.params[0], M, N, K, ctx.wg_tag)
+            if ctx.has_b and ctx.needs_input_grad[2]:
+                db = _bias_grad_rows(g, grad_sink(ctx.params[1]))
         return dx, dw, db, None
 
 
@@ -223,10 +226,17 @@ class _FusedFF(torch.autograd.Function):
              ptr(ctx.seed), off, ptr(d_pre), ptr(dxn), ptr(gg), stream_ptr())
         W1p, b1p, W2p, b2p = ctx.params
         g2w = gg if gg is not None else g2
-        dw2 = weight_grad(g2w, hd, W2p, M, 128, 128, ctx.wg_tag) if need[4] else None
-        db2 = _bias_grad_rows(g2w, grad_sink(b2p)) if need[5] else None
-        dw1 = weight_grad(d_pre, x2, W1p, M, 128, 128, ctx.wg_tag) if need[2] else None
-        db1 = _bias_grad_rows(d_pre, grad_sink(b1p)) if need[3] else None
+        dw1 = db1 = dw2 = db2 = None
+        if need[4] and need[5]:  # weight and bias gradients in one grouped record
+            dw2, db2 = weight_grad(g2w, hd, W2p, M, 128, 128, ctx.wg_tag, b2p)
+        else:
+            dw2 = weight_grad(g2w, hd, W2p, M, 128, 128, ctx.wg_tag) if need[4] else None
+            db2 = _bias_grad_rows(g2w, grad_sink(b2p)) if need[5] else None
+        if need[2] and need[3]:
+            dw1, db1 = weight_grad(d_pre, x2, W1p, M, 128, 128, ctx.wg_tag, b1p)
+        else:
+            dw1 = weight_grad(d_pre, x2, W1p, M, 128, 128, ctx.wg_tag) if need[2] else None
+            db1 = _bias_grad_rows(d_pre, grad_sink(b1p)) if need[3] else None
         return (dxn.reshape(shp) if need[0] else None, gy if need[1] else None, dw1, db1, dw2,
                 db2, None, None, None)
 

@@ -365,6 +365,58 @@ def test_wgrad_group(case, cuda):
         assert err < 2e-6, (M, N, K, err)
 
 
+@pytest.mark.parametrize("case", ["lf_prior", "hf_prior", "ragged_chunked"])
+def test_wgrad_group_bias(case, cuda):
+    """tvq_wgrad_group_bias: the Linear bias gradients db_i += column sums of dY_i taken in
+    the grouped weight-gradient launch (every other record has one; the rest keep
+    db = NULL), against torch fp64; dW unchanged bit for bit by the bias rows riding
+    along; run twice, bitwise equal."""
+    from timevqvae.hip import wgrad
+    gen = torch.Generator().manual_seed(5)
+    if case == "lf_prior":
+        shapes = [(384, 128, 6400), (128, 128, 6400), (128, 128, 6400), (128, 128, 6400)] * 2
+    elif case == "hf_prior":
+        shapes = [(192, 32, 24832), (32, 64, 24832), (32, 32, 24832), (64, 32, 24832)]
+    else:
+        shapes = [(33 + 7 * i, 70 - 2 * i, 1001 + 97 * i) for i in range(28)]
+    nw = sum(m * n for m, n, _ in shapes)
+    flat = torch.randn(nw + sum(m for m, _, _ in shapes), generator=gen)
+    recs, off, boff = [], 0, nw
+    for i, (M, N, K) in enumerate(shapes):
+        pad = 3 if case == "ragged_chunked" and i % 3 == 1 else 0
+        dy = torch.randn(K, M + pad, generator=gen) / K ** 0.5
+        x = torch.randn(K, N + pad, generator=gen)
+        recs.append((dy, M + pad, x, N + pad, off, boff if i % 2 == 0 else None, M, N, K))
+        off += M * N
+        boff += M
+    outs = []
+    for with_bias in (True, True, False):
+        fd = flat.to(cuda)
+        rr = []
+        for dy, ldy, x, ldx, o, bo, M, N, K in recs:
+            r = (dy.to(cuda), ldy, x.to(cuda), ldx, fd[o:o + M * N], N, M, N, K)
+            if with_bias:
+                r = r + (fd[bo:bo + M] if bo is not None else None,)
+            rr.append(r)
+        wgrad.launch(rr)
+        outs.append(fd.cpu())
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0][:nw], outs[2][:nw])  # dW: the bias rows change nothing
+    for dy, ldy, x, ldx, o, bo, M, N, K in recs:
+        if bo is None:
+            continue
+        ref = dy[:, :M].double().sum(0) + flat[bo:bo + M].double()
+        err = float((outs[0][bo:bo + M].double() - ref).abs().max() / ref.abs().max())
+        assert err < 2e-6, (M, N, K, err)
+    # the records without a bias output leave their bias rows alone
+    keep = torch.ones(flat.numel(), dtype=torch.bool)
+    for dy, ldy, x, ldx, o, bo, M, N, K in recs:
+        if bo is not None:
+            keep[bo:bo + M] = False
+    keep[:nw] = False
+    assert torch.equal(outs[0][keep], flat[keep])
+
+
 def test_wgrad_group_forms_bitwise_equal(cuda):
     """The wide 128x64 form (16-byte-aligned operands) and the 64x64 form (the same data
     one float off alignment) sum every element in the same order: equal bit for bit, so a

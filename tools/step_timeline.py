@@ -3,7 +3,9 @@
 The step's last kernels are its AdamW launches (`per_step` of them, one per optimizer):
 the last step is everything after the previous step's final AdamW through the last one.
 Prints its wall span, per-queue busy time and kernel families ranked by time per queue.
-usage: python tools/step_timeline.py trace.csv [per_step] [top]"""
+usage: python tools/step_timeline.py trace.csv [per_step] [top] [seq_out]
+seq_out: also write every queue's kernel sequence (start offset, duration, gap to the
+previous kernel on that queue) to that file."""
 import collections
 import csv
 import re
@@ -40,6 +42,17 @@ def main():
             f[k][1] += 1
         for k, (d, c) in sorted(f.items(), key=lambda x: -x[1][0])[:top]:
             print(f"   {d / 1e3:8.1f} us {c:4d}x  {k[:110]}")
+    if len(sys.argv) > 4:
+        with open(sys.argv[4], "w") as f:
+            for qid, rs in q.items():
+                f.write(f"queue {qid}\n")
+                prev = None
+                for r in rs:
+                    s0, s1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                    gap = (s0 - prev) / 1e3 if prev is not None else 0.0
+                    f.write(f"{(s0 - t0) / 1e3:9.1f} {(s1 - s0) / 1e3:7.2f} {gap:6.2f}  "
+                            f"{fam(r['Kernel_Name'])[:100]}\n")
+                    prev = s1
 
 
 if __name__ == "__main__":
