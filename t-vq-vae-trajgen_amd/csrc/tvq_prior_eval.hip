@@ -573,512 +573,6 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Two waves per sequence (prior_lf_eval2_kernel): one wave per SIMD left every norm, softmax,
-// GELU and load stall of a sequence exposed on its SIMD; with the sequence's work split over
-// two waves (2048 waves for 1024 sequences, two per SIMD) one wave's VALU phases run under
-// the other's MFMA chains.  The split keeps both waves' MFMA counts equal (4224 each):
-//   * attention: wave w is head w (its q / k / v tiles, S, softmax, O), and its out-
-//     projection partial W_o[:, 64w:64w+64] O_w^T;
-//   * feed-forward: wave w computes ff1 output tiles 2w, 2w+1 (+ GELU on its half) and the
-//     ff2 partial over those 64 inner features;
-//   * project_in / project_out / pred_head: wave w computes output tiles 2w, 2w+1;
-//   * tied logits: wave w takes half of the code tiles.
-// Wave w owns the residual stream's tiles 2w, 2w+1 (the features it computes in the N
-// splits); the whole x is gathered through LDS where a norm or a GEMM needs it.  A split-K
-// partial's other-wave tiles go to LDS as they finish and each wave adds the other's partial
-// to its own tiles in the fixed order y_0 + y_1, so both waves hold bitwise-identical x.
-// Each wave consumes its own packed weight stream (tiles in its order of use).
-
-constexpr int PE2_PER_LAYER = 16;  // q0 q1 k0 k1 v0 v1 (64 steps), wo x4 (32), ff1 x2 (64), ff2 x4 (32)
-
-__device__ __forceinline__ int pe2_kt0(int K) { return ((K + 31) / 32 + 1) / 2; }
-__device__ __forceinline__ int pe2_ntiles(int depth, int K, int w) {
-  const int Kt = (K + 31) / 32;
-  return 6 + PE2_PER_LAYER * depth + (w == 0 ? pe2_kt0(K) : Kt - pe2_kt0(K));
-}
-__device__ __forceinline__ PeTile pe2_tile(const PriorArgs& a, int w, int idx) {
-  if (idx < 2) return {a.w_in, 64 * w + 32 * idx, 0, 64, PE_D, nullptr};
-  idx -= 2;
-  if (idx < PE2_PER_LAYER * a.depth) {
-    const PriorLayer& L = a.L[idx / PE2_PER_LAYER];
-    const int j = idx % PE2_PER_LAYER;
-    if (j < 6) {
-      const int m = j / 2, u = j % 2;
-      return {m == 0 ? L.wq : (m == 1 ? L.wk : L.wv), 64 * w + 32 * u, 0, 64, PE_D, L.g_attn};
-    }
-    if (j < 10) return {L.wo, 32 * (j - 6), 64 * w, 32, PE_D, nullptr};
-    if (j < 12) return {L.w1, 64 * w + 32 * (j - 10), 0, 64, PE_D, L.g_ff};
-    return {L.w2, 32 * (j - 12), 64 * w, 32, PE_D, nullptr};
-  }
-  idx -= PE2_PER_LAYER * a.depth;
-  if (idx < 2) return {a.w_out, 64 * w + 32 * idx, 0, 64, PE_D, a.g_final};
-  idx -= 2;
-  if (idx < 2) return {a.wp, 64 * w + 32 * idx, 0, 64, PE_D, nullptr};
-  idx -= 2;
-  return {a.tok_emb, 32 * ((w == 0 ? 0 : pe2_kt0(a.K)) + idx), 0, 64, a.K, nullptr};
-}
-// float4 offset of tile idx within wave w's stream (64-step tiles 1024, 32-step tiles 512)
-__device__ __forceinline__ int64_t pe2_tile_off(int idx, int depth) {
-  if (idx < 2) return 1024 * idx;
-  const int li = min((idx - 2) / PE2_PER_LAYER, depth);
-  const int j = idx - 2 - PE2_PER_LAYER * li;  // >= 0; past the layers: tiles after them
-  int64_t off = 2048 + (int64_t)12288 * li;
-  if (li == depth) return off + 1024 * (int64_t)j;
-  if (j < 6) return off + 1024 * j;
-  if (j < 10) return off + 6144 + 512 * (j - 6);
-  if (j < 12) return off + 8192 + 1024 * (j - 10);
-  return off + 10240 + 512 * (j - 12);
-}
-__device__ __forceinline__ int64_t pe2_stream_len(int depth, int K, int w) {
-  return pe2_tile_off(pe2_ntiles(depth, K, w), depth);
-}
-
-// blockIdx.x over wave 0's tiles, then wave 1's
-__global__ __launch_bounds__(256) void prior_pack2_kernel(PriorArgs a, float4* __restrict__ out) {
-  const int n0 = pe2_ntiles(a.depth, a.K, 0);
-  const int w = (int)blockIdx.x < n0 ? 0 : 1;
-  const int idx = (int)blockIdx.x - (w ? n0 : 0);
-  const PeTile t = pe2_tile(a, w, idx);
-  float4* dst = out + (w ? pe2_stream_len(a.depth, a.K, 0) : 0) + pe2_tile_off(idx, a.depth);
-  const int n4 = t.ns / 4 * 64;
-  for (int e = threadIdx.x; e < n4; e += 256) {
-    const int T4 = e >> 6, l = e & 63;
-    const int row = t.row0 + (l & 31);
-    const int k = t.k0 + 32 * (T4 >> 2) + 8 * (T4 & 3) + 4 * (l >> 5);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row < t.rows) v = *reinterpret_cast<const float4*>(t.w + (int64_t)row * PE_D + k);
-    if (t.gk) {
-      const float4 g = *reinterpret_cast<const float4*>(t.gk + k);
-      v.x *= g.x; v.y *= g.y; v.z *= g.z; v.w *= g.w;
-    }
-    dst[e] = v;
-  }
-}
-
-// The two-wave kernel's stream consumer: the lane's 16-B groups form one sequence across
-// tiles; a ring of PE2_D groups stays in flight (each group's load is issued as the group
-// PE2_D before it is consumed: PE2_D x 4 MFMAs = 1024 cycles ahead at PE2_D = 4), 16
-// registers instead of a whole tile plus the next tile's head.
-#ifndef PE2_D
-#define PE2_D 4
-#endif
-struct PeStream2 {
-  const float4* __restrict__ src;
-  int pos;    // group index of the next group to consume
-  int total;  // groups in the stream
-  int lane;
-  float4 q[PE2_D];
-};
-__device__ __forceinline__ void pe2_stream_begin(PeStream2& st) {
-  st.pos = 0;
-#pragma unroll
-  for (int i = 0; i < PE2_D; ++i)
-    st.q[i] = i < st.total ? st.src[(int64_t)i * 64 + st.lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-}
-template <bool WA, int NS, class BV>
-__device__ __forceinline__ floatx16 pe2_gemm(PeStream2& st, BV bv, floatx16 acc) {
-  constexpr int G = NS / 4;
-  static_assert(G % PE2_D == 0, "tile groups must fill the ring");
-#pragma unroll
-  for (int T4 = 0; T4 < G; ++T4) {
-    const float4 w4 = st.q[T4 % PE2_D];
-    const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float b = bv(4 * T4 + e);
-      acc = WA ? pe_mfma(wv[e], b, acc) : pe_mfma(b, wv[e], acc);
-    }
-    // branch-free: past the stream's end the last group is re-read (never consumed)
-    const int nxt = min(st.pos + T4 + PE2_D, st.total - 1);
-    st.q[T4 % PE2_D] = (st.src + __builtin_amdgcn_readfirstlane(nxt) * 64)[st.lane];
-  }
-  st.pos += G;
-  return acc;
-}
-
-// the RMSNorm factor of pe_rms: y = x * f
-__device__ __forceinline__ float pe_rms_factor(const floatx16 (&x)[4]) {
-  float ss = 0.f;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) ss = fmaf(x[t][r], x[t][r], ss);
-  ss += __shfl_xor(ss, 32, 64);
-  return 1.0f / fmaxf(sqrtf(ss), 1e-12f) * sqrtf((float)PE_D);
-}
-
-// pe_layernorm with the affine vectors loaded one output tile at a time (16 + 16 registers
-// instead of 64 + 64)
-__device__ __forceinline__ void pe2_layernorm(floatx16 (&x)[4], const float* __restrict__ w,
-                                              const float* __restrict__ b, float eps, int h) {
-  float s = 0.f;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s += x[t][r];
-  s += __shfl_xor(s, 32, 64);
-  const float mean = s / (float)PE_D;
-  float v = 0.f;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float d = x[t][r] - mean;
-      v = fmaf(d, d, v);
-    }
-  v += __shfl_xor(v, 32, 64);
-  const float rstd = 1.0f / sqrtf(v / (float)PE_D + eps);
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    floatx16 wv, bv;
-    pe_load_tile_vec(w, t, h, wv);
-    if (b) pe_load_tile_vec(b, t, h, bv);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float y = (x[t][r] - mean) * rstd * wv[r];
-      if (b) y += bv[r];
-      x[t][r] = y;
-    }
-  }
-}
-
-// LDS exchange of register tiles: buf[wave][slot][quad][lane] (ds_write_b128 / ds_read_b128,
-// 64 lanes x 16 B contiguous per instruction: conflict-free).  Every exchange is write,
-// barrier, read, barrier, so one 16 KB buffer serves all of them.
-typedef float4 Pe2Buf[2][2][4][64];
-__device__ __forceinline__ void pe2_put(Pe2Buf& buf, int w, int slot, const floatx16& v, int l) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    buf[w][slot][q][l] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-}
-__device__ __forceinline__ void pe2_get(Pe2Buf& buf, int w, int slot, floatx16& v, int l) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 t = buf[w][slot][q][l];
-    v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
-  }
-}
-// my tiles 2W, 2W+1 + the other wave's -> the whole x
-template <int W>
-__device__ __forceinline__ void pe2_gather(Pe2Buf& buf, const floatx16 (&mine)[2],
-                                           floatx16 (&x)[4], int l) {
-  pe2_put(buf, W, 0, mine[0], l);
-  pe2_put(buf, W, 1, mine[1], l);
-  __syncthreads();
-  x[2 * W] = mine[0];
-  x[2 * W + 1] = mine[1];
-  pe2_get(buf, 1 - W, 0, x[2 * (1 - W)], l);
-  pe2_get(buf, 1 - W, 1, x[2 * (1 - W) + 1], l);
-  __syncthreads();
-}
-
-// Split-K output tile ot of a branch (the wave's partial over its K half): the other wave's
-// tiles go to LDS as soon as they are done, mine stay in registers (yo)
-template <int W>
-__device__ __forceinline__ void pe2_keep_or_send(Pe2Buf& buf, int ot, const floatx16& y,
-                                                 floatx16 (&yo)[2], int l) {
-  if ((ot >> 1) == W) yo[ot & 1] = y;
-  else pe2_put(buf, W, ot & 1, y, l);
-}
-// my tiles of y_0 + y_1 (the same order on both waves)
-template <int W>
-__device__ __forceinline__ void pe2_reduce_mine(Pe2Buf& buf, floatx16 (&yo)[2], int l) {
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    floatx16 o;
-    pe2_get(buf, 1 - W, j, o, l);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) yo[j][r] = W == 0 ? yo[j][r] + o[r] : o[r] + yo[j][r];
-  }
-  __syncthreads();
-}
-
-template <int W>
-__device__ __forceinline__ void prior_lf_eval2_body(const PriorArgs& a,
-                                                    const float4* __restrict__ wstream,
-                                                    Pe2Buf& buf) {
-  const int l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
-  const int b = blockIdx.x;
-  const int n = a.n, ntok = a.n + 1;
-  const bool live = r32 < ntok;
-  PeStream2 st;
-  st.src = wstream + (W ? pe2_stream_len(a.depth, a.K, 0) : 0);
-  st.total = (int)(pe2_stream_len(a.depth, a.K, W) / 64);
-  st.lane = l;
-  pe2_stream_begin(st);
-  // ---- embedding (both waves): cls row, then token + position rows (zeros on padding)
-  floatx16 x[4];
-  {
-    const float* src;
-    const float* pos = nullptr;
-    if (r32 == 0) {
-      const int64_t c = a.cls ? a.cls[b] : (int64_t)a.n_classes;
-      src = a.cls_emb + c * PE_D;
-    } else {
-      const int i = live ? r32 - 1 : 0;
-      src = a.tok_emb + a.s[(int64_t)b * a.ss + i] * PE_D;
-      pos = a.pos_emb + (int64_t)i * PE_D;
-    }
-    pe_load_vec(src, h, x);
-    if (pos) {
-      floatx16 p[4];
-      pe_load_vec(pos, h, p);
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) x[t][r] += p[t][r];
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) x[t][r] = live ? x[t][r] : 0.f;
-  }
-  // ---- project_in (my output tiles) + post_emb_norm on the gathered x
-  {
-    floatx16 y2[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      pe_zero(y2[j]);
-      y2[j] = pe2_gemm<true, 64>(st, [&](int t) { return x[t >> 4][t & 15]; }, y2[j]);
-    }
-    pe2_gather<W>(buf, y2, x, l);
-    pe2_layernorm(x, a.post_gamma, nullptr, 1e-5f, h);
-  }
-  // x stays whole between the branches; inside a branch only my half (xo) is kept next to
-  // the branch's RMSNorm input xn
-  floatx16 xo[2];
-  for (int li = 0; li < a.depth; ++li) {
-    const PriorLayer L = a.L[li];
-    floatx16 yo[2];
-    {  // attention, head W: partial y = W_o[:, 64W : 64W + 64] O_W^T
-      floatx16 xn[4];
-      {
-        const float f = pe_rms_factor(x);  // g_attn folded into q / k / v
-        xo[0] = x[2 * W];
-        xo[1] = x[2 * W + 1];
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) xn[t][r] = x[t][r] * f;
-      }
-      auto bn = [&](int t) { return xn[t >> 4][t & 15]; };
-      floatx16 q[2], k[2], s;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        pe_zero(q[u]);
-        q[u] = pe2_gemm<true, 64>(st, bn, q[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        pe_zero(k[u]);
-        k[u] = pe2_gemm<true, 64>(st, bn, k[u]);
-      }
-      pe_zero(s);
-#pragma unroll
-      for (int t = 0; t < 32; ++t) s = pe_mfma(k[t >> 4][t & 15], q[t >> 4][t & 15], s);
-      float mx = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float sv = pe_crow(i, h) < ntok ? s[i] * 0.125f : -INFINITY;  // 64^-1/2
-        s[i] = sv;
-        mx = fmaxf(mx, sv);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      float sum = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float e = expf(s[i] - mx);
-        s[i] = e;
-        sum += e;
-      }
-      sum += __shfl_xor(sum, 32, 64);
-      const float inv = 1.0f / sum;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[i] *= inv;
-      floatx16 v[2], o[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        pe_zero(v[u]);
-        v[u] = pe2_gemm<false, 64>(st, bn, v[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        pe_zero(o[u]);
-#pragma unroll
-        for (int t = 0; t < 16; ++t) o[u] = pe_mfma(v[u][t], s[t], o[u]);
-      }
-#pragma unroll
-      for (int ot = 0; ot < 4; ++ot) {
-        floatx16 y;
-        pe_zero(y);
-        y = pe2_gemm<true, 32>(st, [&](int t) { return o[t >> 4][t & 15]; }, y);
-        pe2_keep_or_send<W>(buf, ot, y, yo, l);
-      }
-    }
-    pe2_reduce_mine<W>(buf, yo, l);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) xo[j][r] = live ? yo[j][r] + xo[j][r] : 0.f;
-    pe2_gather<W>(buf, xo, x, l);
-    {  // feed-forward: u = GELU(W1 xn + b1) tiles 2W, 2W+1; partial y = W2[:, 64W:64W+64] u^T
-      floatx16 u[2];
-      {
-        floatx16 xn[4];
-        const float f = pe_rms_factor(x);  // g_ff folded into ff1
-        xo[0] = x[2 * W];
-        xo[1] = x[2 * W + 1];
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) xn[t][r] = x[t][r] * f;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          floatx16 bv, acc;
-          pe_load_tile_vec(L.b1, 2 * W + j, h, bv);
-          pe_zero(acc);
-          acc = pe2_gemm<true, 64>(st, [&](int t) { return xn[t >> 4][t & 15]; }, acc);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) u[j][r] = pe_gelu(acc[r] + bv[r]);
-        }
-      }
-#pragma unroll
-      for (int ot = 0; ot < 4; ++ot) {
-        floatx16 y;
-        pe_zero(y);
-        y = pe2_gemm<true, 32>(st, [&](int t) { return u[t >> 4][t & 15]; }, y);
-        pe2_keep_or_send<W>(buf, ot, y, yo, l);
-      }
-    }
-    pe2_reduce_mine<W>(buf, yo, l);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      floatx16 bv;
-      pe_load_tile_vec(L.b2, 2 * W + j, h, bv);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) xo[j][r] = live ? (yo[j][r] + bv[r]) + xo[j][r] : 0.f;
-    }
-    pe2_gather<W>(buf, xo, x, l);
-  }
-  // ---- final_norm + project_out (my tiles), gathered
-  {
-    const float f = pe_rms_factor(x);  // g_final folded into project_out
-    floatx16 y2[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      pe_zero(y2[j]);
-      y2[j] = pe2_gemm<true, 64>(st, [&](int t) { return x[t >> 4][t & 15] * f; }, y2[j]);
-    }
-    pe2_gather<W>(buf, y2, x, l);
-  }
-  // ---- pred_head: LayerNorm_{w,b}(GELU(x W_p^T + b_p)), my tiles then gathered
-  {
-    floatx16 y2[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      floatx16 bv, acc;
-      pe_load_tile_vec(a.bp, 2 * W + j, h, bv);
-      pe_zero(acc);
-      acc = pe2_gemm<true, 64>(st, [&](int t) { return x[t >> 4][t & 15]; }, acc);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) y2[j][r] = pe_gelu(acc[r] + bv[r]);
-    }
-    pe2_gather<W>(buf, y2, x, l);
-    pe2_layernorm(x, a.ln_w, a.ln_b, a.ln_eps, h);
-  }
-  auto bx = [&](int t) { return x[t >> 4][t & 15]; };
-  // ---- tied logits over this wave's code tiles
-  const int Kt = (a.K + 31) / 32;
-  const int cb = W == 0 ? 0 : pe2_kt0(a.K), ce = W == 0 ? pe2_kt0(a.K) : Kt;
-  const int ldb = a.K + 1;
-  if (a.sampled) {
-    const int tok = r32;
-    const bool tok_ok = tok >= 1 && tok <= n;
-    const int64_t t = (int64_t)b * n + (tok_ok ? tok - 1 : 0);
-    const float* brow = a.bias + (int64_t)(tok_ok ? tok - 1 : 0) * ldb;
-    // every lane reads a valid row (t is clamped for the cls / padding lanes, which store
-    // nothing): race_tile<true> dereferences it unconditionally
-    const float* grow = a.gumbel ? a.gumbel + t * a.K : nullptr;
-    const uint32_t key = a.gumbel ? 0u : race_key(mix_seed(a.seed_ptr, a.offset));
-    float* lout = (a.logits && tok_ok) ? a.logits + t * a.K : nullptr;
-    RaceState rs;
-    race_init(rs);
-    for (int c = cb; c < ce; ++c) {
-      const int c0 = 32 * c;
-      float v[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int code = c0 + race_crow(r, h);
-        v[r] = code < a.K ? brow[code] : 0.f;
-      }
-      floatx16 acc;
-      pe_zero(acc);
-      acc = pe2_gemm<true, 64>(st, bx, acc);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] += acc[r];
-      if (lout) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int code = c0 + race_crow(r, h);
-          if (code < a.K) lout[code] = v[r];
-        }
-      }
-      if (a.gumbel) race_tile<true>(rs, v, c0, h, a.K, grow, key, (uint32_t)t * (uint32_t)a.K);
-      else race_tile<false>(rs, v, c0, h, a.K, grow, key, (uint32_t)t * (uint32_t)a.K);
-    }
-    race_halves(rs);
-    // the two waves' code halves meet in LDS (wave 1 publishes, wave 0 finishes)
-    float* fb = reinterpret_cast<float*>(&buf[0][0][0][0]);
-    double* db = reinterpret_cast<double*>(fb + 256);
-    if (W == 1 && l < 32) {
-      fb[l] = rs.m;
-      fb[32 + l] = rs.best;
-      fb[64 + l] = rs.bl;
-      reinterpret_cast<int*>(fb)[96 + l] = rs.bk;
-      db[l] = rs.s;
-    }
-    __syncthreads();
-    if (W == 0 && h == 0) {
-      race_merge(rs, fb[l], db[l], fb[32 + l], fb[64 + l], reinterpret_cast<int*>(fb)[96 + l]);
-      int pick;
-      float p;
-      race_result(rs, pick, p);
-      if (tok_ok) {
-        const int64_t s0 = a.s[(int64_t)b * a.ss + tok - 1];
-        const bool known = s0 != a.mask_id;
-        a.sampled[t] = known ? s0 : (int64_t)pick;
-        a.selp[t] = known ? INFINITY : p;
-      }
-    }
-    return;
-  }
-  float* out = a.logits + (int64_t)b * n * a.K;
-  for (int c = cb; c < ce; ++c) {
-    const int code = 32 * c + r32;
-    floatx16 acc;
-    pe_zero(acc);
-    acc = pe2_gemm<false, 64>(st, bx, acc);
-    if (code < a.K) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int tok = pe_crow(r, h);
-        if (tok >= 1 && tok <= n)
-          out[(int64_t)(tok - 1) * a.K + code] = acc[r] + a.bias[(int64_t)(tok - 1) * ldb + code];
-      }
-    }
-  }
-}
-
-// two waves (128 threads) per sequence
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) void prior_lf_eval2_kernel(PriorArgs a,
-                                                             const float4* __restrict__ wstream) {
-  __shared__ Pe2Buf buf;
-  if (threadIdx.x < 64) prior_lf_eval2_body<0>(a, wstream, buf);
-  else prior_lf_eval2_body<1>(a, wstream, buf);
-}
-
 }  // namespace tvq
 
 using namespace tvq;
@@ -1120,34 +614,21 @@ static int prior_lf_eval_launch(PriorArgs& a, const int64_t* s, int64_t B, int64
   const int ntiles = 4 + 28 * (int)depth + 8 + (int)((K + 31) / 32);
   hipStream_t st = (hipStream_t)stream;
   float4* ws = reinterpret_cast<float4*>(workspace);
-  // TVQ_PRIOR_WAVES=2: the two-wave kernel.  Measured slower (sampler batch 5.86 vs 5.57 ms,
-  // 356 vs 327 us per launch, tools/gpu_r4j.sh): the LDS exchanges, barriers and the work
-  // both waves repeat (norm statistics, LayerNorms) cost more than the second wave hides --
-  // the one-wave kernel's MFMA pipe was already ~64 % busy with its VALU phases mostly
-  // short (profiles/r04_prior_pmc.txt)
-  static const bool two = [] {
-    const char* e = getenv("TVQ_PRIOR_WAVES");
-    return e && e[0] == '2';
-  }();
-  if (two) {
-    // both waves' streams: 6 + 16 * depth tiles each, plus the code tiles
-    const int ntiles2 = 12 + 2 * PE2_PER_LAYER * (int)depth + (int)((K + 31) / 32);
-    if (!ready)
-      hipLaunchKernelGGL(prior_pack2_kernel, dim3((unsigned)ntiles2), dim3(256), 0, st, a, ws);
-    hipLaunchKernelGGL(prior_lf_eval2_kernel, dim3((unsigned)B), dim3(128), 0, st, a,
-                       (const float4*)ws);
-  } else {
-    const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32;  // as the workspace
-    a.ftab = reinterpret_cast<float*>(ws + tiles64 * 1024 + depth * 8 * 512);
-    if (!ready) {  // weights -> folded tables + packed stream
-      hipLaunchKernelGGL(prior_fold_kernel, dim3((unsigned)(K + 1 + n + n_classes + 1)), dim3(128),
-                         0, st, a);
-      hipLaunchKernelGGL(prior_pack_kernel, dim3((unsigned)(ntiles - 4)), dim3(256), 0, st, a, ws, 4);
-    }
-    hipLaunchKernelGGL(prior_lf_eval_kernel, dim3((unsigned)B), dim3(64), 0, st, a,
-                       (const float4*)ws);
+  // (A two-wave-per-sequence form -- heads / feed-forward halves split over two waves, the
+  // residual stream exchanged through LDS -- measured slower in round 4: sampler batch 5.86
+  // vs 5.57 ms, 356 vs 327 us per launch; the LDS exchanges, barriers and the work both
+  // waves repeat cost more than the second wave hides, the one-wave kernel's MFMA pipe
+  // being ~64 % busy already (profiles/r04_prior_pmc.txt).  Removed in round 5.)
+  const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32;  // as the workspace
+  a.ftab = reinterpret_cast<float*>(ws + tiles64 * 1024 + depth * 8 * 512);
+  if (!ready) {  // weights -> folded tables + packed stream
+    hipLaunchKernelGGL(prior_fold_kernel, dim3((unsigned)(K + 1 + n + n_classes + 1)), dim3(128),
+                       0, st, a);
+    hipLaunchKernelGGL(prior_pack_kernel, dim3((unsigned)(ntiles - 4)), dim3(256), 0, st, a, ws, 4);
   }
-  TVQ_PLAN("prior_lf_eval waves=%d", two ? 2 : 1);
+  hipLaunchKernelGGL(prior_lf_eval_kernel, dim3((unsigned)B), dim3(64), 0, st, a,
+                     (const float4*)ws);
+  TVQ_PLAN("prior_lf_eval waves=1");
   return launch_status(name);
 }
 

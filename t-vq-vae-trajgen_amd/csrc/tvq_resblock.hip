@@ -53,9 +53,6 @@ namespace tvq {
 #ifndef RB_NW
 #define RB_NW 8
 #endif
-#ifndef RB_LIN
-#define RB_LIN 0
-#endif
 constexpr int RB_T = 64 * RB_NW;  // one image per block
 
 template <int C_, int W_>
@@ -63,21 +60,15 @@ struct RB {
   static constexpr int C = C_, W = W_;
   static constexpr int P = 3 * W, MT = P / 16;       // positions, 16-position tiles
   static constexpr int NR = (C + 15) / 16, CT = 16 * NR;  // 16-row channel tiles
-  // Halo planes (LDS bank map: MI355X_MICROARCH.md §LDS, ds_read_b32 bank = dword mod 32).
-  // LIN (W >= 32): row stride WP == 3 and plane stride PS == 9 (mod 32), so the window cell
-  // of reduction index r = c*9 + t sits at bank r + const: 16 consecutive weight-gradient
-  // columns read 16 distinct banks, and a conv step whose lane pairs (kq, kq^1) carry
-  // reductions r and r + 16 reads the two 16-bank halves (tools/rb_banks.py: C = 16 / 8
-  // backward 3840 -> 96 / 288 extra LDS cycles per image).  Otherwise (W = 16) the round-3
-  // layout: WP = W + 2, PS == 2 mod 32 (LIN doubles those planes for little gain).
-  // Measured (round 4, tools/gpu_r4c.sh): SQ_LDS_BANK_CONFLICT of rb_bwd1/2<16,32> 482K ->
-  // 62K per launch, but fused fwd+bwd 66.8 -> 69.2 us (C=16), 57.1 -> 59.2 (C=8) and the
-  // joint step +25 us: the kernels are bound by their global-memory phases, not the LDS,
-  // and LIN adds address / permutation work.  Off by default; -DRB_LIN=1 builds it.
-  static constexpr bool LIN = RB_LIN && W >= 32;
-  static constexpr int WP = LIN ? W + 2 + ((3 - (W + 2) % 32) + 32) % 32 : W + 2;
+  // Halo planes (LDS bank map: MI355X_MICROARCH.md §LDS, ds_read_b32 bank = dword mod 32):
+  // row stride WP = W + 2, plane stride PS == 2 mod 32.  (Round 4 measured a bank-linear
+  // layout -- WP == 3, PS == 9 mod 32, permuted reduction order -- that cut
+  // SQ_LDS_BANK_CONFLICT of rb_bwd1/2<16,32> 482K -> 62K per launch but ran slower, fused
+  // fwd+bwd 66.8 -> 69.2 us: these kernels are bound by their global-memory phases, not
+  // the LDS; it was removed in round 5.)
+  static constexpr int WP = W + 2;
   static constexpr int HW = 5 * WP;                  // halo plane cells
-  static constexpr int PS = HW + (((LIN ? 9 : 2) - HW % 32) + 32) % 32;  // plane stride
+  static constexpr int PS = HW + ((2 - HW % 32) + 32) % 32;  // plane stride
   static constexpr int K = 9 * C;                    // conv reduction length
   static constexpr int KST = K + ((2 - K % 32) + 32) % 32;  // panel row stride == 2 mod 32
   static constexpr int KC = K + 1, KT = (KC + 15) / 16;     // wgrad columns (+bias), tiles
@@ -107,12 +98,9 @@ struct RB {
   static constexpr int PARTC = NCH * C * PR;         // conv chunk partials (floats)
   static constexpr int PARTW = WPS > 1 ? WPS * C * KCR : 0;  // wgrad chunk partials
   // backward kernels' LDS: G planes | S planes | panel | conv partials | wgrad partials |
-  // ones plane K1 | zeros plane K0 = K1 + PS; LIN puts K1 at the residue (mod 32) whose
-  // bias / padding reads miss the real columns' banks (tools/rb_banks.py)
-  static constexpr int K1RES = C == 8 ? 1 : 0;
-  static constexpr int K1_0 = 2 * PLANE + PANEL + PARTC + PARTW;
-  static constexpr int K1OFF = LIN ? K1_0 + ((K1RES - K1_0 % 32) + 32) % 32 : K1_0;
-  static constexpr int CONSTP = K1OFF - K1_0 + 2 * PS;  // padding + ones plane + zeros plane
+  // ones plane K1 | zeros plane K0 = K1 + PS
+  static constexpr int K1OFF = 2 * PLANE + PANEL + PARTC + PARTW;
+  static constexpr int CONSTP = 2 * PS;  // ones plane + zeros plane
   static_assert(P % 16 == 0 && W % 4 == 0 && C % NCH == 0 && CPC % 4 == 0 &&
                     RB_NW % (NR * NCH) == 0 && RB_NW % WPS == 0 && PSTEPS % WPS == 0,
                 "unsupported ResBlock geometry");
@@ -206,7 +194,7 @@ __device__ __forceinline__ void rb_border(float* __restrict__ dst) {
       o = 4 * R::WP + (r - R::WP);
     } else {
       const int k = r - 2 * R::WP;
-      o = (1 + (k >> 1)) * R::WP + ((k & 1) ? R::W + 1 : 0);  // LIN rows carry a pad cell
+      o = (1 + (k >> 1)) * R::WP + ((k & 1) ? R::W + 1 : 0);
     }
     dst[c * R::PS + o] = 0.f;
   }
@@ -233,25 +221,7 @@ __device__ __forceinline__ void rb_load_panel(const float* __restrict__ w, float
   }
 }
 
-// LIN step order of a chunk's NCHK reductions (rb_conv_items): step s, lane group kq carry
-// r = 32 b + 2 i + 16 (kq & 1) + (kq >> 1) for s = 8 b + i inside the chunk's full 32-blocks
-// (lanes kq, kq ^ 1 of one 32-lane half 16 banks apart), then the tail r = 4 s + kq
-template <class R>
-__device__ __forceinline__ constexpr int rb_lin_r(int s, int kq) {
-  constexpr int NB = R::NCHK / 32;
-  return s < 8 * NB ? 32 * (s >> 3) + 2 * (s & 7) + 16 * (kq & 1) + (kq >> 1) : 4 * s + kq;
-}
-// its inverse: the panel column (4 s + kq) of reduction r
-template <class R>
-__device__ __forceinline__ int rb_lin_col(int r) {
-  constexpr int NB = R::NCHK / 32;
-  if (r >= 32 * NB) return r;
-  const int b = r >> 5, rr = r & 31, lo = rr & 15;
-  return 4 * (8 * b + (lo >> 1)) + 2 * (lo & 1) + (rr >> 4);
-}
-
-// TRANS: the panel of the data gradient (rows = input channels, k = n*9 + t); LIN stores
-// its taps reversed (column r = n*9 + 8 - t), so the flipped gather reads plane tap r % 9
+// TRANS: the panel of the data gradient (rows = input channels, k = n*9 + t)
 template <class R, bool TRANS = false>
 __device__ __forceinline__ void rb_put_panel(float* __restrict__ A, const float (&v)[R::UP]) {
 #pragma unroll
@@ -259,17 +229,7 @@ __device__ __forceinline__ void rb_put_panel(float* __restrict__ A, const float 
     const int i = threadIdx.x + u * RB_T;
     if (i < R::NPAN) {
       const int row = i / R::K, k = i - row * R::K;
-      int col = k;
-      if constexpr (R::LIN) {
-        const int ch = k / R::NCHK;
-        int r = k - ch * R::NCHK;
-        if (TRANS) {
-          const int t0 = r % 9;
-          r += 8 - 2 * t0;
-        }
-        col = ch * R::NCHK + rb_lin_col<R>(r);
-      }
-      A[row * R::KST + col] = v[u];
+      A[row * R::KST + k] = v[u];
     }
   }
 }
@@ -304,37 +264,15 @@ __device__ __forceinline__ void rb_conv_items(const float* __restrict__ A,
   floatx4 acc[R::CNF];
 #pragma unroll
   for (int f = 0; f < R::CNF; ++f) acc[f] = floatx4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (R::LIN) {
-    // step s reads reduction rb_lin_r(s, kq) = c*9 + t of the chunk: plane cell
-    // c*PS + tap(t) (the data gradient's panel holds the reversed tap, so the same cell)
-    int loff[R::NSTEP];
 #pragma unroll
-    for (int s = 0; s < R::NSTEP; ++s) {
-      const int r0 = rb_lin_r<R>(s, 0), r1 = rb_lin_r<R>(s, 1), r2 = rb_lin_r<R>(s, 2),
-                r3 = rb_lin_r<R>(s, 3);
-      auto off = [](int r) {
-        const int c = r / 9, t = r - 9 * c, kh = t / 3;
-        return c * R::PS + kh * R::WP + (t - 3 * kh);
-      };
-      loff[s] = kq == 0 ? off(r0) : kq == 1 ? off(r1) : kq == 2 ? off(r2) : off(r3);
+  for (int g = 0; g < R::CPC / 4; ++g)
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const float a = ap[g * 36 + 4 * s];
+#pragma unroll
+      for (int f = 0; f < R::CNF; ++f)
+        acc[f] = mfma16x16x4(a, sp[f][g * 4 * R::PS + roff[s]], acc[f]);
     }
-#pragma unroll
-    for (int s = 0; s < R::NSTEP; ++s) {
-      const float a = ap[4 * s];
-#pragma unroll
-      for (int f = 0; f < R::CNF; ++f) acc[f] = mfma16x16x4(a, sp[f][loff[s]], acc[f]);
-    }
-  } else {
-#pragma unroll
-    for (int g = 0; g < R::CPC / 4; ++g)
-#pragma unroll
-      for (int s = 0; s < 9; ++s) {
-        const float a = ap[g * 36 + 4 * s];
-#pragma unroll
-        for (int f = 0; f < R::CNF; ++f)
-          acc[f] = mfma16x16x4(a, sp[f][g * 4 * R::PS + roff[s]], acc[f]);
-      }
-  }
 #pragma unroll
   for (int f = 0; f < R::CNF; ++f) {
     const int mt = m + R::CMS * f;
@@ -393,19 +331,10 @@ __device__ __forceinline__ void rb_wgrad_items(const float* __restrict__ G,
 #pragma unroll
     for (int f = 0; f < R::WNF; ++f) acc[nr][f] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int pbase = pc * R::WSTEPS * 4;
-  // LIN: a step's 4 positions are w, w + 16 (lanes kq, kq ^ 1: 16 banks apart) and w + 1,
-  // w + 17 of a 32-position row block
-  const int lpo = R::LIN ? 16 * (kq & 1) + (kq >> 1) : kq;
 #pragma unroll
   for (int s = 0; s < R::WSTEPS; ++s) {
-    int po;
-    if constexpr (R::LIN) {
-      const int st = pc * R::WSTEPS + s, p32 = 32 * (st >> 3);
-      po = (p32 / R::W) * R::WP + p32 % R::W + 2 * (st & 7) + lpo;
-    } else {
-      const int p0 = pbase + 4 * s;                       // 4 | W: one row
-      po = p0 + 2 * (p0 / R::W) + lpo;                   // (p0 / W) * WP + p0 % W + kq
-    }
+    const int p0 = pbase + 4 * s;                         // 4 | W: one row
+    const int po = p0 + 2 * (p0 / R::W) + kq;            // (p0 / W) * WP + p0 % W + kq
     float ga[R::NR], sb[R::WNF];
 #pragma unroll
     for (int nr = 0; nr < R::NR; ++nr) ga[nr] = gp[nr][po];

@@ -21,13 +21,22 @@ def _case(kind, M, V, gen):
         return torch.where(hot, torch.full_like(idx, V - 1), idx)
     if kind == "sparse":
         return torch.randint(0, 7, (M,), generator=gen) * (V // 7)
+    if kind == "invalid":  # out-of-range indices (-1, V + 3) are skipped by the group-by
+        idx = torch.randint(0, V, (M,), generator=gen)
+        bad = torch.rand(M, generator=gen)
+        idx = torch.where(bad < 0.05, torch.full_like(idx, -1), idx)
+        return torch.where(bad > 0.95, torch.full_like(idx, V + 3), idx)
     raise ValueError(kind)
 
 
 @pytest.mark.parametrize("kind,M,V,D", [
     ("uniform", 24576, 513, 128), ("skewed", 24576, 513, 128), ("sparse", 6144, 513, 128),
     ("uniform", 256, 6, 256), ("skewed", 6144, 513, 64), ("uniform", 32768, 1024, 32),
-    ("skewed", 40000, 300, 128), ("uniform", 3, 1, 128), ("skewed", 8192, 5000, 32)])
+    ("skewed", 40000, 300, 128), ("uniform", 3, 1, 128), ("skewed", 8192, 5000, 32),
+    # the single-block sort at its largest LDS footprint (M = 2048, V = 1024: ~68 KB), skewed,
+    # and out-of-range indices on both paths
+    ("skewed", 2048, 1024, 128), ("uniform", 2048, 1000, 64), ("invalid", 2048, 1024, 64),
+    ("invalid", 6144, 513, 128)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_embedding_bwd_groupby(kind, M, V, D, accumulate, cuda):
     from timevqvae.hip._native import call, plan_trace, ptr, stream_ptr, value
@@ -36,7 +45,8 @@ def test_embedding_bwd_groupby(kind, M, V, D, accumulate, cuda):
     g = torch.randn(M, D, generator=gen)
     t0 = torch.randn(V, D, generator=gen)
     ref = t0.double() * accumulate
-    ref = ref.index_add(0, idx, g.double())
+    ok = (idx >= 0) & (idx < V)
+    ref = ref.index_add(0, idx[ok], g[ok].double())
     idd, gd = idx.to(cuda), g.to(cuda)
     outs = []
     for _ in range(2):
