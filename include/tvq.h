@@ -343,6 +343,39 @@ int tvq_resblock_bwd(const float* dy, const float* x, const float* h, int64_t B,
                      const int64_t* seed_ptr, uint64_t offset, float* dx, float* da1, float* dw1,
                      float* db1, float* dbn_w, float* dbn_b, float* da2, float* dw2, float* db2,
                      int64_t accumulate, void* workspace, tvq_stream_t stream);
+/* Fused projection ResBlock (in_channels != out_channels, the 1x1 `proj` on the skip) on the
+ * LF band's W = 8 maps: Ci -> Co in {64 -> 128, 128 -> 64}, H = 3 (csrc/tvq_resblock_w8p.hip;
+ * reference vq_vae.py:13-62):
+ *   y = (proj(x) + bp) + Dropout_p(conv2(Snake_a2(BN(conv1(Snake_a1(x)) + b1))) + b2)
+ * workspace: tvq_resblock_proj_workspace bytes (0 = shape unsupported); saved: the
+ * backward's activations (h | Snake_a1(x) | Snake_a2(BN(h))), tvq_resblock_proj_saved_floats
+ * floats; save: 4 Co floats (batch mean | invstd | scale | shift).  The backward writes dx and
+ * every parameter gradient ((+)= with accumulate), the conv / proj weight-gradient slab sums
+ * joining an open deferral scope (tvq_conv_wgrad_defer_begin). */
+int64_t tvq_resblock_proj_workspace(int64_t B, int64_t Ci, int64_t Co, int64_t H, int64_t W);
+int64_t tvq_resblock_proj_saved_floats(int64_t B, int64_t Ci, int64_t Co, int64_t H, int64_t W);
+int tvq_resblock_proj_train_fwd(const float* x, int64_t B, int64_t Ci, int64_t Co, int64_t H,
+                                int64_t W, const float* a1, const float* w1, const float* b1,
+                                const float* bn_w, const float* bn_b, float* running_mean,
+                                float* running_var, int64_t* nbt, float momentum, float eps,
+                                const float* a2, const float* w2, const float* b2,
+                                const float* wp, const float* bp, float drop_p,
+                                const int64_t* seed_ptr, uint64_t offset, float* saved, float* y,
+                                float* save, void* workspace, tvq_stream_t stream);
+int tvq_resblock_proj_eval_fwd(const float* x, int64_t B, int64_t Ci, int64_t Co, int64_t H,
+                               int64_t W, const float* a1, const float* w1, const float* b1,
+                               const float* bn_w, const float* bn_b, const float* running_mean,
+                               const float* running_var, float eps, const float* a2,
+                               const float* w2, const float* b2, const float* wp,
+                               const float* bp, float* y, tvq_stream_t stream);
+int tvq_resblock_proj_bwd(const float* dy, const float* x, const float* saved, int64_t B,
+                          int64_t Ci, int64_t Co, int64_t H, int64_t W, const float* a1,
+                          const float* w1, const float* bn_w, const float* save, const float* a2,
+                          const float* w2, const float* wp, float drop_p,
+                          const int64_t* seed_ptr, uint64_t offset, float* dx, float* da1,
+                          float* dw1, float* db1, float* dbn_w, float* dbn_b, float* da2,
+                          float* dw2, float* db2, float* dwp, float* dbp, int64_t accumulate,
+                          void* workspace, tvq_stream_t stream);
 
 /* deterministic column sums of a P x N slab: out[j] (+)= sum_p in[p*ld + j]
  * (workspace: tvq_reduce_rows_workspace floats, may be 0). */

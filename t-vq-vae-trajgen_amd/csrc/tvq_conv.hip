@@ -1909,7 +1909,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(const float* __res
 // quarter of the images over all of the tile's columns (5 x 2 independent 16x16x4 MFMA
 // chains), and the 4 partial tiles are summed in wave order through LDS.  One slab row
 // per W8_IMG images: S = B / W8_IMG splits, summed in order by the deferred slab sum.
-constexpr int W8_IMG = 16;
+#ifndef TVQ_W8_IMG
+#define TVQ_W8_IMG 16
+#endif
+constexpr int W8_IMG = TVQ_W8_IMG;
 
 template <int W, int CB>
 __global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restrict__ G0,

@@ -106,6 +106,18 @@ class ResBlock(nn.Module):
                 x.requires_grad or any(p.requires_grad for p in self.parameters()))
             if not needs_grad and not (self.training and c[5].p > 0):
                 return resblock.resblock_eval(x, _a(c[0]), c[1], c[2], _a(c[3]), c[4])
+        if (not isinstance(self.proj, nn.Identity) and self.proj.bias is not None
+                and resblock.proj_supported(x, c[1].in_channels, c[4].out_channels)):
+            # the projection block as 2 (eval: 1) fused launches, csrc/tvq_resblock_w8p.hip
+            if c[2].training:
+                p = c[5].p if self.training else 0.0
+                return resblock.resblock_proj_train(x, _a(c[0]), c[1], c[2], _a(c[3]), c[4],
+                                                    self.proj, p, self._site)
+            needs_grad = torch.is_grad_enabled() and (
+                x.requires_grad or any(p.requires_grad for p in self.parameters()))
+            if not needs_grad and not (self.training and c[5].p > 0):
+                return resblock.resblock_proj_eval(x, _a(c[0]), c[1], c[2], _a(c[3]), c[4],
+                                                   self.proj)
         s, xs = snake_skip(x, _a(c[0]))  # xs: x, its skip-path gradient summed in Snake bwd
         if bn_eval_fusable(s, c[2], c[1].weight, c[1].bias, c[3].a):
             h = conv2d_bn_eval(s, c[1].weight, c[1].bias, c[2], _a(c[3]))  # one launch

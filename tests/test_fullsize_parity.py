@@ -140,10 +140,10 @@ def test_stride2_small_channel_convs_full_batch(kind, Ci, Co, W, spr, cuda):
 
 
 # --------------------------------------------------------------------------- fused ResBlock
-def _resblock(Cc, seed):
+def _resblock(Cc, seed, Co=None):
     from timevqvae.models.vq_vae import ResBlock
     torch.manual_seed(seed)
-    m = ResBlock(Cc, Cc, False, dropout=0.0)
+    m = ResBlock(Cc, Co or Cc, False, dropout=0.0)
     with torch.no_grad():
         for p in m.parameters():
             p.copy_(torch.randn_like(p) * (0.3 if p.dim() > 1 else 0.5))
@@ -186,6 +186,52 @@ def test_fused_resblock_full_batch_vs_oracle(Cc, W, cuda):
         assert tr.has(f"{pre}_{kern} C{Cc} W{W} B{B}"), (kern, tr.lines)
     if Cc == 64:
         assert tr.has("conv_wgrad_w8"), tr.lines
+    ok, err, s = max_ok(yd, yc)
+    assert ok, ("y", err, s)
+    ok, err, s = max_ok(xd.grad, xc.grad)
+    assert ok, ("dx", err, s)
+    for k, p in md.named_parameters():
+        r = params[k].grad
+        scale = None
+        if k == "convs.1.bias":  # feeds the BatchNorm: true gradient 0
+            scale = float(params["convs.1.weight"].grad.abs().max())
+        ok, err, s = max_ok(p.grad, r, scale)
+        assert ok, (k, err, s)
+    post = md.state_dict()
+    for k, v in ctx.updates.items():
+        if v.is_floating_point():
+            ok, err, s = max_ok(post[k], v)
+            assert ok, (k, err, s)
+        else:
+            assert int(post[k]) == int(v), k
+
+
+@pytest.mark.parametrize("Ci,Co", [(64, 128), (128, 64)])
+def test_fused_proj_resblock_full_batch_vs_oracle(Ci, Co, cuda):
+    """The LF band's projection blocks ResBlock(64, 128) / ResBlock(128, 64) (vq_vae.py:13-62,
+    the 1x1 proj on the skip) at the step's (256, Ci, 3, 8): w8p_fwd1/2, w8p_bwd2/1 and the
+    weight gradients against tvq_oracle.res_block with CPU autograd: output, dx, every
+    parameter gradient, BN running statistics."""
+    m = _resblock(Ci, 7 + Ci, Co)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    gen = torch.Generator().manual_seed(Ci + Co)
+    x = torch.randn(B, Ci, 3, 8, generator=gen) * 1.5
+    gy = torch.randn(B, Co, 3, 8, generator=gen)
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items()
+              if v.is_floating_point() and not k.endswith(("running_mean", "running_var"))}
+    sdo = dict(sd)
+    sdo.update(params)
+    xc = x.clone().requires_grad_(True)
+    ctx = O.Ctx(True)
+    yc = O.res_block(ctx, sdo, "", xc)
+    yc.backward(gy)
+    md = m.to(cuda).train()
+    xd = x.to(cuda).requires_grad_(True)
+    with _trace() as tr:
+        yd = md(xd)
+        yd.backward(gy.to(cuda))
+        torch.cuda.synchronize()
+    assert tr.has(f"w8p_fwd Ci{Ci} Co{Co} B{B}") and tr.has(f"w8p_bwd Ci{Ci} Co{Co} B{B}"), tr.lines
     ok, err, s = max_ok(yd, yc)
     assert ok, ("y", err, s)
     ok, err, s = max_ok(xd.grad, xc.grad)
@@ -293,7 +339,9 @@ def test_stage1_step_full_size_vs_oracle(cuda):
     # the benched variants ran
     for want in ("conv_t32 bk16", "conv_wgrad_s2", "rb_bwd1 C16 W32 B256", "rb_bwd1 C8 W64 B256",
                  "rb_bwd1 C32 W16 B256", "w8_bwd1 C64 W8 B256", "w8_fwd2 C64 W8 B256",
-                 "vq_assign D128 rg6", "conv_wgrad_t32", "conv_wgrad_w8"):
+                 "w8p_fwd Ci64 Co128 B256", "w8p_fwd Ci128 Co64 B256", "w8p_bwd Ci64 Co128 B256",
+                 "w8p_bwd Ci128 Co64 B256", "vq_assign D128 rg6", "conv_wgrad_t32",
+                 "conv_wgrad_w8"):
         assert tr.has(want), (want, sorted(set(tr.lines)))
     assert any(int(s.split("spr=")[1]) > 1 for s in tr.has("conv_wgrad_s2")), tr.has("conv_wgrad_s2")
     # oracle on the same weights, batch and (near-tie-checked) indices
@@ -400,6 +448,7 @@ def test_stage2_step_full_size_vs_oracle(cuda):
         torch.cuda.synchronize()
     assert tr.has("vq_assign D128"), tr.lines
     assert tr.has("w8_eval C64 W8 B256 packed=1"), tr.lines  # the frozen LF encoder
+    assert tr.has("w8p_eval Ci64 Co128 B256 packed=1"), tr.lines
     assert tr.has("attn_branch_fwd B256 S25") and tr.has("attn_branch_bwd B256 S25"), tr.lines
     # tokens: the frozen stage1 (eval) through the oracle, near-ties checked
     e = O.Ctx(False)
