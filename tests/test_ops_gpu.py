@@ -146,9 +146,13 @@ def test_conv_residual_dropout(cuda):
 
 # chunked form (C < 32) and the whole-channel form (C >= 32, B*3W <= 24576), including the
 # step's LF (256, 64, 3, 8) and HF (256, 128, 3, 32) shapes
+# (plus the step's small-channel EncBlock / DecBlock outputs (256, 4|8|16, 3, 128|64|32))
 @pytest.mark.parametrize("B,C,W,snake_on", [(8, 16, 32, True), (4, 4, 128, True), (16, 128, 8, True),
                                             (8, 256, 96, False), (256, 64, 8, True),
-                                            (256, 128, 32, True), (64, 32, 16, False)])
+                                            (256, 128, 32, True), (64, 32, 16, False),
+                                            (256, 4, 128, True), (256, 8, 64, True),
+                                            (256, 16, 32, True), (256, 12, 128, False),
+                                            (100, 8, 64, True)])
 def test_bn_snake_train(B, C, W, snake_on, cuda):
     from timevqvae.hip.norm import bn_snake
     bn_c = torch.nn.BatchNorm2d(C).train()
@@ -172,9 +176,9 @@ def test_bn_snake_train(B, C, W, snake_on, cuda):
         return s
 
     y_c = ref(x_c)
-    y_d = bn_snake(x_d, bn_d, a_d if snake_on else None)
     g = torch.randn(y_c.shape, generator=gen)
     y_c.backward(g)
+    y_d = bn_snake(x_d, bn_d, a_d if snake_on else None)
     y_d.backward(g.to(cuda))
     close(y_d, y_c, what="fwd")
     close(x_d.grad, x_c.grad, tol=2e-5, what="dx")
