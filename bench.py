@@ -91,6 +91,9 @@ class JointTrainer:
                          stage1=s1_frozen).to(device).train()
         self.opt1 = self.s1.configure_optimizers()["optimizer"]
         self.opt2 = self.s2.configure_optimizers()["optimizer"]
+        # the fixed zero_grad -> fwd+bwd -> step loop: each update zeroes the gradients it read,
+        # so the next step's zero_grad launches nothing (hip/optim.py zero_after_step)
+        self.opt1.zero_after_step = self.opt2.zero_after_step = True
         if world > 1:  # identical initial replicas (DDP semantics)
             for p in (self.opt1.flat, self.opt2.flat):
                 dist.broadcast(p, 0)
@@ -253,10 +256,10 @@ class JointTrainer:
         defer = self.world > 1  # sync_codebook all-reduce must sit between segments
 
         def before():
-            for sch, opt in zip(scheds, (self.opt1, self.opt2)):
+            for sch in scheds:
                 if sch is not None:
                     sch.step()
-                opt.push_lr()
+            self.opt1.push_lr(self.opt2)  # both learning rates, one launch
 
         def seg1():
             rng.advance(self.device)

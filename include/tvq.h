@@ -53,6 +53,8 @@ int tvq_counter_capture(int64_t begin);
  * sums of stage1.py:170-198, maskgit.py:155-192). */
 int tvq_fill(float* p, int64_t n, float value, tvq_stream_t stream);
 int tvq_fill_i64(int64_t* p, int64_t n, int64_t value, tvq_stream_t stream);
+/* p[0] = a and (q non-NULL) q[0] = b in one launch. */
+int tvq_fill2(float* p, float a, float* q, float b, tvq_stream_t stream);
 int tvq_add_i64(int64_t* p, int64_t value, tvq_stream_t stream);
 int tvq_sum4(const float* a, const float* b, const float* c, const float* d, float* out,
              float* out_ab, int64_t n, tvq_stream_t stream);
@@ -444,6 +446,12 @@ int tvq_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_
               const int64_t* chunks, int64_t nchunks, const float* lr_step, const float* gates,
               const float* seg_step, float beta1, float beta2, float eps, float weight_decay,
               tvq_stream_t stream);
+/* The same, and with zero_grads != 0 each chunk also zeroes the gradient values it has read
+ * (the next step's zero_grad folded into the update: FusedAdamW(zero_after_step=True)). */
+int tvq_adamw_zero(float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                   const int64_t* chunks, int64_t nchunks, const float* lr_step,
+                   const float* gates, const float* seg_step, float beta1, float beta2, float eps,
+                   float weight_decay, int64_t zero_grads, tvq_stream_t stream);
 /* x-transformers layer dropout (random() < p skips a branch) drawn on the device for
  * n <= 256 branches: keep[i] = U(seed, offset, i) >= p; touched[i] = keep[i], or
  * max(touched[i], keep[i]) when accumulate (a second pass of the prior in one step). */

@@ -2458,12 +2458,16 @@ struct RdRec {
 static std::vector<RdRec> g_rd;
 static bool g_rd_on = false, g_rd_paused = false;
 
-constexpr int PACK_BATCH = 24;
+// one launch repacks a whole step's weights (a stage1 + stage2 step records ~70): 36 bytes
+// per entry keep PACK_BATCH of them inside a 4 KB kernel-argument block
+constexpr int PACK_BATCH = 96;
 struct PackBatch {
   const float* src[PACK_BATCH];
-  int64_t wsn[PACK_BATCH], wsc[PACK_BATCH], off[PACK_BATCH];
+  int64_t off[PACK_BATCH];
+  int wsn[PACK_BATCH], wsc[PACK_BATCH];
   int N[PACK_BATCH], C[PACK_BATCH], KK[PACK_BATCH];
 };
+static_assert(sizeof(PackBatch) <= 3900, "pack batch kernel arguments");
 
 // blockIdx.y = entry; blocks stride over the entry's N*C*KK elements ([tap][c][n] order)
 __global__ void conv_pack_multi_kernel(PackBatch b, float* __restrict__ arena) {
@@ -2478,7 +2482,7 @@ __global__ void conv_pack_multi_kernel(PackBatch b, float* __restrict__ arena) {
     const int64_t r = i / N;
     const int c = (int)(r % C);
     const int tap = (int)(r / C);
-    out[i] = w[n * b.wsn[j] + c * b.wsc[j] + tap];
+    out[i] = w[(int64_t)n * b.wsn[j] + (int64_t)c * b.wsc[j] + tap];
   }
 }
 
@@ -3340,7 +3344,7 @@ extern "C" int tvq_conv_packcache_begin(int64_t id, float* arena, int64_t cap_fl
     int64_t most = 0;
     for (size_t i = i0; i < pc.entries.size() && n < PACK_BATCH; ++i, ++n) {
       const PackEntry& p = pc.entries[i];
-      b.src[n] = p.src; b.wsn[n] = p.wsn; b.wsc[n] = p.wsc; b.off[n] = p.off;
+      b.src[n] = p.src; b.wsn[n] = (int)p.wsn; b.wsc[n] = (int)p.wsc; b.off[n] = p.off;
       b.N[n] = p.N; b.C[n] = p.C; b.KK[n] = p.KK;
       const int64_t t = (int64_t)p.N * p.C * p.KK;
       most = t > most ? t : most;

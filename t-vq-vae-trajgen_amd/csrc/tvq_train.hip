@@ -61,7 +61,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p,
                                                     const float* __restrict__ lr_step,
                                                     const float* __restrict__ gates,
                                                     const float* __restrict__ seg_step, float b1,
-                                                    float b2, float eps, float wd) {
+                                                    float b2, float eps, float wd,
+                                                    float* __restrict__ gz) {
   const int64_t start = chunks[3 * blockIdx.x];
   const int len = (int)chunks[3 * blockIdx.x + 1];
   const int seg = (int)chunks[3 * blockIdx.x + 2];
@@ -77,6 +78,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p,
   for (int j = threadIdx.x; j < len; j += 256) {
     const int64_t i = start + j;
     const float gi = g[i];
+    if (gz) gz[i] = 0.f;  // the next step's zero_grad, done where the gradient is read
     float pi = p[i] * decay;
     float mi = m[i];
     mi = mi + w1 * (gi - mi);
@@ -177,18 +179,27 @@ extern "C" int tvq_adamw_begin(float* lr_step, float lr, const float* gates, flo
   return launch_status("tvq_adamw_begin");
 }
 
-extern "C" int tvq_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
-                         const int64_t* chunks, int64_t nchunks, const float* lr_step,
-                         const float* gates, const float* seg_step, float beta1, float beta2,
-                         float eps, float weight_decay, tvq_stream_t stream) {
+extern "C" int tvq_adamw_zero(float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                              const int64_t* chunks, int64_t nchunks, const float* lr_step,
+                              const float* gates, const float* seg_step, float beta1, float beta2,
+                              float eps, float weight_decay, int64_t zero_grads,
+                              tvq_stream_t stream) {
   TVQ_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && chunks && lr_step && gates &&
                     seg_step && nchunks >= 0,
                 "tvq_adamw: bad arguments");
   if (nchunks == 0) return TVQ_OK;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)stream,
                      params, grads, exp_avg, exp_avg_sq, chunks, lr_step, gates, seg_step, beta1,
-                     beta2, eps, weight_decay);
+                     beta2, eps, weight_decay, zero_grads ? grads : nullptr);
   return launch_status("tvq_adamw");
+}
+
+extern "C" int tvq_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                         const int64_t* chunks, int64_t nchunks, const float* lr_step,
+                         const float* gates, const float* seg_step, float beta1, float beta2,
+                         float eps, float weight_decay, tvq_stream_t stream) {
+  return tvq_adamw_zero(params, const_cast<float*>(grads), exp_avg, exp_avg_sq, chunks, nchunks,
+                        lr_step, gates, seg_step, beta1, beta2, eps, weight_decay, 0, stream);
 }
 
 extern "C" int tvq_layer_drop(const int64_t* seed_ptr, uint64_t offset, float p, int64_t n,
@@ -256,6 +267,18 @@ extern "C" int tvq_fill(float* p, int64_t n, float value, tvq_stream_t stream) {
   hipLaunchKernelGGL(fill_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p,
                      n, value, vec);
   return launch_status("tvq_fill");
+}
+
+// p[0] = a, q[0] = b in one launch (two optimizers' learning rates before a replay)
+__global__ void fill2_kernel(float* __restrict__ p, float a, float* __restrict__ q, float b) {
+  if (threadIdx.x == 0) p[0] = a;
+  if (threadIdx.x == 1 && q) q[0] = b;
+}
+
+extern "C" int tvq_fill2(float* p, float a, float* q, float b, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(p, "tvq_fill2: bad arguments");
+  hipLaunchKernelGGL(fill2_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, p, a, q, b);
+  return launch_status("tvq_fill2");
 }
 
 extern "C" int tvq_fill_i64(int64_t* p, int64_t n, int64_t value, tvq_stream_t stream) {

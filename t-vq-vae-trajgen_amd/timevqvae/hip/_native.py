@@ -66,6 +66,7 @@ sig("tvq_counter_capture", I64)
 sig("tvq_plan_trace", I64)
 sig("tvq_plan_read", ctypes.c_char_p, I64, restype=I64)
 sig("tvq_fill", P, I64, ctypes.c_float, P)
+sig("tvq_fill2", P, ctypes.c_float, P, ctypes.c_float, P)
 sig("tvq_fill_i64", P, I64, I64, P)
 sig("tvq_add_i64", P, I64, P)
 sig("tvq_sum4", P, P, P, P, P, P, I64, P)
@@ -144,6 +145,7 @@ sig("tvq_adamw_chunk", restype=I64)
 sig("tvq_adamw_gates", P, I64, P, P)
 sig("tvq_adamw_begin", P, F32, P, P, I64, P)
 sig("tvq_adamw", P, P, P, P, P, I64, P, P, P, F32, F32, F32, F32, P)
+sig("tvq_adamw_zero", P, P, P, P, P, I64, P, P, P, F32, F32, F32, F32, I64, P)
 sig("tvq_layer_drop", P, ctypes.c_uint64, F32, I64, P, P, I64, P)
 
 # --- MaskGIT transformer ---------------------------------------------------------

@@ -84,15 +84,29 @@ class FusedAdamW(torch.optim.Optimizer):
         self.gates = torch.ones(self.nseg, device=dev, dtype=torch.float32)
         self.seg_step = torch.zeros(self.nseg, device=dev, dtype=torch.float32)
         self.has_gates = any(gate_ptrs)
+        # zero_after_step (opt-in, a fixed zero_grad -> backward -> step loop such as
+        # bench.JointTrainer's replayed step): the update zeroes each gradient value after
+        # reading it, and the next zero_grad() -- when nothing else ran in between -- has
+        # nothing left to fill.  .grad then reads 0 after step() (torch keeps it until
+        # zero_grad), so it is off by default.
+        self.zero_after_step = False
+        self._clean = False
 
-    def push_lr(self):
+    def push_lr(self, other=None):
         """Write param_groups[0]['lr'] into the device {lr, step} pair (for graph replays,
-        whose captured update reads the lr from the device: step(lr_on_device=True))."""
-        call("tvq_fill", ptr(self.lr_step), 1, float(self.param_groups[0]["lr"]), stream_ptr())
+        whose captured update reads the lr from the device: step(lr_on_device=True));
+        `other`: a second FusedAdamW whose lr goes in the same launch."""
+        call("tvq_fill2", ptr(self.lr_step), float(self.param_groups[0]["lr"]),
+             ptr(other.lr_step) if other is not None else None,
+             float(other.param_groups[0]["lr"]) if other is not None else 0.0, stream_ptr())
 
     def zero_grad(self, set_to_none: bool = False):
         # gradients accumulate in place into the flat buffer views
         _grad_epoch[0] += 1
+        if self.zero_after_step and self._clean:
+            self._clean = False  # zeroed by the last step()'s update
+            return
+        self._clean = False
         call("tvq_fill", ptr(self.flat_grad), self.flat_grad.numel(), 0.0, stream_ptr())
 
     def gather_gates(self):
@@ -130,8 +144,9 @@ class FusedAdamW(torch.optim.Optimizer):
             self.gather_gates()
         call("tvq_adamw_begin", ptr(self.lr_step), -1.0 if lr_on_device else float(g["lr"]),
              ptr(self.gates), ptr(self.seg_step), self.nseg, s)
-        call("tvq_adamw", ptr(self.flat), ptr(self.flat_grad), ptr(self.exp_avg),
+        call("tvq_adamw_zero", ptr(self.flat), ptr(self.flat_grad), ptr(self.exp_avg),
              ptr(self.exp_avg_sq), ptr(self.chunks), self.nchunks, ptr(self.lr_step),
              ptr(self.gates), ptr(self.seg_step), float(b1), float(b2), float(g["eps"]),
-             float(g["weight_decay"]), s)
+             float(g["weight_decay"]), int(self.zero_after_step), s)
+        self._clean = self.zero_after_step
         return loss
