@@ -276,10 +276,11 @@ class JointTrainer:
                 u.reduce()
 
         def seg2():
+            from timevqvae.hip.optim import step_pair
             for u in self._pending:
                 u.apply()
-            self.opt1.step(lr_on_device=True, gates_ready=True)
-            self.opt2.step(lr_on_device=True, gates_ready=True)
+            # both AdamW updates: two launches (tvq_adamw2) instead of four
+            step_pair(self.opt1, self.opt2, lr_on_device=True, gates_ready=True)
 
         if self.world == 1 and os.environ.get("TVQ_ONE_GRAPH", "1") != "0":
             # one replica: nothing runs between the segments (no collectives, no deferred

@@ -452,6 +452,15 @@ int tvq_adamw_zero(float* params, float* grads, float* exp_avg, float* exp_avg_s
                    const int64_t* chunks, int64_t nchunks, const float* lr_step,
                    const float* gates, const float* seg_step, float beta1, float beta2, float eps,
                    float weight_decay, int64_t zero_grads, tvq_stream_t stream);
+/* Two optimizers' steps in two launches (both step-count updates, then both updates):
+ * for k in {0, 1} exactly tvq_adamw_begin(lr_step[k], lr[k], gates[k], seg_step[k], nseg[k])
+ * followed by tvq_adamw_zero(params[k], ... , zero_grads).  Host arrays of length 2. */
+int tvq_adamw2(float* const* params, float* const* grads, float* const* exp_avg,
+               float* const* exp_avg_sq, const int64_t* const* chunks, const int64_t* nchunks,
+               float* const* lr_step, const float* lr, const float* const* gates,
+               float* const* seg_step, const int64_t* nseg, const float* beta1,
+               const float* beta2, const float* eps, const float* weight_decay,
+               int64_t zero_grads, tvq_stream_t stream);
 /* x-transformers layer dropout (random() < p skips a branch) drawn on the device for
  * n <= 256 branches: keep[i] = U(seed, offset, i) >= p; touched[i] = keep[i], or
  * max(touched[i], keep[i]) when accumulate (a second pass of the prior in one step). */

@@ -54,18 +54,28 @@ __global__ void loss_bwd_kernel(const float* __restrict__ input, const float* __
 // which is what x-transformers' layer dropout produces for a skipped branch.
 constexpr int ADAMW_CHUNK = 4096;
 
-__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p,
-                                                    const float* __restrict__ g,
-                                                    float* __restrict__ m, float* __restrict__ v,
-                                                    const int64_t* __restrict__ chunks,
-                                                    const float* __restrict__ lr_step,
-                                                    const float* __restrict__ gates,
-                                                    const float* __restrict__ seg_step, float b1,
-                                                    float b2, float eps, float wd,
-                                                    float* __restrict__ gz) {
-  const int64_t start = chunks[3 * blockIdx.x];
-  const int len = (int)chunks[3 * blockIdx.x + 1];
-  const int seg = (int)chunks[3 * blockIdx.x + 2];
+struct AdamArgs {  // one optimizer's flat buffers and hyper-parameters
+  float *p, *m, *v;
+  const float* g;
+  const int64_t* chunks;
+  const float *lr_step, *gates;
+  float* seg_step;
+  float b1, b2, eps, wd;
+  float* gz;  // the gradient again when the update zeroes what it reads, else null
+  int nchunks;
+};
+
+__device__ __forceinline__ void adamw_chunk(float* __restrict__ p, const float* __restrict__ g,
+                                            float* __restrict__ m, float* __restrict__ v,
+                                            const int64_t* __restrict__ chunks,
+                                            const float* __restrict__ lr_step,
+                                            const float* __restrict__ gates,
+                                            const float* __restrict__ seg_step, float b1,
+                                            float b2, float eps, float wd,
+                                            float* __restrict__ gz, int chunk) {
+  const int64_t start = chunks[3 * chunk];
+  const int len = (int)chunks[3 * chunk + 1];
+  const int seg = (int)chunks[3 * chunk + 2];
   if (gates[seg] == 0.f) return;
   const double lr = lr_step[0];
   const double t = seg_step[seg];
@@ -91,6 +101,29 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p,
   }
 }
 
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p,
+                                                    const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    const int64_t* __restrict__ chunks,
+                                                    const float* __restrict__ lr_step,
+                                                    const float* __restrict__ gates,
+                                                    const float* __restrict__ seg_step, float b1,
+                                                    float b2, float eps, float wd,
+                                                    float* __restrict__ gz) {
+  adamw_chunk(p, g, m, v, chunks, lr_step, gates, seg_step, b1, b2, eps, wd, gz, blockIdx.x);
+}
+
+// two optimizers' updates in one launch: blocks [0, a0.nchunks) update the first
+struct AdamPair {
+  AdamArgs o[2];
+};
+__global__ __launch_bounds__(256) void adamw2_kernel(AdamPair a) {
+  const int k = (int)blockIdx.x >= a.o[0].nchunks ? 1 : 0;
+  const AdamArgs& o = a.o[k];
+  adamw_chunk(o.p, o.g, o.m, o.v, o.chunks, o.lr_step, o.gates, o.seg_step, o.b1, o.b2, o.eps,
+              o.wd, o.gz, (int)blockIdx.x - (k ? a.o[0].nchunks : 0));
+}
+
 // gates[s] = *gate_ptr[s] (1 where the segment has no gate); then the per-segment step
 // counts advance where the gate is set (torch keeps state['step'] per parameter)
 __global__ void adamw_gates_kernel(const int64_t* __restrict__ gate_ptrs, int64_t nseg,
@@ -102,15 +135,30 @@ __global__ void adamw_gates_kernel(const int64_t* __restrict__ gate_ptrs, int64_
   }
 }
 
-__global__ void adamw_begin_kernel(float* __restrict__ lr_step, float lr,
-                                   const float* __restrict__ gates, float* __restrict__ seg_step,
-                                   int64_t nseg) {
-  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+__device__ __forceinline__ void adamw_begin(float* __restrict__ lr_step, float lr,
+                                            const float* __restrict__ gates,
+                                            float* __restrict__ seg_step, int64_t nseg,
+                                            int64_t s) {
   if (s == 0) {
     if (lr >= 0.f) lr_step[0] = lr;
     lr_step[1] += 1.0f;
   }
   if (s < nseg && gates[s] != 0.f) seg_step[s] += 1.0f;
+}
+
+__global__ void adamw_begin_kernel(float* __restrict__ lr_step, float lr,
+                                   const float* __restrict__ gates, float* __restrict__ seg_step,
+                                   int64_t nseg) {
+  adamw_begin(lr_step, lr, gates, seg_step, nseg, blockIdx.x * (int64_t)blockDim.x + threadIdx.x);
+}
+
+// both optimizers' step counts (blockIdx.y = optimizer)
+__global__ void adamw_begin2_kernel(AdamPair a, float lr0, float lr1, int64_t nseg0,
+                                    int64_t nseg1) {
+  const int k = blockIdx.y;
+  const AdamArgs& o = a.o[k];
+  adamw_begin(const_cast<float*>(o.lr_step), k ? lr1 : lr0, o.gates, o.seg_step, k ? nseg1 : nseg0,
+              blockIdx.x * (int64_t)blockDim.x + threadIdx.x);
 }
 
 // layer-dropout decisions of one x-transformers layer stack (random() < p skips a
@@ -192,6 +240,36 @@ extern "C" int tvq_adamw_zero(float* params, float* grads, float* exp_avg, float
                      params, grads, exp_avg, exp_avg_sq, chunks, lr_step, gates, seg_step, beta1,
                      beta2, eps, weight_decay, zero_grads ? grads : nullptr);
   return launch_status("tvq_adamw");
+}
+
+// Two FusedAdamW updates (their begin + update) as two launches instead of four: the same
+// arithmetic per optimizer as tvq_adamw_begin + tvq_adamw_zero.
+extern "C" int tvq_adamw2(float* const* params, float* const* grads, float* const* exp_avg,
+                          float* const* exp_avg_sq, const int64_t* const* chunks,
+                          const int64_t* nchunks, float* const* lr_step, const float* lr,
+                          const float* const* gates, float* const* seg_step, const int64_t* nseg,
+                          const float* beta1, const float* beta2, const float* eps,
+                          const float* weight_decay, int64_t zero_grads, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && chunks && nchunks && lr_step && lr &&
+                    gates && seg_step && nseg && beta1 && beta2 && eps && weight_decay,
+                "tvq_adamw2: bad arguments");
+  AdamPair a;
+  for (int k = 0; k < 2; ++k) {
+    TVQ_CHECK_ARG(params[k] && grads[k] && exp_avg[k] && exp_avg_sq[k] && chunks[k] && lr_step[k] &&
+                      gates[k] && seg_step[k] && nchunks[k] >= 0 && nseg[k] >= 0,
+                  "tvq_adamw2: bad optimizer %d", k);
+    a.o[k] = {params[k], exp_avg[k], exp_avg_sq[k], grads[k], chunks[k], lr_step[k], gates[k],
+              seg_step[k], beta1[k], beta2[k], eps[k], weight_decay[k],
+              zero_grads ? grads[k] : nullptr, (int)nchunks[k]};
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nmax = nseg[0] > nseg[1] ? nseg[0] : nseg[1];
+  hipLaunchKernelGGL(adamw_begin2_kernel, dim3((unsigned)blocks_for(nmax + 1, 1 << 20), 2),
+                     dim3(256), 0, st, a, lr[0], lr[1], nseg[0], nseg[1]);
+  if (nchunks[0] + nchunks[1] > 0)
+    hipLaunchKernelGGL(adamw2_kernel, dim3((unsigned)(nchunks[0] + nchunks[1])), dim3(256), 0, st,
+                       a);
+  return launch_status("tvq_adamw2");
 }
 
 extern "C" int tvq_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,

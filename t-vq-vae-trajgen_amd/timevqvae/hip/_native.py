@@ -146,6 +146,7 @@ sig("tvq_adamw_gates", P, I64, P, P)
 sig("tvq_adamw_begin", P, F32, P, P, I64, P)
 sig("tvq_adamw", P, P, P, P, P, I64, P, P, P, F32, F32, F32, F32, P)
 sig("tvq_adamw_zero", P, P, P, P, P, I64, P, P, P, F32, F32, F32, F32, I64, P)
+sig("tvq_adamw2", P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I64, P)
 sig("tvq_layer_drop", P, ctypes.c_uint64, F32, I64, P, P, I64, P)
 
 # --- MaskGIT transformer ---------------------------------------------------------

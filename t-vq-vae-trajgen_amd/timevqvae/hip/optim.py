@@ -15,6 +15,8 @@ Each parameter is one segment of the flat buffer with its own step count; a
 parameter tagged `_tvq_gate = (module, i)` (set by the transformer Encoder) is updated
 only when `module._touched[i]` is non-zero after the step's forward passes.
 """
+import ctypes
+
 import torch
 
 from . import streams
@@ -150,3 +152,35 @@ class FusedAdamW(torch.optim.Optimizer):
              float(g["weight_decay"]), int(self.zero_after_step), s)
         self._clean = self.zero_after_step
         return loss
+
+
+@torch.no_grad()
+def step_pair(a: "FusedAdamW", b: "FusedAdamW", lr_on_device=False, gates_ready=False):
+    """a.step(); b.step() -- the same arithmetic -- as two launches instead of four
+    (tvq_adamw2: both optimizers' step counts, then both updates); both zero the gradients
+    they read when their zero_after_step is set (it must agree)."""
+    if a.zero_after_step != b.zero_after_step:
+        raise ValueError("step_pair: zero_after_step differs")
+    streams.join(a.flat.device, backward_done=True)
+    if not gates_ready:
+        a.gather_gates()
+        b.gather_gates()
+    P2 = ctypes.c_void_p * 2
+    I2 = ctypes.c_int64 * 2
+    F2 = ctypes.c_float * 2
+    opts = (a, b)
+    gs = [o.param_groups[0] for o in opts]
+    # every host array is kept in `keep` until the call returns (ctypes passes addresses)
+    keep = [P2(*[ptr(o.flat) for o in opts]), P2(*[ptr(o.flat_grad) for o in opts]),
+            P2(*[ptr(o.exp_avg) for o in opts]), P2(*[ptr(o.exp_avg_sq) for o in opts]),
+            P2(*[ptr(o.chunks) for o in opts]), I2(a.nchunks, b.nchunks),
+            P2(*[ptr(o.lr_step) for o in opts]),
+            F2(*[-1.0 if lr_on_device else float(g["lr"]) for g in gs]),
+            P2(*[ptr(o.gates) for o in opts]), P2(*[ptr(o.seg_step) for o in opts]),
+            I2(a.nseg, b.nseg), F2(*[g["betas"][0] for g in gs]),
+            F2(*[g["betas"][1] for g in gs]), F2(*[g["eps"] for g in gs]),
+            F2(*[g["weight_decay"] for g in gs])]
+    call("tvq_adamw2", *[ctypes.addressof(k) for k in keep], int(a.zero_after_step),
+         stream_ptr())
+    a._clean = a.zero_after_step
+    b._clean = b.zero_after_step

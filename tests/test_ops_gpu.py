@@ -741,3 +741,40 @@ def test_upsample_nearest_t(B, Lin, D, Lout, cuda):
     assert torch.equal(yd.cpu(), yc.detach())
     close(xd.grad, xc.grad, what="dx")
 
+
+
+@pytest.mark.parametrize("zero_after", [False, True])
+def test_adamw_step_pair_equals_two_steps(zero_after, cuda):
+    """hip.optim.step_pair (tvq_adamw2: both optimizers' step counts, then both updates, two
+    launches) gives the same bits as two FusedAdamW.step calls, with different
+    hyper-parameters per optimizer; with zero_after_step the gradients read are zeroed and the
+    next zero_grad launches nothing."""
+    from timevqvae.hip.optim import FusedAdamW, step_pair
+    gen = torch.Generator().manual_seed(4)
+
+    def make():
+        torch.manual_seed(0)
+        m1 = torch.nn.Sequential(torch.nn.Linear(37, 19), torch.nn.Linear(19, 5)).to(cuda)
+        m2 = torch.nn.Linear(300, 77).to(cuda)
+        o1 = FusedAdamW(m1.parameters(), lr=1e-3, weight_decay=0.01)
+        o2 = FusedAdamW(m2.parameters(), lr=3e-4, betas=(0.8, 0.95), eps=1e-6, weight_decay=0.1)
+        o1.zero_after_step = o2.zero_after_step = zero_after
+        return o1, o2
+
+    ref, got = make(), make()
+    for _ in range(3):
+        g1 = torch.randn(ref[0].numel, generator=gen).to(cuda)
+        g2 = torch.randn(ref[1].numel, generator=gen).to(cuda)
+        for (o1, o2) in (ref, got):
+            o1.zero_grad()
+            o2.zero_grad()
+            o1.flat_grad += g1
+            o2.flat_grad += g2
+        ref[0].step()
+        ref[1].step()
+        step_pair(*got)
+        for a, b in zip(ref, got):
+            assert torch.equal(a.flat, b.flat) and torch.equal(a.exp_avg, b.exp_avg)
+            assert torch.equal(a.exp_avg_sq, b.exp_avg_sq) and torch.equal(a.seg_step, b.seg_step)
+            assert torch.equal(a.flat_grad, b.flat_grad)
+            assert bool((b.flat_grad == 0).all()) == zero_after

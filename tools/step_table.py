@@ -28,8 +28,13 @@ def main():
         starts = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
         sel = rows[starts[-steps]:]
     else:
-        ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
-        first = ends[-1 - 2 * steps] + 1
+        # a step ends at its AdamW: one adamw2_kernel (both optimizers) or two adamw_kernel
+        ends = [i for i, r in enumerate(rows) if "adamw2_kernel" in r["Kernel_Name"]]
+        per = 1
+        if not ends:
+            ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
+            per = 2
+        first = ends[-1 - per * steps] + 1
         sel = rows[first:ends[-1] + 1]
     t0 = int(sel[0]["Start_Timestamp"])
     t1 = max(int(r["End_Timestamp"]) for r in sel)

@@ -1,6 +1,7 @@
 """Critical-path view of one graph-replayed step from a rocprofv3 kernel_trace.csv.
 
-The step's last kernels are its AdamW launches (`per_step` of them, one per optimizer):
+The step's last kernels are its AdamW launches (`per_step` of them, one per optimizer; one
+adamw2_kernel for both when the trace has it):
 the last step is everything after the previous step's final AdamW through the last one.
 Prints its wall span, per-queue busy time and kernel families ranked by time per queue.
 usage: python tools/step_timeline.py trace.csv [per_step] [top] [seq_out]
@@ -21,7 +22,11 @@ def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
     per = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 25
-    ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
+    ends = [i for i, r in enumerate(rows) if "adamw2_kernel" in r["Kernel_Name"]]
+    if ends:  # one launch for both optimizers
+        per = 1
+    else:
+        ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
     step = rows[ends[-1 - per] + 1:ends[-1] + 1]
     starts = ends[::per]
     t0 = int(step[0]["Start_Timestamp"])
