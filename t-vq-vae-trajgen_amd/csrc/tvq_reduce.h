@@ -22,8 +22,9 @@ constexpr int RR_ONE_ROWS = 256;
 void reduce_rows_batch(const RrJob* jobs, int n, hipStream_t st);
 // stable group-by of indices in [0,V): offsets[V+1], perm[M]; scratch: group_by_scratch_ints ints
 int64_t group_by_scratch_ints(int64_t M, int64_t V);
+// counts / countsf (optional, V each): the per-value counts as int32 and float
 void group_by_i32(const int32_t* idx, int64_t M, int64_t V, int* offsets, int* perm, int* scratch,
-                  hipStream_t st);
+                  hipStream_t st, int32_t* counts = nullptr, float* countsf = nullptr);
 void group_by_i64(const int64_t* idx, int64_t M, int64_t V, int* offsets, int* perm, int* scratch,
                   hipStream_t st);
 // Rows for seg_rowsum: row m -> src + (m / N)*sB + (m % N)*sN, element d at + d*sD.

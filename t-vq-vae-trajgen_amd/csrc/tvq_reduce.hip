@@ -313,7 +313,9 @@ __global__ __launch_bounds__(1024) void gb_scan_kernel(const int* __restrict__ h
                                                        int V, int* __restrict__ chunk_off,
                                                        int* __restrict__ offsets,
                                                        int* __restrict__ seg_start,
-                                                       int* __restrict__ chunk_v) {
+                                                       int* __restrict__ chunk_v,
+                                                       int32_t* __restrict__ counts,
+                                                       float* __restrict__ countsf) {
   extern __shared__ int tot[];  // [V]
   const int per = (V + 1023) / 1024;
   const int v0 = threadIdx.x * per;
@@ -325,6 +327,10 @@ __global__ __launch_bounds__(1024) void gb_scan_kernel(const int* __restrict__ h
 #pragma unroll 16
     for (int c = 0; c < chunks; ++c) s += hist[(int64_t)c * V + v];
     tot[v] = s;
+    if (counts) {  // the per-value counts (the VQ statistics' counts / cluster sizes)
+      counts[v] = s;
+      countsf[v] = (float)s;
+    }
     t_loc += s;
     s_loc += seg_chunks_of(s);
   }
@@ -373,7 +379,9 @@ __global__ __launch_bounds__(GB1_T) void gb_sort1_kernel(const IT* __restrict__ 
                                                          int* __restrict__ offsets,
                                                          int* __restrict__ perm,
                                                          int* __restrict__ seg_start,
-                                                         int* __restrict__ chunk_v) {
+                                                         int* __restrict__ chunk_v,
+                                                         int32_t* __restrict__ counts,
+                                                         float* __restrict__ countsf) {
   extern __shared__ int gb1_smem[];
   int* hist = gb1_smem;  // [16][V]: counts, then each wave's running offsets
   unsigned short* vals = reinterpret_cast<unsigned short*>(gb1_smem + 16 * V);  // [M]
@@ -411,6 +419,10 @@ __global__ __launch_bounds__(GB1_T) void gb_sort1_kernel(const IT* __restrict__ 
   if (tid < V) {
     offsets[tid] = ex_t;
     seg_start[tid] = ex_c;
+    if (counts) {
+      counts[tid] = tot;
+      countsf[tid] = (float)tot;
+    }
     seg_chunk_info(chunk_v, tid, ex_t, tot, ex_c, nc);
     int run = ex_t;
     for (int k = 0; k < 16; ++k) {
@@ -504,7 +516,7 @@ int64_t group_by_scratch_ints(int64_t M, int64_t V) {
 
 template <typename IT>
 static void group_by_t(const IT* idx, int64_t M, int64_t V, int* offsets, int* perm, int* scratch,
-                       hipStream_t st) {
+                       hipStream_t st, int32_t* counts, float* countsf) {
   const int chunks = (int)((M + GB_CHUNK - 1) / GB_CHUNK);
   int* hist = scratch;
   int* coff = scratch + (int64_t)chunks * V;
@@ -514,14 +526,14 @@ static void group_by_t(const IT* idx, int64_t M, int64_t V, int* offsets, int* p
     const size_t lds = (size_t)16 * V * 4 + (size_t)M * 2;  // <= 68 KB
     TVQ_PLAN("group_by sort1 M%lld V%lld", (long long)M, (long long)V);
     hipLaunchKernelGGL(gb_sort1_kernel<IT>, dim3(1), dim3(GB1_T), lds, st, idx, (int)M, (int)V,
-                       offsets, perm, seg_start, chunk_v);
+                       offsets, perm, seg_start, chunk_v, counts, countsf);
     return;
   }
   TVQ_PLAN("group_by 3-launch M%lld V%lld", (long long)M, (long long)V);
   hipLaunchKernelGGL(gb_hist_kernel<IT>, dim3(chunks), dim3(256), V * sizeof(int), st, idx, M,
                      (int)V, hist);
   hipLaunchKernelGGL(gb_scan_kernel, dim3(1), dim3(1024), V * sizeof(int), st, hist, chunks, (int)V,
-                     coff, offsets, seg_start, chunk_v);
+                     coff, offsets, seg_start, chunk_v, counts, countsf);
   if (V <= GB_PLACE_MAX_V)
     hipLaunchKernelGGL(gb_place_kernel<IT>, dim3(chunks), dim3(GB_CHUNK),
                        (size_t)(GB_CHUNK / 64) * V * sizeof(int), st, idx, M, (int)V, coff, perm);
@@ -531,12 +543,12 @@ static void group_by_t(const IT* idx, int64_t M, int64_t V, int* offsets, int* p
 }
 
 void group_by_i32(const int32_t* idx, int64_t M, int64_t V, int* offsets, int* perm, int* scratch,
-                  hipStream_t st) {
-  group_by_t<int32_t>(idx, M, V, offsets, perm, scratch, st);
+                  hipStream_t st, int32_t* counts, float* countsf) {
+  group_by_t<int32_t>(idx, M, V, offsets, perm, scratch, st, counts, countsf);
 }
 void group_by_i64(const int64_t* idx, int64_t M, int64_t V, int* offsets, int* perm, int* scratch,
                   hipStream_t st) {
-  group_by_t<int64_t>(idx, M, V, offsets, perm, scratch, st);
+  group_by_t<int64_t>(idx, M, V, offsets, perm, scratch, st, nullptr, nullptr);
 }
 
 // Segmented row sums in one launch: block c takes chunk c of the sorted rows (SEG_CH rows of

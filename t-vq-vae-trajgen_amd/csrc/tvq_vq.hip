@@ -244,15 +244,6 @@ __global__ __launch_bounds__(128 * RG) void vq_assign_kernel(
 }
 
 // counts[k] = offsets[k+1] - offsets[k] (from the stable group-by of idx32)
-__global__ void vq_counts_kernel(const int* __restrict__ offsets, int K, int32_t* __restrict__ counts,
-                                 float* __restrict__ cs_batch) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  const int c = offsets[k + 1] - offsets[k];
-  counts[k] = c;
-  cs_batch[k] = (float)c;
-}
-
 __global__ void vq_ema_kernel(const float* __restrict__ cs_batch, const float* __restrict__ es_batch,
                               int D, float decay, float alpha, float* __restrict__ cluster_size,
                               float* __restrict__ embed_avg) {
@@ -427,9 +418,8 @@ extern "C" int tvq_vq_stats(const float* x, int64_t B, int64_t N, int64_t D, int
   int* scratch = perm + M;
   const int64_t ints = (K + 1) + M + group_by_scratch_ints(M, K);
   float* part = (float*)(workspace + ((ints + 3) / 4) * 4);
-  group_by_i32(idx32, M, K, offsets, perm, scratch, st);
-  hipLaunchKernelGGL(vq_counts_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st, offsets,
-                     (int)K, counts, cs_batch);
+  // the per-code counts (and their float copy, cs_batch) come out of the group-by's scan
+  group_by_i32(idx32, M, K, offsets, perm, scratch, st, counts, cs_batch);
   if (es_batch) {
     SegRows r;
     r.src = x; r.N = N; r.sB = sB; r.sN = sN; r.sD = sD; r.D = (int)D;

@@ -129,9 +129,12 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
     call("tvq_vq_assign_rows", ptr(x), B, N, D, sB, sN, sD, ptr(embed), ptr(ee), K,
          int(bool(straight_through)), float(svq_temp or 0.0), ptr(gumbel), ptr(seed), off,
          ptr(out), ptr(idx), ptr(idx32), ptr(partial), ptr(rows), s)
-    commit = None
-    if straight_through:  # the loss reads it: stays on the current stream
-        commit = torch.empty((), device=dev, dtype=torch.float32)
+    commit = torch.empty((), device=dev, dtype=torch.float32) if straight_through else None
+    # the commitment mean is read only by the loss report at the band's end (its gradient
+    # does not need it): it joins the statistics' finish launch unless those are skipped or
+    # offloaded to another stream (then it is finished here, on the current stream)
+    late = not (_indices_only[0] and not ema) and "vq" not in streams.OFFLOAD
+    if straight_through and not late:
         call("tvq_vq_finalize", None, None, K, D, float(eps), None, None, M, None, ptr(partial),
              nb, ptr(commit), s)
     # per-code statistics, EMA and perplexity: nothing downstream of the quantised output
@@ -140,13 +143,18 @@ def vq_codebook_pass(x, embed, cluster_size, embed_avg, *, straight_through, ema
     if _indices_only[0] and not ema:
         return out, idx, commit, None, None
     src = rows.view(1, M, D) if rows is not None else x
+    cm = (partial, nb, commit) if straight_through and late else (None, 0, None)
     with streams.offload(src, idx32, kind="vq"):
         counts, perp = _codebook_stats(src, idx32, embed, cluster_size, embed_avg, ema, decay,
-                                       eps, sync)
+                                       eps, sync, cm)
     return out, idx, commit, perp, counts
 
 
-def _codebook_stats(x, idx32, embed, cluster_size, embed_avg, ema, decay, eps, sync):
+def _codebook_stats(x, idx32, embed, cluster_size, embed_avg, ema, decay, eps, sync,
+                    cm=(None, 0, None)):
+    """cm = (commit partials, their count, commit): the commitment mean, finished by the
+    same vq_finalize launch as the perplexity."""
+    cpart, nb, commit = cm
     B, N, D = x.shape
     K = embed.shape[0]
     M = B * N
@@ -163,7 +171,7 @@ def _codebook_stats(x, idx32, embed, cluster_size, embed_avg, ema, decay, eps, s
     if ema and _pending is not None:
         _pending.append(CodebookUpdate(cs_b, es_b, cluster_size, embed_avg, embed, decay, eps, sync))
         call("tvq_vq_finalize", None, None, K, D, float(eps), None, ptr(counts), M, ptr(perp),
-             None, 0, None, s)
+             ptr(cpart), nb, ptr(commit), s)
     elif ema:
         if sync is not None:
             sync(cs_b)
@@ -172,11 +180,11 @@ def _codebook_stats(x, idx32, embed, cluster_size, embed_avg, ema, decay, eps, s
         call("tvq_vq_ema", ptr(cs_b), ptr(es_b), K, D, float(decay), ptr(cluster_size),
              ptr(embed_avg), s)
         call("tvq_vq_finalize", ptr(cluster_size), ptr(embed_avg), K, D, float(eps), ptr(embed),
-             ptr(counts), M, ptr(perp), None, 0, None, s)
+             ptr(counts), M, ptr(perp), ptr(cpart), nb, ptr(commit), s)
         streams.fence(embed.data_ptr())
     else:
         call("tvq_vq_finalize", None, None, K, D, float(eps), None, ptr(counts), M, ptr(perp),
-             None, 0, None, s)
+             ptr(cpart), nb, ptr(commit), s)
     return counts, perp
 
 
