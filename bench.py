@@ -155,10 +155,9 @@ class JointTrainer:
         from timevqvae.hip.conv import wgrad_deferred
         with (packs.scope() if packs is not None else contextlib.nullcontext()), \
                 streams.concurrent():
-            out2 = self.s2.training_step(batch, 0)
             with wgrad_deferred(this_stream_only=True), wgrad.grouped():
-                out2["loss"].backward(self._one)
-        return out2
+                hist2 = self.s2.forward_backward(batch, self._one)
+        return hist2()
 
     def _fwd_bwd(self, batch, defer, only=None, packs=None):
         """zero_grad, then stage1's LF and HF bands (forward+backward, one side stream
@@ -183,14 +182,15 @@ class JointTrainer:
                 bands = tuple(os.environ.get("TVQ_BENCH_BANDS", "HF,LF").split(","))
                 hist1 = self.s1.forward_backward(batch, 0, bands) if only != "stage2" else None
             if only != "stage1":
-                out2 = self.s2.training_step(batch, 0)
-                # Linear weight gradients: one grouped launch per stream; the conv and norm
-                # weight-gradient reductions issued on this stream: one batch at the end
+                # each prior backpropagated from its own loss on its own stream
+                # (MaskGIT.forward_backward); Linear weight gradients: one grouped launch per
+                # stream, the conv / norm weight-gradient reductions one batch per stream
                 with wgrad_deferred(this_stream_only=True), wgrad.grouped():
-                    out2["loss"].backward(self._one)  # cached ones: no fill launch per step
+                    hist2 = self.s2.forward_backward(batch, self._one)  # cached ones root
             else:
-                out2 = {"loss": torch.zeros(())}
-        return (hist1() if hist1 else {"loss": torch.zeros(())}), out2, pend
+                hist2 = None
+        return ((hist1() if hist1 else {"loss": torch.zeros(())}),
+                (hist2() if hist2 else {"loss": torch.zeros(())}), pend)
 
     def step(self, batch):
         if self.graph is not None:

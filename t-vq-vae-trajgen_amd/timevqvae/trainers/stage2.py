@@ -31,6 +31,22 @@ class Stage2(nn.Module):
         return {"loss": mask_pred_loss, "mask_pred_loss": mask_pred_loss,
                 "mask_pred_loss_l": loss_l, "mask_pred_loss_h": loss_h}
 
+    def forward_backward(self, batch, one):
+        """training_step + the backward of its loss, each prior backpropagated from its own
+        loss on its own stream (MaskGIT.forward_backward: the same gradients as
+        loss.backward()).  `one`: a cached 0-dim ones tensor.  Returns a callable building
+        training_step's dict; call it after the streams are joined."""
+        x, y = batch
+        total = self.maskgit.forward_backward(x, y, one)
+        if self._sched is not None:
+            self._sched.step()
+
+        def out():
+            loss, (loss_l, loss_h) = total()
+            return {"loss": loss, "mask_pred_loss": loss, "mask_pred_loss_l": loss_l,
+                    "mask_pred_loss_h": loss_h}
+        return out
+
     @torch.no_grad()
     def validation_step(self, batch, batch_idx):
         self.eval()

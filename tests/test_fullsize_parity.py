@@ -497,3 +497,50 @@ def test_stage2_step_full_size_vs_oracle(cuda):
     for k, v in outs["hf"][2].updates.items():
         if k.endswith(("running_mean", "running_var")):
             assert rel(post[k], v) < 1e-5, k
+
+
+def test_stage2_per_prior_backward_roots_bitwise(cuda):
+    """MaskGIT.forward_backward (each prior backpropagated from its own loss on its own
+    stream, the bench's stage2 path) gives bit for bit the gradients and losses of
+    forward() + loss.backward() on the same draws (B = 256, the bench's priors, layer dropout
+    on the device seed, reset between the two runs)."""
+    from timevqvae.hip import rng, streams, wgrad
+    from timevqvae.hip.conv import PackCache, wgrad_deferred
+    from timevqvae.trainers import Stage1, Stage2
+    from timevqvae.utils import set_seed
+    set_seed(0)
+    cfg = _bench_config()
+    s1 = Stage1(T, C, cfg)
+    s2 = Stage2(None, None, T, C, 5, config=cfg, stage1=copy.deepcopy(s1)).to(cuda).train()
+    mg = s2.maskgit
+    opt = s2.configure_optimizers()["optimizer"]
+    s2._sched = None
+    nl, nh = mg.num_tokens_l, mg.num_tokens_h
+    g = torch.Generator().manual_seed(7)
+    npr = np.random.default_rng(3)
+    draws = {"ratio_l": npr.uniform(0, 1, B), "rand_l": torch.rand(B, nl, generator=g),
+             "ratio_h": npr.uniform(0, 1, B), "rand_h": torch.rand(B, nh, generator=g),
+             "cls_l": torch.rand(B, 1, generator=g), "cls_h": torch.rand(B, 1, generator=g)}
+    x, y = _batch()
+    xd, yd = x.to(cuda), y.to(cuda)
+    one = torch.ones((), device=cuda)
+    packs = PackCache(cuda)
+    res = []
+    for split in (False, True):
+        rng.manual_seed(11)
+        rng.restart_calls()
+        opt.zero_grad()
+        with packs.scope(), streams.concurrent():
+            with wgrad_deferred(this_stream_only=True), wgrad.grouped():
+                if split:
+                    total = mg.forward_backward(xd, yd, one, draws=draws)
+                else:
+                    loss, parts = mg(xd, yd, draws=draws)
+                    loss.backward(one)
+        if split:
+            loss, parts = total()
+        torch.cuda.synchronize()
+        res.append((opt.flat_grad.clone(), float(loss), [float(p) for p in parts]))
+    assert res[0][0].abs().sum() > 0
+    assert torch.equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1] and res[0][2] == res[1][2]
