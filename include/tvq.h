@@ -345,6 +345,31 @@ int tvq_resblock_bwd(const float* dy, const float* x, const float* h, int64_t B,
                      const int64_t* seed_ptr, uint64_t offset, float* dx, float* da1, float* dw1,
                      float* db1, float* dbn_w, float* dbn_b, float* da2, float* dw2, float* db2,
                      int64_t accumulate, void* workspace, tvq_stream_t stream);
+/* Two consecutive identity ResBlocks of the encoder / decoder stacks (vq_vae.py:143-170,
+ * 211-251: n_resnet_blocks = 2 per level) as one chain: forward rb_fwd1(1) | rb_fwd21 |
+ * rb_fwd2(2), backward rb_bwd2(2) | rb_bwd12 | rb_bwd1(1), the middle launch running one
+ * block's last kernel and the other's first on the same images with the activation handed
+ * over in registers; bitwise equal to the two blocks' tvq_resblock_train_fwd / _bwd.
+ * Parameter arrays (host arrays of device pointers): p = {a1, w1, b1, bn_w, bn_b, a2, w2, b2},
+ * rs = {running_mean, running_var}, q = {a1, w1, bn_w, save, a2, w2},
+ * g = {da1, dw1, db1, dbn_w, dbn_b, da2, dw2, db2}.  Each block has its own workspace
+ * (tvq_resblock_workspace bytes) and saved buffers; y1 (block 1's output) is block 2's
+ * input, dy1 receives the gradient at it.  1 when the shape takes this path (C in
+ * {8, 16, 32}), else 0. */
+int tvq_resblock_pair_supported(int64_t B, int64_t C, int64_t H, int64_t W);
+int tvq_resblock_pair_train_fwd(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
+                                const float* const* p1, const float* const* p2,
+                                float* const* rs1, float* const* rs2, int64_t* nbt1,
+                                int64_t* nbt2, float momentum, float eps, float drop_p,
+                                const int64_t* seed_ptr, uint64_t offset1, uint64_t offset2,
+                                float* h1, float* y1, float* save1, float* h2, float* y2,
+                                float* save2, void* ws1, void* ws2, tvq_stream_t stream);
+int tvq_resblock_pair_bwd(const float* dy, const float* x, int64_t B, int64_t C, int64_t H,
+                          int64_t W, const float* const* q1, const float* const* q2,
+                          const float* h1, const float* y1, const float* h2, float drop_p,
+                          const int64_t* seed_ptr, uint64_t offset1, uint64_t offset2, float* dx,
+                          float* dy1, float* const* g1, float* const* g2, int64_t accumulate,
+                          void* ws1, void* ws2, tvq_stream_t stream);
 /* Fused projection ResBlock (in_channels != out_channels, the 1x1 `proj` on the skip) on the
  * LF band's W = 8 maps: Ci -> Co in {64 -> 128, 128 -> 64}, H = 3 (csrc/tvq_resblock_w8p.hip;
  * reference vq_vae.py:13-62):

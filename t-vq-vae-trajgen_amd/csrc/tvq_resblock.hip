@@ -469,9 +469,16 @@ __device__ __forceinline__ void rb_batch_sums(const double* __restrict__ part, i
 }
 
 // ---------------------------------------------------------------- kernels
+// The kernels' bodies take the block's LDS and, for the fused pairs of consecutive
+// ResBlocks (rb_fwd21 / rb_bwd12 below), the activation handed over in registers: the
+// elementwise layout (RBElems) is the same in every kernel of a shape, so each lane hands
+// over exactly the elements it consumes next.
 template <class R>
-__global__ __launch_bounds__(RB_T) void rb_fwd1_kernel(RBArgs a) {
-  extern __shared__ double rb_smem[];
+using RBRegs = float[R::CPW][R::PPL];
+
+template <class R, bool XREG>
+__device__ __forceinline__ void rb_fwd1_body(const RBArgs& a, double* rb_smem,
+                                             const RBRegs<R>& xin) {
   float* S = reinterpret_cast<float*>(rb_smem);
   float* A = S + R::PLANE;
   float* Pc = A + R::PANEL;
@@ -481,7 +488,14 @@ __global__ __launch_bounds__(RB_T) void rb_fwd1_kernel(RBArgs a) {
   const RBElems<R> el;
   float v[R::CPW][R::PPL], pv[R::UP], a1[R::CPW], b1[R::CPW];
   rb_load_panel<R, false>(a.w1, pv);  // first: the panel store waits for these alone
-  rb_load<R>(a.x, img0, el, v);
+  if constexpr (XREG) {
+#pragma unroll
+    for (int u = 0; u < R::CPW; ++u)
+#pragma unroll
+      for (int q = 0; q < R::PPL; ++q) v[u][q] = xin[u][q];
+  } else {
+    rb_load<R>(a.x, img0, el, v);
+  }
   rb_param<R>(a.a1, el, a1);
   rb_param<R>(a.b1, el, b1);
   rb_border<R>(S);
@@ -515,8 +529,15 @@ __global__ __launch_bounds__(RB_T) void rb_fwd1_kernel(RBArgs a) {
 }
 
 template <class R>
-__global__ __launch_bounds__(RB_T) void rb_fwd2_kernel(RBArgs a) {
+__global__ __launch_bounds__(RB_T) void rb_fwd1_kernel(RBArgs a) {
   extern __shared__ double rb_smem[];
+  RBRegs<R> none;
+  rb_fwd1_body<R, false>(a, rb_smem, none);
+}
+
+// yout: this lane's y elements (the next block's input in a fused pair)
+template <class R>
+__device__ __forceinline__ void rb_fwd2_body(const RBArgs& a, double* rb_smem, RBRegs<R>& yout) {
   float* S = reinterpret_cast<float*>(rb_smem);
   float* A = S + R::PLANE;
   float* Pc = A + R::PANEL;
@@ -561,13 +582,32 @@ __global__ __launch_bounds__(RB_T) void rb_fwd2_kernel(RBArgs a) {
   for (int u = 0; u < R::CPW; ++u)
 #pragma unroll
     for (int q = 0; q < R::PPL; ++q) {
+      yout[u][q] = 0.f;
       if (!el.ok(u, q)) continue;
       const int64_t gi = el.gi(img0, u, q);
       float val = rb_conv_at<R>(Pc, el, u, q) + b2[u];
       if (a.drop_p > 0.f)
         val = uniform01(seed, (uint64_t)gi) >= a.drop_p ? val * a.drop_scale : 0.f;
-      a.y[gi] = xr[u][q] + val;
+      yout[u][q] = xr[u][q] + val;
+      a.y[gi] = yout[u][q];
     }
+}
+
+template <class R>
+__global__ __launch_bounds__(RB_T) void rb_fwd2_kernel(RBArgs a) {
+  extern __shared__ double rb_smem[];
+  RBRegs<R> y;
+  rb_fwd2_body<R>(a, rb_smem, y);
+}
+
+// fwd2 of ResBlock 1 and fwd1 of ResBlock 2 (its input = ResBlock 1's output) in one launch
+template <class R>
+__global__ __launch_bounds__(RB_T) void rb_fwd21_kernel(RBArgs a1, RBArgs a2) {
+  extern __shared__ double rb_smem[];
+  RBRegs<R> y;
+  rb_fwd2_body<R>(a1, rb_smem, y);
+  __syncthreads();  // LDS reused
+  rb_fwd1_body<R, true>(a2, rb_smem, y);
 }
 
 template <class R>
@@ -626,9 +666,9 @@ __global__ __launch_bounds__(RB_T) void rb_eval_kernel(RBArgs a) {
       if (el.ok(u, q)) a.y[el.gi(img0, u, q)] = v[u][q] + (rb_conv_at<R>(Pc, el, u, q) + b2[u]);
 }
 
-template <class R>
-__global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
-  extern __shared__ double rb_smem[];
+template <class R, bool DYREG>
+__device__ __forceinline__ void rb_bwd2_body(const RBArgs& a, double* rb_smem,
+                                             const RBRegs<R>& dyin) {
   float* G = reinterpret_cast<float*>(rb_smem);  // g2 planes
   float* S = G + R::PLANE;                         // s2 planes
   float* A = S + R::PLANE;                         // transposed w2
@@ -642,7 +682,14 @@ __global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
   float vg[R::CPW][R::PPL], vh[R::CPW][R::PPL], pv[R::UP];
   float a2[R::CPW], sc[R::CPW], sh[R::CPW], mu[R::CPW], is[R::CPW];
   rb_load_panel<R, true>(a.w2, pv);
-  rb_load<R>(a.dy, img0, el, vg);
+  if constexpr (DYREG) {
+#pragma unroll
+    for (int u = 0; u < R::CPW; ++u)
+#pragma unroll
+      for (int q = 0; q < R::PPL; ++q) vg[u][q] = dyin[u][q];
+  } else {
+    rb_load<R>(a.dy, img0, el, vg);
+  }
   rb_load<R>(a.h, img0, el, vh);
   rb_param<R>(a.a2, el, a2);
   rb_param<R>(a.save + 2 * R::C, el, sc);
@@ -703,8 +750,15 @@ __global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
 }
 
 template <class R>
-__global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
+__global__ __launch_bounds__(RB_T) void rb_bwd2_kernel(RBArgs a) {
   extern __shared__ double rb_smem[];
+  RBRegs<R> none;
+  rb_bwd2_body<R, false>(a, rb_smem, none);
+}
+
+// dxout: this lane's dx elements (the previous block's output gradient in a fused pair)
+template <class R>
+__device__ __forceinline__ void rb_bwd1_body(const RBArgs& a, double* rb_smem, RBRegs<R>& dxout) {
   float* G = reinterpret_cast<float*>(rb_smem);  // dh planes
   float* S = G + R::PLANE;                         // s1 planes
   float* A = S + R::PLANE;                         // transposed w1
@@ -769,6 +823,7 @@ __global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
 #pragma unroll
     for (int q = 0; q < R::PPL; ++q) {
       s[0][u][q] = 0.0;
+      dxout[u][q] = 0.f;
       if (!el.ok(u, q)) continue;
       const float av = a1[u], inv_a = 1.0f / av;
       const float xv = vx[u][q];
@@ -777,13 +832,32 @@ __global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
       sincosf(av * xv, &sn, &cs);
       const float t = 2.0f * sn * cs;
       // snake_bwd_kernel, plus the identity skip's gradient
-      a.dx[el.gi(img0, u, q)] = (gs + gs * inv_a * t * av) + vy[u][q];
+      dxout[u][q] = (gs + gs * inv_a * t * av) + vy[u][q];
+      a.dx[el.gi(img0, u, q)] = dxout[u][q];
       s[0][u][q] = (double)(gs * inv_a * t * xv) - (double)(gs * (sn * sn) * inv_a * inv_a);
     }
   RB_MARK(5);
   // this image's da1 term per channel -> its row of the da1 slab
   rb_slab_row_sums<R>(s, 0, el, b, a.slabda);
   RB_MARK(6);
+}
+
+template <class R>
+__global__ __launch_bounds__(RB_T) void rb_bwd1_kernel(RBArgs a) {
+  extern __shared__ double rb_smem[];
+  RBRegs<R> dx;
+  rb_bwd1_body<R>(a, rb_smem, dx);
+}
+
+// bwd1 of ResBlock 2 and bwd2 of ResBlock 1 (its output gradient = ResBlock 2's input
+// gradient) in one launch
+template <class R>
+__global__ __launch_bounds__(RB_T) void rb_bwd12_kernel(RBArgs a2, RBArgs a1) {
+  extern __shared__ double rb_smem[];
+  RBRegs<R> d;
+  rb_bwd1_body<R>(a2, rb_smem, d);
+  __syncthreads();  // LDS reused
+  rb_bwd2_body<R, true>(a1, rb_smem, d);
 }
 
 // ---------------------------------------------------------------- host side
@@ -832,6 +906,28 @@ static void rb_launch(int kind, const RBArgs& a, hipStream_t st) {
 #endif
 }
 
+// a fused pair of consecutive ResBlocks' kernels: kind 0 = rb_fwd21 (first = block 1,
+// second = block 2), kind 1 = rb_bwd12 (first = block 2, second = block 1)
+template <class R>
+static void rb_launch_pair(int kind, const RBArgs& first, const RBArgs& second, hipStream_t st) {
+  const size_t lf = rb_lds<R>(0) > rb_lds<R>(1) ? rb_lds<R>(0) : rb_lds<R>(1);
+  const size_t lb = rb_lds<R>(3) > rb_lds<R>(4) ? rb_lds<R>(3) : rb_lds<R>(4);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rb_fwd21_kernel<R>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lf);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rb_bwd12_kernel<R>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+    attr = true;
+  }
+  const dim3 grid(first.B), block(RB_T);
+  TVQ_PLAN("%s C%d W%d B%d", kind == 0 ? "rb_fwd21" : "rb_bwd12", R::C, R::W, first.B);
+  if (kind == 0)
+    hipLaunchKernelGGL(rb_fwd21_kernel<R>, grid, block, lf, st, first, second);
+  else
+    hipLaunchKernelGGL(rb_bwd12_kernel<R>, grid, block, lb, st, first, second);
+}
+
 // the (C, W) instantiations: C in {8, 16, 32}, W in {16, 32, 64}, C*W <= 1024
 #define RB_SHAPES(X) X(8, 16) X(8, 32) X(8, 64) X(16, 16) X(16, 32) X(16, 64) X(32, 16) X(32, 32)
 
@@ -856,6 +952,18 @@ static bool rb_dispatch(int C, int W, int kind, const RBArgs* a_in, hipStream_t 
     }                                                                           \
     if (a) rb_launch<R>(kind, *a, st);                                          \
     return true;                                                                \
+  }
+  RB_SHAPES(RB_CASE)
+#undef RB_CASE
+  return false;
+}
+
+static bool rb_dispatch_pair(int C, int W, int kind, const RBArgs& first,
+                             const RBArgs& second, hipStream_t st) {
+#define RB_CASE(CC, WW)                                    \
+  if (C == CC && W == WW) {                                \
+    rb_launch_pair<RB<CC, WW>>(kind, first, second, st);   \
+    return true;                                           \
   }
   RB_SHAPES(RB_CASE)
 #undef RB_CASE
@@ -909,6 +1017,61 @@ int w8_bwd(const float* dy, const float* x, const float* saved, int64_t B, const
            float* da1, float* dw1, float* db1, float* dbn_w, float* dbn_b, float* da2, float* dw2,
            float* db2, int64_t accumulate, void* workspace, hipStream_t st);
 
+static RBArgs rb_fwd_args(const float* x, int64_t B, int64_t C, int64_t W, const float* a1,
+                          const float* w1, const float* b1, const float* bn_w, const float* bn_b,
+                          float* running_mean, float* running_var, int64_t* nbt, float momentum,
+                          float eps, const float* a2, const float* w2, const float* b2,
+                          float drop_p, const int64_t* seed_ptr, uint64_t offset, float* h,
+                          float* y, float* save, void* workspace) {
+  RBArgs a = {};
+  a.x = x; a.h = h; a.a1 = a1; a.w1 = w1; a.b1 = b1; a.a2 = a2; a.w2 = w2; a.b2 = b2;
+  a.save = save; a.h_out = h; a.y = y;
+  a.part = (double*)workspace;
+  a.B = (int)B;
+  a.drop_p = drop_p;
+  a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  a.seed_ptr = seed_ptr;
+  a.offset = offset;
+  a.fin = {(int)C, (int)B, B * 3 * W, eps, momentum, bn_w, bn_b, running_mean, running_var,
+           nbt, save, save + C, save + 2 * C, save + 3 * C};
+  return a;
+}
+
+static RBArgs rb_bwd_args(const float* dy, const float* x, const float* h, int64_t B, int64_t C,
+                          int64_t W, const float* a1, const float* w1, const float* bn_w,
+                          const float* save, const float* a2, const float* w2, float drop_p,
+                          const int64_t* seed_ptr, uint64_t offset, float* dx, float* dbn_w,
+                          float* dbn_b, int64_t accumulate, void* workspace) {
+  const RBWs w = rb_ws(B, C, W);
+  char* ws = (char*)workspace;
+  RBArgs a = {};
+  a.x = x; a.h = h; a.dy = dy; a.a1 = a1; a.w1 = w1; a.a2 = a2; a.w2 = w2; a.bn_w = bn_w;
+  a.save = save;
+  a.slabda2 = (float*)(ws + w.slabda2);
+  a.du = (float*)(ws + w.du); a.dx = dx;
+  a.slab1 = (float*)(ws + w.slab1); a.slab2 = (float*)(ws + w.slab2);
+  a.slabda = (float*)(ws + w.slabda);
+  a.part = (double*)(ws + w.part);
+  a.B = (int)B; a.accumulate = (int)accumulate;
+  a.drop_p = drop_p;
+  a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  a.seed_ptr = seed_ptr; a.offset = offset;
+  a.invN = 1.0f / (float)(B * 3 * W);
+  a.bfin = {(int)C, (int)B, nullptr, dbn_w, dbn_b, nullptr, (int)accumulate};
+  return a;
+}
+
+// the weight gradients out of the backward kernels' per-image slabs (deferred in a
+// wgrad_deferred region)
+static void rb_bwd_finish(const RBArgs& a, int64_t C, float* da1, float* dw1, float* db1,
+                          float* da2, float* dw2, float* db2, hipStream_t st) {
+  const int64_t kc = 9 * C + 1;
+  conv_wgrad_finish(a.slab2, a.B, C, kc, dw2, db2, a.accumulate, st);
+  conv_wgrad_finish(a.slab1, a.B, C, kc, dw1, db1, a.accumulate, st);
+  conv_wgrad_finish(a.slabda, a.B, C, 1, da1, nullptr, a.accumulate, st);
+  conv_wgrad_finish(a.slabda2, a.B, C, 1, da2, nullptr, a.accumulate, st);
+}
+
 }  // namespace tvq
 
 using namespace tvq;
@@ -954,17 +1117,9 @@ extern "C" int tvq_resblock_train_fwd(const float* x, int64_t B, int64_t C, int6
     return w8_train_fwd(x, B, a1, w1, b1, bn_w, bn_b, running_mean, running_var,
                         num_batches_tracked, momentum, eps, a2, w2, b2, drop_p, seed_ptr, offset, h,
                         y, save, workspace, st);
-  RBArgs a = {};
-  a.x = x; a.h = h; a.a1 = a1; a.w1 = w1; a.b1 = b1; a.a2 = a2; a.w2 = w2; a.b2 = b2;
-  a.save = save; a.h_out = h; a.y = y;
-  a.part = (double*)workspace;
-  a.B = (int)B;
-  a.drop_p = drop_p;
-  a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
-  a.seed_ptr = seed_ptr;
-  a.offset = offset;
-  a.fin = {(int)C, (int)B, B * 3 * W, eps, momentum, bn_w, bn_b, running_mean, running_var,
-           num_batches_tracked, save, save + C, save + 2 * C, save + 3 * C};
+  const RBArgs a = rb_fwd_args(x, B, C, W, a1, w1, b1, bn_w, bn_b, running_mean, running_var,
+                               num_batches_tracked, momentum, eps, a2, w2, b2, drop_p, seed_ptr,
+                               offset, h, y, save, workspace);
   rb_dispatch((int)C, (int)W, 0, &a, st, nullptr);
   rb_dispatch((int)C, (int)W, 1, &a, st, nullptr);
   return launch_status("tvq_resblock_train_fwd");
@@ -1009,30 +1164,81 @@ extern "C" int tvq_resblock_bwd(const float* dy, const float* x, const float* h,
   if (w8)
     return w8_bwd(dy, x, h, B, a1, w1, bn_w, save, a2, w2, drop_p, seed_ptr, offset, dx, da1, dw1,
                   db1, dbn_w, dbn_b, da2, dw2, db2, accumulate, workspace, st);
-  const RBWs w = rb_ws(B, C, W);
-  char* ws = (char*)workspace;
-  float* slab2 = (float*)(ws + w.slab2);
-  float* slab1 = (float*)(ws + w.slab1);
-  RBArgs a = {};
-  a.x = x; a.h = h; a.dy = dy; a.a1 = a1; a.w1 = w1; a.a2 = a2; a.w2 = w2; a.bn_w = bn_w;
-  a.save = save;
-  float* slabda = (float*)(ws + w.slabda);
-  float* slabda2 = (float*)(ws + w.slabda2);
-  a.slabda2 = slabda2;
-  a.du = (float*)(ws + w.du); a.dx = dx; a.slab1 = slab1; a.slab2 = slab2; a.slabda = slabda;
-  a.part = (double*)(ws + w.part);
-  a.B = (int)B; a.accumulate = (int)accumulate;
-  a.drop_p = drop_p;
-  a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
-  a.seed_ptr = seed_ptr; a.offset = offset;
-  a.invN = 1.0f / (float)(B * 3 * W);
-  a.bfin = {(int)C, (int)B, nullptr, dbn_w, dbn_b, nullptr, (int)accumulate};
+  const RBArgs a = rb_bwd_args(dy, x, h, B, C, W, a1, w1, bn_w, save, a2, w2, drop_p, seed_ptr,
+                               offset, dx, dbn_w, dbn_b, accumulate, workspace);
   rb_dispatch((int)C, (int)W, 3, &a, st, nullptr);
   rb_dispatch((int)C, (int)W, 4, &a, st, nullptr);
-  const int64_t kc = 9 * C + 1;
-  conv_wgrad_finish(slab2, (int)B, C, kc, dw2, db2, (int)accumulate, st);
-  conv_wgrad_finish(slab1, (int)B, C, kc, dw1, db1, (int)accumulate, st);
-  conv_wgrad_finish(slabda, (int)B, C, 1, da1, nullptr, (int)accumulate, st);
-  conv_wgrad_finish(slabda2, (int)B, C, 1, da2, nullptr, (int)accumulate, st);
+  rb_bwd_finish(a, C, da1, dw1, db1, da2, dw2, db2, st);
   return launch_status("tvq_resblock_bwd");
+}
+
+extern "C" int tvq_resblock_pair_supported(int64_t B, int64_t C, int64_t H, int64_t W) {
+  return !w8_supported(B, C, H, W) && rb_supported(B, C, H, W);
+}
+
+extern "C" int tvq_resblock_pair_train_fwd(const float* x, int64_t B, int64_t C, int64_t H,
+                                           int64_t W, const float* const* p1,
+                                           const float* const* p2, float* const* rs1,
+                                           float* const* rs2, int64_t* nbt1, int64_t* nbt2,
+                                           float momentum, float eps, float drop_p,
+                                           const int64_t* seed_ptr, uint64_t offset1,
+                                           uint64_t offset2, float* h1, float* y1, float* save1,
+                                           float* h2, float* y2, float* save2, void* ws1,
+                                           void* ws2, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(tvq_resblock_pair_supported(B, C, H, W),
+                "tvq_resblock_pair_train_fwd: unsupported shape");
+  TVQ_CHECK_ARG(x && p1 && p2 && rs1 && rs2 && h1 && y1 && save1 && h2 && y2 && save2 && ws1 &&
+                    ws2 && aligned16(x) && aligned16(h1) && aligned16(h2) && aligned16(y1),
+                "tvq_resblock_pair_train_fwd: bad arguments");
+  for (int i = 0; i < 8; ++i)
+    TVQ_CHECK_ARG((p1[i] && p2[i]) || i == 2 || i == 3 || i == 4 || i == 7,
+                  "tvq_resblock_pair_train_fwd: missing parameter");
+  TVQ_CHECK_ARG(rs1[0] && rs1[1] && rs2[0] && rs2[1],
+                "tvq_resblock_pair_train_fwd: missing running statistics");
+  TVQ_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || seed_ptr),
+                "tvq_resblock_pair_train_fwd: bad dropout");
+  hipStream_t st = (hipStream_t)stream;
+  // p = {a1, w1, b1, bn_w, bn_b, a2, w2, b2}, rs = {running_mean, running_var}
+  const RBArgs a1 = rb_fwd_args(x, B, C, W, p1[0], p1[1], p1[2], p1[3], p1[4], rs1[0], rs1[1],
+                                nbt1, momentum, eps, p1[5], p1[6], p1[7], drop_p, seed_ptr,
+                                offset1, h1, y1, save1, ws1);
+  const RBArgs a2 = rb_fwd_args(y1, B, C, W, p2[0], p2[1], p2[2], p2[3], p2[4], rs2[0], rs2[1],
+                                nbt2, momentum, eps, p2[5], p2[6], p2[7], drop_p, seed_ptr,
+                                offset2, h2, y2, save2, ws2);
+  rb_dispatch((int)C, (int)W, 0, &a1, st, nullptr);
+  rb_dispatch_pair((int)C, (int)W, 0, a1, a2, st);
+  rb_dispatch((int)C, (int)W, 1, &a2, st, nullptr);
+  return launch_status("tvq_resblock_pair_train_fwd");
+}
+
+extern "C" int tvq_resblock_pair_bwd(const float* dy, const float* x, int64_t B, int64_t C,
+                                     int64_t H, int64_t W, const float* const* q1,
+                                     const float* const* q2, const float* h1, const float* y1,
+                                     const float* h2, float drop_p, const int64_t* seed_ptr,
+                                     uint64_t offset1, uint64_t offset2, float* dx, float* dy1,
+                                     float* const* g1, float* const* g2, int64_t accumulate,
+                                     void* ws1, void* ws2, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(tvq_resblock_pair_supported(B, C, H, W), "tvq_resblock_pair_bwd: unsupported shape");
+  TVQ_CHECK_ARG(dy && x && q1 && q2 && h1 && y1 && h2 && dx && dy1 && g1 && g2 && ws1 && ws2 &&
+                    aligned16(dy) && aligned16(x) && aligned16(h1) && aligned16(h2) &&
+                    aligned16(y1) && aligned16(dy1),
+                "tvq_resblock_pair_bwd: bad arguments");
+  for (int i = 0; i < 6; ++i)
+    TVQ_CHECK_ARG((q1[i] && q2[i]) || i == 2, "tvq_resblock_pair_bwd: missing parameter");
+  for (int i = 0; i < 8; ++i)
+    TVQ_CHECK_ARG((g1[i] && g2[i]) || i == 3 || i == 4, "tvq_resblock_pair_bwd: missing gradient");
+  TVQ_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || seed_ptr),
+                "tvq_resblock_pair_bwd: bad dropout");
+  hipStream_t st = (hipStream_t)stream;
+  // q = {a1, w1, bn_w, save, a2, w2}, g = {da1, dw1, db1, dbn_w, dbn_b, da2, dw2, db2}
+  const RBArgs b2 = rb_bwd_args(dy, y1, h2, B, C, W, q2[0], q2[1], q2[2], q2[3], q2[4], q2[5],
+                                drop_p, seed_ptr, offset2, dy1, g2[3], g2[4], accumulate, ws2);
+  const RBArgs b1 = rb_bwd_args(dy1, x, h1, B, C, W, q1[0], q1[1], q1[2], q1[3], q1[4], q1[5],
+                                drop_p, seed_ptr, offset1, dx, g1[3], g1[4], accumulate, ws1);
+  rb_dispatch((int)C, (int)W, 3, &b2, st, nullptr);
+  rb_dispatch_pair((int)C, (int)W, 1, b2, b1, st);
+  rb_dispatch((int)C, (int)W, 4, &b1, st, nullptr);
+  rb_bwd_finish(b2, C, g2[0], g2[1], g2[2], g2[5], g2[6], g2[7], st);
+  rb_bwd_finish(b1, C, g1[0], g1[1], g1[2], g1[5], g1[6], g1[7], st);
+  return launch_status("tvq_resblock_pair_bwd");
 }

@@ -121,6 +121,11 @@ sig("tvq_resblock_train_fwd", P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, F32
 sig("tvq_resblock_eval_fwd", P, I64, I64, I64, I64, P, P, P, P, P, P, P, F32, P, P, P, P, P)
 sig("tvq_resblock_bwd", P, P, P, I64, I64, I64, I64, P, P, P, P, P, P, F32, P, U64, P, P, P, P,
     P, P, P, P, P, I64, P, P)
+sig("tvq_resblock_pair_supported", I64, I64, I64, I64, restype=ctypes.c_int)
+sig("tvq_resblock_pair_train_fwd", P, I64, I64, I64, I64, P, P, P, P, P, P, F32, F32, F32, P, U64,
+    U64, P, P, P, P, P, P, P, P, P)
+sig("tvq_resblock_pair_bwd", P, P, I64, I64, I64, I64, P, P, P, P, P, F32, P, U64, U64, P, P, P, P,
+    I64, P, P, P)
 sig("tvq_resblock_proj_workspace", I64, I64, I64, I64, I64, restype=I64)
 sig("tvq_resblock_proj_saved_floats", I64, I64, I64, I64, I64, restype=I64)
 sig("tvq_resblock_proj_train_fwd", P, I64, I64, I64, I64, I64, P, P, P, P, P, P, P, P, F32, F32, P,

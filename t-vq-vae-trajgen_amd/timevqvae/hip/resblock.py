@@ -7,6 +7,7 @@ as 2 launches forward (training), 1 (eval), 2 backward, instead of one kernel pe
 `supported()` says when it applies; models/vq_vae.ResBlock falls back to the per-op path
 otherwise (or when TVQ_RESBLOCK_FUSED=0).
 """
+import ctypes
 import os
 
 import torch
@@ -102,6 +103,106 @@ def resblock_eval(x, a1, conv1, bn, a2, conv2):
          ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var), float(bn.eps),
          ptr(a2), ptr(conv2.weight), ptr(conv2.bias), ptr(y), stream_ptr())
     return y
+
+
+# ------------------------------------------------------- two consecutive ResBlocks
+PAIR_ENABLED = os.environ.get("TVQ_RESBLOCK_PAIR", "1") != "0"
+
+
+def pair_supported(x):
+    """Two consecutive identity ResBlocks on x's shape as one chain of 3 launches forward
+    and 3 backward (rb_fwd1 | rb_fwd21 | rb_fwd2, rb_bwd2 | rb_bwd12 | rb_bwd1) instead of
+    2 + 2 each: the middle launch runs block 1's second kernel and block 2's first on the
+    same images, the activation handed over in registers.  The C = 64 LF shape has its own
+    kernels (tvq_resblock_w8.hip) and is not paired."""
+    if not (ENABLED and PAIR_ENABLED) or x.dim() != 4 or not x.is_cuda:
+        return False
+    return bool(value("tvq_resblock_pair_supported", *x.shape))
+
+
+def _arr(ts):
+    return (ctypes.c_void_p * len(ts))(*[ptr(t) for t in ts])
+
+
+class _ResBlockPairTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, *args):
+        p1, p2 = args[0:8], args[8:16]
+        rm1, rv1, nbt1, rm2, rv2, nbt2, momentum, eps, drop_p, site1, site2 = args[16:]
+        x = x.contiguous()
+        B, C, H, W = x.shape
+        hs = value("tvq_resblock_saved_floats", B, C, H, W)
+        h1 = torch.empty(hs, device=x.device)
+        h2 = torch.empty(hs, device=x.device)
+        y1 = torch.empty_like(x)
+        y2 = torch.empty_like(x)
+        save1 = torch.empty(4 * C, device=x.device)
+        save2 = torch.empty(4 * C, device=x.device)
+        seed = rng.seed_tensor(x.device) if drop_p > 0 else None
+        # the offsets the two blocks draw in this order when run one by one
+        off1 = rng.call_offset(site1) if drop_p > 0 else 0
+        off2 = rng.call_offset(site2) if drop_p > 0 else 0
+        keep = [_arr(p1), _arr(p2), _arr([rm1, rv1]), _arr([rm2, rv2])]
+        ws1, ws2 = _ws(x), _ws(x)
+        call("tvq_resblock_pair_train_fwd", ptr(x), B, C, H, W, *keep, ptr(nbt1), ptr(nbt2),
+             float(momentum), float(eps), float(drop_p), ptr(seed), off1, off2, ptr(h1), ptr(y1),
+             ptr(save1), ptr(h2), ptr(y2), ptr(save2), ptr(ws1), ptr(ws2), stream_ptr())
+        ctx.save_for_backward(x, h1, y1, save1, h2, save2)
+        ctx.params = (p1, p2)
+        ctx.drop = (float(drop_p), off1, off2)
+        ctx.seed = seed
+        return y2
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, h1, y1, save1, h2, save2 = ctx.saved_tensors
+        p1, p2 = ctx.params
+        B, C, H, W = x.shape
+        dev = x.device
+        g = gy.contiguous()
+        dx = torch.empty_like(x)
+        dy1 = torch.empty_like(x)
+        params = tuple(p1) + tuple(p2)
+        has = [p is not None for p in params]
+        sinks = [grad_sink(p) if p is not None else None for p in params]
+        direct = all((s is not None) == hh for s, hh in zip(sinks, has))
+        if direct:
+            grads = sinks
+        else:
+            grads = [torch.empty(p.shape, device=dev) if p is not None else None for p in params]
+        ws1, ws2 = _ws(x), _ws(x)
+        drop_p, off1, off2 = ctx.drop
+
+        def q(p, save):  # {a1, w1, bn_w, save, a2, w2}
+            return _arr([p[0], p[1], p[3], save, p[5], p[6]])
+
+        keep = [q(p1, save1), q(p2, save2), _arr(grads[0:8]), _arr(grads[8:16])]
+        with _immediate(not direct):
+            call("tvq_resblock_pair_bwd", ptr(g), ptr(x), B, C, H, W, keep[0], keep[1], ptr(h1),
+                 ptr(y1), ptr(h2), drop_p, ptr(ctx.seed), off1, off2, ptr(dx), ptr(dy1), keep[2],
+                 keep[3], int(direct), ptr(ws1), ptr(ws2), stream_ptr())
+        _keep(ws1)
+        _keep(ws2)
+        out = [dx] + [None if direct else gr for gr in grads]
+        return tuple(out) + (None,) * 11
+
+
+def _block_args(rb):
+    c = rb.convs
+    return (c[0].a, c[1].weight, c[1].bias, c[2].weight, c[2].bias, c[3].a, c[4].weight,
+            c[4].bias)
+
+
+def resblock_pair_train(x, rb1, rb2, drop_p):
+    """Training-mode fused pair of identity ResBlocks (models/vq_vae.ResBlock rb1, rb2 with
+    equal BN momentum / eps and dropout p); bitwise equal to rb2(rb1(x)) on the fused path."""
+    bn1, bn2 = rb1.convs[2], rb2.convs[2]
+    if bn1.momentum is None or bn2.momentum is None:
+        raise NotImplementedError("cumulative-average BatchNorm is not on the path")
+    return _ResBlockPairTrain.apply(x, *_block_args(rb1), *_block_args(rb2), bn1.running_mean,
+                                    bn1.running_var, bn1.num_batches_tracked, bn2.running_mean,
+                                    bn2.running_var, bn2.num_batches_tracked, bn1.momentum,
+                                    bn1.eps, float(drop_p), int(rb1._site), int(rb2._site))
 
 
 # ---------------------------------------------------------------- projection ResBlock

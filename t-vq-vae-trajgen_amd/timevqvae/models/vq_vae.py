@@ -90,6 +90,14 @@ class ResBlock(nn.Module):
                      if in_channels != out_channels else nn.Identity())
         self._site = rng.new_site()
 
+    def fused_train_p(self, x):
+        """The dropout p of the fused identity training path when it applies to x, else None."""
+        c = self.convs
+        if (isinstance(self.proj, nn.Identity) and c[2].training
+                and resblock.supported(x, c[1].in_channels, c[4].out_channels)):
+            return c[5].p if self.training else 0.0
+        return None
+
     def forward(self, x):
         c = self.convs
         if isinstance(self.proj, nn.Identity) and resblock.supported(x, c[1].in_channels,
@@ -127,6 +135,38 @@ class ResBlock(nn.Module):
         r = xs if isinstance(self.proj, nn.Identity) else conv2d(xs, self.proj.weight, self.proj.bias)
         p = c[5].p if self.training else 0.0
         return conv2d(h, c[4].weight, c[4].bias, residual=r, drop_p=p, site=self._site)
+
+
+def _pairable(l1, l2, x):
+    """Two consecutive identity ResBlocks that take the fused training path with equal
+    dropout and BN hyper-parameters (run as one resblock.resblock_pair_train chain)."""
+    if not (isinstance(l1, ResBlock) and isinstance(l2, ResBlock)):
+        return None
+    p1 = l1.fused_train_p(x)
+    if p1 is None or p1 != l2.fused_train_p(x) or not resblock.pair_supported(x):
+        return None
+    b1, b2 = l1.convs[2], l2.convs[2]
+    if b1.momentum != b2.momentum or b1.eps != b2.eps or b1.momentum is None:
+        return None
+    return p1
+
+
+def run_layers(layers, x, layer_fn):
+    """layer_fn over layers in order, consecutive pairable ResBlocks as one fused pair."""
+    i, n = 0, len(layers)
+    while i < n:
+        p = _pairable(layers[i], layers[i + 1], x) if i + 1 < n else None
+        if p is not None:
+            x = resblock.resblock_pair_train(x, layers[i], layers[i + 1], p)
+            i += 2
+        else:
+            x = layer_fn(layers[i], x)
+            i += 1
+    return x
+
+
+def _call(layer, x):
+    return layer(x)
 
 
 class VQVAEEncBlock(nn.Module):
@@ -193,9 +233,7 @@ class VQVAEEncoder(nn.Module):
 
     def encode_timefreq(self, u):
         """Run the conv stack on a band-copied STFT image u (B, 2C, 3, T+1)."""
-        out = u
-        for layer in self.encoder:
-            out = layer(out)
+        out = run_layers(self.encoder, u, _call)
         if not self.is_num_tokens_updated:
             self.H_prime = torch.tensor(out.shape[2])
             self.W_prime = torch.tensor(out.shape[3])
@@ -233,12 +271,13 @@ class VQVAEDecoder(nn.Module):
         self.interp = nn.Upsample(input_length, mode="linear")
         self.linear = nn.Linear(input_length, input_length)
 
+    @staticmethod
+    def _layer(layer, x):
+        if isinstance(layer, nn.ConvTranspose2d):
+            return conv_transpose2d(x, layer.weight, layer.bias, stride_w=2)
+        return layer(x)
+
     def forward(self, x):
-        out = x
-        for layer in self.decoder:
-            if isinstance(layer, nn.ConvTranspose2d):
-                out = conv_transpose2d(out, layer.weight, layer.bias, stride_w=2)
-            else:
-                out = layer(out)
+        out = run_layers(self.decoder, x, self._layer)
         out = istft_decode(out, self.x_channels, self.band, self.input_length)  # (b c l)
         return linear(out, self.linear.weight, self.linear.bias, residual=out)

@@ -89,6 +89,76 @@ def test_fused_resblock_train_matches_per_op(B, C, W, drop):
         assert ((y2 - x) == 0).float().mean().item() > 0.2
 
 
+PAIR_SHAPES = [(8, 8, 64), (8, 16, 32), (4, 16, 16), (3, 32, 16), (2, 32, 32), (5, 8, 16)]
+
+
+def _run_pair(ms, x, paired):
+    from timevqvae.hip import resblock, rng
+    from timevqvae.hip._native import plan_trace
+    from timevqvae.models.vq_vae import run_layers
+    prev = resblock.PAIR_ENABLED
+    resblock.PAIR_ENABLED = paired
+    try:
+        rng._calls[0] = 0
+        for m in ms:
+            m.train(True)
+            for p in m.parameters():
+                p.grad = None
+        xx = x.clone().requires_grad_(True)
+        with plan_trace() as tr:
+            y = run_layers(ms, xx, lambda layer, v: layer(v))
+            gy = torch.cos(torch.arange(y.numel(), device=y.device, dtype=torch.float32)).view_as(y)
+            y.backward(gy)
+        torch.cuda.synchronize()
+        grads = {f"{i}.{n}": p.grad.clone() for i, m in enumerate(ms)
+                 for n, p in m.named_parameters()}
+        grads["x"] = xx.grad.clone()
+        bufs = {f"{i}.{n}": b.clone() for i, m in enumerate(ms) for n, b in m.named_buffers()}
+        return y.detach(), grads, bufs, tr.lines
+    finally:
+        resblock.PAIR_ENABLED = prev
+
+
+@pytest.mark.parametrize("B,C,W", PAIR_SHAPES)
+@pytest.mark.parametrize("drop", [0.0, 0.3])
+def test_resblock_pair_bitwise_equals_two_blocks(B, C, W, drop):
+    """rb_fwd21 / rb_bwd12 (block 1's second kernel and block 2's first in one launch, the
+    activation handed over in registers) compute exactly what the two blocks' separate
+    launches do: y, every gradient and the BN running statistics bitwise equal."""
+    from timevqvae.hip import resblock
+    x = torch.randn(B, C, 3, W, device="cuda")
+    assert resblock.pair_supported(x)
+    ms_a = [_block(C, drop, seed=1), _block(C, drop, seed=2)]
+    ms_b = [_block(C, drop, seed=1), _block(C, drop, seed=2)]
+    for ma, mb in zip(ms_a, ms_b):
+        mb._site = ma._site
+    ya, ga, ba, ta = _run_pair(ms_a, x, paired=False)
+    yb, gb, bb, tb = _run_pair(ms_b, x, paired=True)
+    assert not any("rb_fwd21" in t for t in ta)
+    assert any(t.startswith(f"rb_fwd21 C{C} W{W}") for t in tb), tb
+    assert any(t.startswith(f"rb_bwd12 C{C} W{W}") for t in tb), tb
+    assert torch.equal(ya, yb)
+    for k in ga:
+        assert torch.equal(ga[k], gb[k]), k
+    for k in ba:
+        assert torch.equal(ba[k], bb[k]), k
+
+
+def test_resblock_pair_not_used_for_w8_or_eval():
+    from timevqvae.hip import resblock
+    x = torch.randn(4, 64, 3, 8, device="cuda")
+    assert resblock.supported(x, 64, 64) and not resblock.pair_supported(x)
+    x = torch.randn(4, 16, 3, 32, device="cuda")
+    ms = [_block(16, 0.0, seed=1), _block(16, 0.0, seed=2)]
+    from timevqvae.hip._native import plan_trace
+    from timevqvae.models.vq_vae import run_layers
+    for m in ms:
+        m.eval()
+    with torch.no_grad(), plan_trace() as tr:
+        run_layers(ms, x, lambda layer, v: layer(v))
+    assert not any("rb_fwd21" in t for t in tr.lines)
+
+
 def test_fused_resblock_w8_eval_packed_and_unpacked():
     """The C = 64 eval kernel reads packed weights inside a pack-cache scope and the raw
     (n, c, tap) weights outside one: the same results either way."""
