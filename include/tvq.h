@@ -354,8 +354,9 @@ int tvq_resblock_bwd(const float* dy, const float* x, const float* h, int64_t B,
  * rs = {running_mean, running_var}, q = {a1, w1, bn_w, save, a2, w2},
  * g = {da1, dw1, db1, dbn_w, dbn_b, da2, dw2, db2}.  Each block has its own workspace
  * (tvq_resblock_workspace bytes) and saved buffers; y1 (block 1's output) is block 2's
- * input, dy1 receives the gradient at it.  1 when the shape takes this path (C in
- * {8, 16, 32}), else 0. */
+ * input, dy1 receives the gradient at it.  C = 64, W = 8 (tvq_resblock_w8.hip): w8_fwd21 /
+ * w8_bwd12, the BN finish launches between.  1 when the shape takes this path (C in
+ * {8, 16, 32} or the C = 64 LF maps), else 0. */
 int tvq_resblock_pair_supported(int64_t B, int64_t C, int64_t H, int64_t W);
 int tvq_resblock_pair_train_fwd(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
                                 const float* const* p1, const float* const* p2,

@@ -1016,6 +1016,17 @@ int w8_bwd(const float* dy, const float* x, const float* saved, int64_t B, const
            const float* w2, float drop_p, const int64_t* seed_ptr, uint64_t offset, float* dx,
            float* da1, float* dw1, float* db1, float* dbn_w, float* dbn_b, float* da2, float* dw2,
            float* db2, int64_t accumulate, void* workspace, hipStream_t st);
+int w8_pair_train_fwd(const float* x, int64_t B, const float* const* p1, const float* const* p2,
+                      float* const* rs1, float* const* rs2, int64_t* nbt1, int64_t* nbt2,
+                      float momentum, float eps, float drop_p, const int64_t* seed_ptr,
+                      uint64_t off1, uint64_t off2, float* saved1, float* y1, float* save1,
+                      float* saved2, float* y2, float* save2, void* ws1, void* ws2,
+                      hipStream_t st);
+int w8_pair_bwd(const float* dy, const float* x, int64_t B, const float* const* q1,
+                const float* const* q2, const float* saved1, const float* y1,
+                const float* saved2, float drop_p, const int64_t* seed_ptr, uint64_t off1,
+                uint64_t off2, float* dx, float* dy1, float* const* g1, float* const* g2,
+                int64_t accumulate, void* ws1, void* ws2, hipStream_t st);
 
 static RBArgs rb_fwd_args(const float* x, int64_t B, int64_t C, int64_t W, const float* a1,
                           const float* w1, const float* b1, const float* bn_w, const float* bn_b,
@@ -1173,7 +1184,7 @@ extern "C" int tvq_resblock_bwd(const float* dy, const float* x, const float* h,
 }
 
 extern "C" int tvq_resblock_pair_supported(int64_t B, int64_t C, int64_t H, int64_t W) {
-  return !w8_supported(B, C, H, W) && rb_supported(B, C, H, W);
+  return w8_supported(B, C, H, W) || rb_supported(B, C, H, W);
 }
 
 extern "C" int tvq_resblock_pair_train_fwd(const float* x, int64_t B, int64_t C, int64_t H,
@@ -1198,6 +1209,9 @@ extern "C" int tvq_resblock_pair_train_fwd(const float* x, int64_t B, int64_t C,
   TVQ_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || seed_ptr),
                 "tvq_resblock_pair_train_fwd: bad dropout");
   hipStream_t st = (hipStream_t)stream;
+  if (w8_supported(B, C, H, W))
+    return w8_pair_train_fwd(x, B, p1, p2, rs1, rs2, nbt1, nbt2, momentum, eps, drop_p, seed_ptr,
+                             offset1, offset2, h1, y1, save1, h2, y2, save2, ws1, ws2, st);
   // p = {a1, w1, b1, bn_w, bn_b, a2, w2, b2}, rs = {running_mean, running_var}
   const RBArgs a1 = rb_fwd_args(x, B, C, W, p1[0], p1[1], p1[2], p1[3], p1[4], rs1[0], rs1[1],
                                 nbt1, momentum, eps, p1[5], p1[6], p1[7], drop_p, seed_ptr,
@@ -1230,6 +1244,9 @@ extern "C" int tvq_resblock_pair_bwd(const float* dy, const float* x, int64_t B,
   TVQ_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || seed_ptr),
                 "tvq_resblock_pair_bwd: bad dropout");
   hipStream_t st = (hipStream_t)stream;
+  if (w8_supported(B, C, H, W))
+    return w8_pair_bwd(dy, x, B, q1, q2, h1, y1, h2, drop_p, seed_ptr, offset1, offset2, dx, dy1,
+                       g1, g2, accumulate, ws1, ws2, st);
   // q = {a1, w1, bn_w, save, a2, w2}, g = {da1, dw1, db1, dbn_w, dbn_b, da2, dw2, db2}
   const RBArgs b2 = rb_bwd_args(dy, y1, h2, B, C, W, q2[0], q2[1], q2[2], q2[3], q2[4], q2[5],
                                 drop_p, seed_ptr, offset2, dy1, g2[3], g2[4], accumulate, ws2);

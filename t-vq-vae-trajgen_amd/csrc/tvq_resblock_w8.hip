@@ -159,20 +159,26 @@ __device__ __forceinline__ float conv_at(const float* __restrict__ red, int n, i
 }
 
 // ---------------------------------------------------------------- kernels
-__global__ __launch_bounds__(T) void w8_fwd1_kernel(Args a) {
-  extern __shared__ float sm[];
+// The kernels' bodies take the block's LDS, the weight registers and, for a fused pair of
+// consecutive ResBlocks (w8_fwd21 / w8_bwd12 below), the activation handed over in
+// registers (every kernel has the same elementwise layout) with the next body's weights
+// already loaded (issued right after the first body's last MFMA).
+__device__ __forceinline__ void fwd1_body(const Args& a, float* sm, float (&wa)[9][8],
+                                          const float (*xin)[4]) {
   float* S = sm;
   float* red = sm + PLANE;
   const int b = blockIdx.x, p = el_p();
   const int64_t img0 = (int64_t)b * C * P;
-  float wa[9][8], xv[4], av[4], bv[4];
+  float xv[4], av[4], bv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    xv[j] = a.x[img0 + el_c(j) * P + (p < P ? p : 0)];
+    xv[j] = xin ? (*xin)[j] : a.x[img0 + el_c(j) * P + (p < P ? p : 0)];
     av[j] = a.a1[el_c(j)];
     bv[j] = a.b1[el_c(j)];
   }
-  load_w(a.w1, wa);  // after the staging operands: their wait leaves the weights in flight
+  // after the staging operands: their wait leaves the weights in flight (a pair's second
+  // body has them already)
+  if (!xin) load_w(a.w1, wa);
   border(S);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -204,13 +210,20 @@ __global__ __launch_bounds__(T) void w8_fwd1_kernel(Args a) {
   }
 }
 
-__global__ __launch_bounds__(T) void w8_fwd2_kernel(Args a) {
+__global__ __launch_bounds__(T) void w8_fwd1_kernel(Args a) {
   extern __shared__ float sm[];
+  float wa[9][8];
+  fwd1_body(a, sm, wa, nullptr);
+}
+
+// next: the following body's weights, loaded into wa once this conv is done with them
+__device__ __forceinline__ void fwd2_body(const Args& a, float* sm, float (&wa)[9][8],
+                                          float (&yout)[4], const WView* next) {
   float* S = sm;
   float* red = sm + PLANE;
   const int b = blockIdx.x, p = el_p();
   const int64_t img0 = (int64_t)b * C * P;
-  float wa[9][8], hv[4], xv[4], av[4], bv[4];
+  float hv[4], xv[4], av[4], bv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t gi = img0 + el_c(j) * P + (p < P ? p : 0);
@@ -237,17 +250,35 @@ __global__ __launch_bounds__(T) void w8_fwd2_kernel(Args a) {
   }
   __syncthreads();
   conv<false>(wa, S, red);
+  if (next) load_w(*next, wa);
   __syncthreads();
   const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = el_c(j);
+    yout[j] = 0.f;
     if (p >= P) continue;
     const int64_t gi = img0 + c * P + p;
     float v = conv_at(red, c, p) + bv[j];
     if (a.drop_p > 0.f) v = uniform01(seed, (uint64_t)gi) >= a.drop_p ? v * a.drop_scale : 0.f;
-    a.y[gi] = xv[j] + v;
+    yout[j] = xv[j] + v;
+    a.y[gi] = yout[j];
   }
+}
+
+__global__ __launch_bounds__(T) void w8_fwd2_kernel(Args a) {
+  extern __shared__ float sm[];
+  float wa[9][8], y[4];
+  fwd2_body(a, sm, wa, y, nullptr);
+}
+
+// fwd2 of ResBlock 1 and fwd1 of ResBlock 2 (its input = ResBlock 1's output) in one launch
+__global__ __launch_bounds__(T) void w8_fwd21_kernel(Args a1, Args a2) {
+  extern __shared__ float sm[];
+  float wa[9][8], y[4];
+  fwd2_body(a1, sm, wa, y, &a2.w1);
+  __syncthreads();  // LDS reused
+  fwd1_body(a2, sm, wa, &y);
 }
 
 __global__ __launch_bounds__(T) void w8_eval_kernel(Args a) {
@@ -296,20 +327,20 @@ __global__ __launch_bounds__(T) void w8_eval_kernel(Args a) {
   }
 }
 
-__global__ __launch_bounds__(T) void w8_bwd2_kernel(Args a) {
-  extern __shared__ float sm[];
+__device__ __forceinline__ void bwd2_body(const Args& a, float* sm, float (&wa)[9][8],
+                                          const float (*dyin)[4]) {
   float* G = sm;
   float* red = sm + PLANE;
   const int b = blockIdx.x, p = el_p();
   const int64_t img0 = (int64_t)b * C * P;
-  float wa[9][8], gv[4], hv[4];
+  float gv[4], hv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t gi = img0 + el_c(j) * P + (p < P ? p : 0);
-    gv[j] = a.dy[gi];
+    gv[j] = dyin ? (*dyin)[j] : a.dy[gi];
     hv[j] = a.h[gi];
   }
-  load_w(a.w2, wa);
+  if (!dyin) load_w(a.w2, wa);
   border(G);
   const uint64_t seed = a.drop_p > 0.f ? mix_seed(a.seed_ptr, a.offset) : 0ull;
 #pragma unroll
@@ -357,13 +388,19 @@ __global__ __launch_bounds__(T) void w8_bwd2_kernel(Args a) {
   }
 }
 
-__global__ __launch_bounds__(T) void w8_bwd1_kernel(Args a) {
+__global__ __launch_bounds__(T) void w8_bwd2_kernel(Args a) {
   extern __shared__ float sm[];
+  float wa[9][8];
+  bwd2_body(a, sm, wa, nullptr);
+}
+
+__device__ __forceinline__ void bwd1_body(const Args& a, float* sm, float (&wa)[9][8],
+                                          float (&dxout)[4], const WView* next) {
   float* G = sm;
   float* red = sm + PLANE;
   const int b = blockIdx.x, p = el_p();
   const int64_t img0 = (int64_t)b * C * P;
-  float wa[9][8], dv[4], hv[4], xv[4], yv[4];
+  float dv[4], hv[4], xv[4], yv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t gi = img0 + el_c(j) * P + (p < P ? p : 0);
@@ -393,11 +430,13 @@ __global__ __launch_bounds__(T) void w8_bwd1_kernel(Args a) {
   }
   __syncthreads();
   conv<true>(wa, G, red);
+  if (next) load_w(*next, wa);
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = el_c(j);
     double s0 = 0.0;
+    dxout[j] = 0.f;
     if (p < P) {
       const int64_t gi = img0 + c * P + p;
       const float av = a.a1[c], inv_a = 1.0f / av;
@@ -406,12 +445,29 @@ __global__ __launch_bounds__(T) void w8_bwd1_kernel(Args a) {
       sincosf(av * xv[j], &sn, &cs);
       const float tt = 2.0f * sn * cs;
       // snake_bwd_kernel, plus the identity skip's gradient
-      a.dx[gi] = (gs + gs * inv_a * tt * av) + yv[j];
+      dxout[j] = (gs + gs * inv_a * tt * av) + yv[j];
+      a.dx[gi] = dxout[j];
       s0 = (double)(gs * inv_a * tt * xv[j]) - (double)(gs * (sn * sn) * inv_a * inv_a);
     }
     s0 = half_sum_d(s0);
     if ((threadIdx.x & 31) == 0) a.slabda[(int64_t)b * C + c] = (float)s0;
   }
+}
+
+__global__ __launch_bounds__(T) void w8_bwd1_kernel(Args a) {
+  extern __shared__ float sm[];
+  float wa[9][8], dx[4];
+  bwd1_body(a, sm, wa, dx, nullptr);
+}
+
+// bwd1 of ResBlock 2 and bwd2 of ResBlock 1 (its output gradient = ResBlock 2's input
+// gradient) in one launch
+__global__ __launch_bounds__(T) void w8_bwd12_kernel(Args a2, Args a1) {
+  extern __shared__ float sm[];
+  float wa[9][8], d[4];
+  bwd1_body(a2, sm, wa, d, &a1.w2);
+  __syncthreads();  // LDS reused
+  bwd2_body(a1, sm, wa, &d);
 }
 
 constexpr size_t LDS = 4 * (size_t)(PLANE + RED);
@@ -421,7 +477,8 @@ static void set_lds() {
   if (done) return;
   const void* ks[] = {(const void*)&w8_fwd1_kernel, (const void*)&w8_fwd2_kernel,
                       (const void*)&w8_eval_kernel, (const void*)&w8_bwd2_kernel,
-                      (const void*)&w8_bwd1_kernel};
+                      (const void*)&w8_bwd1_kernel, (const void*)&w8_fwd21_kernel,
+                      (const void*)&w8_bwd12_kernel};
   for (const void* k : ks)
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
   done = true;
@@ -577,6 +634,146 @@ int w8_bwd(const float* dy, const float* x, const float* saved, int64_t B, const
   }
   conv_wgrad_finish(slabda1, (int)B, C, 1, da1, nullptr, (int)accumulate, st);
   return launch_status("tvq_resblock_bwd");
+}
+
+// Two consecutive ResBlock(64, 64)s (tvq_resblock_pair_train_fwd / _bwd): p = {a1, w1, b1,
+// bn_w, bn_b, a2, w2, b2}, rs = {running_mean, running_var}; 5 launches forward instead of 6
+// (w8_fwd21 = block 1's fwd2 + block 2's fwd1), 4 + weight gradients backward instead of 5.
+int w8_pair_train_fwd(const float* x, int64_t B, const float* const* p1, const float* const* p2,
+                      float* const* rs1, float* const* rs2, int64_t* nbt1, int64_t* nbt2,
+                      float momentum, float eps, float drop_p, const int64_t* seed_ptr,
+                      uint64_t off1, uint64_t off2, float* saved1, float* y1, float* save1,
+                      float* saved2, float* y2, float* save2, void* ws1, void* ws2,
+                      hipStream_t st) {
+  using namespace w8;
+  set_lds();
+  const int64_t img = B * C * P;
+  Args A[2];
+  const float* const* ps[2] = {p1, p2};
+  float* const* rss[2] = {rs1, rs2};
+  int64_t* nbts[2] = {nbt1, nbt2};
+  const float* xs[2] = {x, y1};
+  float* saveds[2] = {saved1, saved2};
+  float* ys[2] = {y1, y2};
+  float* saves[2] = {save1, save2};
+  void* wss[2] = {ws1, ws2};
+  const uint64_t offs[2] = {off1, off2};
+  for (int i = 0; i < 2; ++i) {
+    const Ws L = ws_layout(B);
+    char* ws = (char*)wss[i];
+    float* pk = (float*)(ws + L.pk);
+    const float* const* p = ps[i];
+    Args& a = A[i];
+    a = Args{};
+    a.x = xs[i]; a.a1 = p[0]; a.b1 = p[2]; a.a2 = p[5]; a.b2 = p[7];
+    a.w1 = view(p[1], false, pk, st);
+    a.w2 = view(p[6], false, pk + K * C, st);
+    a.h_out = saveds[i]; a.h = saveds[i]; a.y = ys[i];
+    a.part = (double*)(ws + L.part);
+    a.B = (int)B;
+    a.drop_p = drop_p;
+    a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+    a.seed_ptr = seed_ptr; a.offset = offs[i];
+    float* sv = saves[i];
+    a.fin = {C, (int)B, B * P, eps, momentum, p[3], p[4], rss[i][0], rss[i][1], nbts[i],
+             sv, sv + C, sv + 2 * C, sv + 3 * C};
+    a.fin.chunks = (int)B;
+    a.save = sv;
+  }
+  TVQ_PLAN("w8_fwd1 C%d W%d B%lld", C, W, (long long)B);
+  A[0].s_out = saved1 + img;  // s1 of block 1
+  hipLaunchKernelGGL(w8_fwd1_kernel, dim3((unsigned)B), dim3(T), LDS, st, A[0]);
+  bn_stats_final_launch(A[0].part, A[0].fin, st);
+  TVQ_PLAN("w8_fwd21 C%d W%d B%lld", C, W, (long long)B);
+  A[0].s_out = saved1 + 2 * img;  // s2 of block 1
+  A[1].s_out = saved2 + img;      // s1 of block 2
+  hipLaunchKernelGGL(w8_fwd21_kernel, dim3((unsigned)B), dim3(T), LDS, st, A[0], A[1]);
+  bn_stats_final_launch(A[1].part, A[1].fin, st);
+  TVQ_PLAN("w8_fwd2 C%d W%d B%lld", C, W, (long long)B);
+  A[1].s_out = saved2 + 2 * img;
+  hipLaunchKernelGGL(w8_fwd2_kernel, dim3((unsigned)B), dim3(T), LDS, st, A[1]);
+  return launch_status("tvq_resblock_pair_train_fwd");
+}
+
+// q = {a1, w1, bn_w, save, a2, w2}, g = {da1, dw1, db1, dbn_w, dbn_b, da2, dw2, db2}
+int w8_pair_bwd(const float* dy, const float* x, int64_t B, const float* const* q1,
+                const float* const* q2, const float* saved1, const float* y1,
+                const float* saved2, float drop_p, const int64_t* seed_ptr, uint64_t off1,
+                uint64_t off2, float* dx, float* dy1, float* const* g1, float* const* g2,
+                int64_t accumulate, void* ws1, void* ws2, hipStream_t st) {
+  using namespace w8;
+  set_lds();
+  const Ws L = ws_layout(B);
+  const int64_t img = B * C * P;
+  // index 0: block 2 (runs first), 1: block 1
+  const float* const* qs[2] = {q2, q1};
+  float* const* gs[2] = {g2, g1};
+  const float* dys[2] = {dy, dy1};
+  const float* xs[2] = {y1, x};
+  const float* saveds[2] = {saved2, saved1};
+  float* dxs[2] = {dy1, dx};
+  void* wss[2] = {ws2, ws1};
+  const uint64_t offs[2] = {off2, off1};
+  Args A[2];
+  for (int i = 0; i < 2; ++i) {
+    char* ws = (char*)wss[i];
+    float* pk = (float*)(ws + L.pk);
+    const float* const* q = qs[i];
+    float* const* g = gs[i];
+    Args& a = A[i];
+    a = Args{};
+    a.x = xs[i]; a.h = saveds[i]; a.dy = dys[i]; a.du_in = (float*)(ws + L.du);
+    a.a1 = q[0]; a.a2 = q[4]; a.bn_w = q[2]; a.save = q[3];
+    a.w1 = view(q[1], true, pk + 2 * K * C, st);
+    a.w2 = view(q[5], true, pk + 3 * K * C, st);
+    a.du = (float*)(ws + L.du); a.dx = dxs[i];
+    a.part = (double*)(ws + L.part);
+    a.B = (int)B; a.accumulate = (int)accumulate;
+    a.drop_p = drop_p;
+    a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+    a.seed_ptr = seed_ptr; a.offset = offs[i];
+    a.invN = 1.0f / (float)(B * P);
+    float* coef = (float*)(ws + L.slabda2);
+    a.bfin = {C, (int)B, coef, g[3], g[4], g[5], (int)accumulate};
+    a.coef = coef;
+  }
+  auto ws_of = [&](int i, size_t off) { return (float*)((char*)wss[i] + off); };
+  TVQ_PLAN("w8_bwd2 C%d W%d B%lld", C, W, (long long)B);
+  A[0].g_out = ws_of(0, L.g2);
+  hipLaunchKernelGGL(w8_bwd2_kernel, dim3((unsigned)B), dim3(T), LDS, st, A[0]);
+  int rc = launch_status("tvq_resblock_pair_bwd");
+  if (rc) return rc;
+  bn_bwd_final_launch(A[0].part, A[0].bfin, st);
+  TVQ_PLAN("w8_bwd12 C%d W%d B%lld", C, W, (long long)B);
+  A[0].g_out = ws_of(0, L.dh); A[0].slabda = ws_of(0, L.slabda1);
+  A[1].g_out = ws_of(1, L.g2);
+  hipLaunchKernelGGL(w8_bwd12_kernel, dim3((unsigned)B), dim3(T), LDS, st, A[0], A[1]);
+  rc = launch_status("tvq_resblock_pair_bwd");
+  if (rc) return rc;
+  bn_bwd_final_launch(A[1].part, A[1].bfin, st);
+  TVQ_PLAN("w8_bwd1 C%d W%d B%lld", C, W, (long long)B);
+  A[1].g_out = ws_of(1, L.dh); A[1].slabda = ws_of(1, L.slabda1);
+  hipLaunchKernelGGL(w8_bwd1_kernel, dim3((unsigned)B), dim3(T), LDS, st, A[1]);
+  rc = launch_status("tvq_resblock_pair_bwd");
+  if (rc) return rc;
+  for (int i = 0; i < 2; ++i) {
+    float* const* g = gs[i];
+    const float* s1 = saveds[i] + img;
+    const float* s2 = saveds[i] + 2 * img;
+    float* g2b = ws_of(i, L.g2);
+    float* dh = ws_of(i, L.dh);
+    if (!conv_wgrad_w8_pair(s2, g2b, ws_of(i, L.wg2), g[6], g[7], s1, dh, ws_of(i, L.wg1), g[1],
+                            g[2], B, C, C, (int)accumulate, st)) {
+      rc = tvq_conv2d_wgrad(s2, B, C, 3, W, g2b, C, W, 3, 3, 1, 0, g[6], g[7], accumulate,
+                            ws_of(i, L.wg2), st);
+      if (rc) return rc;
+      rc = tvq_conv2d_wgrad(s1, B, C, 3, W, dh, C, W, 3, 3, 1, 0, g[1], g[2], accumulate,
+                            ws_of(i, L.wg1), st);
+      if (rc) return rc;
+    }
+    conv_wgrad_finish(ws_of(i, L.slabda1), (int)B, C, 1, g[0], nullptr, (int)accumulate, st);
+  }
+  return launch_status("tvq_resblock_pair_bwd");
 }
 
 }  // namespace tvq

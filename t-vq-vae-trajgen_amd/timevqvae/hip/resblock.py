@@ -113,8 +113,8 @@ def pair_supported(x):
     """Two consecutive identity ResBlocks on x's shape as one chain of 3 launches forward
     and 3 backward (rb_fwd1 | rb_fwd21 | rb_fwd2, rb_bwd2 | rb_bwd12 | rb_bwd1) instead of
     2 + 2 each: the middle launch runs block 1's second kernel and block 2's first on the
-    same images, the activation handed over in registers.  The C = 64 LF shape has its own
-    kernels (tvq_resblock_w8.hip) and is not paired."""
+    same images, the activation handed over in registers; for the LF band's C = 64 blocks
+    (tvq_resblock_w8.hip) w8_fwd21 / w8_bwd12 likewise, their BN finish launches between."""
     if not (ENABLED and PAIR_ENABLED) or x.dim() != 4 or not x.is_cuda:
         return False
     return bool(value("tvq_resblock_pair_supported", *x.shape))

@@ -89,7 +89,8 @@ def test_fused_resblock_train_matches_per_op(B, C, W, drop):
         assert ((y2 - x) == 0).float().mean().item() > 0.2
 
 
-PAIR_SHAPES = [(8, 8, 64), (8, 16, 32), (4, 16, 16), (3, 32, 16), (2, 32, 32), (5, 8, 16)]
+PAIR_SHAPES = [(8, 8, 64), (8, 16, 32), (4, 16, 16), (3, 32, 16), (2, 32, 32), (5, 8, 16),
+               (8, 64, 8), (3, 64, 8), (256, 64, 8)]
 
 
 def _run_pair(ms, x, paired):
@@ -122,8 +123,8 @@ def _run_pair(ms, x, paired):
 @pytest.mark.parametrize("B,C,W", PAIR_SHAPES)
 @pytest.mark.parametrize("drop", [0.0, 0.3])
 def test_resblock_pair_bitwise_equals_two_blocks(B, C, W, drop):
-    """rb_fwd21 / rb_bwd12 (block 1's second kernel and block 2's first in one launch, the
-    activation handed over in registers) compute exactly what the two blocks' separate
+    """rb_fwd21 / rb_bwd12 and, C = 64, w8_fwd21 / w8_bwd12 (block 1's second kernel and
+    block 2's first in one launch, the activation handed over in registers) compute exactly what the two blocks' separate
     launches do: y, every gradient and the BN running statistics bitwise equal."""
     from timevqvae.hip import resblock
     x = torch.randn(B, C, 3, W, device="cuda")
@@ -134,9 +135,10 @@ def test_resblock_pair_bitwise_equals_two_blocks(B, C, W, drop):
         mb._site = ma._site
     ya, ga, ba, ta = _run_pair(ms_a, x, paired=False)
     yb, gb, bb, tb = _run_pair(ms_b, x, paired=True)
-    assert not any("rb_fwd21" in t for t in ta)
-    assert any(t.startswith(f"rb_fwd21 C{C} W{W}") for t in tb), tb
-    assert any(t.startswith(f"rb_bwd12 C{C} W{W}") for t in tb), tb
+    k = "w8" if C == 64 else "rb"
+    assert not any("fwd21" in t for t in ta)
+    assert any(t.startswith(f"{k}_fwd21 C{C} W{W}") for t in tb), tb
+    assert any(t.startswith(f"{k}_bwd12 C{C} W{W}") for t in tb), tb
     assert torch.equal(ya, yb)
     for k in ga:
         assert torch.equal(ga[k], gb[k]), k
@@ -144,10 +146,7 @@ def test_resblock_pair_bitwise_equals_two_blocks(B, C, W, drop):
         assert torch.equal(ba[k], bb[k]), k
 
 
-def test_resblock_pair_not_used_for_w8_or_eval():
-    from timevqvae.hip import resblock
-    x = torch.randn(4, 64, 3, 8, device="cuda")
-    assert resblock.supported(x, 64, 64) and not resblock.pair_supported(x)
+def test_resblock_pair_not_used_in_eval():
     x = torch.randn(4, 16, 3, 32, device="cuda")
     ms = [_block(16, 0.0, seed=1), _block(16, 0.0, seed=2)]
     from timevqvae.hip._native import plan_trace
@@ -156,7 +155,7 @@ def test_resblock_pair_not_used_for_w8_or_eval():
         m.eval()
     with torch.no_grad(), plan_trace() as tr:
         run_layers(ms, x, lambda layer, v: layer(v))
-    assert not any("rb_fwd21" in t for t in tr.lines)
+    assert not any("fwd21" in t for t in tr.lines)
 
 
 def test_fused_resblock_w8_eval_packed_and_unpacked():
