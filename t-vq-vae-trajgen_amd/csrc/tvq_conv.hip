@@ -1904,15 +1904,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(const float* __res
 //   dW[n][c*9 + tap] (+ dB[n]) = sum_{b, p} dY[b, n, p] * X[b, c, window(p, tap)].
 // conv_wgrad_halo_kernel staged one image per step and wrote one 64 x 577 slab per 1-3
 // images (43 MB of HBM traffic per op for 3.3 MB of algorithmic bytes).  Here block
-// (s, nb, cb) owns a 32-row x (CB*9 [+1]) column tile and W8_IMG images: it loads all their
-// dY rows (16-B loads) and input halo planes into LDS at once, the 4 waves each reduce a
-// quarter of the images over all of the tile's columns (5 x 2 independent 16x16x4 MFMA
-// chains), and the 4 partial tiles are summed in wave order through LDS.  One slab row
-// per W8_IMG images: S = B / W8_IMG splits, summed in order by the deferred slab sum.
+// (s, nb, cb) owns a 32-row x (CB*9 [+1]) column tile and W8_IMG images, walked in stages of
+// 4 (one per wave) through two LDS buffers: stage s + 1's dY rows (16-B loads) and input
+// halo rows are in registers while stage s multiplies, and are stored behind its MFMAs
+// (round 5; loading all 16 images before the first MFMA left the MFMA pipe idle through the
+// load and the memory idle through the MFMAs, one 86 KB block per CU).  Each wave reduces
+// its images over all of the tile's columns (5 x 2 independent 16x16x4 MFMA chains), and
+// the 4 partial tiles are summed in wave order through LDS.  One slab row per W8_IMG
+// images: S = B / W8_IMG splits, summed in order by the deferred slab sum.
 #ifndef TVQ_W8_IMG
 #define TVQ_W8_IMG 16
 #endif
 constexpr int W8_IMG = TVQ_W8_IMG;
+constexpr int W8_STG = 4;  // images per pipeline stage (one per wave)
 
 template <int W, int CB>
 __global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restrict__ G0,
@@ -1927,8 +1931,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restr
   constexpr int KB = CB * 9 + 1, KT = (KB + 15) / 16;  // columns (+ bias), 16-col tiles
   constexpr int TW = KT * 16;                        // combine-buffer row length
   extern __shared__ float smem[];
-  float* Gs = smem;                                  // [IMG][32][GST]
-  float* Hs = smem + W8_IMG * 32 * GST;              // [IMG][CB + 1][PS] (plane CB: ones)
+  // W8_STG images per stage (one per wave), two stage buffers: stage s + 1's loads are in
+  // registers while stage s multiplies, and its LDS stores follow the MFMAs
+  constexpr int STG = W8_STG, NSTG = W8_IMG / STG;
+  static_assert(STG == 4 && W8_IMG % STG == 0, "one image per wave and stage");
+  const int hs_img = (CB + 1) * PS;
+  const int gbuf = STG * 32 * GST, hbuf = STG * hs_img;
+  float* Gs = smem;                                  // [2][STG][32][GST]
+  float* Hs = smem + 2 * gbuf;                       // [2][STG][CB + 1][PS] (plane CB: ones)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 15, kq = lane >> 4;
   // a pair launch (conv_wgrad_w8_pair) stacks a second problem of the same shape on the
@@ -1941,50 +1951,52 @@ __global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restr
   const bool bias = c0 + CB >= C && kcols > C * 9;   // this block also owns the bias column
   const int b0 = s * W8_IMG;
   const int ni = min(W8_IMG, B - b0);
-  const int hs_img = (CB + 1) * PS;
-  // zero padding and the ones planes
-  for (int e = tid; e < W8_IMG * hs_img; e += 256) Hs[e] = (e % hs_img) >= CB * PS ? 1.f : 0.f;
-  __syncthreads();
-  {  // every load of the group in flight before the first LDS store
-    constexpr int GQ = P / 4, GU = (W8_IMG * 32 * GQ + 255) / 256;
-    float4 gv[GU];
+  constexpr int GQ = P / 4, GN = STG * 32 * GQ, GU = (GN + 255) / 256;
+  constexpr int XQ = W / 4, XN = STG * CB * 3 * XQ, XU = (XN + 255) / 256;
+  float4 gv[GU], xv[XU];
+  auto load = [&](int sg) {  // stage sg's dY rows and input rows into registers
 #pragma unroll
     for (int u = 0; u < GU; ++u) {
       const int e = tid + u * 256;
-      const int ii = e / (32 * GQ), r = (e / GQ) % 32, q = e % GQ;
+      const int ii = e / (32 * GQ), r = (e / GQ) % 32, q = e % GQ, im = sg * STG + ii;
       gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ii < ni && n0 + r < N)
-        gv[u] = *reinterpret_cast<const float4*>(G + ((int64_t)(b0 + ii) * N + n0 + r) * P + 4 * q);
+      if (e < GN && im < ni && n0 + r < N)
+        gv[u] = *reinterpret_cast<const float4*>(G + ((int64_t)(b0 + im) * N + n0 + r) * P + 4 * q);
     }
-    constexpr int XQ = W / 4, XU = (W8_IMG * CB * 3 * XQ + 255) / 256;
-    float4 xv[XU];
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
       const int e = tid + u * 256;
-      const int ii = e / (CB * 3 * XQ), c = (e / (3 * XQ)) % CB, hq = e % (3 * XQ);
+      const int ii = e / (CB * 3 * XQ), c = (e / (3 * XQ)) % CB, hq = e % (3 * XQ), im = sg * STG + ii;
       xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ii < ni && c0 + c < C)
-        xv[u] = *reinterpret_cast<const float4*>(X + ((int64_t)(b0 + ii) * C + c0 + c) * P + 4 * hq);
+      if (e < XN && im < ni && c0 + c < C)
+        xv[u] = *reinterpret_cast<const float4*>(X + ((int64_t)(b0 + im) * C + c0 + c) * P + 4 * hq);
     }
+  };
+  auto store = [&](int buf) {  // the registers into stage buffer buf (interior cells only)
 #pragma unroll
     for (int u = 0; u < GU; ++u) {
       const int e = tid + u * 256;
-      if (e < W8_IMG * 32 * GQ) {
+      if (e < GN) {
         const int ii = e / (32 * GQ), r = (e / GQ) % 32, q = e % GQ;
-        *reinterpret_cast<float4*>(Gs + (ii * 32 + r) * GST + 4 * q) = gv[u];
+        *reinterpret_cast<float4*>(Gs + buf * gbuf + (ii * 32 + r) * GST + 4 * q) = gv[u];
       }
     }
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
       const int e = tid + u * 256;
-      if (e < W8_IMG * CB * 3 * XQ) {
+      if (e < XN) {
         const int ii = e / (CB * 3 * XQ), c = (e / (3 * XQ)) % CB, hq = e % (3 * XQ);
         const int h = hq / XQ, q = hq % XQ;
-        float* d = Hs + ii * hs_img + c * PS + (h + 1) * WP + 1 + 4 * q;
+        float* d = Hs + buf * hbuf + ii * hs_img + c * PS + (h + 1) * WP + 1 + 4 * q;
         d[0] = xv[u].x; d[1] = xv[u].y; d[2] = xv[u].z; d[3] = xv[u].w;
       }
     }
-  }
+  };
+  load(0);
+  // zero padding and the ones planes of both buffers (the stores only write interiors)
+  for (int e = tid; e < 2 * hbuf; e += 256) Hs[e] = (e % hs_img) >= CB * PS ? 1.f : 0.f;
+  __syncthreads();
+  store(0);
   __syncthreads();
   int koff[KT];
 #pragma unroll
@@ -1997,22 +2009,30 @@ __global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restr
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int t = 0; t < KT; ++t) acc[i][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int ii = wid; ii < ni; ii += 4) {
-    const float* gb = Gs + ii * 32 * GST + j * GST + kq;
-    const float* hb = Hs + ii * hs_img + kq;
+  // wave w reduces images w, w + 4, ... (stage by stage), as the unstaged form did
+  for (int sg = 0; sg < NSTG; ++sg) {
+    const int cur = sg & 1;
+    if (sg + 1 < NSTG) load(sg + 1);
+    if (sg * STG + wid < ni) {
+      const float* gb = Gs + cur * gbuf + wid * 32 * GST + j * GST + kq;
+      const float* hb = Hs + cur * hbuf + wid * hs_img + kq;
 #pragma unroll
-    for (int m0 = 0; m0 < P; m0 += 4) {
-      const int base = (m0 / W) * WP + (m0 % W);   // positions m0 .. m0+3: one row
-      const float a0 = gb[m0], a1 = gb[16 * GST + m0];
+      for (int m0 = 0; m0 < P; m0 += 4) {
+        const int base = (m0 / W) * WP + (m0 % W);   // positions m0 .. m0+3: one row
+        const float a0 = gb[m0], a1 = gb[16 * GST + m0];
 #pragma unroll
-      for (int t = 0; t < KT; ++t) {
-        const float bv = hb[base + koff[t]];
-        acc[0][t] = mfma16x16x4(a0, bv, acc[0][t]);
-        acc[1][t] = mfma16x16x4(a1, bv, acc[1][t]);
+        for (int t = 0; t < KT; ++t) {
+          const float bv = hb[base + koff[t]];
+          acc[0][t] = mfma16x16x4(a0, bv, acc[0][t]);
+          acc[1][t] = mfma16x16x4(a1, bv, acc[1][t]);
+        }
       }
     }
+    // buffer cur ^ 1 was last read in stage sg - 1, before the previous barrier
+    if (sg + 1 < NSTG) store(cur ^ 1);
+    __syncthreads();
   }
-  __syncthreads();  // Gs / Hs reads done: the combine buffer aliases them
+  // the last stage's barrier: Gs / Hs reads done, the combine buffer aliases them
   float* red = smem;  // [4 waves][32 rows][TW]
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -2037,7 +2057,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restr
 template <int W, int CB>
 static size_t w8_lds(int PS) {
   constexpr int P = 3 * W, GST = P + 4;
-  const size_t a = (size_t)W8_IMG * 32 * GST + (size_t)W8_IMG * (CB + 1) * PS;
+  const size_t a = (size_t)2 * W8_STG * 32 * GST + (size_t)2 * W8_STG * (CB + 1) * PS;
   const size_t red = (size_t)4 * 32 * (((CB * 9 + 1 + 15) / 16) * 16);
   return 4 * (a > red ? a : red);
 }
