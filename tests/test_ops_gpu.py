@@ -778,3 +778,27 @@ def test_adamw_step_pair_equals_two_steps(zero_after, cuda):
             assert torch.equal(a.exp_avg_sq, b.exp_avg_sq) and torch.equal(a.seg_step, b.seg_step)
             assert torch.equal(a.flat_grad, b.flat_grad)
             assert bool((b.flat_grad == 0).all()) == zero_after
+
+
+@pytest.mark.parametrize("D", [32, 64, 128, 256, 48])
+@pytest.mark.parametrize("M", [1, 7, 1000, 99328])
+def test_norm_fwd_narrow_rows_vs_torch(D, M):
+    """RMSNorm / LayerNorm forward on the narrow-row vector kernels (D = 4L, 64/L rows per
+    wave; D = 48 takes the one-wave-per-row form) against torch fp32, ragged row counts
+    (tolerance: fp32 sums in another order, rel 1e-5 of the output scale)."""
+    from timevqvae.hip._native import plan_trace
+    from timevqvae.hip.xf import layer_norm, rmsnorm
+    torch.manual_seed(D + M)
+    x = torch.randn(M, D, device="cuda") * 3 + 0.5
+    g = torch.rand(D, device="cuda") + 0.5
+    b = torch.randn(D, device="cuda")
+    with torch.no_grad(), plan_trace() as tr:
+        y = rmsnorm(x, g)
+        z = layer_norm(x, g, b, 1e-5)
+    vec = D in (32, 64, 128, 256)
+    assert any(t.startswith(f"rmsnorm_fwd_vec D{D}") for t in tr.lines) == vec
+    assert any(t.startswith(f"layernorm_fwd_vec D{D}") for t in tr.lines) == vec
+    ref_y = x / x.norm(dim=-1, keepdim=True).clamp_min(1e-12) * D ** 0.5 * g
+    ref_z = F.layer_norm(x, (D,), g, b, 1e-5)
+    assert (y - ref_y).abs().max().item() <= 1e-5 * ref_y.abs().max().item()
+    assert (z - ref_z).abs().max().item() <= 1e-5 * ref_z.abs().max().item()
