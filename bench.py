@@ -819,14 +819,18 @@ def rb64_fwd_leg(device):
 
 
 def roofline_leg(device, ms_per_step):
-    """bench JSON `roofline`: the step's top kernel by summed time, the grouped Linear
-    weight gradients of the LF prior (dominant_leg), at top level (also under
-    `wgrad_group`); the VQ codebook assignment (`vq_assign`); the fused ResBlock backward
-    (`resblock_bwd`, resblock_bwd_leg); the LF prior's Linear forward (`linear_fwd`); the LF
-    64-channel conv weight gradient (`conv_wgrad`, conv_wgrad_leg); the whole step against
-    the fp32 MFMA peak (`step`); the largest single conv on MFMA (`conv_t32`)."""
-    out = dominant_leg(device)
-    out["wgrad_group"] = dict(out)
+    """bench JSON `roofline`: the step's top kernel by summed time in the committed step
+    table (profiles/r05_step_kernel_stats.csv: conv_t32_kernel<F,3,3>, the HF 128 -> 128
+    3x3 conv, 2 launches and 158 us per step; conv_t32_leg) at top level (also under
+    `conv_t32`); the grouped Linear weight gradients of the LF prior (`wgrad_group`,
+    dominant_leg: the top kernel of rounds 3-4); the VQ codebook assignment (`vq_assign`);
+    the fused ResBlock backward (`resblock_bwd`, resblock_bwd_leg); the LF prior's Linear
+    forward (`linear_fwd`); the LF 64-channel conv weight gradient (`conv_wgrad`,
+    conv_wgrad_leg); the whole step against the fp32 MFMA peak (`step`)."""
+    t32 = conv_t32_leg(device)
+    out = dict(t32)
+    out["conv_t32"] = t32
+    out["wgrad_group"] = dominant_leg(device)
     out["vq_assign"] = vq_assign_leg(device)
     out["resblock_bwd"] = resblock_bwd_leg(device)
     out["linear_fwd"] = linear_fwd_leg(device)
@@ -838,7 +842,6 @@ def roofline_leg(device, ms_per_step):
                    "source": "tools/count_step_flops.py -> profiles/r03_step_flops.json"}
     out["step_frac"] = out["step"]["frac"]
     out["cu_weighted"] = cu_weighted_leg()
-    out["conv_t32"] = conv_t32_leg(device)
     out["attn_branch"] = attn_branch_leg(device)
     out["conv_n16"] = conv_n16_leg(device)
     out["rb64_fwd"] = rb64_fwd_leg(device)
@@ -883,7 +886,8 @@ def conv_t32_leg(device):
             "achieved": round(achieved, 2), "peak": 157.3, "unit": "TFLOP/s",
             "frac": round(achieved / 157.3, 4),
             "algorithmic_bytes": 4 * (256 * 128 * 3 * 32 * 2 + 128 * 128 * 9),
-            "avg_launch_ms": round(ms, 4), "flops_per_launch": flops}, "t32")
+            "avg_launch_ms": round(ms, 4), "avg_launch_us": round(ms * 1e3, 2),
+            "flops_per_launch": flops}, "t32")
 
 
 def sampler_leg(tr, device, num=1024, reps=5, graph_reps=20, world=1):
