@@ -839,7 +839,7 @@ def roofline_leg(device, ms_per_step):
     out["step"] = {"bound": "mfma", "gflop": STEP_GFLOP, "achieved": round(tf, 2),
                    "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                    "frac": round(tf / FP32_PEAK_TFLOPS, 4),
-                   "source": "tools/count_step_flops.py -> profiles/r03_step_flops.json"}
+                   "source": "tools/count_step_flops.py -> profiles/r05_step_flops.json (step_gflop_at_B256)"}
     out["step_frac"] = out["step"]["frac"]
     out["cu_weighted"] = cu_weighted_leg()
     out["attn_branch"] = attn_branch_leg(device)
