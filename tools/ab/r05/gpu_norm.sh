@@ -4,8 +4,8 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests/test_ops_gpu.py -k norm_fwd tests/test_prior_eval.py tests/test_stage2.py \
-  tests/test_stage2_golden.py tests/test_sampler_full.py -x -q --timeout 200 --timeout-method thread \
+timeout -k 10 500 python -u -m pytest ${R5T:-tests/test_resblock.py tests/test_sampler_full.py tests/test_sampler.py} \
+  -x -q --timeout 200 --timeout-method thread \
   > gpurun_out/norm_tests.log 2>&1 || { tail -30 gpurun_out/norm_tests.log; exit 1; }
 tail -2 gpurun_out/norm_tests.log
 A="--steps 10 --warmup 3 --no-roofline --no-config0 --no-cpu-baseline --no-stage-legs"

@@ -23,8 +23,15 @@ def t(fn, n=20):
     return a.elapsed_time(b) / n * 1000
 
 
+from timevqvae.hip._native import lib  # noqa: E402
+
 torch.manual_seed(0)
 up = Upscale(128, 128, 256).cuda().eval()
+BITS = int(sys.argv[1]) if len(sys.argv) > 1 else 0  # tvq_conv_config bits to add (16: BK 32)
+if BITS:
+    cur = lib().tvq_conv_config(-1)
+    lib().tvq_conv_config(cur | BITS)
+    print("conv config", cur, "->", cur | BITS)
 c = up.conv
 for B in (256, 1024):
     x = torch.randn(B, 128, 96, device="cuda")
