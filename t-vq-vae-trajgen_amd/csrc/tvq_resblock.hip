@@ -99,7 +99,11 @@ struct RB {
   static constexpr int PARTW = WPS > 1 ? WPS * C * KCR : 0;  // wgrad chunk partials
   // backward kernels' LDS: G planes | S planes | panel | conv partials | wgrad partials |
   // ones plane K1 | zeros plane K0 = K1 + PS
-  static constexpr int K1OFF = 2 * PLANE + PANEL + PARTC + PARTW;
+  // the weight-gradient partials are summed (rb_wgrad_sum) before the conv items write
+  // theirs, so the two share one region (round 5: RB<16,32>'s backward 99 -> 74 KB, two
+  // blocks per CU beside the other streams' kernels)
+  static constexpr int PARTCW = PARTC > PARTW ? PARTC : PARTW;
+  static constexpr int K1OFF = 2 * PLANE + PANEL + PARTCW;
   static constexpr int CONSTP = 2 * PS;  // ones plane + zeros plane
   static_assert(P % 16 == 0 && W % 4 == 0 && C % NCH == 0 && CPC % 4 == 0 &&
                     RB_NW % (NR * NCH) == 0 && RB_NW % WPS == 0 && PSTEPS % WPS == 0,
@@ -673,7 +677,7 @@ __device__ __forceinline__ void rb_bwd2_body(const RBArgs& a, double* rb_smem,
   float* S = G + R::PLANE;                         // s2 planes
   float* A = S + R::PLANE;                         // transposed w2
   float* Pc = A + R::PANEL;
-  float* Pw = Pc + R::PARTC;
+  float* Pw = Pc;  // summed before the conv items write Pc
   float* K1 = reinterpret_cast<float*>(rb_smem) + R::K1OFF;  // ones | zeros planes
   const int b = blockIdx.x;
   const int64_t img0 = (int64_t)b * R::C * R::P;
@@ -717,11 +721,15 @@ __device__ __forceinline__ void rb_bwd2_body(const RBArgs& a, double* rb_smem,
   RB_MARK(2);
   float* slab_row = a.slab2 + (int64_t)b * R::C * R::KC;
   rb_wgrad_items<R>(G, S, K1, Pw, slab_row);
+  if (R::WPS > 1) {  // the partials, then the region is the conv items'
+    __syncthreads();
+    rb_wgrad_sum<R>(Pw, slab_row);
+    __syncthreads();
+  }
   RB_MARK(3);
   rb_conv_items<R, true>(A, G, Pc);
   __syncthreads();
   RB_MARK(4);
-  rb_wgrad_sum<R>(Pw, slab_row);
   double s[3][R::CPW][R::PPL];
 #pragma unroll
   for (int u = 0; u < R::CPW; ++u)
@@ -763,7 +771,7 @@ __device__ __forceinline__ void rb_bwd1_body(const RBArgs& a, double* rb_smem, R
   float* S = G + R::PLANE;                         // s1 planes
   float* A = S + R::PLANE;                         // transposed w1
   float* Pc = A + R::PANEL;
-  float* Pw = Pc + R::PARTC;
+  float* Pw = Pc;  // summed before the conv items write Pc
   float* K1 = reinterpret_cast<float*>(rb_smem) + R::K1OFF;  // ones | zeros planes
   const int b = blockIdx.x, l = threadIdx.x & 63;
   const int64_t img0 = (int64_t)b * R::C * R::P;
@@ -812,11 +820,15 @@ __device__ __forceinline__ void rb_bwd1_body(const RBArgs& a, double* rb_smem, R
   RB_MARK(2);
   float* slab_row = a.slab1 + (int64_t)b * R::C * R::KC;
   rb_wgrad_items<R>(G, S, K1, Pw, slab_row);
+  if (R::WPS > 1) {  // the partials, then the region is the conv items'
+    __syncthreads();
+    rb_wgrad_sum<R>(Pw, slab_row);
+    __syncthreads();
+  }
   RB_MARK(3);
   rb_conv_items<R, true>(A, G, Pc);
   __syncthreads();
   RB_MARK(4);
-  rb_wgrad_sum<R>(Pw, slab_row);
   double s[1][R::CPW][R::PPL];
 #pragma unroll
   for (int u = 0; u < R::CPW; ++u)
@@ -863,12 +875,12 @@ __global__ __launch_bounds__(RB_T) void rb_bwd12_kernel(RBArgs a2, RBArgs a1) {
 // ---------------------------------------------------------------- host side
 template <class R>
 static size_t rb_lds(int kind) {
-  const size_t PL = R::PLANE, PA = R::PANEL, PC = R::PARTC, PW = R::PARTW + R::CONSTP;
+  const size_t PL = R::PLANE, PA = R::PANEL, PC = R::PARTC;
   switch (kind) {
     case 0: return 4 * (PL + PA + PC);               // fwd1
     case 1: return 4 * (PL + PA + PC);               // fwd2
     case 2: return 4 * (2 * PL + PA + PC);           // eval
-    default: return 4 * (2 * PL + PA + PC + PW);     // bwd2, bwd1
+    default: return 4 * (2 * PL + PA + R::PARTCW + R::CONSTP);  // bwd2, bwd1
   }
 }
 
