@@ -715,7 +715,10 @@ __global__ __launch_bounds__(NW * 64) void conv_t32_kernel(const float* __restri
 // (112 KB, 18 barriers for a 3x3 128-channel conv) runs the 128->128 conv at 78.7 us vs
 // 86.7 us for BK = 32 (56 KB); in the joint step, where the LDS is shared with the
 // concurrent streams' kernels, the two are within 0.5 % (7.29 vs 7.25 ms).
-static int g_t32_bk = 64;  // K-stage depth: 64, or 32 / 16 with tvq_conv_config bit 16 / 32
+#ifndef TVQ_T32_BK
+#define TVQ_T32_BK 64
+#endif
+static int g_t32_bk = TVQ_T32_BK;  // K-stage depth: 64, or 32 / 16 (tvq_conv_config bit 16 / 32)
 static int g_t32_nw = 12;  // waves per block (12, or 4 with tvq_conv_config bit 64)
 // 64-channel tile for narrow maps (tvq_conv_config bit 128 turns it on).  Off by default:
 // at the LF band's 64->64 3x3 conv (6144 positions, 64 blocks) it takes 27.5 us against
