@@ -402,7 +402,7 @@ def config0_leg(device, cpu=True):
         del tr
     if cpu:
         from oracle import cpu_baseline
-        threads = int(os.environ.get("TVQ_CPU_THREADS", min(16, os.cpu_count() or 1)))
+        threads = cpu_threads()
         for b in (32, 256):
             s = cpu_baseline.measure_stage1(threads, b, 128, 256, steps=5, warmup=2)
             out[f"cpu_B{b}_ms_per_step"] = round(s * 1e3, 1)
@@ -965,22 +965,140 @@ def sampler_leg(tr, device, num=1024, reps=5, graph_reps=20, world=1):
     return out
 
 
+def host_cpus():
+    """(CPUs this process may run on = len(sched_getaffinity), the cgroup CPU quota in CPUs
+    or None when unlimited)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
+def cpu_threads():
+    """Torch threads of the CPU legs: TVQ_CPU_THREADS, else every CPU of the process's
+    affinity mask (the host's cores)."""
+    return int(os.environ.get("TVQ_CPU_THREADS", host_cpus()[0]))
+
+
 def cpu_baseline_leg():
     """the CPU port of the joint step (oracle/cpu_baseline.py, every
     reference dropout on) on the host's cores: 2 untimed warmups, then the median of 5
-    timed steps; the CPU model is recorded.  The port is checked against the reference's
-    own CPU step in the build container (tools/cpu_ref_compare.py ->
-    profiles/r03_cpu_ref_compare.json)."""
+    timed steps; the CPU model is recorded.  Timed at the affinity count (`cores`) and at
+    16 threads (the box's nominal share); `value` is the faster of the two, so the
+    baseline is the strongest this host gives.  The port is checked against the
+    reference's own CPU step in the build container (tools/cpu_ref_compare.py ->
+    profiles/r06_cpu_ref_compare.json)."""
     from oracle import cpu_baseline
-    threads = int(os.environ.get("TVQ_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    med, ts = cpu_baseline.measure(threads, steps=5, warmup=2, detail=True)
-    return {"value": round(1.0 / med, 4), "unit": "steps/s", "cores": threads, "kind": "port",
+    aff, quota = host_cpus()
+    threads = cpu_threads()
+    runs = {}
+    for n in dict.fromkeys((threads, min(16, threads))):
+        med, ts = cpu_baseline.measure(n, steps=5, warmup=2, detail=True)
+        runs[n] = (med, ts)
+    best = min(runs, key=lambda n: runs[n][0])
+    med, ts = runs[best]
+    return {"value": round(1.0 / med, 4), "unit": "steps/s", "cores": best, "kind": "port",
+            "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "by_threads": {str(n): round(1.0 / r[0], 4) for n, r in runs.items()},
             "cpu_model": cpu_baseline.cpu_model(),
             "step_s": [round(t, 4) for t in ts],
             "sample": f"median of 5 timed joint steps (after 2 untimed warmups) of "
-                      f"oracle/cpu_baseline.py at B=256,C=6,T=256,K=512 on {threads} torch "
-                      f"threads, every reference dropout on: {med:.3f} s/step "
-                      f"(port vs reference's own CPU step: profiles/r03_cpu_ref_compare.json)"}
+                      f"oracle/cpu_baseline.py at B=256,C=6,T=256,K=512, every reference "
+                      f"dropout on, timed at {' and '.join(str(n) for n in runs)} torch threads "
+                      f"(affinity {aff} CPUs, cgroup quota {quota}); the faster, {best} "
+                      f"threads: {med:.3f} s/step (port vs reference's own CPU step: "
+                      f"profiles/r06_cpu_ref_compare.json)"}
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(nproc, argv):
+    """`bench.py --gpus N` (N > 1) started without WORLD_SIZE: this parent never touches the
+    GPU (it does not import the package, query devices or create a stream).  It starts N
+    fresh child processes of this same script (no exec), each with RANK = LOCAL_RANK = i,
+    WORLD_SIZE = N, LOCAL_WORLD_SIZE = N and MASTER_ADDR / MASTER_PORT on 127.0.0.1 -- the
+    environment `torch.distributed.run --nnodes 1 --nproc-per-node N` gives, replacing the
+    reference's single-device Lightning Trainer (scripts/train.py:33-43, devices=1).  Rank 0's
+    stdout is the bench line; every other rank's stdout goes to stderr.  When a rank exits
+    non-zero the others are terminated (by their own PIDs) and the parent exits with that
+    rank's status; it returns 0 only when all N ranks returned 0."""
+    import signal
+    import subprocess
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nproc),
+                    "LOCAL_WORLD_SIZE": str(nproc), "GROUP_RANK": "0",
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=None if r == 0 else sys.stderr))
+    status = 0
+    live = list(range(nproc))
+    while live:
+        for r in list(live):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            live.remove(r)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"bench launcher: rank {r} exited with {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for o in live:
+                    try:
+                        procs[o].send_signal(signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.05)
+        if status and live:  # give them 30 s to leave, then SIGKILL the stragglers
+            deadline = time.time() + 30
+            while time.time() < deadline and any(procs[o].poll() is None for o in live):
+                time.sleep(0.1)
+            for o in live:
+                if procs[o].poll() is None:
+                    procs[o].kill()
+                    procs[o].wait()
+            live = []
+    return status
+
+
+def dry_launch(args):
+    """--dry-launch: the process-group half of the N-rank path without a model (the launcher
+    test): every rank joins the group, checks the world size against --gpus, and the ranks
+    exchange their ids with one all-reduce; rank 0 prints one JSON line.  --dry-fail-rank R
+    makes rank R exit 3 after joining (the launcher must then exit non-zero)."""
+    backend = os.environ.get("TVQ_BENCH_BACKEND", "nccl")
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if backend == "nccl":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dist.init_process_group(backend)
+    assert dist.get_world_size() == args.gpus == world, (dist.get_world_size(), args.gpus)
+    if args.dry_fail_rank == rank:
+        print(f"rank {rank}: forced failure (--dry-fail-rank)", file=sys.stderr, flush=True)
+        os._exit(3)
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else "cpu"
+    ids = torch.zeros(world, dtype=torch.int64, device=dev)
+    ids[rank] = rank + 1
+    dist.all_reduce(ids)
+    if rank == 0:
+        print(json.dumps({"dry_launch": True, "world_size": dist.get_world_size(),
+                          "backend": dist.get_backend(), "ranks": [int(v) - 1 for v in ids]}),
+              flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def main():
@@ -994,11 +1112,24 @@ def main():
     ap.add_argument("--no-config0", action="store_true")
     ap.add_argument("--no-stage-legs", action="store_true", help="skip the per-stage legs")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="launcher check: join the process group, exchange rank ids, no model")
+    ap.add_argument("--dry-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args.gpus, sys.argv[1:]))
+    if args.dry_launch:
+        return dry_launch(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N ranks "
+                         f"with `python bench.py --gpus N` or torch.distributed.run "
+                         f"--nproc-per-node N ... bench.py --gpus N")
     # rehearsal of the N > 1 path on a one-GPU box (all ranks on cuda:0 over gloo; RCCL
     # refuses two ranks on one device): TVQ_BENCH_REHEARSAL=1.  Timings so obtained are not
     # scaling numbers.
@@ -1006,8 +1137,12 @@ def main():
     if rehearsal:
         local = 0
     if world > 1:
+        if not rehearsal and torch.cuda.device_count() < world:
+            raise SystemExit(f"bench.py: {world} ranks but {torch.cuda.device_count()} visible GPUs")
         torch.cuda.set_device(local)
         dist.init_process_group("gloo" if rehearsal else "nccl")
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+        assert rehearsal or dist.get_backend() == "nccl", dist.get_backend()
     device = torch.device("cuda", local)
     tr = JointTrainer(device, world)
     batch = synthetic_batch(1234 + rank, device)
@@ -1035,11 +1170,6 @@ def main():
         elapsed = max(rank_elapsed)
     loss1 = float(out1["loss"].detach().sum())
     loss2 = float(out2["loss"].detach())
-    # each stage's optimizer step alone (graph-replayed; the reference trains them one after
-    # the other), beside the concurrent joint step
-    alone = None
-    if world == 1 and not args.eager and not args.no_stage_legs:
-        alone = {w: round(tr.stage_alone_ms(batch, w), 3) for w in ("stage1", "stage2")}
 
     if rank == 0:
         value = world * args.steps / elapsed
@@ -1067,14 +1197,6 @@ def main():
             "losses": {"stage1": round(loss1, 5), "stage2": round(loss2, 5)},
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 3),
         }
-        if alone is not None:
-            res["stage1_ms_per_step"] = alone["stage1"]
-            res["stage2_ms_per_step"] = alone["stage2"]
-            res["sequential_ms_per_step"] = round(alone["stage1"] + alone["stage2"], 3)
-            res["ms_per_step_is"] = ("stage1 and stage2 steps run concurrently on one GPU "
-                                     "(independent: stage2 trains on a frozen stage1 snapshot); "
-                                     "sequential_ms_per_step = the two stages alone, one after "
-                                     "the other, as the reference trains them")
         if world > 1:
             res["dist"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
                            "rank_elapsed_s": [round(v, 6) for v in rank_elapsed],
@@ -1091,9 +1213,23 @@ def main():
             res["cpu_baseline"] = cpu_baseline_leg()
     if not args.no_sampler:  # every rank: replicas sample concurrently at world > 1
         samp = sampler_leg(tr, device, world=world)
+    # each stage's optimizer step alone (graph-replayed; the reference trains them one after
+    # the other), beside the concurrent joint step -- last, since its extra optimizer steps
+    # move the weights, LR schedule, BN statistics and codebooks the sampler leg reads
+    alone = None
+    if world == 1 and not args.eager and not args.no_stage_legs:
+        alone = {w: round(tr.stage_alone_ms(batch, w), 3) for w in ("stage1", "stage2")}
     if rank == 0:
         if not args.no_sampler:
             res["sampler"] = samp
+        if alone is not None:
+            res["stage1_ms_per_step"] = alone["stage1"]
+            res["stage2_ms_per_step"] = alone["stage2"]
+            res["sequential_ms_per_step"] = round(alone["stage1"] + alone["stage2"], 3)
+            res["ms_per_step_is"] = ("stage1 and stage2 steps run concurrently on one GPU "
+                                     "(independent: stage2 trains on a frozen stage1 snapshot); "
+                                     "sequential_ms_per_step = the two stages alone, one after "
+                                     "the other, as the reference trains them")
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

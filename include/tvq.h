@@ -34,8 +34,13 @@ typedef void* tvq_stream_t; /* hipStream_t */
 const char* tvq_last_error(void);
 int tvq_abi_version(void);
 /* Source stamp compiled in by csrc/Makefile: the first 16 hex digits of the sha1 of every
- * csrc *.hip / *.h (sorted by name) followed by include/tvq.h. */
+ * csrc *.hip / *.h (sorted by name) followed by include/tvq.h.  The same 16 digits follow the
+ * literal "tvq_source_hash=" in the library file, so a loader can read the stamp without
+ * mapping the library. */
 const char* tvq_source_hash(void);
+/* The EXTRA build defines the library was compiled with (A/B builds; "" by default).  Kept
+ * out of the source stamp so an A/B build still names the sources it came from. */
+const char* tvq_build_extra(void);
 /* Register a zeroed pool of n int32 counters on `device` (a HIP device index).  The
  * kernels that finish a grid-level reduction in their last-arriving block (BatchNorm /
  * Snake statistics, column sums, split-K slabs) take slots from it and leave them

@@ -76,7 +76,14 @@ __device__ __forceinline__ void adamw_chunk(float* __restrict__ p, const float* 
   const int64_t start = chunks[3 * chunk];
   const int len = (int)chunks[3 * chunk + 1];
   const int seg = (int)chunks[3 * chunk + 2];
-  if (gates[seg] == 0.f) return;
+  if (gates[seg] == 0.f) {
+    // a gated-off segment is not updated, but its gradient is still cleared (the next
+    // step's zero_grad), so a non-finite value left by a dropped branch cannot survive
+    // until the gate reopens
+    if (gz)
+      for (int j = threadIdx.x; j < len; j += 256) gz[start + j] = 0.f;
+    return;
+  }
   const double lr = lr_step[0];
   const double t = seg_step[seg];
   const double bc1 = 1.0 - pow((double)b1, t);

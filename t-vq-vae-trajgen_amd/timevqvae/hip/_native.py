@@ -47,20 +47,21 @@ def source_hash():
 
 
 def built_hash(path=None):
-    """tvq_source_hash() of the built library at `path` (None if missing or unstamped),
-    read without initialising the GPU."""
+    """tvq_source_hash() of the built library at `path` (None if missing or unstamped), read
+    from the file's bytes (the literal "tvq_source_hash=<16 hex>" the Makefile compiles in):
+    the library is not loaded, so a later ctypes.CDLL of a rebuilt file in this process is
+    not handed a stale mapping, and the GPU is not initialised."""
+    import re
     path = path or LIB_PATH
     if not os.path.exists(path):
         return None
-    try:
-        f = ctypes.CDLL(path).tvq_source_hash
-    except (OSError, AttributeError):
-        return None
-    f.restype = ctypes.c_char_p
-    return f().decode()
+    with open(path, "rb") as f:
+        m = re.search(rb"tvq_source_hash=([0-9a-f]{16})", f.read())
+    return m.group(1).decode() if m else None
 
 
 sig("tvq_source_hash", restype=ctypes.c_char_p)
+sig("tvq_build_extra", restype=ctypes.c_char_p)
 sig("tvq_counter_pool", I64, P, I64)
 sig("tvq_counter_capture", I64)
 sig("tvq_plan_trace", I64)

@@ -135,6 +135,32 @@ class MaskGIT(nn.Module):
         RNG: {"ratio_l", "rand_l", "ratio_h", "rand_h"} for _randomly_mask_tokens
         (np.random.uniform ratios, torch.rand scores) and {"cls_l", "cls_h"} for the
         class-drop draws of each transformer (bidirectional_transformer.py:140-143)."""
+        loss_l, loss_h = self._priors(x, y, draws, None)
+        return add_losses(loss_l, loss_h), (loss_l, loss_h)
+
+    def forward_backward(self, x, y, one, draws=None):
+        """forward(x, y) and the backward of its loss in one pass, each prior's backward issued
+        on that prior's own stream right after its loss: the two priors are disjoint
+        subgraphs of loss_l + loss_h (d/d loss_l = d/d loss_h = 1), so backpropagating each
+        from its own root gives exactly the gradients of the sum -- and the LF prior's
+        backward does not wait for the HF prior's forward (nor the HF backward for the LF
+        forward) at a join before the loss.  `one`: a cached 0-dim ones tensor (the root
+        gradient).  Returns a callable that builds (loss, (loss_l, loss_h)); call it after
+        the streams are joined (the enclosing streams.concurrent() region's exit)."""
+        loss_l, loss_h = self._priors(x, y, draws, one)
+
+        def total():
+            with torch.no_grad():
+                return add_losses(loss_l.detach(), loss_h.detach()), (loss_l.detach(),
+                                                                      loss_h.detach())
+        return total
+
+    def _priors(self, x, y, draws, one):
+        """The body forward() and forward_backward() share (maskgit.py:155-192): encode with
+        the frozen stage1, mask both token sequences, run the HF prior on a side stream
+        concurrently with the LF prior, each to its masked cross-entropy.  `one` given: each
+        prior's backward from its own loss right after it, and the side stream is left for
+        the enclosing concurrent region to join; `one` None: forward only, joined here."""
         self.encoder_l.eval()
         self.vq_model_l.eval()
         self.encoder_h.eval()
@@ -149,60 +175,23 @@ class MaskGIT(nn.Module):
         self.transformer_h._class_rand = dr.get("cls_h")
         try:
             with streams.branch(x.device) as br:  # HF transformer concurrently with LF
-                br.inputs(y, s_l_M, s_h_M, s_h, keep_h)
+                br.inputs(y, s_l_M, s_h_M, s_h, keep_h, *(() if one is None else (one,)))
                 with wgrad.tag("prior_h"):  # its weight gradients: one grouped launch
                     logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
-                    mask_pred_loss_h = masked_cross_entropy(logits_h, s_h, keep_h)
-                br.outputs(mask_pred_loss_h)
-            with wgrad.tag("prior_l"):
-                logits_l = self.masked_prediction(self.transformer_l, y, s_l_M)
-                mask_pred_loss_l = masked_cross_entropy(logits_l, s_l, keep_l)
-            br.join()
-        finally:
-            self.transformer_l._class_rand = self.transformer_h._class_rand = None
-        return add_losses(mask_pred_loss_l, mask_pred_loss_h), (mask_pred_loss_l, mask_pred_loss_h)
-
-    def forward_backward(self, x, y, one, draws=None):
-        """forward(x, y) and the backward of its loss in one pass, each prior's backward issued
-        on that prior's own stream right after its loss: the two priors are disjoint
-        subgraphs of loss_l + loss_h (d/d loss_l = d/d loss_h = 1), so backpropagating each
-        from its own root gives exactly the gradients of the sum -- and the LF prior's
-        backward does not wait for the HF prior's forward (nor the HF backward for the LF
-        forward) at a join before the loss.  `one`: a cached 0-dim ones tensor (the root
-        gradient).  Returns a callable that builds (loss, (loss_l, loss_h)); call it after
-        the streams are joined (the enclosing streams.concurrent() region's exit)."""
-        self.encoder_l.eval()
-        self.vq_model_l.eval()
-        self.encoder_h.eval()
-        self.vq_model_h.eval()
-        dr = draws or {}
-        s_l, s_h = self.encode_tokens(x)
-        s_l_M, keep_l = self._randomly_mask_tokens(s_l, self.mask_token_ids["lf"], x.device,
-                                                   dr.get("ratio_l"), dr.get("rand_l"))
-        s_h_M, keep_h = self._randomly_mask_tokens(s_h, self.mask_token_ids["hf"], x.device,
-                                                   dr.get("ratio_h"), dr.get("rand_h"))
-        self.transformer_l._class_rand = dr.get("cls_l")
-        self.transformer_h._class_rand = dr.get("cls_h")
-        try:
-            with streams.branch(x.device) as br:
-                br.inputs(y, s_l_M, s_h_M, s_h, keep_h, one)
-                with wgrad.tag("prior_h"):
-                    logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
                     loss_h = masked_cross_entropy(logits_h, s_h, keep_h)
-                    torch.autograd.backward(loss_h, one)
+                    if one is not None:
+                        torch.autograd.backward(loss_h, one)
                 br.outputs(loss_h)
             with wgrad.tag("prior_l"):
                 logits_l = self.masked_prediction(self.transformer_l, y, s_l_M)
                 loss_l = masked_cross_entropy(logits_l, s_l, keep_l)
-                torch.autograd.backward(loss_l, one)
+                if one is not None:
+                    torch.autograd.backward(loss_l, one)
+            if one is None:
+                br.join()
         finally:
             self.transformer_l._class_rand = self.transformer_h._class_rand = None
-
-        def total():
-            with torch.no_grad():
-                return add_losses(loss_l.detach(), loss_h.detach()), (loss_l.detach(),
-                                                                      loss_h.detach())
-        return total
+        return loss_l, loss_h
 
     def _randomly_mask_tokens(self, s, mask_token_id, device, ratio=None, rand=None):
         """maskgit.py:194-216 on device; returns (s_M, mask) with mask=True for kept tokens.

@@ -54,3 +54,23 @@ def test_library_stamp_matches_sources():
     assert _native.built_hash() == _native.source_hash(), (
         f"libtvq_hip.so was built from other sources ({_native.built_hash()} vs "
         f"{_native.source_hash()}): run __graft_entry__.build()")
+
+
+@pytest.mark.gpu
+def test_mapped_library_is_the_trees(cuda):
+    """On the GPU box: the libtvq_hip.so this process actually mapped (after a kernel ran
+    through it) is the in-tree file, and its compiled-in stamp -- asked of the mapped library
+    itself, not read from the file -- equals the hash of the sources in this tree."""
+    import torch
+    from timevqvae.hip import _native
+    h = _native.lib()
+    x = torch.zeros(64, device=cuda)
+    _native.call("tvq_fill", _native.ptr(x), 64, 1.5, _native.stream_ptr())
+    torch.cuda.synchronize()
+    assert float(x.sum()) == 96.0
+    mapped = sorted({ln.split()[-1] for ln in open("/proc/self/maps")
+                     if ln.rstrip().endswith("libtvq_hip.so")})
+    assert mapped == [os.path.realpath(_native.LIB_PATH)], mapped
+    stamp = h.tvq_source_hash().decode()
+    assert stamp == _native.source_hash(), f"mapped library {stamp} != sources {_native.source_hash()}"
+    print(f"mapped {mapped[0]} stamp {stamp} extra '{h.tvq_build_extra().decode()}'")

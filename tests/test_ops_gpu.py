@@ -780,6 +780,36 @@ def test_adamw_step_pair_equals_two_steps(zero_after, cuda):
             assert bool((b.flat_grad == 0).all()) == zero_after
 
 
+def test_adamw_zero_after_step_clears_gated_segments(cuda):
+    """zero_after_step with a gated-off segment (layer dropout skipped the branch): the
+    segment's parameters and moments are untouched, and its gradient -- here a NaN a dropped
+    branch could leave -- is still cleared, so it cannot be applied when the gate reopens."""
+    from timevqvae.hip.optim import FusedAdamW, step_pair
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(300, 20), torch.nn.Linear(20, 7)).to(cuda)
+    o = FusedAdamW(m.parameters(), lr=1e-3, weight_decay=0.01)
+    o2 = FusedAdamW(torch.nn.Linear(5, 3).to(cuda).parameters(), lr=1e-3)
+    o.zero_after_step = o2.zero_after_step = True
+    o.zero_grad()
+    o2.zero_grad()
+    o.flat_grad.normal_()
+    o.flat_grad[:6000] = float("nan")  # the first segment: Linear(300, 20).weight
+    before = o.flat.clone()
+    o.gates.fill_(1.0)
+    o.gates[0] = 0.0
+    o2.gates.fill_(1.0)
+    step_pair(o, o2, gates_ready=True)
+    torch.cuda.synchronize()
+    assert bool((o.flat_grad == 0).all())
+    assert torch.equal(o.flat[:6000], before[:6000])
+    assert bool((o.exp_avg[:6000] == 0).all()) and float(o.seg_step[0]) == 0.0
+    assert bool(torch.isfinite(o.flat).all()) and not torch.equal(o.flat[6000:], before[6000:])
+    o.gates.fill_(1.0)  # the gate reopens: the update sees a zero gradient, not the NaN
+    o.zero_grad()
+    o.step(gates_ready=True)
+    assert bool(torch.isfinite(o.flat).all())
+
+
 @pytest.mark.parametrize("D", [32, 64, 128, 256, 48])
 @pytest.mark.parametrize("M", [1, 7, 1000, 99328])
 def test_norm_fwd_narrow_rows_vs_torch(D, M):
