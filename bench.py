@@ -980,39 +980,37 @@ def host_cpus():
 
 
 def cpu_threads():
-    """Torch threads of the CPU legs: TVQ_CPU_THREADS, else every CPU of the process's
-    affinity mask (the host's cores)."""
-    return int(os.environ.get("TVQ_CPU_THREADS", host_cpus()[0]))
+    """Torch threads of the CPU legs: TVQ_CPU_THREADS, else the CPUs this process can use
+    (the host's cores) = its affinity mask, capped by the cgroup CPU quota.  On
+    the GPU box the mask holds all 256 CPUs of the EPYC 9575F pair but the quota is 16 CPUs,
+    and the port's joint step measured 0.69 / 1.07 / 2.29 s at 16 / 32 / 64 threads there
+    (profiles/r06_cpu_threads_probe.txt): threads beyond the quota only wait for it."""
+    if "TVQ_CPU_THREADS" in os.environ:
+        return int(os.environ["TVQ_CPU_THREADS"])
+    aff, quota = host_cpus()
+    return max(1, min(aff, int(quota))) if quota else aff
 
 
 def cpu_baseline_leg():
     """the CPU port of the joint step (oracle/cpu_baseline.py, every
-    reference dropout on) on the host's cores: 2 untimed warmups, then the median of 5
-    timed steps; the CPU model is recorded.  Timed at the affinity count (`cores`) and at
-    16 threads (the box's nominal share); `value` is the faster of the two, so the
-    baseline is the strongest this host gives.  The port is checked against the
-    reference's own CPU step in the build container (tools/cpu_ref_compare.py ->
-    profiles/r06_cpu_ref_compare.json)."""
+    reference dropout on) on the CPUs this process may use (cpu_threads): 2 untimed warmups,
+    then the median of 5 timed steps; the CPU model, the affinity mask size and the cgroup
+    quota are recorded.  The port is checked against the reference's own CPU step in the
+    build container (tools/cpu_ref_compare.py -> profiles/r06_cpu_ref_compare.json)."""
     from oracle import cpu_baseline
     aff, quota = host_cpus()
     threads = cpu_threads()
-    runs = {}
-    for n in dict.fromkeys((threads, min(16, threads))):
-        med, ts = cpu_baseline.measure(n, steps=5, warmup=2, detail=True)
-        runs[n] = (med, ts)
-    best = min(runs, key=lambda n: runs[n][0])
-    med, ts = runs[best]
-    return {"value": round(1.0 / med, 4), "unit": "steps/s", "cores": best, "kind": "port",
+    med, ts = cpu_baseline.measure(threads, steps=5, warmup=2, detail=True)
+    return {"value": round(1.0 / med, 4), "unit": "steps/s", "cores": threads, "kind": "port",
             "affinity_cpus": aff, "cgroup_cpu_quota": quota,
-            "by_threads": {str(n): round(1.0 / r[0], 4) for n, r in runs.items()},
             "cpu_model": cpu_baseline.cpu_model(),
             "step_s": [round(t, 4) for t in ts],
             "sample": f"median of 5 timed joint steps (after 2 untimed warmups) of "
                       f"oracle/cpu_baseline.py at B=256,C=6,T=256,K=512, every reference "
-                      f"dropout on, timed at {' and '.join(str(n) for n in runs)} torch threads "
-                      f"(affinity {aff} CPUs, cgroup quota {quota}); the faster, {best} "
-                      f"threads: {med:.3f} s/step (port vs reference's own CPU step: "
-                      f"profiles/r06_cpu_ref_compare.json)"}
+                      f"dropout on, on {threads} torch threads = the CPUs this process may use "
+                      f"(affinity mask {aff} CPUs capped by the cgroup quota of {quota} CPUs; "
+                      f"profiles/r06_cpu_threads_probe.txt): {med:.3f} s/step (port vs the "
+                      f"reference's own CPU step: profiles/r06_cpu_ref_compare.json)"}
 
 
 def _free_port():

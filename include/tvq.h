@@ -819,6 +819,29 @@ int tvq_minmax_transform(const double* X, int64_t N, int64_t L, int64_t F, const
 int tvq_minmax_inverse(const float* x, int64_t N, int64_t L, int64_t F, const double* scale,
                        const double* min_, float* out, tvq_stream_t stream);
 
+/* ---- Upscale's first conv on the nearest-upsampled LF tokens (tvq_upscale.hip;
+ * reference bidirectional_transformer.py:12-30 Upscale.forward: interpolate(nearest, m) ->
+ * Conv1d(d, H, 3, padding 1) [-> GELU [-> BatchNorm1d eval]]), computed on the n-token grid:
+ * Z = x Wcat^T with Wcat = [W_0; W_1; W_2] (3 H, d), then out[f j + r] = b + A_{j-1 or j}
+ * + B_j + C_{j or j+1}; the backward forms the per-token window sums S = [S_0 | S_1 | S_2]
+ * of dY, dx = S Wcat, dWcat = S^T x.  f = m / n >= 2 (integer), n <= 64, m <= 240. */
+/* Wcat[(t H + c) d + k] = w[(c d + k) 3 + t] for w (H, d, 3). */
+int tvq_ups_pack(const float* w, int64_t H, int64_t D, float* wcat, tvq_stream_t stream);
+/* dw[(c d + k) 3 + t] (+)= dwcat[(t H + c) d + k]. */
+int tvq_ups_wscatter(const float* dwcat, int64_t H, int64_t D, float* dw, int64_t accumulate,
+                     tvq_stream_t stream);
+/* z (B n, 3 H) -> out (B, H, f n).  mode 0: out = GELU(v) and pre = v (training, the
+ * erff GELU of tvq_gelu_fwd); 1: out = v; 2: out = BN_eval(GELU(v)) from the running
+ * statistics (sampling).  v = conv + bias (bias may be NULL). */
+int tvq_ups_combine(const float* z, int64_t B, int64_t n, int64_t f, int64_t H,
+                    const float* bias, int64_t mode, const float* bn_w, const float* bn_b,
+                    const float* bn_rm, const float* bn_rv, float bn_eps, float* out, float* pre,
+                    tvq_stream_t stream);
+/* s (B n, 3 H) = window sums of dY1 = dy (B, H, f n) [* GELU'(pre) when pre != NULL];
+ * part (B, H) (optional) = per-image sums of dY1 (the bias gradient's partials). */
+int tvq_ups_sums(const float* dy, const float* pre, int64_t B, int64_t n, int64_t f, int64_t H,
+                 float* s, float* part, tvq_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,10 @@ def built_hash(path=None):
 
 sig("tvq_source_hash", restype=ctypes.c_char_p)
 sig("tvq_build_extra", restype=ctypes.c_char_p)
+sig("tvq_ups_pack", P, I64, I64, P, P)
+sig("tvq_ups_wscatter", P, I64, I64, P, I64, P)
+sig("tvq_ups_combine", P, I64, I64, I64, I64, P, I64, P, P, P, P, F32, P, P, P)
+sig("tvq_ups_sums", P, P, I64, I64, I64, I64, P, P, P)
 sig("tvq_counter_pool", I64, P, I64)
 sig("tvq_counter_capture", I64)
 sig("tvq_plan_trace", I64)

@@ -35,10 +35,14 @@ from ..hip.xf import (attn_branch, attn_branch_supported, batch_colsum, drop_fir
                       upsample_nearest_t)
 from ..hip._native import call, grad_sink, ptr, stream_ptr, value
 from ..hip.sample import codebook_gather_nchw, full_tokens, maskgit_sample, tied_logits_sample
+from ..hip.upscale import supported as ups_supported
+from ..hip.upscale import upsample_conv_gelu, upsample_conv_gelu_bn_eval
 
 # the HF prior's sampling step straight from its head (no logits in memory); 0: form the
 # logits and sample them (A/B and diagnosis)
 FUSED_SAMPLE = os.environ.get("TVQ_FUSED_SAMPLE", "1") != "0"
+# Upscale's first conv on the LF token grid (hip.upscale); False: upsample, then conv (tests)
+UPS_ON_TOKENS = os.environ.get("TVQ_UPS_TOKENS", "1") != "0"
 
 
 # ------------------------------------------------------------------ x-transformers tree
@@ -292,15 +296,25 @@ class Upscale(nn.Module):
 
     def forward(self, x, upscale_size: int):
         """x: (b n d) -> (b m d)."""
-        x = upsample_nearest_t(x, upscale_size)          # b n d -> b d m, one kernel
+        x = self.first(x, upscale_size)
         c = self.conv
-        if bn_eval_fusable(x, c[2], c[0].weight, c[0].bias):  # eval: one launch
-            x = conv2d_bn_eval(x, c[0].weight, c[0].bias, c[2], None, pre_gelu=True)
-        else:
-            x = gelu(conv2d(x, c[0].weight, c[0].bias))
-            x = bn_snake(x, c[2], None)
         x = conv2d(x, c[3].weight, c[3].bias)
         return x.transpose(1, 2)                         # b m d
+
+    def first(self, x, upscale_size: int):
+        """BN(GELU(conv(interpolate(x^T, m)))) -> (b, H, m).  For an integer ratio m / n >= 2
+        the conv runs on the n tokens (hip.upscale: f x fewer FLOPs, the upsampled input is
+        never formed); otherwise upsample then conv."""
+        c = self.conv
+        w, b, bn = c[0].weight, c[0].bias, c[2]
+        if UPS_ON_TOKENS and ups_supported(x, upscale_size, w):
+            if bn_eval_fusable(x, bn, w, b):  # sampling: GEMM + one combine launch
+                return upsample_conv_gelu_bn_eval(x, upscale_size, w, b, bn)
+            return bn_snake(upsample_conv_gelu(x, upscale_size, w, b), bn, None)
+        x = upsample_nearest_t(x, upscale_size)          # b n d -> b d m, one kernel
+        if bn_eval_fusable(x, bn, w, b):  # eval: one launch
+            return conv2d_bn_eval(x, w, b, bn, None, pre_gelu=True)
+        return bn_snake(gelu(conv2d(x, w, b)), bn, None)
 
 
 # ------------------------------------------------------------------ the prior
@@ -475,12 +489,7 @@ class BidirectionalTransformer(nn.Module):
         Wc = gemm(lin.weight, 2 * D, 1, W_out, d, 1, lin.weight.shape[0], d, 2 * D)
         # x1 = cat(C[cls], Upscale'(tl) + Th[s_h] + P[:n]) = project_in(embed)
         tl = self._tok(s_M_l, self.tok_emb_l.weight, "lf", self._site_l)
-        x = upsample_nearest_t(tl, n)
-        if bn_eval_fusable(x, up[2], up[0].weight, up[0].bias):
-            x = conv2d_bn_eval(x, up[0].weight, up[0].bias, up[2], None, pre_gelu=True)
-        else:
-            x = gelu(conv2d(x, up[0].weight, up[0].bias))
-            x = bn_snake(x, up[2], None)
+        x = self.projector.first(tl, n)
         r = codebook_gather_nchw(s_M_h, Th, 1, n).view(B, d, n)  # Th[s_h] channels-first
         with PackCache.paused():  # W2c is computed per call: never cached
             u = conv2d(x, W2c, b2c, residual=r)  # (B, d, n)
