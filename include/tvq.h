@@ -819,6 +819,26 @@ int tvq_minmax_transform(const double* X, int64_t N, int64_t L, int64_t F, const
 int tvq_minmax_inverse(const float* x, int64_t N, int64_t L, int64_t F, const double* scale,
                        const double* min_, float* out, tvq_stream_t stream);
 
+/* ---- Training EncBlock / DecBlock conv with the BatchNorm statistics in its epilogue
+ * (reference vq_vae.py:65-121: Conv2d(3x4, stride (1,2), replicate) / ConvTranspose2d ->
+ * BatchNorm2d -> Snake).  tvq_conv_bnstats_blocks: the per-block partials per channel that
+ * tvq_conv2d_fwd_bnstats writes for this shape (transposed: ConvTranspose2d), 0 when the shape
+ * does not take the stride-2 kernels.  tvq_conv2d_fwd_bnstats: y = conv(x) + bias as
+ * tvq_conv2d_fwd / tvq_convT2d_fwd, plus part[(n blocks + blk) 2 + k] = (sum, sum of squares)
+ * of y over block blk's outputs of channel n (fp64).  tvq_bn_train_apply_part: the BatchNorm
+ * (+ Snake) training forward of tvq_bn_train_fwd from those partials (one launch). */
+int64_t tvq_conv_bnstats_blocks(int64_t B, int64_t Ci, int64_t H, int64_t Wi, int64_t Co,
+                                int64_t KH, int64_t KW, int64_t SW, int64_t transposed);
+int tvq_conv2d_fwd_bnstats(const float* x, int64_t B, int64_t Ci, int64_t H, int64_t Wi,
+                           const float* w, const float* bias, int64_t Co, int64_t KH, int64_t KW,
+                           int64_t SW, int64_t replicate, int64_t transposed, float* y,
+                           double* part, tvq_stream_t stream);
+int tvq_bn_train_apply_part(const float* x, int64_t B, int64_t C, int64_t HW, const double* part,
+                            int64_t nblk, const float* w, const float* b, float* running_mean,
+                            float* running_var, int64_t* num_batches_tracked, float momentum,
+                            float eps, const float* snake_a, float* y, float* save_mean,
+                            float* save_invstd, float* scale_shift, tvq_stream_t stream);
+
 /* ---- Upscale's first conv on the nearest-upsampled LF tokens (tvq_upscale.hip;
  * reference bidirectional_transformer.py:12-30 Upscale.forward: interpolate(nearest, m) ->
  * Conv1d(d, H, 3, padding 1) [-> GELU [-> BatchNorm1d eval]]), computed on the n-token grid:

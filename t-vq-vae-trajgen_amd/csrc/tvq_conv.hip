@@ -109,6 +109,10 @@ struct Epi {
   const float* snake_a;
   float bn_eps;
   int gelu;  // GELU (erf form) on conv + bias before the BN (Upscale: Conv1d -> GELU -> BN)
+  // training BatchNorm statistics of the stored output (the stride-2 kernels' STATS form,
+  // tvq_conv2d_fwd_bnstats): per-block (sum, sum of squares) in fp64 at
+  // bn_part[(n * gridDim.x + blockIdx.x) * 2 + k]; null: off
+  double* bn_part;
 };
 
 // bn_eval_snake_kernel's BN arithmetic (tvq_norm.hip) for channel n: v -> v sc + sh, then
@@ -1302,8 +1306,40 @@ constexpr int S2_SEG = 64;                 // output positions per segment
 constexpr int S2_XRF = 2 * S2_SEG + 2;     // F: staged columns (stride 2, 4 taps)
 constexpr int S2_XRT = S2_SEG / 2 + 4;     // T: staged columns (source offsets -2..2)
 
+// STATS epilogue of the stride-2 kernels (4 waves): lane (r16, g4) holds its positions' sums
+// of channels 4 g4 + r in s1 / s2 (fp64); the 16 lanes of a g4 group are combined by a fixed
+// xor tree, the 4 waves in wave order, and each channel's block partial is written for
+// bn_apply_part_kernel (tvq_norm.hip), which finishes the statistics in the consumer.
+// Replaces the BatchNorm's separate statistics pass over the conv output (bn_stats_partial).
+__device__ __forceinline__ void s2_bn_stats_block(double (&s1)[4], double (&s2)[4], int nbase,
+                                                  int N, double* __restrict__ part) {
+  __shared__ double red[4][16][2];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      s1[r] += __shfl_xor(s1[r], o, 64);
+      s2[r] += __shfl_xor(s2[r], o, 64);
+    }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[wid][nbase + r][0] = s1[r];
+      red[wid][nbase + r][1] = s2[r];
+    }
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < 2 * N) {
+    const int n = t >> 1, k = t & 1;
+    part[((int64_t)n * gridDim.x + blockIdx.x) * 2 + k] =
+        ((red[0][n][k] + red[1][n][k]) + red[2][n][k]) + red[3][n][k];
+  }
+}
+
 // F: out[b,n,h,wo] = sum_{c,kh,kw} w(n,c,kh,kw) in[b,c,h+kh-1,2wo+kw-opw], H = 3
-template <bool REPL, int CS, bool POST = false>
+template <bool REPL, int CS, bool POST = false, bool STATS = false>
 __global__ __launch_bounds__(256) void conv_s2f_kernel(const float* __restrict__ in,
                                                        const float* __restrict__ wt,
                                                        float* __restrict__ out, ConvGeom g, Epi e) {
@@ -1378,6 +1414,21 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(const float* __restrict__
     epi_store<1, POST>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + (pv ? wo : 0),
                        hw, nbase, g.N, pv, false, &pt);
   }
+  if constexpr (STATS) {  // (no dropout / residual on this path: the stored value is acc + b)
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int tile = wid * 3 + t;
+      if (w0 + (tile & 3) * 16 + r16 >= g.Wo) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double v = (double)(acc[t][r] + bv[0][r]);
+        s1[r] += v;
+        s2[r] += v * v;
+      }
+    }
+    s2_bn_stats_block(s1, s2, nbase, g.N, e.bn_part);
+  }
 }
 
 // T: out[b,n,h,wo] = sum w(n,c,kh,kw) in[b,c,h-kh+oph,(wo-kw+opw)/2] over the integer
@@ -1385,7 +1436,7 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(const float* __restrict__
 // of a replicate-padded conv): the canvas (5 rows, Wo = Wx + 2 columns) is folded onto
 // out = dx (3 rows, Wx columns) in the epilogue -- rows 0+1, 2, 3+4; canvas columns 0 / Wx+1
 // onto dx columns 0 / Wx-1 through LDS -- instead of a canvas store and a fold launch.
-template <int CS, int HO, bool FOLD = false, bool POST = false>
+template <int CS, int HO, bool FOLD = false, bool POST = false, bool STATS = false>
 __global__ __launch_bounds__(256) void conv_s2t_kernel(const float* __restrict__ in,
                                                        const float* __restrict__ wt,
                                                        float* __restrict__ out, ConvGeom g, Epi e) {
@@ -1478,6 +1529,20 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(const float* __restrict__
     epi_store<1, POST>(out, e, seed, bv, a, ((int64_t)b * g.N * g.Hout + h) * g.Wo + (pv ? wo : 0),
                        hw, nbase, g.N, pv, false, &pt);
   }
+  if constexpr (STATS) {
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    if (pv) {
+#pragma unroll
+      for (int h = 0; h < HO; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double v = (double)(acc[h][r] + bv[0][r]);
+          s1[r] += v;
+          s2[r] += v * v;
+        }
+    }
+    s2_bn_stats_block(s1, s2, nbase, g.N, e.bn_part);
+  }
 }
 
 static int g_conv_s2 = 1;  // conv_s2f / conv_s2t enabled (tvq_conv_config bit 512 turns them off)
@@ -1498,10 +1563,14 @@ static void launch_s2(int kind, const float* in, const float* wt, float* out, co
                       const Epi& e, hipStream_t st) {
   const dim3 grid((unsigned)(g.B * ((g.Wo + S2_SEG - 1) / S2_SEG)));
   const int cs = (g.C + 3) / 4;
-  TVQ_PLAN("conv_s2%s cs%d hout%d", kind == 1 ? "f" : "t", 4 * cs, g.Hout);
+  TVQ_PLAN("conv_s2%s cs%d hout%d%s", kind == 1 ? "f" : "t", 4 * cs, g.Hout,
+           e.bn_part ? " bnstats" : "");
 #define S2F(CSV)                                                                                \
   do {                                                                                          \
-    if (e.bn_rv)                                                                                \
+    if (e.bn_part)                                                                              \
+      hipLaunchKernelGGL((conv_s2f_kernel<REPL, CSV, false, true>), grid, dim3(256), 0, st, in,  \
+                         wt, out, g, e);                                                        \
+    else if (e.bn_rv)                                                                           \
       hipLaunchKernelGGL((conv_s2f_kernel<REPL, CSV, true>), grid, dim3(256), 0, st, in, wt, out, \
                          g, e);                                                                 \
     else                                                                                        \
@@ -1509,7 +1578,10 @@ static void launch_s2(int kind, const float* in, const float* wt, float* out, co
   } while (0)
 #define S2T(CSV, HOV)                                                                            \
   do {                                                                                           \
-    if (e.bn_rv)                                                                                 \
+    if (e.bn_part)                                                                               \
+      hipLaunchKernelGGL((conv_s2t_kernel<CSV, HOV, false, false, true>), grid, dim3(256), 0, st, \
+                         in, wt, out, g, e);                                                     \
+    else if (e.bn_rv)                                                                            \
       hipLaunchKernelGGL((conv_s2t_kernel<CSV, HOV, false, true>), grid, dim3(256), 0, st, in, wt, \
                          out, g, e);                                                             \
     else                                                                                         \
@@ -3553,6 +3625,53 @@ extern "C" int tvq_convT2d_fwd(const float* x, int64_t B, int64_t Ci, int64_t H,
   TVQ_DISPATCH_KIND(kind, 0, M_)
 #undef M_
   return launch_status("tvq_convT2d_fwd");
+}
+
+// The training EncBlock / DecBlock conv with its BatchNorm's statistics in the epilogue
+// (reference vq_vae.py:65-121: Conv2d / ConvTranspose2d (3x4, stride (1,2)) -> BatchNorm2d):
+// tvq_conv_bnstats_blocks gives the number of per-block partials per channel (0: this shape
+// does not take the stride-2 kernels, use tvq_conv2d_fwd + tvq_bn_train_fwd); part holds
+// Co x blocks x 2 doubles for tvq_bn_train_apply_part.
+static bool bnstats_geom(int64_t B, int64_t Ci, int64_t H, int64_t Wi, int64_t Co, int64_t KH,
+                         int64_t KW, int64_t SW, int64_t transposed, ConvGeom* gout) {
+  if (B <= 0 || Ci <= 0 || Co <= 0 || Wi <= 0 || kind_of((int)KH, (int)KW, (int)SW) != 0)
+    return false;
+  const ConvGeom g = transposed ? geom_convT_fwd(B, Ci, H, Wi, Co, KH, KW, SW)
+                                : geom_conv_fwd(B, Ci, H, Wi, Co, KH, KW, SW);
+  if (!geom_ok(g) || s2_kind(transposed ? GATHER_T : GATHER_F, g) != (transposed ? 2 : 1))
+    return false;
+  *gout = g;
+  return true;
+}
+
+extern "C" int64_t tvq_conv_bnstats_blocks(int64_t B, int64_t Ci, int64_t H, int64_t Wi,
+                                           int64_t Co, int64_t KH, int64_t KW, int64_t SW,
+                                           int64_t transposed) {
+  ConvGeom g;
+  if (!bnstats_geom(B, Ci, H, Wi, Co, KH, KW, SW, transposed, &g)) return 0;
+  return (int64_t)g.B * ((g.Wo + S2_SEG - 1) / S2_SEG);
+}
+
+extern "C" int tvq_conv2d_fwd_bnstats(const float* x, int64_t B, int64_t Ci, int64_t H,
+                                      int64_t Wi, const float* w, const float* bias, int64_t Co,
+                                      int64_t KH, int64_t KW, int64_t SW, int64_t replicate,
+                                      int64_t transposed, float* y, double* part,
+                                      tvq_stream_t stream) {
+  ConvGeom g;
+  TVQ_CHECK_ARG(x && w && y && part &&
+                    bnstats_geom(B, Ci, H, Wi, Co, KH, KW, SW, transposed, &g) &&
+                    !(transposed && replicate),
+                "tvq_conv2d_fwd_bnstats: unsupported (see tvq_conv_bnstats_blocks)");
+  Epi e = make_epi(bias, nullptr, 0.f, nullptr, 0);
+  e.bn_part = part;
+  hipStream_t st = (hipStream_t)stream;
+  if (transposed)
+    launch_s2<false>(2, x, w, y, g, e, st);
+  else if (replicate)
+    launch_s2<true>(1, x, w, y, g, e, st);
+  else
+    launch_s2<false>(1, x, w, y, g, e, st);
+  return launch_status("tvq_conv2d_fwd_bnstats");
 }
 
 // Eval-mode conv -> BatchNorm(running statistics) -> Snake in one launch: the BN affine

@@ -107,6 +107,64 @@ __global__ __launch_bounds__(256) void affine_snake_kernel(const float* __restri
   }
 }
 
+// Training BatchNorm (+ Snake) from the per-block statistics the producing conv wrote in its
+// epilogue (tvq_conv2d_fwd_bnstats, the stride-2 EncBlock / DecBlock convs): block (c, ch)
+// sums channel c's nblk partial pairs in one fixed order -- the same in every block of the
+// channel, so all agree bit for bit -- finalizes them (bn_final_channel's arithmetic; block
+// (c, 0) writes save / running statistics, block (0, 0) num_batches_tracked) and applies
+// affine + Snake (affine_snake_kernel's arithmetic) to chunk ch of the channel.  One launch
+// instead of bn_stats_partial (a full read of x) + affine_snake.
+__global__ __launch_bounds__(256) void bn_apply_part_kernel(const float* __restrict__ x, int B,
+                                                            int C, int HW, Div16 dhw, int chunks,
+                                                            const double* __restrict__ part,
+                                                            int nblk, BNFinal f,
+                                                            const float* __restrict__ a,
+                                                            float* __restrict__ y) {
+  __shared__ double red[4];
+  const int c = blockIdx.x, ch = blockIdx.y;
+  const double* pc = part + (int64_t)c * nblk * 2;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i0 = threadIdx.x; i0 < nblk; i0 += 256 * 4) {
+    double v[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 256 * u;
+      v[u][0] = i < nblk ? pc[2 * i] : 0.0;
+      v[u][1] = i < nblk ? pc[2 * i + 1] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s1 += v[u][0];
+      s2 += v[u][1];
+    }
+  }
+  s1 = block_sum_d(s1, red);
+  s2 = block_sum_d(s2, red);
+  if (c == 0 && ch == 0 && threadIdx.x == 0 && f.nbt) f.nbt[0] += 1;
+  float sc, sh;
+  bn_final_from_sums(s1, s2, c, f, ch == 0 && threadIdx.x == 0, sc, sh);
+  const float av = a ? a[c] : 1.f;
+  const int tot = B * HW;
+  const int per = (tot + chunks - 1) / chunks;
+  const int lo = ch * per, hi = min(tot, lo + per);
+  for (int i0 = lo + threadIdx.x; i0 < hi; i0 += 256 * NU) {
+    float v[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = i0 + u * 256;
+      v[u] = x[chan_off(i < hi ? i : lo, C, c, HW, dhw)];
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = i0 + u * 256;
+      if (i >= hi) continue;
+      float t = fmaf(v[u], sc, sh);
+      if (a) t = snake_fwd(t, av);
+      y[chan_off(i, C, c, HW, dhw)] = t;
+    }
+  }
+}
+
 // backward partials: [c][chunk][3] = (sum ds, sum ds*xhat, sum da-term); with `cnt`
 // the last block of channel c finalizes it
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
@@ -460,6 +518,29 @@ extern "C" int tvq_bn_train_fwd(const float* x, int64_t B, int64_t C, int64_t HW
                      (int)(B * C * HW), (int)C, (int)HW, dhw, scale_shift, scale_shift + C, snake_a,
                      y);
   return launch_status("tvq_bn_train_fwd");
+}
+
+// Training BatchNorm (+Snake) forward from the producing conv's per-block statistics (part:
+// C x nblk x 2 doubles, tvq_conv2d_fwd_bnstats); same outputs as tvq_bn_train_fwd.
+extern "C" int tvq_bn_train_apply_part(const float* x, int64_t B, int64_t C, int64_t HW,
+                                       const double* part, int64_t nblk, const float* w,
+                                       const float* b, float* running_mean, float* running_var,
+                                       int64_t* num_batches_tracked, float momentum, float eps,
+                                       const float* snake_a, float* y, float* save_mean,
+                                       float* save_invstd, float* scale_shift,
+                                       tvq_stream_t stream) {
+  TVQ_CHECK_ARG(x && y && part && nblk > 0 && save_mean && save_invstd && scale_shift && B > 0 &&
+                    C > 0,
+                "tvq_bn_train_apply_part: bad arguments");
+  TVQ_CHECK_ARG(norm_dims_ok(B, C, HW), "tvq_bn_train_apply_part: tensor too large");
+  const int chunks = bn_chunks(B, HW);
+  const BNFinal f = {(int)C, chunks, B * HW, eps, momentum, w, b, running_mean, running_var,
+                     num_batches_tracked, save_mean, save_invstd, scale_shift, scale_shift + C};
+  TVQ_PLAN("bn_apply_part C%lld nblk%lld", (long long)C, (long long)nblk);
+  hipLaunchKernelGGL(bn_apply_part_kernel, dim3((unsigned)C, (unsigned)chunks), dim3(256), 0,
+                     (hipStream_t)stream, x, (int)B, (int)C, (int)HW, make_div16(HW), chunks, part,
+                     (int)nblk, f, snake_a, y);
+  return launch_status("tvq_bn_train_apply_part");
 }
 
 // Eval-mode BatchNorm (+Snake) from running statistics. scale_shift: 2*C floats scratch.

@@ -62,6 +62,9 @@ def built_hash(path=None):
 
 sig("tvq_source_hash", restype=ctypes.c_char_p)
 sig("tvq_build_extra", restype=ctypes.c_char_p)
+sig("tvq_conv_bnstats_blocks", I64, I64, I64, I64, I64, I64, I64, I64, I64, restype=I64)
+sig("tvq_conv2d_fwd_bnstats", P, I64, I64, I64, I64, P, P, I64, I64, I64, I64, I64, I64, P, P, P)
+sig("tvq_bn_train_apply_part", P, I64, I64, I64, P, I64, P, P, P, P, P, F32, F32, P, P, P, P, P, P)
 sig("tvq_ups_pack", P, I64, I64, P, P)
 sig("tvq_ups_wscatter", P, I64, I64, P, I64, P)
 sig("tvq_ups_combine", P, I64, I64, I64, I64, P, I64, P, P, P, P, F32, P, P, P)

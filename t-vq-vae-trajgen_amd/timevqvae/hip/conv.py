@@ -274,6 +274,79 @@ def conv_transpose2d(x, weight, bias=None, stride_w=2):
     return _ConvT2d.apply(x, weight, bias, int(stride_w))
 
 
+def bnstats_blocks(x, weight, stride_w, transposed):
+    """Per-channel partials tvq_conv2d_fwd_bnstats writes for this conv (0: the shape does not
+    take the stride-2 kernels; the conv and its BatchNorm then run apart)."""
+    if x.dim() != 4 or weight.dim() != 4:
+        return 0
+    B, Ci, H, Wi = x.shape
+    Co = weight.shape[1] if transposed else weight.shape[0]
+    KH, KW = weight.shape[2], weight.shape[3]
+    return int(value("tvq_conv_bnstats_blocks", B, Ci, H, Wi, Co, KH, KW, int(stride_w),
+                     int(bool(transposed))))
+
+
+def _bnstats_fwd(ctx, x, w, b, SW, replicate, transposed):
+    x = x.contiguous()
+    w = w.contiguous()
+    B, Ci, H, Wi = x.shape
+    Co = w.shape[1] if transposed else w.shape[0]
+    KH, KW = w.shape[2], w.shape[3]
+    Wo = value("tvq_conv_out_width", Wi, KW, SW, int(bool(transposed)))
+    nblk = value("tvq_conv_bnstats_blocks", B, Ci, H, Wi, Co, KH, KW, SW, int(bool(transposed)))
+    y = torch.empty((B, Co, H, Wo), device=x.device, dtype=torch.float32)
+    part = torch.empty((Co, nblk, 2), device=x.device, dtype=torch.float64)
+    call("tvq_conv2d_fwd_bnstats", ptr(x), B, Ci, H, Wi, ptr(w), ptr(b), Co, KH, KW, SW,
+         int(bool(replicate)), int(bool(transposed)), ptr(y), ptr(part), stream_ptr())
+    ctx.mark_non_differentiable(part)
+    return x, w, y, part
+
+
+class _Conv2dStats(_Conv2d):
+    """conv2d (stride-2 EncBlock conv) that also returns its output's per-block BatchNorm
+    statistics (tvq_conv2d_fwd_bnstats); backward = _Conv2d's."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, SW, replicate):
+        x4, w4, y, part = _bnstats_fwd(ctx, x, w, b, SW, replicate, False)
+        ctx.save_for_backward(x4, w4)
+        ctx.cfg = (SW, replicate, 0.0, 0, False, b is not None, False, 4)
+        ctx.seed = None
+        ctx.params = (w, b)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, gy, gpart):
+        return _Conv2d.backward(ctx, gy)[:5]
+
+
+class _ConvT2dStats(_ConvT2d):
+    """conv_transpose2d (stride-2 DecBlock conv) + per-block BatchNorm statistics."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, SW):
+        x4, w4, y, part = _bnstats_fwd(ctx, x, w, b, SW, False, True)
+        ctx.save_for_backward(x4, w4)
+        ctx.SW = SW
+        ctx.has_b = b is not None
+        ctx.params = (w, b)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, gy, gpart):
+        return _ConvT2d.backward(ctx, gy)
+
+
+def conv2d_bnstats(x, weight, bias, stride_w=2, replicate=False):
+    """(conv2d(x), per-block BatchNorm statistics of it) for bn_snake_part; the caller checks
+    bnstats_blocks(x, weight, stride_w, False) > 0 first."""
+    return _Conv2dStats.apply(x, weight, bias, int(stride_w), bool(replicate))
+
+
+def conv_transpose2d_bnstats(x, weight, bias, stride_w=2):
+    return _ConvT2dStats.apply(x, weight, bias, int(stride_w))
+
+
 FUSED_BN_EVAL = os.environ.get("TVQ_FUSED_BN_EVAL", "1") != "0"
 
 

@@ -29,29 +29,68 @@ class _BNSnakeTrain(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        x, w, a, save = ctx.saved_tensors
+        return _bn_snake_bwd(ctx, gy)
+
+
+class _BNSnakeTrainPart(torch.autograd.Function):
+    """The training BatchNorm (+ Snake) forward from the producing conv's per-block statistics
+    (hip.conv.conv2d_bnstats: tvq_bn_train_apply_part, one launch); backward = _BNSnakeTrain's."""
+
+    @staticmethod
+    def forward(ctx, x, part, w, b, a, running_mean, running_var, nbt, momentum, eps):
+        ctx.params = (w, b, a)
+        a = a.reshape(-1) if a is not None else None
+        x = x.contiguous()
         B, C, HW = _dims(x)
-        dev = x.device
-        g = gy.contiguous()
-        dx = torch.empty_like(x)
-        has_w, has_b, has_a = ctx.has
-        sinks = [grad_sink(p) if h else None for p, h in zip(ctx.params, ctx.has)]
-        direct = all((s is not None) == h for s, h in zip(sinks, ctx.has))
-        if direct:
-            dw, db, da = sinks
-        else:
-            dw = torch.empty(C, device=dev) if has_w else None
-            db = torch.empty(C, device=dev) if has_b else None
-            da = torch.empty(C, device=dev) if has_a else None
-        ws = torch.empty(value("tvq_bn_workspace", B, C, HW), device=dev, dtype=torch.uint8)
-        call("tvq_bn_bwd", ptr(g), ptr(x), B, C, HW, ptr(w), ptr(a), ptr(save[:C]),
-             ptr(save[C:2 * C]), ptr(save[2 * C:]), ptr(dx), ptr(dw), ptr(db), ptr(da), int(direct),
-             ptr(ws), stream_ptr())
-        if direct:
-            return dx, None, None, None, None, None, None, None, None
-        if da is not None:
-            da = da.view_as(ctx.params[2])
-        return dx, dw, db, da, None, None, None, None, None
+        y = torch.empty_like(x)
+        save = torch.empty(4 * C, device=x.device, dtype=torch.float32)
+        call("tvq_bn_train_apply_part", ptr(x), B, C, HW, ptr(part), part.shape[1], ptr(w), ptr(b),
+             ptr(running_mean), ptr(running_var), ptr(nbt), float(momentum), float(eps), ptr(a),
+             ptr(y), ptr(save[:C]), ptr(save[C:2 * C]), ptr(save[2 * C:]), stream_ptr())
+        ctx.save_for_backward(x, w, a, save)
+        ctx.has = (w is not None, b is not None, a is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        dx, dw, db, da = _bn_snake_bwd(ctx, gy)[:4]
+        return dx, None, dw, db, da, None, None, None, None, None
+
+
+def bn_snake_part(x, part, bn, a=None):
+    """snake_a(BatchNorm_train(x)) with the statistics the conv that produced x wrote
+    (hip.conv.conv2d_bnstats / conv_transpose2d_bnstats)."""
+    if bn.momentum is None:
+        raise NotImplementedError("cumulative-average BatchNorm (momentum=None) is not on the path")
+    return _BNSnakeTrainPart.apply(x, part, bn.weight, bn.bias, a, bn.running_mean,
+                                   bn.running_var, bn.num_batches_tracked, bn.momentum, bn.eps)
+
+
+def _bn_snake_bwd(ctx, gy):
+    """Backward of the training BatchNorm (+ Snake) (tvq_bn_bwd), shared by both forwards."""
+    x, w, a, save = ctx.saved_tensors
+    B, C, HW = _dims(x)
+    dev = x.device
+    g = gy.contiguous()
+    dx = torch.empty_like(x)
+    has_w, has_b, has_a = ctx.has
+    sinks = [grad_sink(p) if h else None for p, h in zip(ctx.params, ctx.has)]
+    direct = all((s is not None) == h for s, h in zip(sinks, ctx.has))
+    if direct:
+        dw, db, da = sinks
+    else:
+        dw = torch.empty(C, device=dev) if has_w else None
+        db = torch.empty(C, device=dev) if has_b else None
+        da = torch.empty(C, device=dev) if has_a else None
+    ws = torch.empty(value("tvq_bn_workspace", B, C, HW), device=dev, dtype=torch.uint8)
+    call("tvq_bn_bwd", ptr(g), ptr(x), B, C, HW, ptr(w), ptr(a), ptr(save[:C]),
+         ptr(save[C:2 * C]), ptr(save[2 * C:]), ptr(dx), ptr(dw), ptr(db), ptr(da), int(direct),
+         ptr(ws), stream_ptr())
+    if direct:
+        return dx, None, None, None, None, None, None, None, None
+    if da is not None:
+        da = da.view_as(ctx.params[2])
+    return dx, dw, db, da, None, None, None, None, None
 
 
 def bn_snake(x, bn, a=None):

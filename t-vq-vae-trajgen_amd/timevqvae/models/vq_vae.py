@@ -3,7 +3,8 @@ timevqvae/models/vq_vae.py (state_dict keys `encoder.{i}.block.0.weight`,
 `convs.{0..5}`, `proj`, `decoder.{i}`, `linear` ... are identical), executed by
 the HIP kernels:
 
-  VQVAEEncBlock  replicate-pad Conv2d(3x4, s(1,2)) -> [BN + Snake fused]
+  VQVAEEncBlock  replicate-pad Conv2d(3x4, s(1,2)) with the BN statistics in its epilogue
+                 -> [BN finish + apply + Snake in one launch]
   ResBlock       Snake -> Conv2d(3x3) -> [BN + Snake] -> Conv2d(3x3) with the
                  dropout and the residual (identity or 1x1 proj) fused into the
                  second conv's epilogue
@@ -12,18 +13,26 @@ the HIP kernels:
                  band-mask + iSTFT + linear-interp kernel, then Linear(T,T) with
                  the residual in the GEMM epilogue.
 """
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
 
 from ..hip import resblock, rng
-from ..hip.conv import (bn_eval_fusable, conv2d, conv2d_bn_eval, conv_transpose2d,
-                        conv_transpose2d_bn_eval)
+from ..hip.conv import (bn_eval_fusable, bnstats_blocks, conv2d, conv2d_bn_eval,
+                        conv2d_bnstats, conv_transpose2d, conv_transpose2d_bn_eval,
+                        conv_transpose2d_bnstats)
 from ..hip.linear import linear
-from ..hip.norm import bn_snake, snake, snake_skip
+from ..hip.norm import bn_snake, bn_snake_part, snake, snake_skip
 from ..hip.signal import istft_decode, stft_encode
 from ..utils import SnakeActivation
 from ..utils.train_utils import band_of
+
+
+# training Enc/DecBlocks: the BatchNorm statistics in the stride-2 conv's epilogue
+# (tvq_conv2d_fwd_bnstats + tvq_bn_train_apply_part); False: conv, then the BN's own passes
+BN_STATS_IN_CONV = os.environ.get("TVQ_BN_STATS", "1") != "0"
 
 
 def _a(snake_mod):
@@ -186,6 +195,10 @@ class VQVAEEncBlock(nn.Module):
         if bn_eval_fusable(x, b[1], b[0].weight, b[0].bias, b[2].a):
             return conv2d_bn_eval(x, b[0].weight, b[0].bias, b[1], _a(b[2]), stride_w=2,
                                   replicate=True)
+        if self.training and BN_STATS_IN_CONV and bnstats_blocks(x, b[0].weight, 2, False):
+            # the BN statistics in the conv's epilogue, finished by the apply launch
+            h, part = conv2d_bnstats(x, b[0].weight, b[0].bias, stride_w=2, replicate=True)
+            return bn_snake_part(h, part, b[1], _a(b[2]))
         h = conv2d(x, b[0].weight, b[0].bias, stride_w=2, replicate=True)
         return bn_snake(h, b[1], _a(b[2]))
 
@@ -205,6 +218,9 @@ class VQVAEDecBlock(nn.Module):
             raise NotImplementedError("DecBlock dropout>0 is not on the path")
         if bn_eval_fusable(x, b[1], b[0].weight, b[0].bias, b[2].a):
             return conv_transpose2d_bn_eval(x, b[0].weight, b[0].bias, b[1], _a(b[2]))
+        if self.training and BN_STATS_IN_CONV and bnstats_blocks(x, b[0].weight, 2, True):
+            h, part = conv_transpose2d_bnstats(x, b[0].weight, b[0].bias, stride_w=2)
+            return bn_snake_part(h, part, b[1], _a(b[2]))
         h = conv_transpose2d(x, b[0].weight, b[0].bias, stride_w=2)
         return bn_snake(h, b[1], _a(b[2]))
 
