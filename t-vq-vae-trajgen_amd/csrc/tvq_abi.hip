@@ -47,19 +47,12 @@ int g_capture_depth = 0;
 constexpr int kMaxDevices = 64;
 CounterPool g_pools[kMaxDevices];
 std::mutex g_pool_mu;
-// TVQ_FUSED_FINISH: comma list of the finish classes done in-launch (default
-// "norm,reduce"; "0" = none).  Split-K slabs (gemm, conv) finished by one block per
-// tile measured slower than the separate all-CU finishing launch, so they are off.
+// The finish classes done in-launch: norm and reduce.  Split-K slabs (gemm, conv)
+// finished by one block per tile measured slower than the separate all-CU finishing
+// launch, so they keep it (round 4/5 A/B; the switch was retired in round 6).
 bool fused_finish_enabled(FinishClass cls) {
   static const unsigned mask = [] {
-    const char* e = getenv("TVQ_FUSED_FINISH");
-    const char* v = e ? e : "norm,reduce";
-    unsigned m = 0;
-    if (strstr(v, "norm")) m |= 1u << FIN_NORM;
-    if (strstr(v, "reduce")) m |= 1u << FIN_REDUCE;
-    if (strstr(v, "gemm")) m |= 1u << FIN_GEMM;
-    if (strstr(v, "conv")) m |= 1u << FIN_CONV;
-    return m;
+    return (1u << FIN_NORM) | (1u << FIN_REDUCE);
   }();
   return (mask >> cls) & 1u;
 }

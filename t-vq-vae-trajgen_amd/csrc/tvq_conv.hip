@@ -1993,14 +1993,17 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_kernel(const float* __res
 constexpr int W8_IMG = TVQ_W8_IMG;
 constexpr int W8_STG = 4;  // images per pipeline stage (one per wave)
 
+// up to 4 problems of one shape in a launch, stacked on blockIdx.y (the fused ResBlocks'
+// conv1 / conv2 weight gradients, tvq_resblock_w8.hip / tvq_resblock.hip)
+struct W8Probs {
+  const float* G[4];
+  const float* X[4];
+  float* slab[4];
+};
+
 template <int W, int CB>
-__global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restrict__ G0,
-                                                           const float* __restrict__ X0,
-                                                           float* __restrict__ slab0, int B, int C,
-                                                           int N, int kcols, int PS,
-                                                           const float* __restrict__ G1 = nullptr,
-                                                           const float* __restrict__ X1 = nullptr,
-                                                           float* __restrict__ slab1 = nullptr) {
+__global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(W8Probs pr, int B, int C, int N,
+                                                           int kcols, int PS) {
   constexpr int P = 3 * W, WP = W + 2;
   constexpr int GST = P + 4;                         // dY row stride in LDS (16-B aligned)
   constexpr int KB = CB * 9 + 1, KT = (KB + 15) / 16;  // columns (+ bias), 16-col tiles
@@ -2016,12 +2019,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_w8_kernel(const float* __restr
   float* Hs = smem + 2 * gbuf;                       // [2][STG][CB + 1][PS] (plane CB: ones)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 15, kq = lane >> 4;
-  // a pair launch (conv_wgrad_w8_pair) stacks a second problem of the same shape on the
-  // upper half of blockIdx.y
-  const int nty = (N + 31) / 32, pb = (int)blockIdx.y >= nty;
-  const float* __restrict__ G = pb ? G1 : G0;
-  const float* __restrict__ X = pb ? X1 : X0;
-  float* __restrict__ slab = pb ? slab1 : slab0;
+  // a multi-problem launch (conv_wgrad_w8_pair, conv_wgrad_wn_multi) stacks the problems of
+  // the same shape on blockIdx.y
+  const int nty = (N + 31) / 32, pb = (int)blockIdx.y / nty;
+  const float* __restrict__ G = pr.G[pb];
+  const float* __restrict__ X = pr.X[pb];
+  float* __restrict__ slab = pr.slab[pb];
   const int s = blockIdx.x, n0 = ((int)blockIdx.y - pb * nty) * 32, c0 = blockIdx.z * CB;
   const bool bias = c0 + CB >= C && kcols > C * 9;   // this block also owns the bias column
   const int b0 = s * W8_IMG;
@@ -2137,14 +2140,8 @@ static size_t w8_lds(int PS) {
   return 4 * (a > red ? a : red);
 }
 
-// the shapes conv_wgrad_w8_kernel takes (TVQ_CONV_W8=0 turns it off, for A/B)
-static bool w8_on() {
-  static const bool v = [] {
-    const char* e = getenv("TVQ_CONV_W8");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
+// the shapes conv_wgrad_w8_kernel takes
+static bool w8_on() { return true; }
 static bool w8_fits(int64_t B, int64_t C, int64_t H, int64_t Wi, int64_t N, int64_t Wo, int64_t KH,
                     int64_t KW, int64_t SW, int64_t replicate) {
   return w8_on() && KH == 3 && KW == 3 && SW == 1 && !replicate && H == 3 && Wi == Wo &&
@@ -2322,14 +2319,10 @@ __global__ __launch_bounds__(WT_T) void conv_wgrad_t32_kernel(const float* __res
     sl[(int64_t)(n0 + tid) * g.kcols + g.Kred] = bsum;
 }
 
-// TVQ_CONV_WT32=0 turns the wide-map weight-gradient kernel off (comparisons)
+// the shapes the wide-map weight-gradient kernel takes
 static bool wt32_fits(int64_t B, int64_t C, int64_t H, int64_t Wi, int64_t N, int64_t Wo,
                       int64_t KH, int64_t KW, int64_t SW, int64_t replicate) {
-  static const int on = [] {
-    const char* s = getenv("TVQ_CONV_WT32");
-    return s ? atoi(s) : 1;
-  }();
-  return on && SW == 1 && !replicate && KW == 3 && (KH == 1 || KH == 3) && Wi == Wo &&
+  return SW == 1 && !replicate && KW == 3 && (KH == 1 || KH == 3) && Wi == Wo &&
          Wi % 32 == 0 && N >= 64 && C >= 64 && B * C * H * Wi < (1ll << 31) &&
          B * N * H * Wo < (1ll << 31);
 }
@@ -2358,14 +2351,8 @@ struct WHaloPlan {
   size_t lds;
 };
 
-// slab floats cap of the halo weight gradient (TVQ_WHALO_SLAB_MAX overrides, for A/B)
-static int64_t whalo_slab_max() {
-  static const int64_t v = [] {
-    const char* e = getenv("TVQ_WHALO_SLAB_MAX");
-    return e ? (int64_t)atoll(e) : (int64_t)(8 << 20);  // 8M: LF 64-ch leg 26 vs 30 us at 4M
-  }();
-  return v;
-}
+// slab floats cap of the halo weight gradient (8M: LF 64-ch leg 26 vs 30 us at 4M)
+static int64_t whalo_slab_max() { return (int64_t)(8 << 20); }
 
 // split count depends only on (N, C, KK, B) so the workspace query can reproduce it
 static int whalo_splits(int64_t N, int64_t C, int KK, int64_t B, int nblk, int cblk) {
@@ -2843,22 +2830,10 @@ __global__ __launch_bounds__(64 * NW) void conv_d32_kernel(const float* __restri
   }
 }
 
-// TVQ_CONV_D32: 0 off; otherwise the largest position count it takes (default 8192:
-// the narrow LF maps, 6,144 positions); TVQ_CONV_D32_NW: waves per block (4 or 8)
-static int d32_max_pos() {
-  static const int v = [] {
-    const char* s = getenv("TVQ_CONV_D32");
-    return s ? (atoi(s) == 1 ? 8192 : atoi(s)) : 8192;
-  }();
-  return v;
-}
-static int d32_nw() {
-  static const int v = [] {
-    const char* s = getenv("TVQ_CONV_D32_NW");
-    return s ? atoi(s) : 4;
-  }();
-  return v;
-}
+// the largest position count the direct narrow-map conv takes (the LF maps, 6,144
+// positions) and its waves per block
+static int d32_max_pos() { return 8192; }
+static int d32_nw() { return 4; }
 
 template <int MODE, int KH, int KW, int SW, bool REPL, int NW>
 static bool launch_d32_nw(const float* in, const float* wt, float* out, const ConvGeom& g,
@@ -2988,13 +2963,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_d32_kernel(const float* __rest
   }
 }
 
-static bool wd32_on() {
-  static const bool v = [] {
-    const char* e = getenv("TVQ_CONV_WD32");
-    return e && atoi(e) != 0;
-  }();
-  return v;
-}
+static bool wd32_on() { return false; }  // measured slower than the halo kernel (below)
 
 // the direct weight gradient's split count (<= max_s, the workspace's slab count)
 static int wd32_splits(const ConvGeom& g, int kcols, int max_s, int* pps) {
@@ -3010,14 +2979,8 @@ static int wd32_splits(const ConvGeom& g, int kcols, int max_s, int* pps) {
 
 // the 16 / 48-channel convs into 128 on the 32x32-MFMA tile with a 16 / 32-wide K stage
 // instead of the halo tile: HF 16 -> 128 3x3 forward and the 128 -> 16 conv's data gradient
-// 32.2 / 30.9 -> 22.1 / 20.3 us, step -30 us (tools/gpu_t32s_ab.sh); TVQ_T32_SMALLC=0 off
-static bool t32_smallc() {
-  static const int on = [] {
-    const char* v = getenv("TVQ_T32_SMALLC");
-    return v ? atoi(v) : 1;
-  }();
-  return on != 0;
-}
+// 32.2 / 30.9 -> 22.1 / 20.3 us, step -30 us (tools/gpu_t32s_ab.sh)
+static bool t32_smallc() { return true; }
 
 // staged GEMM; `slab` (nullable) enables split-K with splits*N*Mpos floats of partials
 template <int MODE, int KH, int KW, int SW, bool REPL>
@@ -3923,10 +3886,47 @@ static void w8_pair_launch(const float* x0, const float* dy0, float* ws0, float*
   }
   const int kcols = (int)(C * 9 + 1);
   TVQ_PLAN("conv_wgrad_w8 pair S=%d", S);
-  hipLaunchKernelGGL((conv_wgrad_w8_kernel<8, 8>), grid, dim3(256), (w8_lds<8, 8>(PS)), st, dy0, x0,
-                     ws0, (int)B, (int)C, (int)N, kcols, PS, dy1, x1, ws1);
+  const W8Probs pr = {{dy0, dy1, nullptr, nullptr}, {x0, x1, nullptr, nullptr}, {ws0, ws1, nullptr, nullptr}};
+  hipLaunchKernelGGL((conv_wgrad_w8_kernel<8, 8>), grid, dim3(256), (w8_lds<8, 8>(PS)), st, pr,
+                     (int)B, (int)C, (int)N, kcols, PS);
   wgrad_finish(ws0, S, N, kcols, dw0, db0, accumulate, st);
   wgrad_finish(ws1, S, N, kcols, dw1, db1, accumulate, st);
+}
+
+// n <= 4 weight (+ bias) gradients of 3x3 stride-1 zero-padded convs of one shape on
+// (B, C, 3, 16) maps in one launch (conv_wgrad_w8_kernel<16, 8>: the fused RB<32, 16>
+// ResBlocks' conv1 / conv2, tvq_resblock.hip): problem i reduces dy[i] against x[i] into its
+// S = B / 16 slab rows ws[i] (S * N * (9 C + 1) floats), summed in order by the deferred slab
+// sum into dw[i] / db[i].
+int64_t conv_wgrad_w16_slab_floats(int64_t B, int64_t C, int64_t N) {
+  return (B / W8_IMG) * N * (C * 9 + 1);
+}
+bool conv_wgrad_w16_fits(int64_t B, int64_t C, int64_t N) {
+  return B % W8_IMG == 0 && C % 8 == 0 && N % 32 == 0 && B > 0;
+}
+void conv_wgrad_w16_multi(int n, const float* const* x, const float* const* dy, float* const* ws,
+                          float* const* dw, float* const* db, int64_t B, int64_t C, int64_t N,
+                          int accumulate, hipStream_t st) {
+  const int S = (int)(B / W8_IMG);
+  const int PS = whalo_plane_stride(5 * (16 + 2), 9, 3, 16 + 2, 1, 8);
+  const dim3 grid((unsigned)S, (unsigned)(n * (N / 32)), (unsigned)(C / 8));
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_w8_kernel<16, 8>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    attr = true;
+  }
+  W8Probs pr = {};
+  for (int i = 0; i < n; ++i) {
+    pr.G[i] = dy[i];
+    pr.X[i] = x[i];
+    pr.slab[i] = ws[i];
+  }
+  const int kcols = (int)(C * 9 + 1);
+  TVQ_PLAN("conv_wgrad_w16 n=%d S=%d", n, S);
+  hipLaunchKernelGGL((conv_wgrad_w8_kernel<16, 8>), grid, dim3(256), (w8_lds<16, 8>(PS)), st, pr,
+                     (int)B, (int)C, (int)N, kcols, PS);
+  for (int i = 0; i < n; ++i) wgrad_finish(ws[i], S, N, kcols, dw[i], db[i], accumulate, st);
 }
 bool conv_wgrad_w8_pair(const float* x0, const float* dy0, float* ws0, float* dw0, float* db0,
                         const float* x1, const float* dy1, float* ws1, float* dw1, float* db1,
@@ -3985,8 +3985,10 @@ extern "C" int tvq_conv2d_wgrad(const float* x, int64_t B, int64_t Ci, int64_t H
     }
     const size_t lds = w8_lds<8, 8>(PS);
     TVQ_PLAN("conv_wgrad_w8 S=%d", S);
-    hipLaunchKernelGGL((conv_wgrad_w8_kernel<8, 8>), grid, dim3(256), lds, st, dy, x, workspace,
-                       (int)B, (int)Ci, (int)Co, kcols, PS);
+    const W8Probs pr = {{dy, nullptr, nullptr, nullptr}, {x, nullptr, nullptr, nullptr},
+                        {workspace, nullptr, nullptr, nullptr}};
+    hipLaunchKernelGGL((conv_wgrad_w8_kernel<8, 8>), grid, dim3(256), lds, st, pr, (int)B, (int)Ci,
+                       (int)Co, kcols, PS);
     wgrad_finish(workspace, S, Co, kcols, dw, db, (int)accumulate, st);
     return launch_status("tvq_conv2d_wgrad(w8)");
   }
@@ -4109,9 +4111,4 @@ extern "C" int tvq_channel_sum(const float* x, int64_t B, int64_t C, int64_t HW,
   return launch_status("tvq_channel_sum");
 }
 
-// TVQ_CONV_CONFIG=<bits> sets tvq_conv_config at load time (benchmark A/B switches)
-static const int g_conv_config_env = [] {
-  const char* v = getenv("TVQ_CONV_CONFIG");
-  if (v && *v) tvq_conv_config(atoi(v));
-  return 0;
-}();
+

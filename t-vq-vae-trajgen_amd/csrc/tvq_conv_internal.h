@@ -26,4 +26,11 @@ const float* conv_pack_view(const float* w, int N, int C, int KK, int64_t wsn, i
 bool conv_wgrad_w8_pair(const float* x0, const float* dy0, float* ws0, float* dw0, float* db0,
                         const float* x1, const float* dy1, float* ws1, float* dw1, float* db1,
                         int64_t B, int64_t C, int64_t N, int accumulate, hipStream_t st);
+// n <= 4 such gradients on (B, C, 3, 16) maps in one launch (the fused RB<32, 16> ResBlocks),
+// each into its own conv_wgrad_w16_slab_floats slab, summed by the deferral scope's flush.
+bool conv_wgrad_w16_fits(int64_t B, int64_t C, int64_t N);
+int64_t conv_wgrad_w16_slab_floats(int64_t B, int64_t C, int64_t N);
+void conv_wgrad_w16_multi(int n, const float* const* x, const float* const* dy, float* const* ws,
+                          float* const* dw, float* const* db, int64_t B, int64_t C, int64_t N,
+                          int accumulate, hipStream_t st);
 }  // namespace tvq

@@ -246,15 +246,7 @@ using namespace tvq;
 // M = 25600, N = 128, K = 128 projections nor the train step.)  Deep-K GEMMs that stay
 // small get split-K instead.  The tile does not change the k order: results are bitwise
 // the same for every tile.
-static int gemm_min_blocks() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("TVQ_GEMM_MIN_BLOCKS");
-    v = e ? atoi(e) : 256;
-    if (v < 1) v = 1;
-  }
-  return v;
-}
+static int gemm_min_blocks() { return 256; }
 static void choose_tile(int64_t M, int64_t N, int* TM, int* TN) {
   static const int cand[4][2] = {{128, 64}, {64, 64}, {64, 32}, {32, 32}};
   const int64_t want = gemm_min_blocks();

@@ -312,28 +312,9 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // Size thresholds below which the staged generic kernel takes the call (default 0: the
 // direct kernels measured equal or faster at every step shape, profiles/r02_gemm_ab.txt).
-static int dk_min_k() {
-  static const int v = [] {
-    const char* e = getenv("TVQ_GEMM_DK_MIN_K");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-static int kt_min_tiles() {
-  static const int v = [] {
-    const char* e = getenv("TVQ_GEMM_KT_MIN_TILES");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-static bool direct_off() {
-  static const bool off = [] {  // TVQ_GEMM_DIRECT=0: skinny / generic kernels only
-    const char* e = getenv("TVQ_GEMM_DIRECT");
-    return e && e[0] == '0';
-  }();
-  return off;
-}
+static int dk_min_k() { return 0; }
+static int kt_min_tiles() { return 0; }
+static bool direct_off() { return false; }
 
 template <int TNW, int KS, int G>
 static void launch_dk(const GemmArgs& g, int kw, hipStream_t st) {

@@ -246,10 +246,7 @@ static void launch_rb2_e(const GemmArgs& g, int xcd, hipStream_t st) {
 
 template <int KH, bool BKC>
 static void launch_rb2(const GemmArgs& g, hipStream_t st) {
-  static const int xcd = [] {  // TVQ_GEMM_XCD=0: row-major 2-D grid (comparisons)
-    const char* e = getenv("TVQ_GEMM_XCD");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
+  constexpr int xcd = 1;  // XCD-aware tile map
   if (g.R && g.accumulate) launch_rb2_e<KH, BKC, true, true>(g, xcd, st);
   else if (g.R) launch_rb2_e<KH, BKC, true, false>(g, xcd, st);
   else if (g.accumulate) launch_rb2_e<KH, BKC, false, true>(g, xcd, st);
@@ -292,11 +289,7 @@ static void launch_wn(const GemmArgs& g, int wn, hipStream_t st) {
 }
 
 bool gemm_skinny(const GemmArgs& g, hipStream_t st) {
-  static const bool off = [] {  // TVQ_GEMM_SKINNY=0: generic kernel only (comparisons)
-    const char* e = getenv("TVQ_GEMM_SKINNY");
-    return e && e[0] == '0';
-  }();
-  if (off || g.sak != 1 || g.K > 512 || (g.K & 3) || (g.sam & 3) || !aligned16(g.A)) return false;
+  if (g.sak != 1 || g.K > 512 || (g.K & 3) || (g.sam & 3) || !aligned16(g.A)) return false;
   const bool bkc = g.sbk == 1;
   if (bkc && ((g.sbn & 3) || !aligned16(g.B))) return false;
   if (!bkc && g.sbn != 1) return false;

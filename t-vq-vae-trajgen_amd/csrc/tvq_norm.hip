@@ -435,15 +435,13 @@ __global__ __launch_bounds__(256) void bn_eval_snake_kernel(
   }
 }
 
-// whole-channel form for C >= TVQ_BN_CHAN channels (default 32; 0: off) of <= BNC_T*48
-// elements; returns the per-thread element count PT (0: the chunked form)
+// whole-channel form for C >= 32 channels of <= BNC_T*48 elements (smaller C: 16-32
+// blocks leave the chip idle, measured slower); returns the per-thread element count PT
+// (0: the chunked form)
 static int bn_chan_pt(int64_t B, int64_t C, int64_t HW) {
-  static const int cmin = [] {
-    const char* s = getenv("TVQ_BN_CHAN");
-    return s ? atoi(s) : 32;
-  }();
+  constexpr int cmin = 32;
   const int64_t n = B * HW;
-  if (cmin <= 0 || C < cmin || n > (int64_t)BNC_T * 48) return 0;
+  if (C < cmin || n > (int64_t)BNC_T * 48) return 0;
   const int64_t pt = (n + BNC_T - 1) / BNC_T;
   return pt <= 8 ? 8 : pt <= 16 ? 16 : pt <= 24 ? 24 : pt <= 32 ? 32 : 48;
 }

@@ -105,6 +105,11 @@ struct RB {
   static constexpr int PARTCW = PARTC > PARTW ? PARTC : PARTW;
   static constexpr int K1OFF = 2 * PLANE + PANEL + PARTCW;
   static constexpr int CONSTP = 2 * PS;  // ones plane + zeros plane
+  // external weight gradients (C = 32 at W = 16): the backward kernels write the conv
+  // operands (g and s planes) and conv_wgrad_w16_multi reduces them over images in one
+  // launch per ResBlock (pair), instead of a C x (9C + 1) slab row per image (37 KB, 12x the
+  // image's activations); taken when RBArgs::wext is set (B % 16 == 0)
+  static constexpr bool WEXT = C_ == 32 && W_ == 16;
   static_assert(P % 16 == 0 && W % 4 == 0 && C % NCH == 0 && CPC % 4 == 0 &&
                     RB_NW % (NR * NCH) == 0 && RB_NW % WPS == 0 && PSTEPS % WPS == 0,
                 "unsupported ResBlock geometry");
@@ -116,6 +121,11 @@ struct RBArgs {  // every pointer / scalar a fused ResBlock kernel reads or writ
   const float *bn_w, *bn_b, *rmean, *rvar;  // eval
   const float* save;                         // mean | invstd | scale | shift (C each)
   float *h_out, *y, *du, *dx, *slab1, *slab2, *slabda, *slabda2;
+  // RB::WEXT shapes with wext set: the (B, C, 3, W) conv operand planes the backward writes
+  // (conv1: g = dh, s = Snake_a1(x); conv2: g = Dropout'(dy), s = Snake_a2(BN(h))) and the
+  // small slabs conv_wgrad_w16_multi reduces them into
+  float *gp1, *sp1, *gp2, *sp2, *wsl1, *wsl2;
+  int wext;
   double* part;
   float eps, drop_p, drop_scale, invN;
   const int64_t* seed_ptr;
@@ -714,17 +724,27 @@ __device__ __forceinline__ void rb_bwd2_body(const RBArgs& a, double* rb_smem,
       float d = vg[u][q];
       if (a.drop_p > 0.f)
         d = uniform01(seed, (uint64_t)el.gi(img0, u, q)) >= a.drop_p ? d * a.drop_scale : 0.f;
+      const float sv = snake_f(fmaf(vh[u][q], sc[u], sh[u]), a2[u], 1.0f / a2[u]);
       G[el.cell(u, q)] = d;
-      S[el.cell(u, q)] = snake_f(fmaf(vh[u][q], sc[u], sh[u]), a2[u], 1.0f / a2[u]);
+      S[el.cell(u, q)] = sv;
+      if constexpr (R::WEXT) {
+        if (a.wext) {
+          const int64_t gi = el.gi(img0, u, q);
+          a.gp2[gi] = d;
+          a.sp2[gi] = sv;
+        }
+      }
     }
   __syncthreads();
   RB_MARK(2);
-  float* slab_row = a.slab2 + (int64_t)b * R::C * R::KC;
-  rb_wgrad_items<R>(G, S, K1, Pw, slab_row);
-  if (R::WPS > 1) {  // the partials, then the region is the conv items'
-    __syncthreads();
-    rb_wgrad_sum<R>(Pw, slab_row);
-    __syncthreads();
+  if (!(R::WEXT && a.wext)) {
+    float* slab_row = a.slab2 + (int64_t)b * R::C * R::KC;
+    rb_wgrad_items<R>(G, S, K1, Pw, slab_row);
+    if (R::WPS > 1) {  // the partials, then the region is the conv items'
+      __syncthreads();
+      rb_wgrad_sum<R>(Pw, slab_row);
+      __syncthreads();
+    }
   }
   RB_MARK(3);
   rb_conv_items<R, true>(A, G, Pc);
@@ -813,17 +833,28 @@ __device__ __forceinline__ void rb_bwd1_body(const RBArgs& a, double* rb_smem, R
     for (int q = 0; q < R::PPL; ++q) {
       if (!el.ok(u, q)) continue;
       const float xhat = (vh[u][q] - mu[u]) * is[u];
-      G[el.cell(u, q)] = bw[u] * is[u] * (vd[u][q] - md[u] - xhat * mx[u]);
-      S[el.cell(u, q)] = snake_f(vx[u][q], a1[u], 1.0f / a1[u]);
+      const float gv = bw[u] * is[u] * (vd[u][q] - md[u] - xhat * mx[u]);
+      const float sv = snake_f(vx[u][q], a1[u], 1.0f / a1[u]);
+      G[el.cell(u, q)] = gv;
+      S[el.cell(u, q)] = sv;
+      if constexpr (R::WEXT) {
+        if (a.wext) {
+          const int64_t gi = el.gi(img0, u, q);
+          a.gp1[gi] = gv;
+          a.sp1[gi] = sv;
+        }
+      }
     }
   __syncthreads();
   RB_MARK(2);
-  float* slab_row = a.slab1 + (int64_t)b * R::C * R::KC;
-  rb_wgrad_items<R>(G, S, K1, Pw, slab_row);
-  if (R::WPS > 1) {  // the partials, then the region is the conv items'
-    __syncthreads();
-    rb_wgrad_sum<R>(Pw, slab_row);
-    __syncthreads();
+  if (!(R::WEXT && a.wext)) {
+    float* slab_row = a.slab1 + (int64_t)b * R::C * R::KC;
+    rb_wgrad_items<R>(G, S, K1, Pw, slab_row);
+    if (R::WPS > 1) {  // the partials, then the region is the conv items'
+      __syncthreads();
+      rb_wgrad_sum<R>(Pw, slab_row);
+      __syncthreads();
+    }
   }
   RB_MARK(3);
   rb_conv_items<R, true>(A, G, Pc);
@@ -1010,6 +1041,14 @@ static RBWs rb_ws(int64_t B, int64_t C, int64_t W) {
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// the external-weight-gradient form (RB::WEXT) for this shape and batch
+static bool rb_wext(int64_t B, int64_t C, int64_t W) {
+  if (!(C == 32 && W == 16) || !conv_wgrad_w16_fits(B, C, C)) return false;
+  // the g / s planes and the small slab fit in the per-image slab region they replace
+  const int64_t pl = B * C * 3 * W;
+  return 2 * pl + conv_wgrad_w16_slab_floats(B, C, C) <= B * C * (9 * C + 1);
+}
+
 // the LF band's 64-channel ResBlock on (B, 64, 3, 8) (tvq_resblock_w8.hip)
 bool w8_supported(int64_t B, int64_t C, int64_t H, int64_t W);
 int64_t w8_workspace(int64_t B);
@@ -1075,6 +1114,12 @@ static RBArgs rb_bwd_args(const float* dy, const float* x, const float* h, int64
   a.slab1 = (float*)(ws + w.slab1); a.slab2 = (float*)(ws + w.slab2);
   a.slabda = (float*)(ws + w.slabda);
   a.part = (double*)(ws + w.part);
+  if (rb_wext(B, C, W)) {  // the planes and small slabs in the big slabs' regions
+    const int64_t pl = B * C * 3 * W;
+    a.wext = 1;
+    a.gp2 = a.slab2; a.sp2 = a.slab2 + pl; a.wsl2 = a.slab2 + 2 * pl;
+    a.gp1 = a.slab1; a.sp1 = a.slab1 + pl; a.wsl1 = a.slab1 + 2 * pl;
+  }
   a.B = (int)B; a.accumulate = (int)accumulate;
   a.drop_p = drop_p;
   a.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
@@ -1089,10 +1134,40 @@ static RBArgs rb_bwd_args(const float* dy, const float* x, const float* h, int64
 static void rb_bwd_finish(const RBArgs& a, int64_t C, float* da1, float* dw1, float* db1,
                           float* da2, float* dw2, float* db2, hipStream_t st) {
   const int64_t kc = 9 * C + 1;
-  conv_wgrad_finish(a.slab2, a.B, C, kc, dw2, db2, a.accumulate, st);
-  conv_wgrad_finish(a.slab1, a.B, C, kc, dw1, db1, a.accumulate, st);
+  if (a.wext) {  // both convs' weight gradients from the planes, one launch
+    const float* x[2] = {a.sp2, a.sp1};
+    const float* dy[2] = {a.gp2, a.gp1};
+    float* ws[2] = {a.wsl2, a.wsl1};
+    float* dw[2] = {dw2, dw1};
+    float* db[2] = {db2, db1};
+    conv_wgrad_w16_multi(2, x, dy, ws, dw, db, a.B, C, C, a.accumulate, st);
+  } else {
+    conv_wgrad_finish(a.slab2, a.B, C, kc, dw2, db2, a.accumulate, st);
+    conv_wgrad_finish(a.slab1, a.B, C, kc, dw1, db1, a.accumulate, st);
+  }
   conv_wgrad_finish(a.slabda, a.B, C, 1, da1, nullptr, a.accumulate, st);
   conv_wgrad_finish(a.slabda2, a.B, C, 1, da2, nullptr, a.accumulate, st);
+}
+
+// a pair's four weight gradients in one launch when both blocks take the planes
+static void rb_bwd_finish_pair(const RBArgs& b2, const RBArgs& b1, int64_t C, float* const* g2,
+                               float* const* g1, hipStream_t st) {
+  // g = {da1, dw1, db1, dbn_w, dbn_b, da2, dw2, db2}
+  if (!(b2.wext && b1.wext)) {
+    rb_bwd_finish(b2, C, g2[0], g2[1], g2[2], g2[5], g2[6], g2[7], st);
+    rb_bwd_finish(b1, C, g1[0], g1[1], g1[2], g1[5], g1[6], g1[7], st);
+    return;
+  }
+  const float* x[4] = {b2.sp2, b2.sp1, b1.sp2, b1.sp1};
+  const float* dy[4] = {b2.gp2, b2.gp1, b1.gp2, b1.gp1};
+  float* ws[4] = {b2.wsl2, b2.wsl1, b1.wsl2, b1.wsl1};
+  float* dw[4] = {g2[6], g2[1], g1[6], g1[1]};
+  float* db[4] = {g2[7], g2[2], g1[7], g1[2]};
+  conv_wgrad_w16_multi(4, x, dy, ws, dw, db, b2.B, C, C, b2.accumulate, st);
+  conv_wgrad_finish(b2.slabda, b2.B, C, 1, g2[0], nullptr, b2.accumulate, st);
+  conv_wgrad_finish(b2.slabda2, b2.B, C, 1, g2[5], nullptr, b2.accumulate, st);
+  conv_wgrad_finish(b1.slabda, b1.B, C, 1, g1[0], nullptr, b1.accumulate, st);
+  conv_wgrad_finish(b1.slabda2, b1.B, C, 1, g1[5], nullptr, b1.accumulate, st);
 }
 
 }  // namespace tvq
@@ -1267,7 +1342,6 @@ extern "C" int tvq_resblock_pair_bwd(const float* dy, const float* x, int64_t B,
   rb_dispatch((int)C, (int)W, 3, &b2, st, nullptr);
   rb_dispatch_pair((int)C, (int)W, 1, b2, b1, st);
   rb_dispatch((int)C, (int)W, 4, &b1, st, nullptr);
-  rb_bwd_finish(b2, C, g2[0], g2[1], g2[2], g2[5], g2[6], g2[7], st);
-  rb_bwd_finish(b1, C, g1[0], g1[1], g1[2], g1[5], g1[6], g1[7], st);
+  rb_bwd_finish_pair(b2, b1, C, g2, g1, st);
   return launch_status("tvq_resblock_pair_bwd");
 }

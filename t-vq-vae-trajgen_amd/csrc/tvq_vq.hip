@@ -315,14 +315,7 @@ extern "C" int tvq_vq_sqnorm(const float* E, int64_t K, int64_t D, float* ee, tv
 // workgroup -- the HF band's 24576 rows as 256 workgroups, one per CU: 55 us, where 64-row
 // workgroups (384: two on half the CUs) took 60 us and 48 / 32-row ones 66 / 85 us (each
 // workgroup streams the whole codebook through LDS); else 4 (64 rows)
-static int vq_rg(int64_t M) {
-  static const int forced = [] {
-    const char* e = getenv("TVQ_VQ_RG");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced == 1 || forced == 2 || forced == 3 || forced == 4 || forced == 6) return forced;
-  return M >= 256 * 96 ? 6 : 4;
-}
+static int vq_rg(int64_t M) { return M >= 256 * 96 ? 6 : 4; }
 
 extern "C" int64_t tvq_vq_assign_nblocks(int64_t M) {
   const int rg = vq_rg(M);

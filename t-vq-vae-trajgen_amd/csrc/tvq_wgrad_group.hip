@@ -391,11 +391,6 @@ __global__ __launch_bounds__(256) void wgrad_group_reduce_kernel(WgGroup G) {
 }
 
 // ---------------------------------------------------------------------------------------
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
 // Tile classes: 4 = the wide 128 x 64 form, 2 = 64 x 64, 1 = 32 x 32.  MFMA steps per
 // chunk: 8 at 64 x 64 and 128 x 64 (2 waves per SIMD without spills), 16 at 32 x 32.
 __host__ __device__ constexpr int wg_kc(int tw) { return tw == 1 ? 16 : 8; }
@@ -415,14 +410,13 @@ static int wg_units(int64_t M, int64_t N, int tw) {
 }
 
 static int wg_class(int64_t M, int64_t N, bool wide_ok) {
-  static const bool wide_on = env_int("TVQ_WG_WIDE", 1) != 0;
+  constexpr bool wide_on = true;
   if (M <= 32 || N <= 32) return 1;
   return (wide_on && wide_ok && M % 4 == 0 && N % 2 == 0) ? 4 : 2;
 }
 
 static int wg_splits(int units, int tw) {
-  static const int t2 = env_int("TVQ_WG_UNITS", 1000);
-  static const int t1 = env_int("TVQ_WG_UNITS1", 1024);
+  constexpr int t2 = 1000, t1 = 1024;  // ~work units per launch (tile classes 2/4, 1)
   int64_t s = ((tw == 1 ? t1 : t2) + units / 2) / (units > 0 ? units : 1);
   return (int)(s < 1 ? 1 : (s > 64 ? 64 : s));
 }

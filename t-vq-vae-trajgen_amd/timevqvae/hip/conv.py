@@ -35,6 +35,9 @@ USE_WORKSPACE = True  # tests flip this to cover the no-workspace (in-place weig
 _defer_keep = None  # workspaces of deferred weight-gradient reductions (wgrad_deferred)
 
 
+DEFER_WGRAD = True  # False (tests): every weight-gradient split sum at once
+
+
 @contextlib.contextmanager
 def wgrad_deferred(this_stream_only=False):
     """Inside the scope the conv weight-gradient split sums are recorded and run by a few
@@ -45,7 +48,7 @@ def wgrad_deferred(this_stream_only=False):
     accumulated into a flat gradient (a backward that runs on several streams); the others
     run at once."""
     global _defer_keep
-    if _defer_keep is not None or os.environ.get("TVQ_WGRAD_DEFER", "1") == "0":
+    if _defer_keep is not None or not DEFER_WGRAD:
         yield  # nested (the outer scope flushes) or switched off
         return
     if this_stream_only:
@@ -299,6 +302,7 @@ def _bnstats_fwd(ctx, x, w, b, SW, replicate, transposed):
     call("tvq_conv2d_fwd_bnstats", ptr(x), B, Ci, H, Wi, ptr(w), ptr(b), Co, KH, KW, SW,
          int(bool(replicate)), int(bool(transposed)), ptr(y), ptr(part), stream_ptr())
     ctx.mark_non_differentiable(part)
+    ctx.set_materialize_grads(False)  # no zero-filled gradient for `part` (an aten fill)
     return x, w, y, part
 
 
@@ -347,7 +351,7 @@ def conv_transpose2d_bnstats(x, weight, bias, stride_w=2):
     return _ConvT2dStats.apply(x, weight, bias, int(stride_w))
 
 
-FUSED_BN_EVAL = os.environ.get("TVQ_FUSED_BN_EVAL", "1") != "0"
+FUSED_BN_EVAL = True  # False (tests): the eval conv and BN as separate launches
 
 
 def bn_eval_fusable(x, bn, *params):

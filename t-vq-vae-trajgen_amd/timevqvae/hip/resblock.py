@@ -5,7 +5,7 @@ C = 64 on the LF band's (B, 64, 3, 8) maps:
   y = x + Dropout_p(conv2(Snake_a2(BN(conv1(Snake_a1(x)) + b1))) + b2)
 as 2 launches forward (training), 1 (eval), 2 backward, instead of one kernel per op.
 `supported()` says when it applies; models/vq_vae.ResBlock falls back to the per-op path
-otherwise (or when TVQ_RESBLOCK_FUSED=0).
+otherwise (or when ENABLED is False: the tests' per-op comparison).
 """
 import ctypes
 import os
@@ -16,7 +16,7 @@ from . import rng
 from ._native import call, grad_sink, ptr, stream_ptr, value
 from .conv import _immediate, _keep
 
-ENABLED = os.environ.get("TVQ_RESBLOCK_FUSED", "1") != "0"
+ENABLED = True
 
 
 def supported(x, C_in, C_out):
@@ -106,7 +106,7 @@ def resblock_eval(x, a1, conv1, bn, a2, conv2):
 
 
 # ------------------------------------------------------- two consecutive ResBlocks
-PAIR_ENABLED = os.environ.get("TVQ_RESBLOCK_PAIR", "1") != "0"
+PAIR_ENABLED = True
 
 
 def pair_supported(x):

@@ -25,20 +25,20 @@ Measured on MI355X (bench.py, config B, hipGraph): one stream 14.4 ms/step; LF||
 branches 10.8; stage1 || stage2 (bench.JointTrainer) with stage1's LF||HF: 8.1.
 Fine-grained forks (every weight gradient or codebook statistic on an aux stream,
 `offload`) cost more in graph edges than they hide (+1 to +3 ms), so they are off
-unless TVQ_STREAMS_OFFLOAD names them.
+unless OFFLOAD names them.
 """
 import contextlib
 import os
 
 import torch
 
-ENABLED = os.environ.get("TVQ_STREAMS", "1") != "0"
+ENABLED = True  # False (tests): one stream
 # offload classes: "grad" (weight/bias gradients into the flat sinks), "vq" (codebook
 # statistics + EMA).  Each offload is a fork + join edge in the captured graph, which
 # costs more than a small kernel it takes off the critical path, so the default is none.
-OFFLOAD = set(filter(None, os.environ.get("TVQ_STREAMS_OFFLOAD", "").split(",")))
+OFFLOAD = set()
 # branch keys to run inline instead (experiments: "hf", "stage2")
-INLINE = set(filter(None, os.environ.get("TVQ_STREAMS_INLINE", "").split(",")))
+INLINE = set()
 
 _side = {}      # (device index, parent stream id, key) -> side stream
 _used = {}      # parent stream id -> side streams forked from it since the last full join

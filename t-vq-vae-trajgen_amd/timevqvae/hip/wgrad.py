@@ -22,8 +22,8 @@ import torch
 
 from ._native import call, ptr, value
 
-ENABLED = os.environ.get("TVQ_WGRAD_GROUP", "1") != "0"
-_DEBUG = os.environ.get("TVQ_WGRAD_DEBUG", "0") != "0"  # print each launch's shapes
+ENABLED = True   # False: every weight gradient at once (tests)
+_DEBUG = False   # print each launch's shapes
 
 _pending = None  # (stream, tag) -> list of records while a scope is active
 _tag = [None]

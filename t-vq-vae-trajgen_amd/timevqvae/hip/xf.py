@@ -183,7 +183,7 @@ def linear_act(x, weight, bias=None, gelu=False):
 
 
 # ---------------------------------------------------------------- fused feed-forward
-FUSED_FF = os.environ.get("TVQ_FUSED_FF", "1") != "0"
+FUSED_FF = True
 
 
 class _FusedFF(torch.autograd.Function):
@@ -251,7 +251,7 @@ def fused_ff(xn, r, w1, b1, w2, b2, gate, p, site):
 
 
 # ---------------------------------------------------------------- fused attention branch
-FUSED_ATTN = os.environ.get("TVQ_FUSED_ATTN", "1") != "0"
+FUSED_ATTN = True
 
 
 class _AttnBranch(torch.autograd.Function):
@@ -676,7 +676,7 @@ def gelu(x):
 
 
 # --------------------------------------------------------------------------- fused LF prior
-PRIOR_FUSED = os.environ.get("TVQ_PRIOR_FUSED", "1") != "0"
+PRIOR_FUSED = True
 
 
 def prior_lf_eval_supported(tf, s):

@@ -40,9 +40,9 @@ from ..hip.upscale import upsample_conv_gelu, upsample_conv_gelu_bn_eval
 
 # the HF prior's sampling step straight from its head (no logits in memory); 0: form the
 # logits and sample them (A/B and diagnosis)
-FUSED_SAMPLE = os.environ.get("TVQ_FUSED_SAMPLE", "1") != "0"
+FUSED_SAMPLE = True
 # Upscale's first conv on the LF token grid (hip.upscale); False: upsample, then conv (tests)
-UPS_ON_TOKENS = os.environ.get("TVQ_UPS_TOKENS", "1") != "0"
+UPS_ON_TOKENS = True
 
 
 # ------------------------------------------------------------------ x-transformers tree

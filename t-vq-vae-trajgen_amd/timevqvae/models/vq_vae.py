@@ -13,8 +13,6 @@ the HIP kernels:
                  band-mask + iSTFT + linear-interp kernel, then Linear(T,T) with
                  the residual in the GEMM epilogue.
 """
-import os
-
 import numpy as np
 import torch
 import torch.nn as nn
@@ -31,8 +29,9 @@ from ..utils.train_utils import band_of
 
 
 # training Enc/DecBlocks: the BatchNorm statistics in the stride-2 conv's epilogue
-# (tvq_conv2d_fwd_bnstats + tvq_bn_train_apply_part); False: conv, then the BN's own passes
-BN_STATS_IN_CONV = os.environ.get("TVQ_BN_STATS", "1") != "0"
+# (tvq_conv2d_fwd_bnstats + tvq_bn_train_apply_part); False (tests): conv, then the BN's
+# own passes
+BN_STATS_IN_CONV = True
 
 
 def _a(snake_mod):

@@ -91,7 +91,7 @@ class GraphedSampler:
         self.packs = PackCache(self.device)
         # the LF decoder needs only the final LF tokens: it runs on a side stream while the
         # HF prior's pass and the HF decoder run (TVQ_SAMPLER_OVERLAP=0: one stream)
-        overlap = os.environ.get("TVQ_SAMPLER_OVERLAP", "1") != "0" and self.device.type == "cuda"
+        overlap = self.device.type == "cuda"
         self._side = torch.cuda.Stream(self.device) if overlap else None
 
         def batch():

@@ -186,6 +186,8 @@ def test_fused_resblock_full_batch_vs_oracle(Cc, W, cuda):
         assert tr.has(f"{pre}_{kern} C{Cc} W{W} B{B}"), (kern, tr.lines)
     if Cc == 64:
         assert tr.has("conv_wgrad_w8"), tr.lines
+    if Cc == 32:  # the image-batched weight gradients of both convs from the g / s planes
+        assert tr.has("conv_wgrad_w16 n=2 S=16"), tr.lines
     ok, err, s = max_ok(yd, yc)
     assert ok, ("y", err, s)
     ok, err, s = max_ok(xd.grad, xc.grad)

@@ -137,10 +137,11 @@ def test_deferred_wgrad_reductions_match_immediate(cuda, monkeypatch):
     bit for bit as reducing after every conv, eager and graphed."""
     import bench
     batch = _batch(cuda, B=32, C=6, L=256)
-    monkeypatch.setenv("TVQ_WGRAD_DEFER", "0")
+    from timevqvae.hip import conv as hconv
+    monkeypatch.setattr(hconv, "DEFER_WGRAD", False)
     ref = bench.JointTrainer(cuda, 1, cfg=_cfg(), length=256, channels=6)
     lr = [tuple(float(o["loss"].detach().sum()) for o in ref.step(batch)) for _ in range(7)]
-    monkeypatch.setenv("TVQ_WGRAD_DEFER", "1")
+    monkeypatch.setattr(hconv, "DEFER_WGRAD", True)
     d = bench.JointTrainer(cuda, 1, cfg=_cfg(), length=256, channels=6)
     ld = [tuple(float(o["loss"].detach().sum()) for o in d.step(batch)) for _ in range(3)]
     d.capture(batch)  # 2 eager warmup steps (deferral on), then capture

@@ -90,7 +90,8 @@ def test_fused_resblock_train_matches_per_op(B, C, W, drop):
 
 
 PAIR_SHAPES = [(8, 8, 64), (8, 16, 32), (4, 16, 16), (3, 32, 16), (2, 32, 32), (5, 8, 16),
-               (8, 64, 8), (3, 64, 8), (256, 64, 8)]
+               (8, 64, 8), (3, 64, 8), (256, 64, 8),
+               (32, 32, 16), (256, 32, 16)]  # B % 16 == 0: RB<32,16> external weight gradients
 
 
 def _run_pair(ms, x, paired):
