@@ -80,6 +80,7 @@ __global__ __launch_bounds__(UPS_T) void ups_combine_kernel(const float* __restr
                                                             float* __restrict__ out,
                                                             float* __restrict__ pre) {
   extern __shared__ float zs[];  // [3][n][UPS_CT + 1]
+  __shared__ float cbias[UPS_CT], csc[UPS_CT], csh[UPS_CT];
   constexpr int RS = UPS_CT + 1;
   const int b = blockIdx.x, c0 = blockIdx.y * UPS_CT;
   const int nc = min(UPS_CT, H - c0);
@@ -88,28 +89,53 @@ __global__ __launch_bounds__(UPS_T) void ups_combine_kernel(const float* __restr
     const int cc = e % UPS_CT, tj = e / UPS_CT, t = tj / n, j = tj - t * n;
     zs[tj * RS + cc] = cc < nc ? z[((int64_t)b * n + j) * ld + t * H + c0 + cc] : 0.f;
   }
+  if (threadIdx.x < nc) {  // per-channel terms once per block
+    const int c = c0 + threadIdx.x;
+    cbias[threadIdx.x] = bias ? bias[c] : 0.f;
+    if (mode == 2) {
+      const float inv = 1.0f / sqrtf(bn.rv[c] + bn.eps);
+      const float sc = (bn.w ? bn.w[c] : 1.f) * inv;
+      csc[threadIdx.x] = sc;
+      csh[threadIdx.x] = (bn.b ? bn.b[c] : 0.f) - bn.rm[c] * sc;
+    }
+  }
   __syncthreads();
   const float* A = zs;
   const float* Bm = zs + n * RS;
   const float* Cm = zs + 2 * n * RS;
-  for (int e = threadIdx.x; e < nc * m; e += UPS_T) {
-    const int cc = e / m, i = e - cc * m;
-    const int c = c0 + cc;
-    const int j = i / f, r = i - j * f;
+  // output i = f j + r: b + A_{j-1 or j} + B_j + C_{j or j+1}
+  auto value = [&](int cc, int j, int r) {
     const float a = r == 0 ? (j > 0 ? A[(j - 1) * RS + cc] : 0.f) : A[j * RS + cc];
     const float cv = r == f - 1 ? (j + 1 < n ? Cm[(j + 1) * RS + cc] : 0.f) : Cm[j * RS + cc];
-    float v = (bias ? bias[c] : 0.f) + (a + (Bm[j * RS + cc] + cv));
-    const int64_t o = ((int64_t)b * H + c) * m + i;
-    if (mode == 0) {
-      pre[o] = v;
-      v = ups_gelu(v);
-    } else if (mode == 2) {
-      const float inv = 1.0f / sqrtf(bn.rv[c] + bn.eps);
-      const float sc = (bn.w ? bn.w[c] : 1.f) * inv;
-      const float sh = (bn.b ? bn.b[c] : 0.f) - bn.rm[c] * sc;
-      v = fmaf(gelu_as(v), sc, sh);
+    return cbias[cc] + (a + (Bm[j * RS + cc] + cv));
+  };
+  auto post = [&](int cc, float v) {
+    return mode == 2 ? fmaf(gelu_as(v), csc[cc], csh[cc]) : (mode == 0 ? ups_gelu(v) : v);
+  };
+  if ((f & 3) == 0) {  // 4 consecutive outputs of one token per thread: 16-B stores
+    const int mq = m >> 2;
+    for (int e = threadIdx.x; e < nc * mq; e += UPS_T) {
+      const int cc = e / mq, i0 = 4 * (e - cc * mq);
+      const int j = i0 / f, r0 = i0 - j * f;
+      float v[4], y[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[k] = value(cc, j, r0 + k);
+        y[k] = post(cc, v[k]);
+      }
+      const int64_t o = ((int64_t)b * H + c0 + cc) * m + i0;
+      if (mode == 0) *reinterpret_cast<float4*>(pre + o) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(out + o) = make_float4(y[0], y[1], y[2], y[3]);
     }
-    out[o] = v;
+    return;
+  }
+  for (int e = threadIdx.x; e < nc * m; e += UPS_T) {
+    const int cc = e / m, i = e - cc * m;
+    const int j = i / f, r = i - j * f;
+    const float v = value(cc, j, r);
+    const int64_t o = ((int64_t)b * H + c0 + cc) * m + i;
+    if (mode == 0) pre[o] = v;
+    out[o] = post(cc, v);
   }
 }
 
@@ -123,12 +149,31 @@ __global__ __launch_bounds__(UPS_T) void ups_sums_kernel(const float* __restrict
   const int b = blockIdx.x, c0 = blockIdx.y * UPS_CT;
   const int nc = min(UPS_CT, H - c0);
   const int m = f * n, RS = m + 1, ld = 3 * H;
-  for (int e = threadIdx.x; e < nc * m; e += UPS_T) {
-    const int cc = e / m, i = e - cc * m;
-    const int64_t o = ((int64_t)b * H + c0 + cc) * m + i;
-    float g = dy[o];
-    if (pre) g = g * ups_gelu_grad(pre[o]);
-    gs[cc * RS + i] = g;
+  if ((m & 3) == 0) {  // 16-B loads
+    const int mq = m >> 2;
+    for (int e = threadIdx.x; e < nc * mq; e += UPS_T) {
+      const int cc = e / mq, i0 = 4 * (e - cc * mq);
+      const int64_t o = ((int64_t)b * H + c0 + cc) * m + i0;
+      const float4 g4 = *reinterpret_cast<const float4*>(dy + o);
+      float g[4] = {g4.x, g4.y, g4.z, g4.w};
+      if (pre) {
+        const float4 p4 = *reinterpret_cast<const float4*>(pre + o);
+        g[0] *= ups_gelu_grad(p4.x);
+        g[1] *= ups_gelu_grad(p4.y);
+        g[2] *= ups_gelu_grad(p4.z);
+        g[3] *= ups_gelu_grad(p4.w);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) gs[cc * RS + i0 + k] = g[k];
+    }
+  } else {
+    for (int e = threadIdx.x; e < nc * m; e += UPS_T) {
+      const int cc = e / m, i = e - cc * m;
+      const int64_t o = ((int64_t)b * H + c0 + cc) * m + i;
+      float g = dy[o];
+      if (pre) g = g * ups_gelu_grad(pre[o]);
+      gs[cc * RS + i] = g;
+    }
   }
   __syncthreads();
   for (int e = threadIdx.x; e < n * UPS_CT; e += UPS_T) {
@@ -190,8 +235,9 @@ extern "C" int tvq_ups_combine(const float* z, int64_t B, int64_t n, int64_t f, 
                                const float* bias, int64_t mode, const float* bn_w,
                                const float* bn_b, const float* bn_rm, const float* bn_rv,
                                float bn_eps, float* out, float* pre, tvq_stream_t stream) {
-  TVQ_CHECK_ARG(z && out && ups_dims_ok(B, n, f, H) && mode >= 0 && mode <= 2,
-                "tvq_ups_combine: bad arguments");
+  TVQ_CHECK_ARG(z && out && ups_dims_ok(B, n, f, H) && mode >= 0 && mode <= 2 &&
+                    ((uintptr_t)out & 15) == 0 && ((uintptr_t)pre & 15) == 0,
+                "tvq_ups_combine: bad arguments (out / pre 16-byte aligned)");
   TVQ_CHECK_ARG(mode != 0 || pre, "tvq_ups_combine: mode 0 needs pre");
   TVQ_CHECK_ARG(mode != 2 || (bn_rm && bn_rv), "tvq_ups_combine: mode 2 needs running statistics");
   const UpsBN bn = {bn_w, bn_b, bn_rm, bn_rv, bn_eps};
@@ -206,7 +252,9 @@ extern "C" int tvq_ups_combine(const float* z, int64_t B, int64_t n, int64_t f, 
 
 extern "C" int tvq_ups_sums(const float* dy, const float* pre, int64_t B, int64_t n, int64_t f,
                             int64_t H, float* s, float* part, tvq_stream_t stream) {
-  TVQ_CHECK_ARG(dy && s && ups_dims_ok(B, n, f, H), "tvq_ups_sums: bad arguments");
+  TVQ_CHECK_ARG(dy && s && ups_dims_ok(B, n, f, H) && ((uintptr_t)dy & 15) == 0 &&
+                    ((uintptr_t)pre & 15) == 0,
+                "tvq_ups_sums: bad arguments (dy / pre 16-byte aligned)");
   const size_t lds = (size_t)UPS_CT * (f * n + 1) * sizeof(float);
   TVQ_PLAN("ups_sums B%lld n%lld f%lld H%lld", (long long)B, (long long)n, (long long)f,
            (long long)H);
