@@ -111,6 +111,14 @@ def test_fused_prior_draw(depth, K, n, B, cond, cuda):
     assert torch.equal(a, b)
     fin = torch.isfinite(pb)
     assert float(((pa[fin] - pb[fin]).abs() / pb[fin]).max()) < 2e-6
+    # the product form (no logits copy: the sampler's launch) draws the same codes with the
+    # same p(sampled) bits
+    with torch.no_grad():
+        rng.manual_seed(8)
+        c, pc = xf.prior_lf_eval_sample(m, sg, yg, K, site=3)
+        torch.cuda.synchronize()
+    assert torch.equal(c, a)
+    assert torch.equal(pc, pa)
 
 
 def test_fused_prior_declines_unaligned_weights(cuda):
