@@ -568,7 +568,18 @@ def conv_wgrad_leg(device):
             "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, "wgrad")
 
 
-def resblock_bwd_leg(device, C=16, W=32):
+def resblock_bwd32_leg(device):
+    """The same op at C = 32 on (256, 32, 3, 16) (the LF band's level-3 ResBlocks, 4 ops per
+    step), where round 6 replaced the per-image C x (9C+1) slab rows (37 KB per image per
+    conv, 12x the image's activations) by the g / s operand planes and one image-batched
+    weight-gradient launch (conv_wgrad_w16: both convs' dW|db over 16-image blocks): rb_bwd2
+    + rb_bwd1 + conv_wgrad_w16 + the batched ordered sum of its 16-row slabs.  Algorithmic
+    work as resblock_bwd_leg's formula: 4 * 2 * 256*48*32*288 (+bias) = 0.906 GFLOP;
+    bytes 4 * B*C*P*4 + weights = 6.37 MB."""
+    return resblock_bwd_leg(device, C=32, W=16, leg="rb32bwd")
+
+
+def resblock_bwd_leg(device, C=16, W=32, leg="rbbwd"):
     """The round-3a top kernel by summed time (profiles/r03a_step_kernel_stats.csv): the fused
     ResBlock backward (csrc/tvq_resblock.hip rb_bwd2 + rb_bwd1, reference vq_vae.py:13-62) at
     its most frequent shape, C = 16 on (256, 16, 3, 32) (8 ops per step).  One op = rb_bwd2
@@ -618,15 +629,18 @@ def resblock_bwd_leg(device, C=16, W=32):
     flops = 2.0 * (2.0 * B * P * C * K) + 2.0 * (2.0 * B * P * C * (K + 1))
     byts = 4.0 * (4 * B * C * P + 2 * (C * K + C) + 2 * (C * K + C))
     tf = flops / (us * 1e-6) / 1e12
-    return _with_traffic({"bound": "mfma", "kernel": "fused ResBlock backward, C=16 on (256,16,3,32): "
-                                       "rb_bwd2_kernel + rb_bwd1_kernel<RB<16,32>> + one "
-                                       "batched ordered slab-sum launch (16x16x4 fp32 MFMA, "
-                                       "8 waves per image)",
+    kern = (f"fused ResBlock backward, C={C} on (256,{C},3,{W}): rb_bwd2_kernel + "
+            f"rb_bwd1_kernel<RB<{C},{W}>> + one batched ordered slab-sum launch (16x16x4 fp32 "
+            f"MFMA, 8 waves per image)") if leg == "rbbwd" else (
+            f"fused ResBlock backward, C={C} on (256,{C},3,{W}): rb_bwd2_kernel + rb_bwd1_kernel"
+            f"<RB<{C},{W}>> writing the g / s planes + conv_wgrad_w8_kernel<16,8> (both weight "
+            f"gradients, 16 images per block) + the batched ordered sum of its 16-row slabs")
+    return _with_traffic({"bound": "mfma", "kernel": kern,
             "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / FP32_PEAK_TFLOPS, 4),
             "algorithmic_bytes": byts, "flops_per_launch": flops, "avg_launch_us": round(us, 2),
-            "launches_per_op": 3,
-            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, "rbbwd")
+            "launches_per_op": 3 if leg == "rbbwd" else 4,
+            "hbm_frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}, leg)
 
 
 def vq_assign_leg(device):
@@ -833,6 +847,7 @@ def roofline_leg(device, ms_per_step):
     out["wgrad_group"] = dominant_leg(device)
     out["vq_assign"] = vq_assign_leg(device)
     out["resblock_bwd"] = resblock_bwd_leg(device)
+    out["resblock_bwd32"] = resblock_bwd32_leg(device)
     out["linear_fwd"] = linear_fwd_leg(device)
     out["conv_wgrad"] = conv_wgrad_leg(device)
     tf = STEP_GFLOP / ms_per_step  # GFLOP / ms = TFLOP/s

@@ -21,6 +21,9 @@ fi
 if [ "$LEG" = rbbwd ]; then
   python tools/roof_traffic.py $O $O/traffic.json "fused ResBlock backward C=16 on (256,16,3,32): rb_bwd2_kernel + rb_bwd1_kernel + one batched ordered slab-sum launch" rb_bwd2_kernel rb_bwd1_kernel reduce_rows
 fi
+if [ "$LEG" = rb32bwd ]; then
+  python tools/roof_traffic.py $O $O/traffic.json "fused ResBlock backward C=32 on (256,32,3,16): rb_bwd2_kernel + rb_bwd1_kernel (g / s planes) + conv_wgrad_w8_kernel<16,8> + the batched ordered slab sum" rb_bwd2_kernel rb_bwd1_kernel conv_wgrad_w8_kernel reduce_rows
+fi
 if [ "$LEG" = linfwd ]; then
   python tools/roof_traffic.py $O $O/traffic.json "LF prior Linear forward (6400x128)x(128x128) + bias + residual: gemm_rb2_kernel<64,true>" gemm_rb2_kernel
 fi
