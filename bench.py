@@ -428,7 +428,7 @@ HBM_PEAK_GBS = 8000.0
 
 # PMC evidence of the roofline legs: profiles/<PROFILE_TAG>_<leg>_traffic.json, written by
 # tools/gpu_roofline.sh + tools/roof_traffic.py on the tree named in its "tree" field
-PROFILE_TAG = "r05"
+PROFILE_TAG = "r06"
 
 
 def _traffic(leg):
