@@ -861,6 +861,15 @@ int tvq_ups_combine(const float* z, int64_t B, int64_t n, int64_t f, int64_t H,
  * part (B, H) (optional) = per-image sums of dY1 (the bias gradient's partials). */
 int tvq_ups_sums(const float* dy, const float* pre, int64_t B, int64_t n, int64_t f, int64_t H,
                  float* s, float* part, tvq_stream_t stream);
+/* The HF prior's project_in with Upscale's second conv folded in (training; reference
+ * bidirectional_transformer.py:194-231 + x-transformers ContinuousTransformerWrapper.project_in):
+ * z (B, m+1, d) = cat(Cp, v^T + R + P) with v (B, d, m) = conv(u, W_l W2) + W_l b2, R (B m, d) =
+ * th W_h^T, P (m, d) = pos[:m] W_in^T, Cp (B, d) = cls W_in^T; the backward splits dz into
+ * dv (B, d, m), dR (B m, d) and dCp (B, d).  d (m + 1) <= 16384. */
+int tvq_hfe_assemble(const float* v, const float* R, const float* P, const float* Cp, int64_t B,
+                     int64_t m, int64_t d, float* z, tvq_stream_t stream);
+int tvq_hfe_assemble_bwd(const float* dz, int64_t B, int64_t m, int64_t d, float* dv, float* dR,
+                         float* dCp, tvq_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -200,6 +200,63 @@ __global__ __launch_bounds__(UPS_T) void ups_sums_kernel(const float* __restrict
   }
 }
 
+// ---- the HF prior's project_in with Upscale's second conv folded in (training).
+// z = project_in(cat(cls, cat(Upscale(tl), th) + pos)) is assembled from the folded pieces
+// (hip/upscale.py hf_embed_folded): v = conv(u, W_l W2) + W_l b2 (B, d, m), R = th W_h^T
+// (B m, d), P = pos[:m] W_in^T (m, d), Cp = cls W_in^T (B, d):
+//   z[b, 0] = Cp[b],   z[b, 1 + i] = (v[b, :, i] + R[b m + i]) + P[i]
+// One block per image: v[b] staged through LDS (coalesced both ways).  The backward splits
+// dz back: dCp[b] = dz[b, 0], dR = dz[:, 1:] (contiguous), dv[b] = dz[b, 1:]^T.
+constexpr int HFE_T = 256;
+__global__ __launch_bounds__(HFE_T) void hfe_assemble_kernel(const float* __restrict__ v,
+                                                             const float* __restrict__ R,
+                                                             const float* __restrict__ P,
+                                                             const float* __restrict__ Cp, int m,
+                                                             int d, float* __restrict__ z) {
+  extern __shared__ float vs[];  // [d][m + 1]
+  const int b = blockIdx.x, RS = m + 1;
+  for (int e = threadIdx.x; e < d * m; e += HFE_T) {
+    const int f = e / m, i = e - f * m;
+    vs[f * RS + i] = v[((int64_t)b * d + f) * m + i];
+  }
+  __syncthreads();
+  float* zb = z + (int64_t)b * (m + 1) * d;
+  for (int e = threadIdx.x; e < (m + 1) * d; e += HFE_T) {
+    const int row = e / d, f = e - row * d;
+    if (row == 0) {
+      zb[e] = Cp[(int64_t)b * d + f];
+    } else {
+      const int i = row - 1;
+      zb[e] = (vs[f * RS + i] + R[((int64_t)b * m + i) * d + f]) + P[(int64_t)i * d + f];
+    }
+  }
+}
+
+__global__ __launch_bounds__(HFE_T) void hfe_assemble_bwd_kernel(const float* __restrict__ dz,
+                                                                 int m, int d,
+                                                                 float* __restrict__ dv,
+                                                                 float* __restrict__ dR,
+                                                                 float* __restrict__ dCp) {
+  extern __shared__ float gs[];  // [d][m + 1]
+  const int b = blockIdx.x, RS = m + 1;
+  const float* zb = dz + (int64_t)b * (m + 1) * d;
+  for (int e = threadIdx.x; e < (m + 1) * d; e += HFE_T) {
+    const int row = e / d, f = e - row * d;
+    const float g = zb[e];
+    if (row == 0) {
+      dCp[(int64_t)b * d + f] = g;
+    } else {
+      dR[((int64_t)b * m + row - 1) * d + f] = g;
+      gs[f * RS + row - 1] = g;
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < d * m; e += HFE_T) {
+    const int f = e / m, i = e - f * m;
+    dv[((int64_t)b * d + f) * m + i] = gs[f * RS + i];
+  }
+}
+
 static bool ups_dims_ok(int64_t B, int64_t n, int64_t f, int64_t H) {
   // LDS: the combine holds 3 n (UPS_CT + 1) floats, the sums UPS_CT (f n + 1): <= 64 KB
   return B > 0 && n > 0 && f >= 2 && H > 0 && f * n <= 240 && n <= 64 &&
@@ -262,4 +319,24 @@ extern "C" int tvq_ups_sums(const float* dy, const float* pre, int64_t B, int64_
                      dim3(UPS_T), lds, (hipStream_t)stream, dy, pre, (int)n, (int)f, (int)H, s,
                      part);
   return launch_status("tvq_ups_sums");
+}
+
+extern "C" int tvq_hfe_assemble(const float* v, const float* R, const float* P, const float* Cp,
+                                int64_t B, int64_t m, int64_t d, float* z, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(v && R && P && Cp && z && B > 0 && m > 0 && d > 0 && d * (m + 1) * 4 <= 64 * 1024,
+                "tvq_hfe_assemble: bad arguments");
+  hipLaunchKernelGGL(hfe_assemble_kernel, dim3((unsigned)B), dim3(HFE_T),
+                     (size_t)d * (m + 1) * sizeof(float), (hipStream_t)stream, v, R, P, Cp, (int)m,
+                     (int)d, z);
+  return launch_status("tvq_hfe_assemble");
+}
+
+extern "C" int tvq_hfe_assemble_bwd(const float* dz, int64_t B, int64_t m, int64_t d, float* dv,
+                                    float* dR, float* dCp, tvq_stream_t stream) {
+  TVQ_CHECK_ARG(dz && dv && dR && dCp && B > 0 && m > 0 && d > 0 && d * (m + 1) * 4 <= 64 * 1024,
+                "tvq_hfe_assemble_bwd: bad arguments");
+  hipLaunchKernelGGL(hfe_assemble_bwd_kernel, dim3((unsigned)B), dim3(HFE_T),
+                     (size_t)d * (m + 1) * sizeof(float), (hipStream_t)stream, dz, (int)m, (int)d,
+                     dv, dR, dCp);
+  return launch_status("tvq_hfe_assemble_bwd");
 }

@@ -36,13 +36,15 @@ from ..hip.xf import (attn_branch, attn_branch_supported, batch_colsum, drop_fir
 from ..hip._native import call, grad_sink, ptr, stream_ptr, value
 from ..hip.sample import codebook_gather_nchw, full_tokens, maskgit_sample, tied_logits_sample
 from ..hip.upscale import supported as ups_supported
-from ..hip.upscale import upsample_conv_gelu, upsample_conv_gelu_bn_eval
+from ..hip.upscale import (hf_embed_folded, hf_embed_supported, upsample_conv_gelu,
+                           upsample_conv_gelu_bn_eval)
 
 # the HF prior's sampling step straight from its head (no logits in memory); 0: form the
 # logits and sample them (A/B and diagnosis)
 FUSED_SAMPLE = True
 # Upscale's first conv on the LF token grid (hip.upscale); False: upsample, then conv (tests)
 UPS_ON_TOKENS = True
+HF_EMBED_FOLD = True  # False (tests): Upscale's last conv and project_in unfolded
 
 
 # ------------------------------------------------------------------ x-transformers tree
@@ -205,7 +207,11 @@ class ContinuousTransformerWrapper(nn.Module):
         self.project_out = nn.Linear(dim, dim_out, bias=False)
 
     def forward(self, x):
-        x = linear(x, self.project_in.weight)
+        return self.forward_projected(linear(x, self.project_in.weight))
+
+    def forward_projected(self, x):
+        """forward() after project_in (its input already projected, e.g. by the HF prior's
+        folded embedding)."""
         x = self.post_emb_norm(x)
         x = self.attn_layers(x)
         return linear(x, self.project_out.weight)
@@ -415,9 +421,21 @@ class BidirectionalTransformer(nn.Module):
         device = s_M_l.device
         tl = self._tok(s_M_l, self.tok_emb_l.weight, "lf", self._site_l)
         th = self._tok(s_M_h, self.tok_emb_h.weight, "hf", self._site_h)
-        tl = self.projector(tl, upscale_size=th.shape[1])
-        cls_emb = self.class_embedding(class_condition, s_M_l.shape[0], device)
         n = th.shape[1]
+        if HF_EMBED_FOLD:
+            x = self.projector.first(tl, n)  # (b, H, m)
+            W_in = self.blocks.project_in.weight
+            up = self.projector.conv
+            if hf_embed_supported(x, th, W_in, up[3].weight, self.pos_emb.weight):
+                # Upscale's last conv and project_in as one folded op (hip.upscale)
+                cls_emb = self.class_embedding(class_condition, s_M_l.shape[0], device)
+                z = hf_embed_folded(x, th, cls_emb, W_in, up[3].weight, up[3].bias,
+                                    self.pos_emb.weight)
+                return self._head(drop_first_token(self.blocks.forward_projected(z)))
+            tl = conv2d(x, up[3].weight, up[3].bias).transpose(1, 2)
+        else:
+            tl = self.projector(tl, upscale_size=n)
+        cls_emb = self.class_embedding(class_condition, s_M_l.shape[0], device)
         # cat(cls, cat(tl, th, -1) + pos) in one kernel
         embed = embed_assemble(cls_emb, tl, th, self.pos_emb.weight, n)
         embed = self.blocks(embed)
