@@ -144,3 +144,43 @@ def linear(x, weight, bias=None, residual=None, gate=None):
     if residual is x and gate is None and weight.shape[0] == weight.shape[1]:
         return _LinearSelfRes.apply(x, weight, bias)
     return _Linear.apply(x, weight, bias, residual, gate)
+
+
+class _WeightProduct(torch.autograd.Function):
+    """W = W1 W2 for two Linears that meet without a nonlinearity between them (x W2^T W1^T =
+    x (W1 W2)^T); backward dW1 = dW W2^T, dW2 = W1^T dW, accumulated into the flat-gradient
+    sinks when they exist (tiny GEMMs)."""
+
+    @staticmethod
+    def forward(ctx, w1, w2):
+        w1 = w1.contiguous()
+        w2 = w2.contiguous()
+        M, K = w1.shape
+        N = w2.shape[1]
+        ctx.save_for_backward(w1, w2)
+        ctx.params = (w1, w2)
+        return gemm(w1, K, 1, w2, N, 1, M, N, K)
+
+    @staticmethod
+    def backward(ctx, g):
+        w1, w2 = ctx.saved_tensors
+        M, K = w1.shape
+        N = w2.shape[1]
+        g = g.contiguous()
+        out = [None, None]
+        if ctx.needs_input_grad[0]:
+            sk = grad_sink(ctx.params[0])
+            d = sk if sk is not None else torch.empty_like(w1)
+            gemm(g, N, 1, w2, 1, N, M, K, N, out=d, ldc=K, accumulate=sk is not None)
+            out[0] = None if sk is not None else d
+        if ctx.needs_input_grad[1]:
+            sk = grad_sink(ctx.params[1])
+            d = sk if sk is not None else torch.empty_like(w2)
+            gemm(w1, 1, K, g, N, 1, K, N, M, out=d, ldc=N, accumulate=sk is not None)
+            out[1] = None if sk is not None else d
+        return out[0], out[1]
+
+
+def weight_product(w1, w2):
+    """w1 @ w2 with autograd into w1 / w2 (their flat-gradient sinks when present)."""
+    return _WeightProduct.apply(w1, w2)

@@ -26,7 +26,7 @@ import torch.nn as nn
 
 from ..hip import rng, streams
 from ..hip.conv import PackCache, bn_eval_fusable, conv2d, conv2d_bn_eval
-from ..hip.linear import gemm, linear
+from ..hip.linear import gemm, linear, weight_product
 from ..hip.norm import bn_snake
 from ..hip.xf import (attn_branch, attn_branch_supported, batch_colsum, drop_first_token,
                       embed_assemble, embedding, fused_ff, fused_ff_supported, gelu,
@@ -44,6 +44,7 @@ from ..hip.upscale import (hf_embed_folded, hf_embed_supported, upsample_conv_ge
 FUSED_SAMPLE = True
 # Upscale's first conv on the LF token grid (hip.upscale); False: upsample, then conv (tests)
 UPS_ON_TOKENS = True
+HEAD_FOLD = True  # False (tests): project_out and pred_head's Linear as two GEMMs
 HF_EMBED_FOLD = True  # False (tests): Upscale's last conv and project_in unfolded
 
 
@@ -209,10 +210,12 @@ class ContinuousTransformerWrapper(nn.Module):
     def forward(self, x):
         return self.forward_projected(linear(x, self.project_in.weight))
 
-    def forward_projected(self, x):
+    def forward_projected(self, x, project_out=True):
         """forward() after project_in (its input already projected, e.g. by the HF prior's
-        folded embedding)."""
+        folded embedding); project_out=False: without project_out (folded into the head)."""
         x = self.post_emb_norm(x)
+        if not project_out:
+            return self.attn_layers(x)
         x = self.attn_layers(x)
         return linear(x, self.project_out.weight)
 
@@ -395,6 +398,23 @@ class BidirectionalTransformer(nn.Module):
         h = linear_act(x, lin.weight, lin.bias, gelu=True)
         return layer_norm(h, ln.weight, ln.bias, ln.eps)
 
+    def _blocks_head(self, x, projected=False):
+        """pred_head(drop_first(blocks(x))) (bidirectional_transformer.py:186-191,233-236).
+        HEAD_FOLD: project_out and pred_head's Linear meet without a nonlinearity, so they run
+        as one Linear with W_p W_out (hip.linear.weight_product): the (B, n + 1, in_dim)
+        project_out output is never formed (the same function up to fp32 reassociation).
+        projected: x has already been through project_in."""
+        blk = self.blocks
+        if not HEAD_FOLD:
+            x = blk.forward_projected(x) if projected else blk(x)
+            return self._head(drop_first_token(x))
+        if not projected:
+            x = linear(x, blk.project_in.weight)
+        x = drop_first_token(blk.forward_projected(x, project_out=False))
+        lin, ln = self.pred_head[0], self.pred_head[2]
+        h = linear_act(x, weight_product(lin.weight, blk.project_out.weight), lin.bias, gelu=True)
+        return layer_norm(h, ln.weight, ln.bias, ln.eps)
+
     def forward_lf(self, s_M_l, class_condition: Union[None, torch.Tensor] = None):
         """bidirectional_transformer.py:166-192."""
         if prior_lf_eval_supported(self, s_M_l):
@@ -409,8 +429,7 @@ class BidirectionalTransformer(nn.Module):
         cls_emb = self.class_embedding(class_condition, s_M_l.shape[0], device)
         n = tok.shape[1]
         embed = embed_assemble(cls_emb, tok, None, self.pos_emb.weight, n)  # cat(cls, tok + pos)
-        embed = self.blocks(embed)
-        return self._head(drop_first_token(embed))
+        return self._blocks_head(embed)
 
     def forward_hf(self, s_M_l, s_M_h, class_condition=None):
         """bidirectional_transformer.py:194-236."""
@@ -431,15 +450,14 @@ class BidirectionalTransformer(nn.Module):
                 cls_emb = self.class_embedding(class_condition, s_M_l.shape[0], device)
                 z = hf_embed_folded(x, th, cls_emb, W_in, up[3].weight, up[3].bias,
                                     self.pos_emb.weight)
-                return self._head(drop_first_token(self.blocks.forward_projected(z)))
+                return self._blocks_head(z, projected=True)
             tl = conv2d(x, up[3].weight, up[3].bias).transpose(1, 2)
         else:
             tl = self.projector(tl, upscale_size=n)
         cls_emb = self.class_embedding(class_condition, s_M_l.shape[0], device)
         # cat(cls, cat(tl, th, -1) + pos) in one kernel
         embed = embed_assemble(cls_emb, tl, th, self.pos_emb.weight, n)
-        embed = self.blocks(embed)
-        return self._head(drop_first_token(embed))
+        return self._blocks_head(embed)
 
     def sample(self, s_M_l, s_M_h=None, class_condition=None, mask_id=None, gumbel=None,
                site=0, want_logits=False, first=True):
