@@ -422,6 +422,10 @@ SAMPLER_GFLOP_1024 = 375.0
 # (LF project_in folded into the embedding tables; the HF project_in folded into Upscale's last
 # conv and the token table, project_out composed with pred_head's Linear).
 SAMPLER_EXEC_GFLOP_1024 = 343.2
+# What the train step executes (tools/count_step_flops.py `step_executed_gflop_at_B256`): the
+# algorithmic count less the Linears the priors' training forwards compose away (Upscale's last
+# conv with the HF project_in's tl half, project_out with pred_head's Linear in both priors).
+STEP_EXEC_GFLOP = 152.22
 FP32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 
@@ -854,6 +858,8 @@ def roofline_leg(device, ms_per_step):
     out["step"] = {"bound": "mfma", "gflop": STEP_GFLOP, "achieved": round(tf, 2),
                    "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                    "frac": round(tf / FP32_PEAK_TFLOPS, 4),
+                   "executed_gflop": STEP_EXEC_GFLOP,
+                   "executed_frac": round(STEP_EXEC_GFLOP / ms_per_step / FP32_PEAK_TFLOPS, 4),
                    "source": "tools/count_step_flops.py -> profiles/r05_step_flops.json (step_gflop_at_B256)"}
     out["step_frac"] = out["step"]["frac"]
     out["cu_weighted"] = cu_weighted_leg()

@@ -20,6 +20,9 @@ _head_hf_eval and the LF prior's folded tables), from the config.yaml shapes:
   HF project_in (256 -> 32) on 97 tokens: its th half gathered from a projected table;
   HF project_out (32 -> 256) then pred_head's Linear (256 -> 128): one 32 -> 128 Linear.
 (the folded tables themselves, once per batch, are < 0.05 GFLOP and not subtracted)
+`step_executed_gflop_at_B256`: the train step less what the priors' training forwards fold
+(Upscale's last conv with the HF project_in's tl half; project_out with pred_head's Linear in
+both priors; the weight products themselves, < 0.02 GFLOP per step, not subtracted).
 
 usage: python tools/count_step_flops.py [B] > profiles/r05_step_flops.json"""
 import json
@@ -56,7 +59,16 @@ def main():
              + 2 * n_h * H_up * 3 * (D_h - d_h)  # Upscale last conv 256 -> 128 vs -> 32
              + 2 * (n_h + 1) * 2 * D_h * d_h  # HF project_in
              + 2 * n_h * (d_h * 2 * D_h + 2 * D_h * D_h - d_h * D_h))  # project_out + pred_head
+    # the train step (B = 256): what the priors' folded training forwards skip, each Linear /
+    # conv counted 3x (forward, input gradient, weight gradient)
+    L_l = 128
+    step_saved = 3 * (2 * n_h * H_up * 3 * (D_h - d_h)  # Upscale last conv -> 32 channels
+                      + 2 * (n_h + 1) * 2 * D_h * d_h - 2 * n_h * D_h * d_h  # HF project_in
+                      + 2 * (n_h + 1) * d_h * 2 * D_h + 2 * n_h * 2 * D_h * D_h
+                      - 2 * n_h * d_h * D_h  # HF project_out + pred_head -> one 32 -> 128
+                      + 2 * (n_l + 1) * L_l * L_l)  # LF project_out folded into pred_head
     out = {"batch_counted": B,
+           "step_executed_gflop_at_B256": ((f1 + f2) / B - step_saved) * 256 / 1e9,
            "sampler_gflop_per_1024": fs / B * 1024 / 1e9, "sampler_by_op": bys,
            "sampler_executed_gflop_per_1024": fs / B * 1024 / 1e9 - saved * 1024 / 1e9,
            "stage1_gflop_per_traj": f1 / B / 1e9, "stage2_gflop_per_traj": f2 / B / 1e9,
