@@ -419,9 +419,10 @@ STEP_GFLOP = 169.78
 SAMPLER_GFLOP_1024 = 375.0
 # What the sampler batch executes (tools/count_step_flops.py `sampler_executed_gflop_per_1024`):
 # the reference algorithm's count less the Linears the eval heads compose away while sampling
-# (LF project_in folded into the embedding tables; the HF project_in folded into Upscale's last
+# (LF project_in folded into the embedding tables and project_out composed with pred_head's
+# Linear; the HF project_in folded into Upscale's last
 # conv and the token table, project_out composed with pred_head's Linear).
-SAMPLER_EXEC_GFLOP_1024 = 343.2
+SAMPLER_EXEC_GFLOP_1024 = 334.8
 # What the train step executes (tools/count_step_flops.py `step_executed_gflop_at_B256`): the
 # algorithmic count less the Linears the priors' training forwards compose away (Upscale's last
 # conv with the HF project_in's tl half, project_out with pred_head's Linear in both priors).

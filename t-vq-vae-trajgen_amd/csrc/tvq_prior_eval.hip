@@ -7,7 +7,7 @@
 //   x = LayerNorm_gamma(x W_in^T)                              (project_in, post_emb_norm)
 //   depth x { x += Attn(RMSNorm(x)) W_o^T ; x += W2 GELU(W1 RMSNorm(x) + b1) + b2 }
 //   x = RMSNorm(x) W_out^T                                     (final_norm, project_out)
-//   h = LayerNorm_{w,b,1e-12}(GELU(x W_p^T + b_p))              (pred_head)
+//   h = LayerNorm_{w,b,1e-12}(GELU(x W_p^T + b_p))              (pred_head; W_p W_out composed)
 //   logits[:, i-1, k] = h_i . tok_emb[k] + bias[i-1, k],  i = 1..n, k < K   (tied logits)
 //
 // Layout ("token on the lane"): the sequence (n + 1 <= 32 tokens, cls first) sits on the 32
@@ -22,13 +22,14 @@
 //   softmax over the registers + one xor-32 shuffle,
 //   O^T = V^T P^T (A = V regs, B = P regs),
 // and the out-projection / FF consume O^T / GELU(u)^T from registers.  Norm statistics
-// are a register sum + one xor-32 shuffle.  Per step and sequence this is 8448 MFMAs
-// (config.yaml LF prior: depth 4, width 128, 2 heads x 64, ff 128, K = 512); the
+// are a register sum + one xor-32 shuffle.  Per step and sequence this is 7936 MFMAs
+// (config.yaml LF prior: depth 4, width 128, 2 heads x 64, ff 128, K = 512; 8448 less
+// project_in, folded into the embedding tables, and project_out, composed into pred_head); the
 // unfused path ran ~30 launches per step, each streaming activations through HBM.
 //
 // Weights: every Linear's 32-row tiles are consumed in one fixed order (project_in, per
-// layer q/k/v per head and the head's out-projection columns, ff1, ff2, then project_out,
-// pred_head, the tied-logit code tiles).  prior_pack_kernel writes them once per call
+// layer q/k/v per head and the head's out-projection columns, ff1, ff2, then the composed
+// project_out / pred_head weight, the tied-logit code tiles).  prior_pack_kernel writes them once per call
 // into a stream in the MFMA operand order (tile -> 16-B group T4 -> lane): every load is one
 // coalesced 1-KB row, and each wave loads the first groups of tile i+1 while it multiplies
 // tile i, so a tile never starts on an L2 round trip.  (A 4-wave block staging the stream
@@ -75,6 +76,9 @@ struct PriorArgs {
   // project_in folded into the embedding tables (one-wave kernel): rows tok [0, K+1),
   // pos [K+1, K+1+n), cls [K+1+n, ...) of (table row) W_in^T, written by prior_fold_kernel
   float* ftab;
+  // project_out (with final_norm's g) composed with pred_head's Linear: wc = W_p W_out diag(g)
+  // (128 x 128, written by prior_headfold_kernel), packed as the 4 head tiles
+  float* wc;
 };
 
 __device__ __forceinline__ floatx16 pe_mfma(float a, float b, floatx16 c) {
@@ -98,7 +102,7 @@ struct PeTile {
   const float* gk;  // per-column factor folded into the packed tile (an RMSNorm's g), or null
 };
 __device__ __forceinline__ int pe_ntiles(int depth, int K) {
-  return 4 + 28 * depth + 8 + (K + 31) / 32;
+  return 4 + 28 * depth + 4 + (K + 31) / 32;
 }
 __device__ __forceinline__ PeTile pe_tile(const PriorArgs& a, int idx) {
   if (idx < 4) return {a.w_in, 32 * idx, 0, 64, PE_D, nullptr};
@@ -118,9 +122,7 @@ __device__ __forceinline__ PeTile pe_tile(const PriorArgs& a, int idx) {
     return {L.w2, 32 * (j - 24), 0, 64, PE_D, nullptr};
   }
   idx -= 28 * a.depth;
-  if (idx < 4) return {a.w_out, 32 * idx, 0, 64, PE_D, a.g_final};
-  idx -= 4;
-  if (idx < 4) return {a.wp, 32 * idx, 0, 64, PE_D, nullptr};
+  if (idx < 4) return {a.wc, 32 * idx, 0, 64, PE_D, nullptr};  // W_p W_out diag(g_final)
   idx -= 4;
   return {a.tok_emb, 32 * idx, 0, 64, a.K, nullptr};  // code rows >= K are packed as zeros
 }
@@ -183,6 +185,19 @@ __global__ __launch_bounds__(128) void prior_fold_kernel(PriorArgs a) {
     acc = fmaf(x.w, y.w, acc);
   }
   a.ftab[(int64_t)r * PE_D + j] = acc;
+}
+
+// final_norm -> project_out -> pred_head's Linear without a nonlinearity between the two
+// Linears: wc[i][k] = (sum_j W_p[i][j] W_out[j][k]) g_final[k], one row per block, the j sum
+// in order (the same function up to fp32 reassociation; 256 MFMAs per sequence
+// and 4 weight tiles leave the launch)
+__global__ __launch_bounds__(128) void prior_headfold_kernel(PriorArgs a) {
+  const int i = blockIdx.x, k = threadIdx.x;
+  const float* wp = a.wp + (int64_t)i * PE_D;
+  float acc = 0.f;
+#pragma unroll 8
+  for (int j = 0; j < PE_D; ++j) acc = fmaf(wp[j], a.w_out[(int64_t)j * PE_D + k], acc);
+  a.wc[(int64_t)i * PE_D + k] = acc * a.g_final[k];
 }
 
 // a per-feature vector (D floats) in the register layout: v[tile][r] = p[32*tile + crow(r,h)]
@@ -258,17 +273,6 @@ __device__ __forceinline__ floatx16 pe_gemm(PeStream& st, BV bv, floatx16 acc) {
   st.off = noff;
   st.idx = nidx;
   return acc;
-}
-
-// y^T = W x^T over the full width (4 output tiles, K = 128): out[t] (no bias)
-__device__ __forceinline__ void pe_linear(PeStream& st, const floatx16 (&x)[4],
-                                          floatx16 (&out)[4]) {
-#pragma unroll
-  for (int ot = 0; ot < 4; ++ot) {
-    floatx16 acc;
-    pe_zero(acc);
-    out[ot] = pe_gemm<true, 64>(st, [&](int t) { return x[t >> 4][t & 15]; }, acc);
-  }
 }
 
 // x-transformers RMSNorm (rmsnorm_fwd_kernel): x * (1 / max(|x|, 1e-12)) * sqrt(D) * g;
@@ -501,16 +505,12 @@ __global__ __launch_bounds__(64) void prior_lf_eval_kernel(PriorArgs a,
 #pragma unroll
       for (int r = 0; r < 16; ++r) x[t][r] = live ? y[t][r] + x[t][r] : 0.f;
   }
-  // ---- final_norm + project_out (no bias)
+  // ---- final_norm, project_out and pred_head: LayerNorm_{w,b}(GELU(RMSNorm(x) (W_p W_out)^T
+  // + b_p)) (g_final folded into wc)
   {
-    floatx16 xn[4];
-    pe_rms(x, xn);  // g_final folded into project_out
-    pe_linear(st, xn, x);
-  }
-  // ---- pred_head: LayerNorm_{w,b}(GELU(x W_p^T + b_p))
-  {
-    floatx16 y[4];
-    pe_linear_bias(st, x, a.bp, h, y);
+    floatx16 xn[4], y[4];
+    pe_rms(x, xn);
+    pe_linear_bias(st, xn, a.bp, h, y);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -581,9 +581,10 @@ using namespace tvq;
 extern "C" int64_t tvq_prior_lf_eval_workspace(int64_t depth, int64_t K, int64_t n,
                                                int64_t n_classes) {
   if (depth < 1 || depth > PE_MAXDEPTH || K < 1 || n < 1 || n_classes < 0) return -1;
-  const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32;  // 64-step tiles
+  const int64_t tiles64 = 4 + 20 * depth + 4 + (K + 31) / 32;  // 64-step tiles
   const int64_t stream = (tiles64 * 1024 + depth * 8 * 512) * 16;
-  return stream + (K + 1 + n + n_classes + 1) * PE_D * 4;  // + the folded tables
+  // + the folded tables + the composed head weight
+  return stream + (K + 1 + n + n_classes + 1) * PE_D * 4 + PE_D * PE_D * 4;
 }
 
 static int prior_lf_eval_launch(PriorArgs& a, const int64_t* s, int64_t B, int64_t n,
@@ -611,7 +612,7 @@ static int prior_lf_eval_launch(PriorArgs& a, const int64_t* s, int64_t B, int64
                   "tvq_prior_lf_eval: weight pointers must be non-null and 16-byte aligned");
   TVQ_CHECK_ARG(workspace && ((uintptr_t)workspace & 15) == 0,
                 "tvq_prior_lf_eval: workspace must be non-null and 16-byte aligned");
-  const int ntiles = 4 + 28 * (int)depth + 8 + (int)((K + 31) / 32);
+  const int ntiles = 4 + 28 * (int)depth + 4 + (int)((K + 31) / 32);
   hipStream_t st = (hipStream_t)stream;
   float4* ws = reinterpret_cast<float4*>(workspace);
   // (A two-wave-per-sequence form -- heads / feed-forward halves split over two waves, the
@@ -619,11 +620,13 @@ static int prior_lf_eval_launch(PriorArgs& a, const int64_t* s, int64_t B, int64
   // vs 5.57 ms, 356 vs 327 us per launch; the LDS exchanges, barriers and the work both
   // waves repeat cost more than the second wave hides, the one-wave kernel's MFMA pipe
   // being ~64 % busy already (profiles/r04_prior_pmc.txt).  Removed in round 5.)
-  const int64_t tiles64 = 4 + 20 * depth + 8 + (K + 31) / 32;  // as the workspace
+  const int64_t tiles64 = 4 + 20 * depth + 4 + (K + 31) / 32;  // as the workspace
   a.ftab = reinterpret_cast<float*>(ws + tiles64 * 1024 + depth * 8 * 512);
-  if (!ready) {  // weights -> folded tables + packed stream
+  a.wc = a.ftab + (K + 1 + n + n_classes + 1) * PE_D;  // 16-B aligned (PE_D floats per row)
+  if (!ready) {  // weights -> folded tables, the composed head weight, packed stream
     hipLaunchKernelGGL(prior_fold_kernel, dim3((unsigned)(K + 1 + n + n_classes + 1)), dim3(128),
                        0, st, a);
+    hipLaunchKernelGGL(prior_headfold_kernel, dim3(PE_D), dim3(PE_D), 0, st, a);
     hipLaunchKernelGGL(prior_pack_kernel, dim3((unsigned)(ntiles - 4)), dim3(256), 0, st, a, ws, 4);
   }
   hipLaunchKernelGGL(prior_lf_eval_kernel, dim3((unsigned)B), dim3(64), 0, st, a,

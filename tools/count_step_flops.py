@@ -15,7 +15,8 @@ priors' forwards, then both decoders) is counted the same way, per 1024 trajecto
 `sampler_executed_gflop_per_1024` is what the HIP sampler executes: the same count less the
 Linears its eval heads compose away (hip path, models/bidirectional_transformer.py
 _head_hf_eval and the LF prior's folded tables), from the config.yaml shapes:
-  LF project_in (128 -> 128) on 25 tokens x 10 decoding steps, folded into the tables;
+  LF project_in (128 -> 128) on 25 tokens x 10 decoding steps, folded into the tables, and
+  LF project_out (128 -> 128) composed with pred_head's Linear (one 128 -> 128 Linear);
   HF Upscale's last conv 256 -> 128 (k 3) becomes 256 -> 32 (project_in's tl half folded in);
   HF project_in (256 -> 32) on 97 tokens: its th half gathered from a projected table;
   HF project_out (32 -> 256) then pred_head's Linear (256 -> 128): one 32 -> 128 Linear.
@@ -55,7 +56,7 @@ def main():
     # sampler (BASELINE configs[4]): one batch = 10 LF + 1 HF prior forwards + both decoders
     fs, bys = count(cpu_baseline.sampler_fn(num=B))
     n_l, n_h, d_l, D_h, d_h, H_up, steps_l = 24, 96, 128, 128, 32, 256, 10
-    saved = (2 * d_l * d_l * (n_l + 1) * steps_l  # LF project_in
+    saved = (2 * 2 * d_l * d_l * (n_l + 1) * steps_l  # LF project_in; project_out composed
              + 2 * n_h * H_up * 3 * (D_h - d_h)  # Upscale last conv 256 -> 128 vs -> 32
              + 2 * (n_h + 1) * 2 * D_h * d_h  # HF project_in
              + 2 * n_h * (d_h * 2 * D_h + 2 * D_h * D_h - d_h * D_h))  # project_out + pred_head
