@@ -1,5 +1,9 @@
-"""A/B of two GraphedSampler variants on one box, alternated: python tools/sampler_ab.py KIND
-KIND prep: the HF eval tables on the prep stream (default) vs on the HF pass."""
+"""A/B of two GraphedSampler variants on one box, alternated: a module-level boolean switch
+of the package flipped for variant B before its capture (each variant keeps the flag value it
+was captured with: the graph holds the launches).
+usage: python tools/sampler_ab.py [module:FLAG]   e.g. models.bidirectional_transformer:FUSED_SAMPLE
+(no argument: the default sampler against itself, the noise floor)."""
+import importlib
 import os
 import sys
 
@@ -13,9 +17,17 @@ from timevqvae.utils.sample_utils import GraphedSampler  # noqa: E402
 
 dev = torch.device("cuda", 0)
 mg = bench.JointTrainer(dev, 1).s2.maskgit.eval()
-kind = sys.argv[1] if len(sys.argv) > 1 else "prep"
-variants = {"A": GraphedSampler(mg, 1024, dev, prep=True),
-            "B": GraphedSampler(mg, 1024, dev, prep=False)}
+spec = sys.argv[1] if len(sys.argv) > 1 else None
+variants = {"A": GraphedSampler(mg, 1024, dev)}
+if spec:
+    mod_name, flag = spec.split(":")
+    mod = importlib.import_module("timevqvae." + mod_name)
+    old = getattr(mod, flag)
+    setattr(mod, flag, not old)
+    variants["B"] = GraphedSampler(mg, 1024, dev)
+    setattr(mod, flag, old)
+else:
+    variants["B"] = GraphedSampler(mg, 1024, dev)
 
 
 def t(s, n=20):
@@ -35,4 +47,4 @@ for r in range(4):
     for k, s in variants.items():
         res[k].append(t(s))
 for k, v in res.items():
-    print(kind, k, " ".join(f"{x:.3f}" for x in v), "min %.3f" % min(v), flush=True)
+    print(spec, k, " ".join(f"{x:.3f}" for x in v), "min %.3f" % min(v), flush=True)
