@@ -112,18 +112,30 @@ __global__ __launch_bounds__(256) void maskgit_remask_kernel(
 }
 
 // out[b, d, p] = E[idx[b, p], d]: codebook lookup written straight into the decoder's
-// NCHW input (maskgit.py:461-469 embedding + 'b n c -> b c (h w)')
+// NCHW input (maskgit.py:461-469 embedding + 'b n c -> b c (h w)').  A block takes CG_PT
+// positions of one image: their codebook rows are read whole (coalesced, d contiguous) into
+// an LDS tile [d][p] and written out along p (coalesced), instead of one 4-byte gather per
+// output element with a row stride of D floats between neighbouring lanes.
+constexpr int CG_PT = 64;
 __global__ __launch_bounds__(256) void codebook_gather_nchw_kernel(
-    const int64_t* __restrict__ idx, int B, int P, int D, const float* __restrict__ E,
+    const int64_t* __restrict__ idx, int P, int D, const float* __restrict__ E,
     float* __restrict__ out) {
-  const int64_t tot = (int64_t)B * D * P;
-  for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < tot;
-       o += (int64_t)gridDim.x * blockDim.x) {
-    const int p = (int)(o % P);
-    const int64_t r = o / P;
-    const int d = (int)(r % D);
-    const int b = (int)(r / D);
-    out[o] = E[idx[(int64_t)b * P + p] * D + d];
+  extern __shared__ float cg_tile[];  // [D][CG_PT + 1]
+  __shared__ int rows[CG_PT];
+  const int ntile = (P + CG_PT - 1) / CG_PT;
+  const int b = blockIdx.x / ntile, p0 = (blockIdx.x - b * ntile) * CG_PT;
+  const int np = min(CG_PT, P - p0);
+  if (threadIdx.x < np) rows[threadIdx.x] = (int)idx[(int64_t)b * P + p0 + threadIdx.x];
+  __syncthreads();
+  for (int e = threadIdx.x; e < np * D; e += 256) {
+    const int j = e / D, d = e - j * D;
+    cg_tile[d * (CG_PT + 1) + j] = E[(int64_t)rows[j] * D + d];
+  }
+  __syncthreads();
+  float* ob = out + (int64_t)b * D * P + p0;
+  for (int e = threadIdx.x; e < np * D; e += 256) {
+    const int d = e / np, j = e - d * np;
+    ob[(int64_t)d * P + j] = cg_tile[d * (CG_PT + 1) + j];
   }
 }
 
@@ -297,11 +309,12 @@ extern "C" int tvq_maskgit_remask(const float* selp, int64_t B, int64_t n, int64
 
 extern "C" int tvq_codebook_gather_nchw(const int64_t* idx, int64_t B, int64_t P, int64_t D,
                                         const float* E, float* out, tvq_stream_t stream) {
-  TVQ_CHECK_ARG(idx && E && out && B > 0 && P > 0 && D > 0, "tvq_codebook_gather_nchw: bad args");
-  const int64_t tot = B * D * P;
-  const int blocks = (int)((tot + 255) / 256 < 8192 ? (tot + 255) / 256 : 8192);
-  hipLaunchKernelGGL(codebook_gather_nchw_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                     idx, (int)B, (int)P, (int)D, E, out);
+  const int64_t blocks = B * ((P + CG_PT - 1) / CG_PT);
+  TVQ_CHECK_ARG(idx && E && out && B > 0 && P > 0 && D > 0 && D <= 512 && blocks < (1ll << 31),
+                "tvq_codebook_gather_nchw: bad args");
+  hipLaunchKernelGGL(codebook_gather_nchw_kernel, dim3((unsigned)blocks), dim3(256),
+                     (size_t)D * (CG_PT + 1) * sizeof(float), (hipStream_t)stream, idx, (int)P,
+                     (int)D, E, out);
   return launch_status("tvq_codebook_gather_nchw");
 }
 

@@ -197,13 +197,18 @@ def test_mask_by_random_topk_exact_k(cuda):
     assert m.sum(1).eq(17).all() and not m[:, :10].any()
 
 
-def test_codebook_gather_nchw(cuda):
+@pytest.mark.parametrize("B,V,D,H,W", [(5, 50, 16, 3, 8), (7, 513, 128, 3, 32),
+                                         (3, 513, 32, 1, 96), (2, 9, 5, 3, 43)])
+def test_codebook_gather_nchw(B, V, D, H, W, cuda):
+    """Bit-exact lookups at the decoders' (3 x 8 / 3 x 32 tokens, D 128) and the HF eval
+    head's projected-table (D 32) shapes, and a ragged one (positions not a multiple of the
+    64-position tile)."""
     from timevqvae.hip.sample import codebook_gather_nchw
     g = torch.Generator().manual_seed(3)
-    E = torch.randn(50, 16, generator=g)
-    s = torch.randint(0, 50, (5, 3 * 8), generator=g)
-    out = codebook_gather_nchw(s.to(cuda), E.to(cuda), 3, 8)
-    want = E[s].transpose(1, 2).reshape(5, 16, 3, 8)
+    E = torch.randn(V, D, generator=g)
+    s = torch.randint(0, V, (B, H * W), generator=g)
+    out = codebook_gather_nchw(s.to(cuda), E.to(cuda), H, W)
+    want = E[s].transpose(1, 2).reshape(B, D, H, W)
     assert torch.equal(out.cpu(), want)
 
 
