@@ -6,6 +6,8 @@ set -o pipefail
 mkdir -p gpurun_out/r6ev
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 git_tree=$(cat tools/.tree 2>/dev/null || echo unknown)
+PART=${PART:-all}  # A: tests, smoke, bench, step / sampler tables; B: the roofline legs
+if [ "$PART" != B ]; then
 timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/r6ev/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/r6ev/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/r6ev/pytest_gpu.log
 timeout -k 10 600 python __graft_entry__.py smoke > gpurun_out/r6ev/smoke.log 2>&1 || { tail -20 gpurun_out/r6ev/smoke.log; exit 1; }
@@ -26,6 +28,8 @@ T=$(find gpurun_out/r6ev/samp -name "*kernel_trace.csv" | head -1)
 python tools/step_table.py "$T" 5 gpurun_out/r6ev/sampler_batch_kernels.csv add_i64_kernel > /dev/null
 head -4 gpurun_out/r6ev/sampler_batch_kernels.csv
 rm -f "$T"
+fi
+[ "$PART" = A ] && { echo evidence-A-done; exit 0; }
 for LEG in dominant wgrad rbbwd rb32bwd vqassign linfwd t32 attn n16 rb64; do
   LEG=$LEG bash tools/gpu_roofline.sh > gpurun_out/r6ev/roof_$LEG.log 2>&1 || { tail -20 gpurun_out/r6ev/roof_$LEG.log; exit 1; }
   echo "$LEG $(grep -o '"traffic_bytes": [0-9]*' gpurun_out/roof_$LEG/traffic.json)"
