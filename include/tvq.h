@@ -870,6 +870,20 @@ int tvq_hfe_assemble(const float* v, const float* R, const float* P, const float
                      int64_t m, int64_t d, float* z, tvq_stream_t stream);
 int tvq_hfe_assemble_bwd(const float* dz, int64_t B, int64_t m, int64_t d, float* dv, float* dR,
                          float* dCp, tvq_stream_t stream);
+/* The priors' training loss head in one launch (+ a count, a transpose and a final launch):
+ * logits = h W[:K]^T + bias[m mod n] (bidirectional_transformer.py:186-191), the masked
+ * cross-entropy of maskgit.py:183-191 and, for the backward that starts at this loss with the
+ * root gradient *gscale, dlogits = keep ? 0 : (softmax - onehot(target)) * gscale / cnt and
+ * dh = dlogits W[:K] -- the logits never reach memory.  h (M, 128), W (>= K, 128), bias (n,
+ * ldb >= K), target int64 (M), keep bool (M); out = {loss, cnt}.  K in {64, 128, 256, 512};
+ * workspace: tvq_tied_logits_ce_workspace(M, K) floats. */
+int64_t tvq_tied_logits_ce_workspace(int64_t M, int64_t K);
+int tvq_tied_logits_ce(const float* h, int64_t M, int64_t D, const float* W, int64_t K,
+                       const float* bias, int64_t n, int64_t ldb, const int64_t* target,
+                       const bool* keep, const float* gscale, float* dlogits, float* dh,
+                       float* out, float* workspace, tvq_stream_t stream);
+/* out[0] = a[0] / b[0] (device scalars). */
+int tvq_scalar_ratio(const float* a, const float* b, float* out, tvq_stream_t stream);
 
 #ifdef __cplusplus
 }

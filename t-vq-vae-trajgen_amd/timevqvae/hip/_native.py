@@ -71,6 +71,9 @@ sig("tvq_ups_combine", P, I64, I64, I64, I64, P, I64, P, P, P, P, F32, P, P, P)
 sig("tvq_ups_sums", P, P, I64, I64, I64, I64, P, P, P)
 sig("tvq_hfe_assemble", P, P, P, P, I64, I64, I64, P, P)
 sig("tvq_hfe_assemble_bwd", P, I64, I64, I64, P, P, P, P)
+sig("tvq_tied_logits_ce_workspace", I64, I64, restype=I64)
+sig("tvq_tied_logits_ce", P, I64, I64, P, I64, P, I64, I64, P, P, P, P, P, P, P, P)
+sig("tvq_scalar_ratio", P, P, P, P)
 sig("tvq_counter_pool", I64, P, I64)
 sig("tvq_counter_capture", I64)
 sig("tvq_plan_trace", I64)

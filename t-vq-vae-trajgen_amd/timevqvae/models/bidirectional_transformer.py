@@ -291,6 +291,78 @@ class _TiedLogits(torch.autograd.Function):
         return dh, dW, dbias, None
 
 
+TIED_CE_FUSED = True  # False (tests): logits GEMM + masked CE forward / backward launches
+
+
+def tied_ce_supported(h, W, K):
+    return (h.is_cuda and h.dim() == 3 and h.shape[-1] == 128 and W.shape[1] == 128
+            and K in (64, 128, 256, 512) and W.shape[0] >= K)
+
+
+class _TiedLogitsCE(torch.autograd.Function):
+    """masked_cross_entropy(h @ W[:K]^T + bias[:, :K], target, keep) for a backward that starts
+    at this loss with root gradient `gscale` (MaskGIT.forward_backward): tvq_tied_logits_ce
+    computes the loss, the logits' gradient D and dh = D W[:K] in the forward, the logits never
+    reaching memory (bidirectional_transformer.py:186-191, maskgit.py:183-191).  The backward
+    adds the tied-table and bias gradients (D^T h, the batch column sums of D) and returns dh;
+    a root gradient other than `gscale` (not the forward_backward use) rescales them first."""
+
+    @staticmethod
+    def forward(ctx, h, W, bias, K, target, keep, gscale):
+        B, n, D = h.shape
+        M = B * n
+        h2 = h.reshape(M, D).contiguous()
+        dev = h.device
+        ws = torch.empty(value("tvq_tied_logits_ce_workspace", M, K), device=dev)
+        dl = torch.empty((M, K), device=dev)
+        dh = torch.empty((M, D), device=dev)
+        out = torch.empty(2, device=dev)
+        call("tvq_tied_logits_ce", ptr(h2), M, D, ptr(W.contiguous()), K, ptr(bias), bias.shape[0],
+             bias.stride(0), ptr(target.reshape(-1).contiguous()),
+             ptr(keep.reshape(-1).contiguous()), ptr(gscale), ptr(dl), ptr(dh), ptr(out), ptr(ws),
+             stream_ptr())
+        ctx.save_for_backward(h2, dl, dh, gscale)
+        ctx.W, ctx.bias = W, bias
+        ctx.cfg = (B, n, D, K, tuple(bias.shape))
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        h2, dl, dh, gscale = ctx.saved_tensors
+        B, n, D, K, bshape = ctx.cfg
+        M = B * n
+        if g.data_ptr() != gscale.data_ptr():  # another root gradient: D, dh scale by g / gscale
+            from ..hip.linear import scale_by
+            r = torch.empty(1, device=g.device)
+            call("tvq_scalar_ratio", ptr(g.reshape(1).contiguous()), ptr(gscale), ptr(r), stream_ptr())
+            dl, dh = scale_by(dl, r), scale_by(dh, r)
+        need = ctx.needs_input_grad
+        dW = dbias = None
+        if need[1]:
+            sink = grad_sink(ctx.W)
+            if sink is not None:
+                with streams.offload(dl, h2):
+                    gemm(dl, 1, K, h2, D, 1, K, D, M, out=sink, ldc=D, accumulate=True)
+            else:
+                dW = torch.zeros_like(ctx.W)
+                gemm(dl, 1, K, h2, D, 1, K, D, M, out=dW, ldc=D)
+        if need[2]:
+            sink = grad_sink(ctx.bias)
+            if sink is not None:
+                with streams.offload(dl):
+                    batch_colsum(dl.view(B, n, K), sink, bshape[1], True)
+            else:
+                dbias = torch.zeros(bshape, device=g.device)
+                batch_colsum(dl.view(B, n, K), dbias, bshape[1], False)
+        return (dh.view(B, n, D) if need[0] else None), dW, dbias, None, None, None, None
+
+
+def tied_logits_ce(h, W, bias, K, target, keep, gscale):
+    """The prior's masked CE loss from its head output h (B, n, 128) in one fused pass; the
+    backward is meant to start here with root gradient `gscale` (see _TiedLogitsCE)."""
+    return _TiedLogitsCE.apply(h, W, bias, int(K), target, keep, gscale)
+
+
 class Upscale(nn.Module):
     """bidirectional_transformer.py:12-30: nearest x(m/n) -> Conv1d(k3) -> GELU -> BN1d -> Conv1d(k3)."""
 

@@ -22,6 +22,7 @@ from ..hip.loss import add_losses
 from ..hip.vq import indices_only
 from ..hip.xf import mask_tokens, masked_cross_entropy
 from ..utils import freeze, quantize, zero_pad_high_freq, zero_pad_low_freq
+from . import bidirectional_transformer as bt
 from .bidirectional_transformer import BidirectionalTransformer
 from .vq import VectorQuantize
 from .vq_vae import VQVAEEncoder
@@ -177,14 +178,13 @@ class MaskGIT(nn.Module):
             with streams.branch(x.device) as br:  # HF transformer concurrently with LF
                 br.inputs(y, s_l_M, s_h_M, s_h, keep_h, *(() if one is None else (one,)))
                 with wgrad.tag("prior_h"):  # its weight gradients: one grouped launch
-                    logits_h = self.masked_prediction(self.transformer_h, y, s_l_M, s_h_M)
-                    loss_h = masked_cross_entropy(logits_h, s_h, keep_h)
+                    loss_h = self._prior_loss(self.transformer_h, y, (s_l_M, s_h_M), s_h, keep_h,
+                                              one)
                     if one is not None:
                         torch.autograd.backward(loss_h, one)
                 br.outputs(loss_h)
             with wgrad.tag("prior_l"):
-                logits_l = self.masked_prediction(self.transformer_l, y, s_l_M)
-                loss_l = masked_cross_entropy(logits_l, s_l, keep_l)
+                loss_l = self._prior_loss(self.transformer_l, y, (s_l_M,), s_l, keep_l, one)
                 if one is not None:
                     torch.autograd.backward(loss_l, one)
             if one is None:
@@ -192,6 +192,20 @@ class MaskGIT(nn.Module):
         finally:
             self.transformer_l._class_rand = self.transformer_h._class_rand = None
         return loss_l, loss_h
+
+    def _prior_loss(self, tf, y, s_in, target, keep, one):
+        """masked_cross_entropy(masked_prediction(tf, y, *s_in), target, keep) (maskgit.py:
+        180-191).  With `one` (the root gradient of forward_backward) and no guidance mixing,
+        the tied logits, the loss and its gradient down to the head output run as one fused
+        pass (bidirectional_transformer.tied_logits_ce): the logits never reach memory."""
+        if one is not None and bt.TIED_CE_FUSED and (y is None or self.cfg_scale == 1.0):
+            h = tf._embed_hf(*s_in, y) if tf.kind == "hf" else tf._embed_lf(s_in[0], y)
+            W = tf.tok_emb_h.weight if tf.kind == "hf" else tf.tok_emb_l.weight
+            if bt.tied_ce_supported(h, W, tf.codebook_size):
+                return bt.tied_logits_ce(h, W, tf.bias, tf.codebook_size, target, keep, one)
+            logits = bt._TiedLogits.apply(h, W, tf.bias, tf.codebook_size)
+            return masked_cross_entropy(logits, target, keep)
+        return masked_cross_entropy(self.masked_prediction(tf, y, *s_in), target, keep)
 
     def _randomly_mask_tokens(self, s, mask_token_id, device, ratio=None, rand=None):
         """maskgit.py:194-216 on device; returns (s_M, mask) with mask=True for kept tokens.
