@@ -3928,6 +3928,37 @@ void conv_wgrad_w16_multi(int n, const float* const* x, const float* const* dy, 
                      (int)B, (int)C, (int)N, kcols, PS);
   for (int i = 0; i < n; ++i) wgrad_finish(ws[i], S, N, kcols, dw[i], db[i], accumulate, st);
 }
+// n <= 4 weight (+ bias) gradients of 3x3 stride-1 zero-padded C -> N convs on (B, C, 3, 8)
+// maps in one conv_wgrad_w8_kernel<8, 8> launch (the LF ResBlock pair's four convs):
+// problem i into its slab ws[i], each summed in order into dw[i] / db[i] (bit for bit the
+// sums of one launch per problem)
+bool conv_wgrad_w8_fits(int64_t B, int64_t C, int64_t N) {
+  return w8_fits(B, C, 3, 8, N, 8, 3, 3, 1, 0);
+}
+void conv_wgrad_w8_multi(int n, const float* const* x, const float* const* dy, float* const* ws,
+                         float* const* dw, float* const* db, int64_t B, int64_t C, int64_t N,
+                         int accumulate, hipStream_t st) {
+  const int S = (int)(B / W8_IMG);
+  const int PS = whalo_plane_stride(5 * (8 + 2), 9, 3, 8 + 2, 1, 8);
+  const dim3 grid((unsigned)S, (unsigned)(n * (N / 32)), (unsigned)(C / 8));
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_w8_kernel<8, 8>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    attr = true;
+  }
+  W8Probs pr = {};
+  for (int i = 0; i < n; ++i) {
+    pr.G[i] = dy[i];
+    pr.X[i] = x[i];
+    pr.slab[i] = ws[i];
+  }
+  const int kcols = (int)(C * 9 + 1);
+  TVQ_PLAN("conv_wgrad_w8 n=%d S=%d", n, S);
+  hipLaunchKernelGGL((conv_wgrad_w8_kernel<8, 8>), grid, dim3(256), (w8_lds<8, 8>(PS)), st, pr,
+                     (int)B, (int)C, (int)N, kcols, PS);
+  for (int i = 0; i < n; ++i) wgrad_finish(ws[i], S, N, kcols, dw[i], db[i], accumulate, st);
+}
 bool conv_wgrad_w8_pair(const float* x0, const float* dy0, float* ws0, float* dw0, float* db0,
                         const float* x1, const float* dy1, float* ws1, float* dw1, float* db1,
                         int64_t B, int64_t C, int64_t N, int accumulate, hipStream_t st) {

@@ -28,6 +28,10 @@ bool conv_wgrad_w8_pair(const float* x0, const float* dy0, float* ws0, float* dw
                         int64_t B, int64_t C, int64_t N, int accumulate, hipStream_t st);
 // n <= 4 such gradients on (B, C, 3, 16) maps in one launch (the fused RB<32, 16> ResBlocks),
 // each into its own conv_wgrad_w16_slab_floats slab, summed by the deferral scope's flush.
+bool conv_wgrad_w8_fits(int64_t B, int64_t C, int64_t N);
+void conv_wgrad_w8_multi(int n, const float* const* x, const float* const* dy, float* const* ws,
+                         float* const* dw, float* const* db, int64_t B, int64_t C, int64_t N,
+                         int accumulate, hipStream_t st);
 bool conv_wgrad_w16_fits(int64_t B, int64_t C, int64_t N);
 int64_t conv_wgrad_w16_slab_floats(int64_t B, int64_t C, int64_t N);
 void conv_wgrad_w16_multi(int n, const float* const* x, const float* const* dy, float* const* ws,

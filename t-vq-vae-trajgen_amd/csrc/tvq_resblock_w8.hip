@@ -756,6 +756,30 @@ int w8_pair_bwd(const float* dy, const float* x, int64_t B, const float* const* 
   hipLaunchKernelGGL(w8_bwd1_kernel, dim3((unsigned)B), dim3(T), LDS, st, A[1]);
   rc = launch_status("tvq_resblock_pair_bwd");
   if (rc) return rc;
+  if (conv_wgrad_w8_fits(B, C, C)) {  // the pair's four weight gradients in one launch
+    const float* x[4];
+    const float* dy[4];
+    float* wsl[4];
+    float* dw[4];
+    float* db[4];
+    for (int i = 0; i < 2; ++i) {
+      float* const* g = gs[i];
+      x[2 * i] = saveds[i] + 2 * img;  // conv2: (s2, g2)
+      dy[2 * i] = ws_of(i, L.g2);
+      wsl[2 * i] = ws_of(i, L.wg2);
+      dw[2 * i] = g[6];
+      db[2 * i] = g[7];
+      x[2 * i + 1] = saveds[i] + img;  // conv1: (s1, dh)
+      dy[2 * i + 1] = ws_of(i, L.dh);
+      wsl[2 * i + 1] = ws_of(i, L.wg1);
+      dw[2 * i + 1] = g[1];
+      db[2 * i + 1] = g[2];
+    }
+    conv_wgrad_w8_multi(4, x, dy, wsl, dw, db, B, C, C, (int)accumulate, st);
+    for (int i = 0; i < 2; ++i)
+      conv_wgrad_finish(ws_of(i, L.slabda1), (int)B, C, 1, gs[i][0], nullptr, (int)accumulate, st);
+    return launch_status("tvq_resblock_pair_bwd");
+  }
   for (int i = 0; i < 2; ++i) {
     float* const* g = gs[i];
     const float* s1 = saveds[i] + img;
