@@ -18,9 +18,10 @@
 //     16 c + 4 g + r (r = 0..3, consecutive: one float4 of D per tile) of token i.
 //   dh: rows = features (8 tiles of 16), cols = tokens; step (c, r) takes k-slot g = code
 //     16 c + 4 g + r, i.e. the lane's own D register r of tile c as the B operand, and
-//     A = W^T[f][that code] from the transposed table (float4 per 4 steps); the lane ends with
-//     features 16 ft + 4 g + r of token i (one float4 of dh per feature tile).
-// All NT logit tiles stay in registers (NT * 4 floats per lane).
+//     A = W[that code][f]; the lane ends with features 16 ft + 4 g + r of token i (one float4
+//     of dh per feature tile).
+// All NT logit tiles stay in registers (NT * 4 floats per lane); the W tiles come through a
+// double-buffered LDS ring shared by the block's 4 waves (two sweeps: logits, then dh).
 #include <math.h>
 
 #include "tvq_common.h"
@@ -32,7 +33,6 @@ constexpr int TLCE_D = 128;
 struct TlceArgs {
   const float* h;       // (M, 128)
   const float* W;       // (>= K, 128) tied table
-  const float* WT;      // (128, K) its transpose (tlce_transpose_kernel)
   const float* bias;    // (n, ldb)
   int64_t ldb;
   const int64_t* target;
@@ -64,28 +64,46 @@ __global__ __launch_bounds__(1024) void tlce_count_kernel(const bool* __restrict
   }
 }
 
-// WT[f][k] = W[k][f] for k < K (one 32 x 32 tile per block through LDS)
-__global__ __launch_bounds__(256) void tlce_transpose_kernel(const float* __restrict__ W, int K,
-                                                             float* __restrict__ WT) {
-  __shared__ float t[32][33];
-  const int k0 = blockIdx.x * 32, f0 = blockIdx.y * 32;
-  for (int e = threadIdx.x; e < 1024; e += 256) {
-    const int r = e >> 5, c = e & 31;
-    t[r][c] = W[(int64_t)(k0 + r) * TLCE_D + f0 + c];
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < 1024; e += 256) {
-    const int r = e >> 5, c = e & 31;
-    WT[(int64_t)(f0 + r) * K + k0 + c] = t[c][r];
-  }
+// W tiles (32 codes x 128 features) are shared by the block's 4 waves (64 tokens) through a
+// double-buffered LDS ring: each tile is read from L2 once per block and sweep (the logits
+// sweep, then the dh sweep), not once per wave; one barrier per 32 codes.  Row stride 132
+// floats (16-B reads of 16 rows spread over the banks).
+constexpr int TLCE_RS = 132, TLCE_ROWS = 32, TLCE_TILE = TLCE_ROWS * TLCE_RS;
+
+// one 32-code tile = 1024 float4, 4 per thread (named registers: no array to index)
+struct TlceStage {
+  float4 r0, r1, r2, r3;
+};
+__device__ __forceinline__ float4 tlce_ld(const float* __restrict__ W, int j, int u) {
+  const int e = threadIdx.x + 256 * u, row = e >> 5, col = (e & 31) * 4;
+  return *reinterpret_cast<const float4*>(W + (int64_t)(TLCE_ROWS * j + row) * TLCE_D + col);
+}
+__device__ __forceinline__ void tlce_st(float* buf, int u, float4 v) {
+  const int e = threadIdx.x + 256 * u, row = e >> 5, col = (e & 31) * 4;
+  *reinterpret_cast<float4*>(buf + row * TLCE_RS + col) = v;
+}
+__device__ __forceinline__ void tlce_tile_load(const float* __restrict__ W, int j, TlceStage& r) {
+  r.r0 = tlce_ld(W, j, 0);
+  r.r1 = tlce_ld(W, j, 1);
+  r.r2 = tlce_ld(W, j, 2);
+  r.r3 = tlce_ld(W, j, 3);
+}
+__device__ __forceinline__ void tlce_tile_store(float* buf, const TlceStage& r) {
+  tlce_st(buf, 0, r.r0);
+  tlce_st(buf, 1, r.r1);
+  tlce_st(buf, 2, r.r2);
+  tlce_st(buf, 3, r.r3);
 }
 
 template <int NT>
 __global__ __launch_bounds__(256, 2) void tlce_kernel(TlceArgs a) {
+  __shared__ float wl[2 * TLCE_TILE];
+  constexpr int NJ = NT / 2;  // 32-code tiles
   const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t t0 = wave * 16;
-  if (t0 >= a.M) return;  // wave-uniform
+  // every wave of the block takes part in the LDS ring (barriers); rows past M compute on a
+  // clamped row and store nothing
   const bool ok = t0 + i < a.M;
   const int64_t m = ok ? t0 + i : a.M - 1;
   constexpr int K = NT * 16;
@@ -100,39 +118,40 @@ __global__ __launch_bounds__(256, 2) void tlce_kernel(TlceArgs a) {
     xb[4 * q + 3] = v.w;
   }
   const float* brow = a.bias + (int64_t)(m % a.n) * a.ldb + 4 * g;
-  // ---- logits, all NT tiles in registers; A operands prefetched one tile ahead
+  // ---- logits sweep: all NT 16-code tiles in registers
   floatx4 L[NT];
-  float4 wa[8], wn[8];
+  TlceStage st;
+  tlce_tile_load(a.W, 0, st);
+  tlce_tile_store(wl, st);
+  __syncthreads();
 #pragma unroll
-  for (int q = 0; q < 8; ++q)
-    wa[q] = *reinterpret_cast<const float4*>(a.W + (int64_t)i * TLCE_D + 32 * g + 4 * q);
+  for (int j = 0; j < NJ; ++j) {
+    if (j + 1 < NJ) tlce_tile_load(a.W, j + 1, st);
 #pragma unroll
-  for (int c = 0; c < NT; ++c) {
-    if (c + 1 < NT) {
+    for (int hf = 0; hf < 2; ++hf) {
+      const int c = 2 * j + hf;
+      const float* wt = wl + (j & 1) * TLCE_TILE + (16 * hf + i) * TLCE_RS + 32 * g;
+      const float b0 = brow[16 * c], b1 = brow[16 * c + 1], b2 = brow[16 * c + 2],
+                  b3 = brow[16 * c + 3];  // bias rows are K + 1 long: not 16-byte aligned
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        wn[q] = *reinterpret_cast<const float4*>(a.W + (int64_t)(16 * (c + 1) + i) * TLCE_D +
-                                                 32 * g + 4 * q);
+      for (int q = 0; q < 8; ++q) {
+        const float4 w = *reinterpret_cast<const float4*>(wt + 4 * q);
+        acc = mfma16x16x4(w.x, xb[4 * q], acc);
+        acc = mfma16x16x4(w.y, xb[4 * q + 1], acc);
+        acc = mfma16x16x4(w.z, xb[4 * q + 2], acc);
+        acc = mfma16x16x4(w.w, xb[4 * q + 3], acc);
+      }
+      L[c][0] = acc[0] + b0;
+      L[c][1] = acc[1] + b1;
+      L[c][2] = acc[2] + b2;
+      L[c][3] = acc[3] + b3;
     }
-    const float b0 = brow[16 * c], b1 = brow[16 * c + 1], b2 = brow[16 * c + 2],
-                b3 = brow[16 * c + 3];  // bias rows are K + 1 long: not 16-byte aligned
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      acc = mfma16x16x4(wa[q].x, xb[4 * q], acc);
-      acc = mfma16x16x4(wa[q].y, xb[4 * q + 1], acc);
-      acc = mfma16x16x4(wa[q].z, xb[4 * q + 2], acc);
-      acc = mfma16x16x4(wa[q].w, xb[4 * q + 3], acc);
-    }
-    L[c][0] = acc[0] + b0;
-    L[c][1] = acc[1] + b1;
-    L[c][2] = acc[2] + b2;
-    L[c][3] = acc[3] + b3;
-    if (c + 1 < NT) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) wa[q] = wn[q];
-    }
+    if (j + 1 < NJ) tlce_tile_store(wl + ((j + 1) & 1) * TLCE_TILE, st);
+    __syncthreads();
   }
+  // the dh sweep's first tile, loading while the softmax runs
+  tlce_tile_load(a.W, 0, st);
   // ---- softmax statistics of token i over the 4 lane groups (xor 16, xor 32)
   float mx = -INFINITY;
 #pragma unroll
@@ -168,24 +187,28 @@ __global__ __launch_bounds__(256, 2) void tlce_kernel(TlceArgs a) {
     }
     if (ok) *reinterpret_cast<float4*>(drow + 16 * c) = make_float4(L[c][0], L[c][1], L[c][2], L[c][3]);
   }
-  // ---- dh = D W: A = W^T[16 ft + i][16 c + 4 g + r] (float4 over r), B = D register r of tile c
+  // ---- dh sweep: dh^T = W^T D^T; A = W[16 c + 4 g + r][16 ft + i] from the LDS tile, B = D
+  // register r of tile c
+  tlce_tile_store(wl, st);
+  __syncthreads();
   floatx4 dacc[8];
 #pragma unroll
   for (int ft = 0; ft < 8; ++ft) dacc[ft] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const float* wtb = a.WT + (int64_t)i * K + 4 * g;
 #pragma unroll
-  for (int c = 0; c < NT; ++c) {
-    float4 w4[8];
+  for (int j = 0; j < NJ; ++j) {
+    if (j + 1 < NJ) tlce_tile_load(a.W, j + 1, st);
 #pragma unroll
-    for (int ft = 0; ft < 8; ++ft)
-      w4[ft] = *reinterpret_cast<const float4*>(wtb + (int64_t)(16 * ft) * K + 16 * c);
+    for (int hf = 0; hf < 2; ++hf) {
+      const int c = 2 * j + hf;
+      const float* wt = wl + (j & 1) * TLCE_TILE + (16 * hf + 4 * g) * TLCE_RS + i;
 #pragma unroll
-    for (int ft = 0; ft < 8; ++ft) {
-      dacc[ft] = mfma16x16x4(w4[ft].x, L[c][0], dacc[ft]);
-      dacc[ft] = mfma16x16x4(w4[ft].y, L[c][1], dacc[ft]);
-      dacc[ft] = mfma16x16x4(w4[ft].z, L[c][2], dacc[ft]);
-      dacc[ft] = mfma16x16x4(w4[ft].w, L[c][3], dacc[ft]);
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int ft = 0; ft < 8; ++ft)
+          dacc[ft] = mfma16x16x4(wt[r * TLCE_RS + 16 * ft], L[c][r], dacc[ft]);
     }
+    if (j + 1 < NJ) tlce_tile_store(wl + ((j + 1) & 1) * TLCE_TILE, st);
+    __syncthreads();
   }
   if (ok) {
     float* hrow = a.dh + m * TLCE_D + 4 * g;
@@ -198,7 +221,7 @@ __global__ __launch_bounds__(256, 2) void tlce_kernel(TlceArgs a) {
   float ls = (masked && g == 0) ? lse - lt : 0.f;
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1) ls += __shfl_xor(ls, o, 64);
-  if (lane == 0) a.part[wave] = ls;
+  if (lane == 0 && t0 < a.M) a.part[wave] = ls;
 }
 
 // loss = sum of the wave partials (fixed order) / cnt; out = {loss, cnt}
@@ -223,8 +246,8 @@ static bool tlce_nt_ok(int64_t K) { return K == 64 || K == 128 || K == 256 || K 
 
 extern "C" int64_t tvq_tied_logits_ce_workspace(int64_t M, int64_t K) {
   if (M < 1 || !tlce_nt_ok(K)) return -1;
-  // stats (4) | WT (128 K) | wave partials
-  return 4 + TLCE_D * K + (M + 15) / 16;
+  // stats (4) | wave partials
+  return 4 + (M + 15) / 16;
 }
 
 extern "C" int tvq_tied_logits_ce(const float* h, int64_t M, int64_t D, const float* W, int64_t K,
@@ -240,14 +263,11 @@ extern "C" int tvq_tied_logits_ce(const float* h, int64_t M, int64_t D, const fl
                 "tvq_tied_logits_ce: pointers must be 16-byte aligned");
   hipStream_t st = (hipStream_t)stream;
   float* stats = workspace;
-  float* WT = workspace + 4;
-  float* part = WT + TLCE_D * K;
+  float* part = workspace + 4;
   const int64_t waves = (M + 15) / 16;
   hipLaunchKernelGGL(tlce_count_kernel, dim3(1), dim3(1024), 0, st, keep, M, gscale, stats);
-  hipLaunchKernelGGL(tlce_transpose_kernel, dim3((unsigned)(K / 32), TLCE_D / 32), dim3(256), 0,
-                     st, W, (int)K, WT);
   TlceArgs a;
-  a.h = h; a.W = W; a.WT = WT; a.bias = bias; a.ldb = ldb; a.target = target; a.keep = keep;
+  a.h = h; a.W = W; a.bias = bias; a.ldb = ldb; a.target = target; a.keep = keep;
   a.stats = stats; a.D = dlogits; a.dh = dh; a.part = part; a.M = M; a.n = (int)n; a.K = (int)K;
   const dim3 grid((unsigned)((waves + 3) / 4));
   TVQ_PLAN("tied_logits_ce M=%lld K=%lld", (long long)M, (long long)K);
