@@ -14,6 +14,18 @@ for r in csv.reader(open(sys.argv[1])):
     if "tlce" in r[0] or r[0] == "Name":
         print(r[0][:50], r[1], r[3], r[5], r[6])
 PY
+T=$(find gpurun_out/tlce/prof -name "*kernel_trace.csv" | head -1)
+python - "$T" <<'PY'
+import collections, csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+gk = [k for k in rows[0] if "Grid" in k]
+by = collections.defaultdict(list)
+for r in rows:
+    if "tlce_kernel" in r["Kernel_Name"]:
+        by[tuple(r[k] for k in gk)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+for k, v in by.items():
+    print("tlce grid", k, "n", len(v), "avg us %.1f" % (sum(v) / len(v)))
+PY
 find gpurun_out/tlce/prof -name "*kernel_trace.csv" -delete
 for rep in 1 2; do
 timeout -k 10 300 python bench.py --steps 40 --warmup 5 --no-roofline --no-config0 --no-cpu-baseline --no-sampler > gpurun_out/tlce/bench.log 2>&1 || { tail -5 gpurun_out/tlce/bench.log; exit 1; }

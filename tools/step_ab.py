@@ -28,9 +28,13 @@ if sys.argv[1].startswith("env:"):  # env:NAME=VALUE (bench-level capture switch
     old = "unset"
 else:
     mod_name, flag = sys.argv[1].split(":")
+    newval = None
+    if "=" in flag:  # module:NAME=INT
+        flag, newval = flag.split("=")
+        newval = int(newval)
     mod = importlib.import_module("timevqvae." + mod_name)
     old = getattr(mod, flag)
-    for name, val in (("A", old), ("B", not old)):
+    for name, val in (("A", old), ("B", (not old) if newval is None else newval)):
         setattr(mod, flag, val)
         tr = bench.JointTrainer(dev, 1)
         tr.capture(batch)
