@@ -65,7 +65,7 @@ __global__ __launch_bounds__(1024) void tlce_count_kernel(const bool* __restrict
 }
 
 // W tiles (32 codes x 128 features) are shared by the block's 4 waves (64 tokens) through a
-// double-buffered LDS ring: each tile is read from L2 once per block and sweep (the logits
+// 3-deep LDS ring: each tile is read from L2 once per block and sweep (the logits
 // sweep, then the dh sweep), not once per wave; one barrier per 32 codes.  Row stride 132
 // floats (16-B reads of 16 rows spread over the banks).
 constexpr int TLCE_RS = 132, TLCE_ROWS = 32, TLCE_TILE = TLCE_ROWS * TLCE_RS;
@@ -97,7 +97,7 @@ __device__ __forceinline__ void tlce_tile_store(float* buf, const TlceStage& r) 
 
 template <int NT>
 __global__ __launch_bounds__(256, 2) void tlce_kernel(TlceArgs a) {
-  __shared__ float wl[2 * TLCE_TILE];
+  __shared__ float wl[3 * TLCE_TILE];  // 3-deep ring: tile j + 2 loads while j computes
   constexpr int NJ = NT / 2;  // 32-code tiles
   const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -123,14 +123,18 @@ __global__ __launch_bounds__(256, 2) void tlce_kernel(TlceArgs a) {
   TlceStage st;
   tlce_tile_load(a.W, 0, st);
   tlce_tile_store(wl, st);
+  if (NJ > 1) tlce_tile_load(a.W, 1, st);
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    if (j + 1 < NJ) tlce_tile_load(a.W, j + 1, st);
+    // tile j + 1 (loaded during the previous iteration) into its slot, then tile j + 2 loads
+    // while tile j computes
+    if (j + 1 < NJ) tlce_tile_store(wl + ((j + 1) % 3) * TLCE_TILE, st);
+    if (j + 2 < NJ) tlce_tile_load(a.W, j + 2, st);
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       const int c = 2 * j + hf;
-      const float* wt = wl + (j & 1) * TLCE_TILE + (16 * hf + i) * TLCE_RS + 32 * g;
+      const float* wt = wl + (j % 3) * TLCE_TILE + (16 * hf + i) * TLCE_RS + 32 * g;
       const float b0 = brow[16 * c], b1 = brow[16 * c + 1], b2 = brow[16 * c + 2],
                   b3 = brow[16 * c + 3];  // bias rows are K + 1 long: not 16-byte aligned
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -147,7 +151,6 @@ __global__ __launch_bounds__(256, 2) void tlce_kernel(TlceArgs a) {
       L[c][2] = acc[2] + b2;
       L[c][3] = acc[3] + b3;
     }
-    if (j + 1 < NJ) tlce_tile_store(wl + ((j + 1) & 1) * TLCE_TILE, st);
     __syncthreads();
   }
   // the dh sweep's first tile, loading while the softmax runs
@@ -190,24 +193,25 @@ __global__ __launch_bounds__(256, 2) void tlce_kernel(TlceArgs a) {
   // ---- dh sweep: dh^T = W^T D^T; A = W[16 c + 4 g + r][16 ft + i] from the LDS tile, B = D
   // register r of tile c
   tlce_tile_store(wl, st);
+  if (NJ > 1) tlce_tile_load(a.W, 1, st);
   __syncthreads();
   floatx4 dacc[8];
 #pragma unroll
   for (int ft = 0; ft < 8; ++ft) dacc[ft] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    if (j + 1 < NJ) tlce_tile_load(a.W, j + 1, st);
+    if (j + 1 < NJ) tlce_tile_store(wl + ((j + 1) % 3) * TLCE_TILE, st);
+    if (j + 2 < NJ) tlce_tile_load(a.W, j + 2, st);
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       const int c = 2 * j + hf;
-      const float* wt = wl + (j & 1) * TLCE_TILE + (16 * hf + 4 * g) * TLCE_RS + i;
+      const float* wt = wl + (j % 3) * TLCE_TILE + (16 * hf + 4 * g) * TLCE_RS + i;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int ft = 0; ft < 8; ++ft)
           dacc[ft] = mfma16x16x4(wt[r * TLCE_RS + 16 * ft], L[c][r], dacc[ft]);
     }
-    if (j + 1 < NJ) tlce_tile_store(wl + ((j + 1) & 1) * TLCE_TILE, st);
     __syncthreads();
   }
   if (ok) {
