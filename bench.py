@@ -18,6 +18,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "t-vq-vae-trajgen_amd"))
 sys.path.insert(0, ROOT)
 
+# kernel arguments in device memory (a HIP runtime option, read at its initialisation): the
+# graph-replayed step's ~480 launches and the sampler's ~90 (same box, alternated processes:
+# stage1 alone 2.80 -> 2.76-2.79 ms, sampler 4.71-4.73 -> 4.69-4.71 ms, joint within noise;
+# profiles/r06_issue_order_ab.txt).  Inherited by the ranks bench.py launches.
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
