@@ -21,7 +21,7 @@
 //     A = W[that code][f]; the lane ends with features 16 ft + 4 g + r of token i (one float4
 //     of dh per feature tile).
 // All NT logit tiles stay in registers (NT * 4 floats per lane); the W tiles come through a
-// double-buffered LDS ring shared by the block's 4 waves (two sweeps: logits, then dh).
+// 3-deep LDS ring of 32-code tiles shared by the block's 4 waves (two sweeps: logits, then dh).
 #include <math.h>
 
 #include "tvq_common.h"
