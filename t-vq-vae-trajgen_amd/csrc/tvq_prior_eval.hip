@@ -219,7 +219,9 @@ __device__ __forceinline__ void pe_load_vec(const float* __restrict__ p, int h, 
 // tile is multiplied, so each tile starts on operands already in registers and its other
 // groups arrive (in order) behind them.
 #ifndef PE_PRE
-#define PE_PRE 4  // 16-B groups of the next tile loaded during the current one
+// 16-B groups of the next tile loaded during the current one (2 measured best of 1 / 2 / 4 / 8:
+// the sampler batch 0.3 % faster than 4, 8 2.5 % slower; profiles/r06_prior_sched_ab.txt)
+#define PE_PRE 2
 #endif
 struct PeStream {
   const float4* __restrict__ src;
