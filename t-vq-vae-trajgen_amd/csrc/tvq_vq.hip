@@ -1,9 +1,10 @@
 // VQ codebook kernels (K7/K8/K9 in SURVEY.md §2.2) for gfx950.
 //
 // assign: 16 RG token rows per workgroup of 2 RG waves (RG per launch, vq_rg: 6 for the
-// HF band's 24576 rows -- one workgroup per CU -- and 4 for the LF band's 6144).  Each wave
+// HF band's 24576 rows -- one workgroup per CU -- and 2 for the LF band's 6144).  Each wave
 // keeps its 16 rows' x values in registers as fp32 MFMA A-fragments (D/4 VGPRs) for the
-// whole launch and streams the codebook through LDS in 128-code chunks; waves 0..RG-1 own
+// whole launch and streams the codebook through LDS in 128-code chunks (two buffers: the
+// next chunk's global loads are in flight during this chunk's MFMAs); waves 0..RG-1 own
 // code columns [0,64) of every chunk, waves RG..2RG-1 columns [64,128).  x.E^T runs on
 // v_mfma_f32_16x16x4_f32 (exact fp32 FMA chains); the argmin is a running
 // per-lane (value, index) pair merged across the 16 code lanes by shuffles and
@@ -86,8 +87,8 @@ __global__ __launch_bounds__(128 * RG) void vq_assign_kernel(
   constexpr int S = D + 8;  // LDS row stride (floats): conflict-free ds_read_b128 B-fragments
   constexpr int NQ = D / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* es = smem;                       // [VQ_CK][S]
-  float* xx_s = smem + VQ_CK * S;         // [VQ_BM]
+  float* es = smem;                       // [2][VQ_CK][S]
+  float* xx_s = smem + 2 * VQ_CK * S;     // [VQ_BM]
   float* bv_s = xx_s + VQ_BM;             // [2][VQ_BM]
   int* bi_s = (int*)(bv_s + 2 * VQ_BM);   // [2][VQ_BM]
   float* red = (float*)(bi_s + 2 * VQ_BM);  // [NW]
@@ -122,20 +123,42 @@ __global__ __launch_bounds__(128 * RG) void vq_assign_kernel(
 #pragma unroll
   for (int r = 0; r < 4; ++r) { bestv[r] = INFINITY; besti[r] = INT_MAX; }
 
-  for (int c0 = 0; c0 < K; c0 += VQ_CK) {
-    __syncthreads();  // previous chunk consumed (and xx_s visible on first pass)
-    // stage codebook chunk [c0, c0+VQ_CK) into LDS (float4, coalesced along d)
-    for (int e = tid; e < VQ_CK * (D / 4); e += VQ_T) {
+  // two chunk buffers: chunk c + 1 is loaded into registers before chunk c's MFMAs and
+  // written to the other buffer after them, one barrier per chunk
+  constexpr int PF = (VQ_CK * (D / 4) + VQ_T - 1) / VQ_T;
+  auto stage_load = [&](int c0, float4* pf) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + i * VQ_T;
       const int c = e / (D / 4), d4 = e - c * (D / 4);
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (c0 + c < K) v = *reinterpret_cast<const float4*>(E + (int64_t)(c0 + c) * D + 4 * d4);
-      *reinterpret_cast<float4*>(es + c * S + 4 * d4) = v;
+      pf[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < VQ_CK * (D / 4) && c0 + c < K)
+        pf[i] = *reinterpret_cast<const float4*>(E + (int64_t)(c0 + c) * D + 4 * d4);
     }
-    __syncthreads();
+  };
+  auto stage_store = [&](float* buf, const float4* pf) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + i * VQ_T;
+      const int c = e / (D / 4), d4 = e - c * (D / 4);
+      if (e < VQ_CK * (D / 4)) *reinterpret_cast<float4*>(buf + c * S + 4 * d4) = pf[i];
+    }
+  };
+  {
+    float4 pf[PF];
+    stage_load(0, pf);
+    stage_store(es, pf);
+  }
+  __syncthreads();
+  for (int c0 = 0, cb = 0; c0 < K; c0 += VQ_CK, cb ^= 1) {
+    float4 pf[PF];
+    const bool more = c0 + VQ_CK < K;
+    if (more) stage_load(c0 + VQ_CK, pf);
+    const float* ebuf = es + cb * (VQ_CK * S);
     floatx4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const float* eb = es + (ch * 64 + r16) * S + 4 * g;
+    const float* eb = ebuf + (ch * 64 + r16) * S + 4 * g;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       float4 bq[4];
@@ -167,6 +190,8 @@ __global__ __launch_bounds__(128 * RG) void vq_assign_kernel(
         if (v < bestv[r] || (v != v && bestv[r] == bestv[r])) { bestv[r] = v; besti[r] = code; }
       }
     }
+    if (more) stage_store(es + (cb ^ 1) * (VQ_CK * S), pf);
+    __syncthreads();
   }
   // merge across the 16 code lanes of each row group
 #pragma unroll
@@ -314,8 +339,10 @@ extern "C" int tvq_vq_sqnorm(const float* E, int64_t K, int64_t D, float* ee, tv
 // row groups per workgroup: 6 (96 rows, 12 waves) when that still fills every CU with a
 // workgroup -- the HF band's 24576 rows as 256 workgroups, one per CU: 55 us, where 64-row
 // workgroups (384: two on half the CUs) took 60 us and 48 / 32-row ones 66 / 85 us (each
-// workgroup streams the whole codebook through LDS); else 4 (64 rows)
-static int vq_rg(int64_t M) { return M >= 256 * 96 ? 6 : 4; }
+// workgroup streams the whole codebook through LDS; single-buffered then, 53 us now); else 2
+// (32 rows: the LF band's 6144 rows as 192 workgroups, 32.5 us where 96 64-row ones took 39.6,
+// double-buffered both; tools/ab/r06/gpu_vqab.sh)
+static int vq_rg(int64_t M) { return M >= 256 * 96 ? 6 : 2; }
 
 extern "C" int64_t tvq_vq_assign_nblocks(int64_t M) {
   const int rg = vq_rg(M);
@@ -366,11 +393,10 @@ extern "C" int tvq_vq_assign_rows(const float* x, int64_t B, int64_t N, int64_t 
                        M, N, sB, sN, sD, E, ee, (int)K, training, quant, idx, idx32,         \
                        commit_partial, sv, xt);
 #define TVQ_ASSIGN_ST(DD, ST) \
-  TVQ_ASSIGN_RG(DD, ST, 1) TVQ_ASSIGN_RG(DD, ST, 2) TVQ_ASSIGN_RG(DD, ST, 3) \
-  TVQ_ASSIGN_RG(DD, ST, 4) TVQ_ASSIGN_RG(DD, ST, 6)
+  TVQ_ASSIGN_RG(DD, ST, 2) TVQ_ASSIGN_RG(DD, ST, 6)
 #define TVQ_ASSIGN(DD)                                                                       \
   case DD: {                                                                                 \
-    const size_t lds = (size_t)VQ_CK * (DD + 8) * 4 + lds_tail;                              \
+    const size_t lds = (size_t)2 * VQ_CK * (DD + 8) * 4 + lds_tail;                              \
     if (sv.temp > 0.f) {                                                                     \
       TVQ_ASSIGN_ST(DD, true)                                                                \
     } else {                                                                                 \
