@@ -3477,10 +3477,18 @@ extern "C" int tvq_conv_wgrad_defer_flush(tvq_stream_t stream) {
     const hipStream_t st = g_rd.front().st;
     jobs.clear();
     std::vector<RdRec> rest;
+    int64_t bytes = 0;
     for (const RdRec& r : g_rd) {
-      if (r.st == st) jobs.push_back(r.job);
-      else rest.push_back(r);
+      if (r.st == st) {
+        jobs.push_back(r.job);
+        bytes += r.job.P * r.job.N * 4;
+        TVQ_PLAN("wgrad_flush_job st=%p P=%lld N=%lld", (void*)st, (long long)r.job.P,
+                 (long long)r.job.N);
+      } else {
+        rest.push_back(r);
+      }
     }
+    TVQ_PLAN("wgrad_flush st=%p jobs=%d MB=%.1f", (void*)st, (int)jobs.size(), bytes / 1e6);
     reduce_rows_batch(jobs.data(), (int)jobs.size(), st);
     g_rd.swap(rest);
   }
